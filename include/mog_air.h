@@ -1,0 +1,132 @@
+/*
+ * mog_air.h — C ABI of the MI355X-native AIR hot path (libmog_air.so).
+ *
+ * Plain pointers and sizes only: every float / int pointer is DEVICE memory
+ * (HBM of the current HIP device) unless stated otherwise, `stream` is a
+ * hipStream_t passed as void*.  Every entry point is asynchronous on `stream`
+ * and returns 0 on success, MOG_ERR_INVALID (1001) for a rejected argument, or
+ * a hipError_t code from the launch.  No entry point allocates, frees or
+ * synchronises, so any sequence of calls can be captured into a hipGraph.
+ *
+ * The reference (taufikxu/MOG-ASR) is Python/TF-1.12 with no FFI; each entry
+ * point below names the reference interface (file:line) whose behaviour it
+ * replaces.  INTEGRATION.md shows the ctypes binding used by the Python host
+ * (mog-asr_amd/mog_air/_lib.py).
+ */
+#ifndef MOG_AIR_H
+#define MOG_AIR_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MOG_ERR_INVALID 1001
+
+/* ---- dense layers / matmul ------------------------------------------------
+ * Replaces tf.matmul + bias_add + activation of contrib.layers.fully_connected
+ * (air/vae.py:18-41, air/air_model.py:462-499,596-600), the LSTM kernel matmul
+ * (air_model.py:454-456, TF BasicLSTMCell) and their gradients.
+ * Batched over `batch` (<= 8) problems given as HOST arrays of device
+ * pointers.  A(m,k) = transA ? A[k*lda+m] : A[m*lda+k]; B likewise.
+ * epi: 0 store(+bias) 1 relu 2 softplus(TF) 3 sigmoid(acc+bias+aux*aux_scale)
+ *      4 acc*sigmoid(aux) 5 atomic-add 6 relu-backward (aux = activation).
+ * With splitk == 1 every output is one k-ordered fp32 fma chain (bit-exact
+ * with the oracle).  splitk > 1 requires epi 5. */
+int mog_gemm_f32(int batch, const float* const* A, const float* const* B, float* const* C,
+                 const float* const* bias, const float* const* Cin, float* const* Cpre,
+                 const float* const* aux, int M, int N, int K, int lda, int ldb, int ldc,
+                 int ldaux, int transA, int transB, int epi, float aux_scale, int splitk,
+                 void* stream);
+
+/* ---- spatial transformer -------------------------------------------------
+ * air/transformer.py:18-175 transformer(U, theta, out_size) for N images:
+ * U [N, Hin*Win], theta [N, 6] (row-major 2x3), out [N, Hout*Wout].
+ * accumulate = 1 fuses the canvas update of air_model.py:665-675:
+ * out[n] += mask[n] != 0 ? z[n] * w : 0 (z, mask [N]). */
+int mog_stn_forward(const float* U, int N, int Hin, int Win, const float* theta, int Hout,
+                    int Wout, float* out, const float* z, const float* mask, int accumulate,
+                    void* stream);
+
+/* Gradient of transformer() (TF GatherV2 grad = UnsortedSegmentSum + the
+ * affine-grid chain): G [N, Hout*Wout] upstream, scaled per image by gscale[n]
+ * (may be NULL).  Writes dU [N, Hin*Win] (may be NULL), dtheta [N, 6] (may be
+ * NULL) and dot[n] = sum_p G[n,p] * out[n,p] (may be NULL). */
+int mog_stn_backward(const float* U, int N, int Hin, int Win, const float* theta, int Hout,
+                     int Wout, const float* G, const float* gscale, float* dU, float* dtheta,
+                     float* dot, void* stream);
+
+/* ---- LSTM cell (TF-1.12 BasicLSTMCell, air_model.py:454-456,812-815) -----
+ * G [B, 4H] gate pre-activations (i,j,f,o) WITHOUT bias when `bias` != NULL. */
+int mog_lstm_cell_forward(const float* G, const float* bias, const float* c_prev, float* c_out,
+                          float* h_out, int B, int H, void* stream);
+int mog_lstm_cell_backward(const float* G, const float* bias, const float* c_prev,
+                           const float* c_cur, const float* dh, const float* dc, float* dG,
+                           float* dc_prev, float* dGsum, int B, int H, void* stream);
+
+/* ---- per-step scalars ----------------------------------------------------
+ * air_model.py:458-520 (head outputs, scale/shift sampling, theta),
+ * :552-577 (theta^-1), :590-663 (concrete z_pres, KL, stop/digits),
+ * :677-705 (scale/shift KLs), loop predicate :428-432 via live[step+1].
+ * hid/w2/b2: HOST arrays of 5 device pointers (scale-mean, scale-logvar,
+ * shift-mean, shift-logvar, z_pres log-odds). rec: [16, B] saved records. */
+int mog_air_step_forward(int B, int HS, int HZ, int step, int train, int use_num_prior,
+                         float thr, float temperature, float prior_lo, float prior_bias,
+                         float s_pm, float s_pv, float s_plv, float h_pm, float h_pv, float h_plv,
+                         const float* const* hid, const float* const* w2,
+                         const float* const* b2, const float* eps_scale,
+                         const float* eps_shift, const float* u, float* stop, float* runloss,
+                         int* digits, int* live, float* rec, float* theta_fwd,
+                         float* theta_back, float* scale_out, float* shift_out,
+                         float* zprob_out, float* zkl_out, float* skl_out, float* shkl_out,
+                         float* zmask, float* zval, void* stream);
+/* Backward of the above: writes dout [5][B, 2] and dhid [5][B, HS] (head
+ * strides dout_hs / dhid_hs elements). */
+int mog_air_step_backward(int B, int HS, int train, int use_num_prior, float temperature,
+                          float prior_lo, float prior_bias, float s_pm, float s_pv, float h_pm,
+                          float h_pv, float grad_scale, const float* rec, const float* eps_scale,
+                          const float* eps_shift, const float* dtheta_fwd,
+                          const float* dtheta_back, const float* dot, const float* const* hid,
+                          const float* const* w2, float* dout, long dout_hs, float* dhid,
+                          long dhid_hs, void* stream);
+
+/* ---- VAE latent sample + KL (air/vae.py:27-30, air_model.py:718-736) ---- */
+int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, float v_plv, const float* mu,
+                           const float* lv, const float* eps, float* z, const float* act,
+                           float* runloss, float* vkl, void* stream);
+int mog_vae_sample_backward(int B, int Z, float v_pm, float v_pv, float grad_scale,
+                            const float* mu, const float* lv, const float* eps, const float* dz,
+                            const float* act, float* dmu, float* dlv, void* stream);
+/* TF SigmoidGrad: dm = dr * r * (1 - r) (vae.py:46). */
+int mog_sigmoid_backward(const float* r, const float* dr, float* dm, long n, void* stream);
+
+/* ---- reconstruction loss (air_model.py:866-900) -------------------------- */
+int mog_recon_loss(const float* x, const float* canvas, const float* runloss, const int* digits,
+                   const int* targets, int B, int C2, float grad_scale, float* recon,
+                   float* bce, float* mse, float* loss, float* acc, float* dcanvas,
+                   void* stream);
+/* out[k] = mean_b a_k[b] for the non-NULL a_k (k < 4). */
+int mog_batch_mean(const float* a0, const float* a1, const float* a2, const float* a3, int B,
+                   float* out, void* stream);
+/* out[n] += sum_r X[r*ld + n]  (BiasAddGrad) */
+int mog_colsum_add(const float* X, int R, int N, int ld, float* out, void* stream);
+int mog_add(const float* a, const float* b, float* out, long n, void* stream);
+
+/* ---- optimizer (air_model.py:941-999) ------------------------------------
+ * Per-tensor inf/nan -> 0, clip_by_norm(clip), TF ApplyAdam with lr_t given.
+ * off/len: tensor table; block_tensor/block_start: block -> (tensor, first
+ * element), chunks of mog_optim_chunk_elems() elements; all device arrays.
+ * sumsq [n_tensors] must be zero on entry. */
+int mog_optim_chunk_elems(void);
+int mog_clip_adam(float* params, float* grads, float* m, float* v, const long* off,
+                  const long* len, const int* block_tensor, const long* block_start,
+                  int nblocks, float* sumsq, float clip, float lr_t, float beta1, float beta2,
+                  float eps, void* stream);
+
+/* ---- noise (tf.random_normal / random_uniform sites, perf mode) --------- */
+int mog_rng_fill(float* out, long n, unsigned long long seed, unsigned long long offset,
+                 int normal, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MOG_AIR_H */

@@ -1,0 +1,602 @@
+// Per-object-step cell kernels of the AIR loop (air/air_model.py:435-736) and
+// the reconstruction loss (:866-900), forward and backward, for gfx950.
+//
+// The GEMM-shaped pieces (LSTM x/h projections, head hidden layers, VAE
+// layers) run on the MFMA GEMM (gemm_f32.hip / vae_fused.hip); what remains
+// per step is O(B) scalar logic and O(B*H) gate elementwise work, fused here:
+//   lstm_gates_fwd/bwd   BasicLSTMCell gates (TF-1.12, i,j,f,o, forget_bias 1)
+//   step_scalars_fwd     head output layers (k-ordered fma chains), Gaussian
+//                        sampling of scale/shift (:458-498, _sample_from_mvn
+//                        :186-192), theta / theta^-1 (:500-577), concrete
+//                        z_pres sample (concrete.py:20-27) + KL (:30-64),
+//                        stopping sum / digit count / live flag (:428-432,
+//                        :644-663), scale & shift KLs (:677-705)
+//   step_scalars_bwd     the matching hand-derived backward
+//   vae_sample_fwd/bwd   z = mu + eps sqrt(exp(lv)) (vae.py:27-30) + VAE KL
+//                        (air_model.py:718-736)
+//   recon_loss           clip, BCE, MSE, per-image loss, dL/dcanvas (:866-900)
+#include "mog_common.h"
+
+namespace {
+
+// ------------------------------------------------------------------ LSTM ---
+// G: [B, 4H] pre-activation (i, j, f, o); bias added here when `bias` != null
+// (step 0, where the h-projection of the zero state is skipped).
+__global__ __launch_bounds__(256) void lstm_fwd_kernel(const float* __restrict__ G,
+                                                       const float* __restrict__ bias,
+                                                       const float* __restrict__ c_prev,
+                                                       float* c_out, float* h_out, int B, int H) {
+#pragma clang fp contract(off)
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)B * H) return;
+  const int b = idx / H, u = idx - (long)b * H;
+  const float* g = G + (size_t)b * 4 * H;
+  float gi = g[u], gj = g[H + u], gf = g[2 * H + u], go = g[3 * H + u];
+  if (bias) {
+    gi = gi + bias[u]; gj = gj + bias[H + u]; gf = gf + bias[2 * H + u]; go = go + bias[3 * H + u];
+  }
+  const float c0 = c_prev ? c_prev[idx] : 0.0f;
+  const float nc = c0 * mog_sigmoidf(gf + 1.0f) + mog_sigmoidf(gi) * mog_tanhf(gj);
+  c_out[idx] = nc;
+  h_out[idx] = mog_tanhf(nc) * mog_sigmoidf(go);
+}
+
+// dh, dc (incoming, may alias dc_prev_out? no) -> dG [B,4H], dc_prev [B,H];
+// dGsum += dG (sum over steps for the hoisted x-projection gradient).
+__global__ __launch_bounds__(256) void lstm_bwd_kernel(
+    const float* __restrict__ G, const float* __restrict__ bias, const float* __restrict__ c_prev,
+    const float* __restrict__ c_cur, const float* __restrict__ dh, const float* __restrict__ dc,
+    float* dG, float* dc_prev, float* dGsum, int B, int H) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)B * H) return;
+  const int b = idx / H, u = idx - (long)b * H;
+  const float* g = G + (size_t)b * 4 * H;
+  float gi = g[u], gj = g[H + u], gf = g[2 * H + u], go = g[3 * H + u];
+  if (bias) {
+    gi = gi + bias[u]; gj = gj + bias[H + u]; gf = gf + bias[2 * H + u]; go = go + bias[3 * H + u];
+  }
+  const float si = mog_sigmoidf(gi), tj = mog_tanhf(gj), sf = mog_sigmoidf(gf + 1.0f);
+  const float so = mog_sigmoidf(go);
+  const float c0 = c_prev ? c_prev[idx] : 0.0f;
+  const float tc = mog_tanhf(c_cur[idx]);
+  const float dhv = dh[idx];
+  const float dct = (dc ? dc[idx] : 0.0f) + dhv * so * (1.0f - tc * tc);
+  const float dgo = dhv * tc * so * (1.0f - so);
+  const float dgf = dct * c0 * sf * (1.0f - sf);
+  const float dgi = dct * tj * si * (1.0f - si);
+  const float dgj = dct * si * (1.0f - tj * tj);
+  float* d = dG + (size_t)b * 4 * H;
+  d[u] = dgi; d[H + u] = dgj; d[2 * H + u] = dgf; d[3 * H + u] = dgo;
+  if (dGsum) {
+    float* s = dGsum + (size_t)b * 4 * H;
+    s[u] += dgi; s[H + u] += dgj; s[2 * H + u] += dgf; s[3 * H + u] += dgo;
+  }
+  if (dc_prev) dc_prev[idx] = dct * sf;
+}
+
+// -------------------------------------------------------- step scalars ---
+struct StepCfg {
+  int B, H, HS, HZ, train, use_num_prior, step;
+  float thr, temperature, prior_lo, prior_bias;
+  float s_pm, s_pv, s_plv, h_pm, h_pv, h_plv;
+  float grad_scale;  // dL/d(per-image loss) = 1/B_global
+};
+
+// record slots [NREC][B] per step
+enum {
+  R_SM, R_SLV, R_HM0, R_HM1, R_HLV0, R_HLV1, R_LO, R_S, R_TX, R_TY, R_Y, R_Z,
+  R_ACT_OLD, R_ACT, R_LIVE, R_ZC, R_NREC
+};
+
+struct HeadPtrs {
+  const float* hid[5];  // post-relu hidden [B, HS] for sm, slv, hm, hlv, lo
+  const float* w2[5];   // [HS, k]
+  const float* b2[5];   // [k]
+};
+
+__device__ __forceinline__ float chain_dot(const float* a, const float* w, int K, int ldw) {
+#pragma clang fp contract(off)
+  float acc = 0.0f;
+  for (int k = 0; k < K; ++k) acc = fmaf(a[k], w[(size_t)k * ldw], acc);
+  return acc;
+}
+
+__device__ __forceinline__ float lse0(float a) {
+#pragma clang fp contract(off)
+  float m = a > 0.0f ? a : 0.0f;
+  if (!(m - m == 0.0f)) m = 0.0f;
+  return mog_logf(mog_expf(0.0f - m) + mog_expf(a - m)) + m;
+}
+
+__device__ __forceinline__ float concrete_kl(float y, float plo, float pT, float qlo, float qT) {
+#pragma clang fp contract(off)
+  const float eps = 1e-9f;
+  const float lse_p = lse0(-y * pT + plo);
+  const float log_prior = ((mog_logf(pT + eps) - y * (pT + 1.0f)) + plo) - 2.0f * lse_p;
+  const float lse_q = lse0(-y * qT + qlo);
+  const float log_post = ((mog_logf(qT + eps) - y * (qT + 1.0f)) + qlo) - 2.0f * lse_q;
+  return log_post - log_prior;
+}
+
+__device__ __forceinline__ float gauss_kl_term(float plv, float lv, float var, float pv,
+                                               float mean, float pm) {
+#pragma clang fp contract(off)
+  const float d = mean - pm;
+  return (((plv - lv) - 1.0f) + var / pv) + (d * d) / pv;
+}
+
+struct StepFwdIO {
+  const float* eps_scale;  // [B]
+  const float* eps_shift;  // [B,2]
+  const float* u;          // [B]
+  float* stop;             // [B] state
+  float* runloss;          // [B] state
+  int* digits;             // [B] state
+  int* live;               // [T+1] flags; live[step] read, live[step+1] set
+  float* rec;              // [R_NREC, B] records for this step
+  float* theta_fwd;        // [B,6]
+  float* theta_back;       // [B,6]
+  float* scale_out;        // [B]
+  float* shift_out;        // [B,2]
+  float* zprob_out;        // [B]
+  float* zkl_out;          // [B]
+  float* skl_out;          // [B]
+  float* shkl_out;         // [B]
+  float* zmask;            // [B] active (canvas mask)
+  float* zval;             // [B] z_pres value (canvas coefficient)
+};
+
+__global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp, StepFwdIO io) {
+#pragma clang fp contract(off)
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  const int B = cfg.B;
+  if (b >= B) return;
+  const int HS = cfg.HS, HZ = cfg.HZ;
+  const float sm = chain_dot(hp.hid[0] + (size_t)b * HS, hp.w2[0], HS, 1) + hp.b2[0][0];
+  const float slv = chain_dot(hp.hid[1] + (size_t)b * HS, hp.w2[1], HS, 1) + hp.b2[1][0];
+  const float hm0 = chain_dot(hp.hid[2] + (size_t)b * HS, hp.w2[2], HS, 2) + hp.b2[2][0];
+  const float hm1 = chain_dot(hp.hid[2] + (size_t)b * HS, hp.w2[2] + 1, HS, 2) + hp.b2[2][1];
+  const float hv0 = chain_dot(hp.hid[3] + (size_t)b * HS, hp.w2[3], HS, 2) + hp.b2[3][0];
+  const float hv1 = chain_dot(hp.hid[3] + (size_t)b * HS, hp.w2[3] + 1, HS, 2) + hp.b2[3][1];
+  const float lo = chain_dot(hp.hid[4] + (size_t)b * HZ, hp.w2[4], HZ, 1) + hp.b2[4][0];
+
+  // scale / shift sampling (air_model.py:471-477, :492-498; :186-192)
+  const float svar = mog_expf(slv);
+  const float s = mog_sigmoidf(sm + io.eps_scale[b] * sqrtf(svar));
+  const float hvar0 = mog_expf(hv0), hvar1 = mog_expf(hv1);
+  const float tx = mog_tanhf(hm0 + io.eps_shift[2 * b] * sqrtf(hvar0));
+  const float ty = mog_tanhf(hm1 + io.eps_shift[2 * b + 1] * sqrtf(hvar1));
+  float* tf = io.theta_fwd + (size_t)b * 6;
+  tf[0] = s; tf[1] = 0.0f; tf[2] = tx; tf[3] = 0.0f; tf[4] = s; tf[5] = ty;
+  const float is = 1.0f / s;
+  float* tb = io.theta_back + (size_t)b * 6;
+  tb[0] = is; tb[1] = 0.0f; tb[2] = -tx / s; tb[3] = 0.0f; tb[4] = is; tb[5] = -ty / s;
+  io.scale_out[b] = s;
+  io.shift_out[2 * b] = tx;
+  io.shift_out[2 * b + 1] = ty;
+
+  // z_pres (air_model.py:590-620, concrete.py:20-27)
+  const float eps = 1e-9f;
+  const float uu = io.u[b];
+  const float noise = mog_logf(uu + eps) - mog_logf((1.0f - uu) + eps);
+  const float y = (lo + noise) / cfg.temperature;
+  float z = mog_sigmoidf(y);
+  if (!cfg.train) z = rintf(z);
+  io.zprob_out[b] = mog_sigmoidf(lo);
+
+  // z_pres KL with the OLD stopping sum (:622-653)
+  const int live = io.live[cfg.step];
+  float kl_end = 0.0f;
+  if (cfg.use_num_prior) kl_end = concrete_kl(y, -100.0f, cfg.temperature, lo, cfg.temperature);
+  const float zkl = concrete_kl(y, cfg.prior_lo + cfg.prior_bias, cfg.temperature, lo,
+                                cfg.temperature);
+  const float stop_old = io.stop[b];
+  const bool act_old = stop_old < cfg.thr;
+  float rl = io.runloss[b];
+  if (live) rl = rl + (act_old ? zkl : kl_end);
+  io.zkl_out[b] = zkl;
+
+  // stopping sum, digit count, live flag for the next step (:428-432, :659-663)
+  const float stop_new = stop_old + (1.0f - z);
+  io.stop[b] = stop_new;
+  const bool act = stop_new < cfg.thr;
+  if (act) {
+    io.digits[b] += 1;
+    io.live[cfg.step + 1] = 1;
+  }
+
+  // scale & shift KLs with the NEW stopping sum (:677-705)
+  const float skl = 0.5f * gauss_kl_term(cfg.s_plv, slv, svar, cfg.s_pv, sm, cfg.s_pm);
+  if (act) rl = rl + skl;
+  const float shs = gauss_kl_term(cfg.h_plv, hv0, hvar0, cfg.h_pv, hm0, cfg.h_pm) +
+                    gauss_kl_term(cfg.h_plv, hv1, hvar1, cfg.h_pv, hm1, cfg.h_pm);
+  const float shkl = 0.5f * shs;
+  if (act) rl = rl + shkl;
+  io.runloss[b] = rl;
+  io.skl_out[b] = skl;
+  io.shkl_out[b] = shkl;
+  io.zmask[b] = act ? 1.0f : 0.0f;
+  io.zval[b] = z;
+
+  float* r = io.rec;
+  r[R_SM * B + b] = sm; r[R_SLV * B + b] = slv;
+  r[R_HM0 * B + b] = hm0; r[R_HM1 * B + b] = hm1;
+  r[R_HLV0 * B + b] = hv0; r[R_HLV1 * B + b] = hv1;
+  r[R_LO * B + b] = lo; r[R_S * B + b] = s; r[R_TX * B + b] = tx; r[R_TY * B + b] = ty;
+  r[R_Y * B + b] = y; r[R_Z * B + b] = z;
+  r[R_ACT_OLD * B + b] = act_old ? 1.0f : 0.0f;
+  r[R_ACT * B + b] = act ? 1.0f : 0.0f;
+  r[R_LIVE * B + b] = live ? 1.0f : 0.0f;
+  r[R_ZC * B + b] = act ? z : 0.0f;
+}
+
+struct StepBwdIO {
+  const float* rec;         // [R_NREC, B]
+  const float* eps_scale;   // [B]
+  const float* eps_shift;   // [B,2]
+  const float* dtheta_fwd;  // [B,6] from STN-read backward
+  const float* dtheta_back; // [B,6] from STN-write backward (already z*active scaled)
+  const float* dot;         // [B] sum_p dcanvas*w  (canvas -> z_pres)
+  float* dout;              // [5][B, 2] grads wrt head outputs, head stride dout_hs
+  long dout_hs;
+};
+
+__global__ __launch_bounds__(256) void step_bwd_kernel(StepCfg cfg, StepBwdIO io) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  const int B = cfg.B;
+  if (b >= B) return;
+  const float* r = io.rec;
+  const float sm = r[R_SM * B + b], slv = r[R_SLV * B + b];
+  const float hm0 = r[R_HM0 * B + b], hm1 = r[R_HM1 * B + b];
+  const float hv0 = r[R_HLV0 * B + b], hv1 = r[R_HLV1 * B + b];
+  const float lo = r[R_LO * B + b], s = r[R_S * B + b], tx = r[R_TX * B + b];
+  const float ty = r[R_TY * B + b], y = r[R_Y * B + b], z = r[R_Z * B + b];
+  const bool act_old = r[R_ACT_OLD * B + b] != 0.0f, act = r[R_ACT * B + b] != 0.0f;
+  const bool live = r[R_LIVE * B + b] != 0.0f;
+  const float gL = cfg.grad_scale;
+  const float T = cfg.temperature;
+
+  // theta gradients -> (s, tx, ty)
+  const float* dr = io.dtheta_fwd + (size_t)b * 6;
+  const float* dw = io.dtheta_back + (size_t)b * 6;
+  const float da = dw[0] + dw[4];
+  const float s2 = s * s;
+  float ds = dr[0] + dr[4] + da * (-1.0f / s2) + dw[2] * (tx / s2) + dw[5] * (ty / s2);
+  float dtx = dr[2] - dw[2] / s;
+  float dty = dr[5] - dw[5] / s;
+
+  // z_pres: canvas term + concrete KL (train model only)
+  float dz = act ? io.dot[b] : 0.0f;
+  float dy = cfg.train ? dz * z * (1.0f - z) : 0.0f;
+  const float aq = -y * T + lo;
+  const float ap = -y * T + (cfg.prior_lo + cfg.prior_bias);
+  const float sq = mog_sigmoidf(aq), sp = mog_sigmoidf(ap);
+  const float wz = (live && act_old) ? gL : 0.0f;
+  float dlo = 0.0f;
+  dy += wz * (2.0f * T * (sq - sp));
+  dlo += wz * (1.0f - 2.0f * sq);
+  if (cfg.use_num_prior) {
+    const float we = (live && !act_old) ? gL : 0.0f;
+    const float spe = mog_sigmoidf(-y * T + -100.0f);
+    dy += we * (2.0f * T * (sq - spe));
+    dlo += we * (1.0f - 2.0f * sq);
+  }
+  dlo += dy / T;
+
+  // scale: s = sigmoid(sm + e*sqrt(exp(slv)))
+  const float wn = act ? gL : 0.0f;
+  const float dpre_s = ds * s * (1.0f - s);
+  const float svar = mog_expf(slv);
+  const float dsm = dpre_s + wn * (sm - cfg.s_pm) / cfg.s_pv;
+  const float dslv = dpre_s * io.eps_scale[b] * 0.5f * sqrtf(svar) +
+                     wn * 0.5f * (-1.0f + svar / cfg.s_pv);
+  // shift: t = tanh(hm + e*sqrt(exp(hlv)))
+  const float dpx = dtx * (1.0f - tx * tx), dpy = dty * (1.0f - ty * ty);
+  const float hvar0 = mog_expf(hv0), hvar1 = mog_expf(hv1);
+  const float dhm0 = dpx + wn * (hm0 - cfg.h_pm) / cfg.h_pv;
+  const float dhm1 = dpy + wn * (hm1 - cfg.h_pm) / cfg.h_pv;
+  const float dhv0 = dpx * io.eps_shift[2 * b] * 0.5f * sqrtf(hvar0) +
+                     wn * 0.5f * (-1.0f + hvar0 / cfg.h_pv);
+  const float dhv1 = dpy * io.eps_shift[2 * b + 1] * 0.5f * sqrtf(hvar1) +
+                     wn * 0.5f * (-1.0f + hvar1 / cfg.h_pv);
+  float* o = io.dout + 2 * b;
+  const long hs = io.dout_hs;
+  o[0] = dsm; o[1] = 0.0f;
+  o[hs] = dslv; o[hs + 1] = 0.0f;
+  o[2 * hs] = dhm0; o[2 * hs + 1] = dhm1;
+  o[3 * hs] = dhv0; o[3 * hs + 1] = dhv1;
+  o[4 * hs] = dlo; o[4 * hs + 1] = 0.0f;
+}
+
+// dHh_z[b][l] = relu'(Hh) * sum_c dout_z[b][c] W2_z[l][c]
+__global__ __launch_bounds__(256) void heads_hidden_bwd_kernel(HeadPtrs hp, const float* dout,
+                                                               long dout_hs, float* dhid,
+                                                               long dhid_hs, int B, int HS) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= 5L * B * HS) return;
+  const int zh = idx / ((long)B * HS);
+  const long rem = idx - (long)zh * B * HS;
+  const int b = rem / HS, l = rem - (long)b * HS;
+  const int k = (zh == 2 || zh == 3) ? 2 : 1;
+  const float h = hp.hid[zh][(size_t)b * HS + l];
+  float v = 0.0f;
+  if (h > 0.0f) {
+    v = dout[zh * dout_hs + b * 2] * hp.w2[zh][l * k];
+    if (k == 2) v += dout[zh * dout_hs + b * 2 + 1] * hp.w2[zh][l * k + 1];
+  }
+  dhid[zh * dhid_hs + (long)b * HS + l] = v;
+}
+
+// --------------------------------------------------------- VAE sample ---
+struct VaeCfg {
+  int B, Z;
+  float v_pm, v_pv, v_plv, grad_scale;
+};
+
+// z = mu + eps*sqrt(exp(lv)); vkl = 0.5*sum_k term_k (sequential); runloss += act ? vkl : 0
+__global__ __launch_bounds__(256) void vae_sample_fwd_kernel(VaeCfg c, const float* mu,
+                                                             const float* lv, const float* eps,
+                                                             float* z, const float* act,
+                                                             float* runloss, float* vkl_out) {
+#pragma clang fp contract(off)
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= c.B) return;
+  float sum = 0.0f;
+  for (int k = 0; k < c.Z; ++k) {
+    const size_t i = (size_t)b * c.Z + k;
+    const float l = lv[i];
+    const float var = mog_expf(l);
+    z[i] = mu[i] + eps[i] * sqrtf(var);
+    sum = sum + gauss_kl_term(c.v_plv, l, var, c.v_pv, mu[i], c.v_pm);
+  }
+  const float vkl = 0.5f * sum;
+  vkl_out[b] = vkl;
+  if (act[b] != 0.0f) runloss[b] = runloss[b] + vkl;
+}
+
+__global__ __launch_bounds__(256) void vae_sample_bwd_kernel(VaeCfg c, const float* mu,
+                                                             const float* lv, const float* eps,
+                                                             const float* dz, const float* act,
+                                                             float* dmu, float* dlv) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)c.B * c.Z) return;
+  const int b = i / c.Z;
+  const float wn = act[b] != 0.0f ? c.grad_scale : 0.0f;
+  const float var = mog_expf(lv[i]);
+  const float g = dz[i];
+  dmu[i] = g + wn * (mu[i] - c.v_pm) / c.v_pv;
+  dlv[i] = g * eps[i] * 0.5f * sqrtf(var) + wn * 0.5f * (-1.0f + var / c.v_pv);
+}
+
+// dm = dr * r * (1 - r)   (TF SigmoidGrad)
+__global__ __launch_bounds__(256) void sigmoid_bwd_kernel(const float* r, const float* dr,
+                                                          float* dm, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float v = r[i];
+  dm[i] = dr[i] * v * (1.0f - v);
+}
+
+// ---------------------------------------------------------------- loss ---
+// One block per image: clip, BCE, MSE, per-image loss, dL/dcanvas.
+__global__ __launch_bounds__(256) void recon_loss_kernel(
+    const float* __restrict__ x, const float* __restrict__ canvas,
+    const float* __restrict__ runloss, const int* __restrict__ digits,
+    const int* __restrict__ targets, int C2, float grad_scale, float* recon, float* bce_out,
+    float* mse_out, float* loss_out, float* acc_out, float* dcanvas) {
+#pragma clang fp contract(off)
+  __shared__ float red[4];
+  const int b = blockIdx.x;
+  const float* xb = x + (size_t)b * C2;
+  const float* cb = canvas + (size_t)b * C2;
+  float bce = 0.0f, mse = 0.0f;
+  for (int p = threadIdx.x; p < C2; p += 256) {
+    const float c = cb[p];
+    const float r = fmaxf(fminf(c, 1.0f), 0.0f);
+    const float xv = xb[p];
+    const float lr = mog_logf(r + 1e-10f);
+    const float l1r = mog_logf((1.0f - r) + 1e-10f);
+    bce = bce + (xv * lr + (1.0f - xv) * l1r);
+    const float d = xv - r;
+    mse = mse + d * d;
+    if (recon) recon[(size_t)b * C2 + p] = r;
+    if (dcanvas) {
+      const bool pass = (c >= 0.0f) && (c <= 1.0f);  // TF Min/Max grads pass at equality
+      const float g = -(xv * (1.0f / (r + 1e-10f)) - (1.0f - xv) * (1.0f / ((1.0f - r) + 1e-10f)));
+      dcanvas[(size_t)b * C2 + p] = pass ? g * grad_scale : 0.0f;
+    }
+  }
+  bce = mog_block_sum256(bce, red);
+  __syncthreads();
+  mse = mog_block_sum256(mse, red);
+  if (threadIdx.x == 0) {
+    bce_out[b] = -bce;
+    mse_out[b] = mse;
+    loss_out[b] = runloss[b] + (-bce);
+    if (acc_out) acc_out[b] = (targets && targets[b] == digits[b]) ? 1.0f : 0.0f;
+  }
+}
+
+// mean over B of up to 4 per-image vectors -> out[4] (single block, fixed order)
+__global__ __launch_bounds__(256) void batch_mean_kernel(const float* a0, const float* a1,
+                                                         const float* a2, const float* a3,
+                                                         int B, float inv, float* out) {
+  __shared__ float red[4];
+  const float* v[4] = {a0, a1, a2, a3};
+  for (int k = 0; k < 4; ++k) {
+    if (!v[k]) continue;
+    float s = 0.0f;
+    for (int b = threadIdx.x; b < B; b += 256) s += v[k][b];
+    s = mog_block_sum256(s, red);
+    __syncthreads();
+    if (threadIdx.x == 0) out[k] = s * inv;
+  }
+}
+
+// column sums of X [R, N] (row stride ld) -> atomically added into out[N]
+__global__ __launch_bounds__(256) void colsum_kernel(const float* X, int R, int N, int ld,
+                                                     int rows_per_block, float* out) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= N) return;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(R, r0 + rows_per_block);
+  float s = 0.0f;
+  for (int r = r0; r < r1; ++r) s += X[(size_t)r * ld + col];
+  atomicAdd(out + col, s);
+}
+
+// out[i] = a[i] + b[i]
+__global__ __launch_bounds__(256) void add_kernel(const float* a, const float* b, float* out,
+                                                  long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = a[i] + b[i];
+}
+
+}  // namespace
+
+// ============================================================== C ABI ======
+extern "C" int mog_lstm_cell_forward(const float* G, const float* bias, const float* c_prev,
+                                     float* c_out, float* h_out, int B, int H, void* stream) {
+  MOG_CHECK_ARG(G && c_out && h_out && B >= 0 && H > 0);
+  if (B == 0) return 0;
+  lstm_fwd_kernel<<<mog_cdiv((long)B * H, 256), 256, 0, mog_stream(stream)>>>(G, bias, c_prev,
+                                                                              c_out, h_out, B, H);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_lstm_cell_backward(const float* G, const float* bias, const float* c_prev,
+                                      const float* c_cur, const float* dh, const float* dc,
+                                      float* dG, float* dc_prev, float* dGsum, int B, int H,
+                                      void* stream) {
+  MOG_CHECK_ARG(G && c_cur && dh && dG && B >= 0 && H > 0);
+  if (B == 0) return 0;
+  lstm_bwd_kernel<<<mog_cdiv((long)B * H, 256), 256, 0, mog_stream(stream)>>>(
+      G, bias, c_prev, c_cur, dh, dc, dG, dc_prev, dGsum, B, H);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_air_step_forward(
+    int B, int HS, int HZ, int step, int train, int use_num_prior, float thr, float temperature,
+    float prior_lo, float prior_bias, float s_pm, float s_pv, float s_plv, float h_pm, float h_pv,
+    float h_plv, const float* const* hid, const float* const* w2, const float* const* b2,
+    const float* eps_scale, const float* eps_shift, const float* u, float* stop, float* runloss,
+    int* digits, int* live, float* rec, float* theta_fwd, float* theta_back, float* scale_out,
+    float* shift_out, float* zprob_out, float* zkl_out, float* skl_out, float* shkl_out,
+    float* zmask, float* zval, void* stream) {
+  MOG_CHECK_ARG(B >= 0 && hid && w2 && b2 && eps_scale && eps_shift && u && stop && runloss);
+  MOG_CHECK_ARG(digits && live && rec && theta_fwd && theta_back && scale_out && shift_out);
+  MOG_CHECK_ARG(zprob_out && zkl_out && skl_out && shkl_out && zmask && zval);
+  if (B == 0) return 0;
+  StepCfg c;
+  c.B = B; c.H = 0; c.HS = HS; c.HZ = HZ; c.train = train; c.use_num_prior = use_num_prior;
+  c.step = step; c.thr = thr; c.temperature = temperature; c.prior_lo = prior_lo;
+  c.prior_bias = prior_bias; c.s_pm = s_pm; c.s_pv = s_pv; c.s_plv = s_plv; c.h_pm = h_pm;
+  c.h_pv = h_pv; c.h_plv = h_plv; c.grad_scale = 0.0f;
+  HeadPtrs hp;
+  for (int i = 0; i < 5; ++i) {
+    MOG_CHECK_ARG(hid[i] && w2[i] && b2[i]);
+    hp.hid[i] = hid[i]; hp.w2[i] = w2[i]; hp.b2[i] = b2[i];
+  }
+  StepFwdIO io{eps_scale, eps_shift, u,       stop,     runloss,  digits,    live,
+               rec,       theta_fwd, theta_back, scale_out, shift_out, zprob_out, zkl_out,
+               skl_out,   shkl_out,  zmask,   zval};
+  step_fwd_kernel<<<mog_cdiv(B, 256), 256, 0, mog_stream(stream)>>>(c, hp, io);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_air_step_backward(int B, int HS, int train, int use_num_prior,
+                                     float temperature, float prior_lo, float prior_bias,
+                                     float s_pm, float s_pv, float h_pm, float h_pv,
+                                     float grad_scale, const float* rec, const float* eps_scale,
+                                     const float* eps_shift, const float* dtheta_fwd,
+                                     const float* dtheta_back, const float* dot,
+                                     const float* const* hid, const float* const* w2,
+                                     float* dout, long dout_hs, float* dhid, long dhid_hs,
+                                     void* stream) {
+  MOG_CHECK_ARG(B >= 0 && rec && eps_scale && eps_shift && dtheta_fwd && dtheta_back && dot);
+  MOG_CHECK_ARG(hid && w2 && dout && dhid);
+  if (B == 0) return 0;
+  StepCfg c;
+  c.B = B; c.H = 0; c.HS = HS; c.HZ = HS; c.train = train; c.use_num_prior = use_num_prior;
+  c.step = 0; c.thr = 0.0f; c.temperature = temperature; c.prior_lo = prior_lo;
+  c.prior_bias = prior_bias; c.s_pm = s_pm; c.s_pv = s_pv; c.s_plv = 0.0f; c.h_pm = h_pm;
+  c.h_pv = h_pv; c.h_plv = 0.0f; c.grad_scale = grad_scale;
+  StepBwdIO io{rec, eps_scale, eps_shift, dtheta_fwd, dtheta_back, dot, dout, dout_hs};
+  hipStream_t s = mog_stream(stream);
+  step_bwd_kernel<<<mog_cdiv(B, 256), 256, 0, s>>>(c, io);
+  HeadPtrs hp;
+  for (int i = 0; i < 5; ++i) {
+    MOG_CHECK_ARG(hid[i] && w2[i]);
+    hp.hid[i] = hid[i]; hp.w2[i] = w2[i]; hp.b2[i] = nullptr;
+  }
+  heads_hidden_bwd_kernel<<<mog_cdiv(5L * B * HS, 256), 256, 0, s>>>(hp, dout, dout_hs, dhid,
+                                                                      dhid_hs, B, HS);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, float v_plv,
+                                      const float* mu, const float* lv, const float* eps,
+                                      float* z, const float* act, float* runloss, float* vkl,
+                                      void* stream) {
+  MOG_CHECK_ARG(B >= 0 && Z > 0 && mu && lv && eps && z && act && runloss && vkl);
+  if (B == 0) return 0;
+  VaeCfg c{B, Z, v_pm, v_pv, v_plv, 0.0f};
+  vae_sample_fwd_kernel<<<mog_cdiv(B, 256), 256, 0, mog_stream(stream)>>>(c, mu, lv, eps, z, act,
+                                                                         runloss, vkl);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_vae_sample_backward(int B, int Z, float v_pm, float v_pv, float grad_scale,
+                                       const float* mu, const float* lv, const float* eps,
+                                       const float* dz, const float* act, float* dmu,
+                                       float* dlv, void* stream) {
+  MOG_CHECK_ARG(B >= 0 && Z > 0 && mu && lv && eps && dz && act && dmu && dlv);
+  if (B == 0) return 0;
+  VaeCfg c{B, Z, v_pm, v_pv, 0.0f, grad_scale};
+  vae_sample_bwd_kernel<<<mog_cdiv((long)B * Z, 256), 256, 0, mog_stream(stream)>>>(
+      c, mu, lv, eps, dz, act, dmu, dlv);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_sigmoid_backward(const float* r, const float* dr, float* dm, long n,
+                                    void* stream) {
+  MOG_CHECK_ARG(r && dr && dm && n >= 0);
+  if (n == 0) return 0;
+  sigmoid_bwd_kernel<<<mog_cdiv(n, 256), 256, 0, mog_stream(stream)>>>(r, dr, dm, n);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_recon_loss(const float* x, const float* canvas, const float* runloss,
+                              const int* digits, const int* targets, int B, int C2,
+                              float grad_scale, float* recon, float* bce, float* mse,
+                              float* loss, float* acc, float* dcanvas, void* stream) {
+  MOG_CHECK_ARG(x && canvas && runloss && digits && bce && mse && loss && B >= 0 && C2 > 0);
+  if (B == 0) return 0;
+  recon_loss_kernel<<<B, 256, 0, mog_stream(stream)>>>(x, canvas, runloss, digits, targets, C2,
+                                                       grad_scale, recon, bce, mse, loss, acc,
+                                                       dcanvas);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_batch_mean(const float* a0, const float* a1, const float* a2, const float* a3,
+                              int B, float* out, void* stream) {
+  MOG_CHECK_ARG(out && B > 0);
+  batch_mean_kernel<<<1, 256, 0, mog_stream(stream)>>>(a0, a1, a2, a3, B, 1.0f / (float)B, out);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_colsum_add(const float* X, int R, int N, int ld, float* out, void* stream) {
+  MOG_CHECK_ARG(X && out && R >= 0 && N >= 0);
+  if (R == 0 || N == 0) return 0;
+  const int rpb = 256;
+  dim3 g(mog_cdiv(N, 256), mog_cdiv(R, rpb));
+  colsum_kernel<<<g, 256, 0, mog_stream(stream)>>>(X, R, N, ld, rpb, out);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_add(const float* a, const float* b, float* out, long n, void* stream) {
+  MOG_CHECK_ARG(a && b && out && n >= 0);
+  if (n == 0) return 0;
+  add_kernel<<<mog_cdiv(n, 256), 256, 0, mog_stream(stream)>>>(a, b, out, n);
+  MOG_LAUNCH_RET();
+}

@@ -1,0 +1,283 @@
+// Generic fp32 GEMM on the gfx950 fp32-input MFMA (v_mfma_f32_16x16x4_f32).
+//
+// C[m][n] = epilogue( chain_k A(m,k) B(k,n) ), optionally batched over up to
+// MOG_GEMM_MAXB independent problems (pointer arrays) and split over K.
+//
+// Bit-exactness contract: with splitk == 1 each output
+// element is ONE fp32 fma chain over k in natural order, starting from 0 (or
+// from Cin), exactly like the oracle's dense() loop — the 16x16x4 f32 MFMA is
+// a k-ordered fma chain on gfx950 and the k loop below walks k upward.  The
+// bias is added with a separate rounding (TF matmul + bias_add,
+// contrib/layers fully_connected as used at vae.py:18-41, air_model.py:462-499).
+//
+// Replaces the TF-1.12 MatMul / BiasAdd / Softplus / Relu / Sigmoid op groups
+// of the hot path (SURVEY.md §2 table "TF op group on the hot path").
+#include "mog_common.h"
+
+namespace {
+
+enum {
+  EPI_STORE = 0,          // C = acc (+ bias)
+  EPI_RELU = 1,           // C = relu(acc + bias), Cpre = acc + bias
+  EPI_SOFTPLUS = 2,       // C = softplus_tf(acc + bias), Cpre = acc + bias
+  EPI_SIGMOID_NOISE = 3,  // C = sigmoid((acc + bias) + aux*scale), Cpre = acc + bias
+  EPI_SOFTPLUS_BWD = 4,   // C = acc * sigmoid(aux)        (dX through softplus)
+  EPI_ATOMIC = 5,         // C += acc  (atomic; split-K / batch reduction)
+  EPI_RELU_BWD = 6,       // C = aux > 0 ? acc : 0          (dX through relu)
+};
+
+constexpr int MAXB = 8;
+struct GemmPtrs {
+  const float* A[MAXB];
+  const float* B[MAXB];
+  float* C[MAXB];
+  const float* bias[MAXB];
+  const float* Cin[MAXB];
+  float* Cpre[MAXB];
+  const float* aux[MAXB];
+};
+struct GemmDims {
+  int M, N, K, lda, ldb, ldc, ldaux, splitk, kchunk, vecA, vecB;
+  float aux_scale;
+};
+
+constexpr int BM = 64, BN = 64, BK = 16, PADF = 16;
+
+template <bool TA, bool TB, int EPI>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
+#pragma clang fp contract(off)
+  __shared__ float As[BK][BM + PADF];
+  __shared__ float Bs[BK][BN + PADF];
+  const int z = blockIdx.z / D.splitk, ks = blockIdx.z - z * D.splitk;
+  const float* __restrict__ A = P.A[z];
+  const float* __restrict__ Bm = P.B[z];
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kbeg = ks * D.kchunk;
+  const int kend = min(D.K, kbeg + D.kchunk);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  const int M = D.M, N = D.N;
+
+  floatx4 acc[2][2];
+  const float* Cin = P.Cin[z];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = 0.0f;
+        if (Cin != nullptr && ks == 0) {
+          const int row = m0 + wm + mi * 16 + (lane >> 4) * 4 + r;
+          const int col = n0 + wn + ni * 16 + (lane & 15);
+          if (row < M && col < N) v = Cin[(size_t)row * D.ldc + col];
+        }
+        acc[mi][ni][r] = v;
+      }
+
+  float ra[4], rb[4];
+  auto load_tiles = [&](int k0) {
+    // ---- A tile: BM x BK ----
+    if (!TA) {
+      const int row = t >> 2, kc = (t & 3) * 4;
+      const int gm = m0 + row, gk = k0 + kc;
+      if (D.vecA && gm < M && gk + 3 < kend) {
+        const float4 v = *reinterpret_cast<const float4*>(A + (size_t)gm * D.lda + gk);
+        ra[0] = v.x; ra[1] = v.y; ra[2] = v.z; ra[3] = v.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          ra[i] = (gm < M && gk + i < kend) ? A[(size_t)gm * D.lda + gk + i] : 0.0f;
+      }
+    } else {
+      const int k = t >> 4, mc = (t & 15) * 4;
+      const int gk = k0 + k, gm = m0 + mc;
+      if (D.vecA && gk < kend && gm + 3 < M) {
+        const float4 v = *reinterpret_cast<const float4*>(A + (size_t)gk * D.lda + gm);
+        ra[0] = v.x; ra[1] = v.y; ra[2] = v.z; ra[3] = v.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          ra[i] = (gk < kend && gm + i < M) ? A[(size_t)gk * D.lda + gm + i] : 0.0f;
+      }
+    }
+    // ---- B tile: BK x BN ----
+    if (!TB) {
+      const int k = t >> 4, nc = (t & 15) * 4;
+      const int gk = k0 + k, gn = n0 + nc;
+      if (D.vecB && gk < kend && gn + 3 < N) {
+        const float4 v = *reinterpret_cast<const float4*>(Bm + (size_t)gk * D.ldb + gn);
+        rb[0] = v.x; rb[1] = v.y; rb[2] = v.z; rb[3] = v.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          rb[i] = (gk < kend && gn + i < N) ? Bm[(size_t)gk * D.ldb + gn + i] : 0.0f;
+      }
+    } else {
+      const int n = t >> 2, kc = (t & 3) * 4;
+      const int gn = n0 + n, gk = k0 + kc;
+      if (D.vecB && gn < N && gk + 3 < kend) {
+        const float4 v = *reinterpret_cast<const float4*>(Bm + (size_t)gn * D.ldb + gk);
+        rb[0] = v.x; rb[1] = v.y; rb[2] = v.z; rb[3] = v.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          rb[i] = (gn < N && gk + i < kend) ? Bm[(size_t)gn * D.ldb + gk + i] : 0.0f;
+      }
+    }
+  };
+  auto store_tiles = [&]() {
+    if (!TA) {
+      const int row = t >> 2, kc = (t & 3) * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) As[kc + i][row] = ra[i];
+    } else {
+      const int k = t >> 4, mc = (t & 15) * 4;
+      *reinterpret_cast<float4*>(&As[k][mc]) = make_float4(ra[0], ra[1], ra[2], ra[3]);
+    }
+    if (!TB) {
+      const int k = t >> 4, nc = (t & 15) * 4;
+      *reinterpret_cast<float4*>(&Bs[k][nc]) = make_float4(rb[0], rb[1], rb[2], rb[3]);
+    } else {
+      const int n = t >> 2, kc = (t & 3) * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Bs[kc + i][n] = rb[i];
+    }
+  };
+
+  if (kbeg < kend) {
+    load_tiles(kbeg);
+    store_tiles();
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+      const bool has_next = k0 + BK < kend;
+      if (has_next) load_tiles(k0 + BK);
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        const int k = kk * 4 + (lane >> 4);
+        const float a0 = As[k][wm + (lane & 15)];
+        const float a1 = As[k][wm + 16 + (lane & 15)];
+        const float b0 = Bs[k][wn + (lane & 15)];
+        const float b1 = Bs[k][wn + 16 + (lane & 15)];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+      __syncthreads();
+      if (has_next) {
+        store_tiles();
+        __syncthreads();
+      }
+    }
+  }
+
+  float* C = P.C[z];
+  const float* bias = P.bias[z];
+  const float* aux = P.aux[z];
+  float* Cpre = P.Cpre[z];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + mi * 16 + (lane >> 4) * 4 + r;
+        const int col = n0 + wn + ni * 16 + (lane & 15);
+        if (row >= M || col >= N) continue;
+        const size_t o = (size_t)row * D.ldc + col;
+        float v = acc[mi][ni][r];
+        if (EPI == EPI_ATOMIC) {
+          atomicAdd(C + o, v);
+          continue;
+        }
+        if (EPI == EPI_SOFTPLUS_BWD) {
+          C[o] = v * mog_sigmoidf(aux[(size_t)row * D.ldaux + col]);
+          continue;
+        }
+        if (EPI == EPI_RELU_BWD) {
+          C[o] = aux[(size_t)row * D.ldaux + col] > 0.0f ? v : 0.0f;
+          continue;
+        }
+        if (bias != nullptr) v = v + bias[col];
+        if (EPI == EPI_STORE) {
+          C[o] = v;
+        } else {
+          if (Cpre != nullptr) Cpre[o] = v;
+          if (EPI == EPI_RELU) C[o] = v > 0.0f ? v : 0.0f;
+          if (EPI == EPI_SOFTPLUS) C[o] = mog_softplusf(v);
+          if (EPI == EPI_SIGMOID_NOISE)
+            C[o] = mog_sigmoidf(v + aux[(size_t)row * D.ldaux + col] * D.aux_scale);
+        }
+      }
+}
+
+template <bool TA, bool TB>
+void launch_epi(int epi, dim3 g, hipStream_t s, const GemmPtrs& P, const GemmDims& D) {
+  switch (epi) {
+    case EPI_STORE: gemm_f32_kernel<TA, TB, EPI_STORE><<<g, 256, 0, s>>>(P, D); break;
+    case EPI_RELU: gemm_f32_kernel<TA, TB, EPI_RELU><<<g, 256, 0, s>>>(P, D); break;
+    case EPI_SOFTPLUS: gemm_f32_kernel<TA, TB, EPI_SOFTPLUS><<<g, 256, 0, s>>>(P, D); break;
+    case EPI_SIGMOID_NOISE:
+      gemm_f32_kernel<TA, TB, EPI_SIGMOID_NOISE><<<g, 256, 0, s>>>(P, D); break;
+    case EPI_SOFTPLUS_BWD:
+      gemm_f32_kernel<TA, TB, EPI_SOFTPLUS_BWD><<<g, 256, 0, s>>>(P, D); break;
+    case EPI_ATOMIC: gemm_f32_kernel<TA, TB, EPI_ATOMIC><<<g, 256, 0, s>>>(P, D); break;
+    case EPI_RELU_BWD: gemm_f32_kernel<TA, TB, EPI_RELU_BWD><<<g, 256, 0, s>>>(P, D); break;
+  }
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const* B,
+                            float* const* C, const float* const* bias,
+                            const float* const* Cin, float* const* Cpre,
+                            const float* const* aux, int M, int N, int K, int lda, int ldb,
+                            int ldc, int ldaux, int transA, int transB, int epi,
+                            float aux_scale, int splitk, void* stream) {
+  MOG_CHECK_ARG(batch >= 1 && batch <= MAXB);
+  MOG_CHECK_ARG(M >= 0 && N >= 0 && K >= 0 && splitk >= 1);
+  MOG_CHECK_ARG(epi >= EPI_STORE && epi <= EPI_RELU_BWD);
+  MOG_CHECK_ARG(splitk == 1 || epi == EPI_ATOMIC);
+  MOG_CHECK_ARG(A && B && C);
+  if (M == 0 || N == 0) return 0;
+  GemmPtrs P;
+  bool va = true, vb = true;
+  for (int i = 0; i < MAXB; ++i) {
+    const bool on = i < batch;
+    P.A[i] = on ? A[i] : nullptr;
+    P.B[i] = on ? B[i] : nullptr;
+    P.C[i] = on ? C[i] : nullptr;
+    P.bias[i] = (on && bias) ? bias[i] : nullptr;
+    P.Cin[i] = (on && Cin) ? Cin[i] : nullptr;
+    P.Cpre[i] = (on && Cpre) ? Cpre[i] : nullptr;
+    P.aux[i] = (on && aux) ? aux[i] : nullptr;
+    if (on) {
+      MOG_CHECK_ARG(P.A[i] && P.B[i] && P.C[i]);
+      va = va && aligned16(P.A[i]);
+      vb = vb && aligned16(P.B[i]);
+      if (epi == EPI_SIGMOID_NOISE || epi == EPI_SOFTPLUS_BWD || epi == EPI_RELU_BWD)
+        MOG_CHECK_ARG(P.aux[i] != nullptr);
+    }
+  }
+  GemmDims D;
+  D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc; D.ldaux = ldaux;
+  D.aux_scale = aux_scale;
+  D.vecA = va && (lda % 4 == 0);
+  D.vecB = vb && (ldb % 4 == 0);
+  int kchunk = (K + splitk - 1) / splitk;
+  kchunk = ((kchunk + BK - 1) / BK) * BK;
+  if (kchunk == 0) kchunk = BK;
+  D.kchunk = kchunk;
+  D.splitk = (K + kchunk - 1) / kchunk;
+  if (D.splitk < 1) D.splitk = 1;
+  dim3 g(mog_cdiv(N, BN), mog_cdiv(M, BM), batch * D.splitk);
+  hipStream_t s = mog_stream(stream);
+  if (!transA && !transB) launch_epi<false, false>(epi, g, s, P, D);
+  else if (!transA && transB) launch_epi<false, true>(epi, g, s, P, D);
+  else if (transA && !transB) launch_epi<true, false>(epi, g, s, P, D);
+  else launch_epi<true, true>(epi, g, s, P, D);
+  MOG_LAUNCH_RET();
+}

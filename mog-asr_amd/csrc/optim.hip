@@ -1,0 +1,86 @@
+// Fused multi-tensor gradient processing + TF-1.12 Adam (air/air_model.py:941-999).
+//
+// Per tensor (the reference loops over variables, :963-972):
+//   g = where(isinf(g), 0, g); g = where(isnan(g), 0, g)
+//   g = clip_by_norm(g, clip) = (g * clip) / max(||g||_2, clip)
+// then ApplyAdam (epsilon outside the bias correction, TF training_ops):
+//   m += (g - m) * (1 - b1);  v += (g*g - v) * (1 - b2)
+//   var -= (m * lr_t) / (sqrt(v) + eps),  lr_t = lr sqrt(1 - b2^t) / (1 - b1^t)
+// Two launches: (1) sanitize + per-tensor sum of squares, (2) clip + Adam.
+// The tensor table maps a block to (tensor, chunk) so one launch covers all
+// ~36 parameter tensors of the flat parameter buffer.
+#include "mog_common.h"
+
+namespace {
+
+constexpr int CHUNK = 4096;  // elements per block
+
+__global__ __launch_bounds__(256) void sanitize_sumsq_kernel(float* g, const long* off,
+                                                            const long* len,
+                                                            const int* block_tensor,
+                                                            const long* block_start,
+                                                            float* sumsq) {
+  __shared__ float red[4];
+  const int ti = block_tensor[blockIdx.x];
+  const long base = off[ti], n = len[ti];
+  const long c0 = block_start[blockIdx.x];
+  const long c1 = min(n, c0 + CHUNK);
+  float s = 0.0f;
+  for (long i = c0 + threadIdx.x; i < c1; i += 256) {
+    float v = g[base + i];
+    if (isinf(v) || isnan(v)) {
+      v = 0.0f;
+      g[base + i] = 0.0f;
+    }
+    s += v * v;
+  }
+  s = mog_block_sum256(s, red);
+  if (threadIdx.x == 0) atomicAdd(sumsq + ti, s);
+}
+
+__global__ __launch_bounds__(256) void clip_adam_kernel(float* p, const float* g, float* m,
+                                                       float* v, const long* off, const long* len,
+                                                       const int* block_tensor,
+                                                       const long* block_start,
+                                                       const float* sumsq, float clip,
+                                                       float lr_t, float b1, float b2,
+                                                       float eps) {
+#pragma clang fp contract(off)
+  const int ti = block_tensor[blockIdx.x];
+  const long base = off[ti], n = len[ti];
+  const long c0 = block_start[blockIdx.x];
+  const long c1 = min(n, c0 + CHUNK);
+  const float l2 = sumsq[ti];
+  const float norm = l2 > 0.0f ? sqrtf(l2) : l2;
+  const float denom = fmaxf(norm, clip);
+  for (long i = c0 + threadIdx.x; i < c1; i += 256) {
+    const long k = base + i;
+    const float gc = (g[k] * clip) / denom;
+    float mm = m[k], vv = v[k];
+    mm = mm + (gc - mm) * (1.0f - b1);
+    vv = vv + (gc * gc - vv) * (1.0f - b2);
+    m[k] = mm;
+    v[k] = vv;
+    p[k] = p[k] - (mm * lr_t) / (sqrtf(vv) + eps);
+  }
+}
+
+}  // namespace
+
+extern "C" int mog_optim_chunk_elems(void) { return CHUNK; }
+
+// `sumsq` must be zeroed by the caller (it is an in/out accumulator).
+extern "C" int mog_clip_adam(float* params, float* grads, float* m, float* v, const long* off,
+                             const long* len, const int* block_tensor, const long* block_start,
+                             int nblocks, float* sumsq, float clip, float lr_t, float beta1,
+                             float beta2, float eps, void* stream) {
+  MOG_CHECK_ARG(params && grads && m && v && off && len && block_tensor && block_start && sumsq);
+  MOG_CHECK_ARG(nblocks >= 0);
+  if (nblocks == 0) return 0;
+  hipStream_t s = mog_stream(stream);
+  sanitize_sumsq_kernel<<<nblocks, 256, 0, s>>>(grads, off, len, block_tensor, block_start,
+                                                sumsq);
+  clip_adam_kernel<<<nblocks, 256, 0, s>>>(params, grads, m, v, off, len, block_tensor,
+                                           block_start, sumsq, clip, lr_t, beta1, beta2, eps);
+  MOG_LAUNCH_RET();
+}

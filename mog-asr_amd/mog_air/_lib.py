@@ -1,0 +1,86 @@
+"""ctypes binding of libmog_air.so (the C ABI declared in include/mog_air.h).
+
+The product path has no fallback: if the HIP library is missing or fails to
+load, every op raises.  Build it with ``make -C mog-asr_amd`` (or
+``__graft_entry__.build()``)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from typing import List
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libmog_air.so")
+HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "mog_air.h"))
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+F = ctypes.c_float
+L = ctypes.c_long
+ULL = ctypes.c_ulonglong
+
+# argtypes per entry point (mirrors include/mog_air.h)
+_SIGS = {
+    "mog_gemm_f32": [I, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, I, P],
+    "mog_stn_forward": [P, I, I, I, P, I, I, P, P, P, I, P],
+    "mog_stn_backward": [P, I, I, I, P, I, I, P, P, P, P, P, P],
+    "mog_lstm_cell_forward": [P, P, P, P, P, I, I, P],
+    "mog_lstm_cell_backward": [P, P, P, P, P, P, P, P, P, I, I, P],
+    "mog_air_step_forward": [I, I, I, I, I, I, F, F, F, F, F, F, F, F, F, F, P, P, P, P, P, P,
+                             P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "mog_air_step_backward": [I, I, I, I, F, F, F, F, F, F, F, F, P, P, P, P, P, P, P, P, P,
+                              L, P, L, P],
+    "mog_vae_sample_forward": [I, I, F, F, F, P, P, P, P, P, P, P, P],
+    "mog_vae_sample_backward": [I, I, F, F, F, P, P, P, P, P, P, P, P],
+    "mog_sigmoid_backward": [P, P, P, L, P],
+    "mog_recon_loss": [P, P, P, P, P, I, I, F, P, P, P, P, P, P, P],
+    "mog_batch_mean": [P, P, P, P, I, P, P],
+    "mog_colsum_add": [P, I, I, I, P, P],
+    "mog_add": [P, P, P, L, P],
+    "mog_optim_chunk_elems": [],
+    "mog_clip_adam": [P, P, P, P, P, P, P, P, I, P, F, F, F, F, F, P],
+    "mog_rng_fill": [P, L, ULL, ULL, I, P],
+}
+
+_lib = None
+
+
+class MogError(RuntimeError):
+    pass
+
+
+def header_symbols() -> List[str]:
+    """Entry points declared in include/mog_air.h."""
+    with open(HEADER_PATH) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\bint\s+(mog_\w+)\s*\(", src)))
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MogError(
+            f"HIP library not found at {LIB_PATH}; build it with `make -C mog-asr_amd` "
+            "(there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = I
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        what = "invalid argument" if rc == 1001 else f"hipError {rc}"
+        raise MogError(f"{name} failed: {what}")
+
+
+def ptr_array(ptrs) -> ctypes.Array:
+    return (ctypes.c_void_p * len(ptrs))(*ptrs)

@@ -1,0 +1,621 @@
+"""AIRModel — drop-in host object for the reference's AIR baseline model
+(air/air_model.py:13-1146), running the per-object-step loop on MI355X HIP
+kernels (libmog_air.so) with a hand-scheduled forward and backward.
+
+Reference surface kept (air_model.py:15-51, training_air_original.py:158-209):
+the constructor keyword arguments, variable sharing between a train model and
+a test model (``reuse``), annealing schedules (air_model.py:139-147,164-184)
+and the result attributes ``loss, accuracy, mse_loss, global_step,
+rec_num_digits, rec_scales, rec_shifts, rec_st_back, rec_windows, rec_latents,
+reconstruction, reconstruction_loss, z_pres_probs, z_pres_kls, scale_kls,
+shift_kls, vae_kls, accuracy_instance``.  TF's ``sess.run([model.training,
+...])`` becomes ``model.step(images, targets)``; fetching the test model's
+tensors becomes ``model.infer(images, targets)``.
+
+Loop semantics: the data-dependent ``tf.while_loop`` (air_model.py:428-432)
+runs max_steps iterations on the device with the predicate folded into a
+per-step ``live`` flag; every loss term, count and gradient is identical to
+the early exit, and the ``rec_*`` outputs are sliced to the executed steps.
+No host synchronisation happens inside a train step.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import ops
+from .ops import (EPI_ATOMIC, EPI_RELU, EPI_SIGMOID_NOISE, EPI_SOFTPLUS, EPI_SOFTPLUS_BWD,
+                  EPI_STORE, dp, gemm, stream_ptr)
+from .params import ParamStore, param_specs
+
+# step-record slots (air_cell.hip enum)
+R_SM, R_SLV, R_HM0, R_HM1, R_HLV0, R_HLV1, R_LO, R_S, R_TX, R_TY, R_Y, R_Z = range(12)
+R_ACT_OLD, R_ACT, R_LIVE, R_ZC, R_NREC = 12, 13, 14, 15, 16
+
+_SCOPES: Dict[str, ParamStore] = {}
+
+
+def _f32log(v: float) -> float:
+    return float(np.log(np.float32(v), dtype=np.float32))
+
+
+def annealed_value(schedule: dict, global_step: int, eps=1e-9) -> float:
+    """tf.train.exponential_decay (+min/max/log) in fp32 (air_model.py:164-184)."""
+    f = np.float32
+    p = f(global_step) / f(schedule["iters"])
+    if schedule.get("staircase", False):
+        p = np.floor(p)
+    v = f(schedule["init"]) * np.power(f(schedule["factor"]), p, dtype=np.float32)
+    if "min" in schedule:
+        v = np.maximum(v, f(schedule["min"]))
+    if "max" in schedule:
+        v = np.minimum(v, f(schedule["max"]))
+    if schedule.get("log", False):
+        v = np.log(v + f(eps), dtype=np.float32)
+    return float(v)
+
+
+def marginal_objective(num_prior, max_steps) -> np.ndarray:
+    """The ``-ap`` per-step prior bias (air_model.py:86-107)."""
+    obj = np.zeros([max_steps])
+    buf = 1.0 - 1.0 / len(num_prior)
+    for ind in range(max_steps):
+        if ind not in num_prior and ind < max(num_prior):
+            obj[ind] = 1.0
+        else:
+            if ind == max(num_prior):
+                break
+            obj[ind] = buf
+            if ind in num_prior:
+                buf -= 1.0 / len(num_prior)
+    for ind in range(max_steps):
+        if obj[ind] == 1.0:
+            obj[ind] = 100
+        elif obj[ind] == 0.0:
+            obj[ind] = -100.0
+        else:
+            obj[ind] = np.log(obj[ind] / (1.0 - obj[ind]))
+    return obj.astype(np.float32)
+
+
+class _Workspace:
+    """All per-batch device buffers of one train step (HBM-resident, reused)."""
+
+    def __init__(self, m: "AIRModel", B: int):
+        dev = m.device
+        T, H, C2, W2, Z = m.max_steps, m.rnn_units, m.C2, m.W2, m.vae_latent_dimensions
+        R1, R2 = m.vae_recognition_units
+        G1, G2 = m.vae_generative_units
+        HS = m.scale_hidden_units
+        e = lambda *s: torch.empty(s, device=dev, dtype=torch.float32)  # noqa: E731
+        self.B = B
+        self.Gx = e(B, 4 * H)
+        self.G = e(T, B, 4 * H)
+        self.c = e(T, B, H)
+        self.h = e(T, B, H)
+        self.hid = e(5, T, B, HS)
+        self.rec = e(T, R_NREC, B)
+        self.th_f = e(T, B, 6)
+        self.th_b = e(T, B, 6)
+        self.scale = e(T, B)
+        self.shift = e(T, B, 2)
+        self.zprob, self.zkl, self.skl, self.shkl = e(T, B), e(T, B), e(T, B), e(T, B)
+        self.zmask, self.zval, self.vkl = e(T, B), e(T, B), e(T, B)
+        self.g = e(T, B, W2)
+        self.a1pre, self.a1 = e(T, B, R1), e(T, B, R1)
+        self.a2pre, self.a2 = e(T, B, R2), e(T, B, R2)
+        self.mu, self.lv, self.z = e(T, B, Z), e(T, B, Z), e(T, B, Z)
+        self.d1pre, self.d1 = e(T, B, G1), e(T, B, G1)
+        self.d2pre, self.d2 = e(T, B, G2), e(T, B, G2)
+        self.mpre, self.r = e(T, B, W2), e(T, B, W2)
+        self.canvas = e(B, C2)
+        self.stop, self.runloss = e(B), e(B)
+        self.digits = torch.empty(B, device=dev, dtype=torch.int32)
+        self.live = torch.empty(T + 1, device=dev, dtype=torch.int32)
+        self.recon = e(B, C2)
+        self.bce, self.mse, self.loss_b, self.acc_b = e(B), e(B), e(B), e(B)
+        self.means = e(4)
+        # noise
+        self.eps_scale, self.eps_shift = e(T, B), e(T, B, 2)
+        self.eps_z, self.eps_x, self.u = e(T, B, Z), e(T, B, W2), e(T, B)
+        self._bwd = False
+
+    def alloc_backward(self, m: "AIRModel"):
+        if self._bwd:
+            return
+        dev, B = m.device, self.B
+        T, H, C2, W2, Z = m.max_steps, m.rnn_units, m.C2, m.W2, m.vae_latent_dimensions
+        R1, R2 = m.vae_recognition_units
+        G1, G2 = m.vae_generative_units
+        HS = m.scale_hidden_units
+        e = lambda *s: torch.empty(s, device=dev, dtype=torch.float32)  # noqa: E731
+        self.dcanvas = e(B, C2)
+        self.dr = e(B, W2)
+        self.dm = e(T, B, W2)
+        self.dd2, self.dd1 = e(T, B, G2), e(T, B, G1)
+        self.dz = e(B, Z)
+        self.dmu, self.dlv = e(T, B, Z), e(T, B, Z)
+        self.tmp_a2 = e(B, R2)
+        self.da2, self.da1 = e(T, B, R2), e(T, B, R1)
+        self.dg = e(B, W2)
+        self.dth_f, self.dth_b, self.dot = e(B, 6), e(B, 6), e(B)
+        self.dout = e(5, T, B, 2)
+        self.dhid = e(5, T, B, HS)
+        self.dh = e(T, B, H)
+        self.dc = e(2, B, H)
+        self.dG = e(T, B, 4 * H)
+        self.dGsum = e(B, 4 * H)
+        self._bwd = True
+
+
+class AIRModel:
+    """See module docstring.  Extra keyword-only arguments (not in the
+    reference): ``device``, ``seed`` (weight init), ``noise_seed`` (device
+    Philox noise), ``grad_world`` (data-parallel world size folded into the
+    loss-mean gradient scale)."""
+
+    def __init__(self, input_images=None, target_num_digits=None, max_steps=3, max_digits=2,
+                 rnn_units=256, canvas_size=50, windows_size=28, vae_latent_dimensions=50,
+                 vae_recognition_units=(512, 256), vae_generative_units=(256, 512),
+                 scale_prior_mean=-1.0, scale_prior_variance=0.1, shift_prior_mean=0.0,
+                 shift_prior_variance=1.0, vae_prior_mean=0.0, vae_prior_variance=1.0,
+                 vae_likelihood_std=0.3, scale_hidden_units=64, shift_hidden_units=64,
+                 z_pres_hidden_units=64, z_pres_prior_log_odds=-2.0, z_pres_temperature=1.0,
+                 stopping_threshold=0.99, learning_rate=1e-3, gradient_clipping_norm=100.0,
+                 cnn=True, cnn_filters=8, num_summary_images=60, train=False, reuse=False,
+                 scope="air", annealing_schedules=None, generation_batch_size=64,
+                 num_prior=None, *, device=None, seed: int = 1235, noise_seed: int = 1235,
+                 grad_world: int = 1):
+        if cnn:
+            raise NotImplementedError(
+                "cnn=True (air_model.py:763-810) is outside the hot-path scope; the entry "
+                "points use cnn=False")
+        if not (scale_hidden_units == shift_hidden_units == z_pres_hidden_units):
+            raise NotImplementedError("heads must share one hidden width")
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        if self.device.type != "cuda":
+            raise RuntimeError("AIRModel runs on a HIP device only (no CPU fallback)")
+        _lib.load()
+        self.input_images = input_images
+        self.target_num_digits = target_num_digits
+        self.max_steps, self.max_digits = int(max_steps), max_digits
+        self.rnn_units = int(rnn_units)
+        self.canvas_size, self.windows_size = int(canvas_size), int(windows_size)
+        self.C2, self.W2 = self.canvas_size ** 2, self.windows_size ** 2
+        self.vae_latent_dimensions = int(vae_latent_dimensions)
+        self.vae_recognition_units = tuple(vae_recognition_units)
+        self.vae_generative_units = tuple(vae_generative_units)
+        self.scale_prior_mean, self.scale_prior_variance = scale_prior_mean, scale_prior_variance
+        self.shift_prior_mean, self.shift_prior_variance = shift_prior_mean, shift_prior_variance
+        self.vae_prior_mean, self.vae_prior_variance = vae_prior_mean, vae_prior_variance
+        self.vae_likelihood_std = vae_likelihood_std
+        self.scale_hidden_units = scale_hidden_units
+        self.shift_hidden_units = shift_hidden_units
+        self.z_pres_hidden_units = z_pres_hidden_units
+        self.z_pres_prior_log_odds = z_pres_prior_log_odds
+        self.z_pres_temperature = z_pres_temperature
+        self.stopping_threshold = stopping_threshold
+        self.learning_rate = learning_rate
+        self.gradient_clipping_norm = gradient_clipping_norm
+        self.num_summary_images = num_summary_images
+        self.train = bool(train)
+        self.scope = scope
+        self.annealing_schedules = dict(annealing_schedules or {})
+        self.generation_batch_size = generation_batch_size
+        self.num_prior = num_prior
+        self.noise_seed = int(noise_seed)
+        self.grad_world = int(grad_world)
+        self._noise_ctr = 0
+        self.scale_prior_log_variance = _f32log(scale_prior_variance)
+        self.shift_prior_log_variance = _f32log(shift_prior_variance)
+        self.vae_prior_log_variance = _f32log(vae_prior_variance)
+        self.marginal = (marginal_objective(num_prior, self.max_steps)
+                         if num_prior is not None else None)
+        specs = param_specs(self.C2, self.rnn_units, self.W2, self.vae_recognition_units,
+                            self.vae_generative_units, self.vae_latent_dimensions,
+                            scale_hidden_units, z_pres_hidden_units)
+        if reuse:
+            if scope not in _SCOPES:
+                raise ValueError(f"reuse=True but scope {scope!r} has no variables yet")
+            self.params = _SCOPES[scope]
+            if self.params.specs != specs:
+                raise ValueError("reused scope has different variable shapes")
+        else:
+            self.params = ParamStore(specs, self.device, seed=seed)
+            _SCOPES[scope] = self.params
+        self._ws: Optional[_Workspace] = None
+        self._last_T = None
+        self._outputs_ready = False
+
+    # ----------------------------------------------------------- helpers ---
+    @property
+    def global_step(self) -> int:
+        return self.params.global_step
+
+    def hyper(self, name: str) -> float:
+        """Current value of a possibly-annealed hyper-parameter, evaluated at
+        the pre-increment global step (as in the reference forward pass)."""
+        if name in self.annealing_schedules:
+            return annealed_value(self.annealing_schedules[name], self.params.global_step)
+        return float(getattr(self, name))
+
+    def _workspace(self, B: int) -> _Workspace:
+        if self._ws is None or self._ws.B != B:
+            self._ws = _Workspace(self, B)
+        return self._ws
+
+    def _P(self, name):
+        return self.params.view("air/rnn/" + name)
+
+    def _G(self, name):
+        return self.params.g("air/rnn/" + name)
+
+    _HEADS = ("scale/mean", "scale/log_variance", "shift/mean", "shift/log_variance",
+              "z_pres/log_odds")
+    _VAE = ("recognition_1", "recognition_2", "rec_mean", "rec_log_variance", "generative_1",
+            "generative_2", "gen_mean")
+
+    def _fill_noise(self, ws: _Workspace, noise: Optional[Dict[str, torch.Tensor]]):
+        if noise is not None:
+            for k in ("eps_scale", "eps_shift", "eps_z", "eps_x", "u"):
+                src = noise[k]
+                dst = getattr(ws, k)
+                if tuple(src.shape) != tuple(dst.shape):
+                    raise ValueError(f"noise[{k}] has shape {tuple(src.shape)}, "
+                                     f"expected {tuple(dst.shape)}")
+                dst.copy_(src)
+            return
+        for k, normal in (("eps_scale", True), ("eps_shift", True), ("eps_z", True),
+                          ("eps_x", True), ("u", False)):
+            buf = getattr(ws, k)
+            ops.rng_fill(buf, self.noise_seed, self._noise_ctr, normal)
+            self._noise_ctr += (buf.numel() + 3) // 4
+
+    # ----------------------------------------------------------- forward ---
+    def _forward(self, X: torch.Tensor, targets: Optional[torch.Tensor], ws: _Workspace,
+                 need_grad: bool) -> None:
+        B, T, H = ws.B, self.max_steps, self.rnn_units
+        C, W, C2, W2 = self.canvas_size, self.windows_size, self.C2, self.W2
+        Z = self.vae_latent_dimensions
+        R1, R2 = self.vae_recognition_units
+        G1, G2 = self.vae_generative_units
+        HS = self.scale_hidden_units
+        s = stream_ptr()
+        K = self._P("rnn/basic_lstm_cell/kernel")
+        bK = self._P("rnn/basic_lstm_cell/bias")
+        Wx, Wh = K[:C2], K[C2:]
+        ws.canvas.zero_()
+        ws.stop.zero_()
+        ws.runloss.zero_()
+        ws.digits.zero_()
+        ws.live.zero_()
+        ws.live[0] = 1
+        prior_lo = self.hyper("z_pres_prior_log_odds")
+        temperature = self.hyper("z_pres_temperature")
+        thr = self.hyper("stopping_threshold")
+        lik_std = self.hyper("vae_likelihood_std")
+        # hoisted x-projection of the LSTM input (input is loop-invariant in AIR)
+        gemm([X], [Wx], [ws.Gx], B, 4 * H, C2, C2, 4 * H, 4 * H)
+        w1 = [self._P(h + "/hidden/weights") for h in self._HEADS]
+        b1 = [self._P(h + "/hidden/biases") for h in self._HEADS]
+        w2 = [self._P(h + "/output/weights") for h in self._HEADS]
+        b2 = [self._P(h + "/output/biases") for h in self._HEADS]
+        vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
+        vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
+        w2a = _lib.ptr_array([dp(x) for x in w2])
+        b2a = _lib.ptr_array([dp(x) for x in b2])
+        for t in range(T):
+            if t == 0:
+                _lib.call("mog_lstm_cell_forward", dp(ws.Gx), dp(bK), None, dp(ws.c[0]),
+                          dp(ws.h[0]), B, H, s)
+            else:
+                gemm([ws.h[t - 1]], [Wh], [ws.G[t]], B, 4 * H, H, H, 4 * H, 4 * H, bias=[bK],
+                     Cin=[ws.Gx])
+                _lib.call("mog_lstm_cell_forward", dp(ws.G[t]), None, dp(ws.c[t - 1]),
+                          dp(ws.c[t]), dp(ws.h[t]), B, H, s)
+            hid_t = [ws.hid[z, t] for z in range(5)]
+            gemm([ws.h[t]] * 5, w1, hid_t, B, HS, H, H, HS, HS, epi=EPI_RELU, bias=b1)
+            bias_t = float(self.marginal[t]) if self.marginal is not None else 0.0
+            rec = ws.rec[t]
+            _lib.call("mog_air_step_forward", B, HS, HS, t, int(self.train),
+                      int(self.marginal is not None), thr, temperature, prior_lo, bias_t,
+                      float(self.scale_prior_mean), float(self.scale_prior_variance),
+                      self.scale_prior_log_variance, float(self.shift_prior_mean),
+                      float(self.shift_prior_variance), self.shift_prior_log_variance,
+                      _lib.ptr_array([dp(x) for x in hid_t]), w2a, b2a, dp(ws.eps_scale[t]),
+                      dp(ws.eps_shift[t]), dp(ws.u[t]), dp(ws.stop), dp(ws.runloss),
+                      dp(ws.digits), dp(ws.live), dp(rec), dp(ws.th_f[t]), dp(ws.th_b[t]),
+                      dp(ws.scale[t]), dp(ws.shift[t]), dp(ws.zprob[t]), dp(ws.zkl[t]),
+                      dp(ws.skl[t]), dp(ws.shkl[t]), dp(ws.zmask[t]), dp(ws.zval[t]), s)
+            # STN read: canvas -> 28x28 glimpse (air_model.py:523-531)
+            ops.stn_forward(X, ws.th_f[t], (W, W), out=ws.g[t])
+            # glimpse VAE (vae.py:5-48)
+            gemm([ws.g[t]], [vw["recognition_1"]], [ws.a1[t]], B, R1, W2, W2, R1, R1,
+                 epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]], Cpre=[ws.a1pre[t]])
+            gemm([ws.a1[t]], [vw["recognition_2"]], [ws.a2[t]], B, R2, R1, R1, R2, R2,
+                 epi=EPI_SOFTPLUS, bias=[vb["recognition_2"]], Cpre=[ws.a2pre[t]])
+            gemm([ws.a2[t], ws.a2[t]], [vw["rec_mean"], vw["rec_log_variance"]],
+                 [ws.mu[t], ws.lv[t]], B, Z, R2, R2, Z, Z,
+                 bias=[vb["rec_mean"], vb["rec_log_variance"]])
+            _lib.call("mog_vae_sample_forward", B, Z, float(self.vae_prior_mean),
+                      float(self.vae_prior_variance), self.vae_prior_log_variance,
+                      dp(ws.mu[t]), dp(ws.lv[t]), dp(ws.eps_z[t]), dp(ws.z[t]),
+                      dp(ws.zmask[t]), dp(ws.runloss), dp(ws.vkl[t]), s)
+            gemm([ws.z[t]], [vw["generative_1"]], [ws.d1[t]], B, G1, Z, Z, G1, G1,
+                 epi=EPI_SOFTPLUS, bias=[vb["generative_1"]], Cpre=[ws.d1pre[t]])
+            gemm([ws.d1[t]], [vw["generative_2"]], [ws.d2[t]], B, G2, G1, G1, G2, G2,
+                 epi=EPI_SOFTPLUS, bias=[vb["generative_2"]], Cpre=[ws.d2pre[t]])
+            gemm([ws.d2[t]], [vw["gen_mean"]], [ws.r[t]], B, W2, G2, G2, W2, W2,
+                 epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]], Cpre=[ws.mpre[t]],
+                 aux=[ws.eps_x[t]], ldaux=W2, aux_scale=float(lik_std))
+            # STN write + masked canvas accumulation (air_model.py:580-588, 665-675)
+            ops.stn_forward(ws.r[t], ws.th_b[t], (C, C), out=ws.canvas, z=ws.zval[t],
+                            mask=ws.zmask[t], accumulate=True)
+        # reconstruction loss (air_model.py:866-900)
+        gscale = 1.0 / (B * self.grad_world)
+        _lib.call("mog_recon_loss", dp(X), dp(ws.canvas), dp(ws.runloss), dp(ws.digits),
+                  dp(targets), B, C2, float(gscale), dp(ws.recon), dp(ws.bce), dp(ws.mse),
+                  dp(ws.loss_b), dp(ws.acc_b) if targets is not None else None,
+                  dp(ws.dcanvas) if need_grad else None, s)
+        _lib.call("mog_batch_mean", dp(ws.loss_b), dp(ws.acc_b) if targets is not None else None,
+                  dp(ws.mse), None, B, dp(ws.means), s)
+        self._outputs_ready = True
+
+    # ---------------------------------------------------------- backward ---
+    def _backward(self, X: torch.Tensor, ws: _Workspace) -> None:
+        B, T, H = ws.B, self.max_steps, self.rnn_units
+        C, W, C2, W2 = self.canvas_size, self.windows_size, self.C2, self.W2
+        Z = self.vae_latent_dimensions
+        R1, R2 = self.vae_recognition_units
+        G1, G2 = self.vae_generative_units
+        HS = self.scale_hidden_units
+        s = stream_ptr()
+        st = self.params
+        st.grad.zero_()
+        K = self._P("rnn/basic_lstm_cell/kernel")
+        bK = self._P("rnn/basic_lstm_cell/bias")
+        Wh = K[C2:]
+        vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
+        w1 = [self._P(h + "/hidden/weights") for h in self._HEADS]
+        w2 = [self._P(h + "/output/weights") for h in self._HEADS]
+        w2a = _lib.ptr_array([dp(x) for x in w2])
+        gscale = 1.0 / (B * self.grad_world)
+        prior_lo = self.hyper("z_pres_prior_log_odds")
+        temperature = self.hyper("z_pres_temperature")
+        ws.dh[T - 1].zero_()
+        ws.dGsum.zero_()
+        for t in reversed(range(T)):
+            rec = ws.rec[t]
+            # STN write backward: dr, dtheta_back, dot = <dcanvas, w>
+            ops.stn_backward(ws.r[t], ws.th_b[t], (C, C), ws.dcanvas, gscale=rec[R_ZC],
+                             dU=ws.dr, dtheta=ws.dth_b, dot=ws.dot, want_dot=True)
+            _lib.call("mog_sigmoid_backward", dp(ws.r[t]), dp(ws.dr), dp(ws.dm[t]), B * W2, s)
+            gemm([ws.dm[t]], [vw["gen_mean"]], [ws.dd2[t]], B, G2, W2, W2, W2, G2,
+                 transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d2pre[t]], ldaux=G2)
+            gemm([ws.dd2[t]], [vw["generative_2"]], [ws.dd1[t]], B, G1, G2, G2, G2, G1,
+                 transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d1pre[t]], ldaux=G1)
+            gemm([ws.dd1[t]], [vw["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z, transB=True)
+            _lib.call("mog_vae_sample_backward", B, Z, float(self.vae_prior_mean),
+                      float(self.vae_prior_variance), float(gscale), dp(ws.mu[t]),
+                      dp(ws.lv[t]), dp(ws.eps_z[t]), dp(ws.dz), dp(ws.zmask[t]),
+                      dp(ws.dmu[t]), dp(ws.dlv[t]), s)
+            gemm([ws.dmu[t]], [vw["rec_mean"]], [ws.tmp_a2], B, R2, Z, Z, Z, R2, transB=True)
+            gemm([ws.dlv[t]], [vw["rec_log_variance"]], [ws.da2[t]], B, R2, Z, Z, Z, R2,
+                 transB=True, epi=EPI_SOFTPLUS_BWD, Cin=[ws.tmp_a2], aux=[ws.a2pre[t]],
+                 ldaux=R2)
+            gemm([ws.da2[t]], [vw["recognition_2"]], [ws.da1[t]], B, R1, R2, R2, R2, R1,
+                 transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.a1pre[t]], ldaux=R1)
+            gemm([ws.da1[t]], [vw["recognition_1"]], [ws.dg], B, W2, R1, R1, R1, W2,
+                 transB=True)
+            # STN read backward: dtheta only (the canvas input has no gradient)
+            ops.stn_backward(X, ws.th_f[t], (W, W), ws.dg, want_dU=False, dtheta=ws.dth_f)
+            hid_t = [ws.hid[z, t] for z in range(5)]
+            dhid_t = [ws.dhid[z, t] for z in range(5)]
+            _lib.call("mog_air_step_backward", B, HS, int(self.train),
+                      int(self.marginal is not None), temperature, prior_lo,
+                      float(self.marginal[t]) if self.marginal is not None else 0.0,
+                      float(self.scale_prior_mean), float(self.scale_prior_variance),
+                      float(self.shift_prior_mean), float(self.shift_prior_variance),
+                      float(gscale), dp(rec), dp(ws.eps_scale[t]), dp(ws.eps_shift[t]),
+                      dp(ws.dth_f), dp(ws.dth_b), dp(ws.dot),
+                      _lib.ptr_array([dp(x) for x in hid_t]), w2a, dp(ws.dout[0, t]),
+                      T * B * 2, dp(ws.dhid[0, t]), T * B * HS, s)
+            gemm(dhid_t, w1, [ws.dh[t]] * 5, B, H, HS, HS, HS, H, transB=True, epi=EPI_ATOMIC)
+            dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
+            _lib.call("mog_lstm_cell_backward", dp(ws.Gx if t == 0 else ws.G[t]),
+                      dp(bK) if t == 0 else None, dp(ws.c[t - 1]) if t > 0 else None,
+                      dp(ws.c[t]), dp(ws.dh[t]), dp(dc_in), dp(ws.dG[t]), dp(ws.dc[t % 2]),
+                      dp(ws.dGsum), B, H, s)
+            if t > 0:
+                gemm([ws.dG[t]], [Wh], [ws.dh[t - 1]], B, H, 4 * H, 4 * H, 4 * H, H,
+                     transB=True)
+        self._weight_grads(X, ws)
+
+    def _dw(self, X, dY, out, K, M, N, lda, ldb, bias_out=None):
+        """out[M,N] += X^T dY over K rows (split-K, atomics); bias_out += colsum(dY)."""
+        tiles = ((M + 63) // 64) * ((N + 63) // 64)
+        splitk = max(1, min(K // 256, (2048 + tiles - 1) // tiles))
+        gemm([X], [dY], [out], M, N, K, lda, ldb, N, transA=True, epi=EPI_ATOMIC,
+             splitk=splitk)
+        if bias_out is not None:
+            ops.colsum_add(dY, K, N, ldb, bias_out)
+
+    def _weight_grads(self, X, ws):
+        B, T, H = ws.B, self.max_steps, self.rnn_units
+        C2, W2, Z = self.C2, self.W2, self.vae_latent_dimensions
+        R1, R2 = self.vae_recognition_units
+        G1, G2 = self.vae_generative_units
+        HS = self.scale_hidden_units
+        TB = T * B
+        g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
+        gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
+        self._dw(ws.g, ws.da1, g("recognition_1"), TB, W2, R1, W2, R1, gb("recognition_1"))
+        self._dw(ws.a1, ws.da2, g("recognition_2"), TB, R1, R2, R1, R2, gb("recognition_2"))
+        self._dw(ws.a2, ws.dmu, g("rec_mean"), TB, R2, Z, R2, Z, gb("rec_mean"))
+        self._dw(ws.a2, ws.dlv, g("rec_log_variance"), TB, R2, Z, R2, Z, gb("rec_log_variance"))
+        self._dw(ws.z, ws.dd1, g("generative_1"), TB, Z, G1, Z, G1, gb("generative_1"))
+        self._dw(ws.d1, ws.dd2, g("generative_2"), TB, G1, G2, G1, G2, gb("generative_2"))
+        self._dw(ws.d2, ws.dm, g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
+        for zi, head in enumerate(self._HEADS):
+            k = 2 if head.startswith("shift") else 1
+            self._dw(ws.h, ws.dhid[zi], self._G(head + "/hidden/weights"), TB, H, HS, H, HS,
+                     self._G(head + "/hidden/biases"))
+            self._dw(ws.hid[zi], ws.dout[zi], self._G(head + "/output/weights"), TB, HS, k, HS,
+                     2, self._G(head + "/output/biases"))
+        gK = self._G("rnn/basic_lstm_cell/kernel")
+        gbK = self._G("rnn/basic_lstm_cell/bias")
+        if T > 1:
+            self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
+        self._dw(X, ws.dGsum, gK[:C2], B, C2, 4 * H, C2, 4 * H)
+        ops.colsum_add(ws.dG, TB, 4 * H, 4 * H, gbK)
+
+    # ------------------------------------------------------------- API ----
+    def _prep(self, images, targets):
+        X = torch.as_tensor(images, dtype=torch.float32).to(self.device).reshape(-1, self.C2)
+        X = X.contiguous()
+        tg = None
+        if targets is not None:
+            tg = torch.as_tensor(targets).to(self.device, torch.int32).contiguous()
+        return X, tg
+
+    def train_step_async(self, images, targets=None, noise=None) -> None:
+        """One train step (forward, backward, [all-reduce hook], clip, Adam)
+        with no host synchronisation."""
+        if not self.train:
+            raise RuntimeError("train_step on a model built with train=False")
+        X, tg = self._prep(images, targets)
+        ws = self._workspace(X.shape[0])
+        ws.alloc_backward(self)
+        self._fill_noise(ws, noise)
+        self._forward(X, tg, ws, need_grad=True)
+        self._backward(X, ws)
+        if self.grad_hook is not None:
+            self.grad_hook(self.params.grad)
+        self.params.apply_adam(self.hyper("learning_rate"), self.gradient_clipping_norm)
+        self.params.global_step += 1
+        self._X = X
+
+    grad_hook = None  # e.g. data-parallel all-reduce of params.grad (SUM)
+
+    def step(self, images, targets=None, noise=None):
+        """``sess.run([training, loss, accuracy, mse_loss, global_step])``
+        (training_air_original.py:304-310)."""
+        self.train_step_async(images, targets, noise)
+        m = self._ws.means.detach().cpu().numpy()
+        return float(m[0]), float(m[1]), float(m[2]), self.params.global_step
+
+    def compute_gradients(self, images, targets=None, noise=None, canvas_cotangent=None):
+        """Forward + backward only (no optimizer update); returns the gradient
+        dict.  ``canvas_cotangent`` [B, C*C] replaces dL/dcanvas of the BCE
+        term (used by the gradient parity tests)."""
+        X, tg = self._prep(images, targets)
+        ws = self._workspace(X.shape[0])
+        ws.alloc_backward(self)
+        self._fill_noise(ws, noise)
+        self._forward(X, tg, ws, need_grad=True)
+        if canvas_cotangent is not None:
+            ws.dcanvas.copy_(torch.as_tensor(canvas_cotangent, dtype=torch.float32))
+        self._backward(X, ws)
+        return self.params.grad_dict()
+
+    def infer(self, images, targets=None, noise=None):
+        """Forward pass only (the test model's fetches)."""
+        X, tg = self._prep(images, targets)
+        ws = self._workspace(X.shape[0])
+        self._fill_noise(ws, noise)
+        self._forward(X, tg, ws, need_grad=False)
+        self._X = X
+        return self
+
+    # ------------------------------------------------------- outputs -------
+    def _T(self) -> int:
+        live = self._ws.live.detach().cpu().numpy()
+        return int(live[: self.max_steps].sum())
+
+    def _bt(self, t: torch.Tensor) -> torch.Tensor:
+        T = self._T()
+        return t[:T].transpose(0, 1)
+
+    @property
+    def executed_steps(self) -> int:
+        return self._T()
+
+    @property
+    def loss(self):
+        return float(self._ws.means[0])
+
+    @property
+    def accuracy(self):
+        return float(self._ws.means[1])
+
+    @property
+    def mse_loss(self):
+        return float(self._ws.means[2])
+
+    @property
+    def rec_num_digits(self):
+        return self._ws.digits
+
+    @property
+    def accuracy_instance(self):
+        return self._ws.acc_b
+
+    @property
+    def rec_scales(self):
+        return self._bt(self._ws.scale).unsqueeze(-1)
+
+    @property
+    def rec_shifts(self):
+        return self._bt(self._ws.shift)
+
+    @property
+    def rec_st_back(self):
+        return self._bt(self._ws.th_b).reshape(self._ws.B, -1, 2, 3)
+
+    @property
+    def rec_windows(self):
+        return self._bt(self._ws.r)
+
+    @property
+    def rec_latents(self):
+        return self._bt(self._ws.z)
+
+    @property
+    def z_pres_probs(self):
+        return self._bt(self._ws.zprob)
+
+    @property
+    def z_pres_kls(self):
+        return self._bt(self._ws.zkl)
+
+    @property
+    def scale_kls(self):
+        return self._bt(self._ws.skl)
+
+    @property
+    def shift_kls(self):
+        return self._bt(self._ws.shkl)
+
+    @property
+    def vae_kls(self):
+        return self._bt(self._ws.vkl)
+
+    @property
+    def reconstruction(self):
+        return self._ws.recon
+
+    @property
+    def reconstruction_loss(self):
+        return self._ws.bce
+
+    @property
+    def canvas(self):
+        return self._ws.canvas
+
+    @property
+    def per_image_loss(self):
+        return self._ws.loss_b

@@ -1,0 +1,125 @@
+"""Typed wrappers of the HIP entry points over torch device tensors.
+
+torch supplies device memory and the current HIP stream only; every
+computation below is a launch of libmog_air.so.  Arguments are validated
+here (device, dtype, contiguity, shape) before any launch, so a shape error
+never reaches a kernel."""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+
+EPI_STORE, EPI_RELU, EPI_SOFTPLUS, EPI_SIGMOID_NOISE = 0, 1, 2, 3
+EPI_SOFTPLUS_BWD, EPI_ATOMIC, EPI_RELU_BWD = 4, 5, 6
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dp(t: Optional[torch.Tensor]):
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def _chk(t: torch.Tensor, name: str, dtype=torch.float32):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a HIP device tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def gemm(A: Sequence[torch.Tensor], B: Sequence[torch.Tensor], C: Sequence[torch.Tensor],
+         M: int, N: int, K: int, lda: int, ldb: int, ldc: int, transA=False, transB=False,
+         epi=EPI_STORE, bias=None, Cin=None, Cpre=None, aux=None, ldaux=0,
+         aux_scale=0.0, splitk=1) -> None:
+    """Batched fp32 MFMA GEMM (see mog_gemm_f32).  A/B/C are sequences of
+    tensors (or views) whose data_ptr is the matrix origin."""
+    nb = len(C)
+    assert len(A) == nb and len(B) == nb and 1 <= nb <= 8
+
+    def arr(xs):
+        if xs is None:
+            return None
+        return _lib.ptr_array([dp(x) for x in xs])
+
+    _lib.call("mog_gemm_f32", nb, arr(A), arr(B), arr(C), arr(bias), arr(Cin), arr(Cpre),
+              arr(aux), M, N, K, lda, ldb, ldc, ldaux, int(transA), int(transB), epi,
+              float(aux_scale), int(splitk), stream_ptr())
+
+
+def dense(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor,
+          epi=EPI_STORE, pre: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = act(x @ w + b), one k-ordered fp32 chain per output."""
+    M, K = x.shape
+    K2, N = w.shape
+    assert K == K2 and out.shape == (M, N)
+    gemm([x], [w], [out], M, N, K, K, N, N, epi=epi, bias=None if b is None else [b],
+         Cpre=None if pre is None else [pre])
+    return out
+
+
+def stn_forward(U: torch.Tensor, theta: torch.Tensor, out_hw, out: Optional[torch.Tensor] = None,
+                z: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
+                accumulate: bool = False) -> torch.Tensor:
+    """transformer() of air/transformer.py:18 for U [N,Hin,Win] (or [N,Hin*Win] with
+    Hin=Win) and theta [N,6]."""
+    _chk(U, "U")
+    _chk(theta, "theta")
+    N = U.shape[0]
+    if U.dim() == 3:
+        Hin, Win = U.shape[1], U.shape[2]
+    else:
+        Hin = Win = int(round(U.shape[1] ** 0.5))
+        assert Hin * Win == U.shape[1]
+    Ho, Wo = out_hw
+    assert theta.shape == (N, 6)
+    if out is None:
+        out = torch.empty((N, Ho * Wo), device=U.device, dtype=torch.float32)
+    assert out.numel() == N * Ho * Wo
+    if accumulate:
+        assert z is not None and mask is not None and z.shape == (N,) and mask.shape == (N,)
+    _lib.call("mog_stn_forward", dp(U), N, Hin, Win, dp(theta), Ho, Wo, dp(out), dp(z), dp(mask),
+              int(accumulate), stream_ptr())
+    return out
+
+
+def stn_backward(U: torch.Tensor, theta: torch.Tensor, out_hw, G: torch.Tensor,
+                 gscale: Optional[torch.Tensor] = None, want_dU=True, want_dtheta=True,
+                 want_dot=False, dU=None, dtheta=None, dot=None):
+    _chk(U, "U")
+    _chk(G, "G")
+    N = U.shape[0]
+    if U.dim() == 3:
+        Hin, Win = U.shape[1], U.shape[2]
+    else:
+        Hin = Win = int(round(U.shape[1] ** 0.5))
+    Ho, Wo = out_hw
+    assert G.numel() == N * Ho * Wo
+    dev = U.device
+    if want_dU and dU is None:
+        dU = torch.empty((N, Hin * Win), device=dev, dtype=torch.float32)
+    if want_dtheta and dtheta is None:
+        dtheta = torch.empty((N, 6), device=dev, dtype=torch.float32)
+    if want_dot and dot is None:
+        dot = torch.empty((N,), device=dev, dtype=torch.float32)
+    _lib.call("mog_stn_backward", dp(U), N, Hin, Win, dp(theta), Ho, Wo, dp(G), dp(gscale),
+              dp(dU if want_dU else None), dp(dtheta if want_dtheta else None),
+              dp(dot if want_dot else None), stream_ptr())
+    return dU, dtheta, dot
+
+
+def colsum_add(X: torch.Tensor, R: int, N: int, ld: int, out: torch.Tensor) -> None:
+    _lib.call("mog_colsum_add", dp(X), R, N, ld, dp(out), stream_ptr())
+
+
+def rng_fill(out: torch.Tensor, seed: int, offset: int, normal: bool) -> None:
+    _chk(out, "out")
+    _lib.call("mog_rng_fill", dp(out), out.numel(), seed & (2 ** 64 - 1),
+              offset & (2 ** 64 - 1), int(normal), stream_ptr())

@@ -274,6 +274,20 @@ def stn(U: np.ndarray, theta: np.ndarray, out_hw: Tuple[int, int]) -> np.ndarray
     return out
 
 
+def dense_chain(x: np.ndarray, w: np.ndarray, b: Optional[np.ndarray] = None) -> np.ndarray:
+    """out = chain_k(x w) (+ b): one fp32 fma chain per output in k order."""
+    lib = _load()
+    x = np.ascontiguousarray(x, np.float32)
+    w = np.ascontiguousarray(w, np.float32)
+    B, K = x.shape
+    N = w.shape[1]
+    out = np.zeros((B, N), np.float32)
+    bb = None if b is None else np.ascontiguousarray(b, np.float32)
+    lib.oracle_dense(_ptr(x), ctypes.c_int(B), ctypes.c_int(K), _ptr(w),
+                     None if bb is None else _ptr(bb), ctypes.c_int(N), _ptr(out))
+    return out
+
+
 def concrete_kl(y, plo, pT, qlo, qT) -> float:
     return float(_load().oracle_concrete_kl(y, plo, pT, qlo, qT))
 

@@ -390,3 +390,20 @@ void oracle_math_vec(int fn, const float* x, float* y, int n) {
     }
   }
 }
+
+/* exported k-ordered dense layer (parity check of the MFMA GEMM) */
+void oracle_dense(const float* in, int B, int K, const float* w, const float* bias, int N,
+                  float* out) {
+  static const float zero = 0.0f;
+  (void)zero;
+  if (bias) {
+    dense(in, B, K, w, bias, N, out);
+  } else {
+    for (int b = 0; b < B; ++b)
+      for (int n = 0; n < N; ++n) {
+        float acc = 0.0f;
+        for (int k = 0; k < K; ++k) acc = fmaf(in[(size_t)b * K + k], w[(size_t)k * N + n], acc);
+        out[(size_t)b * N + n] = acc;
+      }
+  }
+}

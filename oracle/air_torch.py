@@ -247,7 +247,7 @@ def train_step(cfg: AirConfig, P, m, v, t, noise, images, targets, prior_lo):
     out["loss"].backward()
     grads = {k: p_.grad if p_.grad is not None else torch.zeros_like(p_) for k, p_ in P.items()}
     tf_clip_adam_step(P, grads, m, v, t)
-    return float(out["loss"])
+    return float(out["loss"].detach())
 
 
 __all__ = ["transformer", "air_forward", "tf_clip_adam_step", "to_torch", "train_step",

@@ -1,0 +1,93 @@
+"""CPU tests of the host side: the C ABI library loads and exports every
+symbol declared in include/*.h (no compute call without a GPU), and the host
+logic (parameter table, annealing, -ap prior) restates the reference like the
+oracle does."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import air_oracle as ao
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    from mog_air import _lib
+    lib = _lib.load()
+    syms = _lib.header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), s
+    # every declared symbol has a ctypes signature and vice versa
+    assert set(syms) == set(_lib._SIGS)
+
+
+def test_all_headers_symbols_exported():
+    from mog_air import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    inc = os.path.join(ROOT, "include")
+    for fn in os.listdir(inc):
+        src = open(os.path.join(inc, fn)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for name in re.findall(r"\bint\s+(mog_\w+)\s*\(", src):
+            assert hasattr(lib, name), (fn, name)
+
+
+def test_host_only_entry_point():
+    from mog_air import _lib
+    assert _lib.load().mog_optim_chunk_elems() == 4096
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    from mog_air import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(_lib.MogError):
+        _lib.load()
+
+
+def test_param_specs_match_oracle():
+    from mog_air.params import param_specs
+    cfg = ao.AirConfig()
+    mine = param_specs(2500, 256, 784, (512, 256), (256, 512), 50, 64, 64)
+    assert mine == ao.param_specs(cfg)
+    n = sum(int(np.prod(s)) for _, s in mine)
+    assert n == 4011643  # SURVEY.md §0 parameter count
+
+
+def test_param_store_layout_cpu():
+    from mog_air.params import ParamStore, param_specs
+    specs = param_specs(2500, 256, 784, (512, 256), (256, 512), 50, 64, 64)
+    st = ParamStore(specs, torch.device("cpu"), seed=1)
+    for name, shape in specs:
+        assert st.offsets[name] % 64 == 0
+        assert tuple(st.view(name).shape) == tuple(shape)
+    d = st.state_dict()
+    st.load_dict({k: v * 0 + 1 for k, v in d.items()})
+    assert float(st.flat.sum()) == st.n_params
+    assert st.n_blocks == sum(-(-int(np.prod(s)) // 4096) for _, s in specs)
+
+
+def test_annealing_matches_oracle():
+    from mog_air.air_model import annealed_value
+    sched = {"init": 10000.0, "min": 1e-9, "factor": 0.1, "iters": 3000,
+             "staircase": False, "log": True}
+    for step in (0, 1, 100, 3000, 12345, 40000, 10 ** 6):
+        assert annealed_value(sched, step) == float(ao.annealed_log_odds(step))
+
+
+def test_marginal_objective_matches_oracle():
+    from mog_air.air_model import marginal_objective
+    for prior, T in (((1, 3), 4), ((1, 2, 3), 6), ((2, 4), 6), ((3,), 6)):
+        np.testing.assert_array_equal(marginal_objective(prior, T),
+                                      ao.marginal_objective(prior, T))
+
+
+def test_model_rejects_cpu_device():
+    from mog_air.air_model import AIRModel
+    with pytest.raises(RuntimeError):
+        AIRModel(cnn=False, device="cpu")
