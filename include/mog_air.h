@@ -31,12 +31,14 @@ extern "C" {
  * epi: 0 store(+bias) 1 relu 2 softplus(TF) 3 sigmoid(acc+bias+aux*aux_scale)
  *      4 acc*sigmoid(aux) 5 atomic-add 6 relu-backward (aux = activation).
  * With splitk == 1 every output is one k-ordered fp32 fma chain (bit-exact
- * with the oracle).  splitk > 1 requires epi 5. */
+ * with the oracle).  splitk > 1 requires epi 5.  colsum (epi 5 only, may be
+ * NULL): colsum[z][n] += sum_k B_z(k, n) — the bias gradient of a weight-
+ * gradient GEMM dW = X^T dY (TF BiasAddGrad), fused. */
 int mog_gemm_f32(int batch, const float* const* A, const float* const* B, float* const* C,
                  const float* const* bias, const float* const* Cin, float* const* Cpre,
-                 const float* const* aux, int M, int N, int K, int lda, int ldb, int ldc,
-                 int ldaux, int transA, int transB, int epi, float aux_scale, int splitk,
-                 void* stream);
+                 const float* const* aux, float* const* colsum, int M, int N, int K, int lda,
+                 int ldb, int ldc, int ldaux, int transA, int transB, int epi, float aux_scale,
+                 int splitk, void* stream);
 
 /* ---- spatial transformer -------------------------------------------------
  * air/transformer.py:18-175 transformer(U, theta, out_size) for N images:

@@ -146,19 +146,29 @@ struct StepFwdIO {
   float* zval;             // [B] z_pres value (canvas coefficient)
 };
 
+// 8 lanes per image: lanes 0..6 each evaluate one head-output fma chain
+// (scale-mean, scale-logvar, shift-mean x/y, shift-logvar x/y, z_pres
+// log-odds), lane 0 then runs the scalar step logic.
 __global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp, StepFwdIO io) {
 #pragma clang fp contract(off)
-  const int b = blockIdx.x * 256 + threadIdx.x;
   const int B = cfg.B;
-  if (b >= B) return;
+  const int b = blockIdx.x * 32 + (threadIdx.x >> 3);
+  const int j = threadIdx.x & 7;
   const int HS = cfg.HS, HZ = cfg.HZ;
-  const float sm = chain_dot(hp.hid[0] + (size_t)b * HS, hp.w2[0], HS, 1) + hp.b2[0][0];
-  const float slv = chain_dot(hp.hid[1] + (size_t)b * HS, hp.w2[1], HS, 1) + hp.b2[1][0];
-  const float hm0 = chain_dot(hp.hid[2] + (size_t)b * HS, hp.w2[2], HS, 2) + hp.b2[2][0];
-  const float hm1 = chain_dot(hp.hid[2] + (size_t)b * HS, hp.w2[2] + 1, HS, 2) + hp.b2[2][1];
-  const float hv0 = chain_dot(hp.hid[3] + (size_t)b * HS, hp.w2[3], HS, 2) + hp.b2[3][0];
-  const float hv1 = chain_dot(hp.hid[3] + (size_t)b * HS, hp.w2[3] + 1, HS, 2) + hp.b2[3][1];
-  const float lo = chain_dot(hp.hid[4] + (size_t)b * HZ, hp.w2[4], HZ, 1) + hp.b2[4][0];
+  // lane -> (head, output column, width of that head's output)
+  const int head = j == 0 ? 0 : j == 1 ? 1 : j <= 3 ? 2 : j <= 5 ? 3 : 4;
+  const int col = (j == 3 || j == 5) ? 1 : 0;
+  const int kw = (head == 2 || head == 3) ? 2 : 1;
+  float v = 0.0f;
+  if (b < B && j < 7) {
+    const int K = head == 4 ? HZ : HS;
+    v = chain_dot(hp.hid[head] + (size_t)b * K, hp.w2[head] + col, K, kw) + hp.b2[head][col];
+  }
+  const float sm = __shfl(v, 0, 8), slv = __shfl(v, 1, 8);
+  const float hm0 = __shfl(v, 2, 8), hm1 = __shfl(v, 3, 8);
+  const float hv0 = __shfl(v, 4, 8), hv1 = __shfl(v, 5, 8);
+  const float lo = __shfl(v, 6, 8);
+  if (b >= B || j != 0) return;
 
   // scale / shift sampling (air_model.py:471-477, :492-498; :186-192)
   const float svar = mog_expf(slv);
@@ -333,22 +343,28 @@ struct VaeCfg {
   float v_pm, v_pv, v_plv, grad_scale;
 };
 
-// z = mu + eps*sqrt(exp(lv)); vkl = 0.5*sum_k term_k (sequential); runloss += act ? vkl : 0
+// z = mu + eps*sqrt(exp(lv)); vkl = 0.5*sum_k term_k (sequential in k);
+// runloss += act ? vkl : 0.  One wave per image: lane k owns latent k, lane 0
+// then sums the KL terms in k order (Z <= 64).
 __global__ __launch_bounds__(256) void vae_sample_fwd_kernel(VaeCfg c, const float* mu,
                                                              const float* lv, const float* eps,
                                                              float* z, const float* act,
                                                              float* runloss, float* vkl_out) {
 #pragma clang fp contract(off)
-  const int b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= c.B) return;
-  float sum = 0.0f;
-  for (int k = 0; k < c.Z; ++k) {
+  __shared__ float terms[4][64];
+  const int w = threadIdx.x >> 6, k = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + w;
+  if (b < c.B && k < c.Z) {
     const size_t i = (size_t)b * c.Z + k;
     const float l = lv[i];
     const float var = mog_expf(l);
     z[i] = mu[i] + eps[i] * sqrtf(var);
-    sum = sum + gauss_kl_term(c.v_plv, l, var, c.v_pv, mu[i], c.v_pm);
+    terms[w][k] = gauss_kl_term(c.v_plv, l, var, c.v_pv, mu[i], c.v_pm);
   }
+  __syncthreads();
+  if (b >= c.B || k != 0) return;
+  float sum = 0.0f;
+  for (int q = 0; q < c.Z; ++q) sum = sum + terms[w][q];
   const float vkl = 0.5f * sum;
   vkl_out[b] = vkl;
   if (act[b] != 0.0f) runloss[b] = runloss[b] + vkl;
@@ -394,8 +410,10 @@ __global__ __launch_bounds__(256) void recon_loss_kernel(
     const float c = cb[p];
     const float r = fmaxf(fminf(c, 1.0f), 0.0f);
     const float xv = xb[p];
-    const float lr = mog_logf(r + 1e-10f);
-    const float l1r = mog_logf((1.0f - r) + 1e-10f);
+    // the BCE is a 2500-term reduction compared within 1e-5 relative, so the
+    // hardware log (v_log_f32, ~1 ulp) is used here, not the bit-exact spec
+    const float lr = __logf(r + 1e-10f);
+    const float l1r = __logf((1.0f - r) + 1e-10f);
     bce = bce + (xv * lr + (1.0f - xv) * l1r);
     const float d = xv - r;
     mse = mse + d * d;
@@ -500,7 +518,7 @@ extern "C" int mog_air_step_forward(
   StepFwdIO io{eps_scale, eps_shift, u,       stop,     runloss,  digits,    live,
                rec,       theta_fwd, theta_back, scale_out, shift_out, zprob_out, zkl_out,
                skl_out,   shkl_out,  zmask,   zval};
-  step_fwd_kernel<<<mog_cdiv(B, 256), 256, 0, mog_stream(stream)>>>(c, hp, io);
+  step_fwd_kernel<<<mog_cdiv(B, 32), 256, 0, mog_stream(stream)>>>(c, hp, io);
   MOG_LAUNCH_RET();
 }
 
@@ -538,11 +556,11 @@ extern "C" int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, floa
                                       const float* mu, const float* lv, const float* eps,
                                       float* z, const float* act, float* runloss, float* vkl,
                                       void* stream) {
-  MOG_CHECK_ARG(B >= 0 && Z > 0 && mu && lv && eps && z && act && runloss && vkl);
+  MOG_CHECK_ARG(B >= 0 && Z > 0 && Z <= 64 && mu && lv && eps && z && act && runloss && vkl);
   if (B == 0) return 0;
   VaeCfg c{B, Z, v_pm, v_pv, v_plv, 0.0f};
-  vae_sample_fwd_kernel<<<mog_cdiv(B, 256), 256, 0, mog_stream(stream)>>>(c, mu, lv, eps, z, act,
-                                                                         runloss, vkl);
+  vae_sample_fwd_kernel<<<mog_cdiv(B, 4), 256, 0, mog_stream(stream)>>>(c, mu, lv, eps, z, act,
+                                                                       runloss, vkl);
   MOG_LAUNCH_RET();
 }
 

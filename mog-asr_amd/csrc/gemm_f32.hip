@@ -1,7 +1,7 @@
 // Generic fp32 GEMM on the gfx950 fp32-input MFMA (v_mfma_f32_16x16x4_f32).
 //
 // C[m][n] = epilogue( chain_k A(m,k) B(k,n) ), optionally batched over up to
-// MOG_GEMM_MAXB independent problems (pointer arrays) and split over K.
+// MAXB independent problems (pointer arrays) and split over K.
 //
 // Bit-exactness contract: with splitk == 1 each output
 // element is ONE fp32 fma chain over k in natural order, starting from 0 (or
@@ -9,6 +9,15 @@
 // a k-ordered fma chain on gfx950 and the k loop below walks k upward.  The
 // bias is added with a separate rounding (TF matmul + bias_add,
 // contrib/layers fully_connected as used at vae.py:18-41, air_model.py:462-499).
+//
+// Tiles: 64x64 or 128x128 per 256-thread workgroup (2x2 waves, each wave
+// (BM/2)x(BN/2) of 16x16 MFMA tiles), BK = 16, register-staged double
+// buffering (next tile's global loads in flight during the MFMAs).
+//
+// Weight-gradient form: transA + EPI_ATOMIC + split-K computes dW += X^T dY;
+// when `colsum` is given the workgroups of the first M-tile row also add the
+// column sums of their dY tiles into colsum[n] (the bias gradient, TF
+// BiasAddGrad), so no separate reduction pass re-reads dY.
 //
 // Replaces the TF-1.12 MatMul / BiasAdd / Softplus / Relu / Sigmoid op groups
 // of the hot path (SURVEY.md §2 table "TF op group on the hot path").
@@ -35,17 +44,20 @@ struct GemmPtrs {
   const float* Cin[MAXB];
   float* Cpre[MAXB];
   const float* aux[MAXB];
+  float* colsum[MAXB];
 };
 struct GemmDims {
   int M, N, K, lda, ldb, ldc, ldaux, splitk, kchunk, vecA, vecB;
   float aux_scale;
 };
 
-constexpr int BM = 64, BN = 64, BK = 16, PADF = 16;
+constexpr int BK = 16, PADF = 16;
 
-template <bool TA, bool TB, int EPI>
+template <int BM, int BN, bool TA, bool TB, int EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
 #pragma clang fp contract(off)
+  constexpr int MI = BM / 32, NI = BN / 32;     // 16x16 tiles per wave
+  constexpr int NA = BM / 64, NB = BN / 64;     // float4 loads per thread
   __shared__ float As[BK][BM + PADF];
   __shared__ float Bs[BK][BN + PADF];
   const int z = blockIdx.z / D.splitk, ks = blockIdx.z - z * D.splitk;
@@ -55,15 +67,18 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
   const int kbeg = ks * D.kchunk;
   const int kend = min(D.K, kbeg + D.kchunk);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
   const int M = D.M, N = D.N;
+  float* colsum = P.colsum[z];
+  const bool do_cs = colsum != nullptr && blockIdx.y == 0 && t < BN;
+  float cs = 0.0f;
 
-  floatx4 acc[2][2];
+  floatx4 acc[MI][NI];
   const float* Cin = P.Cin[z];
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
+    for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = 0.0f;
@@ -75,73 +90,89 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
         acc[mi][ni][r] = v;
       }
 
-  float ra[4], rb[4];
+  float ra[NA][4], rb[NB][4];
   auto load_tiles = [&](int k0) {
-    // ---- A tile: BM x BK ----
-    if (!TA) {
-      const int row = t >> 2, kc = (t & 3) * 4;
-      const int gm = m0 + row, gk = k0 + kc;
-      if (D.vecA && gm < M && gk + 3 < kend) {
-        const float4 v = *reinterpret_cast<const float4*>(A + (size_t)gm * D.lda + gk);
-        ra[0] = v.x; ra[1] = v.y; ra[2] = v.z; ra[3] = v.w;
-      } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          ra[i] = (gm < M && gk + i < kend) ? A[(size_t)gm * D.lda + gk + i] : 0.0f;
-      }
-    } else {
-      const int k = t >> 4, mc = (t & 15) * 4;
-      const int gk = k0 + k, gm = m0 + mc;
-      if (D.vecA && gk < kend && gm + 3 < M) {
-        const float4 v = *reinterpret_cast<const float4*>(A + (size_t)gk * D.lda + gm);
-        ra[0] = v.x; ra[1] = v.y; ra[2] = v.z; ra[3] = v.w;
-      } else {
+    for (int i = 0; i < NA; ++i) {
+      const int q = t + 256 * i;
+      if (!TA) {
+        const int row = q >> 2, kc = (q & 3) * 4;
+        const int gm = m0 + row, gk = k0 + kc;
+        if (D.vecA && gm < M && gk + 3 < kend) {
+          const float4 v = *reinterpret_cast<const float4*>(A + (size_t)gm * D.lda + gk);
+          ra[i][0] = v.x; ra[i][1] = v.y; ra[i][2] = v.z; ra[i][3] = v.w;
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          ra[i] = (gk < kend && gm + i < M) ? A[(size_t)gk * D.lda + gm + i] : 0.0f;
+          for (int j = 0; j < 4; ++j)
+            ra[i][j] = (gm < M && gk + j < kend) ? A[(size_t)gm * D.lda + gk + j] : 0.0f;
+        }
+      } else {
+        const int k = q / (BM / 4), mc = (q % (BM / 4)) * 4;
+        const int gk = k0 + k, gm = m0 + mc;
+        if (D.vecA && gk < kend && gm + 3 < M) {
+          const float4 v = *reinterpret_cast<const float4*>(A + (size_t)gk * D.lda + gm);
+          ra[i][0] = v.x; ra[i][1] = v.y; ra[i][2] = v.z; ra[i][3] = v.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            ra[i][j] = (gk < kend && gm + j < M) ? A[(size_t)gk * D.lda + gm + j] : 0.0f;
+        }
       }
     }
-    // ---- B tile: BK x BN ----
-    if (!TB) {
-      const int k = t >> 4, nc = (t & 15) * 4;
-      const int gk = k0 + k, gn = n0 + nc;
-      if (D.vecB && gk < kend && gn + 3 < N) {
-        const float4 v = *reinterpret_cast<const float4*>(Bm + (size_t)gk * D.ldb + gn);
-        rb[0] = v.x; rb[1] = v.y; rb[2] = v.z; rb[3] = v.w;
-      } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          rb[i] = (gk < kend && gn + i < N) ? Bm[(size_t)gk * D.ldb + gn + i] : 0.0f;
-      }
-    } else {
-      const int n = t >> 2, kc = (t & 3) * 4;
-      const int gn = n0 + n, gk = k0 + kc;
-      if (D.vecB && gn < N && gk + 3 < kend) {
-        const float4 v = *reinterpret_cast<const float4*>(Bm + (size_t)gn * D.ldb + gk);
-        rb[0] = v.x; rb[1] = v.y; rb[2] = v.z; rb[3] = v.w;
-      } else {
+    for (int i = 0; i < NB; ++i) {
+      const int q = t + 256 * i;
+      if (!TB) {
+        const int k = q / (BN / 4), nc = (q % (BN / 4)) * 4;
+        const int gk = k0 + k, gn = n0 + nc;
+        if (D.vecB && gk < kend && gn + 3 < N) {
+          const float4 v = *reinterpret_cast<const float4*>(Bm + (size_t)gk * D.ldb + gn);
+          rb[i][0] = v.x; rb[i][1] = v.y; rb[i][2] = v.z; rb[i][3] = v.w;
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          rb[i] = (gn < N && gk + i < kend) ? Bm[(size_t)gn * D.ldb + gk + i] : 0.0f;
+          for (int j = 0; j < 4; ++j)
+            rb[i][j] = (gk < kend && gn + j < N) ? Bm[(size_t)gk * D.ldb + gn + j] : 0.0f;
+        }
+      } else {
+        const int n = q >> 2, kc = (q & 3) * 4;
+        const int gn = n0 + n, gk = k0 + kc;
+        if (D.vecB && gn < N && gk + 3 < kend) {
+          const float4 v = *reinterpret_cast<const float4*>(Bm + (size_t)gn * D.ldb + gk);
+          rb[i][0] = v.x; rb[i][1] = v.y; rb[i][2] = v.z; rb[i][3] = v.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            rb[i][j] = (gn < N && gk + j < kend) ? Bm[(size_t)gn * D.ldb + gk + j] : 0.0f;
+        }
       }
     }
   };
   auto store_tiles = [&]() {
-    if (!TA) {
-      const int row = t >> 2, kc = (t & 3) * 4;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) As[kc + i][row] = ra[i];
-    } else {
-      const int k = t >> 4, mc = (t & 15) * 4;
-      *reinterpret_cast<float4*>(&As[k][mc]) = make_float4(ra[0], ra[1], ra[2], ra[3]);
+    for (int i = 0; i < NA; ++i) {
+      const int q = t + 256 * i;
+      if (!TA) {
+        const int row = q >> 2, kc = (q & 3) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) As[kc + j][row] = ra[i][j];
+      } else {
+        const int k = q / (BM / 4), mc = (q % (BM / 4)) * 4;
+        *reinterpret_cast<float4*>(&As[k][mc]) =
+            make_float4(ra[i][0], ra[i][1], ra[i][2], ra[i][3]);
+      }
     }
-    if (!TB) {
-      const int k = t >> 4, nc = (t & 15) * 4;
-      *reinterpret_cast<float4*>(&Bs[k][nc]) = make_float4(rb[0], rb[1], rb[2], rb[3]);
-    } else {
-      const int n = t >> 2, kc = (t & 3) * 4;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) Bs[kc + i][n] = rb[i];
+    for (int i = 0; i < NB; ++i) {
+      const int q = t + 256 * i;
+      if (!TB) {
+        const int k = q / (BN / 4), nc = (q % (BN / 4)) * 4;
+        *reinterpret_cast<float4*>(&Bs[k][nc]) =
+            make_float4(rb[i][0], rb[i][1], rb[i][2], rb[i][3]);
+      } else {
+        const int n = q >> 2, kc = (q & 3) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Bs[kc + j][n] = rb[i][j];
+      }
     }
   };
 
@@ -155,14 +186,20 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
 #pragma unroll
       for (int kk = 0; kk < BK / 4; ++kk) {
         const int k = kk * 4 + (lane >> 4);
-        const float a0 = As[k][wm + (lane & 15)];
-        const float a1 = As[k][wm + 16 + (lane & 15)];
-        const float b0 = Bs[k][wn + (lane & 15)];
-        const float b1 = Bs[k][wn + 16 + (lane & 15)];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+        float a[MI], b[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) a[mi] = As[k][wm + mi * 16 + (lane & 15)];
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) b[ni] = Bs[k][wn + ni * 16 + (lane & 15)];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+      }
+      if (do_cs) {
+#pragma unroll
+        for (int k = 0; k < BK; ++k) cs += Bs[k][t];
       }
       __syncthreads();
       if (has_next) {
@@ -171,15 +208,16 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
       }
     }
   }
+  if (do_cs && n0 + t < N) atomicAdd(colsum + n0 + t, cs);
 
   float* C = P.C[z];
   const float* bias = P.bias[z];
   const float* aux = P.aux[z];
   float* Cpre = P.Cpre[z];
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
+    for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm + mi * 16 + (lane >> 4) * 4 + r;
@@ -212,19 +250,37 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
       }
 }
 
-template <bool TA, bool TB>
+template <int BM, int BN, bool TA, bool TB>
 void launch_epi(int epi, dim3 g, hipStream_t s, const GemmPtrs& P, const GemmDims& D) {
   switch (epi) {
-    case EPI_STORE: gemm_f32_kernel<TA, TB, EPI_STORE><<<g, 256, 0, s>>>(P, D); break;
-    case EPI_RELU: gemm_f32_kernel<TA, TB, EPI_RELU><<<g, 256, 0, s>>>(P, D); break;
-    case EPI_SOFTPLUS: gemm_f32_kernel<TA, TB, EPI_SOFTPLUS><<<g, 256, 0, s>>>(P, D); break;
+    case EPI_STORE: gemm_f32_kernel<BM, BN, TA, TB, EPI_STORE><<<g, 256, 0, s>>>(P, D); break;
+    case EPI_RELU: gemm_f32_kernel<BM, BN, TA, TB, EPI_RELU><<<g, 256, 0, s>>>(P, D); break;
+    case EPI_SOFTPLUS:
+      gemm_f32_kernel<BM, BN, TA, TB, EPI_SOFTPLUS><<<g, 256, 0, s>>>(P, D); break;
     case EPI_SIGMOID_NOISE:
-      gemm_f32_kernel<TA, TB, EPI_SIGMOID_NOISE><<<g, 256, 0, s>>>(P, D); break;
+      gemm_f32_kernel<BM, BN, TA, TB, EPI_SIGMOID_NOISE><<<g, 256, 0, s>>>(P, D); break;
     case EPI_SOFTPLUS_BWD:
-      gemm_f32_kernel<TA, TB, EPI_SOFTPLUS_BWD><<<g, 256, 0, s>>>(P, D); break;
-    case EPI_ATOMIC: gemm_f32_kernel<TA, TB, EPI_ATOMIC><<<g, 256, 0, s>>>(P, D); break;
-    case EPI_RELU_BWD: gemm_f32_kernel<TA, TB, EPI_RELU_BWD><<<g, 256, 0, s>>>(P, D); break;
+      gemm_f32_kernel<BM, BN, TA, TB, EPI_SOFTPLUS_BWD><<<g, 256, 0, s>>>(P, D); break;
+    case EPI_ATOMIC: gemm_f32_kernel<BM, BN, TA, TB, EPI_ATOMIC><<<g, 256, 0, s>>>(P, D); break;
+    case EPI_RELU_BWD:
+      gemm_f32_kernel<BM, BN, TA, TB, EPI_RELU_BWD><<<g, 256, 0, s>>>(P, D); break;
   }
+}
+
+template <int BM, int BN>
+void launch_tile(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, GemmDims D,
+                 int batch) {
+  int kchunk = (D.K + D.splitk - 1) / D.splitk;
+  kchunk = ((kchunk + BK - 1) / BK) * BK;
+  if (kchunk == 0) kchunk = BK;
+  D.kchunk = kchunk;
+  D.splitk = (D.K + kchunk - 1) / kchunk;
+  if (D.splitk < 1) D.splitk = 1;
+  dim3 g(mog_cdiv(D.N, BN), mog_cdiv(D.M, BM), batch * D.splitk);
+  if (!ta && !tb) launch_epi<BM, BN, false, false>(epi, g, s, P, D);
+  else if (!ta && tb) launch_epi<BM, BN, false, true>(epi, g, s, P, D);
+  else if (ta && !tb) launch_epi<BM, BN, true, false>(epi, g, s, P, D);
+  else launch_epi<BM, BN, true, true>(epi, g, s, P, D);
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -234,28 +290,30 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const* B,
                             float* const* C, const float* const* bias,
                             const float* const* Cin, float* const* Cpre,
-                            const float* const* aux, int M, int N, int K, int lda, int ldb,
-                            int ldc, int ldaux, int transA, int transB, int epi,
-                            float aux_scale, int splitk, void* stream) {
+                            const float* const* aux, float* const* colsum, int M, int N, int K,
+                            int lda, int ldb, int ldc, int ldaux, int transA, int transB,
+                            int epi, float aux_scale, int splitk, void* stream) {
   MOG_CHECK_ARG(batch >= 1 && batch <= MAXB);
   MOG_CHECK_ARG(M >= 0 && N >= 0 && K >= 0 && splitk >= 1);
   MOG_CHECK_ARG(epi >= EPI_STORE && epi <= EPI_RELU_BWD);
   MOG_CHECK_ARG(splitk == 1 || epi == EPI_ATOMIC);
-  MOG_CHECK_ARG(A && B && C);
+  MOG_CHECK_ARG(colsum == nullptr || epi == EPI_ATOMIC);
+  MOG_CHECK_ARG(C && (K == 0 || (A && B)));
   if (M == 0 || N == 0) return 0;
   GemmPtrs P;
   bool va = true, vb = true;
   for (int i = 0; i < MAXB; ++i) {
     const bool on = i < batch;
-    P.A[i] = on ? A[i] : nullptr;
-    P.B[i] = on ? B[i] : nullptr;
+    P.A[i] = (on && A) ? A[i] : nullptr;
+    P.B[i] = (on && B) ? B[i] : nullptr;
     P.C[i] = on ? C[i] : nullptr;
     P.bias[i] = (on && bias) ? bias[i] : nullptr;
     P.Cin[i] = (on && Cin) ? Cin[i] : nullptr;
     P.Cpre[i] = (on && Cpre) ? Cpre[i] : nullptr;
     P.aux[i] = (on && aux) ? aux[i] : nullptr;
+    P.colsum[i] = (on && colsum) ? colsum[i] : nullptr;
     if (on) {
-      MOG_CHECK_ARG(P.A[i] && P.B[i] && P.C[i]);
+      MOG_CHECK_ARG(P.C[i] && (K == 0 || (P.A[i] && P.B[i])));
       va = va && aligned16(P.A[i]);
       vb = vb && aligned16(P.B[i]);
       if (epi == EPI_SIGMOID_NOISE || epi == EPI_SOFTPLUS_BWD || epi == EPI_RELU_BWD)
@@ -267,17 +325,15 @@ extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const
   D.aux_scale = aux_scale;
   D.vecA = va && (lda % 4 == 0);
   D.vecB = vb && (ldb % 4 == 0);
-  int kchunk = (K + splitk - 1) / splitk;
-  kchunk = ((kchunk + BK - 1) / BK) * BK;
-  if (kchunk == 0) kchunk = BK;
-  D.kchunk = kchunk;
-  D.splitk = (K + kchunk - 1) / kchunk;
-  if (D.splitk < 1) D.splitk = 1;
-  dim3 g(mog_cdiv(N, BN), mog_cdiv(M, BM), batch * D.splitk);
+  D.splitk = splitk;
+  D.kchunk = 0;
   hipStream_t s = mog_stream(stream);
-  if (!transA && !transB) launch_epi<false, false>(epi, g, s, P, D);
-  else if (!transA && transB) launch_epi<false, true>(epi, g, s, P, D);
-  else if (transA && !transB) launch_epi<true, false>(epi, g, s, P, D);
-  else launch_epi<true, true>(epi, g, s, P, D);
+  // 128x128 tiles once both output dims fill them and the grid still covers
+  // the chip (>= 512 workgroups); 64x64 otherwise.
+  const long big_tiles = (long)mog_cdiv(M, 128) * mog_cdiv(N, 128) * batch * splitk;
+  if (M >= 128 && N >= 128 && big_tiles >= 512)
+    launch_tile<128, 128>(transA, transB, epi, s, P, D, batch);
+  else
+    launch_tile<64, 64>(transA, transB, epi, s, P, D, batch);
   MOG_LAUNCH_RET();
 }

@@ -22,7 +22,7 @@ ULL = ctypes.c_ulonglong
 
 # argtypes per entry point (mirrors include/mog_air.h)
 _SIGS = {
-    "mog_gemm_f32": [I, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, I, P],
+    "mog_gemm_f32": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, I, P],
     "mog_stn_forward": [P, I, I, I, P, I, I, P, P, P, I, P],
     "mog_stn_backward": [P, I, I, I, P, I, I, P, P, P, P, P, P],
     "mog_lstm_cell_forward": [P, P, P, P, P, I, I, P],

@@ -437,12 +437,12 @@ class AIRModel:
 
     def _dw(self, X, dY, out, K, M, N, lda, ldb, bias_out=None):
         """out[M,N] += X^T dY over K rows (split-K, atomics); bias_out += colsum(dY)."""
-        tiles = ((M + 63) // 64) * ((N + 63) // 64)
-        splitk = max(1, min(K // 256, (2048 + tiles - 1) // tiles))
+        big = M >= 128 and N >= 128
+        tiles = ((M + 127) // 128) * ((N + 127) // 128) if big else \
+            ((M + 63) // 64) * ((N + 63) // 64)
+        splitk = max(1, min(K // 256, (1024 + tiles - 1) // tiles))
         gemm([X], [dY], [out], M, N, K, lda, ldb, N, transA=True, epi=EPI_ATOMIC,
-             splitk=splitk)
-        if bias_out is not None:
-            ops.colsum_add(dY, K, N, ldb, bias_out)
+             splitk=splitk, colsum=None if bias_out is None else [bias_out])
 
     def _weight_grads(self, X, ws):
         B, T, H = ws.B, self.max_steps, self.rnn_units
@@ -470,8 +470,8 @@ class AIRModel:
         gbK = self._G("rnn/basic_lstm_cell/bias")
         if T > 1:
             self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
-        self._dw(X, ws.dGsum, gK[:C2], B, C2, 4 * H, C2, 4 * H)
-        ops.colsum_add(ws.dG, TB, 4 * H, 4 * H, gbK)
+        # bias gradient = colsum(sum_t dG_t) = colsum(dGsum), fused here
+        self._dw(X, ws.dGsum, gK[:C2], B, C2, 4 * H, C2, 4 * H, gbK)
 
     # ------------------------------------------------------------- API ----
     def _prep(self, images, targets):

@@ -38,7 +38,7 @@ def _chk(t: torch.Tensor, name: str, dtype=torch.float32):
 def gemm(A: Sequence[torch.Tensor], B: Sequence[torch.Tensor], C: Sequence[torch.Tensor],
          M: int, N: int, K: int, lda: int, ldb: int, ldc: int, transA=False, transB=False,
          epi=EPI_STORE, bias=None, Cin=None, Cpre=None, aux=None, ldaux=0,
-         aux_scale=0.0, splitk=1) -> None:
+         aux_scale=0.0, splitk=1, colsum=None) -> None:
     """Batched fp32 MFMA GEMM (see mog_gemm_f32).  A/B/C are sequences of
     tensors (or views) whose data_ptr is the matrix origin."""
     nb = len(C)
@@ -50,8 +50,8 @@ def gemm(A: Sequence[torch.Tensor], B: Sequence[torch.Tensor], C: Sequence[torch
         return _lib.ptr_array([dp(x) for x in xs])
 
     _lib.call("mog_gemm_f32", nb, arr(A), arr(B), arr(C), arr(bias), arr(Cin), arr(Cpre),
-              arr(aux), M, N, K, lda, ldb, ldc, ldaux, int(transA), int(transB), epi,
-              float(aux_scale), int(splitk), stream_ptr())
+              arr(aux), arr(colsum), M, N, K, lda, ldb, ldc, ldaux, int(transA), int(transB),
+              epi, float(aux_scale), int(splitk), stream_ptr())
 
 
 def dense(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor,
