@@ -34,6 +34,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8192, help="per-GPU batch (configs[1])")
     ap.add_argument("--max-steps", type=int, default=3)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
@@ -102,7 +103,8 @@ def main():
                      annealing_schedules={"z_pres_prior_log_odds": {
                          "init": 10000.0, "min": 1e-9, "factor": 0.1, "iters": 3000,
                          "staircase": False, "log": True}},
-                     device=dev, seed=1235, noise_seed=1235 + rank, grad_world=world)
+                     device=dev, seed=1235, noise_seed=1235 + rank, grad_world=world,
+                     precision=args.precision)
     if world > 1:
         def _allreduce(g):
             dist.all_reduce(g, op=dist.ReduceOp.SUM)
@@ -137,7 +139,7 @@ def main():
             "metric": METRIC, "value": value, "unit": "images/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32", "data": "synthetic",
+            "dtype": args.precision, "data": "synthetic",
             "config": {"workload": "AIR baseline train step (configs[1] batch)",
                        "model": "AIR (LSTM 256, VAE 784-512-256-50, heads 64)",
                        "global_batch": B * world, "per_gpu_batch": B, "canvas": "50x50",

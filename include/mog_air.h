@@ -43,10 +43,11 @@ int mog_gemm_f32(int batch, const float* const* A, const float* const* B, float*
 /* ---- spatial transformer -------------------------------------------------
  * air/transformer.py:18-175 transformer(U, theta, out_size) for N images:
  * U [N, Hin*Win], theta [N, 6] (row-major 2x3), out [N, Hout*Wout].
- * accumulate = 1 fuses the canvas update of air_model.py:665-675:
+ * mode 0: out (fp32) = w;  mode 2: out (bf16) = w;
+ * mode 1 fuses the canvas update of air_model.py:665-675 into fp32 out:
  * out[n] += mask[n] != 0 ? z[n] * w : 0 (z, mask [N]). */
 int mog_stn_forward(const float* U, int N, int Hin, int Win, const float* theta, int Hout,
-                    int Wout, float* out, const float* z, const float* mask, int accumulate,
+                    int Wout, void* out, const float* z, const float* mask, int mode,
                     void* stream);
 
 /* Gradient of transformer() (TF GatherV2 grad = UnsortedSegmentSum + the
@@ -91,15 +92,38 @@ int mog_air_step_backward(int B, int HS, int train, int use_num_prior, float tem
                           const float* const* w2, float* dout, long dout_hs, float* dhid,
                           long dhid_hs, void* stream);
 
-/* ---- VAE latent sample + KL (air/vae.py:27-30, air_model.py:718-736) ---- */
+/* ---- VAE latent sample + KL (air/vae.py:27-30, air_model.py:718-736) ----
+ * z_bf16 (may be NULL): bf16 copy of z with row stride ld_zb (GEMM operand). */
 int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, float v_plv, const float* mu,
-                           const float* lv, const float* eps, float* z, const float* act,
-                           float* runloss, float* vkl, void* stream);
+                           const float* lv, const float* eps, float* z, void* z_bf16, int ld_zb,
+                           const float* act, float* runloss, float* vkl, void* stream);
+/* dmu/dlv fp32 [B,Z] and/or bf16 copies with row stride ld_b (any may be NULL,
+ * but one complete pair must be given). */
 int mog_vae_sample_backward(int B, int Z, float v_pm, float v_pv, float grad_scale,
                             const float* mu, const float* lv, const float* eps, const float* dz,
-                            const float* act, float* dmu, float* dlv, void* stream);
-/* TF SigmoidGrad: dm = dr * r * (1 - r) (vae.py:46). */
-int mog_sigmoid_backward(const float* r, const float* dr, float* dm, long n, void* stream);
+                            const float* act, float* dmu, float* dlv, void* dmu_bf16,
+                            void* dlv_bf16, int ld_b, void* stream);
+/* TF SigmoidGrad: dm = dr * r * (1 - r) (vae.py:46); dm fp32 or bf16. */
+int mog_sigmoid_backward(const float* r, const float* dr, void* dm, long n, int out_bf16,
+                         void* stream);
+
+/* ---- bf16-operand GEMM (configs[1]: bf16 glimpse-VAE) --------------------
+ * tn = 0: C[m][n] = sum_k A[m*lda+k] B[n*ldb+k]   (forward with W^T packed,
+ *         dX with W packed);  K % 8 == 0 (zero-padded buffers).
+ * tn = 1: C[m][n] = sum_k A[k*lda+m] B[k*ldb+n]   (dW = X^T dY, split-K,
+ *         epi 4 fp32 atomics, colsum = fused bias gradient).
+ * epi: 0 store(+bias) 1 softplus 2 sigmoid(acc+bias+aux*aux_scale) [aux fp32]
+ *      3 acc*(1-exp(-aux)) [aux = softplus output, bf16] 4 atomic-add.
+ * A, B, aux(epi 3): bf16; C bf16 when out_bf16 else fp32; Cin fp32 (ldc). */
+int mog_gemm_bf16(int batch, const void* const* A, const void* const* B, void* const* C,
+                  const float* const* bias, const float* const* Cin, const void* const* aux,
+                  float* const* colsum, int M, int N, int K, int lda, int ldb, int ldc,
+                  int ldaux, int tn, int epi, int out_bf16, float aux_scale, int splitk,
+                  void* stream);
+/* fp32 -> bf16 weight packing: dst[r][c] = src[c][r] (transpose) or src[r][c],
+ * zero outside the (src_rows, src_cols) source extent. */
+int mog_cvt_bf16(const float* src, int src_rows, int src_cols, int ld_src, void* dst, int rows,
+                 int cols, int ld_dst, int transpose, void* stream);
 
 /* ---- reconstruction loss (air_model.py:866-900) -------------------------- */
 int mog_recon_loss(const float* x, const float* canvas, const float* runloss, const int* digits,

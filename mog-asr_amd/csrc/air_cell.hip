@@ -348,8 +348,9 @@ struct VaeCfg {
 // then sums the KL terms in k order (Z <= 64).
 __global__ __launch_bounds__(256) void vae_sample_fwd_kernel(VaeCfg c, const float* mu,
                                                              const float* lv, const float* eps,
-                                                             float* z, const float* act,
-                                                             float* runloss, float* vkl_out) {
+                                                             float* z, __bf16* zb, int ldzb,
+                                                             const float* act, float* runloss,
+                                                             float* vkl_out) {
 #pragma clang fp contract(off)
   __shared__ float terms[4][64];
   const int w = threadIdx.x >> 6, k = threadIdx.x & 63;
@@ -358,7 +359,9 @@ __global__ __launch_bounds__(256) void vae_sample_fwd_kernel(VaeCfg c, const flo
     const size_t i = (size_t)b * c.Z + k;
     const float l = lv[i];
     const float var = mog_expf(l);
-    z[i] = mu[i] + eps[i] * sqrtf(var);
+    const float zv = mu[i] + eps[i] * sqrtf(var);
+    z[i] = zv;
+    if (zb) zb[(size_t)b * ldzb + k] = (__bf16)zv;
     terms[w][k] = gauss_kl_term(c.v_plv, l, var, c.v_pv, mu[i], c.v_pm);
   }
   __syncthreads();
@@ -373,24 +376,33 @@ __global__ __launch_bounds__(256) void vae_sample_fwd_kernel(VaeCfg c, const flo
 __global__ __launch_bounds__(256) void vae_sample_bwd_kernel(VaeCfg c, const float* mu,
                                                              const float* lv, const float* eps,
                                                              const float* dz, const float* act,
-                                                             float* dmu, float* dlv) {
+                                                             float* dmu, float* dlv,
+                                                             __bf16* dmub, __bf16* dlvb,
+                                                             int ldb) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)c.B * c.Z) return;
-  const int b = i / c.Z;
+  const int b = i / c.Z, k = i - (long)b * c.Z;
   const float wn = act[b] != 0.0f ? c.grad_scale : 0.0f;
   const float var = mog_expf(lv[i]);
   const float g = dz[i];
-  dmu[i] = g + wn * (mu[i] - c.v_pm) / c.v_pv;
-  dlv[i] = g * eps[i] * 0.5f * sqrtf(var) + wn * 0.5f * (-1.0f + var / c.v_pv);
+  const float vm = g + wn * (mu[i] - c.v_pm) / c.v_pv;
+  const float vl = g * eps[i] * 0.5f * sqrtf(var) + wn * 0.5f * (-1.0f + var / c.v_pv);
+  if (dmu) dmu[i] = vm;
+  if (dlv) dlv[i] = vl;
+  if (dmub) dmub[(size_t)b * ldb + k] = (__bf16)vm;
+  if (dlvb) dlvb[(size_t)b * ldb + k] = (__bf16)vl;
 }
 
-// dm = dr * r * (1 - r)   (TF SigmoidGrad)
+// dm = dr * r * (1 - r)   (TF SigmoidGrad); fp32 or bf16 output
+template <bool BF16>
 __global__ __launch_bounds__(256) void sigmoid_bwd_kernel(const float* r, const float* dr,
-                                                          float* dm, long n) {
+                                                          void* dm, long n) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const float v = r[i];
-  dm[i] = dr[i] * v * (1.0f - v);
+  const float d = dr[i] * v * (1.0f - v);
+  if (BF16) reinterpret_cast<__bf16*>(dm)[i] = (__bf16)d;
+  else reinterpret_cast<float*>(dm)[i] = d;
 }
 
 // ---------------------------------------------------------------- loss ---
@@ -554,33 +566,40 @@ extern "C" int mog_air_step_backward(int B, int HS, int train, int use_num_prior
 
 extern "C" int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, float v_plv,
                                       const float* mu, const float* lv, const float* eps,
-                                      float* z, const float* act, float* runloss, float* vkl,
-                                      void* stream) {
+                                      float* z, void* z_bf16, int ld_zb, const float* act,
+                                      float* runloss, float* vkl, void* stream) {
   MOG_CHECK_ARG(B >= 0 && Z > 0 && Z <= 64 && mu && lv && eps && z && act && runloss && vkl);
+  MOG_CHECK_ARG(!z_bf16 || ld_zb >= Z);
   if (B == 0) return 0;
   VaeCfg c{B, Z, v_pm, v_pv, v_plv, 0.0f};
-  vae_sample_fwd_kernel<<<mog_cdiv(B, 4), 256, 0, mog_stream(stream)>>>(c, mu, lv, eps, z, act,
-                                                                       runloss, vkl);
+  vae_sample_fwd_kernel<<<mog_cdiv(B, 4), 256, 0, mog_stream(stream)>>>(
+      c, mu, lv, eps, z, reinterpret_cast<__bf16*>(z_bf16), ld_zb, act, runloss, vkl);
   MOG_LAUNCH_RET();
 }
 
 extern "C" int mog_vae_sample_backward(int B, int Z, float v_pm, float v_pv, float grad_scale,
                                        const float* mu, const float* lv, const float* eps,
                                        const float* dz, const float* act, float* dmu,
-                                       float* dlv, void* stream) {
-  MOG_CHECK_ARG(B >= 0 && Z > 0 && mu && lv && eps && dz && act && dmu && dlv);
+                                       float* dlv, void* dmu_bf16, void* dlv_bf16, int ld_b,
+                                       void* stream) {
+  MOG_CHECK_ARG(B >= 0 && Z > 0 && mu && lv && eps && dz && act);
+  MOG_CHECK_ARG((dmu && dlv) || (dmu_bf16 && dlv_bf16 && ld_b >= Z));
   if (B == 0) return 0;
   VaeCfg c{B, Z, v_pm, v_pv, 0.0f, grad_scale};
   vae_sample_bwd_kernel<<<mog_cdiv((long)B * Z, 256), 256, 0, mog_stream(stream)>>>(
-      c, mu, lv, eps, dz, act, dmu, dlv);
+      c, mu, lv, eps, dz, act, dmu, dlv, reinterpret_cast<__bf16*>(dmu_bf16),
+      reinterpret_cast<__bf16*>(dlv_bf16), ld_b);
   MOG_LAUNCH_RET();
 }
 
-extern "C" int mog_sigmoid_backward(const float* r, const float* dr, float* dm, long n,
-                                    void* stream) {
+extern "C" int mog_sigmoid_backward(const float* r, const float* dr, void* dm, long n,
+                                    int out_bf16, void* stream) {
   MOG_CHECK_ARG(r && dr && dm && n >= 0);
   if (n == 0) return 0;
-  sigmoid_bwd_kernel<<<mog_cdiv(n, 256), 256, 0, mog_stream(stream)>>>(r, dr, dm, n);
+  if (out_bf16)
+    sigmoid_bwd_kernel<true><<<mog_cdiv(n, 256), 256, 0, mog_stream(stream)>>>(r, dr, dm, n);
+  else
+    sigmoid_bwd_kernel<false><<<mog_cdiv(n, 256), 256, 0, mog_stream(stream)>>>(r, dr, dm, n);
   MOG_LAUNCH_RET();
 }
 

@@ -1,0 +1,340 @@
+// bf16-operand GEMM (fp32 accumulate) on gfx950 v_mfma_f32_16x16x32_bf16 —
+// the glimpse-VAE layers of the bf16 configuration (BASELINE.json configs[1]).
+//
+// Two operand forms, chosen so no layout conversion happens at run time:
+//   NT:  C[m][n] = sum_k A[m][k] * B[n][k]        (A rows and B rows k-contiguous)
+//        forward   Y  = X  W   with B = W^T packed  ([out][in] bf16)
+//        backward  dX = dY W^T with B = W  packed   ([in][out] bf16)
+//   TN:  C[m][n] = sum_k A[k][m] * B[k][n]        (both operands k-major)
+//        weight gradient dW = X^T dY over the batch rows (split-K, fp32 atomics,
+//        fused bias-gradient column sums); fragments come out of the k-major
+//        LDS images with the gfx950 transpose read ds_read_b64_tr_b16.
+// All k extents are multiples of 8 (buffers are padded with zeros), so every
+// global load is a 16-byte vector.  Tile 128x128 or 64x64, BK = 32, 256
+// threads = 2x2 waves, register-staged double buffering.
+#include "mog_common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+enum {
+  B_STORE = 0,           // C = acc (+bias)                       fp32 or bf16 out
+  B_SOFTPLUS = 1,        // C = softplus(acc + bias)              bf16 out
+  B_SIGMOID_NOISE = 2,   // C = sigmoid(acc + bias + aux*scale)   fp32 out (aux fp32)
+  B_SOFTPLUS_BWD = 3,    // C = acc * (1 - exp(-aux))  [aux = softplus output, bf16]
+  B_ATOMIC = 4,          // C += acc (fp32 atomics), optional colsum of B
+};
+
+constexpr int MAXB = 8;
+struct BPtrs {
+  const __bf16* A[MAXB];
+  const __bf16* B[MAXB];
+  void* C[MAXB];
+  const float* bias[MAXB];
+  const float* Cin[MAXB];
+  const void* aux[MAXB];
+  float* colsum[MAXB];
+};
+struct BDims {
+  int M, N, K, lda, ldb, ldc, ldaux, splitk, kchunk, out_bf16;
+  float aux_scale;
+};
+
+constexpr int BKK = 32;
+
+__device__ __forceinline__ float bf2f(__bf16 v) { return (float)v; }
+
+template <int BM, int BN, bool TN, int EPI>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
+  constexpr int MI = BM / 32, NI = BN / 32;
+  // LDS images.  NT: [rows][BKK+8] (k contiguous).  TN: [BKK][cols+8].
+  constexpr int A_ELEMS = TN ? BKK * (BM + 8) : BM * (BKK + 8);
+  constexpr int B_ELEMS = TN ? BKK * (BN + 8) : BN * (BKK + 8);
+  constexpr int NA = (BM * BKK / 8) / 256;  // 16-byte chunks per thread
+  constexpr int NB = (BN * BKK / 8) / 256;
+  __shared__ __attribute__((aligned(16))) __bf16 As[A_ELEMS];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[B_ELEMS];
+  const int z = blockIdx.z / D.splitk, ks = blockIdx.z - z * D.splitk;
+  const __bf16* __restrict__ A = P.A[z];
+  const __bf16* __restrict__ Bm = P.B[z];
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kbeg = ks * D.kchunk;
+  const int kend = min(D.K, kbeg + D.kchunk);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
+  const int M = D.M, N = D.N;
+  float* colsum = P.colsum[z];
+  const bool do_cs = colsum != nullptr && blockIdx.y == 0 && t < BN;
+  float cs = 0.0f;
+
+  floatx4 acc[MI][NI];
+  const float* Cin = P.Cin[z];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = 0.0f;
+        if (Cin != nullptr && ks == 0) {
+          const int row = m0 + wm + mi * 16 + (lane >> 4) * 4 + r;
+          const int col = n0 + wn + ni * 16 + (lane & 15);
+          if (row < M && col < N) v = Cin[(size_t)row * D.ldc + col];
+        }
+        acc[mi][ni][r] = v;
+      }
+
+  uint4 ra[NA], rb[NB];
+  const uint4 zero4 = make_uint4(0, 0, 0, 0);
+  auto load_tiles = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int q = t + 256 * i;
+      if (!TN) {  // A [M][K]: row = q / 4, k chunk = q % 4
+        const int row = q >> 2, kc = (q & 3) * 8;
+        const int gm = m0 + row, gk = k0 + kc;
+        ra[i] = (gm < M && gk < kend)
+                    ? *reinterpret_cast<const uint4*>(A + (size_t)gm * D.lda + gk) : zero4;
+      } else {    // A [K][M]: k row = q / (BM/8), m chunk
+        const int k = q / (BM / 8), mc = (q % (BM / 8)) * 8;
+        const int gk = k0 + k, gm = m0 + mc;
+        ra[i] = (gk < kend && gm < D.lda)
+                    ? *reinterpret_cast<const uint4*>(A + (size_t)gk * D.lda + gm) : zero4;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int q = t + 256 * i;
+      if (!TN) {  // B [N][K]
+        const int row = q >> 2, kc = (q & 3) * 8;
+        const int gn = n0 + row, gk = k0 + kc;
+        rb[i] = (gn < N && gk < kend)
+                    ? *reinterpret_cast<const uint4*>(Bm + (size_t)gn * D.ldb + gk) : zero4;
+      } else {    // B [K][N]
+        const int k = q / (BN / 8), nc = (q % (BN / 8)) * 8;
+        const int gk = k0 + k, gn = n0 + nc;
+        rb[i] = (gk < kend && gn < D.ldb)
+                    ? *reinterpret_cast<const uint4*>(Bm + (size_t)gk * D.ldb + gn) : zero4;
+      }
+    }
+  };
+  auto store_tiles = [&]() {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int q = t + 256 * i;
+      if (!TN) {
+        const int row = q >> 2, kc = (q & 3) * 8;
+        *reinterpret_cast<uint4*>(&As[row * (BKK + 8) + kc]) = ra[i];
+      } else {
+        const int k = q / (BM / 8), mc = (q % (BM / 8)) * 8;
+        *reinterpret_cast<uint4*>(&As[k * (BM + 8) + mc]) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int q = t + 256 * i;
+      if (!TN) {
+        const int row = q >> 2, kc = (q & 3) * 8;
+        *reinterpret_cast<uint4*>(&Bs[row * (BKK + 8) + kc]) = rb[i];
+      } else {
+        const int k = q / (BN / 8), nc = (q % (BN / 8)) * 8;
+        *reinterpret_cast<uint4*>(&Bs[k * (BN + 8) + nc]) = rb[i];
+      }
+    }
+  };
+
+  const int g = lane >> 4, li = lane & 15;
+  // transpose-read lane roles: lane 4q+p of a 16-lane group -> row q, cols 4p..4p+3
+  const int tq = li >> 2, tp = li & 3;
+
+  if (kbeg < kend) {
+    load_tiles(kbeg);
+    store_tiles();
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += BKK) {
+      const bool has_next = k0 + BKK < kend;
+      if (has_next) load_tiles(k0 + BKK);
+      bf16x8 a[MI], b[NI];
+      if (!TN) {
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+          a[mi] = *reinterpret_cast<const bf16x8*>(&As[(wm + mi * 16 + li) * (BKK + 8) + 8 * g]);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          b[ni] = *reinterpret_cast<const bf16x8*>(&Bs[(wn + ni * 16 + li) * (BKK + 8) + 8 * g]);
+      } else {
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+          const __bf16* p0 = &As[(8 * g + tq) * (BM + 8) + wm + mi * 16 + 4 * tp];
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
+          const bf16x4 hi =
+              __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p0 + 4 * (BM + 8)));
+          a[mi] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          const __bf16* p0 = &Bs[(8 * g + tq) * (BN + 8) + wn + ni * 16 + 4 * tp];
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
+          const bf16x4 hi =
+              __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p0 + 4 * (BN + 8)));
+          b[ni] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      }
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+      if (do_cs) {
+        if (TN) {
+#pragma unroll 8
+          for (int k = 0; k < BKK; ++k) cs += bf2f(Bs[k * (BN + 8) + t]);
+        } else {
+#pragma unroll 8
+          for (int k = 0; k < BKK; ++k) cs += bf2f(Bs[t * (BKK + 8) + k]);
+        }
+      }
+      __syncthreads();
+      if (has_next) {
+        store_tiles();
+        __syncthreads();
+      }
+    }
+  }
+  if (do_cs && n0 + t < N) atomicAdd(colsum + n0 + t, cs);
+
+  void* Cv = P.C[z];
+  const float* bias = P.bias[z];
+  const void* aux = P.aux[z];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + mi * 16 + (lane >> 4) * 4 + r;
+        const int col = n0 + wn + ni * 16 + (lane & 15);
+        if (row >= M || col >= N) continue;
+        const size_t o = (size_t)row * D.ldc + col;
+        float v = acc[mi][ni][r];
+        if (EPI == B_ATOMIC) {
+          atomicAdd(reinterpret_cast<float*>(Cv) + o, v);
+          continue;
+        }
+        if (EPI == B_SOFTPLUS_BWD) {
+          const float post = bf2f(reinterpret_cast<const __bf16*>(aux)[(size_t)row * D.ldaux + col]);
+          v = v * (-mog_expm1f(-post));  // sigmoid(pre) = 1 - exp(-softplus(pre))
+        } else {
+          if (bias != nullptr) v = v + bias[col];
+          if (EPI == B_SOFTPLUS) v = mog_softplusf(v);
+          if (EPI == B_SIGMOID_NOISE)
+            v = mog_sigmoidf(v + reinterpret_cast<const float*>(aux)[(size_t)row * D.ldaux + col] *
+                                     D.aux_scale);
+        }
+        if (D.out_bf16) reinterpret_cast<__bf16*>(Cv)[o] = (__bf16)v;
+        else reinterpret_cast<float*>(Cv)[o] = v;
+      }
+}
+
+template <int BM, int BN, bool TN>
+void launch(int epi, dim3 g, hipStream_t s, const BPtrs& P, const BDims& D) {
+  switch (epi) {
+    case B_STORE: gemm_bf16_kernel<BM, BN, TN, B_STORE><<<g, 256, 0, s>>>(P, D); break;
+    case B_SOFTPLUS: gemm_bf16_kernel<BM, BN, TN, B_SOFTPLUS><<<g, 256, 0, s>>>(P, D); break;
+    case B_SIGMOID_NOISE:
+      gemm_bf16_kernel<BM, BN, TN, B_SIGMOID_NOISE><<<g, 256, 0, s>>>(P, D); break;
+    case B_SOFTPLUS_BWD:
+      gemm_bf16_kernel<BM, BN, TN, B_SOFTPLUS_BWD><<<g, 256, 0, s>>>(P, D); break;
+    case B_ATOMIC: gemm_bf16_kernel<BM, BN, TN, B_ATOMIC><<<g, 256, 0, s>>>(P, D); break;
+  }
+}
+
+template <int BM, int BN>
+void launch_tile(bool tn, int epi, hipStream_t s, const BPtrs& P, BDims D, int batch) {
+  int kchunk = (D.K + D.splitk - 1) / D.splitk;
+  kchunk = ((kchunk + BKK - 1) / BKK) * BKK;
+  if (kchunk == 0) kchunk = BKK;
+  D.kchunk = kchunk;
+  D.splitk = (D.K + kchunk - 1) / kchunk;
+  if (D.splitk < 1) D.splitk = 1;
+  dim3 g(mog_cdiv(D.N, BN), mog_cdiv(D.M, BM), batch * D.splitk);
+  if (tn) launch<BM, BN, true>(epi, g, s, P, D);
+  else launch<BM, BN, false>(epi, g, s, P, D);
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int mog_gemm_bf16(int batch, const void* const* A, const void* const* B,
+                             void* const* C, const float* const* bias, const float* const* Cin,
+                             const void* const* aux, float* const* colsum, int M, int N, int K,
+                             int lda, int ldb, int ldc, int ldaux, int tn, int epi, int out_bf16,
+                             float aux_scale, int splitk, void* stream) {
+  MOG_CHECK_ARG(batch >= 1 && batch <= MAXB);
+  MOG_CHECK_ARG(M >= 0 && N >= 0 && K >= 0 && splitk >= 1);
+  MOG_CHECK_ARG(epi >= B_STORE && epi <= B_ATOMIC);
+  MOG_CHECK_ARG(splitk == 1 || epi == B_ATOMIC);
+  MOG_CHECK_ARG(colsum == nullptr || epi == B_ATOMIC);
+  MOG_CHECK_ARG(epi != B_ATOMIC || !out_bf16);
+  MOG_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0);  // 16-byte rows (zero-padded buffers)
+  MOG_CHECK_ARG(tn || K % 8 == 0);
+  MOG_CHECK_ARG(C && A && B);
+  if (M == 0 || N == 0) return 0;
+  BPtrs P;
+  for (int i = 0; i < MAXB; ++i) {
+    const bool on = i < batch;
+    P.A[i] = on ? reinterpret_cast<const __bf16*>(A[i]) : nullptr;
+    P.B[i] = on ? reinterpret_cast<const __bf16*>(B[i]) : nullptr;
+    P.C[i] = on ? C[i] : nullptr;
+    P.bias[i] = (on && bias) ? bias[i] : nullptr;
+    P.Cin[i] = (on && Cin) ? Cin[i] : nullptr;
+    P.aux[i] = (on && aux) ? aux[i] : nullptr;
+    P.colsum[i] = (on && colsum) ? colsum[i] : nullptr;
+    if (on) {
+      MOG_CHECK_ARG(P.A[i] && P.B[i] && P.C[i] && al16(P.A[i]) && al16(P.B[i]));
+      if (epi == B_SIGMOID_NOISE || epi == B_SOFTPLUS_BWD) MOG_CHECK_ARG(P.aux[i] != nullptr);
+    }
+  }
+  BDims D;
+  D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc; D.ldaux = ldaux;
+  D.splitk = splitk; D.kchunk = 0; D.out_bf16 = out_bf16; D.aux_scale = aux_scale;
+  hipStream_t s = mog_stream(stream);
+  const long big = (long)mog_cdiv(M, 128) * mog_cdiv(N, 128) * batch * splitk;
+  if (M >= 128 && N >= 128 && big >= 256)
+    launch_tile<128, 128>(tn != 0, epi, s, P, D, batch);
+  else
+    launch_tile<64, 64>(tn != 0, epi, s, P, D, batch);
+  MOG_LAUNCH_RET();
+}
+
+// ---------------------------------------------------------------------------
+// fp32 -> bf16 conversion with optional transpose and zero padding:
+// dst[r][c] (ld_dst) = src[c][r] (transpose) or src[r][c]; rows x cols is the
+// destination extent, (src_rows, src_cols) the valid source extent.
+namespace {
+__global__ __launch_bounds__(256) void cvt_bf16_kernel(const float* src, int src_rows,
+                                                       int src_cols, int ld_src, __bf16* dst,
+                                                       int rows, int cols, int ld_dst,
+                                                       int transpose) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)rows * cols) return;
+  const int r = i / cols, c = i - (long)r * cols;
+  const int sr = transpose ? c : r, sc = transpose ? r : c;
+  const float v = (sr < src_rows && sc < src_cols) ? src[(size_t)sr * ld_src + sc] : 0.0f;
+  dst[(size_t)r * ld_dst + c] = (__bf16)v;
+}
+}  // namespace
+
+extern "C" int mog_cvt_bf16(const float* src, int src_rows, int src_cols, int ld_src, void* dst,
+                            int rows, int cols, int ld_dst, int transpose, void* stream) {
+  MOG_CHECK_ARG(src && dst && rows >= 0 && cols >= 0);
+  if (rows == 0 || cols == 0) return 0;
+  cvt_bf16_kernel<<<mog_cdiv((long)rows * cols, 256), 256, 0, mog_stream(stream)>>>(
+      src, src_rows, src_cols, ld_src, reinterpret_cast<__bf16*>(dst), rows, cols, ld_dst,
+      transpose);
+  MOG_LAUNCH_RET();
+}

@@ -330,8 +330,10 @@ extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const
   hipStream_t s = mog_stream(stream);
   // 128x128 tiles once both output dims fill them and the grid still covers
   // the chip (>= 512 workgroups); 64x64 otherwise.
+  // (measured: 128x128 is on par for the large NN GEMMs and slower for the
+  // split-K weight-gradient form, so the transposed-A form stays on 64x64)
   const long big_tiles = (long)mog_cdiv(M, 128) * mog_cdiv(N, 128) * batch * splitk;
-  if (M >= 128 && N >= 128 && big_tiles >= 512)
+  if (!transA && M >= 128 && N >= 128 && big_tiles >= 512)
     launch_tile<128, 128>(transA, transB, epi, s, P, D, batch);
   else
     launch_tile<64, 64>(transA, transB, epi, s, P, D, batch);

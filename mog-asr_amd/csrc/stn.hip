@@ -64,10 +64,11 @@ __device__ __forceinline__ float stn_value(const Samp& s, const float* U) {
 }
 
 // mode 0: out = v ; mode 1: out = mask ? out + z*v : out   (canvas accumulate)
+// mode 2: out (bf16) = v  (glimpse as the bf16 A operand of the VAE GEMM)
 template <int MODE>
 __global__ __launch_bounds__(256) void stn_fwd_kernel(const float* __restrict__ U, int Hin,
                                                       int Win, const float* __restrict__ theta,
-                                                      int Hout, int Wout, float* out,
+                                                      int Hout, int Wout, void* outv,
                                                       const float* __restrict__ z,
                                                       const float* __restrict__ mask) {
 #pragma clang fp contract(off)
@@ -81,7 +82,11 @@ __global__ __launch_bounds__(256) void stn_fwd_kernel(const float* __restrict__ 
   if (MODE == 1 && !(mask[n] != 0.0f)) return;
   const Samp s = stn_sample(th, Hin, Win, Hout, Wout, p);
   const float v = stn_value(s, U + (size_t)n * Hin * Win);
-  float* o = out + (size_t)n * P + p;
+  if (MODE == 2) {
+    reinterpret_cast<__bf16*>(outv)[(size_t)n * P + p] = (__bf16)v;
+    return;
+  }
+  float* o = reinterpret_cast<float*>(outv) + (size_t)n * P + p;
   if (MODE == 0) *o = v;
   else *o = *o + z[n] * v;
 }
@@ -152,18 +157,19 @@ __global__ __launch_bounds__(256) void stn_bwd_kernel(
 
 // transformer(U, theta, out_size) forward; see include/mog_air.h
 extern "C" int mog_stn_forward(const float* U, int N, int Hin, int Win, const float* theta,
-                               int Hout, int Wout, float* out, const float* z,
-                               const float* mask, int accumulate, void* stream) {
+                               int Hout, int Wout, void* out, const float* z,
+                               const float* mask, int mode, void* stream) {
   MOG_CHECK_ARG(U && theta && out && N >= 0 && Hin > 0 && Win > 0 && Hout > 0 && Wout > 0);
-  MOG_CHECK_ARG(!accumulate || (z && mask));
+  MOG_CHECK_ARG(mode >= 0 && mode <= 2 && (mode != 1 || (z && mask)));
   if (N == 0) return 0;
   dim3 g(mog_cdiv(Hout * Wout, 256), N);
-  if (accumulate)
-    stn_fwd_kernel<1><<<g, 256, 0, mog_stream(stream)>>>(U, Hin, Win, theta, Hout, Wout, out, z,
-                                                         mask);
+  hipStream_t s = mog_stream(stream);
+  if (mode == 1)
+    stn_fwd_kernel<1><<<g, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, z, mask);
+  else if (mode == 2)
+    stn_fwd_kernel<2><<<g, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, nullptr, nullptr);
   else
-    stn_fwd_kernel<0><<<g, 256, 0, mog_stream(stream)>>>(U, Hin, Win, theta, Hout, Wout, out,
-                                                         nullptr, nullptr);
+    stn_fwd_kernel<0><<<g, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, nullptr, nullptr);
   MOG_LAUNCH_RET();
 }
 

@@ -31,9 +31,11 @@ _SIGS = {
                              P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "mog_air_step_backward": [I, I, I, I, F, F, F, F, F, F, F, F, P, P, P, P, P, P, P, P, P,
                               L, P, L, P],
-    "mog_vae_sample_forward": [I, I, F, F, F, P, P, P, P, P, P, P, P],
-    "mog_vae_sample_backward": [I, I, F, F, F, P, P, P, P, P, P, P, P],
-    "mog_sigmoid_backward": [P, P, P, L, P],
+    "mog_vae_sample_forward": [I, I, F, F, F, P, P, P, P, P, I, P, P, P, P],
+    "mog_vae_sample_backward": [I, I, F, F, F, P, P, P, P, P, P, P, P, P, I, P],
+    "mog_sigmoid_backward": [P, P, P, L, I, P],
+    "mog_gemm_bf16": [I, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, I, P],
+    "mog_cvt_bf16": [P, I, I, I, P, I, I, I, I, P],
     "mog_recon_loss": [P, P, P, P, P, I, I, F, P, P, P, P, P, P, P],
     "mog_batch_mean": [P, P, P, P, I, P, P],
     "mog_colsum_add": [P, I, I, I, P, P],

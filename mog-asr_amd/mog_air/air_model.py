@@ -105,13 +105,22 @@ class _Workspace:
         self.shift = e(T, B, 2)
         self.zprob, self.zkl, self.skl, self.shkl = e(T, B), e(T, B), e(T, B), e(T, B)
         self.zmask, self.zval, self.vkl = e(T, B), e(T, B), e(T, B)
-        self.g = e(T, B, W2)
-        self.a1pre, self.a1 = e(T, B, R1), e(T, B, R1)
-        self.a2pre, self.a2 = e(T, B, R2), e(T, B, R2)
+        self.bf16 = m.precision == "bf16"
         self.mu, self.lv, self.z = e(T, B, Z), e(T, B, Z), e(T, B, Z)
-        self.d1pre, self.d1 = e(T, B, G1), e(T, B, G1)
-        self.d2pre, self.d2 = e(T, B, G2), e(T, B, G2)
-        self.mpre, self.r = e(T, B, W2), e(T, B, W2)
+        self.r = e(T, B, W2)
+        if self.bf16:
+            eb = lambda *s: torch.empty(s, device=dev, dtype=torch.bfloat16)  # noqa: E731
+            Zp = (Z + 7) // 8 * 8
+            self.gb, self.a1b, self.a2b = eb(T, B, W2), eb(T, B, R1), eb(T, B, R2)
+            self.zb = torch.zeros((T, B, Zp), device=dev, dtype=torch.bfloat16)
+            self.d1b, self.d2b = eb(T, B, G1), eb(T, B, G2)
+        else:
+            self.g = e(T, B, W2)
+            self.a1pre, self.a1 = e(T, B, R1), e(T, B, R1)
+            self.a2pre, self.a2 = e(T, B, R2), e(T, B, R2)
+            self.d1pre, self.d1 = e(T, B, G1), e(T, B, G1)
+            self.d2pre, self.d2 = e(T, B, G2), e(T, B, G2)
+            self.mpre = e(T, B, W2)
         self.canvas = e(B, C2)
         self.stop, self.runloss = e(B), e(B)
         self.digits = torch.empty(B, device=dev, dtype=torch.int32)
@@ -135,13 +144,21 @@ class _Workspace:
         e = lambda *s: torch.empty(s, device=dev, dtype=torch.float32)  # noqa: E731
         self.dcanvas = e(B, C2)
         self.dr = e(B, W2)
-        self.dm = e(T, B, W2)
-        self.dd2, self.dd1 = e(T, B, G2), e(T, B, G1)
         self.dz = e(B, Z)
-        self.dmu, self.dlv = e(T, B, Z), e(T, B, Z)
         self.tmp_a2 = e(B, R2)
-        self.da2, self.da1 = e(T, B, R2), e(T, B, R1)
         self.dg = e(B, W2)
+        if self.bf16:
+            eb = lambda *s: torch.empty(s, device=dev, dtype=torch.bfloat16)  # noqa: E731
+            Zp = (Z + 7) // 8 * 8
+            self.dmb, self.dd2b, self.dd1b = eb(T, B, W2), eb(T, B, G2), eb(T, B, G1)
+            self.dmub = torch.zeros((T, B, Zp), device=dev, dtype=torch.bfloat16)
+            self.dlvb = torch.zeros((T, B, Zp), device=dev, dtype=torch.bfloat16)
+            self.da2b, self.da1b = eb(T, B, R2), eb(T, B, R1)
+        else:
+            self.dm = e(T, B, W2)
+            self.dd2, self.dd1 = e(T, B, G2), e(T, B, G1)
+            self.dmu, self.dlv = e(T, B, Z), e(T, B, Z)
+            self.da2, self.da1 = e(T, B, R2), e(T, B, R1)
         self.dth_f, self.dth_b, self.dot = e(B, 6), e(B, 6), e(B)
         self.dout = e(5, T, B, 2)
         self.dhid = e(5, T, B, HS)
@@ -169,7 +186,10 @@ class AIRModel:
                  cnn=True, cnn_filters=8, num_summary_images=60, train=False, reuse=False,
                  scope="air", annealing_schedules=None, generation_batch_size=64,
                  num_prior=None, *, device=None, seed: int = 1235, noise_seed: int = 1235,
-                 grad_world: int = 1):
+                 grad_world: int = 1, precision: str = "fp32"):
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' (bit-exact parity) or 'bf16'")
+        self.precision = precision
         if cnn:
             raise NotImplementedError(
                 "cnn=True (air_model.py:763-810) is outside the hot-path scope; the entry "
@@ -331,31 +351,19 @@ class AIRModel:
                       dp(ws.digits), dp(ws.live), dp(rec), dp(ws.th_f[t]), dp(ws.th_b[t]),
                       dp(ws.scale[t]), dp(ws.shift[t]), dp(ws.zprob[t]), dp(ws.zkl[t]),
                       dp(ws.skl[t]), dp(ws.shkl[t]), dp(ws.zmask[t]), dp(ws.zval[t]), s)
-            # STN read: canvas -> 28x28 glimpse (air_model.py:523-531)
-            ops.stn_forward(X, ws.th_f[t], (W, W), out=ws.g[t])
-            # glimpse VAE (vae.py:5-48)
-            gemm([ws.g[t]], [vw["recognition_1"]], [ws.a1[t]], B, R1, W2, W2, R1, R1,
-                 epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]], Cpre=[ws.a1pre[t]])
-            gemm([ws.a1[t]], [vw["recognition_2"]], [ws.a2[t]], B, R2, R1, R1, R2, R2,
-                 epi=EPI_SOFTPLUS, bias=[vb["recognition_2"]], Cpre=[ws.a2pre[t]])
-            gemm([ws.a2[t], ws.a2[t]], [vw["rec_mean"], vw["rec_log_variance"]],
-                 [ws.mu[t], ws.lv[t]], B, Z, R2, R2, Z, Z,
-                 bias=[vb["rec_mean"], vb["rec_log_variance"]])
-            _lib.call("mog_vae_sample_forward", B, Z, float(self.vae_prior_mean),
-                      float(self.vae_prior_variance), self.vae_prior_log_variance,
-                      dp(ws.mu[t]), dp(ws.lv[t]), dp(ws.eps_z[t]), dp(ws.z[t]),
-                      dp(ws.zmask[t]), dp(ws.runloss), dp(ws.vkl[t]), s)
-            gemm([ws.z[t]], [vw["generative_1"]], [ws.d1[t]], B, G1, Z, Z, G1, G1,
-                 epi=EPI_SOFTPLUS, bias=[vb["generative_1"]], Cpre=[ws.d1pre[t]])
-            gemm([ws.d1[t]], [vw["generative_2"]], [ws.d2[t]], B, G2, G1, G1, G2, G2,
-                 epi=EPI_SOFTPLUS, bias=[vb["generative_2"]], Cpre=[ws.d2pre[t]])
-            gemm([ws.d2[t]], [vw["gen_mean"]], [ws.r[t]], B, W2, G2, G2, W2, W2,
-                 epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]], Cpre=[ws.mpre[t]],
-                 aux=[ws.eps_x[t]], ldaux=W2, aux_scale=float(lik_std))
+            # STN read -> glimpse VAE (air_model.py:523-550, vae.py:5-48)
+            if self.precision == "bf16":
+                self._vae_forward_bf16(X, ws, t, float(lik_std))
+            else:
+                self._vae_forward_fp32(X, ws, t, float(lik_std))
             # STN write + masked canvas accumulation (air_model.py:580-588, 665-675)
             ops.stn_forward(ws.r[t], ws.th_b[t], (C, C), out=ws.canvas, z=ws.zval[t],
                             mask=ws.zmask[t], accumulate=True)
-        # reconstruction loss (air_model.py:866-900)
+        self._forward_loss(X, targets, ws, need_grad)
+
+    def _forward_loss(self, X, targets, ws, need_grad):
+        """reconstruction loss (air_model.py:866-900) + batch means."""
+        B, C2, s = ws.B, self.C2, stream_ptr()
         gscale = 1.0 / (B * self.grad_world)
         _lib.call("mog_recon_loss", dp(X), dp(ws.canvas), dp(ws.runloss), dp(ws.digits),
                   dp(targets), B, C2, float(gscale), dp(ws.recon), dp(ws.bce), dp(ws.mse),
@@ -393,24 +401,10 @@ class AIRModel:
             # STN write backward: dr, dtheta_back, dot = <dcanvas, w>
             ops.stn_backward(ws.r[t], ws.th_b[t], (C, C), ws.dcanvas, gscale=rec[R_ZC],
                              dU=ws.dr, dtheta=ws.dth_b, dot=ws.dot, want_dot=True)
-            _lib.call("mog_sigmoid_backward", dp(ws.r[t]), dp(ws.dr), dp(ws.dm[t]), B * W2, s)
-            gemm([ws.dm[t]], [vw["gen_mean"]], [ws.dd2[t]], B, G2, W2, W2, W2, G2,
-                 transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d2pre[t]], ldaux=G2)
-            gemm([ws.dd2[t]], [vw["generative_2"]], [ws.dd1[t]], B, G1, G2, G2, G2, G1,
-                 transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d1pre[t]], ldaux=G1)
-            gemm([ws.dd1[t]], [vw["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z, transB=True)
-            _lib.call("mog_vae_sample_backward", B, Z, float(self.vae_prior_mean),
-                      float(self.vae_prior_variance), float(gscale), dp(ws.mu[t]),
-                      dp(ws.lv[t]), dp(ws.eps_z[t]), dp(ws.dz), dp(ws.zmask[t]),
-                      dp(ws.dmu[t]), dp(ws.dlv[t]), s)
-            gemm([ws.dmu[t]], [vw["rec_mean"]], [ws.tmp_a2], B, R2, Z, Z, Z, R2, transB=True)
-            gemm([ws.dlv[t]], [vw["rec_log_variance"]], [ws.da2[t]], B, R2, Z, Z, Z, R2,
-                 transB=True, epi=EPI_SOFTPLUS_BWD, Cin=[ws.tmp_a2], aux=[ws.a2pre[t]],
-                 ldaux=R2)
-            gemm([ws.da2[t]], [vw["recognition_2"]], [ws.da1[t]], B, R1, R2, R2, R2, R1,
-                 transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.a1pre[t]], ldaux=R1)
-            gemm([ws.da1[t]], [vw["recognition_1"]], [ws.dg], B, W2, R1, R1, R1, W2,
-                 transB=True)
+            if self.precision == "bf16":
+                self._vae_backward_bf16(ws, t, gscale)
+            else:
+                self._vae_backward_fp32(ws, t, gscale)
             # STN read backward: dtheta only (the canvas input has no gradient)
             ops.stn_backward(X, ws.th_f[t], (W, W), ws.dg, want_dU=False, dtheta=ws.dth_f)
             hid_t = [ws.hid[z, t] for z in range(5)]
@@ -435,14 +429,177 @@ class AIRModel:
                      transB=True)
         self._weight_grads(X, ws)
 
-    def _dw(self, X, dY, out, K, M, N, lda, ldb, bias_out=None):
-        """out[M,N] += X^T dY over K rows (split-K, atomics); bias_out += colsum(dY)."""
+    # ------------------------------------------------------ glimpse VAE ----
+    def _vae_dims(self):
+        R1, R2 = self.vae_recognition_units
+        G1, G2 = self.vae_generative_units
+        return self.W2, R1, R2, self.vae_latent_dimensions, G1, G2
+
+    def _vae_forward_fp32(self, X, ws, t, lik_std):
+        B, W = ws.B, self.windows_size
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
+        vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
+        ops.stn_forward(X, ws.th_f[t], (W, W), out=ws.g[t])
+        gemm([ws.g[t]], [vw["recognition_1"]], [ws.a1[t]], B, R1, W2, W2, R1, R1,
+             epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]], Cpre=[ws.a1pre[t]])
+        gemm([ws.a1[t]], [vw["recognition_2"]], [ws.a2[t]], B, R2, R1, R1, R2, R2,
+             epi=EPI_SOFTPLUS, bias=[vb["recognition_2"]], Cpre=[ws.a2pre[t]])
+        gemm([ws.a2[t], ws.a2[t]], [vw["rec_mean"], vw["rec_log_variance"]],
+             [ws.mu[t], ws.lv[t]], B, Z, R2, R2, Z, Z,
+             bias=[vb["rec_mean"], vb["rec_log_variance"]])
+        self._vae_sample_fwd(ws, t, None, 0)
+        gemm([ws.z[t]], [vw["generative_1"]], [ws.d1[t]], B, G1, Z, Z, G1, G1,
+             epi=EPI_SOFTPLUS, bias=[vb["generative_1"]], Cpre=[ws.d1pre[t]])
+        gemm([ws.d1[t]], [vw["generative_2"]], [ws.d2[t]], B, G2, G1, G1, G2, G2,
+             epi=EPI_SOFTPLUS, bias=[vb["generative_2"]], Cpre=[ws.d2pre[t]])
+        gemm([ws.d2[t]], [vw["gen_mean"]], [ws.r[t]], B, W2, G2, G2, W2, W2,
+             epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]], Cpre=[ws.mpre[t]],
+             aux=[ws.eps_x[t]], ldaux=W2, aux_scale=lik_std)
+
+    def _vae_sample_fwd(self, ws, t, zb, ldzb):
+        _lib.call("mog_vae_sample_forward", ws.B, self.vae_latent_dimensions,
+                  float(self.vae_prior_mean), float(self.vae_prior_variance),
+                  self.vae_prior_log_variance, dp(ws.mu[t]), dp(ws.lv[t]), dp(ws.eps_z[t]),
+                  dp(ws.z[t]), dp(zb), ldzb, dp(ws.zmask[t]), dp(ws.runloss), dp(ws.vkl[t]),
+                  stream_ptr())
+
+    def _vae_backward_fp32(self, ws, t, gscale):
+        B = ws.B
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
+        s = stream_ptr()
+        _lib.call("mog_sigmoid_backward", dp(ws.r[t]), dp(ws.dr), dp(ws.dm[t]), B * W2, 0, s)
+        gemm([ws.dm[t]], [vw["gen_mean"]], [ws.dd2[t]], B, G2, W2, W2, W2, G2,
+             transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d2pre[t]], ldaux=G2)
+        gemm([ws.dd2[t]], [vw["generative_2"]], [ws.dd1[t]], B, G1, G2, G2, G2, G1,
+             transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d1pre[t]], ldaux=G1)
+        gemm([ws.dd1[t]], [vw["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z, transB=True)
+        _lib.call("mog_vae_sample_backward", B, Z, float(self.vae_prior_mean),
+                  float(self.vae_prior_variance), float(gscale), dp(ws.mu[t]), dp(ws.lv[t]),
+                  dp(ws.eps_z[t]), dp(ws.dz), dp(ws.zmask[t]), dp(ws.dmu[t]), dp(ws.dlv[t]),
+                  None, None, 0, s)
+        gemm([ws.dmu[t]], [vw["rec_mean"]], [ws.tmp_a2], B, R2, Z, Z, Z, R2, transB=True)
+        gemm([ws.dlv[t]], [vw["rec_log_variance"]], [ws.da2[t]], B, R2, Z, Z, Z, R2,
+             transB=True, epi=EPI_SOFTPLUS_BWD, Cin=[ws.tmp_a2], aux=[ws.a2pre[t]], ldaux=R2)
+        gemm([ws.da2[t]], [vw["recognition_2"]], [ws.da1[t]], B, R1, R2, R2, R2, R1,
+             transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.a1pre[t]], ldaux=R1)
+        gemm([ws.da1[t]], [vw["recognition_1"]], [ws.dg], B, W2, R1, R1, R1, W2, transB=True)
+
+    # bf16 configuration: VAE GEMM operands bf16 (fp32 accumulate), activations
+    # stored bf16 (post-activation only: softplus' = 1 - exp(-softplus)), the
+    # LSTM / heads / STN / canvas / losses stay fp32.
+    @staticmethod
+    def _pad8(n):
+        return (n + 7) // 8 * 8
+
+    def _pack_bf16(self):
+        """Refresh the bf16 weight packs after a parameter update:
+        wt[name] = W^T [out][in8] (forward B operand), wn[name] = W [in][out8] (dX)."""
+        if getattr(self, "_pack_version", None) == self.params.version:
+            return
+        if not hasattr(self, "_wt"):
+            self._wt, self._wn = {}, {}
+            for n in self._VAE:
+                I, O = self.params.shapes["air/rnn/vae/" + n + "/weights"]
+                bf = dict(device=self.device, dtype=torch.bfloat16)
+                self._wt[n] = torch.zeros((O, self._pad8(I)), **bf)
+                self._wn[n] = torch.zeros((I, self._pad8(O)), **bf)
+        for n in self._VAE:
+            w = self._P("vae/" + n + "/weights")
+            ops.cvt_bf16(w, self._wt[n], transpose=True)
+            ops.cvt_bf16(w, self._wn[n], transpose=False)
+        self._pack_version = self.params.version
+
+    def _vae_forward_bf16(self, X, ws, t, lik_std):
+        from .ops import BF_SIGMOID_NOISE, BF_SOFTPLUS, BF_STORE, gemm_bf16
+        B, W = ws.B, self.windows_size
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        Zp = self._pad8(Z)
+        self._pack_bf16()
+        wt = self._wt
+        vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
+        ops.stn_forward(X, ws.th_f[t], (W, W), out=ws.gb[t])
+        gemm_bf16([ws.gb[t]], [wt["recognition_1"]], [ws.a1b[t]], B, R1, W2, W2, W2, R1,
+                  epi=BF_SOFTPLUS, bias=[vb["recognition_1"]])
+        gemm_bf16([ws.a1b[t]], [wt["recognition_2"]], [ws.a2b[t]], B, R2, R1, R1, R1, R2,
+                  epi=BF_SOFTPLUS, bias=[vb["recognition_2"]])
+        gemm_bf16([ws.a2b[t], ws.a2b[t]], [wt["rec_mean"], wt["rec_log_variance"]],
+                  [ws.mu[t], ws.lv[t]], B, Z, R2, R2, R2, Z, epi=BF_STORE,
+                  bias=[vb["rec_mean"], vb["rec_log_variance"]])
+        self._vae_sample_fwd(ws, t, ws.zb[t], Zp)
+        gemm_bf16([ws.zb[t]], [wt["generative_1"]], [ws.d1b[t]], B, G1, Zp, Zp, Zp, G1,
+                  epi=BF_SOFTPLUS, bias=[vb["generative_1"]])
+        gemm_bf16([ws.d1b[t]], [wt["generative_2"]], [ws.d2b[t]], B, G2, G1, G1, G1, G2,
+                  epi=BF_SOFTPLUS, bias=[vb["generative_2"]])
+        gemm_bf16([ws.d2b[t]], [wt["gen_mean"]], [ws.r[t]], B, W2, G2, G2, G2, W2,
+                  epi=BF_SIGMOID_NOISE, bias=[vb["gen_mean"]], aux=[ws.eps_x[t]], ldaux=W2,
+                  aux_scale=lik_std)
+
+    def _vae_backward_bf16(self, ws, t, gscale):
+        from .ops import BF_SOFTPLUS_BWD, BF_STORE, gemm_bf16
+        B = ws.B
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        Zp = self._pad8(Z)
+        wn = self._wn
+        s = stream_ptr()
+        _lib.call("mog_sigmoid_backward", dp(ws.r[t]), dp(ws.dr), dp(ws.dmb[t]), B * W2, 1, s)
+        gemm_bf16([ws.dmb[t]], [wn["gen_mean"]], [ws.dd2b[t]], B, G2, W2, W2, W2, G2,
+                  epi=BF_SOFTPLUS_BWD, aux=[ws.d2b[t]], ldaux=G2)
+        gemm_bf16([ws.dd2b[t]], [wn["generative_2"]], [ws.dd1b[t]], B, G1, G2, G2, G2, G1,
+                  epi=BF_SOFTPLUS_BWD, aux=[ws.d1b[t]], ldaux=G1)
+        gemm_bf16([ws.dd1b[t]], [wn["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z,
+                  epi=BF_STORE)
+        _lib.call("mog_vae_sample_backward", B, Z, float(self.vae_prior_mean),
+                  float(self.vae_prior_variance), float(gscale), dp(ws.mu[t]), dp(ws.lv[t]),
+                  dp(ws.eps_z[t]), dp(ws.dz), dp(ws.zmask[t]), None, None, dp(ws.dmub[t]),
+                  dp(ws.dlvb[t]), Zp, s)
+        gemm_bf16([ws.dmub[t]], [wn["rec_mean"]], [ws.tmp_a2], B, R2, Zp, Zp, Zp, R2,
+                  epi=BF_STORE)
+        gemm_bf16([ws.dlvb[t]], [wn["rec_log_variance"]], [ws.da2b[t]], B, R2, Zp, Zp, Zp, R2,
+                  epi=BF_SOFTPLUS_BWD, Cin=[ws.tmp_a2], aux=[ws.a2b[t]], ldaux=R2)
+        gemm_bf16([ws.da2b[t]], [wn["recognition_2"]], [ws.da1b[t]], B, R1, R2, R2, R2, R1,
+                  epi=BF_SOFTPLUS_BWD, aux=[ws.a1b[t]], ldaux=R1)
+        gemm_bf16([ws.da1b[t]], [wn["recognition_1"]], [ws.dg], B, W2, R1, R1, R1, W2,
+                  epi=BF_STORE)
+
+    def _dw_bf16(self, X, dY, out, K, M, N, lda, ldb, bias_out):
+        from .ops import BF_ATOMIC, gemm_bf16
         big = M >= 128 and N >= 128
         tiles = ((M + 127) // 128) * ((N + 127) // 128) if big else \
             ((M + 63) // 64) * ((N + 63) // 64)
-        splitk = max(1, min(K // 256, (1024 + tiles - 1) // tiles))
-        gemm([X], [dY], [out], M, N, K, lda, ldb, N, transA=True, epi=EPI_ATOMIC,
-             splitk=splitk, colsum=None if bias_out is None else [bias_out])
+        splitk = max(1, min(K // 512, (1024 + tiles - 1) // tiles))
+        gemm_bf16([X], [dY], [out], M, N, K, lda, ldb, N, tn=True, epi=BF_ATOMIC,
+                  splitk=splitk, colsum=[bias_out])
+
+    def _vae_weight_grads_bf16(self, ws):
+        TB = ws.B * self.max_steps
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        Zp = self._pad8(Z)
+        g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
+        gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
+        self._dw_bf16(ws.gb, ws.da1b, g("recognition_1"), TB, W2, R1, W2, R1,
+                      gb("recognition_1"))
+        self._dw_bf16(ws.a1b, ws.da2b, g("recognition_2"), TB, R1, R2, R1, R2,
+                      gb("recognition_2"))
+        self._dw_bf16(ws.a2b, ws.dmub, g("rec_mean"), TB, R2, Z, R2, Zp, gb("rec_mean"))
+        self._dw_bf16(ws.a2b, ws.dlvb, g("rec_log_variance"), TB, R2, Z, R2, Zp,
+                      gb("rec_log_variance"))
+        self._dw_bf16(ws.zb, ws.dd1b, g("generative_1"), TB, Z, G1, Zp, G1, gb("generative_1"))
+        self._dw_bf16(ws.d1b, ws.dd2b, g("generative_2"), TB, G1, G2, G1, G2,
+                      gb("generative_2"))
+        self._dw_bf16(ws.d2b, ws.dmb, g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
+
+    def _dw(self, X, dY, out, K, M, N, lda, ldb, bias_out=None):
+        """out[M,N] += X^T dY over K rows (split-K, atomics); bias_out += colsum(dY).
+        X, dY, out, bias_out may be lists (one batched launch)."""
+        if not isinstance(out, (list, tuple)):
+            X, dY, out = [X], [dY], [out]
+            bias_out = None if bias_out is None else [bias_out]
+        tiles = ((M + 63) // 64) * ((N + 63) // 64) * len(out)
+        splitk = max(1, min(K // 256, (2048 + tiles - 1) // tiles))
+        gemm(X, dY, out, M, N, K, lda, ldb, N, transA=True, epi=EPI_ATOMIC,
+             splitk=splitk, colsum=bias_out)
 
     def _weight_grads(self, X, ws):
         B, T, H = ws.B, self.max_steps, self.rnn_units
@@ -451,21 +608,28 @@ class AIRModel:
         G1, G2 = self.vae_generative_units
         HS = self.scale_hidden_units
         TB = T * B
-        g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
-        gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
-        self._dw(ws.g, ws.da1, g("recognition_1"), TB, W2, R1, W2, R1, gb("recognition_1"))
-        self._dw(ws.a1, ws.da2, g("recognition_2"), TB, R1, R2, R1, R2, gb("recognition_2"))
-        self._dw(ws.a2, ws.dmu, g("rec_mean"), TB, R2, Z, R2, Z, gb("rec_mean"))
-        self._dw(ws.a2, ws.dlv, g("rec_log_variance"), TB, R2, Z, R2, Z, gb("rec_log_variance"))
-        self._dw(ws.z, ws.dd1, g("generative_1"), TB, Z, G1, Z, G1, gb("generative_1"))
-        self._dw(ws.d1, ws.dd2, g("generative_2"), TB, G1, G2, G1, G2, gb("generative_2"))
-        self._dw(ws.d2, ws.dm, g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
-        for zi, head in enumerate(self._HEADS):
-            k = 2 if head.startswith("shift") else 1
-            self._dw(ws.h, ws.dhid[zi], self._G(head + "/hidden/weights"), TB, H, HS, H, HS,
-                     self._G(head + "/hidden/biases"))
-            self._dw(ws.hid[zi], ws.dout[zi], self._G(head + "/output/weights"), TB, HS, k, HS,
-                     2, self._G(head + "/output/biases"))
+        if self.precision == "bf16":
+            self._vae_weight_grads_bf16(ws)
+        else:
+            g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
+            gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
+            self._dw(ws.g, ws.da1, g("recognition_1"), TB, W2, R1, W2, R1, gb("recognition_1"))
+            self._dw(ws.a1, ws.da2, g("recognition_2"), TB, R1, R2, R1, R2, gb("recognition_2"))
+            self._dw(ws.a2, ws.dmu, g("rec_mean"), TB, R2, Z, R2, Z, gb("rec_mean"))
+            self._dw(ws.a2, ws.dlv, g("rec_log_variance"), TB, R2, Z, R2, Z,
+                     gb("rec_log_variance"))
+            self._dw(ws.z, ws.dd1, g("generative_1"), TB, Z, G1, Z, G1, gb("generative_1"))
+            self._dw(ws.d1, ws.dd2, g("generative_2"), TB, G1, G2, G1, G2, gb("generative_2"))
+            self._dw(ws.d2, ws.dm, g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
+        heads = list(enumerate(self._HEADS))
+        self._dw([ws.h] * 5, [ws.dhid[zi] for zi, _ in heads],
+                 [self._G(h + "/hidden/weights") for _, h in heads], TB, H, HS, H, HS,
+                 [self._G(h + "/hidden/biases") for _, h in heads])
+        for k in (1, 2):
+            sel = [(zi, h) for zi, h in heads if (2 if h.startswith("shift") else 1) == k]
+            self._dw([ws.hid[zi] for zi, _ in sel], [ws.dout[zi] for zi, _ in sel],
+                     [self._G(h + "/output/weights") for _, h in sel], TB, HS, k, HS, 2,
+                     [self._G(h + "/output/biases") for _, h in sel])
         gK = self._G("rnn/basic_lstm_cell/kernel")
         gbK = self._G("rnn/basic_lstm_cell/bias")
         if T > 1:

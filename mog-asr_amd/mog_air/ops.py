@@ -69,7 +69,7 @@ def stn_forward(U: torch.Tensor, theta: torch.Tensor, out_hw, out: Optional[torc
                 z: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
                 accumulate: bool = False) -> torch.Tensor:
     """transformer() of air/transformer.py:18 for U [N,Hin,Win] (or [N,Hin*Win] with
-    Hin=Win) and theta [N,6]."""
+    Hin=Win) and theta [N,6].  A bf16 ``out`` receives the bf16 image."""
     _chk(U, "U")
     _chk(theta, "theta")
     N = U.shape[0]
@@ -82,12 +82,46 @@ def stn_forward(U: torch.Tensor, theta: torch.Tensor, out_hw, out: Optional[torc
     assert theta.shape == (N, 6)
     if out is None:
         out = torch.empty((N, Ho * Wo), device=U.device, dtype=torch.float32)
-    assert out.numel() == N * Ho * Wo
+    assert out.numel() == N * Ho * Wo and out.is_contiguous()
     if accumulate:
         assert z is not None and mask is not None and z.shape == (N,) and mask.shape == (N,)
+        assert out.dtype == torch.float32
+        mode = 1
+    else:
+        mode = 2 if out.dtype == torch.bfloat16 else 0
     _lib.call("mog_stn_forward", dp(U), N, Hin, Win, dp(theta), Ho, Wo, dp(out), dp(z), dp(mask),
-              int(accumulate), stream_ptr())
+              mode, stream_ptr())
     return out
+
+
+BF_STORE, BF_SOFTPLUS, BF_SIGMOID_NOISE, BF_SOFTPLUS_BWD, BF_ATOMIC = 0, 1, 2, 3, 4
+
+
+def gemm_bf16(A, B, C, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, tn=False,
+              epi=BF_STORE, bias=None, Cin=None, aux=None, ldaux=0, aux_scale=0.0, splitk=1,
+              colsum=None) -> None:
+    """Batched bf16-operand MFMA GEMM (see mog_gemm_bf16); output dtype is C's."""
+    nb = len(C)
+    assert len(A) == nb and len(B) == nb and 1 <= nb <= 8
+    out_bf16 = C[0].dtype == torch.bfloat16
+
+    def arr(xs):
+        if xs is None:
+            return None
+        return _lib.ptr_array([dp(x) for x in xs])
+
+    _lib.call("mog_gemm_bf16", nb, arr(A), arr(B), arr(C), arr(bias), arr(Cin), arr(aux),
+              arr(colsum), M, N, K, lda, ldb, ldc, ldaux, int(tn), epi, int(out_bf16),
+              float(aux_scale), int(splitk), stream_ptr())
+
+
+def cvt_bf16(src: torch.Tensor, dst: torch.Tensor, transpose: bool) -> None:
+    """Pack an fp32 [R, C] matrix into a zero-padded bf16 matrix dst
+    ([C', R'] when transposed)."""
+    R, Cc = src.shape
+    rows, cols = dst.shape
+    _lib.call("mog_cvt_bf16", dp(src), R, Cc, Cc, dp(dst), rows, cols, cols, int(transpose),
+              stream_ptr())
 
 
 def stn_backward(U: torch.Tensor, theta: torch.Tensor, out_hw, G: torch.Tensor,

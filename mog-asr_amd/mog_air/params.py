@@ -71,6 +71,7 @@ class ParamStore:
         self.m = torch.zeros(self.total, **f32)
         self.v = torch.zeros(self.total, **f32)
         self.global_step = 0
+        self.version = 0  # bumped on every parameter write (bf16 packs key on it)
         self.adam_t = 0
         self.beta1_power = np.float32(0.9)
         self.beta2_power = np.float32(0.999)
@@ -100,6 +101,7 @@ class ParamStore:
                 lim = np.sqrt(6.0 / (shape[0] + shape[1]))
                 host[o:o + n] = rng.uniform(-lim, lim, n).astype(np.float32)
         self.flat.copy_(torch.from_numpy(host))
+        self.version += 1
 
     def load_dict(self, d: Dict[str, np.ndarray]) -> None:
         host = self.flat.detach().cpu().numpy().copy()
@@ -110,6 +112,7 @@ class ParamStore:
                 o = self.offsets[name]
                 host[o:o + a.size] = a.reshape(-1)
         self.flat.copy_(torch.from_numpy(host))
+        self.version += 1
 
     def state_dict(self) -> Dict[str, np.ndarray]:
         host = self.flat.detach().cpu().numpy()
@@ -159,3 +162,4 @@ class ParamStore:
         self.beta1_power = np.float32(self.beta1_power * np.float32(beta1))
         self.beta2_power = np.float32(self.beta2_power * np.float32(beta2))
         self.adam_t += 1
+        self.version += 1
