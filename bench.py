@@ -23,8 +23,51 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "images/sec/node AIR train step, Multi-MNIST 50×50 max_steps=3, 1/2/4/8 GPU"
+# peaks from /opt/skills/guides/MI355X_MICROARCH.md (dense, spec)
 HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFLOPS = 157.3
+BF16_MFMA_PEAK_TFLOPS = 2500.0
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
+
+
+def kernel_work(name, B, C2=2500, H=256, T=3):
+    """Algorithmic work per launch of a tagged kernel: (bound, amount, unit,
+    peak).  Per-unit figures in DESIGN.md §Roofline."""
+    if name == "lstm_x_projection":          # Gx = X Wx, [B,C2] x [C2,4H], fp32 MFMA
+        return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", FP32_MFMA_PEAK_TFLOPS
+    if name == "lstm_x_projection_grad":     # dWx = X^T dGsum, fp32 MFMA
+        return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", FP32_MFMA_PEAK_TFLOPS
+    if name == "stn_vae_step":               # SURVEY §8 D.3: 30,024 B per image-step
+        return "hbm", B * 30024 / 1e9, "GB/s", HBM_PEAK_GBS
+    return None
+
+
+def roofline(events, B):
+    """Dominant tagged kernel (largest total time in the timed region)."""
+    best = None
+    for name, evs in events.items():
+        durs = [a.elapsed_time(b) * 1e-3 for a, b in evs]  # seconds
+        tot = sum(durs)
+        if kernel_work(name, B) is None:
+            continue
+        if best is None or tot > best[1]:
+            best = (name, tot, durs)
+    if best is None:
+        return None
+    name, tot, durs = best
+    bound, amount, unit, peak = kernel_work(name, B)
+    avg = tot / len(durs)
+    achieved = amount / avg
+    traffic = None
+    try:
+        with open(PMC_SUMMARY) as f:
+            pmc = json.load(f)
+        traffic = pmc.get(name, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return {"kernel": name, "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
+            "frac": achieved / peak, "traffic": traffic, "launches": len(durs),
+            "avg_launch_us": avg * 1e6}
 
 
 def parse():
@@ -118,6 +161,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    model.kernel_events = {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         model.train_step_async(X, K)
@@ -126,6 +170,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    roof = roofline(model.kernel_events, B)
+    model.kernel_events = None
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -145,6 +191,7 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "canvas": "50x50",
                        "max_steps": T, "data_dependent_steps_would_be": executed,
                        "parallelism": f"dp{world}", "loss_last": loss},
+            "roofline": roof,
         }
         if args.cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

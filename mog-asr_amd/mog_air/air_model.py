@@ -252,6 +252,38 @@ class AIRModel:
         self._outputs_ready = False
 
     # ----------------------------------------------------------- helpers ---
+    # Optional per-kernel HIP-event timing (bench.py roofline): when
+    # ``kernel_events`` is a dict, every tagged launch records a (start, end)
+    # event pair on the stream it is launched on.
+    kernel_events = None
+
+    class _NoTimer:
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+    class _Timer:
+        def __init__(self, sink, name):
+            self.sink, self.name = sink, name
+
+        def __enter__(self):
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record(torch.cuda.current_stream())
+            return self
+
+        def __exit__(self, *a):
+            self.e1.record(torch.cuda.current_stream())
+            self.sink.setdefault(self.name, []).append((self.e0, self.e1))
+            return False
+
+    def _timed(self, name):
+        if self.kernel_events is None:
+            return AIRModel._NoTimer()
+        return AIRModel._Timer(self.kernel_events, name)
+
     @property
     def global_step(self) -> int:
         return self.params.global_step
@@ -319,7 +351,8 @@ class AIRModel:
         thr = self.hyper("stopping_threshold")
         lik_std = self.hyper("vae_likelihood_std")
         # hoisted x-projection of the LSTM input (input is loop-invariant in AIR)
-        gemm([X], [Wx], [ws.Gx], B, 4 * H, C2, C2, 4 * H, 4 * H)
+        with self._timed("lstm_x_projection"):
+            gemm([X], [Wx], [ws.Gx], B, 4 * H, C2, C2, 4 * H, 4 * H)
         w1 = [self._P(h + "/hidden/weights") for h in self._HEADS]
         b1 = [self._P(h + "/hidden/biases") for h in self._HEADS]
         w2 = [self._P(h + "/output/weights") for h in self._HEADS]
@@ -635,7 +668,8 @@ class AIRModel:
         if T > 1:
             self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
         # bias gradient = colsum(sum_t dG_t) = colsum(dGsum), fused here
-        self._dw(X, ws.dGsum, gK[:C2], B, C2, 4 * H, C2, 4 * H, gbK)
+        with self._timed("lstm_x_projection_grad"):
+            self._dw(X, ws.dGsum, gK[:C2], B, C2, 4 * H, C2, 4 * H, gbK)
 
     # ------------------------------------------------------------- API ----
     def _prep(self, images, targets):

@@ -23,6 +23,9 @@ for step in "$@"; do
     bench) run bench 400 python bench.py --steps 10 --warmup 3 --cpu-seconds 10 ;;
     benchq) run bench 300 python bench.py --steps 10 --warmup 3 --cpu-baseline 0 ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 2 --cpu-baseline 0 ;;
+    pmc) rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
+         run pmcf 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 3 --warmup 1 --cpu-baseline 0
+         run pmcw 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 3 --warmup 1 --cpu-baseline 0 ;;
     *) run custom 600 bash -c "$step" ;;
   esac
 done
