@@ -10,8 +10,12 @@
 //        fused bias-gradient column sums); fragments come out of the k-major
 //        LDS images with the gfx950 transpose read ds_read_b64_tr_b16.
 // All k extents are multiples of 8 (buffers are padded with zeros), so every
-// global load is a 16-byte vector.  Tile 128x128 or 64x64, BK = 32, 256
-// threads = 2x2 waves, register-staged double buffering.
+// global load is a 16-byte vector.
+//
+// Pipeline: BK = 64, two LDS stages in ONE __shared__ array, register-staged
+// prefetch of tile i+2 while tile i is multiplied and tile i+1 is written to
+// the other stage — one barrier per k-iteration.  Workgroup ids are remapped
+// so that the workgroups sharing an A row-panel run on one XCD (shared L2).
 #include "mog_common.h"
 
 namespace {
@@ -39,13 +43,19 @@ struct BPtrs {
   float* colsum[MAXB];
 };
 struct BDims {
-  int M, N, K, lda, ldb, ldc, ldaux, splitk, kchunk, out_bf16;
+  int M, N, K, lda, ldb, ldc, ldaux, splitk, kchunk, out_bf16, nx, ny;
   float aux_scale;
 };
 
-constexpr int BKK = 32;
+constexpr int BKK = 64;
 
 __device__ __forceinline__ float bf2f(__bf16 v) { return (float)v; }
+
+// bijective XCD-grouping remap of the linear workgroup id (guide §5, T1)
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
 
 template <int BM, int BN, bool TN, int EPI>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
@@ -53,21 +63,28 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
   // LDS images.  NT: [rows][BKK+8] (k contiguous).  TN: [BKK][cols+8].
   constexpr int A_ELEMS = TN ? BKK * (BM + 8) : BM * (BKK + 8);
   constexpr int B_ELEMS = TN ? BKK * (BN + 8) : BN * (BKK + 8);
+  constexpr int STAGE = A_ELEMS + B_ELEMS;
   constexpr int NA = (BM * BKK / 8) / 256;  // 16-byte chunks per thread
   constexpr int NB = (BN * BKK / 8) / 256;
-  __shared__ __attribute__((aligned(16))) __bf16 As[A_ELEMS];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[B_ELEMS];
-  const int z = blockIdx.z / D.splitk, ks = blockIdx.z - z * D.splitk;
+  constexpr int CPR = BKK / 8;              // 16-byte chunks per k-row (NT)
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * STAGE];
+
+  const int nwg = gridDim.x * gridDim.y * gridDim.z;
+  const int orig = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int wg = xcd_remap(orig, nwg);
+  const int bx = wg % D.nx, by = (wg / D.nx) % D.ny, bz = wg / (D.nx * D.ny);
+
+  const int z = bz / D.splitk, ks = bz - z * D.splitk;
   const __bf16* __restrict__ A = P.A[z];
   const __bf16* __restrict__ Bm = P.B[z];
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int m0 = by * BM, n0 = bx * BN;
   const int kbeg = ks * D.kchunk;
   const int kend = min(D.K, kbeg + D.kchunk);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
   const int M = D.M, N = D.N;
   float* colsum = P.colsum[z];
-  const bool do_cs = colsum != nullptr && blockIdx.y == 0 && t < BN;
+  const bool do_cs = colsum != nullptr && by == 0 && t < BN;
   float cs = 0.0f;
 
   floatx4 acc[MI][NI];
@@ -93,12 +110,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int q = t + 256 * i;
-      if (!TN) {  // A [M][K]: row = q / 4, k chunk = q % 4
-        const int row = q >> 2, kc = (q & 3) * 8;
+      if (!TN) {
+        const int row = q / CPR, kc = (q % CPR) * 8;
         const int gm = m0 + row, gk = k0 + kc;
         ra[i] = (gm < M && gk < kend)
                     ? *reinterpret_cast<const uint4*>(A + (size_t)gm * D.lda + gk) : zero4;
-      } else {    // A [K][M]: k row = q / (BM/8), m chunk
+      } else {
         const int k = q / (BM / 8), mc = (q % (BM / 8)) * 8;
         const int gk = k0 + k, gm = m0 + mc;
         ra[i] = (gk < kend && gm < D.lda)
@@ -108,12 +125,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int q = t + 256 * i;
-      if (!TN) {  // B [N][K]
-        const int row = q >> 2, kc = (q & 3) * 8;
+      if (!TN) {
+        const int row = q / CPR, kc = (q % CPR) * 8;
         const int gn = n0 + row, gk = k0 + kc;
         rb[i] = (gn < N && gk < kend)
                     ? *reinterpret_cast<const uint4*>(Bm + (size_t)gn * D.ldb + gk) : zero4;
-      } else {    // B [K][N]
+      } else {
         const int k = q / (BN / 8), nc = (q % (BN / 8)) * 8;
         const int gk = k0 + k, gn = n0 + nc;
         rb[i] = (gk < kend && gn < D.ldb)
@@ -121,12 +138,14 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
       }
     }
   };
-  auto store_tiles = [&]() {
+  auto store_tiles = [&](int stage) {
+    __bf16* As = lds + stage * STAGE;
+    __bf16* Bs = As + A_ELEMS;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int q = t + 256 * i;
       if (!TN) {
-        const int row = q >> 2, kc = (q & 3) * 8;
+        const int row = q / CPR, kc = (q % CPR) * 8;
         *reinterpret_cast<uint4*>(&As[row * (BKK + 8) + kc]) = ra[i];
       } else {
         const int k = q / (BM / 8), mc = (q % (BM / 8)) * 8;
@@ -137,7 +156,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
     for (int i = 0; i < NB; ++i) {
       const int q = t + 256 * i;
       if (!TN) {
-        const int row = q >> 2, kc = (q & 3) * 8;
+        const int row = q / CPR, kc = (q % CPR) * 8;
         *reinterpret_cast<uint4*>(&Bs[row * (BKK + 8) + kc]) = rb[i];
       } else {
         const int k = q / (BN / 8), nc = (q % (BN / 8)) * 8;
@@ -149,26 +168,25 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
   const int g = lane >> 4, li = lane & 15;
   // transpose-read lane roles: lane 4q+p of a 16-lane group -> row q, cols 4p..4p+3
   const int tq = li >> 2, tp = li & 3;
-
-  if (kbeg < kend) {
-    load_tiles(kbeg);
-    store_tiles();
-    __syncthreads();
-    for (int k0 = kbeg; k0 < kend; k0 += BKK) {
-      const bool has_next = k0 + BKK < kend;
-      if (has_next) load_tiles(k0 + BKK);
+  auto compute = [&](int stage) {
+    const __bf16* As = lds + stage * STAGE;
+    const __bf16* Bs = As + A_ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < BKK / 32; ++kk) {
       bf16x8 a[MI], b[NI];
       if (!TN) {
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
-          a[mi] = *reinterpret_cast<const bf16x8*>(&As[(wm + mi * 16 + li) * (BKK + 8) + 8 * g]);
+          a[mi] = *reinterpret_cast<const bf16x8*>(
+              &As[(wm + mi * 16 + li) * (BKK + 8) + kk * 32 + 8 * g]);
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
-          b[ni] = *reinterpret_cast<const bf16x8*>(&Bs[(wn + ni * 16 + li) * (BKK + 8) + 8 * g]);
+          b[ni] = *reinterpret_cast<const bf16x8*>(
+              &Bs[(wn + ni * 16 + li) * (BKK + 8) + kk * 32 + 8 * g]);
       } else {
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi) {
-          const __bf16* p0 = &As[(8 * g + tq) * (BM + 8) + wm + mi * 16 + 4 * tp];
+          const __bf16* p0 = &As[(kk * 32 + 8 * g + tq) * (BM + 8) + wm + mi * 16 + 4 * tp];
           const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
           const bf16x4 hi =
               __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p0 + 4 * (BM + 8)));
@@ -176,7 +194,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
         }
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
-          const __bf16* p0 = &Bs[(8 * g + tq) * (BN + 8) + wn + ni * 16 + 4 * tp];
+          const __bf16* p0 = &Bs[(kk * 32 + 8 * g + tq) * (BN + 8) + wn + ni * 16 + 4 * tp];
           const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
           const bf16x4 hi =
               __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p0 + 4 * (BN + 8)));
@@ -187,21 +205,34 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-      if (do_cs) {
-        if (TN) {
+          acc[mi][ni] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+    }
+    if (do_cs) {
+      if (TN) {
 #pragma unroll 8
-          for (int k = 0; k < BKK; ++k) cs += bf2f(Bs[k * (BN + 8) + t]);
-        } else {
+        for (int k = 0; k < BKK; ++k) cs += bf2f(Bs[k * (BN + 8) + t]);
+      } else {
 #pragma unroll 8
-          for (int k = 0; k < BKK; ++k) cs += bf2f(Bs[t * (BKK + 8) + k]);
-        }
+        for (int k = 0; k < BKK; ++k) cs += bf2f(Bs[t * (BKK + 8) + k]);
+      }
+    }
+  };
+
+  const int nk = kbeg < kend ? (kend - kbeg + BKK - 1) / BKK : 0;
+  if (nk > 0) {
+    load_tiles(kbeg);
+    store_tiles(0);
+    if (nk > 1) load_tiles(kbeg + BKK);
+    __syncthreads();
+    for (int it = 0; it < nk; ++it) {
+      const int cur = it & 1;
+      compute(cur);
+      if (it + 1 < nk) {
+        store_tiles(cur ^ 1);
+        if (it + 2 < nk) load_tiles(kbeg + (it + 2) * BKK);
       }
       __syncthreads();
-      if (has_next) {
-        store_tiles();
-        __syncthreads();
-      }
     }
   }
   if (do_cs && n0 + t < N) atomicAdd(colsum + n0 + t, cs);
@@ -260,7 +291,9 @@ void launch_tile(bool tn, int epi, hipStream_t s, const BPtrs& P, BDims D, int b
   D.kchunk = kchunk;
   D.splitk = (D.K + kchunk - 1) / kchunk;
   if (D.splitk < 1) D.splitk = 1;
-  dim3 g(mog_cdiv(D.N, BN), mog_cdiv(D.M, BM), batch * D.splitk);
+  D.nx = mog_cdiv(D.N, BN);
+  D.ny = mog_cdiv(D.M, BM);
+  dim3 g(D.nx, D.ny, batch * D.splitk);
   if (tn) launch<BM, BN, true>(epi, g, s, P, D);
   else launch<BM, BN, false>(epi, g, s, P, D);
 }
@@ -302,9 +335,11 @@ extern "C" int mog_gemm_bf16(int batch, const void* const* A, const void* const*
   BDims D;
   D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc; D.ldaux = ldaux;
   D.splitk = splitk; D.kchunk = 0; D.out_bf16 = out_bf16; D.aux_scale = aux_scale;
+  D.nx = D.ny = 1;
   hipStream_t s = mog_stream(stream);
+  // 128x128 only when it still gives >= 2 workgroups per CU (2 x 256 CUs)
   const long big = (long)mog_cdiv(M, 128) * mog_cdiv(N, 128) * batch * splitk;
-  if (M >= 128 && N >= 128 && big >= 256)
+  if (M >= 128 && N >= 128 && big >= 512)
     launch_tile<128, 128>(tn != 0, epi, s, P, D, batch);
   else
     launch_tile<64, 64>(tn != 0, epi, s, P, D, batch);

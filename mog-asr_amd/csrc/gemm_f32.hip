@@ -47,11 +47,18 @@ struct GemmPtrs {
   float* colsum[MAXB];
 };
 struct GemmDims {
-  int M, N, K, lda, ldb, ldc, ldaux, splitk, kchunk, vecA, vecB;
+  int M, N, K, lda, ldb, ldc, ldaux, splitk, kchunk, vecA, vecB, nx, ny;
   float aux_scale;
 };
 
 constexpr int BK = 16, PADF = 16;
+
+// bijective XCD-grouping remap of the linear workgroup id (guide §5, T1):
+// consecutive ids (same A row-panel, neighbouring N tiles) share one XCD's L2
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
 
 template <int BM, int BN, bool TA, bool TB, int EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
@@ -60,17 +67,20 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
   constexpr int NA = BM / 64, NB = BN / 64;     // float4 loads per thread
   __shared__ float As[BK][BM + PADF];
   __shared__ float Bs[BK][BN + PADF];
-  const int z = blockIdx.z / D.splitk, ks = blockIdx.z - z * D.splitk;
+  const int nwg = gridDim.x * gridDim.y * gridDim.z;
+  const int wg = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nwg);
+  const int bx = wg % D.nx, by = (wg / D.nx) % D.ny, bz = wg / (D.nx * D.ny);
+  const int z = bz / D.splitk, ks = bz - z * D.splitk;
   const float* __restrict__ A = P.A[z];
   const float* __restrict__ Bm = P.B[z];
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int m0 = by * BM, n0 = bx * BN;
   const int kbeg = ks * D.kchunk;
   const int kend = min(D.K, kbeg + D.kchunk);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
   const int M = D.M, N = D.N;
   float* colsum = P.colsum[z];
-  const bool do_cs = colsum != nullptr && blockIdx.y == 0 && t < BN;
+  const bool do_cs = colsum != nullptr && by == 0 && t < BN;
   float cs = 0.0f;
 
   floatx4 acc[MI][NI];
@@ -276,7 +286,9 @@ void launch_tile(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, Ge
   D.kchunk = kchunk;
   D.splitk = (D.K + kchunk - 1) / kchunk;
   if (D.splitk < 1) D.splitk = 1;
-  dim3 g(mog_cdiv(D.N, BN), mog_cdiv(D.M, BM), batch * D.splitk);
+  D.nx = mog_cdiv(D.N, BN);
+  D.ny = mog_cdiv(D.M, BM);
+  dim3 g(D.nx, D.ny, batch * D.splitk);
   if (!ta && !tb) launch_epi<BM, BN, false, false>(epi, g, s, P, D);
   else if (!ta && tb) launch_epi<BM, BN, false, true>(epi, g, s, P, D);
   else if (ta && !tb) launch_epi<BM, BN, true, false>(epi, g, s, P, D);
