@@ -23,6 +23,7 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 enum {
   B_STORE = 0,           // C = acc (+bias)                       fp32 or bf16 out
@@ -104,8 +105,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
         acc[mi][ni][r] = v;
       }
 
-  uint4 ra[NA], rb[NB];
-  const uint4 zero4 = make_uint4(0, 0, 0, 0);
+  u32x4 ra[NA], rb[NB];
+  const u32x4 zero4 = {0u, 0u, 0u, 0u};
   auto load_tiles = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
@@ -114,12 +115,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
         const int row = q / CPR, kc = (q % CPR) * 8;
         const int gm = m0 + row, gk = k0 + kc;
         ra[i] = (gm < M && gk < kend)
-                    ? *reinterpret_cast<const uint4*>(A + (size_t)gm * D.lda + gk) : zero4;
+                    ? *reinterpret_cast<const u32x4*>(A + (size_t)gm * D.lda + gk) : zero4;
       } else {
         const int k = q / (BM / 8), mc = (q % (BM / 8)) * 8;
         const int gk = k0 + k, gm = m0 + mc;
         ra[i] = (gk < kend && gm < D.lda)
-                    ? *reinterpret_cast<const uint4*>(A + (size_t)gk * D.lda + gm) : zero4;
+                    ? *reinterpret_cast<const u32x4*>(A + (size_t)gk * D.lda + gm) : zero4;
       }
     }
 #pragma unroll
@@ -129,12 +130,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
         const int row = q / CPR, kc = (q % CPR) * 8;
         const int gn = n0 + row, gk = k0 + kc;
         rb[i] = (gn < N && gk < kend)
-                    ? *reinterpret_cast<const uint4*>(Bm + (size_t)gn * D.ldb + gk) : zero4;
+                    ? *reinterpret_cast<const u32x4*>(Bm + (size_t)gn * D.ldb + gk) : zero4;
       } else {
         const int k = q / (BN / 8), nc = (q % (BN / 8)) * 8;
         const int gk = k0 + k, gn = n0 + nc;
         rb[i] = (gk < kend && gn < D.ldb)
-                    ? *reinterpret_cast<const uint4*>(Bm + (size_t)gk * D.ldb + gn) : zero4;
+                    ? *reinterpret_cast<const u32x4*>(Bm + (size_t)gk * D.ldb + gn) : zero4;
       }
     }
   };
@@ -146,10 +147,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
       const int q = t + 256 * i;
       if (!TN) {
         const int row = q / CPR, kc = (q % CPR) * 8;
-        *reinterpret_cast<uint4*>(&As[row * (BKK + 8) + kc]) = ra[i];
+        *reinterpret_cast<u32x4*>(&As[row * (BKK + 8) + kc]) = ra[i];
       } else {
         const int k = q / (BM / 8), mc = (q % (BM / 8)) * 8;
-        *reinterpret_cast<uint4*>(&As[k * (BM + 8) + mc]) = ra[i];
+        *reinterpret_cast<u32x4*>(&As[k * (BM + 8) + mc]) = ra[i];
       }
     }
 #pragma unroll
@@ -157,10 +158,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
       const int q = t + 256 * i;
       if (!TN) {
         const int row = q / CPR, kc = (q % CPR) * 8;
-        *reinterpret_cast<uint4*>(&Bs[row * (BKK + 8) + kc]) = rb[i];
+        *reinterpret_cast<u32x4*>(&Bs[row * (BKK + 8) + kc]) = rb[i];
       } else {
         const int k = q / (BN / 8), nc = (q % (BN / 8)) * 8;
-        *reinterpret_cast<uint4*>(&Bs[k * (BN + 8) + nc]) = rb[i];
+        *reinterpret_cast<u32x4*>(&Bs[k * (BN + 8) + nc]) = rb[i];
       }
     }
   };
@@ -255,15 +256,22 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
           atomicAdd(reinterpret_cast<float*>(Cv) + o, v);
           continue;
         }
+        // bf16 configuration: hardware transcendentals (v_exp/v_log, ~1 ulp);
+        // the bit-exact spec functions are reserved for the fp32 parity path
         if (EPI == B_SOFTPLUS_BWD) {
           const float post = bf2f(reinterpret_cast<const __bf16*>(aux)[(size_t)row * D.ldaux + col]);
-          v = v * (-mog_expm1f(-post));  // sigmoid(pre) = 1 - exp(-softplus(pre))
+          // sigmoid(pre) = 1 - exp(-softplus(pre)); series for small post
+          const float sg = post < 1e-3f ? post * (1.0f - 0.5f * post) : 1.0f - __expf(-post);
+          v = v * sg;
         } else {
           if (bias != nullptr) v = v + bias[col];
-          if (EPI == B_SOFTPLUS) v = mog_softplusf(v);
-          if (EPI == B_SIGMOID_NOISE)
-            v = mog_sigmoidf(v + reinterpret_cast<const float*>(aux)[(size_t)row * D.ldaux + col] *
-                                     D.aux_scale);
+          if (EPI == B_SOFTPLUS)  // TF thresholds, log(exp(x) + 1) between them
+            v = v > -MOG_SOFTPLUS_T ? v : (v < MOG_SOFTPLUS_T ? __expf(v) : __logf(__expf(v) + 1.0f));
+          if (EPI == B_SIGMOID_NOISE) {
+            const float y = v + reinterpret_cast<const float*>(aux)[(size_t)row * D.ldaux + col] *
+                                    D.aux_scale;
+            v = 1.0f / (1.0f + __expf(-y));
+          }
         }
         if (D.out_bf16) reinterpret_cast<__bf16*>(Cv)[o] = (__bf16)v;
         else reinterpret_cast<float*>(Cv)[o] = v;
