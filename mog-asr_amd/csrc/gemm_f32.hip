@@ -64,9 +64,12 @@ template <int BM, int BN, bool TA, bool TB, int EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
 #pragma clang fp contract(off)
   constexpr int MI = BM / 32, NI = BN / 32;     // 16x16 tiles per wave
-  constexpr int NA = BM / 64, NB = BN / 64;     // float4 loads per thread
-  __shared__ float As[BK][BM + PADF];
-  __shared__ float Bs[BK][BN + PADF];
+  constexpr int NA = BM * BK / 1024, NB = BN * BK / 1024;  // float4 loads per thread
+  constexpr int CPR = BK / 4;                              // float4 chunks per k-row
+  constexpr int LDA_S = BM + PADF, LDB_S = BN + PADF;
+  constexpr int STAGE = BK * (LDA_S + LDB_S);
+  // two pipeline stages in ONE shared array: [stage][A: BK x LDA_S | B: BK x LDB_S]
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
   const int nwg = gridDim.x * gridDim.y * gridDim.z;
   const int wg = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nwg);
   const int bx = wg % D.nx, by = (wg / D.nx) % D.ny, bz = wg / (D.nx * D.ny);
@@ -106,7 +109,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
     for (int i = 0; i < NA; ++i) {
       const int q = t + 256 * i;
       if (!TA) {
-        const int row = q >> 2, kc = (q & 3) * 4;
+        const int row = q / CPR, kc = (q % CPR) * 4;
         const int gm = m0 + row, gk = k0 + kc;
         if (D.vecA && gm < M && gk + 3 < kend) {
           const float4 v = *reinterpret_cast<const float4*>(A + (size_t)gm * D.lda + gk);
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
             rb[i][j] = (gk < kend && gn + j < N) ? Bm[(size_t)gk * D.ldb + gn + j] : 0.0f;
         }
       } else {
-        const int n = q >> 2, kc = (q & 3) * 4;
+        const int n = q / CPR, kc = (q % CPR) * 4;
         const int gn = n0 + n, gk = k0 + kc;
         if (D.vecB && gn < N && gk + 3 < kend) {
           const float4 v = *reinterpret_cast<const float4*>(Bm + (size_t)gn * D.ldb + gk);
@@ -157,18 +160,20 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
       }
     }
   };
-  auto store_tiles = [&]() {
+  auto store_tiles = [&](int stage) {
+    float* As = lds + stage * STAGE;
+    float* Bs = As + BK * LDA_S;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int q = t + 256 * i;
       if (!TA) {
-        const int row = q >> 2, kc = (q & 3) * 4;
+        const int row = q / CPR, kc = (q % CPR) * 4;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) As[kc + j][row] = ra[i][j];
+        for (int j = 0; j < 4; ++j) As[(kc + j) * LDA_S + row] = ra[i][j];
       } else {
         const int k = q / (BM / 4), mc = (q % (BM / 4)) * 4;
-        *reinterpret_cast<float4*>(&As[k][mc]) =
-            make_float4(ra[i][0], ra[i][1], ra[i][2], ra[i][3]);
+        *reinterpret_cast<floatx4*>(&As[k * LDA_S + mc]) =
+            floatx4{ra[i][0], ra[i][1], ra[i][2], ra[i][3]};
       }
     }
 #pragma unroll
@@ -176,46 +181,55 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
       const int q = t + 256 * i;
       if (!TB) {
         const int k = q / (BN / 4), nc = (q % (BN / 4)) * 4;
-        *reinterpret_cast<float4*>(&Bs[k][nc]) =
-            make_float4(rb[i][0], rb[i][1], rb[i][2], rb[i][3]);
+        *reinterpret_cast<floatx4*>(&Bs[k * LDB_S + nc]) =
+            floatx4{rb[i][0], rb[i][1], rb[i][2], rb[i][3]};
       } else {
-        const int n = q >> 2, kc = (q & 3) * 4;
+        const int n = q / CPR, kc = (q % CPR) * 4;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Bs[kc + j][n] = rb[i][j];
+        for (int j = 0; j < 4; ++j) Bs[(kc + j) * LDB_S + n] = rb[i][j];
       }
     }
   };
+  auto compute = [&](int stage) {
+    const float* As = lds + stage * STAGE;
+    const float* Bs = As + BK * LDA_S;
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      const int k = kk * 4 + (lane >> 4);
+      float a[MI], b[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) a[mi] = As[k * LDA_S + wm + mi * 16 + (lane & 15)];
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) b[ni] = Bs[k * LDB_S + wn + ni * 16 + (lane & 15)];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+    }
+    if (do_cs) {
+#pragma unroll
+      for (int k = 0; k < BK; ++k) cs += Bs[k * LDB_S + t];
+    }
+  };
 
-  if (kbeg < kend) {
+  // two-stage pipeline: tile it is multiplied from stage it&1 while tile it+1
+  // is written to the other stage and tile it+2's global loads are in flight;
+  // one barrier per k-tile.  The k order of every fma chain is unchanged.
+  const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nk > 0) {
     load_tiles(kbeg);
-    store_tiles();
+    store_tiles(0);
+    if (nk > 1) load_tiles(kbeg + BK);
     __syncthreads();
-    for (int k0 = kbeg; k0 < kend; k0 += BK) {
-      const bool has_next = k0 + BK < kend;
-      if (has_next) load_tiles(k0 + BK);
-#pragma unroll
-      for (int kk = 0; kk < BK / 4; ++kk) {
-        const int k = kk * 4 + (lane >> 4);
-        float a[MI], b[NI];
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) a[mi] = As[k][wm + mi * 16 + (lane & 15)];
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) b[ni] = Bs[k][wn + ni * 16 + (lane & 15)];
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-      }
-      if (do_cs) {
-#pragma unroll
-        for (int k = 0; k < BK; ++k) cs += Bs[k][t];
+    for (int it = 0; it < nk; ++it) {
+      const int cur = it & 1;
+      compute(cur);
+      if (it + 1 < nk) {
+        store_tiles(cur ^ 1);
+        if (it + 2 < nk) load_tiles(kbeg + (it + 2) * BK);
       }
       __syncthreads();
-      if (has_next) {
-        store_tiles();
-        __syncthreads();
-      }
     }
   }
   if (do_cs && n0 + t < N) atomicAdd(colsum + n0 + t, cs);
