@@ -1,10 +1,18 @@
 // Spatial-transformer bilinear sampler (air/transformer.py:18-175) for gfx950.
 //
-// Forward: one thread per output pixel; the affine grid is generated in
-// registers (no meshgrid / BatchMatMul tensors, transformer.py:119-163) and the
-// four corners are gathered from the (L2-resident) source image.  Arithmetic is
-// op-for-op the reference's (no contraction) so outputs are bit-identical to
-// the oracle, including the out-of-window cancellation residue.
+// One workgroup (4 waves) per image: lanes walk output columns (the x-part of
+// the affine grid is per-lane), waves walk output rows — no per-pixel integer
+// division, no meshgrid / BatchMatMul tensors (transformer.py:119-163).  The
+// four corners are gathered from the (L1/L2-resident, <= 16 KB) source image.
+// Arithmetic is op-for-op the reference's (no contraction) so outputs are
+// bit-identical to the oracle, including the out-of-window cancellation
+// residue.
+//
+// A sample whose four clipped corners coincide (x0 == x1 AND y0 == y1) has the
+// value +0 exactly (wa*I + wb*I cancels to 0, then -wa*I + wa*I = +0), so it is
+// written as 0 without gathering, and in the canvas-accumulate mode skipped:
+// c + z*0 == c bit-for-bit.  That removes the canvas read-modify-write outside
+// the write window's cross-shaped support.
 //
 // The write direction (glimpse -> canvas, air_model.py:580-588) fuses the
 // masked canvas accumulation of air_model.py:665-675:
@@ -15,26 +23,26 @@
 // sample whose clipped corners coincide on an axis (x0 == x1 or y0 == y1)
 // contributes an exact mathematical zero to both dU and dtheta (its weights
 // cancel pairwise), so it is skipped — the deterministic form of TF's
-// gradient, which leaves order-dependent rounding residue there.
+// gradient, which leaves order-dependent rounding residue there.  dot =
+// sum_p G w still includes the singly-degenerate residue samples, so it is the
+// exact adjoint of the forward value.
 #include "mog_common.h"
 
 namespace {
 
 struct Samp {
-  float x, y, x0f, x1f, y0f, y1f, xt, yt;
+  float x, y, x0f, x1f, y0f, y1f;
   int ia, ib, ic, id;
-  bool degenerate;
+  bool degenerate;  // corners coincide on at least one axis
+  bool dead;        // corners coincide on both axes: value is +0 exactly
 };
 
-__device__ __forceinline__ Samp stn_sample(const float* th, int Hin, int Win, int Hout,
-                                           int Wout, int p) {
+__device__ __forceinline__ Samp stn_sample(const float* th, int Hin, int Win, float xt,
+                                           float yt) {
 #pragma clang fp contract(off)
   Samp s;
-  const int i = p / Wout, j = p - (p / Wout) * Wout;
-  s.xt = mog_linspace(j, Wout);
-  s.yt = mog_linspace(i, Hout);
-  const float xs = (th[0] * s.xt + th[1] * s.yt) + th[2] * 1.0f;
-  const float ys = (th[3] * s.xt + th[4] * s.yt) + th[5] * 1.0f;
+  const float xs = (th[0] * xt + th[1] * yt) + th[2] * 1.0f;
+  const float ys = (th[3] * xt + th[4] * yt) + th[5] * 1.0f;
   const float wm = (float)Win - 1.001f;
   const float hm = (float)Hin - 1.001f;
   s.x = ((xs + 1.0f) * wm) / 2.0f;
@@ -50,6 +58,7 @@ __device__ __forceinline__ Samp stn_sample(const float* th, int Hin, int Win, in
   s.x0f = (float)x0; s.x1f = (float)x1; s.y0f = (float)y0; s.y1f = (float)y1;
   s.ia = y0 * Win + x0; s.ib = y1 * Win + x0; s.ic = y0 * Win + x1; s.id = y1 * Win + x1;
   s.degenerate = (x0 == x1) || (y0 == y1);
+  s.dead = (x0 == x1) && (y0 == y1);
   return s;
 }
 
@@ -63,6 +72,21 @@ __device__ __forceinline__ float stn_value(const Samp& s, const float* U) {
   return ((wa * Ia + wb * Ib) + wc * Ic) + wd * Id;
 }
 
+// Lane/row mapping: columns per pass CW = 32 (Wout <= 32, two rows per wave)
+// or 64 (one row per wave); Wout > 64 falls back to a column loop.
+struct RowMap {
+  int cw, rw, sub, j;
+};
+__device__ __forceinline__ RowMap row_map(int Wout) {
+  RowMap r;
+  const int lane = threadIdx.x & 63;
+  r.cw = Wout <= 32 ? 32 : 64;
+  r.rw = 64 / r.cw;
+  r.sub = lane / r.cw;
+  r.j = lane % r.cw;
+  return r;
+}
+
 // mode 0: out = v ; mode 1: out = mask ? out + z*v : out   (canvas accumulate)
 // mode 2: out (bf16) = v  (glimpse as the bf16 A operand of the VAE GEMM)
 template <int MODE>
@@ -72,23 +96,35 @@ __global__ __launch_bounds__(256) void stn_fwd_kernel(const float* __restrict__ 
                                                       const float* __restrict__ z,
                                                       const float* __restrict__ mask) {
 #pragma clang fp contract(off)
-  const int n = blockIdx.y;
+  const int n = blockIdx.x;
   const int P = Hout * Wout;
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= P) return;
+  if (MODE == 1 && !(mask[n] != 0.0f)) return;
   float th[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) th[k] = theta[n * 6 + k];
-  if (MODE == 1 && !(mask[n] != 0.0f)) return;
-  const Samp s = stn_sample(th, Hin, Win, Hout, Wout, p);
-  const float v = stn_value(s, U + (size_t)n * Hin * Win);
-  if (MODE == 2) {
-    reinterpret_cast<__bf16*>(outv)[(size_t)n * P + p] = (__bf16)v;
-    return;
+  const float* Un = U + (size_t)n * Hin * Win;
+  const float zn = MODE == 1 ? z[n] : 0.0f;
+  const RowMap rm = row_map(Wout);
+  const int w = threadIdx.x >> 6;
+  for (int j0 = 0; j0 < Wout; j0 += rm.cw) {
+    const int j = j0 + rm.j;
+    if (j >= Wout) continue;
+    const float xt = mog_linspace(j, Wout);
+    for (int i = w * rm.rw + rm.sub; i < Hout; i += 4 * rm.rw) {
+      const float yt = mog_linspace(i, Hout);
+      const Samp s = stn_sample(th, Hin, Win, xt, yt);
+      const size_t o = (size_t)n * P + (size_t)i * Wout + j;
+      if (MODE == 1) {
+        if (s.dead) continue;  // contribution is exactly +0
+        float* out = reinterpret_cast<float*>(outv);
+        out[o] = out[o] + zn * stn_value(s, Un);
+      } else {
+        const float v = s.dead ? 0.0f : stn_value(s, Un);
+        if (MODE == 2) reinterpret_cast<__bf16*>(outv)[o] = (__bf16)v;
+        else reinterpret_cast<float*>(outv)[o] = v;
+      }
+    }
   }
-  float* o = reinterpret_cast<float*>(outv) + (size_t)n * P + p;
-  if (MODE == 0) *o = v;
-  else *o = *o + z[n] * v;
 }
 
 // One block (256 threads) per image.
@@ -96,6 +132,7 @@ __global__ __launch_bounds__(256) void stn_bwd_kernel(
     const float* __restrict__ U, int Hin, int Win, const float* __restrict__ theta, int Hout,
     int Wout, const float* __restrict__ G, const float* __restrict__ gscale, float* dU,
     float* dtheta, float* dot) {
+#pragma clang fp contract(off)
   extern __shared__ float sU[];
   __shared__ float red[8][4];
   const int n = blockIdx.x;
@@ -113,31 +150,41 @@ __global__ __launch_bounds__(256) void stn_bwd_kernel(
   const float wm2 = ((float)Win - 1.001f) / 2.0f;
   const float hm2 = ((float)Hin - 1.001f) / 2.0f;
   float a[7] = {0, 0, 0, 0, 0, 0, 0};
-  for (int p = threadIdx.x; p < P; p += 256) {
-    const float gout = Gn[p];
-    const Samp s = stn_sample(th, Hin, Win, Hout, Wout, p);
-    if (dot != nullptr) a[6] += gout * stn_value(s, Un);
-    const float g = gout * sc;
-    if (s.degenerate || g == 0.0f) continue;
-    const float Ia = Un[s.ia], Ib = Un[s.ib], Ic = Un[s.ic], Id = Un[s.id];
-    const float ax = s.x1f - s.x, bx = s.x - s.x0f, ay = s.y1f - s.y, by = s.y - s.y0f;
-    if (want_dU) {
-      atomicAdd(&sU[s.ia], ax * ay * g);
-      atomicAdd(&sU[s.ib], ax * by * g);
-      atomicAdd(&sU[s.ic], bx * ay * g);
-      atomicAdd(&sU[s.id], bx * by * g);
+  const bool grads = sc != 0.0f && (want_dU || dtheta != nullptr);
+  const RowMap rm = row_map(Wout);
+  const int wv = threadIdx.x >> 6;
+  for (int j0 = 0; j0 < Wout; j0 += rm.cw) {
+    const int j = j0 + rm.j;
+    if (j >= Wout) continue;
+    const float xt = mog_linspace(j, Wout);
+    for (int i = wv * rm.rw + rm.sub; i < Hout; i += 4 * rm.rw) {
+      const float yt = mog_linspace(i, Hout);
+      const Samp s = stn_sample(th, Hin, Win, xt, yt);
+      if (s.dead) continue;  // value and all gradients are exactly 0
+      const float gout = Gn[i * Wout + j];
+      if (dot != nullptr) a[6] += gout * stn_value(s, Un);
+      const float g = gout * sc;
+      if (!grads || s.degenerate || g == 0.0f) continue;
+      const float Ia = Un[s.ia], Ib = Un[s.ib], Ic = Un[s.ic], Id = Un[s.id];
+      const float ax = s.x1f - s.x, bx = s.x - s.x0f, ay = s.y1f - s.y, by = s.y - s.y0f;
+      if (want_dU) {
+        atomicAdd(&sU[s.ia], ax * ay * g);
+        atomicAdd(&sU[s.ib], ax * by * g);
+        atomicAdd(&sU[s.ic], bx * ay * g);
+        atomicAdd(&sU[s.id], bx * by * g);
+      }
+      const float dx = g * (ay * (Ic - Ia) + by * (Id - Ib)) * wm2;
+      const float dy = g * (ax * (Ib - Ia) + bx * (Id - Ic)) * hm2;
+      a[0] += dx * xt; a[1] += dx * yt; a[2] += dx;
+      a[3] += dy * xt; a[4] += dy * yt; a[5] += dy;
     }
-    const float dx = g * (ay * (Ic - Ia) + by * (Id - Ib)) * wm2;
-    const float dy = g * (ax * (Ib - Ia) + bx * (Id - Ic)) * hm2;
-    a[0] += dx * s.xt; a[1] += dx * s.yt; a[2] += dx;
-    a[3] += dy * s.xt; a[4] += dy * s.yt; a[5] += dy;
   }
   // block reduce 7 accumulators
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int l = threadIdx.x & 63;
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
     float v = mog_wave_sum(a[k]);
-    if (l == 0) red[k][w] = v;
+    if (l == 0) red[k][wv] = v;
   }
   __syncthreads();
   if (threadIdx.x < 7) {
@@ -162,14 +209,13 @@ extern "C" int mog_stn_forward(const float* U, int N, int Hin, int Win, const fl
   MOG_CHECK_ARG(U && theta && out && N >= 0 && Hin > 0 && Win > 0 && Hout > 0 && Wout > 0);
   MOG_CHECK_ARG(mode >= 0 && mode <= 2 && (mode != 1 || (z && mask)));
   if (N == 0) return 0;
-  dim3 g(mog_cdiv(Hout * Wout, 256), N);
   hipStream_t s = mog_stream(stream);
   if (mode == 1)
-    stn_fwd_kernel<1><<<g, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, z, mask);
+    stn_fwd_kernel<1><<<N, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, z, mask);
   else if (mode == 2)
-    stn_fwd_kernel<2><<<g, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, nullptr, nullptr);
+    stn_fwd_kernel<2><<<N, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, nullptr, nullptr);
   else
-    stn_fwd_kernel<0><<<g, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, nullptr, nullptr);
+    stn_fwd_kernel<0><<<N, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, nullptr, nullptr);
   MOG_LAUNCH_RET();
 }
 
