@@ -97,6 +97,28 @@ int mog_air_step_backward(int B, int HS, int train, int use_num_prior, float tem
 int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, float v_plv, const float* mu,
                            const float* lv, const float* eps, float* z, void* z_bf16, int ld_zb,
                            const float* act, float* runloss, float* vkl, void* stream);
+/* ---- fused per-object step, bf16 configuration ----
+ * One launch per loop step: glimpse = STN(x, theta_f) (transformer.py:18-175),
+ * the glimpse VAE (vae.py:5-48: recognition 784->512->256 softplus, mean /
+ * log-variance 256->50, z = mu + eps*sqrt(exp(lv)), generative 50->256->512
+ * softplus, r = sigmoid(512->784 + std*eps_x)), the VAE KL into runloss under
+ * `mask` (air_model.py:718-736), and canvas += mask ? zval * STN(r, theta_b)
+ * (air_model.py:580-588, 665-675).  wt[7] are the bf16 W^T packs [out][in8] in
+ * the order recognition_1, recognition_2, rec_mean, rec_log_variance,
+ * generative_1, generative_2, gen_mean; bias[7] fp32 likewise.  Saved for the
+ * backward: gb/a1b/a2b/zb/d1b/d2b (bf16, zb row stride 56), mu/lv/z/r (fp32).
+ * Shapes must be the reference defaults (W 28, 512/256, Z 50, 256/512):
+ * anything else returns MOG_ERR_INVALID.  Replaces the per-step sequence
+ * air_model.py:523-588 (stn_forward + 6 GEMMs + vae_sample + stn accumulate). */
+int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int Z, int G1, int G2,
+                             const float* x, const float* theta_f, const float* theta_b,
+                             const float* mask, const float* zval, const float* eps_z,
+                             const float* eps_x, const void* const* wt,
+                             const float* const* bias, float lik_std, float v_pm, float v_pv,
+                             float v_plv, float* canvas, float* runloss, float* vkl, void* gb,
+                             void* a1b, void* a2b, float* mu, float* lv, float* z, void* zb,
+                             void* d1b, void* d2b, float* r, void* stream);
+
 /* dmu/dlv fp32 [B,Z] and/or bf16 copies with row stride ld_b (any may be NULL,
  * but one complete pair must be given). */
 int mog_vae_sample_backward(int B, int Z, float v_pm, float v_pv, float grad_scale,

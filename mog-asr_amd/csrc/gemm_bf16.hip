@@ -268,8 +268,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
           if (EPI == B_SOFTPLUS)  // TF thresholds, log(exp(x) + 1) between them
             v = v > -MOG_SOFTPLUS_T ? v : (v < MOG_SOFTPLUS_T ? __expf(v) : __logf(__expf(v) + 1.0f));
           if (EPI == B_SIGMOID_NOISE) {
-            const float y = v + reinterpret_cast<const float*>(aux)[(size_t)row * D.ldaux + col] *
-                                    D.aux_scale;
+            const float y = __builtin_fmaf(
+                reinterpret_cast<const float*>(aux)[(size_t)row * D.ldaux + col], D.aux_scale, v);
             v = 1.0f / (1.0f + __expf(-y));
           }
         }

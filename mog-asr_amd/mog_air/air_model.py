@@ -186,10 +186,15 @@ class AIRModel:
                  cnn=True, cnn_filters=8, num_summary_images=60, train=False, reuse=False,
                  scope="air", annealing_schedules=None, generation_batch_size=64,
                  num_prior=None, *, device=None, seed: int = 1235, noise_seed: int = 1235,
-                 grad_world: int = 1, precision: str = "fp32"):
+                 grad_world: int = 1, precision: str = "fp32", fused_step: bool = True):
         if precision not in ("fp32", "bf16"):
             raise ValueError("precision must be 'fp32' (bit-exact parity) or 'bf16'")
         self.precision = precision
+        # bf16: one fused STN-read -> VAE -> STN-write launch per loop step
+        # (vae_step.hip) when the VAE has the reference's default shape
+        self.fused_step = bool(fused_step) and precision == "bf16" and (
+            windows_size == 28 and tuple(vae_recognition_units) == (512, 256)
+            and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512))
         if cnn:
             raise NotImplementedError(
                 "cnn=True (air_model.py:763-810) is outside the hot-path scope; the entry "
@@ -384,6 +389,10 @@ class AIRModel:
                       dp(ws.digits), dp(ws.live), dp(rec), dp(ws.th_f[t]), dp(ws.th_b[t]),
                       dp(ws.scale[t]), dp(ws.shift[t]), dp(ws.zprob[t]), dp(ws.zkl[t]),
                       dp(ws.skl[t]), dp(ws.shkl[t]), dp(ws.zmask[t]), dp(ws.zval[t]), s)
+            if self.fused_step:
+                with self._timed("stn_vae_step"):
+                    self._step_fused(X, ws, t, float(lik_std))
+                continue
             # STN read -> glimpse VAE (air_model.py:523-550, vae.py:5-48)
             if self.precision == "bf16":
                 self._vae_forward_bf16(X, ws, t, float(lik_std))
@@ -568,6 +577,22 @@ class AIRModel:
         gemm_bf16([ws.d2b[t]], [wt["gen_mean"]], [ws.r[t]], B, W2, G2, G2, G2, W2,
                   epi=BF_SIGMOID_NOISE, bias=[vb["gen_mean"]], aux=[ws.eps_x[t]], ldaux=W2,
                   aux_scale=lik_std)
+
+    def _step_fused(self, X, ws, t, lik_std):
+        """STN read + VAE + latent sample/KL + STN write-accumulate in one launch
+        (vae_step.hip; same arithmetic as the unfused bf16 sequence)."""
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        self._pack_bf16()
+        wt = _lib.ptr_array([dp(self._wt[n]) for n in self._VAE])
+        bias = _lib.ptr_array([dp(self._P("vae/" + n + "/biases")) for n in self._VAE])
+        _lib.call("mog_stn_vae_step_forward", ws.B, self.canvas_size, self.windows_size, R1, R2,
+                  Z, G1, G2, dp(X), dp(ws.th_f[t]), dp(ws.th_b[t]), dp(ws.zmask[t]),
+                  dp(ws.zval[t]), dp(ws.eps_z[t]), dp(ws.eps_x[t]), wt, bias, lik_std,
+                  float(self.vae_prior_mean), float(self.vae_prior_variance),
+                  self.vae_prior_log_variance, dp(ws.canvas), dp(ws.runloss), dp(ws.vkl[t]),
+                  dp(ws.gb[t]), dp(ws.a1b[t]), dp(ws.a2b[t]), dp(ws.mu[t]), dp(ws.lv[t]),
+                  dp(ws.z[t]), dp(ws.zb[t]), dp(ws.d1b[t]), dp(ws.d2b[t]), dp(ws.r[t]),
+                  stream_ptr())
 
     def _vae_backward_bf16(self, ws, t, gscale):
         from .ops import BF_SOFTPLUS_BWD, BF_STORE, gemm_bf16

@@ -102,11 +102,11 @@ def _setup(batch=32, seed=0):
     return cfg, P, nz, x, k
 
 
-def _model(cfg, P, scope):
+def _model(cfg, P, scope, fused=True):
     from mog_air.air_model import AIRModel
     m = AIRModel(max_steps=3, scale_prior_variance=0.05, z_pres_prior_log_odds=-0.01,
                  learning_rate=1e-4, gradient_clipping_norm=1.0, cnn=False, train=True,
-                 scope=scope, device=DEV, precision="bf16")
+                 scope=scope, device=DEV, precision="bf16", fused_step=fused)
     m.params.load_dict(P)
     return m
 
@@ -150,3 +150,36 @@ def test_bf16_gradients_vs_float64_autograd():
             worst = max(worst, err)
             assert err < 6e-2, (name, err)
     print(f"bf16 worst relative gradient error {worst:.2e}")
+
+
+@pytest.mark.parametrize("batch", [100, 257])
+def test_fused_step_matches_unfused_bitwise(batch):
+    """vae_step.hip (one launch per loop step) against the unfused sequence
+    (stn_forward + 6 bf16 GEMMs + vae_sample + stn accumulate): same k-ordered
+    MFMA chains and epilogues, so every saved activation and the canvas agree
+    bit for bit, including a ragged last workgroup (batch % 32 != 0)."""
+    cfg, P, nz, x, k = _setup(batch=batch, seed=5)
+    noise = {n: torch.as_tensor(v).to(DEV) for n, v in nz.items()}
+    mf = _model(cfg, P, "fused%d" % batch, fused=True)
+    mu = _model(cfg, P, "unfused%d" % batch, fused=False)
+    assert mf.fused_step and not mu.fused_step
+    mf.infer(x, k, noise=noise)
+    mu.infer(x, k, noise=noise)
+    torch.cuda.synchronize()
+    for name in ("canvas", "runloss", "vkl", "gb", "a1b", "a2b", "mu", "lv", "z", "zb", "d1b",
+                 "d2b", "r"):
+        a, b = getattr(mf._ws, name), getattr(mu._ws, name)
+        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
+                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32)), name
+    assert mf.loss == mu.loss
+
+
+def test_fused_step_gradients_match_unfused():
+    cfg, P, nz, x, k = _setup(batch=48, seed=6)
+    noise = {n: torch.as_tensor(v).to(DEV) for n, v in nz.items()}
+    gf = _model(cfg, P, "gfused", fused=True).compute_gradients(x, k, noise=noise)
+    gu = _model(cfg, P, "gunfused", fused=False).compute_gradients(x, k, noise=noise)
+    # split-K atomics make the weight-gradient sums order-dependent: compare norms
+    for name in gu:
+        d = np.linalg.norm(gf[name] - gu[name]) / max(np.linalg.norm(gu[name]), 1e-30)
+        assert d < 1e-5, (name, d)
