@@ -149,9 +149,8 @@ def main():
                      device=dev, seed=1235, noise_seed=1235 + rank, grad_world=world,
                      precision=args.precision)
     if world > 1:
-        def _allreduce(g):
-            dist.all_reduce(g, op=dist.ReduceOp.SUM)
-        model.grad_hook = _allreduce
+        from mog_air import parallel
+        parallel.attach(model)  # one RCCL all-reduce of the flat gradient per step
     x, k = synthetic(B, 1234 + rank)
     X = torch.from_numpy(x).to(dev)
     K = torch.from_numpy(k).to(dev)

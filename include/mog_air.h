@@ -102,8 +102,9 @@ int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, float v_plv, co
  * the glimpse VAE (vae.py:5-48: recognition 784->512->256 softplus, mean /
  * log-variance 256->50, z = mu + eps*sqrt(exp(lv)), generative 50->256->512
  * softplus, r = sigmoid(512->784 + std*eps_x)), the VAE KL into runloss under
- * `mask` (air_model.py:718-736), and canvas += mask ? zval * STN(r, theta_b)
- * (air_model.py:580-588, 665-675).  wt[7] are the bf16 W^T packs [out][in8] in
+ * `mask` (air_model.py:718-736), and this step's canvas contribution
+ * canvas_part = mask ? zval * STN(r, theta_b) : 0 for every pixel
+ * (air_model.py:580-588, 665-675; summed in step order by mog_recon_loss).  wt[7] are the bf16 W^T packs [out][in8] in
  * the order recognition_1, recognition_2, rec_mean, rec_log_variance,
  * generative_1, generative_2, gen_mean; bias[7] fp32 likewise.  Saved for the
  * backward: gb/a1b/a2b/zb/d1b/d2b (bf16, zb row stride 56), mu/lv/z/r (fp32).
@@ -115,7 +116,7 @@ int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int Z, int G1,
                              const float* mask, const float* zval, const float* eps_z,
                              const float* eps_x, const void* const* wt,
                              const float* const* bias, float lik_std, float v_pm, float v_pv,
-                             float v_plv, float* canvas, float* runloss, float* vkl, void* gb,
+                             float v_plv, float* canvas_part, float* runloss, float* vkl, void* gb,
                              void* a1b, void* a2b, float* mu, float* lv, float* z, void* zb,
                              void* d1b, void* d2b, float* r, void* stream);
 
@@ -148,7 +149,12 @@ int mog_cvt_bf16(const float* src, int src_rows, int src_cols, int ld_src, void*
                  int cols, int ld_dst, int transpose, void* stream);
 
 /* ---- reconstruction loss (air_model.py:866-900) -------------------------- */
-int mog_recon_loss(const float* x, const float* canvas, const float* runloss, const int* digits,
+/* With nparts == 0 the canvas [B, C2] is read.  With nparts > 0 it is the
+ * step-ordered sum of the per-step contributions parts[t] (stride part_stride
+ * elements; written by mog_stn_vae_step_forward) and is stored to `canvas`
+ * when that is non-NULL. */
+int mog_recon_loss(const float* x, float* canvas, const float* parts, int nparts,
+                   long part_stride, const float* runloss, const int* digits,
                    const int* targets, int B, int C2, float grad_scale, float* recon,
                    float* bce, float* mse, float* loss, float* acc, float* dcanvas,
                    void* stream);

@@ -407,34 +407,62 @@ __global__ __launch_bounds__(256) void sigmoid_bwd_kernel(const float* r, const 
 
 // ---------------------------------------------------------------- loss ---
 // One block per image: clip, BCE, MSE, per-image loss, dL/dcanvas.
+__device__ __forceinline__ void recon_pixel(float c, float xv, float grad_scale, float& bce,
+                                            float& mse, float& r_out, float& g_out) {
+#pragma clang fp contract(off)
+  const float r = fmaxf(fminf(c, 1.0f), 0.0f);
+  // the BCE is a 2500-term reduction compared within 1e-5 relative, so the
+  // hardware log (v_log_f32, ~1 ulp) is used here, not the bit-exact spec
+  const float lr = __logf(r + 1e-10f);
+  const float l1r = __logf((1.0f - r) + 1e-10f);
+  bce = bce + (xv * lr + (1.0f - xv) * l1r);
+  const float d = xv - r;
+  mse = mse + d * d;
+  r_out = r;
+  const bool pass = (c >= 0.0f) && (c <= 1.0f);  // TF Min/Max grads pass at equality
+  const float g = -(xv * (1.0f / (r + 1e-10f)) - (1.0f - xv) * (1.0f / ((1.0f - r) + 1e-10f)));
+  g_out = pass ? g * grad_scale : 0.0f;
+}
+
+// One block per image, four pixels per thread-iteration (16-byte accesses).
+// With nparts > 0 the canvas is the step-ordered sum of the per-step
+// contributions ((p0 + p1) + p2 ..., the accumulation order of
+// air_model.py:665-675) and is written to canvas_out when given.
+template <bool VEC>
 __global__ __launch_bounds__(256) void recon_loss_kernel(
-    const float* __restrict__ x, const float* __restrict__ canvas,
+    const float* __restrict__ x, const float* __restrict__ canvas_in,
+    const float* __restrict__ parts, int nparts, long part_stride, float* canvas_out,
     const float* __restrict__ runloss, const int* __restrict__ digits,
     const int* __restrict__ targets, int C2, float grad_scale, float* recon, float* bce_out,
     float* mse_out, float* loss_out, float* acc_out, float* dcanvas) {
 #pragma clang fp contract(off)
   __shared__ float red[4];
   const int b = blockIdx.x;
-  const float* xb = x + (size_t)b * C2;
-  const float* cb = canvas + (size_t)b * C2;
+  const size_t base = (size_t)b * C2;
   float bce = 0.0f, mse = 0.0f;
-  for (int p = threadIdx.x; p < C2; p += 256) {
-    const float c = cb[p];
-    const float r = fmaxf(fminf(c, 1.0f), 0.0f);
-    const float xv = xb[p];
-    // the BCE is a 2500-term reduction compared within 1e-5 relative, so the
-    // hardware log (v_log_f32, ~1 ulp) is used here, not the bit-exact spec
-    const float lr = __logf(r + 1e-10f);
-    const float l1r = __logf((1.0f - r) + 1e-10f);
-    bce = bce + (xv * lr + (1.0f - xv) * l1r);
-    const float d = xv - r;
-    mse = mse + d * d;
-    if (recon) recon[(size_t)b * C2 + p] = r;
-    if (dcanvas) {
-      const bool pass = (c >= 0.0f) && (c <= 1.0f);  // TF Min/Max grads pass at equality
-      const float g = -(xv * (1.0f / (r + 1e-10f)) - (1.0f - xv) * (1.0f / ((1.0f - r) + 1e-10f)));
-      dcanvas[(size_t)b * C2 + p] = pass ? g * grad_scale : 0.0f;
+  constexpr int V = VEC ? 4 : 1;
+  typedef float vec __attribute__((ext_vector_type(V)));
+  for (int p = threadIdx.x * V; p < C2; p += 256 * V) {
+    vec c;
+    if (nparts > 0) {
+      c = *reinterpret_cast<const vec*>(parts + base + p);
+      for (int t = 1; t < nparts; ++t)
+        c = c + *reinterpret_cast<const vec*>(parts + t * part_stride + base + p);
+      if (canvas_out) *reinterpret_cast<vec*>(canvas_out + base + p) = c;
+    } else {
+      c = *reinterpret_cast<const vec*>(canvas_in + base + p);
     }
+    const vec xv = *reinterpret_cast<const vec*>(x + base + p);
+    vec r, g;
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      float ru, gu;
+      recon_pixel(c[u], xv[u], grad_scale, bce, mse, ru, gu);
+      r[u] = ru;
+      g[u] = gu;
+    }
+    if (recon) *reinterpret_cast<vec*>(recon + base + p) = r;
+    if (dcanvas) *reinterpret_cast<vec*>(dcanvas + base + p) = g;
   }
   bce = mog_block_sum256(bce, red);
   __syncthreads();
@@ -603,15 +631,23 @@ extern "C" int mog_sigmoid_backward(const float* r, const float* dr, void* dm, l
   MOG_LAUNCH_RET();
 }
 
-extern "C" int mog_recon_loss(const float* x, const float* canvas, const float* runloss,
-                              const int* digits, const int* targets, int B, int C2,
-                              float grad_scale, float* recon, float* bce, float* mse,
-                              float* loss, float* acc, float* dcanvas, void* stream) {
-  MOG_CHECK_ARG(x && canvas && runloss && digits && bce && mse && loss && B >= 0 && C2 > 0);
+extern "C" int mog_recon_loss(const float* x, float* canvas, const float* parts, int nparts,
+                              long part_stride, const float* runloss, const int* digits,
+                              const int* targets, int B, int C2, float grad_scale, float* recon,
+                              float* bce, float* mse, float* loss, float* acc, float* dcanvas,
+                              void* stream) {
+  MOG_CHECK_ARG(x && runloss && digits && bce && mse && loss && B >= 0 && C2 > 0);
+  MOG_CHECK_ARG(nparts >= 0 && (nparts > 0 ? parts != nullptr && part_stride >= (long)B * C2
+                                           : canvas != nullptr));
   if (B == 0) return 0;
-  recon_loss_kernel<<<B, 256, 0, mog_stream(stream)>>>(x, canvas, runloss, digits, targets, C2,
-                                                       grad_scale, recon, bce, mse, loss, acc,
-                                                       dcanvas);
+  if (C2 % 4 == 0)
+    recon_loss_kernel<true><<<B, 256, 0, mog_stream(stream)>>>(
+        x, canvas, parts, nparts, part_stride, canvas, runloss, digits, targets, C2, grad_scale,
+        recon, bce, mse, loss, acc, dcanvas);
+  else
+    recon_loss_kernel<false><<<B, 256, 0, mog_stream(stream)>>>(
+        x, canvas, parts, nparts, part_stride, canvas, runloss, digits, targets, C2, grad_scale,
+        recon, bce, mse, loss, acc, dcanvas);
   MOG_LAUNCH_RET();
 }
 

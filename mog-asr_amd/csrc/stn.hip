@@ -18,59 +18,16 @@
 // masked canvas accumulation of air_model.py:665-675:
 //      canvas += active ? z * w : 0.
 //
-// Backward: one workgroup per image.  dU is accumulated in LDS (no global
-// atomics; replaces TF's UnsortedSegmentSum), dtheta is block-reduced.  A
-// sample whose clipped corners coincide on an axis (x0 == x1 or y0 == y1)
-// contributes an exact mathematical zero to both dU and dtheta (its weights
-// cancel pairwise), so it is skipped — the deterministic form of TF's
-// gradient, which leaves order-dependent rounding residue there.  dot =
-// sum_p G w still includes the singly-degenerate residue samples, so it is the
-// exact adjoint of the forward value.
-#include "mog_common.h"
+// Backward: one wave per image (see stn_bwd_kernel).  A sample whose clipped
+// corners coincide on an axis (x0 == x1 or y0 == y1) contributes an exact
+// mathematical zero to both dU and dtheta (its weights cancel pairwise), so it
+// is skipped — the deterministic form of TF's gradient, which leaves
+// order-dependent rounding residue there.  dot = sum_p G w still includes the
+// singly-degenerate residue samples, so it is the exact adjoint of the forward
+// value.  dU replaces TF's UnsortedSegmentSum (transformer.py:96-116).
+#include "stn_geom.h"
 
 namespace {
-
-struct Samp {
-  float x, y, x0f, x1f, y0f, y1f;
-  int ia, ib, ic, id;
-  bool degenerate;  // corners coincide on at least one axis
-  bool dead;        // corners coincide on both axes: value is +0 exactly
-};
-
-__device__ __forceinline__ Samp stn_sample(const float* th, int Hin, int Win, float xt,
-                                           float yt) {
-#pragma clang fp contract(off)
-  Samp s;
-  const float xs = (th[0] * xt + th[1] * yt) + th[2] * 1.0f;
-  const float ys = (th[3] * xt + th[4] * yt) + th[5] * 1.0f;
-  const float wm = (float)Win - 1.001f;
-  const float hm = (float)Hin - 1.001f;
-  s.x = ((xs + 1.0f) * wm) / 2.0f;
-  s.y = ((ys + 1.0f) * hm) / 2.0f;
-  const float fx = fminf(fmaxf(floorf(s.x), -1073741824.0f), 1073741824.0f);
-  const float fy = fminf(fmaxf(floorf(s.y), -1073741824.0f), 1073741824.0f);
-  int x0 = (int)fx, y0 = (int)fy;
-  int x1 = x0 + 1, y1 = y0 + 1;
-  x0 = min(max(x0, 0), Win - 1);
-  x1 = min(max(x1, 0), Win - 1);
-  y0 = min(max(y0, 0), Hin - 1);
-  y1 = min(max(y1, 0), Hin - 1);
-  s.x0f = (float)x0; s.x1f = (float)x1; s.y0f = (float)y0; s.y1f = (float)y1;
-  s.ia = y0 * Win + x0; s.ib = y1 * Win + x0; s.ic = y0 * Win + x1; s.id = y1 * Win + x1;
-  s.degenerate = (x0 == x1) || (y0 == y1);
-  s.dead = (x0 == x1) && (y0 == y1);
-  return s;
-}
-
-__device__ __forceinline__ float stn_value(const Samp& s, const float* U) {
-#pragma clang fp contract(off)
-  const float Ia = U[s.ia], Ib = U[s.ib], Ic = U[s.ic], Id = U[s.id];
-  const float wa = (s.x1f - s.x) * (s.y1f - s.y);
-  const float wb = (s.x1f - s.x) * (s.y - s.y0f);
-  const float wc = (s.x - s.x0f) * (s.y1f - s.y);
-  const float wd = (s.x - s.x0f) * (s.y - s.y0f);
-  return ((wa * Ia + wb * Ib) + wc * Ic) + wd * Id;
-}
 
 // Lane/row mapping: columns per pass CW = 32 (Wout <= 32, two rows per wave)
 // or 64 (one row per wave); Wout > 64 falls back to a column loop.
@@ -112,14 +69,14 @@ __global__ __launch_bounds__(256) void stn_fwd_kernel(const float* __restrict__ 
     const float xt = mog_linspace(j, Wout);
     for (int i = w * rm.rw + rm.sub; i < Hout; i += 4 * rm.rw) {
       const float yt = mog_linspace(i, Hout);
-      const Samp s = stn_sample(th, Hin, Win, xt, yt);
+      const Tap s = stn_tap(th, Hin, Win, xt, yt);
       const size_t o = (size_t)n * P + (size_t)i * Wout + j;
       if (MODE == 1) {
         if (s.dead) continue;  // contribution is exactly +0
         float* out = reinterpret_cast<float*>(outv);
-        out[o] = out[o] + zn * stn_value(s, Un);
+        out[o] = out[o] + zn * tap_value(s, Un);
       } else {
-        const float v = s.dead ? 0.0f : stn_value(s, Un);
+        const float v = s.dead ? 0.0f : tap_value(s, Un);
         if (MODE == 2) reinterpret_cast<__bf16*>(outv)[o] = (__bf16)v;
         else reinterpret_cast<float*>(outv)[o] = v;
       }
@@ -127,77 +84,127 @@ __global__ __launch_bounds__(256) void stn_fwd_kernel(const float* __restrict__ 
   }
 }
 
-// One block (256 threads) per image.
+// Backward, one wave per image (no workgroup barriers): lanes walk output
+// columns (the column geometry stays in registers), the wave walks output
+// rows with the cotangent rows prefetched one batch ahead.  The source image
+// is staged in the wave's LDS slice; dU accumulates there with LDS atomics
+// (one wave owns an image, so the accumulation order is fixed).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ __launch_bounds__(256) void stn_bwd_kernel(
-    const float* __restrict__ U, int Hin, int Win, const float* __restrict__ theta, int Hout,
-    int Wout, const float* __restrict__ G, const float* __restrict__ gscale, float* dU,
+    const float* __restrict__ U, int N, int Hin, int Win, const float* __restrict__ theta,
+    int Hout, int Wout, const float* __restrict__ G, const float* __restrict__ gscale, float* dU,
     float* dtheta, float* dot) {
 #pragma clang fp contract(off)
-  extern __shared__ float sU[];
-  __shared__ float red[8][4];
-  const int n = blockIdx.x;
+  extern __shared__ float smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = blockIdx.x * (blockDim.x >> 6) + wv;
+  if (n >= N) return;  // no workgroup barriers below
   const int HWin = Hin * Win, P = Hout * Wout;
   const bool want_dU = dU != nullptr;
-  if (want_dU)
-    for (int i = threadIdx.x; i < HWin; i += 256) sU[i] = 0.0f;
-  __syncthreads();
+  const int slice = (HWin * (want_dU ? 2 : 1) + 3) & ~3;
+  float* sU = smem + wv * slice;
+  float* sD = sU + HWin;
   float th[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) th[k] = theta[n * 6 + k];
-  const float sc = gscale ? gscale[n] : 1.0f;
+  const bool sep = stn_separable(th) && Hin < 32768 && Win < 32768;
   const float* Un = U + (size_t)n * HWin;
-  const float* Gn = G + (size_t)n * P;
-  const float wm2 = ((float)Win - 1.001f) / 2.0f;
-  const float hm2 = ((float)Hin - 1.001f) / 2.0f;
-  float a[7] = {0, 0, 0, 0, 0, 0, 0};
-  const bool grads = sc != 0.0f && (want_dU || dtheta != nullptr);
-  const RowMap rm = row_map(Wout);
-  const int wv = threadIdx.x >> 6;
-  for (int j0 = 0; j0 < Wout; j0 += rm.cw) {
-    const int j = j0 + rm.j;
-    if (j >= Wout) continue;
-    const float xt = mog_linspace(j, Wout);
-    for (int i = wv * rm.rw + rm.sub; i < Hout; i += 4 * rm.rw) {
-      const float yt = mog_linspace(i, Hout);
-      const Samp s = stn_sample(th, Hin, Win, xt, yt);
-      if (s.dead) continue;  // value and all gradients are exactly 0
-      const float gout = Gn[i * Wout + j];
-      if (dot != nullptr) a[6] += gout * stn_value(s, Un);
-      const float g = gout * sc;
-      if (!grads || s.degenerate || g == 0.0f) continue;
-      const float Ia = Un[s.ia], Ib = Un[s.ib], Ic = Un[s.ic], Id = Un[s.id];
-      const float ax = s.x1f - s.x, bx = s.x - s.x0f, ay = s.y1f - s.y, by = s.y - s.y0f;
-      if (want_dU) {
-        atomicAdd(&sU[s.ia], ax * ay * g);
-        atomicAdd(&sU[s.ib], ax * by * g);
-        atomicAdd(&sU[s.ic], bx * ay * g);
-        atomicAdd(&sU[s.id], bx * by * g);
-      }
-      const float dx = g * (ay * (Ic - Ia) + by * (Id - Ib)) * wm2;
-      const float dy = g * (ax * (Ib - Ia) + bx * (Id - Ic)) * hm2;
-      a[0] += dx * xt; a[1] += dx * yt; a[2] += dx;
-      a[3] += dy * xt; a[4] += dy * yt; a[5] += dy;
-    }
-  }
-  // block reduce 7 accumulators
-  const int l = threadIdx.x & 63;
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    float v = mog_wave_sum(a[k]);
-    if (l == 0) red[k][wv] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < 7) {
-    const int k = threadIdx.x;
-    const float v = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
-    if (k < 6) {
-      if (dtheta) dtheta[n * 6 + k] = v;
-    } else if (dot) {
-      dot[n] = v;
-    }
+  if ((HWin & 3) == 0) {
+    const floatx4* src = reinterpret_cast<const floatx4*>(Un);
+    for (int q = lane; q < HWin / 4; q += 64) reinterpret_cast<floatx4*>(sU)[q] = src[q];
+  } else {
+    for (int i = lane; i < HWin; i += 64) sU[i] = Un[i];
   }
   if (want_dU)
-    for (int i = threadIdx.x; i < HWin; i += 256) dU[(size_t)n * HWin + i] = sU[i];
+    for (int i = lane; i < HWin; i += 64) sD[i] = 0.0f;
+  wave_sync();
+  const float sc = gscale ? gscale[n] : 1.0f;
+  const float wm2 = ((float)Win - 1.001f) / 2.0f;
+  const float hm2 = ((float)Hin - 1.001f) / 2.0f;
+  const bool grads = sc != 0.0f && (want_dU || dtheta != nullptr);
+  float a[7] = {0, 0, 0, 0, 0, 0, 0};
+  const float* Gn = G + (size_t)n * P;
+  // Wout <= 32: two output rows per pass (lane halves), else one
+  const int cw = Wout <= 32 ? 32 : 64, rp = 64 / cw;
+  const int sub = lane / cw, jl = lane - sub * cw;
+  for (int j0 = 0; j0 < Wout; j0 += cw) {
+    const int j = j0 + jl;
+    const bool jv = j < Wout;
+    const int jc = jv ? j : Wout - 1;
+    const float xt = mog_linspace(jc, Wout);
+    const float4 ex_sep = axis4(axis_col(th, Hin, Win, Hout, Wout, jc), 1);
+    // Cotangent rows are loaded unpredicated from clamped (always valid)
+    // addresses, so the waitcnt pass can count the one-batch prefetch exactly
+    // (a predicated load makes it wait for everything outstanding).
+    constexpr int BR = 4;  // passes per batch
+    float gq[BR], gn[BR];
+#pragma unroll
+    for (int u = 0; u < BR; ++u) gn[u] = Gn[min(sub + rp * u, Hout - 1) * Wout + jc];
+    for (int i0 = 0; i0 < Hout; i0 += rp * BR) {
+#pragma unroll
+      for (int u = 0; u < BR; ++u) gq[u] = gn[u];
+#pragma unroll
+      for (int u = 0; u < BR; ++u)  // prefetch the next batch
+        gn[u] = Gn[min(i0 + rp * BR + sub + rp * u, Hout - 1) * Wout + jc];
+#pragma unroll
+      for (int u = 0; u < BR; ++u) {
+        const int i = i0 + sub + rp * u;
+        if (!jv || i >= Hout) continue;
+        const float yt = mog_linspace(i, Hout);
+        float4 ex, ey;
+        if (sep) {
+          ex = ex_sep;
+          ey = axis4(axis_row(th, Hin, Win, Hout, Wout, i), Win);
+        } else {
+          const Tap t = stn_tap(th, Hin, Win, xt, yt);
+          ex = make_float4(__int_as_float((int)t.x0f), __int_as_float((int)t.x1f), t.x1f - t.x,
+                           t.x - t.x0f);
+          ey = make_float4(__int_as_float((int)t.y0f * Win), __int_as_float((int)t.y1f * Win),
+                           t.y1f - t.y, t.y - t.y0f);
+        }
+        const int x0 = __float_as_int(ex.x), x1 = __float_as_int(ex.y);
+        const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
+        if (x0 == x1 && y0 == y1) continue;  // value and all gradients exactly 0
+        const float Ia = sU[y0 + x0], Ib = sU[y1 + x0], Ic = sU[y0 + x1], Id = sU[y1 + x1];
+        const float gout = gq[u];
+        if (dot != nullptr) a[6] += gout * sample4(ex, ey, Ia, Ib, Ic, Id);
+        const float g = gout * sc;
+        if (!grads || x0 == x1 || y0 == y1 || g == 0.0f) continue;
+        const float ax = ex.z, bx = ex.w, ay = ey.z, by = ey.w;
+        if (want_dU) {
+          atomicAdd(&sD[y0 + x0], ax * ay * g);
+          atomicAdd(&sD[y1 + x0], ax * by * g);
+          atomicAdd(&sD[y0 + x1], bx * ay * g);
+          atomicAdd(&sD[y1 + x1], bx * by * g);
+        }
+        const float dx = g * (ay * (Ic - Ia) + by * (Id - Ib)) * wm2;
+        const float dy = g * (ax * (Ib - Ia) + bx * (Id - Ic)) * hm2;
+        a[0] += dx * xt; a[1] += dx * yt; a[2] += dx;
+        a[3] += dy * xt; a[4] += dy * yt; a[5] += dy;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) a[k] = mog_wave_sum(a[k]);
+  if (lane == 0) {
+    if (dtheta)
+      for (int k = 0; k < 6; ++k) dtheta[n * 6 + k] = a[k];
+    if (dot) dot[n] = a[6];
+  }
+  if (!want_dU) return;
+  wave_sync();
+  float* dUn = dU + (size_t)n * HWin;
+  if ((HWin & 3) == 0) {
+    for (int q = lane; q < HWin / 4; q += 64)
+      reinterpret_cast<floatx4*>(dUn)[q] = reinterpret_cast<const floatx4*>(sD)[q];
+  } else {
+    for (int i = lane; i < HWin; i += 64) dUn[i] = sD[i];
+  }
 }
 
 }  // namespace
@@ -225,8 +232,12 @@ extern "C" int mog_stn_backward(const float* U, int N, int Hin, int Win, const f
   MOG_CHECK_ARG(U && theta && G && N >= 0 && Hin > 0 && Win > 0 && Hout > 0 && Wout > 0);
   MOG_CHECK_ARG(Hin * Win <= 16384);
   if (N == 0) return 0;
-  const size_t lds = dU ? (size_t)Hin * Win * sizeof(float) : 0;
-  stn_bwd_kernel<<<N, 256, lds, mog_stream(stream)>>>(U, Hin, Win, theta, Hout, Wout, G, gscale,
-                                                      dU, dtheta, dot);
+  const size_t slice = ((size_t)Hin * Win * (dU ? 2 : 1) + 3) & ~(size_t)3;
+  int wpb = 4;  // waves (images) per workgroup, within 64 KiB of LDS
+  while (wpb > 1 && slice * sizeof(float) * wpb > 64 * 1024) wpb >>= 1;
+  MOG_CHECK_ARG(slice * sizeof(float) * wpb <= 160 * 1024);
+  stn_bwd_kernel<<<mog_cdiv(N, wpb), 64 * wpb, slice * sizeof(float) * wpb,
+                   mog_stream(stream)>>>(U, N, Hin, Win, theta, Hout, Wout, G, gscale, dU, dtheta,
+                                         dot);
   MOG_LAUNCH_RET();
 }

@@ -1,24 +1,28 @@
 // Fused per-object step: STN read -> glimpse VAE -> latent sample + KL ->
-// STN write + masked canvas accumulation, one launch per loop step
-// (air_model.py:500-588 + :665-675 + :718-736, vae.py:5-48,
-// transformer.py:18-175).  This is the kernel SURVEY.md §8 D.3 prices at
-// 30,024 algorithmic HBM bytes per image-step.
+// STN write, one launch per loop step (air_model.py:500-588 + :718-736,
+// vae.py:5-48, transformer.py:18-175).  This is the kernel SURVEY.md §8 D.3
+// prices at 30,024 algorithmic HBM bytes per image-step.
 //
-// One workgroup = 4 waves = MB (32) images.  Activations stay in LDS between
-// the six dense layers (bf16, rows padded to kill bank conflicts); the packed
+// One workgroup = 8 waves = MB (32) images.  Activations stay in LDS between
+// the six dense layers (bf16, rows padded against bank conflicts); the packed
 // bf16 weights (W^T, [out][in8]) stream from L2 straight into the MFMA B
-// operand (16 B per lane, one k-step of register prefetch); the A operand is
-// read from LDS with ds_read_b128.  Activations needed by the backward pass
-// (glimpse, softplus outputs, mu/logvar/z, r) are written to HBM as they are
-// produced.  The STN write re-reads r (fp32) that this workgroup just stored
-// (L2-resident, never cached in this CU's L1 before: the launch invalidates
-// L1) and accumulates into the canvas only where the sample is not exactly
-// zero (x0 == x1 && y0 == y1 gives +0; skipping keeps the canvas
-// bit-identical).
+// operand (16 B per lane, four k-steps of register prefetch); the A operand is
+// read from LDS with ds_read_b128.  Activations the backward needs (glimpse,
+// softplus outputs, mu/logvar/z, r) are flushed to HBM with 16-byte stores.
+// The STN write samples r from LDS (fp32) and stores this step's canvas
+// contribution z * w (0 where inactive or where the sample is exactly +0,
+// i.e. x0 == x1 && y0 == y1); mog_recon_loss sums the parts in step order, so
+// the canvas is bit-identical to the running accumulation of
+// air_model.py:665-675 and this kernel never waits on a canvas read.
 //
 // Precision: bf16 MFMA operands, fp32 accumulation and epilogues with
 // hardware transcendentals (the bf16 configuration, BASELINE configs[1]).
-#include "mog_common.h"
+#include <stdio.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "stn_geom.h"
 
 namespace {
 
@@ -29,20 +33,24 @@ constexpr int MB = 32;        // images per workgroup
 constexpr int NW = 8;         // waves per workgroup
 constexpr int NTHR = NW * 64;
 constexpr int W2 = 784;       // 28 x 28 glimpse
-constexpr int KG = 800;       // glimpse k extent padded to a multiple of 32
+constexpr int KG = 800;       // glimpse k extent padded to a multiple of 32 (25 k-steps)
 constexpr int SG = KG + 8;    // LDS row strides (bf16), +16 B against bank conflicts
 constexpr int S512 = 512 + 8, S256 = 256 + 8, SZ = 64 + 8;
-// LDS region A (bytes): glimpse tile, then a2 | mu | lv | z | d1, then r (fp32)
+// LDS region A (bytes): glimpse tile + read tables, then a2 | mu | lv | kl | z | d1,
+// then r (fp32).  Region H: a1, then d2, then the write tables.
+constexpr int REGION_A = MB * W2 * 4;
+constexpr int OFF_TABR = MB * SG * 2;
+constexpr int TABR = 28 + 28;                 // read tables: 28 columns + 28 rows per image
 constexpr int OFF_MU = MB * S256 * 2;
 constexpr int OFF_LV = OFF_MU + MB * 50 * 4;
-constexpr int OFF_Z = OFF_LV + MB * 50 * 4;
+constexpr int OFF_KL = OFF_LV + MB * 50 * 4;
+constexpr int OFF_Z = OFF_KL + MB * 50 * 4;
 constexpr int OFF_D1 = OFF_Z + MB * SZ * 2;
-constexpr int REGION_A = MB * W2 * 4;
-constexpr int OFF_TABR = MB * SG * 2;     // read-phase axis tables (after the glimpse tile)
-constexpr int TABR = 28 + 28;
-constexpr int TABW = 64 + 64;             // write-phase axis tables (in sH), canvas <= 64
-static_assert(OFF_TABR + MB * TABR * 8 <= REGION_A && MB * TABW * 8 <= MB * S512 * 2, "tables");
-static_assert(MB * SG * 2 <= REGION_A && OFF_D1 + MB * S256 * 2 <= REGION_A, "LDS layout");
+constexpr int CTAB_MAX = 52;                  // write tables for canvases up to 52 x 52
+constexpr int REGION_H = MB * 2 * CTAB_MAX * 16;
+static_assert(OFF_TABR + MB * TABR * 16 <= REGION_A, "read tables");
+static_assert(OFF_D1 + MB * S256 * 2 <= REGION_A, "LDS layout");
+static_assert(MB * S512 * 2 <= REGION_H, "region H");
 
 struct StepArgs {
   const float* x;            // [B, C*C] canvas input
@@ -55,7 +63,7 @@ struct StepArgs {
   const __bf16* wt[7];       // packed W^T: r1 [512][784], r2 [256][512], mu [50][256],
                              //             lv [50][256], g1 [256][56], g2 [512][256], go [784][512]
   const float* bias[7];
-  float* canvas;             // [B, C*C] accumulated in place
+  float* part;               // [B, C*C] this step's canvas contribution (written)
   float* runloss;            // [B]
   float* vkl;                // [B]
   __bf16* gb;                // [B, 784]   saved for the backward
@@ -70,158 +78,140 @@ struct StepArgs {
   float* r;                  // [B, 784]
   int B, C;
   float lik_std, v_pm, v_pv, v_plv;
-  int phases;  // profiling aid: bit mask of the phases to run (all by default)
+  int phases;               // profiling aid: bit mask of the phases to run (all by default)
+  long long* tstamp;        // profiling aid: per-block phase timestamps (or null)
 };
 
 __device__ __forceinline__ float softplus_fast(float v) {
   return v > -MOG_SOFTPLUS_T ? v : (v < MOG_SOFTPLUS_T ? __expf(v) : __logf(__expf(v) + 1.0f));
 }
 
-// Bilinear sample geometry (transformer.py:75-116), op-for-op as stn.hip.
-struct Tap {
-  float x, y, x0f, x1f, y0f, y1f;
-  int ia, ib, ic, id;
-  bool dead;  // all four clipped corners coincide: the sample is +0 exactly
-};
-
-__device__ __forceinline__ Tap stn_tap(const float* th, int Hin, int Win, float xt, float yt) {
-#pragma clang fp contract(off)
-  Tap s;
-  const float xs = (th[0] * xt + th[1] * yt) + th[2] * 1.0f;
-  const float ys = (th[3] * xt + th[4] * yt) + th[5] * 1.0f;
-  s.x = ((xs + 1.0f) * ((float)Win - 1.001f)) / 2.0f;
-  s.y = ((ys + 1.0f) * ((float)Hin - 1.001f)) / 2.0f;
-  const float fx = fminf(fmaxf(floorf(s.x), -1073741824.0f), 1073741824.0f);
-  const float fy = fminf(fmaxf(floorf(s.y), -1073741824.0f), 1073741824.0f);
-  int x0 = (int)fx, y0 = (int)fy;
-  int x1 = x0 + 1, y1 = y0 + 1;
-  x0 = min(max(x0, 0), Win - 1);
-  x1 = min(max(x1, 0), Win - 1);
-  y0 = min(max(y0, 0), Hin - 1);
-  y1 = min(max(y1, 0), Hin - 1);
-  s.dead = (x0 == x1) && (y0 == y1);
-  s.x0f = (float)x0; s.x1f = (float)x1; s.y0f = (float)y0; s.y1f = (float)y1;
-  s.ia = y0 * Win + x0; s.ib = y1 * Win + x0; s.ic = y0 * Win + x1; s.id = y1 * Win + x1;
-  return s;
-}
-
-__device__ __forceinline__ float tap_value(const Tap& s, float Ia, float Ib, float Ic, float Id) {
-#pragma clang fp contract(off)
-  const float wa = (s.x1f - s.x) * (s.y1f - s.y);
-  const float wb = (s.x1f - s.x) * (s.y - s.y0f);
-  const float wc = (s.x - s.x0f) * (s.y1f - s.y);
-  const float wd = (s.x - s.x0f) * (s.y - s.y0f);
-  return ((wa * Ia + wb * Ib) + wc * Ic) + wd * Id;
-}
-
-// Axis-aligned transforms (theta01 == theta10 == 0, always so in AIR) make the
-// sample geometry separable: x depends on the output column only, y on the
-// row only (th1*yt is +-0 and adding it leaves the sum bit-identical), so the
-// coordinate and clipped corner pair are tabulated once per column / row:
-// {coordinate, lo | hi << 16}.
-__device__ __forceinline__ float2 axis_entry(float c, float lo_f, float hi_f) {
-  return make_float2(c, __int_as_float((int)lo_f | ((int)hi_f << 16)));
-}
-
-__device__ __forceinline__ Tap tap_from(float2 ex, float2 ey, int Win) {
-  Tap s;
-  const int px = __float_as_int(ex.y), py = __float_as_int(ey.y);
-  const int x0 = px & 0xffff, x1 = px >> 16, y0 = py & 0xffff, y1 = py >> 16;
-  s.x = ex.x; s.y = ey.x;
-  s.x0f = (float)x0; s.x1f = (float)x1; s.y0f = (float)y0; s.y1f = (float)y1;
-  s.ia = y0 * Win + x0; s.ib = y1 * Win + x0; s.ic = y0 * Win + x1; s.id = y1 * Win + x1;
-  s.dead = (x0 == x1) && (y0 == y1);
-  return s;
-}
-
-// Fill tab[m][0..Wout) with column entries and tab[m][Wout..Wout+Hout) with row
-// entries for every image m whose transform (th at sth[m][th_off]) is
-// axis-aligned.  stride = entries per image.
-__device__ __forceinline__ void build_axis_tables(float2* tab, int stride, const float (*sth)[12],
-                                                  int th_off, int Hin, int Win, int Hout,
-                                                  int Wout) {
+// Expanded axis tables of every image's transform (th at sth[m][th_off]):
+// tab[m][0..Wout) columns, tab[m][Wout..Wout+Hout) rows (row entries carry
+// the source pitch Win).  Only read for axis-aligned transforms.
+__device__ __forceinline__ void build_tables(float4* tab, int stride, const float (*sth)[12],
+                                             int th_off, int Hin, int Win, int Hout, int Wout) {
   const int per = Wout + Hout;
   for (int i = threadIdx.x; i < MB * per; i += NTHR) {
     const int m = i / per, n = i - (i / per) * per;
     const float* th = &sth[m][th_off];
-    if (n < Wout) {
-      const Tap t = stn_tap(th, Hin, Win, mog_linspace(n, Wout), mog_linspace(0, Hout));
-      tab[m * stride + n] = axis_entry(t.x, t.x0f, t.x1f);
-    } else {
-      const Tap t = stn_tap(th, Hin, Win, mog_linspace(0, Wout), mog_linspace(n - Wout, Hout));
-      tab[m * stride + n] = axis_entry(t.y, t.y0f, t.y1f);
-    }
+    tab[m * stride + n] = n < Wout ? axis4(axis_col(th, Hin, Win, Hout, Wout, n), 1)
+                                   : axis4(axis_row(th, Hin, Win, Hout, Wout, n - Wout), Win);
   }
 }
 
-// One dense layer over the MB rows held in LDS: epi(row, col, A @ W^T).
-// A: LDS [MB][lda] bf16, zero-padded to K (a multiple of 32); W: global
-// [N][ldw] bf16, k < KW valid.  Waves wbase .. wbase+nw-1 take column tiles
-// round-robin, four per pass; B fragments stream from L2 with a two-k-step
-// register prefetch ring (the k loop is unrolled so the ring is static).
-template <int N, int K, int KW, class Epi>
-__device__ __forceinline__ void dense_layer(const __bf16* A, int lda, const __bf16* __restrict__ W,
-                                            int ldw, int wbase, int nw, Epi epi) {
-  constexpr int NT = (N + 15) / 16;
+// Column tiles tile_base + w + nw*c (c < TPW) of one dense layer over the MB
+// rows held in LDS, for waves wbase .. wbase+nw-1: epi(row, col, acc, aux).
+// A: LDS [MB][lda] bf16, zero-padded to K; W: global [N][ldw] bf16 whose
+// first KW columns are valid.  B fragments stream from L2 straight into the
+// MFMA with a four-k-step register prefetch ring (rolled, branch-free body so
+// the compiler keeps the distance; the ragged tail is peeled at compile
+// time).  Rows past N are clamped to a valid row and k past KW to the row's
+// last 8-element chunk: those values meet only discarded output columns or
+// zero A padding, and every load stays inside the weight pack.  With AUX the
+// epilogue operand aux[row][col] is loaded before the k loop.
+template <int N, int K, int KW, int TPW, bool AUX, class Epi>
+__device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf16* __restrict__ W,
+                                            int ldw, int tile_base, int wbase, int nw,
+                                            const float* __restrict__ aux, int ldaux, int nb,
+                                            Epi epi) {
   constexpr int KS = K / 32;
-  static_assert(K % 32 == 0, "K padded");
+  static_assert(K % 32 == 0 && KW % 8 == 0 && KW <= K, "K padding");
   const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) - wbase;
   if (w < 0 || w >= nw) return;
   const int li = lane & 15, g = lane >> 4;
-  const bf16x8 zero8 = {};
-  for (int ct0 = w; ct0 < NT; ct0 += 4 * nw) {
-    int ct[4];
-    bool cv[4];
+  int ct[TPW];
+  const __bf16* wrow[TPW];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      ct[c] = ct0 + nw * c;
-      cv[c] = ct[c] < NT && ct[c] * 16 + li < N;
-    }
-    floatx4 acc[2][4];
+  for (int c = 0; c < TPW; ++c) {
+    ct[c] = tile_base + w + nw * c;
+    wrow[c] = W + (size_t)min(ct[c] * 16 + li, N - 1) * ldw;
+  }
+  float av[2][TPW][4];
+  if constexpr (AUX) {
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // Rows past N are clamped to a valid row: those columns are discarded by
-    // the epilogue, so their B values never matter.  Past KW (only in the last
-    // k-step of a padded layer) the fragment is zeroed: A is zero there too,
-    // but the bytes beyond the last row are not ours to read.
-    const __bf16* wrow[4];
+      for (int c = 0; c < TPW; ++c)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) wrow[c] = W + (size_t)min(ct[c] * 16 + li, N - 1) * ldw + 8 * g;
-    bf16x8 bq[3][4];
-    auto loadB = [&](int ks, bf16x8* b) {
+        for (int r = 0; r < 4; ++r) {
+          const int row = rt * 16 + g * 4 + r, col = ct[c] * 16 + li;
+          av[rt][c][r] = aux[(size_t)min(row, nb - 1) * ldaux + min(col, N - 1)];  // unpredicated
+        }
+  }
+  floatx4 acc[2][TPW];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (ks * 32 + 32 <= KW)
-          b[c] = *reinterpret_cast<const bf16x8*>(wrow[c] + ks * 32);
-        else
-          b[c] = ks * 32 + 8 * g < KW ? *reinterpret_cast<const bf16x8*>(wrow[c] + ks * 32) : zero8;
-      }
-    };
-    loadB(0, bq[0]);
-    if (KS > 1) loadB(1, bq[1]);
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int c = 0; c < TPW; ++c) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int kmax = KW - 8;
+  auto loadB = [&](int ks, bf16x8* b) {
+    const int k = min(ks * 32 + 8 * g, kmax);
+#pragma unroll
+    for (int c = 0; c < TPW; ++c) b[c] = *reinterpret_cast<const bf16x8*>(wrow[c] + k);
+  };
+  auto step = [&](int ks, const bf16x8* b) {
+    const int k = ks * 32 + 8 * g;
+    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&A[li * lda + k]);
+    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&A[(16 + li) * lda + k]);
+#pragma unroll
+    for (int c = 0; c < TPW; ++c) {
+      acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b[c], acc[0][c], 0, 0, 0);
+      acc[1][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b[c], acc[1][c], 0, 0, 0);
+    }
+  };
+  if constexpr (KS < 4) {
+    bf16x8 q[TPW];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      if (ks + 2 < KS) loadB(ks + 2, bq[(ks + 2) % 3]);
-      const int k = ks * 32 + 8 * g;
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&A[li * lda + k]);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&A[(16 + li) * lda + k]);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bq[ks % 3][c], acc[0][c], 0, 0, 0);
-        acc[1][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bq[ks % 3][c], acc[1][c], 0, 0, 0);
-      }
+      loadB(ks, q);
+      step(ks, q);
     }
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (!cv[c]) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) epi(rt * 16 + g * 4 + r, ct[c] * 16 + li, acc[rt][c][r]);
-      }
+  } else {
+    constexpr int NI = (KS - 4) / 4;   // ring iterations with four refills each
+    constexpr int K0 = 4 * NI;         // first k-step of the peeled tail
+    constexpr int R = KS - K0;         // 4 .. 7 tail steps
+    bf16x8 q0[TPW], q1[TPW], q2[TPW], q3[TPW];
+    loadB(0, q0);
+    loadB(1, q1);
+    loadB(2, q2);
+    loadB(3, q3);
+#pragma unroll 1
+    for (int ks = 0; ks < K0; ks += 4) {
+      step(ks, q0);
+      loadB(ks + 4, q0);
+      __builtin_amdgcn_sched_barrier(0);
+      step(ks + 1, q1);
+      loadB(ks + 5, q1);
+      __builtin_amdgcn_sched_barrier(0);
+      step(ks + 2, q2);
+      loadB(ks + 6, q2);
+      __builtin_amdgcn_sched_barrier(0);
+      step(ks + 3, q3);
+      loadB(ks + 7, q3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    step(K0, q0);
+    if constexpr (R > 4) loadB(K0 + 4, q0);
+    step(K0 + 1, q1);
+    if constexpr (R > 5) loadB(K0 + 5, q1);
+    step(K0 + 2, q2);
+    if constexpr (R > 6) loadB(K0 + 6, q2);
+    step(K0 + 3, q3);
+    if constexpr (R > 4) step(K0 + 4, q0);
+    if constexpr (R > 5) step(K0 + 5, q1);
+    if constexpr (R > 6) step(K0 + 6, q2);
   }
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int c = 0; c < TPW; ++c) {
+      const int col = ct[c] * 16 + li;
+      if (col >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        epi(rt * 16 + g * 4 + r, col, acc[rt][c][r], AUX ? av[rt][c][r] : 0.0f);
+    }
 }
 
 // LDS tile [nb][lds] -> HBM rows [nb][ldg] with 16-byte stores (ncols * sizeof(T) % 16 == 0).
@@ -236,25 +226,33 @@ __device__ __forceinline__ void flush_rows(const T* s, int lds, T* g, int ldg, i
   }
 }
 
+#define STAMP(k) \
+  if (p.tstamp && threadIdx.x == 0) p.tstamp[blockIdx.x * 16 + (k)] = wall_clock64()
+
 __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
 #pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) unsigned char sA[REGION_A];
-  __shared__ __attribute__((aligned(16))) __bf16 sH[MB * S512];
+  __shared__ __attribute__((aligned(16))) unsigned char sHb[REGION_H];
   __shared__ float sth[MB][12];
   __shared__ float szv[MB];
   __shared__ int smask[MB];
-  __shared__ int ssep[MB];  // bit 0: theta_f axis-aligned, bit 1: theta_b
+  __shared__ int ssep[MB];  // bit 0: theta_f axis-aligned, bit 1: theta_b (and tables fit)
   const int tid = threadIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b0 = blockIdx.x * MB;
   const int nb = min(MB, p.B - b0);
   const int C = p.C, C2 = C * C;
   __bf16* sG = reinterpret_cast<__bf16*>(sA);
+  float4* tabR = reinterpret_cast<float4*>(sA + OFF_TABR);
   __bf16* sA2 = reinterpret_cast<__bf16*>(sA);
   float* sMu = reinterpret_cast<float*>(sA + OFF_MU);
   float* sLv = reinterpret_cast<float*>(sA + OFF_LV);
+  float* sKl = reinterpret_cast<float*>(sA + OFF_KL);
   __bf16* sZ = reinterpret_cast<__bf16*>(sA + OFF_Z);
   __bf16* sD1 = reinterpret_cast<__bf16*>(sA + OFF_D1);
   float* sR = reinterpret_cast<float*>(sA);
+  __bf16* sH = reinterpret_cast<__bf16*>(sHb);
+  float4* tabW = reinterpret_cast<float4*>(sHb);
 
   for (int i = tid; i < MB * 12; i += NTHR) {
     const int m = i / 12, k = i % 12;
@@ -269,84 +267,104 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
   }
   __syncthreads();
   if (tid < MB)
-    ssep[tid] = (sth[tid][1] == 0.0f && sth[tid][3] == 0.0f ? 1 : 0) |
-                (sth[tid][7] == 0.0f && sth[tid][9] == 0.0f && C <= 64 ? 2 : 0);
-  float2* tabR = reinterpret_cast<float2*>(sA + OFF_TABR);
-  build_axis_tables(tabR, TABR, sth, 0, C, C, 28, 28);
+    ssep[tid] = (stn_separable(&sth[tid][0]) ? 1 : 0) |
+                (stn_separable(&sth[tid][6]) && C <= CTAB_MAX ? 2 : 0);
+  build_tables(tabR, TABR, sth, 0, C, C, 28, 28);
   __syncthreads();
+  STAMP(0);
 
   // ---- 1. STN read (transformer.py:18-175): glimpse -> LDS bf16 ---------
-  // four samples per thread per pass: 16 independent gathers in flight
+  // Half-wave per glimpse row (lane = column), eight rows per pass so 32
+  // gathers per lane are in flight.
   if (p.phases & 1) {
-    constexpr int UR = 4;
-    for (int base = 0; base < MB * KG; base += NTHR * UR) {
-      Tap tp[UR];
-      int mm[UR];
+    constexpr int UR = 8;
+    const int hw = tid >> 5, j = tid & 31;
+    for (int rr0 = hw; rr0 < MB * 28; rr0 += 16 * UR) {
+      float I[UR][4];
+      float4 ex[UR], ey[UR];
       bool live[UR];
 #pragma unroll
       for (int u = 0; u < UR; ++u) {
-        const int idx = base + u * NTHR + tid;
-        const int m = idx / KG, k = idx - (idx / KG) * KG;
-        mm[u] = idx;
-        live[u] = idx < MB * KG && m < nb && k < W2;
-        const int i = k / 28, j = k - (k / 28) * 28;
-        const int mc = live[u] ? m : 0;
-        tp[u] = (ssep[mc] & 1) ? tap_from(tabR[mc * TABR + j], tabR[mc * TABR + 28 + i], C)
-                               : stn_tap(sth[mc], C, C, mog_linspace(j, 28), mog_linspace(i, 28));
-        live[u] = live[u] && !tp[u].dead;
+        const int rr = rr0 + 16 * u;
+        const int m = rr / 28, i = rr - (rr / 28) * 28;
+        live[u] = rr < MB * 28 && m < nb && j < 28;
+        const int mc = live[u] ? m : 0, jc = min(j, 27);
+        const float* U = p.x + (size_t)(b0 + mc) * C2;
+        if (ssep[mc] & 1) {
+          ex[u] = tabR[mc * TABR + jc];
+          ey[u] = tabR[mc * TABR + 28 + i];
+        } else {  // general affine transform: per-sample geometry
+          const Tap t = stn_tap(sth[mc], C, C, mog_linspace(jc, 28), mog_linspace(i, 28));
+          ex[u] = make_float4(__int_as_float((int)t.x0f), __int_as_float((int)t.x1f),
+                              t.x1f - t.x, t.x - t.x0f);
+          ey[u] = make_float4(__int_as_float((int)t.y0f * C), __int_as_float((int)t.y1f * C),
+                              t.y1f - t.y, t.y - t.y0f);
+        }
+        live[u] = live[u] && !axis4_dead(ex[u], ey[u]);
+        const int x0 = __float_as_int(ex[u].x), x1 = __float_as_int(ex[u].y);
+        const int y0 = __float_as_int(ey[u].x), y1 = __float_as_int(ey[u].y);
+        // unpredicated (all indices are valid clipped corners of a real
+        // image) so the waitcnt pass keeps the 32 gathers in flight
+        I[u][0] = U[y0 + x0];
+        I[u][1] = U[y1 + x0];
+        I[u][2] = U[y0 + x1];
+        I[u][3] = U[y1 + x1];
       }
-      float I[UR][4];
 #pragma unroll
       for (int u = 0; u < UR; ++u) {
-        const float* U = p.x + (size_t)(b0 + mm[u] / KG) * C2;
-        I[u][0] = live[u] ? U[tp[u].ia] : 0.0f;
-        I[u][1] = live[u] ? U[tp[u].ib] : 0.0f;
-        I[u][2] = live[u] ? U[tp[u].ic] : 0.0f;
-        I[u][3] = live[u] ? U[tp[u].id] : 0.0f;
+        const int rr = rr0 + 16 * u;
+        if (rr >= MB * 28 || j >= 28) continue;
+        const int m = rr / 28, i = rr - (rr / 28) * 28;
+        const float v = live[u] ? sample4(ex[u], ey[u], I[u][0], I[u][1], I[u][2], I[u][3]) : 0.0f;
+        sG[m * SG + i * 28 + j] = (__bf16)v;
       }
-#pragma unroll
-      for (int u = 0; u < UR; ++u) {
-        const int idx = mm[u];
-        if (idx >= MB * KG) continue;
-        const float v = live[u] ? tap_value(tp[u], I[u][0], I[u][1], I[u][2], I[u][3]) : 0.0f;
-        const int m = idx / KG, k = idx - (idx / KG) * KG;
-        sG[m * SG + k] = (__bf16)v;
-      }
+    }
+    for (int i = tid; i < MB * (KG - W2); i += NTHR) {  // zero k padding
+      const int m = i / (KG - W2);
+      sG[m * SG + W2 + (i - m * (KG - W2))] = (__bf16)0.0f;
     }
   }
   __syncthreads();
+  STAMP(1);
   if (p.phases & 16) flush_rows(sG, SG, p.gb + (size_t)b0 * W2, W2, W2, nb);
 
-  // ---- 2. a1 = softplus(g W1 + b1)  [MB x 512] -> sH ---------------------
+  // ---- 2. a1 = softplus(g W1 + b1)  [MB x 512] -> H -----------------------
   if (p.phases & 2) {
     const float* bias = p.bias[0];
-    dense_layer<512, KG, W2>(sG, SG, p.wt[0], W2, 0, NW, [&](int m, int n, float v) {
+    dense_tiles<512, KG, W2, 4, false>(sG, SG, p.wt[0], W2, 0, 0, NW, nullptr, 0, nb,
+                                       [&](int m, int n, float v, float) {
       sH[m * S512 + n] = (__bf16)softplus_fast(v + bias[n]);
     });
   }
   __syncthreads();
+  STAMP(2);
   if (p.phases & 16) flush_rows(sH, S512, p.a1b + (size_t)b0 * 512, 512, 512, nb);
-  // ---- 3. a2 = softplus(a1 W2 + b2)  [MB x 256] -> region A ---------------
+  // ---- 3. a2 = softplus(a1 W2 + b2)  [MB x 256] -> A ----------------------
   if (p.phases & 2) {
     const float* bias = p.bias[1];
-    dense_layer<256, 512, 512>(sH, S512, p.wt[1], 512, 0, NW, [&](int m, int n, float v) {
+    dense_tiles<256, 512, 512, 2, false>(sH, S512, p.wt[1], 512, 0, 0, NW, nullptr, 0, nb,
+                                         [&](int m, int n, float v, float) {
       sA2[m * S256 + n] = (__bf16)softplus_fast(v + bias[n]);
     });
   }
   __syncthreads();
+  STAMP(3);
   if (p.phases & 16) flush_rows(sA2, S256, p.a2b + (size_t)b0 * 256, 256, 256, nb);
   // ---- 4. mu | lv = a2 W + b  [MB x 50] fp32 (waves 0-3 | 4-7) ------------
   if (p.phases & 2) {
     const float* bm = p.bias[2];
-    dense_layer<50, 256, 256>(sA2, S256, p.wt[2], 256, 0, 4, [&](int m, int n, float v) {
+    dense_tiles<50, 256, 256, 1, false>(sA2, S256, p.wt[2], 256, 0, 0, 4, nullptr, 0, nb,
+                                        [&](int m, int n, float v, float) {
       sMu[m * 50 + n] = v + bm[n];
     });
     const float* bl = p.bias[3];
-    dense_layer<50, 256, 256>(sA2, S256, p.wt[3], 256, 4, 4, [&](int m, int n, float v) {
+    dense_tiles<50, 256, 256, 1, false>(sA2, S256, p.wt[3], 256, 0, 4, 4, nullptr, 0, nb,
+                                        [&](int m, int n, float v, float) {
       sLv[m * 50 + n] = v + bl[n];
     });
   }
   __syncthreads();
+  STAMP(4);
   // ---- 5. z = mu + eps sqrt(exp(lv)); VAE KL -> runloss (vae.py:27-30) ---
   for (int i = tid; i < MB * 64; i += NTHR) {
     const int m = i >> 6, k = i & 63;
@@ -355,102 +373,107 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
       const size_t o = (size_t)(b0 + m) * 50 + k;
       const float l = sLv[m * 50 + k];
       const float mv = sMu[m * 50 + k];
-      zv = mv + p.eps_z[o] * sqrtf(mog_expf(l));
+      const float var = mog_expf(l);
+      zv = mv + p.eps_z[o] * sqrtf(var);
       p.mu[o] = mv;
       p.lv[o] = l;
       p.z[o] = zv;
       p.zb[(size_t)(b0 + m) * 56 + k] = (__bf16)zv;
+      const float d = mv - p.v_pm;
+      sKl[m * 50 + k] = (((p.v_plv - l) - 1.0f) + var / p.v_pv) + (d * d) / p.v_pv;
     }
     sZ[m * SZ + k] = (__bf16)zv;
   }
+  __syncthreads();
   if (tid < nb) {  // sequential KL sum per image (k order, as vae_sample_fwd_kernel)
     const int m = tid;
+    float t[50];
+#pragma unroll
+    for (int k = 0; k < 50; ++k) t[k] = sKl[m * 50 + k];
     float sum = 0.0f;
-    for (int k = 0; k < 50; ++k) {
-      const float l = sLv[m * 50 + k];
-      const float var = mog_expf(l);
-      const float d = sMu[m * 50 + k] - p.v_pm;
-      sum = sum + ((((p.v_plv - l) - 1.0f) + var / p.v_pv) + (d * d) / p.v_pv);
-    }
+#pragma unroll
+    for (int k = 0; k < 50; ++k) sum = sum + t[k];
     const float vkl = 0.5f * sum;
     p.vkl[b0 + m] = vkl;
     if (smask[m]) p.runloss[b0 + m] = p.runloss[b0 + m] + vkl;
   }
-  __syncthreads();
+  STAMP(5);
   // ---- 6. d1 = softplus(z Wg1 + b)  [MB x 256] ----------------------------
   if (p.phases & 2) {
     const float* bias = p.bias[4];
-    dense_layer<256, 64, 56>(sZ, SZ, p.wt[4], 56, 0, NW, [&](int m, int n, float v) {
+    dense_tiles<256, 64, 56, 2, false>(sZ, SZ, p.wt[4], 56, 0, 0, NW, nullptr, 0, nb,
+                                       [&](int m, int n, float v, float) {
       sD1[m * S256 + n] = (__bf16)softplus_fast(v + bias[n]);
     });
   }
   __syncthreads();
+  STAMP(6);
   if (p.phases & 16) flush_rows(sD1, S256, p.d1b + (size_t)b0 * 256, 256, 256, nb);
-  // ---- 7. d2 = softplus(d1 Wg2 + b)  [MB x 512] -> sH ---------------------
+  // ---- 7. d2 = softplus(d1 Wg2 + b)  [MB x 512] -> H ----------------------
   if (p.phases & 2) {
     const float* bias = p.bias[5];
-    dense_layer<512, 256, 256>(sD1, S256, p.wt[5], 256, 0, NW, [&](int m, int n, float v) {
+    dense_tiles<512, 256, 256, 4, false>(sD1, S256, p.wt[5], 256, 0, 0, NW, nullptr, 0, nb,
+                                         [&](int m, int n, float v, float) {
       sH[m * S512 + n] = (__bf16)softplus_fast(v + bias[n]);
     });
   }
   __syncthreads();
+  STAMP(7);
   if (p.phases & 16) flush_rows(sH, S512, p.d2b + (size_t)b0 * 512, 512, 512, nb);
-  // ---- 8. r = sigmoid(d2 Wgo + b + std eps)  [MB x 784] fp32 -> region A --
+  // ---- 8. r = sigmoid(d2 Wgo + b + std eps)  [MB x 784] fp32 -> A ---------
+  // 49 column tiles: 32 (4 per wave) + 16 (2 per wave) + 1 (wave 0)
   if (p.phases & 2) {
     const float* bias = p.bias[6];
     const float sd = p.lik_std;
     const float* ex = p.eps_x + (size_t)b0 * W2;
-    dense_layer<784, 512, 512>(sH, S512, p.wt[6], 512, 0, NW, [&](int m, int n, float v) {
-      const float e = m < nb ? ex[m * W2 + n] : 0.0f;
+    auto epi = [&](int m, int n, float v, float e) {
       const float y = __builtin_fmaf(e, sd, v + bias[n]);
       sR[m * W2 + n] = 1.0f / (1.0f + __expf(-y));
-    });
+    };
+    dense_tiles<784, 512, 512, 4, true>(sH, S512, p.wt[6], 512, 0, 0, NW, ex, W2, nb, epi);
+    dense_tiles<784, 512, 512, 2, true>(sH, S512, p.wt[6], 512, 32, 0, NW, ex, W2, nb, epi);
+    dense_tiles<784, 512, 512, 1, true>(sH, S512, p.wt[6], 512, 48, 0, 1, ex, W2, nb, epi);
   }
   __syncthreads();
+  STAMP(8);
   if (p.phases & 16) flush_rows(sR, W2, p.r + (size_t)b0 * W2, W2, W2, nb);
-  float2* tabW = reinterpret_cast<float2*>(sH);  // d2 is dead after the last layer
-  if (C <= 64) build_axis_tables(tabW, TABW, sth, 6, 28, 28, C, C);
+  if (C <= CTAB_MAX) build_tables(tabW, 2 * C, sth, 6, 28, 28, C, C);  // d2 is dead
   __syncthreads();
-  // ---- 9. STN write + masked canvas accumulation (air_model.py:580-675) --
-  // canvas += z * w only where the sample is not exactly zero; eight pixels
-  // per thread per pass so the canvas loads overlap.
+  STAMP(9);
+  // ---- 9. STN write (air_model.py:580-588): this step's canvas part -------
+  // part = active ? z * w : 0 for every pixel (write-only; mog_recon_loss sums
+  // the parts in step order).  Lane = canvas column, waves walk (image, row).
   if (p.phases & 8) {
-    constexpr int UW = 8;
-    const int total = nb * C2;
-    const float invC2 = 1.0f / (float)C2, invC = 1.0f / (float)C;
-    for (int base = 0; base < total; base += NTHR * UW) {
-      float v[UW];
-      int off[UW];
-      bool live[UW];
-#pragma unroll
-      for (int u = 0; u < UW; ++u) {
-        const int idx = base + u * NTHR + tid;
-        // exact: |error| of the float quotient << 0.5 / C2 for idx < 2^21
-        const int m = (int)(((float)idx + 0.5f) * invC2);
-        const int k = idx - m * C2;
-        live[u] = idx < total && smask[min(m, MB - 1)];
-        off[u] = idx;
-        v[u] = 0.0f;
-        if (live[u]) {
-          const int i = (int)(((float)k + 0.5f) * invC), j = k - i * C;
-          const Tap t = (ssep[m] & 2)
-                            ? tap_from(tabW[m * TABW + j], tabW[m * TABW + C + i], 28)
-                            : stn_tap(&sth[m][6], 28, 28, mog_linspace(j, C), mog_linspace(i, C));
-          live[u] = !t.dead;
-          if (live[u]) {
-            const float* U = sR + m * W2;
-            v[u] = szv[m] * tap_value(t, U[t.ia], U[t.ib], U[t.ic], U[t.id]);
+    float* out = p.part + (size_t)b0 * C2;
+    for (int j0 = 0; j0 < C; j0 += 64) {
+      const int j = j0 + (tid & 63);
+      int m = 0, i = wv;
+      while (i >= C) { i -= C; ++m; }
+      for (; m < nb;) {
+        float v = 0.0f;
+        if (smask[m] && j < C) {
+          const float* U = sR + m * W2;
+          if (ssep[m] & 2) {
+            const float4 ex = tabW[m * 2 * C + j], ey = tabW[m * 2 * C + C + i];
+            if (!axis4_dead(ex, ey)) {
+              const int x0 = __float_as_int(ex.x), x1 = __float_as_int(ex.y);
+              const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
+              v = szv[m] * sample4(ex, ey, U[y0 + x0], U[y1 + x0], U[y0 + x1], U[y1 + x1]);
+            }
+          } else {
+            const Tap t = stn_tap(&sth[m][6], 28, 28, mog_linspace(j, C), mog_linspace(i, C));
+            if (!t.dead) v = szv[m] * tap_value(t, U);
           }
         }
+        if (j < C) out[(size_t)m * C2 + i * C + j] = v;
+        i += NW;
+        while (i >= C) { i -= C; ++m; }
       }
-      float* cv = p.canvas + (size_t)b0 * C2;
-      float c[UW];
-#pragma unroll
-      for (int u = 0; u < UW; ++u) c[u] = live[u] ? cv[off[u]] : 0.0f;
-#pragma unroll
-      for (int u = 0; u < UW; ++u)
-        if (live[u]) cv[off[u]] = c[u] + v[u];
     }
+  }
+  if (p.tstamp) {
+    __syncthreads();
+    STAMP(10);
   }
 }
 
@@ -462,7 +485,7 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
                                         const float* zval, const float* eps_z,
                                         const float* eps_x, const void* const* wt,
                                         const float* const* bias, float lik_std, float v_pm,
-                                        float v_pv, float v_plv, float* canvas,
+                                        float v_pv, float v_plv, float* canvas_part,
                                         float* runloss, float* vkl, void* gb, void* a1b,
                                         void* a2b, float* mu, float* lv, float* z, void* zb,
                                         void* d1b, void* d2b, float* r, void* stream) {
@@ -470,7 +493,7 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   // the tile shapes are compiled for the reference's default VAE
   MOG_CHECK_ARG(W == 28 && R1 == 512 && R2 == 256 && Z == 50 && G1 == 256 && G2 == 512);
   MOG_CHECK_ARG(x && theta_f && theta_b && mask && zval && eps_z && eps_x && wt && bias);
-  MOG_CHECK_ARG(canvas && runloss && vkl && gb && a1b && a2b && mu && lv && z && zb);
+  MOG_CHECK_ARG(canvas_part && runloss && vkl && gb && a1b && a2b && mu && lv && z && zb);
   MOG_CHECK_ARG(d1b && d2b && r);
   if (B == 0) return 0;
   StepArgs p;
@@ -481,7 +504,7 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
     p.wt[i] = reinterpret_cast<const __bf16*>(wt[i]);
     p.bias[i] = bias[i];
   }
-  p.canvas = canvas; p.runloss = runloss; p.vkl = vkl;
+  p.part = canvas_part; p.runloss = runloss; p.vkl = vkl;
   p.gb = reinterpret_cast<__bf16*>(gb); p.a1b = reinterpret_cast<__bf16*>(a1b);
   p.a2b = reinterpret_cast<__bf16*>(a2b); p.mu = mu; p.lv = lv; p.z = z;
   p.zb = reinterpret_cast<__bf16*>(zb); p.d1b = reinterpret_cast<__bf16*>(d1b);
@@ -489,6 +512,38 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   const char* ph = getenv("MOG_VS_PHASES");
   p.phases = ph ? atoi(ph) : 31;
   p.B = B; p.C = C; p.lik_std = lik_std; p.v_pm = v_pm; p.v_pv = v_pv; p.v_plv = v_plv;
-  stn_vae_step_bf16_kernel<<<mog_cdiv(B, MB), NTHR, 0, mog_stream(stream)>>>(p);
+  // MOG_VS_TIMING=1 (profiling aid): per-phase durations, averaged over
+  // blocks, printed to stderr (synchronizes the stream)
+  static long long* tbuf = nullptr;
+  static size_t tcap = 0;
+  const unsigned nblk = mog_cdiv(B, MB);
+  p.tstamp = nullptr;
+  if (getenv("MOG_VS_TIMING")) {
+    if (tcap < (size_t)nblk * 16) {
+      if (tbuf) (void)hipFree(tbuf);
+      tcap = (size_t)nblk * 16;
+      if (hipMalloc(&tbuf, tcap * sizeof(long long)) != hipSuccess) return MOG_ERR_INVALID;
+    }
+    p.tstamp = tbuf;
+  }
+  stn_vae_step_bf16_kernel<<<nblk, NTHR, 0, mog_stream(stream)>>>(p);
+  if (p.tstamp) {
+    std::vector<long long> h((size_t)nblk * 16);
+    (void)hipStreamSynchronize(mog_stream(stream));
+    (void)hipMemcpy(h.data(), tbuf, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
+    static const char* names[10] = {"stn_read", "L1", "L2", "mu_lv", "sample",
+                                    "g1", "g2", "go", "flush_r+tables", "write"};
+    double acc[11] = {0};
+    long long t0 = h[0], t1 = h[10];
+    for (unsigned b = 0; b < nblk; ++b) {
+      for (int k = 0; k < 10; ++k) acc[k] += (double)(h[b * 16 + k + 1] - h[b * 16 + k]);
+      acc[10] += (double)(h[b * 16 + 10] - h[b * 16]);
+      t0 = std::min(t0, h[b * 16]);
+      t1 = std::max(t1, h[b * 16 + 10]);
+    }
+    fprintf(stderr, "stn_vae_step phases (us, mean over %u blocks; 100 MHz clock):", nblk);
+    for (int k = 0; k < 10; ++k) fprintf(stderr, " %s %.2f", names[k], acc[k] / nblk / 100.0);
+    fprintf(stderr, " | block %.2f | span %.2f\n", acc[10] / nblk / 100.0, (t1 - t0) / 100.0);
+  }
   MOG_LAUNCH_RET();
 }

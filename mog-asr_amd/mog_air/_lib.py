@@ -37,7 +37,7 @@ _SIGS = {
     "mog_sigmoid_backward": [P, P, P, L, I, P],
     "mog_gemm_bf16": [I, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, I, P],
     "mog_cvt_bf16": [P, I, I, I, P, I, I, I, I, P],
-    "mog_recon_loss": [P, P, P, P, P, I, I, F, P, P, P, P, P, P, P],
+    "mog_recon_loss": [P, P, P, I, L, P, P, P, I, I, F, P, P, P, P, P, P, P],
     "mog_batch_mean": [P, P, P, P, I, P, P],
     "mog_colsum_add": [P, I, I, I, P, P],
     "mog_add": [P, P, P, L, P],

@@ -122,6 +122,8 @@ class _Workspace:
             self.d2pre, self.d2 = e(T, B, G2), e(T, B, G2)
             self.mpre = e(T, B, W2)
         self.canvas = e(B, C2)
+        # fused bf16 step: per-step canvas contributions, summed by the loss kernel
+        self.cparts = e(T, B, C2) if m.fused_step else None
         self.stop, self.runloss = e(B), e(B)
         self.digits = torch.empty(B, device=dev, dtype=torch.int32)
         self.live = torch.empty(T + 1, device=dev, dtype=torch.int32)
@@ -345,7 +347,8 @@ class AIRModel:
         K = self._P("rnn/basic_lstm_cell/kernel")
         bK = self._P("rnn/basic_lstm_cell/bias")
         Wx, Wh = K[:C2], K[C2:]
-        ws.canvas.zero_()
+        if not self.fused_step:  # fused: the loss kernel writes the canvas
+            ws.canvas.zero_()
         ws.stop.zero_()
         ws.runloss.zero_()
         ws.digits.zero_()
@@ -407,8 +410,11 @@ class AIRModel:
         """reconstruction loss (air_model.py:866-900) + batch means."""
         B, C2, s = ws.B, self.C2, stream_ptr()
         gscale = 1.0 / (B * self.grad_world)
-        _lib.call("mog_recon_loss", dp(X), dp(ws.canvas), dp(ws.runloss), dp(ws.digits),
-                  dp(targets), B, C2, float(gscale), dp(ws.recon), dp(ws.bce), dp(ws.mse),
+        parts = ws.cparts
+        _lib.call("mog_recon_loss", dp(X), dp(ws.canvas), dp(parts),
+                  self.max_steps if parts is not None else 0, B * C2, dp(ws.runloss),
+                  dp(ws.digits), dp(targets), B, C2, float(gscale), dp(ws.recon), dp(ws.bce),
+                  dp(ws.mse),
                   dp(ws.loss_b), dp(ws.acc_b) if targets is not None else None,
                   dp(ws.dcanvas) if need_grad else None, s)
         _lib.call("mog_batch_mean", dp(ws.loss_b), dp(ws.acc_b) if targets is not None else None,
@@ -589,7 +595,7 @@ class AIRModel:
                   Z, G1, G2, dp(X), dp(ws.th_f[t]), dp(ws.th_b[t]), dp(ws.zmask[t]),
                   dp(ws.zval[t]), dp(ws.eps_z[t]), dp(ws.eps_x[t]), wt, bias, lik_std,
                   float(self.vae_prior_mean), float(self.vae_prior_variance),
-                  self.vae_prior_log_variance, dp(ws.canvas), dp(ws.runloss), dp(ws.vkl[t]),
+                  self.vae_prior_log_variance, dp(ws.cparts[t]), dp(ws.runloss), dp(ws.vkl[t]),
                   dp(ws.gb[t]), dp(ws.a1b[t]), dp(ws.a2b[t]), dp(ws.mu[t]), dp(ws.lv[t]),
                   dp(ws.z[t]), dp(ws.zb[t]), dp(ws.d1b[t]), dp(ws.d2b[t]), dp(ws.r[t]),
                   stream_ptr())

@@ -108,21 +108,26 @@ def test_stn_accumulate_masked():
     np.testing.assert_array_equal(cv.cpu().numpy(), ref)
 
 
-def test_stn_backward_vs_autograd():
+@pytest.mark.parametrize("sep", [True, False])
+@pytest.mark.parametrize("src,dst", [(28, 50), (50, 28), (28, 64)])
+def test_stn_backward_vs_autograd(sep, src, dst):
+    """axis-aligned transforms take the separable (atomic-free) dU path,
+    sheared ones the LDS-atomic path; both against float64 autograd."""
     from mog_air import ops
-    rng = np.random.default_rng(7)
+    rng = np.random.default_rng(7 + src + dst)
     N = 16
-    r = rng.uniform(size=(N, 28, 28))
+    r = rng.uniform(size=(N, src, src))
     s = rng.uniform(0.2, 0.9, N)
     t = rng.uniform(-0.8, 0.8, (N, 2))
-    thb = np.stack([1 / s, 0 * s, -t[:, 0] / s, 0 * s, 1 / s, -t[:, 1] / s], 1)
-    G = rng.standard_normal((N, 2500))
+    sh = np.zeros(N) if sep else rng.uniform(-0.2, 0.2, N)
+    thb = np.stack([1 / s, sh, -t[:, 0] / s, -sh, 1 / s, -t[:, 1] / s], 1)
+    G = rng.standard_normal((N, dst * dst))
     gs = rng.uniform(size=N)
     U = torch.tensor(r, requires_grad=True)
     TH = torch.tensor(thb, requires_grad=True)
-    out = at.transformer(U, TH, (50, 50)).reshape(N, -1)
+    out = at.transformer(U, TH, (dst, dst)).reshape(N, -1)
     (out * torch.tensor(G) * torch.tensor(gs)[:, None]).sum().backward()
-    dU, dth, dot = ops.stn_backward(_cuda(r.reshape(N, -1)), _cuda(thb), (50, 50), _cuda(G),
+    dU, dth, dot = ops.stn_backward(_cuda(r.reshape(N, -1)), _cuda(thb), (dst, dst), _cuda(G),
                                     gscale=_cuda(gs), want_dot=True)
     np.testing.assert_allclose(dU.cpu().numpy(), U.grad.numpy().reshape(N, -1), rtol=1e-4,
                                atol=1e-4)
