@@ -39,6 +39,12 @@ int mog_gemm_f32(int batch, const float* const* A, const float* const* B, float*
                  const float* const* aux, float* const* colsum, int M, int N, int K, int lda,
                  int ldb, int ldc, int ldaux, int transA, int transB, int epi, float aux_scale,
                  int splitk, void* stream);
+/* C = epi(sum_s A_s op(B_s)) as one k-ordered chain over K = nseg * kseg
+ * (nseg <= 8, kseg % 16 == 0; segment s from A[s] / B[s]); epi 0 or 5.  The
+ * five heads' hidden-state gradient dh = sum_z dhid_z W1_z^T in one launch. */
+int mog_gemm_f32_kseg(int nseg, const float* const* A, const float* const* B, float* C,
+                      const float* bias, const float* Cin, int M, int N, int kseg, int lda,
+                      int ldb, int ldc, int transA, int transB, int epi, void* stream);
 
 /* ---- spatial transformer -------------------------------------------------
  * air/transformer.py:18-175 transformer(U, theta, out_size) for N images:
@@ -147,6 +153,10 @@ int mog_gemm_bf16(int batch, const void* const* A, const void* const* B, void* c
  * zero outside the (src_rows, src_cols) source extent. */
 int mog_cvt_bf16(const float* src, int src_rows, int src_cols, int ld_src, void* dst, int rows,
                  int cols, int ld_dst, int transpose, void* stream);
+/* Up to 16 of the above in one launch; dims[7*j ..] = src_rows, src_cols,
+ * ld_src, rows, cols, ld_dst, transpose of job j. */
+int mog_cvt_bf16_batch(int njobs, const float* const* src, void* const* dst, const int* dims,
+                       void* stream);
 
 /* ---- reconstruction loss (air_model.py:866-900) -------------------------- */
 /* With nparts == 0 the canvas [B, C2] is read.  With nparts > 0 it is the

@@ -370,7 +370,49 @@ __global__ __launch_bounds__(256) void cvt_bf16_kernel(const float* src, int src
   const float v = (sr < src_rows && sc < src_cols) ? src[(size_t)sr * ld_src + sc] : 0.0f;
   dst[(size_t)r * ld_dst + c] = (__bf16)v;
 }
+
+// Up to 16 conversions in one launch (the bf16 weight packs of all VAE
+// layers after an optimizer step): job j covers elements [start[j], start[j+1]).
+constexpr int CVT_MAX = 16;
+struct CvtBatch {
+  const float* src[CVT_MAX];
+  __bf16* dst[CVT_MAX];
+  int d[CVT_MAX][7];  // src_rows, src_cols, ld_src, rows, cols, ld_dst, transpose
+  long start[CVT_MAX + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void cvt_bf16_batch_kernel(CvtBatch b) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= b.start[b.n]) return;
+  int j = 0;
+  while (i >= b.start[j + 1]) ++j;
+  const int* d = b.d[j];
+  const long e = i - b.start[j];
+  const int r = e / d[4], c = e - (long)r * d[4];
+  const int sr = d[6] ? c : r, sc = d[6] ? r : c;
+  const float v = (sr < d[0] && sc < d[1]) ? b.src[j][(size_t)sr * d[2] + sc] : 0.0f;
+  b.dst[j][(size_t)r * d[5] + c] = (__bf16)v;
+}
 }  // namespace
+
+extern "C" int mog_cvt_bf16_batch(int njobs, const float* const* src, void* const* dst,
+                                  const int* dims, void* stream) {
+  MOG_CHECK_ARG(njobs >= 0 && njobs <= CVT_MAX && (njobs == 0 || (src && dst && dims)));
+  CvtBatch b;
+  b.n = njobs;
+  b.start[0] = 0;
+  for (int j = 0; j < njobs; ++j) {
+    MOG_CHECK_ARG(src[j] && dst[j] && dims[7 * j + 3] >= 0 && dims[7 * j + 4] >= 0);
+    b.src[j] = src[j];
+    b.dst[j] = reinterpret_cast<__bf16*>(dst[j]);
+    for (int k = 0; k < 7; ++k) b.d[j][k] = dims[7 * j + k];
+    b.start[j + 1] = b.start[j] + (long)dims[7 * j + 3] * dims[7 * j + 4];
+  }
+  if (njobs == 0 || b.start[njobs] == 0) return 0;
+  cvt_bf16_batch_kernel<<<mog_cdiv(b.start[njobs], 256), 256, 0, mog_stream(stream)>>>(b);
+  MOG_LAUNCH_RET();
+}
 
 extern "C" int mog_cvt_bf16(const float* src, int src_rows, int src_cols, int ld_src, void* dst,
                             int rows, int cols, int ld_dst, int transpose, void* stream) {

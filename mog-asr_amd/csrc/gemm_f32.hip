@@ -48,6 +48,7 @@ struct GemmPtrs {
 };
 struct GemmDims {
   int M, N, K, lda, ldb, ldc, ldaux, splitk, kchunk, vecA, vecB, nx, ny;
+  int kseg;  // > 0: K is nseg segments of kseg, segment s read from A[s] / B[s]
   float aux_scale;
 };
 
@@ -105,6 +106,15 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
 
   float ra[NA][4], rb[NB][4];
   auto load_tiles = [&](int k0) {
+    const float* __restrict__ Aq = A;
+    const float* __restrict__ Bq = Bm;
+    int koff = 0;
+    if (D.kseg > 0) {  // a BK tile never straddles two segments (kseg % BK == 0)
+      const int sg = k0 / D.kseg;
+      Aq = P.A[sg];
+      Bq = P.B[sg];
+      koff = sg * D.kseg;
+    }
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int q = t + 256 * i;
@@ -112,23 +122,23 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
         const int row = q / CPR, kc = (q % CPR) * 4;
         const int gm = m0 + row, gk = k0 + kc;
         if (D.vecA && gm < M && gk + 3 < kend) {
-          const float4 v = *reinterpret_cast<const float4*>(A + (size_t)gm * D.lda + gk);
+          const float4 v = *reinterpret_cast<const float4*>(Aq + (size_t)gm * D.lda + (gk - koff));
           ra[i][0] = v.x; ra[i][1] = v.y; ra[i][2] = v.z; ra[i][3] = v.w;
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            ra[i][j] = (gm < M && gk + j < kend) ? A[(size_t)gm * D.lda + gk + j] : 0.0f;
+            ra[i][j] = (gm < M && gk + j < kend) ? Aq[(size_t)gm * D.lda + (gk - koff) + j] : 0.0f;
         }
       } else {
         const int k = q / (BM / 4), mc = (q % (BM / 4)) * 4;
         const int gk = k0 + k, gm = m0 + mc;
         if (D.vecA && gk < kend && gm + 3 < M) {
-          const float4 v = *reinterpret_cast<const float4*>(A + (size_t)gk * D.lda + gm);
+          const float4 v = *reinterpret_cast<const float4*>(Aq + (size_t)(gk - koff) * D.lda + gm);
           ra[i][0] = v.x; ra[i][1] = v.y; ra[i][2] = v.z; ra[i][3] = v.w;
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            ra[i][j] = (gk < kend && gm + j < M) ? A[(size_t)gk * D.lda + gm + j] : 0.0f;
+            ra[i][j] = (gk < kend && gm + j < M) ? Aq[(size_t)(gk - koff) * D.lda + gm + j] : 0.0f;
         }
       }
     }
@@ -139,23 +149,23 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
         const int k = q / (BN / 4), nc = (q % (BN / 4)) * 4;
         const int gk = k0 + k, gn = n0 + nc;
         if (D.vecB && gk < kend && gn + 3 < N) {
-          const float4 v = *reinterpret_cast<const float4*>(Bm + (size_t)gk * D.ldb + gn);
+          const float4 v = *reinterpret_cast<const float4*>(Bq + (size_t)(gk - koff) * D.ldb + gn);
           rb[i][0] = v.x; rb[i][1] = v.y; rb[i][2] = v.z; rb[i][3] = v.w;
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            rb[i][j] = (gk < kend && gn + j < N) ? Bm[(size_t)gk * D.ldb + gn + j] : 0.0f;
+            rb[i][j] = (gk < kend && gn + j < N) ? Bq[(size_t)(gk - koff) * D.ldb + gn + j] : 0.0f;
         }
       } else {
         const int n = q / CPR, kc = (q % CPR) * 4;
         const int gn = n0 + n, gk = k0 + kc;
         if (D.vecB && gn < N && gk + 3 < kend) {
-          const float4 v = *reinterpret_cast<const float4*>(Bm + (size_t)gn * D.ldb + gk);
+          const float4 v = *reinterpret_cast<const float4*>(Bq + (size_t)gn * D.ldb + (gk - koff));
           rb[i][0] = v.x; rb[i][1] = v.y; rb[i][2] = v.z; rb[i][3] = v.w;
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            rb[i][j] = (gn < N && gk + j < kend) ? Bm[(size_t)gn * D.ldb + gk + j] : 0.0f;
+            rb[i][j] = (gn < N && gk + j < kend) ? Bq[(size_t)gn * D.ldb + (gk - koff) + j] : 0.0f;
         }
       }
     }
@@ -353,6 +363,7 @@ extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const
   D.vecB = vb && (ldb % 4 == 0);
   D.splitk = splitk;
   D.kchunk = 0;
+  D.kseg = 0;
   hipStream_t s = mog_stream(stream);
   // 128x128 tiles once both output dims fill them and the grid still covers
   // the chip (>= 512 workgroups); 64x64 otherwise.
@@ -363,5 +374,41 @@ extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const
     launch_tile<128, 128>(transA, transB, epi, s, P, D, batch);
   else
     launch_tile<64, 64>(transA, transB, epi, s, P, D, batch);
+  MOG_LAUNCH_RET();
+}
+
+// C = epi( sum_s A_s op(B_s) ) as ONE k-ordered chain over the concatenated
+// K = nseg * kseg (segment s read from A[s] / B[s]): e.g. the hidden-state
+// gradient of the five heads, dh = sum_z dhid_z W1_z^T (air_model.py:462-499
+// backward), without atomics.
+extern "C" int mog_gemm_f32_kseg(int nseg, const float* const* A, const float* const* B,
+                                 float* C, const float* bias, const float* Cin, int M, int N,
+                                 int kseg, int lda, int ldb, int ldc, int transA, int transB,
+                                 int epi, void* stream) {
+  MOG_CHECK_ARG(nseg >= 1 && nseg <= MAXB && kseg > 0 && kseg % BK == 0);
+  MOG_CHECK_ARG(M >= 0 && N >= 0 && A && B && C);
+  MOG_CHECK_ARG(epi == EPI_STORE || epi == EPI_ATOMIC);
+  if (M == 0 || N == 0) return 0;
+  GemmPtrs P = {};
+  bool va = true, vb = true;
+  for (int i = 0; i < nseg; ++i) {
+    MOG_CHECK_ARG(A[i] && B[i]);
+    P.A[i] = A[i];
+    P.B[i] = B[i];
+    va = va && aligned16(A[i]);
+    vb = vb && aligned16(B[i]);
+  }
+  P.C[0] = C;
+  P.bias[0] = bias;
+  P.Cin[0] = Cin;
+  GemmDims D;
+  D.M = M; D.N = N; D.K = nseg * kseg; D.lda = lda; D.ldb = ldb; D.ldc = ldc; D.ldaux = 0;
+  D.aux_scale = 0.0f;
+  D.vecA = va && (lda % 4 == 0);
+  D.vecB = vb && (ldb % 4 == 0);
+  D.splitk = 1;
+  D.kchunk = 0;
+  D.kseg = kseg;
+  launch_tile<64, 64>(transA, transB, epi, mog_stream(stream), P, D, 1);
   MOG_LAUNCH_RET();
 }

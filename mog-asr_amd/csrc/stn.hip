@@ -25,6 +25,11 @@
 // order-dependent rounding residue there.  dot = sum_p G w still includes the
 // singly-degenerate residue samples, so it is the exact adjoint of the forward
 // value.  dU replaces TF's UnsortedSegmentSum (transformer.py:96-116).
+#include <stdio.h>
+
+#include <algorithm>
+#include <vector>
+
 #include "stn_geom.h"
 
 namespace {
@@ -87,48 +92,34 @@ __global__ __launch_bounds__(256) void stn_fwd_kernel(const float* __restrict__ 
 // Backward, one wave per image (no workgroup barriers): lanes walk output
 // columns (the column geometry stays in registers), the wave walks output
 // rows with the cotangent rows prefetched one batch ahead.  The source image
-// is staged in the wave's LDS slice; dU accumulates there with LDS atomics
-// (one wave owns an image, so the accumulation order is fixed).
+// is staged in the wave's LDS slice.  For axis-aligned transforms (AIR's) the
+// scaled cotangent g is kept as an LDS tile and dU is contracted separably,
+// T = g Wx then dU = Wy^T T, each sum over the contiguous range of canvas
+// columns / rows whose corner pair touches the source column / row (found
+// with wave ballots) — no atomics (LDS float atomics cost ~40 LDS cycles per
+// wave-instruction).  Other transforms accumulate dU with LDS atomics (one
+// wave owns an image, so the order is fixed).
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(256) void stn_bwd_kernel(
-    const float* __restrict__ U, int N, int Hin, int Win, const float* __restrict__ theta,
-    int Hout, int Wout, const float* __restrict__ G, const float* __restrict__ gscale, float* dU,
-    float* dtheta, float* dot) {
+// The per-pixel loop of stn_bwd_kernel, specialised so the hot body has no
+// branches: SEP (axis-aligned: geometry from the tables), DU (0 none,
+// 1 separable g tile, 2 LDS atomics).
+template <bool SEP, int DU>
+__device__ __forceinline__ void bwd_pixels(const float* th, int Hin, int Win, int Hout, int Wout,
+                                           const float* __restrict__ Gn, float sc, bool grads,
+                                           bool want_dot, const float* sU, float* sD, float* sg,
+                                           float4* coltab, const float4* rowtab, float* a) {
 #pragma clang fp contract(off)
-  extern __shared__ float smem[];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int n = blockIdx.x * (blockDim.x >> 6) + wv;
-  if (n >= N) return;  // no workgroup barriers below
-  const int HWin = Hin * Win, P = Hout * Wout;
-  const bool want_dU = dU != nullptr;
-  const int slice = (HWin * (want_dU ? 2 : 1) + 3) & ~3;
-  float* sU = smem + wv * slice;
-  float* sD = sU + HWin;
-  float th[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) th[k] = theta[n * 6 + k];
-  const bool sep = stn_separable(th) && Hin < 32768 && Win < 32768;
-  const float* Un = U + (size_t)n * HWin;
-  if ((HWin & 3) == 0) {
-    const floatx4* src = reinterpret_cast<const floatx4*>(Un);
-    for (int q = lane; q < HWin / 4; q += 64) reinterpret_cast<floatx4*>(sU)[q] = src[q];
-  } else {
-    for (int i = lane; i < HWin; i += 64) sU[i] = Un[i];
-  }
-  if (want_dU)
-    for (int i = lane; i < HWin; i += 64) sD[i] = 0.0f;
-  wave_sync();
-  const float sc = gscale ? gscale[n] : 1.0f;
+  const int lane = threadIdx.x & 63;
   const float wm2 = ((float)Win - 1.001f) / 2.0f;
   const float hm2 = ((float)Hin - 1.001f) / 2.0f;
-  const bool grads = sc != 0.0f && (want_dU || dtheta != nullptr);
-  float a[7] = {0, 0, 0, 0, 0, 0, 0};
-  const float* Gn = G + (size_t)n * P;
+  const float ystep = Hout > 1 ? 2.0f / (float)(Hout - 1) : 0.0f;
+  // lane i holds the geometry of output row i (SEP: Hout <= 64)
+  const float4 ry = SEP ? rowtab[min(lane, Hout - 1)] : make_float4(0.f, 0.f, 0.f, 0.f);
   // Wout <= 32: two output rows per pass (lane halves), else one
   const int cw = Wout <= 32 ? 32 : 64, rp = 64 / cw;
   const int sub = lane / cw, jl = lane - sub * cw;
@@ -137,7 +128,9 @@ __global__ __launch_bounds__(256) void stn_bwd_kernel(
     const bool jv = j < Wout;
     const int jc = jv ? j : Wout - 1;
     const float xt = mog_linspace(jc, Wout);
+    float sdx = 0.0f, sdy = 0.0f;
     const float4 ex_sep = axis4(axis_col(th, Hin, Win, Hout, Wout, jc), 1);
+    if (DU == 1 && jv) coltab[j] = ex_sep;
     // Cotangent rows are loaded unpredicated from clamped (always valid)
     // addresses, so the waitcnt pass can count the one-batch prefetch exactly
     // (a predicated load makes it wait for everything outstanding).
@@ -151,15 +144,36 @@ __global__ __launch_bounds__(256) void stn_bwd_kernel(
 #pragma unroll
       for (int u = 0; u < BR; ++u)  // prefetch the next batch
         gn[u] = Gn[min(i0 + rp * BR + sub + rp * u, Hout - 1) * Wout + jc];
+      // Branch-free row bodies (masks instead of `continue`): the four rows'
+      // LDS gathers can be in flight together.  Every gather index is a
+      // valid clipped corner, so unmasked loads are safe.
 #pragma unroll
       for (int u = 0; u < BR; ++u) {
         const int i = i0 + sub + rp * u;
-        if (!jv || i >= Hout) continue;
-        const float yt = mog_linspace(i, Hout);
+        const bool valid = jv && i < Hout;
+        const int ic = min(i, Hout - 1);
+        const float yt = Hout == 1 ? -1.0f
+                         : (ic == Hout - 1 ? 1.0f : -1.0f + ystep * (float)ic);  // = mog_linspace
         float4 ex, ey;
-        if (sep) {
+        if (SEP) {
           ex = ex_sep;
-          ey = axis4(axis_row(th, Hin, Win, Hout, Wout, i), Win);
+          // row geometry from the lane that owns the row (scalar broadcast, no LDS)
+          const int ia = min(i0 + rp * u, Hout - 1), ib = min(i0 + 1 + rp * u, Hout - 1);
+          const float4 ea = make_float4(
+              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.x), ia)),
+              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.y), ia)),
+              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.z), ia)),
+              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.w), ia)));
+          if (rp == 1) {
+            ey = ea;
+          } else {
+            const float4 eb = make_float4(
+                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.x), ib)),
+                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.y), ib)),
+                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.z), ib)),
+                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.w), ib)));
+            ey = sub ? eb : ea;
+          }
         } else {
           const Tap t = stn_tap(th, Hin, Win, xt, yt);
           ex = make_float4(__int_as_float((int)t.x0f), __int_as_float((int)t.x1f), t.x1f - t.x,
@@ -169,14 +183,19 @@ __global__ __launch_bounds__(256) void stn_bwd_kernel(
         }
         const int x0 = __float_as_int(ex.x), x1 = __float_as_int(ex.y);
         const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
-        if (x0 == x1 && y0 == y1) continue;  // value and all gradients exactly 0
+        const bool dead = x0 == x1 && y0 == y1;
+        const bool degen = x0 == x1 || y0 == y1;
         const float Ia = sU[y0 + x0], Ib = sU[y1 + x0], Ic = sU[y0 + x1], Id = sU[y1 + x1];
         const float gout = gq[u];
-        if (dot != nullptr) a[6] += gout * sample4(ex, ey, Ia, Ib, Ic, Id);
-        const float g = gout * sc;
-        if (!grads || x0 == x1 || y0 == y1 || g == 0.0f) continue;
+        const float pv = gout * sample4(ex, ey, Ia, Ib, Ic, Id);
+        a[6] += (want_dot && valid && !dead) ? pv : 0.0f;
+        const float g0 = gout * sc;
+        const bool use = valid && grads && !degen && g0 != 0.0f;
+        const float g = use ? g0 : 0.0f;  // value and gradients exactly 0 where !use
         const float ax = ex.z, bx = ex.w, ay = ey.z, by = ey.w;
-        if (want_dU) {
+        if (DU == 1) {
+          if (valid) sg[ic * Wout + j] = g;
+        } else if (DU == 2 && use) {
           atomicAdd(&sD[y0 + x0], ax * ay * g);
           atomicAdd(&sD[y1 + x0], ax * by * g);
           atomicAdd(&sD[y0 + x1], bx * ay * g);
@@ -184,11 +203,83 @@ __global__ __launch_bounds__(256) void stn_bwd_kernel(
         }
         const float dx = g * (ay * (Ic - Ia) + by * (Id - Ib)) * wm2;
         const float dy = g * (ax * (Ib - Ia) + bx * (Id - Ic)) * hm2;
-        a[0] += dx * xt; a[1] += dx * yt; a[2] += dx;
-        a[3] += dy * xt; a[4] += dy * yt; a[5] += dy;
+        // the column coordinate xt is constant per lane: sum_rows dx, scaled once
+        sdx += dx; a[1] += dx * yt;
+        sdy += dy; a[4] += dy * yt;
       }
     }
+    a[0] += sdx * xt; a[2] += sdx;
+    a[3] += sdy * xt; a[5] += sdy;
   }
+}
+
+// floats of one wave's LDS slice (max over the atomic and separable layouts)
+__host__ __device__ inline int stn_bwd_slice(int Hin, int Win, int Hout, int Wout, bool dU) {
+  const int hw4 = (Hin * Win + 3) & ~3;
+  const int atomic_l = hw4 * (dU ? 2 : 1) + 4 * Hout;
+  const int sep_l = ((hw4 > ((Hout * Win + 3) & ~3)) ? hw4 : ((Hout * Win + 3) & ~3)) +
+                    ((Hout * Wout + 3) & ~3) + 4 * 64 + 4 * 64 + 2 * 64;
+  return dU && atomic_l < sep_l ? sep_l : atomic_l;
+}
+
+__global__ __launch_bounds__(256) void stn_bwd_kernel(
+    const float* __restrict__ U, int N, int Hin, int Win, const float* __restrict__ theta,
+    int Hout, int Wout, const float* __restrict__ G, const float* __restrict__ gscale, float* dU,
+    float* dtheta, float* dot, long long* ts) {
+#pragma clang fp contract(off)
+  extern __shared__ float smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = blockIdx.x * (blockDim.x >> 6) + wv;
+  if (n >= N) return;  // no workgroup barriers below
+#define TS(k) if (ts && lane == 0) ts[(size_t)n * 8 + (k)] = wall_clock64()
+  TS(0);
+  const int HWin = Hin * Win, P = Hout * Wout;
+  const bool want_dU = dU != nullptr;
+  float th[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) th[k] = theta[n * 6 + k];
+  const bool sep = stn_separable(th) && Hin < 32768 && Win < 32768 && Hout <= 64;
+  // separable dU (no atomics): axis-aligned, increasing maps, extents <= 64
+  const bool sdu = want_dU && sep && th[0] > 0.0f && th[4] > 0.0f && Hin <= 64 && Win <= 64 &&
+                   Hout <= (Win <= 32 ? 64 : 32) && Wout <= 64;
+  const int slice = stn_bwd_slice(Hin, Win, Hout, Wout, want_dU);
+  const int hw4 = (HWin + 3) & ~3;
+  float* sU = smem + wv * slice;
+  // atomic path: [U | dU | rows];  separable path: [U, then T | g | cols | rows | ranges]
+  float* sD = sU + hw4;
+  float* sT = sU;
+  float* sg = sU + max(hw4, (Hout * Win + 3) & ~3);
+  float4* coltab = reinterpret_cast<float4*>(sg + ((P + 3) & ~3));
+  float4* rowtab = sdu ? coltab + 64 : reinterpret_cast<float4*>(sU + hw4 * (want_dU ? 2 : 1));
+  int2* vrange = reinterpret_cast<int2*>(rowtab + 64);
+  const float* Un = U + (size_t)n * HWin;
+  if ((HWin & 3) == 0) {
+    const floatx4* src = reinterpret_cast<const floatx4*>(Un);
+    for (int q = lane; q < HWin / 4; q += 64) reinterpret_cast<floatx4*>(sU)[q] = src[q];
+  } else {
+    for (int i = lane; i < HWin; i += 64) sU[i] = Un[i];
+  }
+  if (want_dU && !sdu)
+    for (int i = lane; i < HWin; i += 64) sD[i] = 0.0f;
+  if (sep)  // row geometry once per image (lane i -> row i)
+    for (int i = lane; i < Hout; i += 64) rowtab[i] = axis4(axis_row(th, Hin, Win, Hout, Wout, i), Win);
+  wave_sync();
+  TS(1);
+  const float sc = gscale ? gscale[n] : 1.0f;
+  const bool grads = sc != 0.0f && (want_dU || dtheta != nullptr);
+  float a[7] = {0, 0, 0, 0, 0, 0, 0};
+  const float* Gn = G + (size_t)n * P;
+  const int mode = __builtin_amdgcn_readfirstlane((sep ? 1 : 0) | (sdu ? 2 : 0) | (want_dU ? 4 : 0));
+  if (mode == 3 || mode == 7)
+    bwd_pixels<true, 1>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, sD, sg, coltab, rowtab, a);
+  else if (mode == 5)
+    bwd_pixels<true, 2>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, sD, sg, coltab, rowtab, a);
+  else if (mode == 1)
+    bwd_pixels<true, 0>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, sD, sg, coltab, rowtab, a);
+  else if (mode & 4)
+    bwd_pixels<false, 2>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, sD, sg, coltab, rowtab, a);
+  else
+    bwd_pixels<false, 0>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, sD, sg, coltab, rowtab, a);
 #pragma unroll
   for (int k = 0; k < 7; ++k) a[k] = mog_wave_sum(a[k]);
   if (lane == 0) {
@@ -196,9 +287,78 @@ __global__ __launch_bounds__(256) void stn_bwd_kernel(
       for (int k = 0; k < 6; ++k) dtheta[n * 6 + k] = a[k];
     if (dot) dot[n] = a[6];
   }
+  TS(2);
   if (!want_dU) return;
   wave_sync();
   float* dUn = dU + (size_t)n * HWin;
+  if (sdu) {
+    // contiguous index ranges (the maps increase): canvas columns j whose
+    // corner pair touches source column u, canvas rows i touching source row v
+    // Degenerate (clipped, x0 == x1) columns carry g == 0: give them sentinel
+    // corners before (left clip) or after (right clip) every source column so
+    // no range includes them — otherwise the ranges of the edge columns 0 and
+    // W-1 would span every clipped canvas column.
+    int x0l = 1 << 30, x1l = 1 << 30, y0l = 1 << 30, y1l = 1 << 30;
+    if (lane < Wout) {
+      const float4 e = coltab[lane];
+      x0l = __float_as_int(e.x);
+      x1l = __float_as_int(e.y);
+      if (x0l == x1l) x0l = x1l = (x0l == 0) ? -1 : (1 << 30);
+    }
+    if (lane < Hout) {
+      const float4 e = rowtab[lane];
+      y0l = __float_as_int(e.x) / Win;
+      y1l = __float_as_int(e.y) / Win;
+      if (y0l == y1l) y0l = y1l = (y0l == 0) ? -1 : (1 << 30);
+    }
+    const int cwi = Win <= 32 ? 32 : 64, rpi = 64 / cwi;
+    const int ul = lane % cwi, half = lane / cwi;
+    int jlo = 0, jhi = -1;
+    for (int u = 0; u < Win; ++u) {
+      const int lo = __popcll(__ballot(x1l < u));
+      const int hi = __popcll(__ballot(x0l <= u)) - 1;
+      if (ul == u) { jlo = lo; jhi = hi; }
+    }
+    for (int v = 0; v < Hin; ++v) {
+      const int lo = __popcll(__ballot(y1l < v));
+      const int hi = __popcll(__ballot(y0l <= v)) - 1;
+      if (lane == 0) vrange[v] = make_int2(lo, hi);
+    }
+    // T[i][u] = sum_j g[i][j] * (x0(j) == u ? x1 - x : x - x0)   (U is dead: T reuses it)
+    // j outer, the lane's rows inner: the row reads are independent (ILP)
+    if (ul < Win) {
+      constexpr int RMAX = 32;  // rows per lane (ceil(Hout / rpi) <= 32, see sdu)
+      float acc[RMAX];
+#pragma unroll
+      for (int r = 0; r < RMAX; ++r) acc[r] = 0.0f;
+      const int nr = (Hout - half + rpi - 1) / rpi;
+      for (int j = jlo; j <= jhi; ++j) {
+        const float4 e = coltab[j];
+        const float w = __float_as_int(e.x) == ul ? e.z : e.w;
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r)  // unpredicated (clamped row): reads stay in flight
+          acc[r] += sg[min(half + rpi * r, Hout - 1) * Wout + j] * w;
+      }
+#pragma unroll
+      for (int r = 0; r < RMAX; ++r)
+        if (r < nr) sT[(half + rpi * r) * Win + ul] = acc[r];
+    }
+    wave_sync();
+    TS(3);
+    // dU[v][u] = sum_i T[i][u] * (y0(i) == v ? y1 - y : y - y0)
+    if (ul < Win)
+      for (int v = half; v < Hin; v += rpi) {
+        const int2 r = vrange[v];
+        float acc = 0.0f;
+        for (int i = r.x; i <= r.y; ++i) {
+          const float4 e = rowtab[i];
+          acc += sT[i * Win + ul] * (__float_as_int(e.x) == v * Win ? e.z : e.w);
+        }
+        dUn[v * Win + ul] = acc;
+      }
+    TS(4);
+    return;
+  }
   if ((HWin & 3) == 0) {
     for (int q = lane; q < HWin / 4; q += 64)
       reinterpret_cast<floatx4*>(dUn)[q] = reinterpret_cast<const floatx4*>(sD)[q];
@@ -232,12 +392,46 @@ extern "C" int mog_stn_backward(const float* U, int N, int Hin, int Win, const f
   MOG_CHECK_ARG(U && theta && G && N >= 0 && Hin > 0 && Win > 0 && Hout > 0 && Wout > 0);
   MOG_CHECK_ARG(Hin * Win <= 16384);
   if (N == 0) return 0;
-  const size_t slice = ((size_t)Hin * Win * (dU ? 2 : 1) + 3) & ~(size_t)3;
-  int wpb = 4;  // waves (images) per workgroup, within 64 KiB of LDS
-  while (wpb > 1 && slice * sizeof(float) * wpb > 64 * 1024) wpb >>= 1;
+  const size_t slice = (size_t)stn_bwd_slice(Hin, Win, Hout, Wout, dU != nullptr);
+  int wpb = 4;  // waves (images) per workgroup, within 80 KiB of LDS
+  while (wpb > 1 && slice * sizeof(float) * wpb > 80 * 1024) --wpb;
   MOG_CHECK_ARG(slice * sizeof(float) * wpb <= 160 * 1024);
+  // MOG_STN_TIMING=1 (profiling aid): per-wave phase durations to stderr
+  static long long* tbuf = nullptr;
+  static size_t tcap = 0;
+  long long* ts = nullptr;
+  if (getenv("MOG_STN_TIMING")) {
+    if (tcap < (size_t)N * 8) {
+      if (tbuf) (void)hipFree(tbuf);
+      tcap = (size_t)N * 8;
+      if (hipMalloc(&tbuf, tcap * sizeof(long long)) != hipSuccess) return MOG_ERR_INVALID;
+    }
+    (void)hipMemset(tbuf, 0, tcap * sizeof(long long));
+    ts = tbuf;
+  }
   stn_bwd_kernel<<<mog_cdiv(N, wpb), 64 * wpb, slice * sizeof(float) * wpb,
                    mog_stream(stream)>>>(U, N, Hin, Win, theta, Hout, Wout, G, gscale, dU, dtheta,
-                                         dot);
+                                         dot, ts);
+  if (ts) {
+    std::vector<long long> h((size_t)N * 8);
+    (void)hipStreamSynchronize(mog_stream(stream));
+    (void)hipMemcpy(h.data(), tbuf, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
+    double acc[4] = {0, 0, 0, 0};
+    int cnt[4] = {0, 0, 0, 0};
+    long long t0 = h[0], t1 = 0;
+    for (int b = 0; b < N; ++b) {
+      for (int k = 0; k < 4; ++k)
+        if (h[b * 8 + k + 1] && h[b * 8 + k]) {
+          acc[k] += (double)(h[b * 8 + k + 1] - h[b * 8 + k]);
+          ++cnt[k];
+        }
+      t0 = std::min(t0, h[b * 8]);
+      for (int k = 0; k < 5; ++k) t1 = std::max(t1, h[b * 8 + k]);
+    }
+    fprintf(stderr, "stn_bwd wave phases (us): stage %.2f main %.2f Tpass %.2f dUpass %.2f | span %.2f\n",
+            cnt[0] ? acc[0] / cnt[0] / 100 : 0.0, cnt[1] ? acc[1] / cnt[1] / 100 : 0.0,
+            cnt[2] ? acc[2] / cnt[2] / 100 : 0.0, cnt[3] ? acc[3] / cnt[3] / 100 : 0.0,
+            (t1 - t0) / 100.0);
+  }
   MOG_LAUNCH_RET();
 }

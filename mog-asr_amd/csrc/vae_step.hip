@@ -444,30 +444,42 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
   // part = active ? z * w : 0 for every pixel (write-only; mog_recon_loss sums
   // the parts in step order).  Lane = canvas column, waves walk (image, row).
   if (p.phases & 8) {
+    // wave w owns images w, w+8, ...: the lane's column geometry stays in
+    // registers, the row entries are LDS broadcasts, four rows per pass
     float* out = p.part + (size_t)b0 * C2;
-    for (int j0 = 0; j0 < C; j0 += 64) {
-      const int j = j0 + (tid & 63);
-      int m = 0, i = wv;
-      while (i >= C) { i -= C; ++m; }
-      for (; m < nb;) {
-        float v = 0.0f;
-        if (smask[m] && j < C) {
-          const float* U = sR + m * W2;
-          if (ssep[m] & 2) {
-            const float4 ex = tabW[m * 2 * C + j], ey = tabW[m * 2 * C + C + i];
-            if (!axis4_dead(ex, ey)) {
-              const int x0 = __float_as_int(ex.x), x1 = __float_as_int(ex.y);
+    constexpr int UW = 4;
+    for (int m = wv; m < nb; m += NW) {
+      float* om = out + (size_t)m * C2;
+      const float* U = sR + m * W2;
+      const bool act = smask[m] != 0, tab = (ssep[m] & 2) != 0;
+      const float zn = szv[m];
+      for (int j0 = 0; j0 < C; j0 += 64) {
+        const int j = j0 + (tid & 63);
+        const bool jv = j < C;
+        const int jc = jv ? j : C - 1;
+        const float4 ex = tabW[m * 2 * C + jc];
+        const int x0 = __float_as_int(ex.x), x1 = __float_as_int(ex.y);
+        for (int i0 = 0; i0 < C; i0 += UW) {
+          float v[UW];
+#pragma unroll
+          for (int u = 0; u < UW; ++u) {
+            const int i = min(i0 + u, C - 1);
+            v[u] = 0.0f;
+            if (!act) continue;
+            if (tab) {
+              const float4 ey = tabW[m * 2 * C + C + i];
               const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
-              v = szv[m] * sample4(ex, ey, U[y0 + x0], U[y1 + x0], U[y0 + x1], U[y1 + x1]);
+              if (!(x0 == x1 && y0 == y1))
+                v[u] = zn * sample4(ex, ey, U[y0 + x0], U[y1 + x0], U[y0 + x1], U[y1 + x1]);
+            } else {
+              const Tap t = stn_tap(&sth[m][6], 28, 28, mog_linspace(jc, C), mog_linspace(i, C));
+              if (!t.dead) v[u] = zn * tap_value(t, U);
             }
-          } else {
-            const Tap t = stn_tap(&sth[m][6], 28, 28, mog_linspace(j, C), mog_linspace(i, C));
-            if (!t.dead) v = szv[m] * tap_value(t, U);
           }
+#pragma unroll
+          for (int u = 0; u < UW; ++u)
+            if (jv && i0 + u < C) om[(i0 + u) * C + j] = v[u];
         }
-        if (j < C) out[(size_t)m * C2 + i * C + j] = v;
-        i += NW;
-        while (i >= C) { i -= C; ++m; }
       }
     }
   }

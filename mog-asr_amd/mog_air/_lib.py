@@ -23,6 +23,7 @@ ULL = ctypes.c_ulonglong
 # argtypes per entry point (mirrors include/mog_air.h)
 _SIGS = {
     "mog_gemm_f32": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, I, P],
+    "mog_gemm_f32_kseg": [I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "mog_stn_forward": [P, I, I, I, P, I, I, P, P, P, I, P],
     "mog_stn_backward": [P, I, I, I, P, I, I, P, P, P, P, P, P],
     "mog_lstm_cell_forward": [P, P, P, P, P, I, I, P],
@@ -37,6 +38,7 @@ _SIGS = {
     "mog_sigmoid_backward": [P, P, P, L, I, P],
     "mog_gemm_bf16": [I, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, I, P],
     "mog_cvt_bf16": [P, I, I, I, P, I, I, I, I, P],
+    "mog_cvt_bf16_batch": [I, P, P, P, P],
     "mog_recon_loss": [P, P, P, I, L, P, P, P, I, I, F, P, P, P, P, P, P, P],
     "mog_batch_mean": [P, P, P, P, I, P, P],
     "mog_colsum_add": [P, I, I, I, P, P],

@@ -20,6 +20,7 @@ No host synchronisation happens inside a train step.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import Dict, Optional
 
@@ -134,6 +135,7 @@ class _Workspace:
         self.eps_scale, self.eps_shift = e(T, B), e(T, B, 2)
         self.eps_z, self.eps_x, self.u = e(T, B, Z), e(T, B, W2), e(T, B)
         self._bwd = False
+        self.materialized = False
 
     def alloc_backward(self, m: "AIRModel"):
         if self._bwd:
@@ -336,7 +338,7 @@ class AIRModel:
 
     # ----------------------------------------------------------- forward ---
     def _forward(self, X: torch.Tensor, targets: Optional[torch.Tensor], ws: _Workspace,
-                 need_grad: bool) -> None:
+                 need_grad: bool, outputs: bool = True) -> None:
         B, T, H = ws.B, self.max_steps, self.rnn_units
         C, W, C2, W2 = self.canvas_size, self.windows_size, self.C2, self.W2
         Z = self.vae_latent_dimensions
@@ -404,22 +406,37 @@ class AIRModel:
             # STN write + masked canvas accumulation (air_model.py:580-588, 665-675)
             ops.stn_forward(ws.r[t], ws.th_b[t], (C, C), out=ws.canvas, z=ws.zval[t],
                             mask=ws.zmask[t], accumulate=True)
-        self._forward_loss(X, targets, ws, need_grad)
+        self._forward_loss(X, targets, ws, need_grad, outputs)
 
-    def _forward_loss(self, X, targets, ws, need_grad):
-        """reconstruction loss (air_model.py:866-900) + batch means."""
+    def _forward_loss(self, X, targets, ws, need_grad, outputs=True):
+        """reconstruction loss (air_model.py:866-900) + batch means.  With
+        outputs=False (train steps) the clipped reconstruction and, in the
+        fused configuration, the summed canvas are not stored; the
+        ``reconstruction`` / ``canvas`` accessors materialize them on demand."""
         B, C2, s = ws.B, self.C2, stream_ptr()
-        gscale = 1.0 / (B * self.grad_world)
         parts = ws.cparts
-        _lib.call("mog_recon_loss", dp(X), dp(ws.canvas), dp(parts),
+        self._loss_inputs = (X, targets)
+        ws.materialized = bool(outputs)
+        gscale = 1.0 / (B * self.grad_world)
+        canvas_ptr = dp(ws.canvas) if (outputs or parts is None) else None
+        _lib.call("mog_recon_loss", dp(X), canvas_ptr, dp(parts),
                   self.max_steps if parts is not None else 0, B * C2, dp(ws.runloss),
-                  dp(ws.digits), dp(targets), B, C2, float(gscale), dp(ws.recon), dp(ws.bce),
-                  dp(ws.mse),
+                  dp(ws.digits), dp(targets), B, C2, float(gscale),
+                  dp(ws.recon) if outputs else None, dp(ws.bce), dp(ws.mse),
                   dp(ws.loss_b), dp(ws.acc_b) if targets is not None else None,
                   dp(ws.dcanvas) if need_grad else None, s)
         _lib.call("mog_batch_mean", dp(ws.loss_b), dp(ws.acc_b) if targets is not None else None,
                   dp(ws.mse), None, B, dp(ws.means), s)
         self._outputs_ready = True
+
+    def _materialize(self):
+        """Store the canvas / reconstruction of the last forward (recomputes
+        the loss kernel once with its output pointers; same values)."""
+        ws = self._ws
+        if ws is None or ws.materialized:
+            return
+        X, targets = self._loss_inputs
+        self._forward_loss(X, targets, ws, need_grad=False, outputs=True)
 
     # ---------------------------------------------------------- backward ---
     def _backward(self, X: torch.Tensor, ws: _Workspace) -> None:
@@ -466,7 +483,10 @@ class AIRModel:
                       dp(ws.dth_f), dp(ws.dth_b), dp(ws.dot),
                       _lib.ptr_array([dp(x) for x in hid_t]), w2a, dp(ws.dout[0, t]),
                       T * B * 2, dp(ws.dhid[0, t]), T * B * HS, s)
-            gemm(dhid_t, w1, [ws.dh[t]] * 5, B, H, HS, HS, HS, H, transB=True, epi=EPI_ATOMIC)
+            # dh[t] += sum_z dhid_z W1_z^T: one chain over K = 5 * HS (no atomics)
+            _lib.call("mog_gemm_f32_kseg", 5, _lib.ptr_array([dp(x) for x in dhid_t]),
+                      _lib.ptr_array([dp(x) for x in w1]), dp(ws.dh[t]), None, dp(ws.dh[t]),
+                      B, H, HS, HS, HS, H, 0, 1, 0, s)
             dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
             _lib.call("mog_lstm_cell_backward", dp(ws.Gx if t == 0 else ws.G[t]),
                       dp(bK) if t == 0 else None, dp(ws.c[t - 1]) if t > 0 else None,
@@ -553,10 +573,19 @@ class AIRModel:
                 bf = dict(device=self.device, dtype=torch.bfloat16)
                 self._wt[n] = torch.zeros((O, self._pad8(I)), **bf)
                 self._wn[n] = torch.zeros((I, self._pad8(O)), **bf)
-        for n in self._VAE:
-            w = self._P("vae/" + n + "/weights")
-            ops.cvt_bf16(w, self._wt[n], transpose=True)
-            ops.cvt_bf16(w, self._wn[n], transpose=False)
+        if not hasattr(self, "_pack_args"):  # one batched launch for all 14 packs
+            srcs, dsts, dims = [], [], []
+            for n in self._VAE:
+                w = self._P("vae/" + n + "/weights")
+                I, O = w.shape
+                wt, wn = self._wt[n], self._wn[n]
+                srcs += [dp(w), dp(w)]
+                dsts += [dp(wt), dp(wn)]
+                dims += [I, O, O, wt.shape[0], wt.shape[1], wt.shape[1], 1,
+                         I, O, O, wn.shape[0], wn.shape[1], wn.shape[1], 0]
+            self._pack_args = (len(srcs), _lib.ptr_array(srcs), _lib.ptr_array(dsts),
+                               (ctypes.c_int * len(dims))(*dims))
+        _lib.call("mog_cvt_bf16_batch", *self._pack_args, stream_ptr())
         self._pack_version = self.params.version
 
     def _vae_forward_bf16(self, X, ws, t, lik_std):
@@ -720,7 +749,7 @@ class AIRModel:
         ws = self._workspace(X.shape[0])
         ws.alloc_backward(self)
         self._fill_noise(ws, noise)
-        self._forward(X, tg, ws, need_grad=True)
+        self._forward(X, tg, ws, need_grad=True, outputs=False)
         self._backward(X, ws)
         if self.grad_hook is not None:
             self.grad_hook(self.params.grad)
@@ -835,6 +864,7 @@ class AIRModel:
 
     @property
     def reconstruction(self):
+        self._materialize()
         return self._ws.recon
 
     @property
@@ -843,6 +873,7 @@ class AIRModel:
 
     @property
     def canvas(self):
+        self._materialize()
         return self._ws.canvas
 
     @property

@@ -25,6 +25,7 @@ def timeit(fn, iters=10):
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+    only_wbwd = len(sys.argv) > 2 and sys.argv[2] == "wbwd"
     dev = "cuda:0"
     rng = np.random.default_rng(0)
     s = rng.uniform(0.3, 0.7, B)
@@ -45,9 +46,13 @@ def main():
         dot = torch.empty(B, device=dev)
         os.environ["MOG_STN_TIMING"] = "1"
         ops.stn_backward(r, thb, (50, 50), G, gscale=zs, dU=dU, dtheta=dth, dot=dot, want_dot=True)
+        ops.stn_backward(x, thf, (28, 28), g28, want_dU=False, dtheta=dth)
         del os.environ["MOG_STN_TIMING"]
         tw = timeit(lambda: ops.stn_backward(r, thb, (50, 50), G, gscale=zs, dU=dU, dtheta=dth,
                                              dot=dot, want_dot=True))
+        if only_wbwd:
+            print(f"sep={sep}: write-bwd {tw:7.1f} us", flush=True)
+            continue
         tr = timeit(lambda: ops.stn_backward(x, thf, (28, 28), g28, want_dU=False, dtheta=dth))
         out = torch.empty(B, 784, device=dev)
         cv = torch.zeros(B, 2500, device=dev)

@@ -42,6 +42,27 @@ def test_gemm_bit_exact_chain(M, N, K):
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
 
 
+def test_gemm_kseg_is_one_chain():
+    """mog_gemm_f32_kseg: five K-segments (the heads' dh = sum_z dhid_z W1_z^T
+    form) equal ONE k-ordered chain over the concatenated K, bit for bit."""
+    from mog_air import _lib
+    rng = np.random.default_rng(11)
+    M, N, ks, S = 300, 256, 64, 5
+    A = [rng.standard_normal((M, ks)).astype(np.float32) for _ in range(S)]
+    W = [rng.standard_normal((N, ks)).astype(np.float32) for _ in range(S)]  # [N][K] (transB)
+    Acat = np.concatenate(A, 1)
+    Wcat = np.concatenate(W, 1)
+    ref = ao.dense_chain(Acat, np.ascontiguousarray(Wcat.T), np.zeros(N, np.float32))
+    dA = [_cuda(a) for a in A]
+    dW = [_cuda(w) for w in W]
+    out = torch.empty((M, N), device=DEV)
+    _lib.call("mog_gemm_f32_kseg", S, _lib.ptr_array([a.data_ptr() for a in dA]),
+              _lib.ptr_array([w.data_ptr() for w in dW]), out.data_ptr(), None, None,
+              M, N, ks, ks, ks, N, 0, 1, 0, None)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("ta,tb", [(False, True), (True, False), (True, True)])
 def test_gemm_transposes(ta, tb):
     from mog_air import ops
