@@ -110,9 +110,13 @@ int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, float v_plv, co
  * softplus, r = sigmoid(512->784 + std*eps_x)), the VAE KL into runloss under
  * `mask` (air_model.py:718-736), and this step's canvas contribution
  * canvas_part = mask ? zval * STN(r, theta_b) : 0 for every pixel
- * (air_model.py:580-588, 665-675; summed in step order by mog_recon_loss).  wt[7] are the bf16 W^T packs [out][in8] in
- * the order recognition_1, recognition_2, rec_mean, rec_log_variance,
- * generative_1, generative_2, gen_mean; bias[7] fp32 likewise.  Saved for the
+ * (air_model.py:580-588, 665-675; summed in step order by mog_recon_loss).
+ * wt[7] are the bf16 W^T packs in B-fragment order (mog_cvt_bf16_batch
+ * transpose 2) in the order recognition_1, recognition_2, rec_mean, rec_log_variance,
+ * generative_1, generative_2, gen_mean; bias[7] fp32 likewise.  eps_x: read
+ * from `eps_x` [B,784] when eps_gen == 0; otherwise generated in-kernel as the
+ * Philox normals mog_rng_fill(eps_x, B*784, eps_seed, eps_offset, 1) would
+ * have written (bit-identical; eps_x may then be NULL).  Saved for the
  * backward: gb/a1b/a2b/zb/d1b/d2b (bf16, zb row stride 56), mu/lv/z/r (fp32).
  * Shapes must be the reference defaults (W 28, 512/256, Z 50, 256/512):
  * anything else returns MOG_ERR_INVALID.  Replaces the per-step sequence
@@ -120,7 +124,8 @@ int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, float v_plv, co
 int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int Z, int G1, int G2,
                              const float* x, const float* theta_f, const float* theta_b,
                              const float* mask, const float* zval, const float* eps_z,
-                             const float* eps_x, const void* const* wt,
+                             const float* eps_x, int eps_gen, unsigned long long eps_seed,
+                             unsigned long long eps_offset, const void* const* wt,
                              const float* const* bias, float lik_std, float v_pm, float v_pv,
                              float v_plv, float* canvas_part, float* runloss, float* vkl, void* gb,
                              void* a1b, void* a2b, float* mu, float* lv, float* z, void* zb,
@@ -154,7 +159,11 @@ int mog_gemm_bf16(int batch, const void* const* A, const void* const* B, void* c
 int mog_cvt_bf16(const float* src, int src_rows, int src_cols, int ld_src, void* dst, int rows,
                  int cols, int ld_dst, int transpose, void* stream);
 /* Up to 16 of the above in one launch; dims[7*j ..] = src_rows, src_cols,
- * ld_src, rows, cols, ld_dst, transpose of job j. */
+ * ld_src, rows, cols, ld_dst, transpose of job j.  transpose == 2 packs W^T
+ * (W = src [src_rows = in][src_cols = out]) in MFMA B-fragment order for
+ * mog_stn_vae_step_forward: rows = out padded to 16, cols = in padded to 32,
+ * element ((ct*(cols/32) + ks)*64 + lane)*8 + q = W[ks*32 + 8*(lane/16) + q]
+ * [ct*16 + lane%16], zero outside the source (ld_dst unused). */
 int mog_cvt_bf16_batch(int njobs, const float* const* src, void* const* dst, const int* dims,
                        void* stream);
 

@@ -389,6 +389,19 @@ __global__ __launch_bounds__(256) void cvt_bf16_batch_kernel(CvtBatch b) {
   while (i >= b.start[j + 1]) ++j;
   const int* d = b.d[j];
   const long e = i - b.start[j];
+  if (d[6] == 2) {
+    // MFMA B-fragment order of W^T (vae_step.hip): element e = ((ct * KS + ks)
+    // * 64 + lane) * 8 + q holds W^T[ct*16 + lane%16][ks*32 + 8*(lane/16) + q],
+    // so one 16-B-per-lane wave load is 1 KiB contiguous
+    const int q = (int)(e & 7), l = (int)((e >> 3) & 63);
+    const long f = e >> 9;                       // ct * KS + ks
+    const int KS = d[4] / 32;
+    const int ct = (int)(f / KS), ks = (int)(f - (long)ct * KS);
+    const int n = ct * 16 + (l & 15), k = ks * 32 + 8 * (l >> 4) + q;
+    const float v = (k < d[0] && n < d[1]) ? b.src[j][(size_t)k * d[2] + n] : 0.0f;
+    b.dst[j][e] = (__bf16)v;
+    return;
+  }
   const int r = e / d[4], c = e - (long)r * d[4];
   const int sr = d[6] ? c : r, sc = d[6] ? r : c;
   const float v = (sr < d[0] && sc < d[1]) ? b.src[j][(size_t)sr * d[2] + sc] : 0.0f;

@@ -5,8 +5,9 @@
 //
 // One workgroup = 8 waves = MB (32) images.  Activations stay in LDS between
 // the six dense layers (bf16, rows padded against bank conflicts); the packed
-// bf16 weights (W^T, [out][in8]) stream from L2 straight into the MFMA B
-// operand (16 B per lane, four k-steps of register prefetch); the A operand is
+// bf16 weights (W^T in MFMA B-fragment order: one 1-KiB contiguous load per
+// fragment) stream from L2 straight into the MFMA B operand (four k-steps of
+// register prefetch); the A operand is
 // read from LDS with ds_read_b128.  Activations the backward needs (glimpse,
 // softplus outputs, mu/logvar/z, r) are flushed to HBM with 16-byte stores.
 // The STN write samples r from LDS (fp32) and stores this step's canvas
@@ -22,6 +23,7 @@
 #include <algorithm>
 #include <vector>
 
+#include "philox.h"
 #include "stn_geom.h"
 
 namespace {
@@ -59,9 +61,11 @@ struct StepArgs {
   const float* mask;         // [B] active (new stopping sum < thr)
   const float* zval;         // [B] z_pres
   const float* eps_z;        // [B, Z]
-  const float* eps_x;        // [B, 784]
-  const __bf16* wt[7];       // packed W^T: r1 [512][784], r2 [256][512], mu [50][256],
-                             //             lv [50][256], g1 [256][56], g2 [512][256], go [784][512]
+  const float* eps_x;        // [B, 784] (read when eps_gen == 0)
+  unsigned long long eps_seed, eps_offset;  // eps_gen: Philox quad (eps_offset + b*196 + k/4)
+  int eps_gen;
+  const __bf16* wt[7];       // W^T in B-fragment order: r1 [512][800], r2 [256][512],
+                             // mu, lv [64][256], g1 [256][64], g2 [512][256], go [784][512]
   const float* bias[7];
   float* part;               // [B, C*C] this step's canvas contribution (written)
   float* runloss;            // [B]
@@ -100,32 +104,32 @@ __device__ __forceinline__ void build_tables(float4* tab, int stride, const floa
   }
 }
 
-// Column tiles tile_base + w + nw*c (c < TPW) of one dense layer over the MB
-// rows held in LDS, for waves wbase .. wbase+nw-1: epi(row, col, acc, aux).
-// A: LDS [MB][lda] bf16, zero-padded to K; W: global [N][ldw] bf16 whose
-// first KW columns are valid.  B fragments stream from L2 straight into the
-// MFMA with a four-k-step register prefetch ring (rolled, branch-free body so
-// the compiler keeps the distance; the ragged tail is peeled at compile
-// time).  Rows past N are clamped to a valid row and k past KW to the row's
-// last 8-element chunk: those values meet only discarded output columns or
-// zero A padding, and every load stays inside the weight pack.  With AUX the
+// Column tiles tile_base + (w + nw*c + rot) % (nw*TPW) of one dense layer
+// over the MB rows held in LDS, for waves wbase .. wbase+nw-1:
+// epi(row, col, acc, aux).  A: LDS [MB][lda] bf16, zero-padded to K.  W: the
+// layer's W^T in B-fragment order (mog_cvt_bf16_batch transpose 2; N padded
+// to 16, K to 32, zeros outside), so each B fragment is one 1-KiB contiguous
+// wave load streamed from L2 straight into the MFMA, with a four-k-step
+// register prefetch ring (rolled, branch-free body so the compiler keeps the
+// distance; the ragged tail is peeled at compile time).  With AUX the
 // epilogue operand aux[row][col] is loaded before the k loop.
-template <int N, int K, int KW, int TPW, bool AUX, class Epi>
+template <int N, int K, int TPW, bool AUX, class Epi>
 __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf16* __restrict__ W,
-                                            int ldw, int tile_base, int wbase, int nw,
+                                            int tile_base, int wbase, int nw,
                                             const float* __restrict__ aux, int ldaux, int nb,
                                             Epi epi) {
   constexpr int KS = K / 32;
-  static_assert(K % 32 == 0 && KW % 8 == 0 && KW <= K, "K padding");
+  static_assert(K % 32 == 0, "K padding");
+  const int rot = (int)(blockIdx.x >> 3);  // spread the CUs of one XCD over the weight columns
   const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) - wbase;
   if (w < 0 || w >= nw) return;
   const int li = lane & 15, g = lane >> 4;
   int ct[TPW];
-  const __bf16* wrow[TPW];
+  const bf16x8* wf[TPW];
 #pragma unroll
   for (int c = 0; c < TPW; ++c) {
-    ct[c] = tile_base + w + nw * c;
-    wrow[c] = W + (size_t)min(ct[c] * 16 + li, N - 1) * ldw;
+    ct[c] = tile_base + (w + nw * c + rot) % (nw * TPW);
+    wf[c] = reinterpret_cast<const bf16x8*>(W) + (size_t)ct[c] * KS * 64 + lane;
   }
   float av[2][TPW][4];
   if constexpr (AUX) {
@@ -144,11 +148,9 @@ __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf
   for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
     for (int c = 0; c < TPW; ++c) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int kmax = KW - 8;
   auto loadB = [&](int ks, bf16x8* b) {
-    const int k = min(ks * 32 + 8 * g, kmax);
 #pragma unroll
-    for (int c = 0; c < TPW; ++c) b[c] = *reinterpret_cast<const bf16x8*>(wrow[c] + k);
+    for (int c = 0; c < TPW; ++c) b[c] = wf[c][ks * 64];
   };
   auto step = [&](int ks, const bf16x8* b) {
     const int k = ks * 32 + 8 * g;
@@ -331,7 +333,7 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
   // ---- 2. a1 = softplus(g W1 + b1)  [MB x 512] -> H -----------------------
   if (p.phases & 2) {
     const float* bias = p.bias[0];
-    dense_tiles<512, KG, W2, 4, false>(sG, SG, p.wt[0], W2, 0, 0, NW, nullptr, 0, nb,
+    dense_tiles<512, KG, 4, false>(sG, SG, p.wt[0], 0, 0, NW, nullptr, 0, nb,
                                        [&](int m, int n, float v, float) {
       sH[m * S512 + n] = (__bf16)softplus_fast(v + bias[n]);
     });
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
   // ---- 3. a2 = softplus(a1 W2 + b2)  [MB x 256] -> A ----------------------
   if (p.phases & 2) {
     const float* bias = p.bias[1];
-    dense_tiles<256, 512, 512, 2, false>(sH, S512, p.wt[1], 512, 0, 0, NW, nullptr, 0, nb,
+    dense_tiles<256, 512, 2, false>(sH, S512, p.wt[1], 0, 0, NW, nullptr, 0, nb,
                                          [&](int m, int n, float v, float) {
       sA2[m * S256 + n] = (__bf16)softplus_fast(v + bias[n]);
     });
@@ -353,12 +355,12 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
   // ---- 4. mu | lv = a2 W + b  [MB x 50] fp32 (waves 0-3 | 4-7) ------------
   if (p.phases & 2) {
     const float* bm = p.bias[2];
-    dense_tiles<50, 256, 256, 1, false>(sA2, S256, p.wt[2], 256, 0, 0, 4, nullptr, 0, nb,
+    dense_tiles<50, 256, 1, false>(sA2, S256, p.wt[2], 0, 0, 4, nullptr, 0, nb,
                                         [&](int m, int n, float v, float) {
       sMu[m * 50 + n] = v + bm[n];
     });
     const float* bl = p.bias[3];
-    dense_tiles<50, 256, 256, 1, false>(sA2, S256, p.wt[3], 256, 0, 4, 4, nullptr, 0, nb,
+    dense_tiles<50, 256, 1, false>(sA2, S256, p.wt[3], 0, 4, 4, nullptr, 0, nb,
                                         [&](int m, int n, float v, float) {
       sLv[m * 50 + n] = v + bl[n];
     });
@@ -401,7 +403,7 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
   // ---- 6. d1 = softplus(z Wg1 + b)  [MB x 256] ----------------------------
   if (p.phases & 2) {
     const float* bias = p.bias[4];
-    dense_tiles<256, 64, 56, 2, false>(sZ, SZ, p.wt[4], 56, 0, 0, NW, nullptr, 0, nb,
+    dense_tiles<256, 64, 2, false>(sZ, SZ, p.wt[4], 0, 0, NW, nullptr, 0, nb,
                                        [&](int m, int n, float v, float) {
       sD1[m * S256 + n] = (__bf16)softplus_fast(v + bias[n]);
     });
@@ -412,7 +414,7 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
   // ---- 7. d2 = softplus(d1 Wg2 + b)  [MB x 512] -> H ----------------------
   if (p.phases & 2) {
     const float* bias = p.bias[5];
-    dense_tiles<512, 256, 256, 4, false>(sD1, S256, p.wt[5], 256, 0, 0, NW, nullptr, 0, nb,
+    dense_tiles<512, 256, 4, false>(sD1, S256, p.wt[5], 0, 0, NW, nullptr, 0, nb,
                                          [&](int m, int n, float v, float) {
       sH[m * S512 + n] = (__bf16)softplus_fast(v + bias[n]);
     });
@@ -421,18 +423,36 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
   STAMP(7);
   if (p.phases & 16) flush_rows(sH, S512, p.d2b + (size_t)b0 * 512, 512, 512, nb);
   // ---- 8. r = sigmoid(d2 Wgo + b + std eps)  [MB x 784] fp32 -> A ---------
-  // 49 column tiles: 32 (4 per wave) + 16 (2 per wave) + 1 (wave 0)
+  // eps_x is staged in the r tile first (generated in-kernel with the same
+  // Philox quads mog_rng_fill would write, or loaded with 16-byte reads); each
+  // epilogue lane reads its eps and overwrites it with r.  49 column tiles:
+  // 32 (4 per wave) + 16 (2 per wave) + 1 (wave 0).
   if (p.phases & 2) {
+    float4* sR4 = reinterpret_cast<float4*>(sR);
+    constexpr int QPR = W2 / 4;  // 196 quads per image
+    if (p.eps_gen) {
+      for (int i = tid; i < nb * QPR; i += NTHR) {
+        const int m = i / QPR, q = i - (i / QPR) * QPR;
+        float v[4];
+        mog_philox_quad(p.eps_seed, p.eps_offset + (unsigned long long)(b0 + m) * QPR + q, true,
+                        v);
+        sR4[i] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    } else {
+      const float4* ex4 = reinterpret_cast<const float4*>(p.eps_x + (size_t)b0 * W2);
+      for (int i = tid; i < nb * QPR; i += NTHR) sR4[i] = ex4[i];
+    }
+    __syncthreads();
     const float* bias = p.bias[6];
     const float sd = p.lik_std;
-    const float* ex = p.eps_x + (size_t)b0 * W2;
-    auto epi = [&](int m, int n, float v, float e) {
+    auto epi = [&](int m, int n, float v, float) {
+      const float e = sR[m * W2 + n];
       const float y = __builtin_fmaf(e, sd, v + bias[n]);
       sR[m * W2 + n] = 1.0f / (1.0f + __expf(-y));
     };
-    dense_tiles<784, 512, 512, 4, true>(sH, S512, p.wt[6], 512, 0, 0, NW, ex, W2, nb, epi);
-    dense_tiles<784, 512, 512, 2, true>(sH, S512, p.wt[6], 512, 32, 0, NW, ex, W2, nb, epi);
-    dense_tiles<784, 512, 512, 1, true>(sH, S512, p.wt[6], 512, 48, 0, 1, ex, W2, nb, epi);
+    dense_tiles<784, 512, 4, false>(sH, S512, p.wt[6], 0, 0, NW, nullptr, 0, nb, epi);
+    dense_tiles<784, 512, 2, false>(sH, S512, p.wt[6], 32, 0, NW, nullptr, 0, nb, epi);
+    dense_tiles<784, 512, 1, false>(sH, S512, p.wt[6], 48, 0, 1, nullptr, 0, nb, epi);
   }
   __syncthreads();
   STAMP(8);
@@ -442,44 +462,49 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
   STAMP(9);
   // ---- 9. STN write (air_model.py:580-588): this step's canvas part -------
   // part = active ? z * w : 0 for every pixel (write-only; mog_recon_loss sums
-  // the parts in step order).  Lane = canvas column, waves walk (image, row).
+  // the parts in step order).  One wave per image; each lane produces four
+  // consecutive canvas pixels (flat order) and stores them with one 16-byte
+  // store.  Dead samples (clipped corners coincide on both axes) are exactly
+  // +0 and are selected, not branched.
   if (p.phases & 8) {
-    // wave w owns images w, w+8, ...: the lane's column geometry stays in
-    // registers, the row entries are LDS broadcasts, four rows per pass
-    float* out = p.part + (size_t)b0 * C2;
-    constexpr int UW = 4;
+    const int lane = tid & 63;
+    const bool vec = (C2 & 3) == 0;  // even C: 16-byte aligned image rows of parts
     for (int m = wv; m < nb; m += NW) {
-      float* om = out + (size_t)m * C2;
+      float* om = p.part + (size_t)(b0 + m) * C2;
       const float* U = sR + m * W2;
       const bool act = smask[m] != 0, tab = (ssep[m] & 2) != 0;
       const float zn = szv[m];
-      for (int j0 = 0; j0 < C; j0 += 64) {
-        const int j = j0 + (tid & 63);
-        const bool jv = j < C;
-        const int jc = jv ? j : C - 1;
-        const float4 ex = tabW[m * 2 * C + jc];
-        const int x0 = __float_as_int(ex.x), x1 = __float_as_int(ex.y);
-        for (int i0 = 0; i0 < C; i0 += UW) {
-          float v[UW];
+      const float4* tcol = tabW + m * 2 * C;
+      const float4* trow = tcol + C;
+      const int nq = vec ? C2 / 4 : C2;
+      const int per = vec ? 4 : 1;
+      for (int q = lane; q < nq; q += 64) {
+        float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (act) {
+          int pix = q * per;
+          int i = pix / C, j = pix - (pix / C) * C;
 #pragma unroll
-          for (int u = 0; u < UW; ++u) {
-            const int i = min(i0 + u, C - 1);
-            v[u] = 0.0f;
-            if (!act) continue;
-            if (tab) {
-              const float4 ey = tabW[m * 2 * C + C + i];
-              const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
-              if (!(x0 == x1 && y0 == y1))
-                v[u] = zn * sample4(ex, ey, U[y0 + x0], U[y1 + x0], U[y0 + x1], U[y1 + x1]);
-            } else {
-              const Tap t = stn_tap(&sth[m][6], 28, 28, mog_linspace(jc, C), mog_linspace(i, C));
-              if (!t.dead) v[u] = zn * tap_value(t, U);
+          for (int e = 0; e < 4; ++e) {
+            if (e < per) {
+              if (tab) {
+                const float4 ex = tcol[j], ey = trow[i];
+                const int x0 = __float_as_int(ex.x), x1 = __float_as_int(ex.y);
+                const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
+                const float s = zn * sample4(ex, ey, U[y0 + x0], U[y1 + x0], U[y0 + x1],
+                                             U[y1 + x1]);
+                v[e] = axis4_dead(ex, ey) ? 0.0f : s;
+              } else {
+                const Tap t = stn_tap(&sth[m][6], 28, 28, mog_linspace(j, C), mog_linspace(i, C));
+                v[e] = t.dead ? 0.0f : zn * tap_value(t, U);
+              }
+              if (++j == C) { j = 0; ++i; }
             }
           }
-#pragma unroll
-          for (int u = 0; u < UW; ++u)
-            if (jv && i0 + u < C) om[(i0 + u) * C + j] = v[u];
         }
+        if (vec)
+          reinterpret_cast<float4*>(om)[q] = make_float4(v[0], v[1], v[2], v[3]);
+        else
+          om[q] = v[0];
       }
     }
   }
@@ -495,7 +520,9 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
                                         int G2, const float* x, const float* theta_f,
                                         const float* theta_b, const float* mask,
                                         const float* zval, const float* eps_z,
-                                        const float* eps_x, const void* const* wt,
+                                        const float* eps_x, int eps_gen,
+                                        unsigned long long eps_seed,
+                                        unsigned long long eps_offset, const void* const* wt,
                                         const float* const* bias, float lik_std, float v_pm,
                                         float v_pv, float v_plv, float* canvas_part,
                                         float* runloss, float* vkl, void* gb, void* a1b,
@@ -504,13 +531,14 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   MOG_CHECK_ARG(B >= 0 && C > 0 && C * C <= 16384);
   // the tile shapes are compiled for the reference's default VAE
   MOG_CHECK_ARG(W == 28 && R1 == 512 && R2 == 256 && Z == 50 && G1 == 256 && G2 == 512);
-  MOG_CHECK_ARG(x && theta_f && theta_b && mask && zval && eps_z && eps_x && wt && bias);
+  MOG_CHECK_ARG(x && theta_f && theta_b && mask && zval && eps_z && (eps_x || eps_gen) && wt && bias);
   MOG_CHECK_ARG(canvas_part && runloss && vkl && gb && a1b && a2b && mu && lv && z && zb);
   MOG_CHECK_ARG(d1b && d2b && r);
   if (B == 0) return 0;
   StepArgs p;
   p.x = x; p.theta_f = theta_f; p.theta_b = theta_b; p.mask = mask; p.zval = zval;
   p.eps_z = eps_z; p.eps_x = eps_x;
+  p.eps_gen = eps_gen; p.eps_seed = eps_seed; p.eps_offset = eps_offset;
   for (int i = 0; i < 7; ++i) {
     MOG_CHECK_ARG(wt[i] && bias[i]);
     p.wt[i] = reinterpret_cast<const __bf16*>(wt[i]);

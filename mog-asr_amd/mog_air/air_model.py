@@ -134,6 +134,7 @@ class _Workspace:
         # noise
         self.eps_scale, self.eps_shift = e(T, B), e(T, B, 2)
         self.eps_z, self.eps_x, self.u = e(T, B, Z), e(T, B, W2), e(T, B)
+        self.eps_x_offset = None  # set when the fused kernel generates eps_x itself
         self._bwd = False
         self.materialized = False
 
@@ -330,10 +331,16 @@ class AIRModel:
                                      f"expected {tuple(dst.shape)}")
                 dst.copy_(src)
             return
+        ws.eps_x_offset = None
         for k, normal in (("eps_scale", True), ("eps_shift", True), ("eps_z", True),
                           ("eps_x", True), ("u", False)):
             buf = getattr(ws, k)
-            ops.rng_fill(buf, self.noise_seed, self._noise_ctr, normal)
+            if k == "eps_x" and self.fused_step:
+                # generated inside the fused step kernel from the same Philox
+                # counters (bit-identical to filling the buffer)
+                ws.eps_x_offset = self._noise_ctr
+            else:
+                ops.rng_fill(buf, self.noise_seed, self._noise_ctr, normal)
             self._noise_ctr += (buf.numel() + 3) // 4
 
     # ----------------------------------------------------------- forward ---
@@ -562,27 +569,30 @@ class AIRModel:
         return (n + 7) // 8 * 8
 
     def _pack_bf16(self):
-        """Refresh the bf16 weight packs after a parameter update:
-        wt[name] = W^T [out][in8] (forward B operand), wn[name] = W [in][out8] (dX)."""
+        """Refresh the bf16 weight packs after a parameter update (one batched
+        launch): wn[name] = W [in][out8] (dX B operand) and either
+        wf[name] = W^T in MFMA B-fragment order (fused step kernel) or
+        wt[name] = W^T [out][in8] (unfused forward GEMMs)."""
         if getattr(self, "_pack_version", None) == self.params.version:
             return
-        if not hasattr(self, "_wt"):
-            self._wt, self._wn = {}, {}
-            for n in self._VAE:
-                I, O = self.params.shapes["air/rnn/vae/" + n + "/weights"]
-                bf = dict(device=self.device, dtype=torch.bfloat16)
-                self._wt[n] = torch.zeros((O, self._pad8(I)), **bf)
-                self._wn[n] = torch.zeros((I, self._pad8(O)), **bf)
-        if not hasattr(self, "_pack_args"):  # one batched launch for all 14 packs
+        if not hasattr(self, "_pack_args"):
+            bf = dict(device=self.device, dtype=torch.bfloat16)
+            self._wt, self._wn, self._wf = {}, {}, {}
             srcs, dsts, dims = [], [], []
             for n in self._VAE:
                 w = self._P("vae/" + n + "/weights")
                 I, O = w.shape
-                wt, wn = self._wt[n], self._wn[n]
+                wn = self._wn[n] = torch.zeros((I, self._pad8(O)), **bf)
+                if self.fused_step:
+                    Np, Kp = (O + 15) // 16 * 16, (I + 31) // 32 * 32
+                    wf = self._wf[n] = torch.zeros((Np, Kp), **bf)
+                    fwd, fdims = wf, [I, O, O, Np, Kp, Kp, 2]
+                else:
+                    wt = self._wt[n] = torch.zeros((O, self._pad8(I)), **bf)
+                    fwd, fdims = wt, [I, O, O, O, wt.shape[1], wt.shape[1], 1]
                 srcs += [dp(w), dp(w)]
-                dsts += [dp(wt), dp(wn)]
-                dims += [I, O, O, wt.shape[0], wt.shape[1], wt.shape[1], 1,
-                         I, O, O, wn.shape[0], wn.shape[1], wn.shape[1], 0]
+                dsts += [dp(fwd), dp(wn)]
+                dims += fdims + [I, O, O, I, wn.shape[1], wn.shape[1], 0]
             self._pack_args = (len(srcs), _lib.ptr_array(srcs), _lib.ptr_array(dsts),
                                (ctypes.c_int * len(dims))(*dims))
         _lib.call("mog_cvt_bf16_batch", *self._pack_args, stream_ptr())
@@ -618,11 +628,14 @@ class AIRModel:
         (vae_step.hip; same arithmetic as the unfused bf16 sequence)."""
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         self._pack_bf16()
-        wt = _lib.ptr_array([dp(self._wt[n]) for n in self._VAE])
+        wt = _lib.ptr_array([dp(self._wf[n]) for n in self._VAE])
+        gen = getattr(ws, "eps_x_offset", None) is not None
+        off = ws.eps_x_offset + t * ws.B * (W2 // 4) if gen else 0
         bias = _lib.ptr_array([dp(self._P("vae/" + n + "/biases")) for n in self._VAE])
         _lib.call("mog_stn_vae_step_forward", ws.B, self.canvas_size, self.windows_size, R1, R2,
                   Z, G1, G2, dp(X), dp(ws.th_f[t]), dp(ws.th_b[t]), dp(ws.zmask[t]),
-                  dp(ws.zval[t]), dp(ws.eps_z[t]), dp(ws.eps_x[t]), wt, bias, lik_std,
+                  dp(ws.zval[t]), dp(ws.eps_z[t]), dp(ws.eps_x[t]), int(gen),
+                  self.noise_seed & (2 ** 64 - 1), off & (2 ** 64 - 1), wt, bias, lik_std,
                   float(self.vae_prior_mean), float(self.vae_prior_variance),
                   self.vae_prior_log_variance, dp(ws.cparts[t]), dp(ws.runloss), dp(ws.vkl[t]),
                   dp(ws.gb[t]), dp(ws.a1b[t]), dp(ws.a2b[t]), dp(ws.mu[t]), dp(ws.lv[t]),

@@ -17,8 +17,8 @@ run() {
 }
 for step in "$@"; do
   case "$step" in
-    pytest) run pytest 600 python -m pytest tests -m gpu -x -q ;;
-    pytestv) run pytest 600 python -m pytest tests -m gpu -q ;;
+    pytest) run pytest 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    pytestv) run pytest 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py --steps 10 --warmup 3 --cpu-seconds 10 ;;
     benchq) run bench 300 python bench.py --steps 10 --warmup 3 --cpu-baseline 0 ;;

@@ -183,3 +183,21 @@ def test_fused_step_gradients_match_unfused():
     for name in gu:
         d = np.linalg.norm(gf[name] - gu[name]) / max(np.linalg.norm(gu[name]), 1e-30)
         assert d < 1e-5, (name, d)
+
+
+def test_fused_step_inkernel_noise_matches_filled_noise():
+    """Perf mode (no injected noise): the fused kernel generates eps_x from the
+    Philox counters mog_rng_fill would have used; every output must equal the
+    unfused sequence that reads the filled eps_x buffer, bit for bit."""
+    cfg, P, nz, x, k = _setup(batch=70, seed=7)
+    mf = _model(cfg, P, "pfused", fused=True)
+    mu = _model(cfg, P, "punfused", fused=False)
+    mf.noise_seed = mu.noise_seed = 4242
+    mf.infer(x, k)
+    mu.infer(x, k)
+    torch.cuda.synchronize()
+    assert mf._ws.eps_x_offset is not None and mu._ws.eps_x_offset is None
+    for name in ("canvas", "runloss", "vkl", "r", "z", "d2b"):
+        a, b = getattr(mf._ws, name), getattr(mu._ws, name)
+        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
+                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32)), name
