@@ -3,18 +3,24 @@
 // vae.py:5-48, transformer.py:18-175).  This is the kernel SURVEY.md §8 D.3
 // prices at 30,024 algorithmic HBM bytes per image-step.
 //
-// One workgroup = 8 waves = MB (32) images.  Activations stay in LDS between
-// the six dense layers (bf16, rows padded against bank conflicts); the packed
-// bf16 weights (W^T in MFMA B-fragment order: one 1-KiB contiguous load per
-// fragment) stream from L2 straight into the MFMA B operand (four k-steps of
-// register prefetch); the A operand is
-// read from LDS with ds_read_b128.  Activations the backward needs (glimpse,
-// softplus outputs, mu/logvar/z, r) are flushed to HBM with 16-byte stores.
-// The STN write samples r from LDS (fp32) and stores this step's canvas
-// contribution z * w (0 where inactive or where the sample is exactly +0,
-// i.e. x0 == x1 && y0 == y1); mog_recon_loss sums the parts in step order, so
-// the canvas is bit-identical to the running accumulation of
-// air_model.py:665-675 and this kernel never waits on a canvas read.
+// One workgroup = 8 waves = MB (32) images, two workgroups per CU (70.5 KB of
+// LDS each), so one workgroup's gathers and stores overlap the other's MFMA
+// phases.  Activations stay in LDS between the six dense layers (bf16, rows
+// padded against bank conflicts), reusing one region: a layer whose output
+// lands on its own input waits for the whole workgroup after its k loop.  The
+// bf16 weights (W^T in MFMA B-fragment order: one 1-KiB contiguous wave load
+// per fragment) stream from L2 straight into the MFMA B operand (four k-steps
+// of register prefetch); the A operand is read from LDS with ds_read_b128.
+// Activations the backward needs (glimpse, softplus outputs, mu/logvar/z, r)
+// are flushed to HBM with 16-byte stores.  The output layer's tiles are
+// transposed through LDS so that the bias + noise + sigmoid epilogue works on
+// four consecutive pixels (one Philox quad of eps_x) and r leaves with 16-byte
+// stores; the STN write then stages r back from L2 sixteen images at a time
+// and stores this step's canvas contribution z * w (0 where inactive or where
+// the sample is exactly +0, i.e. x0 == x1 && y0 == y1); mog_recon_loss sums
+// the parts in step order, so the canvas is bit-identical to the running
+// accumulation of air_model.py:665-675 and this kernel never waits on a
+// canvas read.
 //
 // Precision: bf16 MFMA operands, fp32 accumulation and epilogues with
 // hardware transcendentals (the bf16 configuration, BASELINE configs[1]).
@@ -38,21 +44,27 @@ constexpr int W2 = 784;       // 28 x 28 glimpse
 constexpr int KG = 800;       // glimpse k extent padded to a multiple of 32 (25 k-steps)
 constexpr int SG = KG + 8;    // LDS row strides (bf16), +16 B against bank conflicts
 constexpr int S512 = 512 + 8, S256 = 256 + 8, SZ = 64 + 8;
-// LDS region A (bytes): glimpse tile + read tables, then a2 | mu | lv | kl | z | d1,
-// then r (fp32).  Region H: a1, then d2, then the write tables.
-constexpr int REGION_A = MB * W2 * 4;
-constexpr int OFF_TABR = MB * SG * 2;
-constexpr int TABR = 28 + 28;                 // read tables: 28 columns + 28 rows per image
-constexpr int OFF_MU = MB * S256 * 2;
-constexpr int OFF_LV = OFF_MU + MB * 50 * 4;
-constexpr int OFF_KL = OFF_LV + MB * 50 * 4;
-constexpr int OFF_Z = OFF_KL + MB * 50 * 4;
-constexpr int OFF_D1 = OFF_Z + MB * SZ * 2;
-constexpr int CTAB_MAX = 52;                  // write tables for canvases up to 52 x 52
-constexpr int REGION_H = MB * 2 * CTAB_MAX * 16;
-static_assert(OFF_TABR + MB * TABR * 16 <= REGION_A, "read tables");
-static_assert(OFF_D1 + MB * S256 * 2 <= REGION_A, "LDS layout");
-static_assert(MB * S512 * 2 <= REGION_H, "region H");
+// One LDS arena: region A [0, A_BYTES) then region H [A_BYTES, ARENA).
+//   A: glimpse [32][808] -> a1 [32][520] -> mu | lv | kl fp32, z bf16 -> d2
+//      [32][520] (+ the output layer's transpose scratch behind it)
+//   H: read tables -> a2 [32][264] -> d1 [32][264]
+//   A+H: r staging for 16 images [16][784] fp32 + their write tables
+constexpr int A_BYTES = MB * SG * 2;                     // 51,712
+constexpr int H_BYTES = MB * S256 * 2;                   // 16,896
+constexpr int ARENA = A_BYTES + H_BYTES;                 // 68,608
+constexpr int TABR = 28 + 28;                            // read tables: 28 columns + 28 rows
+constexpr int OFF_MU = 0, OFF_LV = MB * 50 * 4, OFF_KL = 2 * MB * 50 * 4, OFF_Z = 3 * MB * 50 * 4;
+constexpr int OFF_XP = MB * S512 * 2;                    // transpose scratch behind d2
+constexpr int XP_STRIDE = 20;                            // floats per scratch row (conflict-free)
+constexpr int XP_WAVE = 32 * XP_STRIDE * 4;              // 2,560 B per wave
+constexpr int RH = 16;                                   // images per r-staging half
+constexpr int OFF_TABW = RH * W2 * 4;                    // 50,176
+constexpr int CTAB_MAX = 64;                             // write tables for canvases up to 64 x 64
+static_assert(MB * TABR * 8 <= H_BYTES, "read tables");
+static_assert(OFF_Z + MB * SZ * 2 <= A_BYTES, "mu/lv/kl/z");
+static_assert(MB * S512 * 2 <= A_BYTES && MB * S256 * 2 <= H_BYTES, "activations");
+static_assert(OFF_XP + NW * XP_WAVE <= ARENA, "transpose scratch");
+static_assert(OFF_TABW + RH * 2 * CTAB_MAX * 8 <= ARENA, "write tables");
 
 struct StepArgs {
   const float* x;            // [B, C*C] canvas input
@@ -90,39 +102,36 @@ __device__ __forceinline__ float softplus_fast(float v) {
   return v > -MOG_SOFTPLUS_T ? v : (v < MOG_SOFTPLUS_T ? __expf(v) : __logf(__expf(v) + 1.0f));
 }
 
-// Expanded axis tables of every image's transform (th at sth[m][th_off]):
-// tab[m][0..Wout) columns, tab[m][Wout..Wout+Hout) rows (row entries carry
-// the source pitch Win).  Only read for axis-aligned transforms.
-__device__ __forceinline__ void build_tables(float4* tab, int stride, const float (*sth)[12],
+// Axis tables of `nimg` images' transforms (th at sth[m0 + m][th_off]):
+// tab[m*per + n], n < Wout columns then Hout rows, as {coordinate, lo | hi<<16}.
+__device__ __forceinline__ void build_tables(float2* tab, const float (*sth)[12], int m0, int nimg,
                                              int th_off, int Hin, int Win, int Hout, int Wout) {
   const int per = Wout + Hout;
-  for (int i = threadIdx.x; i < MB * per; i += NTHR) {
+  for (int i = threadIdx.x; i < nimg * per; i += NTHR) {
     const int m = i / per, n = i - (i / per) * per;
-    const float* th = &sth[m][th_off];
-    tab[m * stride + n] = n < Wout ? axis4(axis_col(th, Hin, Win, Hout, Wout, n), 1)
-                                   : axis4(axis_row(th, Hin, Win, Hout, Wout, n - Wout), Win);
+    const float* th = &sth[m0 + m][th_off];
+    tab[i] = n < Wout ? axis_col(th, Hin, Win, Hout, Wout, n)
+                      : axis_row(th, Hin, Win, Hout, Wout, n - Wout);
   }
 }
 
 // Column tiles tile_base + (w + nw*c + rot) % (nw*TPW) of one dense layer
-// over the MB rows held in LDS, for waves wbase .. wbase+nw-1:
-// epi(row, col, acc, aux).  A: LDS [MB][lda] bf16, zero-padded to K.  W: the
-// layer's W^T in B-fragment order (mog_cvt_bf16_batch transpose 2; N padded
-// to 16, K to 32, zeros outside), so each B fragment is one 1-KiB contiguous
-// wave load streamed from L2 straight into the MFMA, with a four-k-step
-// register prefetch ring (rolled, branch-free body so the compiler keeps the
-// distance; the ragged tail is peeled at compile time).  With AUX the
-// epilogue operand aux[row][col] is loaded before the k loop.
-template <int N, int K, int TPW, bool AUX, class Epi>
+// over the MB rows held in LDS, for waves wbase .. wbase+nw-1.  A: LDS
+// [MB][lda] bf16, zero-padded to K.  W: the layer's W^T in B-fragment order
+// (mog_cvt_bf16_batch transpose 2; N padded to 16, K to 32, zeros outside),
+// so each B fragment is one 1-KiB contiguous wave load streamed from L2
+// straight into the MFMA, with a register prefetch ring of D k-steps (rolled,
+// branch-free body so the compiler keeps the distance; the ragged tail is
+// peeled at compile time).  SYNC: the whole workgroup meets after the k loop
+// (the epilogue overwrites A; requires nw == NW).  epi(ct, acc[2][4] per tile).
+template <int K, int TPW, bool SYNC, class Epi>
 __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf16* __restrict__ W,
-                                            int tile_base, int wbase, int nw,
-                                            const float* __restrict__ aux, int ldaux, int nb,
-                                            Epi epi) {
+                                            int tile_base, int wbase, int nw, Epi epi) {
   constexpr int KS = K / 32;
   static_assert(K % 32 == 0, "K padding");
   const int rot = (int)(blockIdx.x >> 3);  // spread the CUs of one XCD over the weight columns
   const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) - wbase;
-  if (w < 0 || w >= nw) return;
+  const bool on = w >= 0 && w < nw;
   const int li = lane & 15, g = lane >> 4;
   int ct[TPW];
   const bf16x8* wf[TPW];
@@ -130,18 +139,6 @@ __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf
   for (int c = 0; c < TPW; ++c) {
     ct[c] = tile_base + (w + nw * c + rot) % (nw * TPW);
     wf[c] = reinterpret_cast<const bf16x8*>(W) + (size_t)ct[c] * KS * 64 + lane;
-  }
-  float av[2][TPW][4];
-  if constexpr (AUX) {
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int c = 0; c < TPW; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rt * 16 + g * 4 + r, col = ct[c] * 16 + li;
-          av[rt][c][r] = aux[(size_t)min(row, nb - 1) * ldaux + min(col, N - 1)];  // unpredicated
-        }
   }
   floatx4 acc[2][TPW];
 #pragma unroll
@@ -162,58 +159,62 @@ __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf
       acc[1][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b[c], acc[1][c], 0, 0, 0);
     }
   };
-  if constexpr (KS < 4) {
-    bf16x8 q[TPW];
+  // ring depth: four k-steps of B fragments in flight, two for four-tile waves
+  // (register budget of two workgroups per CU)
+  constexpr int D = TPW >= 4 ? 2 : 4;
+  if (on) {
+    if constexpr (KS < D) {
+      bf16x8 q[TPW];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      loadB(ks, q);
-      step(ks, q);
-    }
-  } else {
-    constexpr int NI = (KS - 4) / 4;   // ring iterations with four refills each
-    constexpr int K0 = 4 * NI;         // first k-step of the peeled tail
-    constexpr int R = KS - K0;         // 4 .. 7 tail steps
-    bf16x8 q0[TPW], q1[TPW], q2[TPW], q3[TPW];
-    loadB(0, q0);
-    loadB(1, q1);
-    loadB(2, q2);
-    loadB(3, q3);
+      for (int ks = 0; ks < KS; ++ks) {
+        loadB(ks, q);
+        step(ks, q);
+      }
+    } else {
+      constexpr int NI = (KS - D) / D;   // ring iterations with D refills each
+      constexpr int K0 = D * NI;         // first k-step of the peeled tail
+      bf16x8 q[D][TPW];
+#pragma unroll
+      for (int d = 0; d < D; ++d) loadB(d, q[d]);
 #pragma unroll 1
-    for (int ks = 0; ks < K0; ks += 4) {
-      step(ks, q0);
-      loadB(ks + 4, q0);
-      __builtin_amdgcn_sched_barrier(0);
-      step(ks + 1, q1);
-      loadB(ks + 5, q1);
-      __builtin_amdgcn_sched_barrier(0);
-      step(ks + 2, q2);
-      loadB(ks + 6, q2);
-      __builtin_amdgcn_sched_barrier(0);
-      step(ks + 3, q3);
-      loadB(ks + 7, q3);
-      __builtin_amdgcn_sched_barrier(0);
+      for (int ks = 0; ks < K0; ks += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          step(ks + d, q[d]);
+          loadB(ks + d + D, q[d]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        step(K0 + d, q[d]);
+        if (K0 + d + D < KS) loadB(K0 + d + D, q[d]);
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+        if (K0 + D + d < KS) step(K0 + D + d, q[d]);
     }
-    step(K0, q0);
-    if constexpr (R > 4) loadB(K0 + 4, q0);
-    step(K0 + 1, q1);
-    if constexpr (R > 5) loadB(K0 + 5, q1);
-    step(K0 + 2, q2);
-    if constexpr (R > 6) loadB(K0 + 6, q2);
-    step(K0 + 3, q3);
-    if constexpr (R > 4) step(K0 + 4, q0);
-    if constexpr (R > 5) step(K0 + 5, q1);
-    if constexpr (R > 6) step(K0 + 6, q2);
   }
+  if constexpr (SYNC) __syncthreads();
+  if (!on) return;
+#pragma unroll
+  for (int c = 0; c < TPW; ++c) {
+    floatx4 a[2] = {acc[0][c], acc[1][c]};
+    epi(ct[c], a);
+  }
+}
+
+// element-wise epilogue into an LDS tile: out[row][col] = f(acc, col) for the
+// lane's 8 accumulators of column tile ct (rows rt*16 + g*4 + r, col ct*16 + li)
+template <class F>
+__device__ __forceinline__ void epi_rows(int ct, const floatx4* a, int N, F f) {
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int col = ct * 16 + li;
+  if (col >= N) return;
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-    for (int c = 0; c < TPW; ++c) {
-      const int col = ct[c] * 16 + li;
-      if (col >= N) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        epi(rt * 16 + g * 4 + r, col, acc[rt][c][r], AUX ? av[rt][c][r] : 0.0f);
-    }
+    for (int r = 0; r < 4; ++r) f(rt * 16 + g * 4 + r, col, a[rt][r]);
 }
 
 // LDS tile [nb][lds] -> HBM rows [nb][ldg] with 16-byte stores (ncols * sizeof(T) % 16 == 0).
@@ -231,30 +232,33 @@ __device__ __forceinline__ void flush_rows(const T* s, int lds, T* g, int ldg, i
 #define STAMP(k) \
   if (p.tstamp && threadIdx.x == 0) p.tstamp[blockIdx.x * 16 + (k)] = wall_clock64()
 
-__global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
+__global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) {
 #pragma clang fp contract(off)
-  __shared__ __attribute__((aligned(16))) unsigned char sA[REGION_A];
-  __shared__ __attribute__((aligned(16))) unsigned char sHb[REGION_H];
+  __shared__ __attribute__((aligned(16))) unsigned char arena[ARENA];
   __shared__ float sth[MB][12];
   __shared__ float szv[MB];
   __shared__ int smask[MB];
   __shared__ int ssep[MB];  // bit 0: theta_f axis-aligned, bit 1: theta_b (and tables fit)
   const int tid = threadIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
   const int b0 = blockIdx.x * MB;
   const int nb = min(MB, p.B - b0);
   const int C = p.C, C2 = C * C;
+  unsigned char* sA = arena;
+  unsigned char* sHb = arena + A_BYTES;
   __bf16* sG = reinterpret_cast<__bf16*>(sA);
-  float4* tabR = reinterpret_cast<float4*>(sA + OFF_TABR);
-  __bf16* sA2 = reinterpret_cast<__bf16*>(sA);
+  __bf16* sA1 = reinterpret_cast<__bf16*>(sA);
+  __bf16* sD2 = reinterpret_cast<__bf16*>(sA);
   float* sMu = reinterpret_cast<float*>(sA + OFF_MU);
   float* sLv = reinterpret_cast<float*>(sA + OFF_LV);
   float* sKl = reinterpret_cast<float*>(sA + OFF_KL);
   __bf16* sZ = reinterpret_cast<__bf16*>(sA + OFF_Z);
-  __bf16* sD1 = reinterpret_cast<__bf16*>(sA + OFF_D1);
-  float* sR = reinterpret_cast<float*>(sA);
-  __bf16* sH = reinterpret_cast<__bf16*>(sHb);
-  float4* tabW = reinterpret_cast<float4*>(sHb);
+  float2* tabR = reinterpret_cast<float2*>(sHb);
+  __bf16* sA2 = reinterpret_cast<__bf16*>(sHb);
+  __bf16* sD1 = reinterpret_cast<__bf16*>(sHb);
+  float* sR = reinterpret_cast<float*>(arena);
+  float2* tabW = reinterpret_cast<float2*>(arena + OFF_TABW);
 
   for (int i = tid; i < MB * 12; i += NTHR) {
     const int m = i / 12, k = i % 12;
@@ -271,7 +275,7 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
   if (tid < MB)
     ssep[tid] = (stn_separable(&sth[tid][0]) ? 1 : 0) |
                 (stn_separable(&sth[tid][6]) && C <= CTAB_MAX ? 2 : 0);
-  build_tables(tabR, TABR, sth, 0, C, C, 28, 28);
+  build_tables(tabR, sth, 0, MB, 0, C, C, 28, 28);
   __syncthreads();
   STAMP(0);
 
@@ -293,8 +297,8 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
         const int mc = live[u] ? m : 0, jc = min(j, 27);
         const float* U = p.x + (size_t)(b0 + mc) * C2;
         if (ssep[mc] & 1) {
-          ex[u] = tabR[mc * TABR + jc];
-          ey[u] = tabR[mc * TABR + 28 + i];
+          ex[u] = axis4(tabR[mc * TABR + jc], 1);
+          ey[u] = axis4(tabR[mc * TABR + 28 + i], C);
         } else {  // general affine transform: per-sample geometry
           const Tap t = stn_tap(sth[mc], C, C, mog_linspace(jc, 28), mog_linspace(i, 28));
           ex[u] = make_float4(__int_as_float((int)t.x0f), __int_as_float((int)t.x1f),
@@ -330,39 +334,39 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
   STAMP(1);
   if (p.phases & 16) flush_rows(sG, SG, p.gb + (size_t)b0 * W2, W2, W2, nb);
 
-  // ---- 2. a1 = softplus(g W1 + b1)  [MB x 512] -> H -----------------------
+  // ---- 2. a1 = softplus(g W1 + b1)  [MB x 512], over the glimpse ----------
   if (p.phases & 2) {
     const float* bias = p.bias[0];
-    dense_tiles<512, KG, 4, false>(sG, SG, p.wt[0], 0, 0, NW, nullptr, 0, nb,
-                                       [&](int m, int n, float v, float) {
-      sH[m * S512 + n] = (__bf16)softplus_fast(v + bias[n]);
+    dense_tiles<KG, 4, true>(sG, SG, p.wt[0], 0, 0, NW, [&](int ct, const floatx4* a) {
+      epi_rows(ct, a, 512, [&](int m, int n, float v) {
+        sA1[m * S512 + n] = (__bf16)softplus_fast(v + bias[n]);
+      });
     });
   }
   __syncthreads();
   STAMP(2);
-  if (p.phases & 16) flush_rows(sH, S512, p.a1b + (size_t)b0 * 512, 512, 512, nb);
-  // ---- 3. a2 = softplus(a1 W2 + b2)  [MB x 256] -> A ----------------------
+  if (p.phases & 16) flush_rows(sA1, S512, p.a1b + (size_t)b0 * 512, 512, 512, nb);
+  // ---- 3. a2 = softplus(a1 W2 + b2)  [MB x 256] -> H ----------------------
   if (p.phases & 2) {
     const float* bias = p.bias[1];
-    dense_tiles<256, 512, 2, false>(sH, S512, p.wt[1], 0, 0, NW, nullptr, 0, nb,
-                                         [&](int m, int n, float v, float) {
-      sA2[m * S256 + n] = (__bf16)softplus_fast(v + bias[n]);
+    dense_tiles<512, 2, false>(sA1, S512, p.wt[1], 0, 0, NW, [&](int ct, const floatx4* a) {
+      epi_rows(ct, a, 256, [&](int m, int n, float v) {
+        sA2[m * S256 + n] = (__bf16)softplus_fast(v + bias[n]);
+      });
     });
   }
   __syncthreads();
   STAMP(3);
   if (p.phases & 16) flush_rows(sA2, S256, p.a2b + (size_t)b0 * 256, 256, 256, nb);
-  // ---- 4. mu | lv = a2 W + b  [MB x 50] fp32 (waves 0-3 | 4-7) ------------
+  // ---- 4. mu | lv = a2 W + b  [MB x 50] fp32 -> A (waves 0-3 | 4-7) ------
   if (p.phases & 2) {
     const float* bm = p.bias[2];
-    dense_tiles<50, 256, 1, false>(sA2, S256, p.wt[2], 0, 0, 4, nullptr, 0, nb,
-                                        [&](int m, int n, float v, float) {
-      sMu[m * 50 + n] = v + bm[n];
+    dense_tiles<256, 1, false>(sA2, S256, p.wt[2], 0, 0, 4, [&](int ct, const floatx4* a) {
+      epi_rows(ct, a, 50, [&](int m, int n, float v) { sMu[m * 50 + n] = v + bm[n]; });
     });
     const float* bl = p.bias[3];
-    dense_tiles<50, 256, 1, false>(sA2, S256, p.wt[3], 0, 4, 4, nullptr, 0, nb,
-                                        [&](int m, int n, float v, float) {
-      sLv[m * 50 + n] = v + bl[n];
+    dense_tiles<256, 1, false>(sA2, S256, p.wt[3], 0, 4, 4, [&](int ct, const floatx4* a) {
+      epi_rows(ct, a, 50, [&](int m, int n, float v) { sLv[m * 50 + n] = v + bl[n]; });
     });
   }
   __syncthreads();
@@ -400,112 +404,165 @@ __global__ __launch_bounds__(NTHR) void stn_vae_step_bf16_kernel(StepArgs p) {
     if (smask[m]) p.runloss[b0 + m] = p.runloss[b0 + m] + vkl;
   }
   STAMP(5);
-  // ---- 6. d1 = softplus(z Wg1 + b)  [MB x 256] ----------------------------
+  // ---- 6. d1 = softplus(z Wg1 + b)  [MB x 256] -> H -----------------------
   if (p.phases & 2) {
     const float* bias = p.bias[4];
-    dense_tiles<256, 64, 2, false>(sZ, SZ, p.wt[4], 0, 0, NW, nullptr, 0, nb,
-                                       [&](int m, int n, float v, float) {
-      sD1[m * S256 + n] = (__bf16)softplus_fast(v + bias[n]);
+    dense_tiles<64, 2, false>(sZ, SZ, p.wt[4], 0, 0, NW, [&](int ct, const floatx4* a) {
+      epi_rows(ct, a, 256, [&](int m, int n, float v) {
+        sD1[m * S256 + n] = (__bf16)softplus_fast(v + bias[n]);
+      });
     });
   }
   __syncthreads();
   STAMP(6);
   if (p.phases & 16) flush_rows(sD1, S256, p.d1b + (size_t)b0 * 256, 256, 256, nb);
-  // ---- 7. d2 = softplus(d1 Wg2 + b)  [MB x 512] -> H ----------------------
+  // ---- 7. d2 = softplus(d1 Wg2 + b)  [MB x 512] -> A ----------------------
   if (p.phases & 2) {
     const float* bias = p.bias[5];
-    dense_tiles<512, 256, 4, false>(sD1, S256, p.wt[5], 0, 0, NW, nullptr, 0, nb,
-                                         [&](int m, int n, float v, float) {
-      sH[m * S512 + n] = (__bf16)softplus_fast(v + bias[n]);
+    dense_tiles<256, 4, false>(sD1, S256, p.wt[5], 0, 0, NW, [&](int ct, const floatx4* a) {
+      epi_rows(ct, a, 512, [&](int m, int n, float v) {
+        sD2[m * S512 + n] = (__bf16)softplus_fast(v + bias[n]);
+      });
     });
   }
   __syncthreads();
   STAMP(7);
-  if (p.phases & 16) flush_rows(sH, S512, p.d2b + (size_t)b0 * 512, 512, 512, nb);
-  // ---- 8. r = sigmoid(d2 Wgo + b + std eps)  [MB x 784] fp32 -> A ---------
-  // eps_x is staged in the r tile first (generated in-kernel with the same
-  // Philox quads mog_rng_fill would write, or loaded with 16-byte reads); each
-  // epilogue lane reads its eps and overwrites it with r.  49 column tiles:
-  // 32 (4 per wave) + 16 (2 per wave) + 1 (wave 0).
+  if (p.phases & 16) flush_rows(sD2, S512, p.d2b + (size_t)b0 * 512, 512, 512, nb);
+  // ---- 8. r = sigmoid(d2 Wgo + b + std eps)  [MB x 784] fp32 -> HBM -------
+  // Each 32 x 16 accumulator tile goes through the wave's LDS scratch so that
+  // a lane owns four consecutive pixels of one row: one Philox quad of eps_x
+  // (generated in-kernel exactly as mog_rng_fill would, or loaded), one
+  // 16-byte store of r.  49 column tiles: 32 (4 per wave) + 16 (2) + 1 (wave 0).
   if (p.phases & 2) {
-    float4* sR4 = reinterpret_cast<float4*>(sR);
-    constexpr int QPR = W2 / 4;  // 196 quads per image
-    if (p.eps_gen) {
-      for (int i = tid; i < nb * QPR; i += NTHR) {
-        const int m = i / QPR, q = i - (i / QPR) * QPR;
-        float v[4];
-        mog_philox_quad(p.eps_seed, p.eps_offset + (unsigned long long)(b0 + m) * QPR + q, true,
-                        v);
-        sR4[i] = make_float4(v[0], v[1], v[2], v[3]);
-      }
-    } else {
-      const float4* ex4 = reinterpret_cast<const float4*>(p.eps_x + (size_t)b0 * W2);
-      for (int i = tid; i < nb * QPR; i += NTHR) sR4[i] = ex4[i];
-    }
-    __syncthreads();
     const float* bias = p.bias[6];
     const float sd = p.lik_std;
-    auto epi = [&](int m, int n, float v, float) {
-      const float e = sR[m * W2 + n];
-      const float y = __builtin_fmaf(e, sd, v + bias[n]);
-      sR[m * W2 + n] = 1.0f / (1.0f + __expf(-y));
+    float* xp = reinterpret_cast<float*>(arena + OFF_XP + wv * XP_WAVE);
+    auto epi = [&](int ct, const floatx4* a) {
+      const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xp[(rt * 16 + g * 4 + r) * XP_STRIDE + li] = a[rt][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int cq = lane & 3, n = ct * 16 + 4 * cq;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int m = h * 16 + (lane >> 2);
+        const float4 v = *reinterpret_cast<const float4*>(&xp[m * XP_STRIDE + 4 * cq]);
+        if (m < nb && n < W2) {
+          float e[4];
+          const size_t q = (size_t)(b0 + m) * (W2 / 4) + (n >> 2);
+          if (p.eps_gen) {
+            mog_philox_quad(p.eps_seed, p.eps_offset + q, true, e);
+          } else {
+            const float4 e4 = reinterpret_cast<const float4*>(p.eps_x)[q];
+            e[0] = e4.x; e[1] = e4.y; e[2] = e4.z; e[3] = e4.w;
+          }
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+          float o[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float y = __builtin_fmaf(e[k], sd, vv[k] + bias[n + k]);
+            o[k] = 1.0f / (1.0f + __expf(-y));
+          }
+          reinterpret_cast<float4*>(p.r)[q] = make_float4(o[0], o[1], o[2], o[3]);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // scratch reads before the next tile
     };
-    dense_tiles<784, 512, 4, false>(sH, S512, p.wt[6], 0, 0, NW, nullptr, 0, nb, epi);
-    dense_tiles<784, 512, 2, false>(sH, S512, p.wt[6], 32, 0, NW, nullptr, 0, nb, epi);
-    dense_tiles<784, 512, 1, false>(sH, S512, p.wt[6], 48, 0, 1, nullptr, 0, nb, epi);
+    dense_tiles<512, 4, false>(sD2, S512, p.wt[6], 0, 0, NW, epi);
+    dense_tiles<512, 2, false>(sD2, S512, p.wt[6], 32, 0, NW, epi);
+    dense_tiles<512, 1, false>(sD2, S512, p.wt[6], 48, 0, 1, epi);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // r stores done before other waves read it
   __syncthreads();
   STAMP(8);
-  if (p.phases & 16) flush_rows(sR, W2, p.r + (size_t)b0 * W2, W2, W2, nb);
-  if (C <= CTAB_MAX) build_tables(tabW, 2 * C, sth, 6, 28, 28, C, C);  // d2 is dead
-  __syncthreads();
   STAMP(9);
   // ---- 9. STN write (air_model.py:580-588): this step's canvas part -------
   // part = active ? z * w : 0 for every pixel (write-only; mog_recon_loss sums
-  // the parts in step order).  One wave per image; each lane produces four
-  // consecutive canvas pixels (flat order) and stores them with one 16-byte
-  // store.  Dead samples (clipped corners coincide on both axes) are exactly
-  // +0 and are selected, not branched.
+  // the parts in step order).  r is staged back from L2 sixteen images at a
+  // time; one wave per image; each lane produces four consecutive canvas
+  // pixels (flat order) and stores them with one 16-byte store.  Dead samples
+  // (clipped corners coincide on both axes) are exactly +0 and are selected,
+  // not branched.
   if (p.phases & 8) {
-    const int lane = tid & 63;
     const bool vec = (C2 & 3) == 0;  // even C: 16-byte aligned image rows of parts
-    for (int m = wv; m < nb; m += NW) {
-      float* om = p.part + (size_t)(b0 + m) * C2;
-      const float* U = sR + m * W2;
-      const bool act = smask[m] != 0, tab = (ssep[m] & 2) != 0;
-      const float zn = szv[m];
-      const float4* tcol = tabW + m * 2 * C;
-      const float4* trow = tcol + C;
-      const int nq = vec ? C2 / 4 : C2;
-      const int per = vec ? 4 : 1;
-      for (int q = lane; q < nq; q += 64) {
-        float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (act) {
-          int pix = q * per;
-          int i = pix / C, j = pix - (pix / C) * C;
+    for (int h0 = 0; h0 < nb; h0 += RH) {
+      const int nh = min(RH, nb - h0);
+      {
+        const float4* src = reinterpret_cast<const float4*>(p.r + (size_t)(b0 + h0) * W2);
+        float4* dst = reinterpret_cast<float4*>(sR);
+        for (int i = tid; i < nh * (W2 / 4); i += NTHR) dst[i] = src[i];
+      }
+      if (C <= CTAB_MAX) build_tables(tabW, sth, h0, nh, 6, 28, 28, C, C);
+      __syncthreads();
+      for (int mm = wv; mm < nh; mm += NW) {
+        const int m = h0 + mm;
+        float* om = p.part + (size_t)(b0 + m) * C2;
+        float4* om4 = reinterpret_cast<float4*>(om);
+        const float* U = sR + mm * W2;
+        const bool act = smask[m] != 0, tab = (ssep[m] & 2) != 0;
+        const float zn = szv[m];
+        const float2* tcol = tabW + mm * 2 * C;
+        const float2* trow = tcol + C;
+        if (!act) {  // inactive: the whole part is +0
+          const int nq = vec ? C2 / 4 : C2;
+          for (int q = lane; q < nq; q += 64) {
+            if (vec) om4[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            else om[q] = 0.0f;
+          }
+        } else if (tab && vec && C <= 128) {
+          // Two-row bands of C/2 16-byte quads: a lane keeps the same four
+          // columns (its x entries stay in registers) across every band and
+          // reads only the two row entries per band.
+          const int QB = C >> 1, NBW = 64 / QB;
+          const bool ln = lane < NBW * QB;
+          const int k = ln ? lane % QB : 0, bs = lane / QB;
+          float4 ex[4];
+          bool br[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            if (e < per) {
-              if (tab) {
-                const float4 ex = tcol[j], ey = trow[i];
-                const int x0 = __float_as_int(ex.x), x1 = __float_as_int(ex.y);
-                const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
-                const float s = zn * sample4(ex, ey, U[y0 + x0], U[y1 + x0], U[y0 + x1],
-                                             U[y1 + x1]);
-                v[e] = axis4_dead(ex, ey) ? 0.0f : s;
-              } else {
+            const int pp = 4 * k + e;
+            br[e] = pp >= C;
+            ex[e] = axis4(tcol[br[e] ? pp - C : pp], 1);
+          }
+          for (int bb = 0; bb < QB; bb += NBW) {
+            const int b = bb + bs;
+            if (!ln || b >= QB) continue;
+            const float4 ey0 = axis4(trow[2 * b], 28), ey1 = axis4(trow[2 * b + 1], 28);
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float4 ey = br[e] ? ey1 : ey0;
+              const int x0 = __float_as_int(ex[e].x), x1 = __float_as_int(ex[e].y);
+              const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
+              const float sv = zn * sample4(ex[e], ey, U[y0 + x0], U[y1 + x0], U[y0 + x1],
+                                            U[y1 + x1]);
+              v[e] = axis4_dead(ex[e], ey) ? 0.0f : sv;
+            }
+            om4[b * QB + k] = make_float4(v[0], v[1], v[2], v[3]);
+          }
+        } else {  // general transform or odd C: per-pixel geometry, flat order
+          const int nq = vec ? C2 / 4 : C2;
+          const int per = vec ? 4 : 1;
+          for (int q = lane; q < nq; q += 64) {
+            float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            int pix = q * per;
+            int i = pix / C, j = pix - (pix / C) * C;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              if (e < per) {
                 const Tap t = stn_tap(&sth[m][6], 28, 28, mog_linspace(j, C), mog_linspace(i, C));
                 v[e] = t.dead ? 0.0f : zn * tap_value(t, U);
+                if (++j == C) { j = 0; ++i; }
               }
-              if (++j == C) { j = 0; ++i; }
             }
+            if (vec) om4[q] = make_float4(v[0], v[1], v[2], v[3]);
+            else om[q] = v[0];
           }
         }
-        if (vec)
-          reinterpret_cast<float4*>(om)[q] = make_float4(v[0], v[1], v[2], v[3]);
-        else
-          om[q] = v[0];
       }
+      __syncthreads();
     }
   }
   if (p.tstamp) {
@@ -572,7 +629,7 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
     (void)hipStreamSynchronize(mog_stream(stream));
     (void)hipMemcpy(h.data(), tbuf, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
     static const char* names[10] = {"stn_read", "L1", "L2", "mu_lv", "sample",
-                                    "g1", "g2", "go", "flush_r+tables", "write"};
+                                    "g1", "g2", "go", "-", "write"};
     double acc[11] = {0};
     long long t0 = h[0], t1 = h[10];
     for (unsigned b = 0; b < nblk; ++b) {
