@@ -70,6 +70,53 @@ def roofline(events, B):
             "avg_launch_us": avg * 1e6}
 
 
+def fused_step_roofline(batch: int, launches: int, dev):
+    """North-star measurement (BASELINE.json): the fused STN-read -> glimpse VAE
+    -> STN-write step kernel alone at `batch` images on this GPU, inputs
+    resident in HBM (theta / masks from one forward pass of a bf16 model on
+    the same synthetic canvases).  Timed with HIP events on the stream the
+    kernel is launched on; algorithmic bytes per image-step = 30,024
+    (SURVEY.md §8 D.3)."""
+    from mog_air.air_model import AIRModel
+    m = AIRModel(max_steps=3, cnn=False, train=True, device=dev, precision="bf16",
+                 scale_prior_variance=0.05, z_pres_prior_log_odds=-0.01,
+                 scope="roofline%d" % batch, seed=77, noise_seed=78)
+    x, k = synthetic(batch, 4321)
+    X = torch.from_numpy(x).to(dev)
+    K = torch.from_numpy(k).to(dev)
+    m.infer(X, K)
+    ws = m._ws
+    for t in range(3):
+        m._step_fused(X, ws, t, 0.3)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    evs = []
+    for i in range(launches):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        m._step_fused(X, ws, i % 3, 0.3)
+        e1.record(s)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    durs = [a.elapsed_time(b) * 1e-3 for a, b in evs]
+    avg = sum(durs) / len(durs)
+    achieved = batch * 30024 / 1e9 / avg
+    traffic = None
+    try:
+        with open(PMC_SUMMARY) as f:
+            traffic = json.load(f).get("stn_vae_step_b%d" % batch, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    out = {"kernel": "stn_vae_step", "batch": batch, "bound": "hbm", "achieved": achieved,
+           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+           "traffic": traffic, "launches": launches, "avg_launch_us": avg * 1e6,
+           "algorithmic_bytes_per_launch": batch * 30024}
+    del m, ws
+    torch.cuda.empty_cache()
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -80,6 +127,9 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--roofline-batch", type=int, default=65536,
+                    help="batch of the stand-alone fused-step roofline run (0: skip)")
+    ap.add_argument("--roofline-launches", type=int, default=30)
     return ap.parse_args()
 
 
@@ -192,6 +242,9 @@ def main():
                        "parallelism": f"dp{world}", "loss_last": loss},
             "roofline": roof,
         }
+        if args.roofline_batch > 0 and world == 1 and args.precision == "bf16":
+            out["fused_step_roofline"] = fused_step_roofline(args.roofline_batch,
+                                                             args.roofline_launches, dev)
         if args.cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out))

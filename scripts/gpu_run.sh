@@ -24,8 +24,8 @@ for step in "$@"; do
     benchq) run bench 300 python bench.py --steps 10 --warmup 3 --cpu-baseline 0 ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 2 --cpu-baseline 0 ;;
     pmc) rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
-         run pmcf 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 3 --warmup 1 --cpu-baseline 0
-         run pmcw 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 3 --warmup 1 --cpu-baseline 0 ;;
+         run pmcf 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --roofline-launches 3
+         run pmcw 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --roofline-launches 3 ;;
     *) run custom 600 bash -c "$step" ;;
   esac
 done

@@ -34,9 +34,10 @@ def load(d, counter):
     return rows
 
 
-def per_kernel(rows, symbol):
+def per_kernel(rows, symbol, grid=None):
     vals = [(int(r["Dispatch_Id"]), float(r["Counter_Value"])) for r in rows
-            if symbol in r["Kernel_Name"]]
+            if symbol in r["Kernel_Name"]
+            and (grid is None or int(float(r.get("Grid_Size", -1))) == grid)]
     return sorted(vals)
 
 
@@ -47,8 +48,14 @@ def main():
     res = {"_note": "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024, "
                     "gfx950 FETCH_SIZE halving corrected; averaged over the largest-fetch "
                     "dispatch of the tagged kernel symbol per train step"}
-    for tag, sym in TAGS.items():
-        fv, wv = per_kernel(fetch, sym), per_kernel(write, sym)
+    jobs = [(tag, sym, None) for tag, sym in TAGS.items()]
+    # the fused step kernel runs at the bench batch (8192: 256 workgroups of
+    # 512 threads) and in the stand-alone north-star roofline run (65,536)
+    jobs = [j for j in jobs if j[0] != "stn_vae_step"] + [
+        ("stn_vae_step", "stn_vae_step", 8192 // 32 * 512),
+        ("stn_vae_step_b65536", "stn_vae_step", 65536 // 32 * 512)]
+    for tag, sym, grid in jobs:
+        fv, wv = per_kernel(fetch, sym, grid), per_kernel(write, sym, grid)
         if not fv or not wv:
             continue
         fmax = max(v for _, v in fv)
@@ -62,7 +69,7 @@ def main():
         wsel = [wmap.get(i) for i in fids if wmap.get(i) is not None] or wsel
         fk = sum(fsel) / len(fsel)
         wk = sum(wsel) / len(wsel)
-        res[tag] = {"kernel_symbol": sym, "fetch_kib": fk, "write_kib": wk,
+        res[tag] = {"kernel_symbol": sym, "grid_threads": grid, "fetch_kib": fk, "write_kib": wk,
                     "dispatches": len(fsel),
                     "hbm_bytes_per_launch": (2.0 * fk + wk) * 1024.0}
     os.makedirs(os.path.dirname(out), exist_ok=True)
