@@ -195,6 +195,17 @@ int mog_clip_adam(float* params, float* grads, float* m, float* v, const long* o
                   int nblocks, float* sumsq, float clip, float lr_t, float beta1, float beta2,
                   float eps, void* stream);
 
+/* ---- generation loop prior draws (air_model.py:1001-1146, vae.py:51-86) --
+ * Per image i < G: s = sigmoid(s_pm + eps_scale[i] sqrt(exp(s_plv))),
+ * (tx, ty) = tanh(h_pm + eps_shift[i][:] sqrt(exp(h_plv))), theta_back[i] =
+ * [[1/s, 0, -tx/s], [0, 1/s, -ty/s]]; per latent element z = v_pm + eps_z
+ * sqrt(exp(v_plv)).  Replaces the scale / shift / rec_sample scopes of
+ * _create_generation (:1013-1035) and vae_generation (vae.py:63-66). */
+int mog_generation_prior(int G, int Z, float s_pm, float s_plv, float h_pm, float h_plv,
+                         float v_pm, float v_plv, const float* eps_scale, const float* eps_shift,
+                         const float* eps_z, float* theta_back, float* scale, float* shift,
+                         float* z, void* stream);
+
 /* ---- noise (tf.random_normal / random_uniform sites, perf mode) --------- */
 int mog_rng_fill(float* out, long n, unsigned long long seed, unsigned long long offset,
                  int normal, void* stream);

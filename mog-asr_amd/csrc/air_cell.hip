@@ -510,6 +510,31 @@ __global__ __launch_bounds__(256) void add_kernel(const float* a, const float* b
   if (i < n) out[i] = a[i] + b[i];
 }
 
+// Generation prior draws (air_model.py:1013-1035 via _sample_from_mvn
+// :186-192; vae.py:63-66): per image the glimpse scale / shift and the
+// backward transform, per latent element z = prior mean + eps sqrt(exp(lv)).
+__global__ __launch_bounds__(256) void gen_prior_kernel(int G, int Z, float s_pm, float s_plv,
+                                                        float h_pm, float h_plv, float v_pm,
+                                                        float v_plv, const float* eps_scale,
+                                                        const float* eps_shift,
+                                                        const float* eps_z, float* theta_back,
+                                                        float* scale, float* shift, float* z) {
+#pragma clang fp contract(off)
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < G * Z) z[i] = v_pm + eps_z[i] * sqrtf(mog_expf(v_plv));
+  if (i >= G) return;
+  const float s = mog_sigmoidf(s_pm + eps_scale[i] * sqrtf(mog_expf(s_plv)));
+  const float hv = sqrtf(mog_expf(h_plv));
+  const float tx = mog_tanhf(h_pm + eps_shift[2 * i] * hv);
+  const float ty = mog_tanhf(h_pm + eps_shift[2 * i + 1] * hv);
+  float* tb = theta_back + (size_t)i * 6;
+  tb[0] = 1.0f / s; tb[1] = 0.0f; tb[2] = -tx / s;
+  tb[3] = 0.0f; tb[4] = 1.0f / s; tb[5] = -ty / s;
+  scale[i] = s;
+  shift[2 * i] = tx;
+  shift[2 * i + 1] = ty;
+}
+
 }  // namespace
 
 // ============================================================== C ABI ======
@@ -671,5 +696,18 @@ extern "C" int mog_add(const float* a, const float* b, float* out, long n, void*
   MOG_CHECK_ARG(a && b && out && n >= 0);
   if (n == 0) return 0;
   add_kernel<<<mog_cdiv(n, 256), 256, 0, mog_stream(stream)>>>(a, b, out, n);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_generation_prior(int G, int Z, float s_pm, float s_plv, float h_pm,
+                                    float h_plv, float v_pm, float v_plv, const float* eps_scale,
+                                    const float* eps_shift, const float* eps_z, float* theta_back,
+                                    float* scale, float* shift, float* z, void* stream) {
+  MOG_CHECK_ARG(G >= 0 && Z > 0 && eps_scale && eps_shift && eps_z && theta_back && scale &&
+                shift && z);
+  if (G == 0) return 0;
+  gen_prior_kernel<<<mog_cdiv((long)G * Z, 256), 256, 0, mog_stream(stream)>>>(
+      G, Z, s_pm, s_plv, h_pm, h_plv, v_pm, v_plv, eps_scale, eps_shift, eps_z, theta_back, scale,
+      shift, z);
   MOG_LAUNCH_RET();
 }

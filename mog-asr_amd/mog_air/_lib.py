@@ -46,6 +46,7 @@ _SIGS = {
     "mog_optim_chunk_elems": [],
     "mog_clip_adam": [P, P, P, P, P, P, P, P, I, P, F, F, F, F, F, P],
     "mog_rng_fill": [P, L, ULL, ULL, I, P],
+    "mog_generation_prior": [I, I, F, F, F, F, F, F, P, P, P, P, P, P, P, P],
 }
 
 _lib = None

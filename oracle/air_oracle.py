@@ -302,6 +302,42 @@ def forward(cfg: AirConfig, params: Dict[str, np.ndarray], noise: Dict[str, np.n
     C2, W2 = cfg.canvas_size ** 2, cfg.windows_size ** 2
     Z, H = cfg.vae_latent_dimensions, cfg.rnn_units
     images = np.ascontiguousarray(images, np.float32).reshape(B, C2)
+    c, mo = _make_cfg(cfg, z_pres_prior_log_odds)
+    specs = param_specs(cfg)
+    plist = [np.ascontiguousarray(params[n], np.float32) for n, _ in specs]
+    for (n, shp), a in zip(specs, plist):
+        assert a.shape == tuple(shp), (n, a.shape, shp)
+    parr = (_FP * len(plist))(*[_ptr(a) for a in plist])
+    nzk = {k: np.ascontiguousarray(v, np.float32) for k, v in noise.items()}
+    nz = _Noise(*[_ptr(nzk[k]) for k in ("eps_scale", "eps_shift", "eps_z", "eps_x", "u")])
+    return _run_forward(lib, cfg, c, parr, nz, images, targets, B, T, C2, W2, Z, H, mo)
+
+
+def generate(cfg: AirConfig, params: Dict[str, np.ndarray], noise: Dict[str, np.ndarray],
+             batch: int, n_steps: int) -> Dict[str, np.ndarray]:
+    """Generation loop (air_model.py:1001-1146): canvas [G, C2] and the
+    backward transforms [n_steps, G, 6] for injected prior noise
+    (eps_scale [T,G], eps_shift [T,G,2], eps_z [T,G,Z], eps_x [T,G,W2])."""
+    lib = _load()
+    c, _ = _make_cfg(cfg, None)
+    specs = param_specs(cfg)
+    plist = [np.ascontiguousarray(params[n], np.float32) for n, _ in specs]
+    parr = (_FP * len(plist))(*[_ptr(a) for a in plist])
+    nzk = {k: np.ascontiguousarray(noise[k], np.float32)
+           for k in ("eps_scale", "eps_shift", "eps_z", "eps_x")}
+    dummy = np.zeros(1, np.float32)
+    nz = _Noise(*[_ptr(nzk[k]) for k in ("eps_scale", "eps_shift", "eps_z", "eps_x")] +
+                [_ptr(dummy)])
+    canvas = np.zeros((batch, cfg.canvas_size ** 2), np.float32)
+    st = np.zeros((n_steps, batch, 6), np.float32)
+    lib.oracle_air_generate(ctypes.byref(c), parr, ctypes.byref(nz), ctypes.c_int(batch),
+                            ctypes.c_int(n_steps), _ptr(canvas), _ptr(st))
+    return {"canvas": canvas, "st_back": st, "digits": np.full(batch, n_steps, np.int32)}
+
+
+def _make_cfg(cfg: AirConfig, z_pres_prior_log_odds):
+    B, T = cfg.batch, cfg.max_steps
+    Z, H = cfg.vae_latent_dimensions, cfg.rnn_units
     c = _Cfg()
     c.B, c.C, c.W, c.max_steps, c.H, c.Z = B, cfg.canvas_size, cfg.windows_size, T, H, Z
     c.R1, c.R2 = cfg.vae_recognition_units
@@ -325,13 +361,10 @@ def forward(cfg: AirConfig, params: Dict[str, np.ndarray], noise: Dict[str, np.n
         c.marginal_objective = _ptr(mo)
     else:
         c.use_num_prior = 0
-    specs = param_specs(cfg)
-    plist = [np.ascontiguousarray(params[n], np.float32) for n, _ in specs]
-    for (n, shp), a in zip(specs, plist):
-        assert a.shape == tuple(shp), (n, a.shape, shp)
-    parr = (_FP * len(plist))(*[_ptr(a) for a in plist])
-    nzk = {k: np.ascontiguousarray(v, np.float32) for k, v in noise.items()}
-    nz = _Noise(*[_ptr(nzk[k]) for k in ("eps_scale", "eps_shift", "eps_z", "eps_x", "u")])
+    return c, mo
+
+
+def _run_forward(lib, cfg, c, parr, nz, images, targets, B, T, C2, W2, Z, H, mo):
     shapes = {
         "scale": (T, B), "shift": (T, B, 2), "st_back": (T, B, 6), "window": (T, B, W2),
         "latent": (T, B, Z), "z_pres_prob": (T, B), "z_pres_kl": (T, B),

@@ -378,6 +378,51 @@ int oracle_air_forward(const AirCfg* cfg, const float* const* P, const AirNoise*
 }
 
 /* vectorised wrappers so tests can pin mog_math.h against libm */
+/* Generation loop (air_model.py:1001-1146, vae.py:51-86), test model: for
+ * n_steps steps, scale ~ sigmoid(N(scale prior)), shift ~ tanh(N(shift
+ * prior)) (_sample_from_mvn, :186-192), z ~ N(vae prior), r = sigmoid(decoder
+ * + std eps_x), and the canvas adds every step's STN-written window
+ * unweighted (the stopping sum stays 0 < thr, :1085-1097).  Noise slots
+ * eps_scale [T,G], eps_shift [T,G,2], eps_z [T,G,Z], eps_x [T,G,W*W]. */
+int oracle_air_generate(const AirCfg* cfg, const float* const* P, const AirNoise* nz, int G,
+                        int n_steps, float* canvas, float* st_back) {
+  const int C = cfg->C, W = cfg->W, C2 = C * C, W2 = W * W, Z = cfg->Z;
+  float* z = (float*)calloc((size_t)G * Z, 4);
+  float* d1 = (float*)calloc((size_t)G * cfg->G1, 4);
+  float* d2 = (float*)calloc((size_t)G * cfg->G2, 4);
+  float* m = (float*)calloc((size_t)G * W2, 4);
+  float* wr = (float*)calloc((size_t)C2, 4);
+  memset(canvas, 0, (size_t)G * C2 * 4);
+  for (int step = 0; step < n_steps; ++step) {
+    const float svar = mog_expf(cfg->scale_prior_logvar);
+    const float hvar = mog_expf(cfg->shift_prior_logvar);
+    const float zvar = mog_expf(cfg->vae_prior_logvar);
+    for (int i = 0; i < G * Z; ++i)
+      z[i] = cfg->vae_prior_mean + nz->eps_z[(size_t)step * G * Z + i] * sqrtf(zvar);
+    dense(z, G, Z, P[P_G1_W], P[P_G1_B], cfg->G1, d1);
+    for (int i = 0; i < G * cfg->G1; ++i) d1[i] = mog_softplusf(d1[i]);
+    dense(d1, G, cfg->G1, P[P_G2_W], P[P_G2_B], cfg->G2, d2);
+    for (int i = 0; i < G * cfg->G2; ++i) d2[i] = mog_softplusf(d2[i]);
+    dense(d2, G, cfg->G2, P[P_GO_W], P[P_GO_B], W2, m);
+    for (int i = 0; i < G * W2; ++i)
+      m[i] = mog_sigmoidf(m[i] + nz->eps_x[(size_t)step * G * W2 + i] * cfg->lik_std);
+    for (int b = 0; b < G; ++b) {
+      const size_t tb = (size_t)step * G + b;
+      const float s = mog_sigmoidf(cfg->scale_prior_mean + nz->eps_scale[tb] * sqrtf(svar));
+      const float tx = mog_tanhf(cfg->shift_prior_mean + nz->eps_shift[tb * 2] * sqrtf(hvar));
+      const float ty = mog_tanhf(cfg->shift_prior_mean + nz->eps_shift[tb * 2 + 1] * sqrtf(hvar));
+      float* stb = st_back + tb * 6;
+      stb[0] = 1.0f / s; stb[1] = 0.0f; stb[2] = -tx / s;
+      stb[3] = 0.0f; stb[4] = 1.0f / s; stb[5] = -ty / s;
+      oracle_stn(m + (size_t)b * W2, W, W, stb, C, C, wr);
+      float* cv = canvas + (size_t)b * C2;
+      for (int p = 0; p < C2; ++p) cv[p] = cv[p] + wr[p];
+    }
+  }
+  free(z); free(d1); free(d2); free(m); free(wr);
+  return n_steps;
+}
+
 void oracle_math_vec(int fn, const float* x, float* y, int n) {
   for (int i = 0; i < n; ++i) {
     switch (fn) {
