@@ -144,6 +144,18 @@ MOG_HD float mog_softplusf(float x) {
   return mog_logf(ex + 1.0f);
 }
 
+/* log1p(x) for x > -1: log(u) * x / (u - 1) with u = 1 + x (exact when
+ * u == 1), the rounding-compensated form; used by the ASR sigmoid
+ * cross-entropy (tf.nn.sigmoid_cross_entropy_with_logits: log1p(exp(-|x|))). */
+MOG_HD float mog_log1pf(float x) {
+  MOG_NOCONTRACT
+  if (x != x) return x;
+  const float u = 1.0f + x;
+  if (u == 1.0f) return x;
+  if (u == mog_bits2f(0x7f800000u)) return u;
+  return mog_logf(u) * (x / (u - 1.0f));
+}
+
 /* d softplus / dx = sigmoid(x), the gradient TF uses (SoftplusGrad). */
 MOG_HD float mog_softplus_grad_from_pre(float x) {
   MOG_NOCONTRACT

@@ -431,6 +431,7 @@ void oracle_math_vec(int fn, const float* x, float* y, int n) {
       case 2: y[i] = mog_expm1f(x[i]); break;
       case 3: y[i] = mog_tanhf(x[i]); break;
       case 4: y[i] = mog_sigmoidf(x[i]); break;
+      case 6: y[i] = mog_log1pf(x[i]); break;
       default: y[i] = mog_softplusf(x[i]); break;
     }
   }

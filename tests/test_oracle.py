@@ -28,6 +28,7 @@ def _ulp_err(got, ref):
     (2, -10.0, 10.0, np.expm1, 3.0),
     (3, -10.0, 10.0, np.tanh, 3.0),
     (4, -30.0, 30.0, lambda x: 1.0 / (1.0 + np.exp(-x)), 3.0),
+    (6, 0.0, 1.0, np.log1p, 3.0),
 ])
 def test_math_spec_vs_libm(fn, lo, hi, ref, tol):
     lib = ao._load()
