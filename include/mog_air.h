@@ -206,6 +206,62 @@ int mog_generation_prior(int G, int Z, float s_pm, float s_plv, float h_pm, floa
                          const float* eps_z, float* theta_back, float* scale, float* shift,
                          float* z, void* stream);
 
+/* ---- AIR-ASR cells and structural losses (air_number_bbox_location.py) ----
+ * Record layout rec[step][28][B]: sm0 sm1 slv0 slv1 sl0 sl1 cm clv cl s tx ty
+ * gsm0 gsm1 gslv0 gslv1 plo lo y z act_old act live zkl skl shkl prn zprob
+ * (zkl / skl / shkl masked as the reference's tf.where, prn live-gated).
+ * w[20] (TF [in,out] layout): inf_shift dense_1 W,b, dense_3 W,b; inf_scale
+ * dense W,b [258,64], dense_1 W,b [66,1], dense_2 W,b, dense_3 W,b; gen_shift
+ * dense_1 W,b, dense_3 W,b; z_pres prior dense_1 W,b; z_pres log-odds
+ * dense_1 W,b.  hid[8] [B,64]: post-relu hidden of inf_shift m / v, z_pres
+ * log-odds, gen_shift m / v, z_pres prior (null with fix_steps >= 0), and the
+ * inf_scale m / v chains over h (finished in place: + shift latent terms,
+ * bias, relu).  gammas[8] = num, margin, element, bbox, size, area, area_min,
+ * area_max.  T <= 8 steps, <= 8 allowed counts. */
+/* U rows [z (Z) | ss (3) | h (H) | 0] of the two LSTMCell inputs (:403-412,
+ * :457-463); null sources read as zeros. */
+int mog_asr_pack(int B, int Z, int H, int ld, const float* z, const float* ss, const float* h,
+                 float* out, void* stream);
+/* dz = dU[:, :Z] + dUg[:, :Z]; dss likewise; dh += dU[:, Z+3:]; dhg += dUg[:, Z+3:] */
+int mog_asr_unpack(int B, int Z, int H, int ld, const float* dU, const float* dUg, float* dz,
+                   float* dss, float* dh, float* dhg, void* stream);
+/* heads, latents, theta, concrete z_pres, KLs, entropy, stop / counts /
+ * live flag of one step (:414-772) */
+int mog_asr_step_forward(int B, int step, int train, int fix_steps, float thr, float temperature,
+                         float scale_prior_mean, float scale_prior_var, float scale_prior_logvar,
+                         float gamma_num, const float* const* w, float* const* hid,
+                         const float* eps_shift, const float* eps_scale, const float* u,
+                         float* stop, int* digits, int* live, float* rec, float* theta_fwd,
+                         float* theta_back, float* ss, float* scale, float* shift, float* zprob,
+                         float* zmask, float* zval, float* zc, void* stream);
+/* per image KL sums (klsum, the reconstruction kernel's runloss), pr_loss
+ * and its area / out / size / overlap terms over the executed steps; zsum[t]
+ * = sum_b z_pres_prob (to be all-reduced over ranks for the margin loss)
+ * (:917-935, :1017-1069).  rec [T][28][B], vkl / zmask [T][B]. */
+int mog_asr_terms(int B, int T, int C, int nc, const int* cons, const float* gammas,
+                  const float* rec, const float* vkl, const float* zmask, const int* live,
+                  float* klsum, float* pr, float* area, float* out, float* size, float* overlap,
+                  float* zsum, void* stream);
+/* loss[b] = (loss[b] + pr[b]) + element[b]; margin[0] (:970-1015, :1078-1079);
+ * cons / gammas are HOST arrays */
+int mog_asr_finalize(int B, int T, int C, int nc, const int* cons, const float* gammas,
+                     float inv_batch_global, const float* rec, const int* live, const float* zsum,
+                     const float* pr, float* loss, float* element, float* margin, void* stream);
+/* dreg [T][4][B]: d loss / d (s, tx, ty, lo) from the regularisers */
+int mog_asr_terms_backward(int B, int T, int C, int nc, const int* cons, const float* gammas,
+                           float grad_scale, float inv_batch_global, const float* rec,
+                           const int* live, const float* zsum, float* dreg, void* stream);
+/* one step's backward of mog_asr_step_forward: douts [B][12] = d(sm0 sm1 slv0
+ * slv1 lo gsm0 gsm1 gslv0 gslv1 plo cm clv), dpre[8] [B,64] hidden-layer
+ * pre-activation gradients; dss [B,3] = gradient reaching this step's latents
+ * from the next step's LSTM inputs (or null) */
+int mog_asr_step_backward(int B, int train, int fix_steps, float temperature,
+                          float scale_prior_mean, float scale_prior_var, float grad_scale,
+                          const float* const* w, float* const* hid, const float* rec,
+                          const float* eps_shift, const float* eps_scale, const float* dtheta_fwd,
+                          const float* dtheta_back, const float* dot, const float* dreg,
+                          const float* dss, float* douts, float* const* dpre, void* stream);
+
 /* ---- noise (tf.random_normal / random_uniform sites, perf mode) --------- */
 int mog_rng_fill(float* out, long n, unsigned long long seed, unsigned long long offset,
                  int normal, void* stream);

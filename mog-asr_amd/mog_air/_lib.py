@@ -47,6 +47,14 @@ _SIGS = {
     "mog_clip_adam": [P, P, P, P, P, P, P, P, I, P, F, F, F, F, F, P],
     "mog_rng_fill": [P, L, ULL, ULL, I, P],
     "mog_generation_prior": [I, I, F, F, F, F, F, F, P, P, P, P, P, P, P, P],
+    "mog_asr_pack": [I, I, I, I, P, P, P, P, P],
+    "mog_asr_unpack": [I, I, I, I, P, P, P, P, P, P, P],
+    "mog_asr_step_forward": [I, I, I, I, F, F, F, F, F, F, P, P, P, P, P, P, P, P, P, P, P, P,
+                             P, P, P, P, P, P, P],
+    "mog_asr_terms": [I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "mog_asr_finalize": [I, I, I, I, P, P, F, P, P, P, P, P, P, P, P],
+    "mog_asr_terms_backward": [I, I, I, I, P, P, F, F, P, P, P, P, P],
+    "mog_asr_step_backward": [I, I, I, F, F, F, F, P, P, P, P, P, P, P, P, P, P, P, P, P],
 }
 
 _lib = None

@@ -310,11 +310,13 @@ class AIRModel:
             self._ws = _Workspace(self, B)
         return self._ws
 
+    _SCOPE_PREFIX = "air/rnn/"  # variable scope of the loop body (air_model.py:127,812)
+
     def _P(self, name):
-        return self.params.view("air/rnn/" + name)
+        return self.params.view(self._SCOPE_PREFIX + name)
 
     def _G(self, name):
-        return self.params.g("air/rnn/" + name)
+        return self.params.g(self._SCOPE_PREFIX + name)
 
     _HEADS = ("scale/mean", "scale/log_variance", "shift/mean", "shift/log_variance",
               "z_pres/log_odds")
@@ -539,6 +541,11 @@ class AIRModel:
                   dp(ws.z[t]), dp(zb), ldzb, dp(ws.zmask[t]), dp(ws.runloss), dp(ws.vkl[t]),
                   stream_ptr())
 
+    def _dz_hook(self, ws, t):
+        """Extra gradient reaching the latent z of step t before the sample
+        backward (none in AIR; the ASR model adds the next step's LSTM-input
+        gradient here)."""
+
     def _vae_backward_fp32(self, ws, t, gscale):
         B = ws.B
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
@@ -550,6 +557,7 @@ class AIRModel:
         gemm([ws.dd2[t]], [vw["generative_2"]], [ws.dd1[t]], B, G1, G2, G2, G2, G1,
              transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d1pre[t]], ldaux=G1)
         gemm([ws.dd1[t]], [vw["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z, transB=True)
+        self._dz_hook(ws, t)
         _lib.call("mog_vae_sample_backward", B, Z, float(self.vae_prior_mean),
                   float(self.vae_prior_variance), float(gscale), dp(ws.mu[t]), dp(ws.lv[t]),
                   dp(ws.eps_z[t]), dp(ws.dz), dp(ws.zmask[t]), dp(ws.dmu[t]), dp(ws.dlv[t]),
@@ -656,6 +664,7 @@ class AIRModel:
                   epi=BF_SOFTPLUS_BWD, aux=[ws.d1b[t]], ldaux=G1)
         gemm_bf16([ws.dd1b[t]], [wn["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z,
                   epi=BF_STORE)
+        self._dz_hook(ws, t)
         _lib.call("mog_vae_sample_backward", B, Z, float(self.vae_prior_mean),
                   float(self.vae_prior_variance), float(gscale), dp(ws.mu[t]), dp(ws.lv[t]),
                   dp(ws.eps_z[t]), dp(ws.dz), dp(ws.zmask[t]), None, None, dp(ws.dmub[t]),
@@ -707,6 +716,19 @@ class AIRModel:
         gemm(X, dY, out, M, N, K, lda, ldb, N, transA=True, epi=EPI_ATOMIC,
              splitk=splitk, colsum=bias_out)
 
+    def _vae_weight_grads_fp32(self, ws):
+        TB = ws.B * self.max_steps
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
+        gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
+        self._dw(ws.g, ws.da1, g("recognition_1"), TB, W2, R1, W2, R1, gb("recognition_1"))
+        self._dw(ws.a1, ws.da2, g("recognition_2"), TB, R1, R2, R1, R2, gb("recognition_2"))
+        self._dw(ws.a2, ws.dmu, g("rec_mean"), TB, R2, Z, R2, Z, gb("rec_mean"))
+        self._dw(ws.a2, ws.dlv, g("rec_log_variance"), TB, R2, Z, R2, Z, gb("rec_log_variance"))
+        self._dw(ws.z, ws.dd1, g("generative_1"), TB, Z, G1, Z, G1, gb("generative_1"))
+        self._dw(ws.d1, ws.dd2, g("generative_2"), TB, G1, G2, G1, G2, gb("generative_2"))
+        self._dw(ws.d2, ws.dm, g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
+
     def _weight_grads(self, X, ws):
         B, T, H = ws.B, self.max_steps, self.rnn_units
         C2, W2, Z = self.C2, self.W2, self.vae_latent_dimensions
@@ -717,16 +739,7 @@ class AIRModel:
         if self.precision == "bf16":
             self._vae_weight_grads_bf16(ws)
         else:
-            g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
-            gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
-            self._dw(ws.g, ws.da1, g("recognition_1"), TB, W2, R1, W2, R1, gb("recognition_1"))
-            self._dw(ws.a1, ws.da2, g("recognition_2"), TB, R1, R2, R1, R2, gb("recognition_2"))
-            self._dw(ws.a2, ws.dmu, g("rec_mean"), TB, R2, Z, R2, Z, gb("rec_mean"))
-            self._dw(ws.a2, ws.dlv, g("rec_log_variance"), TB, R2, Z, R2, Z,
-                     gb("rec_log_variance"))
-            self._dw(ws.z, ws.dd1, g("generative_1"), TB, Z, G1, Z, G1, gb("generative_1"))
-            self._dw(ws.d1, ws.dd2, g("generative_2"), TB, G1, G2, G1, G2, gb("generative_2"))
-            self._dw(ws.d2, ws.dm, g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
+            self._vae_weight_grads_fp32(ws)
         heads = list(enumerate(self._HEADS))
         self._dw([ws.h] * 5, [ws.dhid[zi] for zi, _ in heads],
                  [self._G(h + "/hidden/weights") for _, h in heads], TB, H, HS, H, HS,

@@ -1,0 +1,541 @@
+"""AIRModel of AIR-ASR — drop-in host object for the reference's
+air/air_number_bbox_location.py:13-1361 (the model train_air_pr.py builds),
+running on MI355X HIP kernels: the inference and generative LSTMCells (fp32
+MFMA GEMMs with the loop-invariant x-projection hoisted), the heads and the
+structural regularisers (asr_cell.hip), and the glimpse path shared with the
+AIR model (STN read, glimpse VAE — fused bf16 step kernel or fp32 GEMMs —,
+STN write, reconstruction loss).
+
+Reference surface kept (air_number_bbox_location.py:15-56, train_air_pr.py:
+160-213): the constructor keyword arguments (cnn=True and
+fix_scale_distribution=False are rejected: the entry point uses neither), the
+train / test pair sharing one scope via ``reuse``, the loss of :1078-1079
+with every regulariser, and the result attributes (``loss, accuracy,
+mse_loss, rec_num_digits, rec_scales, rec_shifts, rec_st_back, rec_windows,
+rec_latents, z_pres_probs, reconstruction, log_variables``).
+
+Loop: max_steps iterations on the device, the data-dependent predicate
+(:386-390) folded into a live flag per step; losses, counts and gradients
+equal the early exit.  The KL records are summed per type over the executed
+steps at the end, as the reference's TensorArrays are (:917-923).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib, ops
+from .air_model import AIRModel as _AirBase
+from .air_model import _SCOPES, _Workspace, _f32log, annealed_value
+from .ops import EPI_RELU, EPI_STORE, dp, gemm, stream_ptr
+from .params import ParamStore
+
+# asr_cell.hip record slots
+Q = {n: i for i, n in enumerate(
+    ("sm0 sm1 slv0 slv1 sl0 sl1 cm clv cl s tx ty gsm0 gsm1 gslv0 gslv1 plo lo y z act_old act "
+     "live zkl skl shkl prn zprob").split())}
+NQ = 28
+D_N = 12
+LU = 312  # packed LSTM-input row: z (50) | latents (3) | h (256) | pad (3)
+
+ROOT = "air/air_model/"
+
+
+def asr_param_specs(C2, H, W2, R, G, Z, HS, HZ):
+    """(TF variable name, shape): inference / generative LSTMCell kernels on
+    the concatenated inputs, tf.layers.dense heads numbered in creation order
+    within their scopes (:414-474, :590-609), the glimpse VAE (vae.py)."""
+    p = ROOT
+    specs = [(p + "infer_rnn_running/kernel", (C2 + Z + 3 + H, 4 * H)),
+             (p + "infer_rnn_running/bias", (4 * H,)),
+             (p + "gen_rnn_running/kernel", (Z + 3 + H, 4 * H)),
+             (p + "gen_rnn_running/bias", (4 * H,))]
+
+    def four(scope, kin, kout, extra):
+        return [(p + scope + "/dense/kernel", (kin, HS)), (p + scope + "/dense/bias", (HS,)),
+                (p + scope + "/dense_1/kernel", (HS + extra, kout)),
+                (p + scope + "/dense_1/bias", (kout,)),
+                (p + scope + "/dense_2/kernel", (kin, HS)), (p + scope + "/dense_2/bias", (HS,)),
+                (p + scope + "/dense_3/kernel", (HS + extra, kout)),
+                (p + scope + "/dense_3/bias", (kout,))]
+
+    specs += four("inf_shift", H, 2, 0) + four("inf_scale", H + 2, 1, 2) + four("gen_shift", H, 2, 0)
+    for scope in ("z_pres/prior", "z_pres/log_odds"):
+        specs += [(p + scope + "/dense/kernel", (H, HZ)), (p + scope + "/dense/bias", (HZ,)),
+                  (p + scope + "/dense_1/kernel", (HZ, 1)), (p + scope + "/dense_1/bias", (1,))]
+    v = p + "vae/"
+    R1, R2 = R
+    G1, G2 = G
+    specs += [(v + "recognition_1/weights", (W2, R1)), (v + "recognition_1/biases", (R1,)),
+              (v + "recognition_2/weights", (R1, R2)), (v + "recognition_2/biases", (R2,)),
+              (v + "rec_mean/weights", (R2, Z)), (v + "rec_mean/biases", (Z,)),
+              (v + "rec_log_variance/weights", (R2, Z)), (v + "rec_log_variance/biases", (Z,)),
+              (v + "generative_1/weights", (Z, G1)), (v + "generative_1/biases", (G1,)),
+              (v + "generative_2/weights", (G1, G2)), (v + "generative_2/biases", (G2,)),
+              (v + "gen_mean/weights", (G2, W2)), (v + "gen_mean/biases", (W2,))]
+    return specs
+
+
+class _AsrWorkspace(_Workspace):
+    def __init__(self, m: "AIRModel", B: int):
+        super().__init__(m, B)
+        dev = m.device
+        T, H = m.max_steps, m.rnn_units
+        e = lambda *s: torch.empty(s, device=dev, dtype=torch.float32)  # noqa: E731
+        self.U, self.Ug = e(T, B, LU), e(T, B, LU)
+        self.Gg, self.cg, self.hg = e(T, B, 4 * H), e(T, B, H), e(T, B, H)
+        self.hid8 = e(8, T, B, 64)
+        self.arec = e(T, NQ, B)
+        self.ss = e(T, B, 3)
+        self.zc = e(T, B)
+        self.klsum, self.pr, self.element = e(B), e(B), e(B)
+        self.area, self.outl, self.size, self.over = e(B), e(B), e(B), e(B)
+        self.zsum = e(T)
+        self.margin = e(1)
+        self.cg_prev_zero = torch.zeros((B, H), device=dev, dtype=torch.float32)
+
+    def alloc_backward(self, m):
+        if self._bwd:
+            return
+        super().alloc_backward(m)
+        dev, B = m.device, self.B
+        T, H, Z = m.max_steps, m.rnn_units, m.vae_latent_dimensions
+        e = lambda *s: torch.empty(s, device=dev, dtype=torch.float32)  # noqa: E731
+        self.dreg = e(T, 4, B)
+        self.douts = e(T, B, D_N)
+        self.dpre = e(8, T, B, 64)
+        self.dhg = e(T, B, H)
+        self.dcg = e(2, B, H)
+        self.dGg = e(T, B, 4 * H)
+        self.dGgsum = e(B, 4 * H)
+        self.dU, self.dUg = e(B, LU), e(B, LU)
+        self.dz_carry, self.dss_carry = e(B, Z), e(B, 3)
+
+
+class AIRModel(_AirBase):
+    """See module docstring.  Extra keyword-only arguments as the AIR model
+    (device, seed, noise_seed, grad_world, precision, fused_step)."""
+
+    _SCOPE_PREFIX = ROOT
+
+    def __init__(self, input_images=None, target_num_digits=None, max_steps=3, max_digits=2,
+                 rnn_units=256, canvas_size=50, windows_size=28, vae_latent_dimensions=50,
+                 vae_recognition_units=(512, 256), vae_generative_units=(256, 512),
+                 fix_scale_distribution=True, vae_prior_mean=0.0, vae_prior_variance=1.0,
+                 vae_likelihood_std=0.3, scale_hidden_units=64, shift_hidden_units=64,
+                 z_pres_hidden_units=64, z_pres_prior_log_odds=-2.0, z_pres_temperature=1.0,
+                 stopping_threshold=0.99, learning_rate=1e-3, gradient_clipping_norm=100.0,
+                 cnn=True, cnn_filters=8, num_summary_images=60, train=False, reuse=False,
+                 scope="air", annealing_schedules=None, generation_batch_size=64,
+                 reuse_shift_scale_network=True, constrains_x_y=None, constrains_num=None,
+                 constrains_num_gamma=0.0, constrains_bbox_gamma=0.0, constrains_margin_gamma=0.0,
+                 constrains_num_element_gamma=0.0, constrains_sharesize_gamma=0.0,
+                 constrains_area_gamma=0.0, constrains_area_minmax=(0.0, 0.0), fix_steps=None, *,
+                 device=None, seed: int = 1235, noise_seed: int = 1235, grad_world: int = 1,
+                 precision: str = "fp32", fused_step: bool = True):
+        if cnn:
+            raise NotImplementedError("cnn=True is outside the hot-path scope (train_air_pr.py "
+                                      "uses cnn=False)")
+        if not fix_scale_distribution:
+            raise NotImplementedError("fix_scale_distribution=False (learned scale prior) is not "
+                                      "used by train_air_pr.py")
+        if not (scale_hidden_units == shift_hidden_units == z_pres_hidden_units == 64):
+            raise NotImplementedError("the ASR heads are compiled for 64 hidden units")
+        if rnn_units + vae_latent_dimensions + 3 > LU:
+            raise NotImplementedError("rnn_units + latent + 3 must fit the packed input row")
+        if max_steps > 8:
+            raise NotImplementedError("at most 8 loop steps (regulariser kernels)")
+        cons = list(constrains_num) if constrains_num is not None else [max_steps]
+        if not 1 <= len(cons) <= 8:
+            raise ValueError("1..8 allowed object counts")
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
+        self.precision = precision
+        self.fused_step = bool(fused_step) and precision == "bf16" and (
+            windows_size == 28 and tuple(vae_recognition_units) == (512, 256)
+            and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512))
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        if self.device.type != "cuda":
+            raise RuntimeError("AIRModel runs on a HIP device only (no CPU fallback)")
+        _lib.load()
+        self.input_images, self.target_num_digits = input_images, target_num_digits
+        self.max_steps, self.max_digits = int(max_steps), max_digits
+        self.rnn_units = int(rnn_units)
+        self.canvas_size, self.windows_size = int(canvas_size), int(windows_size)
+        self.C2, self.W2 = self.canvas_size ** 2, self.windows_size ** 2
+        self.vae_latent_dimensions = int(vae_latent_dimensions)
+        self.vae_recognition_units = tuple(vae_recognition_units)
+        self.vae_generative_units = tuple(vae_generative_units)
+        self.fix_scale_distribution = True
+        self.scale_prior_mean, self.scale_prior_variance = -1.0, 0.05  # :70-72
+        self.shift_prior_mean, self.shift_prior_variance = 0.0, 1.0    # generation only
+        self.vae_prior_mean, self.vae_prior_variance = vae_prior_mean, vae_prior_variance
+        self.vae_likelihood_std = vae_likelihood_std
+        self.scale_hidden_units = self.shift_hidden_units = self.z_pres_hidden_units = 64
+        self.z_pres_prior_log_odds = z_pres_prior_log_odds
+        self.z_pres_temperature = z_pres_temperature
+        self.stopping_threshold = stopping_threshold
+        self.learning_rate = learning_rate
+        self.gradient_clipping_norm = gradient_clipping_norm
+        self.num_summary_images = num_summary_images
+        self.train = bool(train)
+        self.scope = scope
+        self.annealing_schedules = dict(annealing_schedules or {})
+        self.generation_batch_size = generation_batch_size
+        self.fix_steps = fix_steps
+        self.constrains_num = cons
+        self.constrains_num_gamma = constrains_num_gamma
+        self.constrains_margin_gamma = constrains_margin_gamma
+        self.constrains_num_element_gamma = constrains_num_element_gamma
+        self.constrains_bbox_gamma = constrains_bbox_gamma
+        self.constrains_sharesize_gamma = constrains_sharesize_gamma
+        self.constrains_area_gamma = constrains_area_gamma
+        self.constrains_area_minmax = tuple(float(v) for v in constrains_area_minmax)
+        self.num_prior = None
+        self.marginal = None
+        self.noise_seed = int(noise_seed)
+        self.grad_world = int(grad_world)
+        self._noise_ctr = 0
+        self.scale_prior_log_variance = _f32log(self.scale_prior_variance)
+        self.shift_prior_log_variance = _f32log(self.shift_prior_variance)
+        self.vae_prior_log_variance = _f32log(vae_prior_variance)
+        specs = asr_param_specs(self.C2, self.rnn_units, self.W2, self.vae_recognition_units,
+                                self.vae_generative_units, self.vae_latent_dimensions, 64, 64)
+        key = "asr:" + scope
+        if reuse:
+            if key not in _SCOPES:
+                raise ValueError(f"reuse=True but scope {scope!r} has no variables yet")
+            self.params = _SCOPES[key]
+            if self.params.specs != specs:
+                raise ValueError("reused scope has different variable shapes")
+        else:
+            self.params = ParamStore(specs, self.device, seed=seed)
+            _SCOPES[key] = self.params
+        self._ws = None
+        self._last_T = None
+        self._outputs_ready = False
+        self._cons_arr = (ctypes.c_int * len(cons))(*cons)
+
+    # zsum_hook / live_hook: data-parallel collectives (parallel.attach)
+    zsum_hook = None
+    live_hook = None
+
+    def _workspace(self, B):
+        if self._ws is None or self._ws.B != B:
+            self._ws = _AsrWorkspace(self, B)
+        return self._ws
+
+    def _N(self, name):
+        return self.params.view(ROOT + name)
+
+    def _Ng(self, name):
+        return self.params.g(ROOT + name)
+
+    _OUT_W = ("inf_shift/dense_1", "inf_shift/dense_3", "inf_scale/dense", "inf_scale/dense_1",
+              "inf_scale/dense_2", "inf_scale/dense_3", "gen_shift/dense_1", "gen_shift/dense_3",
+              "z_pres/prior/dense_1", "z_pres/log_odds/dense_1")
+
+    def _w20(self):
+        ptrs = []
+        for n in self._OUT_W:
+            ptrs += [dp(self._N(n + "/kernel")), dp(self._N(n + "/bias"))]
+        return _lib.ptr_array(ptrs)
+
+    def _gammas(self):
+        g = [self.hyper("constrains_num_gamma"), self.hyper("constrains_margin_gamma"),
+             self.hyper("constrains_num_element_gamma"), self.hyper("constrains_bbox_gamma"),
+             self.hyper("constrains_sharesize_gamma"), self.hyper("constrains_area_gamma"),
+             self.constrains_area_minmax[0], self.constrains_area_minmax[1]]
+        return (ctypes.c_float * 8)(*g)
+
+    def _fill_noise(self, ws, noise):
+        """eps_shift [T,B,2], eps_scale [T,B], eps_z, eps_x, u (injected or
+        device Philox; the fused kernel generates eps_x itself)."""
+        if noise is not None:
+            for k in ("eps_shift", "eps_scale", "eps_z", "eps_x", "u"):
+                dst = ws.eps_scale if k == "eps_scale" else getattr(ws, k)
+                src = torch.as_tensor(noise[k], dtype=torch.float32)
+                if tuple(src.shape) != tuple(dst.shape):
+                    raise ValueError(f"noise[{k}] has shape {tuple(src.shape)}, expected "
+                                     f"{tuple(dst.shape)}")
+                dst.copy_(src)
+            ws.eps_x_offset = None
+            return
+        super()._fill_noise(ws, None)
+
+    # ---------------------------------------------------------- forward ---
+    def _forward(self, X, targets, ws, need_grad, outputs=True):
+        B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
+        C, W, C2 = self.canvas_size, self.windows_size, self.C2
+        s = stream_ptr()
+        Ki = self._N("infer_rnn_running/kernel")
+        Kg = self._N("gen_rnn_running/kernel")
+        bi, bg = self._N("infer_rnn_running/bias"), self._N("gen_rnn_running/bias")
+        if not self.fused_step:
+            ws.canvas.zero_()
+        ws.stop.zero_()
+        ws.runloss.zero_()
+        ws.digits.zero_()
+        ws.live.zero_()
+        ws.live[0] = 1
+        thr = self.hyper("stopping_threshold")
+        temp = self.hyper("z_pres_temperature")
+        lik_std = float(self.hyper("vae_likelihood_std"))
+        fix = -1 if self.fix_steps is None else int(self.fix_steps)
+        w20 = self._w20()
+        # loop-invariant x-projection of the inference LSTM (chain over x first)
+        gemm([X], [Ki[:C2]], [ws.Gx], B, 4 * H, C2, C2, 4 * H, 4 * H)
+        relu_w = [self._N(n + "/kernel") for n in ("inf_shift/dense", "inf_shift/dense_2",
+                                                   "z_pres/log_odds/dense")]
+        relu_b = [self._N(n + "/bias") for n in ("inf_shift/dense", "inf_shift/dense_2",
+                                                 "z_pres/log_odds/dense")]
+        gen_w = [self._N(n + "/kernel") for n in ("gen_shift/dense", "gen_shift/dense_2")]
+        gen_b = [self._N(n + "/bias") for n in ("gen_shift/dense", "gen_shift/dense_2")]
+        sc_w = [self._N("inf_scale/dense/kernel")[:H], self._N("inf_scale/dense_2/kernel")[:H]]
+        for t in range(T):
+            prev = t > 0
+            _lib.call("mog_asr_pack", B, Z, H, LU, dp(ws.z[t - 1]) if prev else None,
+                      dp(ws.ss[t - 1]) if prev else None, dp(ws.h[t - 1]) if prev else None,
+                      dp(ws.U[t]), s)
+            _lib.call("mog_asr_pack", B, Z, H, LU, dp(ws.z[t - 1]) if prev else None,
+                      dp(ws.ss[t - 1]) if prev else None, dp(ws.hg[t - 1]) if prev else None,
+                      dp(ws.Ug[t]), s)
+            KU = Z + 3 + H
+            gemm([ws.U[t]], [Ki[C2:]], [ws.G[t]], B, 4 * H, KU, LU, 4 * H, 4 * H, bias=[bi],
+                 Cin=[ws.Gx])
+            _lib.call("mog_lstm_cell_forward", dp(ws.G[t]), None,
+                      dp(ws.c[t - 1]) if prev else None, dp(ws.c[t]), dp(ws.h[t]), B, H, s)
+            gemm([ws.Ug[t]], [Kg], [ws.Gg[t]], B, 4 * H, KU, LU, 4 * H, 4 * H, bias=[bg])
+            _lib.call("mog_lstm_cell_forward", dp(ws.Gg[t]), None,
+                      dp(ws.cg[t - 1]) if prev else None, dp(ws.cg[t]), dp(ws.hg[t]), B, H, s)
+            hid = [ws.hid8[k, t] for k in range(8)]
+            gemm([ws.h[t]] * 3, relu_w, hid[0:3], B, 64, H, H, 64, 64, epi=EPI_RELU, bias=relu_b)
+            gemm([ws.hg[t]] * 2, gen_w, hid[3:5], B, 64, H, H, 64, 64, epi=EPI_RELU, bias=gen_b)
+            if fix < 0:  # learned prior from the previous generative output (:596-602)
+                gemm([ws.Ug[t][:, Z + 3:]], [self._N("z_pres/prior/dense/kernel")], [hid[5]], B,
+                     64, H, LU, 64, 64, epi=EPI_RELU, bias=[self._N("z_pres/prior/dense/bias")])
+            gemm([ws.h[t]] * 2, sc_w, hid[6:8], B, 64, H, H, 64, 64, epi=EPI_STORE)
+            hid_arr = _lib.ptr_array([dp(x) if (k != 5 or fix < 0) else None
+                                      for k, x in enumerate(hid)])
+            _lib.call("mog_asr_step_forward", B, t, int(self.train), fix, thr, temp,
+                      float(self.scale_prior_mean), float(self.scale_prior_variance),
+                      self.scale_prior_log_variance, float(self.hyper("constrains_num_gamma")),
+                      w20, hid_arr, dp(ws.eps_shift[t]), dp(ws.eps_scale[t]), dp(ws.u[t]),
+                      dp(ws.stop), dp(ws.digits), dp(ws.live), dp(ws.arec[t]), dp(ws.th_f[t]),
+                      dp(ws.th_b[t]), dp(ws.ss[t]), dp(ws.scale[t]), dp(ws.shift[t]),
+                      dp(ws.zprob[t]), dp(ws.zmask[t]), dp(ws.zval[t]), dp(ws.zc[t]), s)
+            if self.live_hook is not None:
+                self.live_hook(ws.live, t)
+            if self.fused_step:
+                self._step_fused(X, ws, t, lik_std)
+                continue
+            if self.precision == "bf16":
+                self._vae_forward_bf16(X, ws, t, lik_std)
+            else:
+                self._vae_forward_fp32(X, ws, t, lik_std)
+            ops.stn_forward(ws.r[t], ws.th_b[t], (C, C), out=ws.canvas, z=ws.zval[t],
+                            mask=ws.zmask[t], accumulate=True)
+        self._forward_loss(X, targets, ws, need_grad, outputs)
+
+    def _forward_loss(self, X, targets, ws, need_grad, outputs=True):
+        """elbo (:917-935, recon :937-962) + pr_loss + element + margin
+        (:964-1079)."""
+        B, T, C2, s = ws.B, self.max_steps, self.C2, stream_ptr()
+        g = self._gammas()
+        _lib.call("mog_asr_terms", B, T, self.canvas_size, len(self.constrains_num),
+                  self._cons_arr, g, dp(ws.arec), dp(ws.vkl), dp(ws.zmask), dp(ws.live),
+                  dp(ws.klsum), dp(ws.pr), dp(ws.area), dp(ws.outl), dp(ws.size), dp(ws.over),
+                  dp(ws.zsum), s)
+        if self.zsum_hook is not None:
+            self.zsum_hook(ws.zsum)
+        parts = ws.cparts
+        self._loss_inputs = (X, targets)
+        ws.materialized = bool(outputs)
+        gscale = 1.0 / (B * self.grad_world)
+        canvas_ptr = dp(ws.canvas) if (outputs or parts is None) else None
+        _lib.call("mog_recon_loss", dp(X), canvas_ptr, dp(parts), T if parts is not None else 0,
+                  B * C2, dp(ws.klsum), dp(ws.digits), dp(targets), B, C2, float(gscale),
+                  dp(ws.recon) if outputs else None, dp(ws.bce), dp(ws.mse), dp(ws.loss_b),
+                  dp(ws.acc_b) if targets is not None else None,
+                  dp(ws.dcanvas) if need_grad else None, s)
+        _lib.call("mog_asr_finalize", B, T, self.canvas_size, len(self.constrains_num),
+                  self._cons_arr, g, float(1.0 / (B * self.grad_world)), dp(ws.arec),
+                  dp(ws.live), dp(ws.zsum), dp(ws.pr), dp(ws.loss_b), dp(ws.element),
+                  dp(ws.margin), s)
+        _lib.call("mog_batch_mean", dp(ws.loss_b), dp(ws.acc_b) if targets is not None else None,
+                  dp(ws.mse), None, B, dp(ws.means), s)
+        _lib.call("mog_add", dp(ws.means), dp(ws.margin), dp(ws.means), 1, s)
+        self._outputs_ready = True
+
+    # --------------------------------------------------------- backward ---
+    def _dz_hook(self, ws, t):
+        if t < self.max_steps - 1:
+            _lib.call("mog_add", dp(ws.dz), dp(ws.dz_carry), dp(ws.dz),
+                      ws.B * self.vae_latent_dimensions, stream_ptr())
+
+    def _backward(self, X, ws):
+        B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
+        C, W, C2 = self.canvas_size, self.windows_size, self.C2
+        s = stream_ptr()
+        self.params.grad.zero_()
+        Ki = self._N("infer_rnn_running/kernel")
+        Kg = self._N("gen_rnn_running/kernel")
+        KU = Z + 3 + H
+        gscale = 1.0 / (B * self.grad_world)
+        fix = -1 if self.fix_steps is None else int(self.fix_steps)
+        w20 = self._w20()
+        ws.dh.zero_()
+        ws.dhg.zero_()
+        ws.dGsum.zero_()
+        ws.dGgsum.zero_()
+        _lib.call("mog_asr_terms_backward", B, T, self.canvas_size, len(self.constrains_num),
+                  self._cons_arr, self._gammas(), float(gscale), float(gscale), dp(ws.arec),
+                  dp(ws.live), dp(ws.zsum), dp(ws.dreg), s)
+        head_w = [self._N(n + "/kernel")[:H] for n in ("inf_shift/dense", "inf_shift/dense_2",
+                                                     "z_pres/log_odds/dense", "inf_scale/dense",
+                                                     "inf_scale/dense_2")]
+        gen_w = [self._N(n + "/kernel") for n in ("gen_shift/dense", "gen_shift/dense_2")]
+        for t in reversed(range(T)):
+            ops.stn_backward(ws.r[t], ws.th_b[t], (C, C), ws.dcanvas, gscale=ws.zc[t],
+                             dU=ws.dr, dtheta=ws.dth_b, dot=ws.dot, want_dot=True)
+            if self.precision == "bf16":
+                self._vae_backward_bf16(ws, t, gscale)
+            else:
+                self._vae_backward_fp32(ws, t, gscale)
+            ops.stn_backward(X, ws.th_f[t], (W, W), ws.dg, want_dU=False, dtheta=ws.dth_f)
+            hid = [ws.hid8[k, t] for k in range(8)]
+            dpre = [ws.dpre[k, t] for k in range(8)]
+            _lib.call("mog_asr_step_backward", B, int(self.train), fix,
+                      float(self.hyper("z_pres_temperature")), float(self.scale_prior_mean),
+                      float(self.scale_prior_variance), float(gscale), w20,
+                      _lib.ptr_array([dp(x) if (k != 5 or fix < 0) else None
+                                      for k, x in enumerate(hid)]),
+                      dp(ws.arec[t]), dp(ws.eps_shift[t]), dp(ws.eps_scale[t]), dp(ws.dth_f),
+                      dp(ws.dth_b), dp(ws.dot), dp(ws.dreg[t]),
+                      dp(ws.dss_carry) if t < T - 1 else None, dp(ws.douts[t]),
+                      _lib.ptr_array([dp(x) if (k != 5 or fix < 0) else None
+                                      for k, x in enumerate(dpre)]), s)
+            # dh[t] += the five heads reading h_t; dhg[t] += the generative shift heads
+            _lib.call("mog_gemm_f32_kseg", 5,
+                      _lib.ptr_array([dp(dpre[k]) for k in (0, 1, 2, 6, 7)]),
+                      _lib.ptr_array([dp(x) for x in head_w]), dp(ws.dh[t]), None, dp(ws.dh[t]),
+                      B, H, 64, 64, 64, H, 0, 1, 0, s)
+            _lib.call("mog_gemm_f32_kseg", 2, _lib.ptr_array([dp(dpre[3]), dp(dpre[4])]),
+                      _lib.ptr_array([dp(x) for x in gen_w]), dp(ws.dhg[t]), None,
+                      dp(ws.dhg[t]), B, H, 64, 64, 64, H, 0, 1, 0, s)
+            if fix < 0 and t > 0:  # the prior at step t reads hg_{t-1}
+                gemm([dpre[5]], [self._N("z_pres/prior/dense/kernel")], [ws.dhg[t - 1]], B, H,
+                     64, 64, 64, H, transB=True, Cin=[ws.dhg[t - 1]])
+            dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
+            _lib.call("mog_lstm_cell_backward", dp(ws.G[t]), None,
+                      dp(ws.c[t - 1]) if t > 0 else None, dp(ws.c[t]), dp(ws.dh[t]), dp(dc_in),
+                      dp(ws.dG[t]), dp(ws.dc[t % 2]), dp(ws.dGsum), B, H, s)
+            dcg_in = ws.dcg[(t + 1) % 2] if t < T - 1 else None
+            _lib.call("mog_lstm_cell_backward", dp(ws.Gg[t]), None,
+                      dp(ws.cg[t - 1]) if t > 0 else None, dp(ws.cg[t]), dp(ws.dhg[t]),
+                      dp(dcg_in), dp(ws.dGg[t]), dp(ws.dcg[t % 2]), dp(ws.dGgsum), B, H, s)
+            if t > 0:
+                gemm([ws.dG[t]], [Ki[C2:]], [ws.dU], B, KU, 4 * H, 4 * H, 4 * H, LU,
+                     transB=True)
+                gemm([ws.dGg[t]], [Kg], [ws.dUg], B, KU, 4 * H, 4 * H, 4 * H, LU, transB=True)
+                _lib.call("mog_asr_unpack", B, Z, H, LU, dp(ws.dU), dp(ws.dUg),
+                          dp(ws.dz_carry), dp(ws.dss_carry), dp(ws.dh[t - 1]),
+                          dp(ws.dhg[t - 1]), s)
+        self._weight_grads(X, ws)
+
+    def _weight_grads(self, X, ws):
+        B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
+        C2, TB, KU = self.C2, ws.B * self.max_steps, Z + 3 + H
+        fix = -1 if self.fix_steps is None else int(self.fix_steps)
+        if self.precision == "bf16":
+            self._vae_weight_grads_bf16(ws)
+        else:
+            self._vae_weight_grads_fp32(ws)
+        G = self._Ng
+        gKi, gKg = G("infer_rnn_running/kernel"), G("gen_rnn_running/kernel")
+        # LSTMCells: x rows from sum_t dG (the x input is loop-invariant)
+        self._dw(X, ws.dGsum, gKi[:C2], B, C2, 4 * H, C2, 4 * H, G("infer_rnn_running/bias"))
+        self._dw(ws.U, ws.dG, gKi[C2:], TB, KU, 4 * H, LU, 4 * H)
+        self._dw(ws.Ug, ws.dGg, gKg, TB, KU, 4 * H, LU, 4 * H, G("gen_rnn_running/bias"))
+        # hidden layers reading h_t, hg_t, hg_{t-1}
+        hs = ("inf_shift/dense", "inf_shift/dense_2", "z_pres/log_odds/dense", "inf_scale/dense",
+              "inf_scale/dense_2")
+        self._dw([ws.h] * 5, [ws.dpre[k] for k in (0, 1, 2, 6, 7)],
+                 [G(n + "/kernel")[:H] for n in hs], TB, H, 64, H, 64,
+                 [G(n + "/bias") for n in hs])
+        self._dw([ws.hg] * 2, [ws.dpre[3], ws.dpre[4]],
+                 [G("gen_shift/dense/kernel"), G("gen_shift/dense_2/kernel")], TB, H, 64, H, 64,
+                 [G("gen_shift/dense/bias"), G("gen_shift/dense_2/bias")])
+        if fix < 0:
+            self._dw(ws.Ug[:, :, Z + 3:], ws.dpre[5], G("z_pres/prior/dense/kernel"), TB, H, 64,
+                     LU, 64, G("z_pres/prior/dense/bias"))
+        # the shift-latent rows of the scale hidden layers
+        self._dw([ws.ss] * 2, [ws.dpre[6], ws.dpre[7]],
+                 [G("inf_scale/dense/kernel")[H:], G("inf_scale/dense_2/kernel")[H:]], TB, 2, 64,
+                 3, 64)
+        # output layers from douts [T, B, 12]
+        d = ws.douts
+        outs = (("inf_shift/dense_1", 0, 0, 2), ("inf_shift/dense_3", 1, 2, 2),
+                ("z_pres/log_odds/dense_1", 2, 4, 1), ("gen_shift/dense_1", 3, 5, 2),
+                ("gen_shift/dense_3", 4, 7, 2))
+        for n, hk, col, k in outs:
+            self._dw(ws.hid8[hk], d[..., col:], G(n + "/kernel"), TB, 64, k, 64, D_N,
+                     G(n + "/bias"))
+        if fix < 0:
+            self._dw(ws.hid8[5], d[..., 9:], G("z_pres/prior/dense_1/kernel"), TB, 64, 1, 64, D_N,
+                     G("z_pres/prior/dense_1/bias"))
+        for n, hk, col in (("inf_scale/dense_1", 6, 10), ("inf_scale/dense_3", 7, 11)):
+            self._dw(ws.hid8[hk], d[..., col:], G(n + "/kernel")[:64], TB, 64, 1, 64, D_N,
+                     G(n + "/bias"))
+            self._dw(ws.ss, d[..., col:], G(n + "/kernel")[64:], TB, 2, 1, 3, D_N)
+
+    # ------------------------------------------------------- outputs -----
+    @property
+    def rec_scales(self):
+        return self._bt(self._ws.scale).unsqueeze(-1)
+
+    @property
+    def z_pres_probs(self):
+        return self._bt(self._ws.zprob)
+
+    def _records(self, name):
+        return self._bt(self._ws.arec[:, Q[name]])
+
+    @property
+    def z_pres_kls(self):
+        return self._records("zkl")
+
+    @property
+    def scale_kls(self):
+        return self._records("skl")
+
+    @property
+    def shift_kls(self):
+        return self._records("shkl")
+
+    @property
+    def vae_kls(self):
+        ws = self._ws
+        return self._bt(ws.vkl * ws.zmask)
+
+    @property
+    def log_variables(self) -> Dict[str, float]:
+        """Batch means of the reference's log_variables (:1080-1084)."""
+        ws = self._ws
+        T = self._T()
+        m = lambda v: float(v.mean())  # noqa: E731
+        kls = {k: float(self._records(k).sum(1).mean()) for k in ("zkl", "skl", "shkl")}
+        return {"z_pres_kl": kls["zkl"], "scale_kl": kls["skl"], "shift_kl": kls["shkl"],
+                "vae_kl": float((ws.vkl * ws.zmask)[:T].sum(0).mean()),
+                "pr_num": float(self._records("prn").sum(1).mean()),
+                "recon": m(ws.bce), "mse": m(ws.mse), "area_loss": m(ws.area),
+                "out_loss": m(ws.outl), "size_loss": m(ws.size), "over_loss": m(ws.over),
+                "num_margin": float(ws.margin[0]), "num_min_KL": m(ws.element),
+                "TotLoss": self.loss, "elbo": m(ws.klsum + ws.bce), "accu": self.accuracy}
+
+    def generate(self, *a, **k):
+        raise NotImplementedError("ASR generation (air_number_bbox_location.py:1124-1361) runs "
+                                  "the generative LSTM prior; not part of this build")

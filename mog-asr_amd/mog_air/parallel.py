@@ -49,3 +49,11 @@ def attach(model, group: Optional[dist.ProcessGroup] = None) -> None:
     if getattr(model, "grad_world", 1) != world:
         raise ValueError(f"model.grad_world={model.grad_world} but the group has {world} ranks")
     model.grad_hook = lambda g: allreduce_grads(g, group)
+    if world > 1 and hasattr(model, "zsum_hook"):
+        # AIR-ASR (air_number_bbox_location.py): the loop predicate is global
+        # over the batch (:386-390) -> MAX of each step's live flag; the margin
+        # loss uses the batch-mean z_pres probabilities (:982-998) -> SUM of
+        # the per-step partial sums.  Both stay on the stream (no host sync).
+        model.live_hook = lambda live, t: dist.all_reduce(live[t + 1:t + 2],
+                                                          op=dist.ReduceOp.MAX, group=group)
+        model.zsum_hook = lambda zsum: dist.all_reduce(zsum, op=dist.ReduceOp.SUM, group=group)

@@ -268,3 +268,62 @@ def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, mod
         log.info("Final Best: elbo:{}\taccu:{}\tmse:{}\tiou:{}".format(*best))
         log.info("\ntraining has ended\n")
     return step
+
+
+TESET_EACH_ITERATION = 200  # (sic) train_air_pr.py:31
+
+
+def train_loop_asr(args, train_model, test_model, tr_x, tr_k, test, canvas, log, models_folder):
+    """The iteration loop of train_air_pr.py:284-400: every step fetches the
+    model's log variables; every 20 iterations their means are logged, every
+    200 the test model runs on the test set (log variables + detection
+    metrics); parameters are saved every 10,000 iterations; the final test
+    when the input runs out."""
+    batcher = records.ShuffleBatcher(tr_x, tr_k, BATCH_SIZE, EPOCHS,
+                                     min_after_dequeue=min(10000, len(tr_k)))
+    saver = Saver(models_folder, "air-model")
+    min_loss, update_flag = 9999999.0, False
+    best = [0.0, 0.0, 0.0, 0.0]
+    logged = {}
+    step = 0
+
+    def test_and_log(tag):
+        nonlocal update_flag
+        tl, ta, tm, sc, sh, nd = run_test(test_model, test, canvas, args.test_batch)
+        p, r, gt_iou, det_iou, g_iou = evaluation(test[3], test[4], sh, sc, nd, csize=canvas)
+        log.info("test:{}\tprecision:{}\trecall:{}\tgtIoU:{:.4f}\tdetectionIoU:{:.4f}"
+                 "\tglobal_iou:{:.4f}".format(tag, p, r, gt_iou, det_iou, g_iou))
+        lv = test_model.log_variables
+        if update_flag:
+            update_flag = False
+            best[:] = [lv["elbo"], lv["accu"], lv["mse"], g_iou]
+        log.info("test:{}\t".format(tag) +
+                 "".join("{}:{:.4f}\t".format(n, v) for n, v in lv.items()))
+        log.info("Current Best: elbo:{}\taccu:{}\tmse:{}\tiou:{}".format(*best))
+
+    log.info("Training...\n")
+    try:
+        while True:
+            if step % SAVE_PARAMS_EACH_ITERATIONS == 0:
+                saver.save(train_model.params, step)
+            x, k = batcher.next_batch()
+            _, _, _, step = train_model.step(x, k)
+            for n, v in train_model.log_variables.items():
+                logged.setdefault(n, []).append(v)
+            if step % LOG_EACH_ITERATION == 0:
+                line = "step:{:6d}\t".format(step)
+                for n, v in logged.items():
+                    if n == "TotLoss" and np.mean(v) < min_loss:
+                        min_loss, update_flag = float(np.mean(v)), True
+                    line += "{}:{:.4f}\t".format(n, np.mean(v))
+                log.info(line)
+                logged = {}
+            if step % TESET_EACH_ITERATION == 0:
+                test_and_log(step)
+            if args.iterations and step >= args.iterations:
+                raise StopIteration
+    except StopIteration:
+        test_and_log("final")
+        log.info("Final Best: elbo:{}\taccu:{}\tmse:{}\tiou:{}".format(*best))
+        log.info("\ntraining has ended\n")
+    return step

@@ -1,0 +1,124 @@
+"""AIR-ASR on the GPU: the HIP path
+(mog_air.asr_model.AIRModel) against the C oracle (oracle/asr_ref.c) on
+identical injected noise — counts, steps, scales, shifts, z_pres
+probabilities, masked KL records and the canvas bit for bit, per-image loss
+within 1e-5 relative, margin within 1e-6 relative — and its gradients
+against float64 torch autograd (oracle/asr_torch.py) under a well-conditioned
+canvas cotangent, for the learned z_pres prior and fix_steps, train and test
+models, fp32 and the bf16 glimpse-VAE configuration."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import air_oracle as ao
+from oracle import asr_oracle as so
+from oracle import asr_torch as st
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _cfg(**kw):
+    base = dict(batch=12, max_steps=4, constrains_num=(1, 3), constrains_num_gamma=0.5,
+                constrains_margin_gamma=100.0, constrains_num_element_gamma=10.0,
+                constrains_bbox_gamma=1.0, constrains_sharesize_gamma=0.3,
+                constrains_area_gamma=0.2, constrains_area_minmax=(17.0, 23.0))
+    base.update(kw)
+    return so.AsrConfig(**base)
+
+
+def _model(cfg, P, scope, precision="fp32"):
+    from mog_air.asr_model import AIRModel
+    m = AIRModel(max_steps=cfg.max_steps, max_digits=cfg.max_steps, canvas_size=cfg.canvas_size,
+                 vae_likelihood_std=cfg.vae_likelihood_std, z_pres_prior_log_odds=-0.01,
+                 z_pres_temperature=cfg.z_pres_temperature,
+                 stopping_threshold=cfg.stopping_threshold, learning_rate=1e-4,
+                 gradient_clipping_norm=1.0, cnn=False, train=cfg.train, scope=scope,
+                 constrains_num=list(cfg.constrains_num),
+                 constrains_num_gamma=cfg.constrains_num_gamma,
+                 constrains_margin_gamma=cfg.constrains_margin_gamma,
+                 constrains_num_element_gamma=cfg.constrains_num_element_gamma,
+                 constrains_bbox_gamma=cfg.constrains_bbox_gamma,
+                 constrains_sharesize_gamma=cfg.constrains_sharesize_gamma,
+                 constrains_area_gamma=cfg.constrains_area_gamma,
+                 constrains_area_minmax=list(cfg.constrains_area_minmax),
+                 fix_steps=cfg.fix_steps, device=DEV, precision=precision)
+    m.params.load_dict(P)
+    return m
+
+
+def _setup(seed, **kw):
+    cfg = _cfg(**kw)
+    P = so.init_params(cfg, seed=seed, bias_scale=0.05)
+    nz = so.make_noise(cfg, seed=seed + 1)
+    x, k = ao.synthetic_canvases(cfg.batch, seed=seed + 2)
+    return cfg, P, nz, x, k
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(train=False), dict(fix_steps=2),
+                                dict(z_pres_temperature=1.0, stopping_threshold=0.99)])
+def test_asr_forward_bit_exact_vs_oracle(kw):
+    cfg, P, nz, x, k = _setup(20, **kw)
+    ref = so.forward(cfg, P, nz, x, k)
+    m = _model(cfg, P, "asrf%d" % hash(tuple(sorted(kw.items()))))
+    m.infer(x, k, noise={n: torch.as_tensor(v).to(DEV) for n, v in nz.items()})
+    T = ref["T"]
+    assert m.executed_steps == T
+    np.testing.assert_array_equal(m.rec_num_digits.cpu().numpy(), ref["digits"])
+    np.testing.assert_array_equal(m.rec_scales[..., 0].cpu().numpy(), ref["scale"].T)
+    np.testing.assert_array_equal(m.rec_shifts.cpu().numpy(), ref["shift"].transpose(1, 0, 2))
+    np.testing.assert_array_equal(m.z_pres_probs.cpu().numpy(), ref["z_pres_prob"].T)
+    np.testing.assert_array_equal(m.z_pres_kls.cpu().numpy(), ref["z_pres_kl"].T)
+    np.testing.assert_array_equal(m.scale_kls.cpu().numpy(), ref["scale_kl"].T)
+    np.testing.assert_array_equal(m.shift_kls.cpu().numpy(), ref["shift_kl"].T)
+    np.testing.assert_array_equal(m.vae_kls.cpu().numpy(), ref["vae_kl"].T)
+    np.testing.assert_array_equal(m.rec_windows.cpu().numpy(), ref["window"].transpose(1, 0, 2))
+    np.testing.assert_array_equal(m.canvas.cpu().numpy(), ref["canvas"])
+    ws = m._ws
+    for key, buf in (("area", ws.area), ("out", ws.outl), ("size", ws.size),
+                     ("overlap", ws.over), ("element", ws.element), ("pr_loss", ws.pr)):
+        np.testing.assert_array_equal(buf.cpu().numpy(), ref[key], err_msg=key)
+    np.testing.assert_allclose(m.per_image_loss.cpu().numpy(), ref["loss"], rtol=1e-5)
+    assert float(ws.margin[0]) == pytest.approx(ref["margin"], rel=1e-6, abs=1e-6)
+    assert abs(m.loss - ref["loss_mean"]) <= max(1e-3, 1e-6 * abs(ref["loss_mean"]))
+
+
+@pytest.mark.parametrize("kw,precision,tol", [(dict(), "fp32", 2e-3),
+                                              (dict(fix_steps=2), "fp32", 2e-3),
+                                              # bf16: the bf16 VAE latents feed the next
+                                              # step's LSTM input in ASR (unlike AIR)
+                                              (dict(), "bf16", 1e-1)])
+def test_asr_gradients_vs_float64_autograd(kw, precision, tol):
+    cfg, P, nz, x, k = _setup(30, **kw)
+    rng = np.random.default_rng(31)
+    Gc = (rng.standard_normal((cfg.batch, cfg.canvas_size ** 2)) * 0.01).astype(np.float32)
+    m = _model(cfg, P, "asrg%s%s" % (precision, cfg.fix_steps), precision)
+    grads = m.compute_gradients(x, k, noise={n: torch.as_tensor(v).to(DEV) for n, v in nz.items()},
+                                canvas_cotangent=torch.as_tensor(Gc).to(DEV))
+    Pt = {n: torch.tensor(v, dtype=torch.float64, requires_grad=True) for n, v in P.items()}
+    out = st.asr_forward(cfg, Pt, nz, torch.tensor(x, dtype=torch.float64),
+                         canvas_cotangent=torch.tensor(Gc, dtype=torch.float64))
+    out["loss"].backward()
+    worst, checked = 0.0, 0
+    for name, p in Pt.items():
+        ref = p.grad.numpy() if p.grad is not None else np.zeros(p.shape)
+        if np.linalg.norm(ref) < 1e-6:
+            assert np.linalg.norm(grads[name]) < 1e-4, name
+            continue
+        err = np.linalg.norm(grads[name] - ref) / np.linalg.norm(ref)
+        worst = max(worst, err)
+        checked += 1
+        assert err < tol, (name, err)
+    assert checked >= 30
+    print(f"ASR {precision} worst relative gradient error {worst:.2e}")
+
+
+def test_asr_train_steps_finite():
+    cfg, P, nz, x, k = _setup(40, batch=64, max_steps=6)
+    m = _model(cfg, P, "asrtrain", "bf16")
+    for i in range(3):
+        loss, acc, mse, gs = m.step(x, k)
+        assert np.isfinite(loss) and 0.0 <= acc <= 1.0
+    assert gs == 3 and np.all(np.isfinite(m.params.flat.cpu().numpy()))
+    lv = m.log_variables
+    assert set(("num_margin", "num_min_KL", "area_loss", "over_loss")) <= set(lv)

@@ -25,3 +25,17 @@ def test_training_air_original_runs(tmp_path, monkeypatch, data, precision):
     assert "iteration final\ttest loss" in text and "globaliou" in text
     assert "training has ended" in text
     assert glob.glob(str(tmp_path / "res_(t)" / "models" / "air-model-0.npz"))
+
+
+@pytest.mark.parametrize("flags", [["-dn", "13", "-gm", "100", "-gne", "10"],
+                                   ["-dn", "3", "-ds", "bbox", "-gb", "1", "-ga", "0.1",
+                                    "--precision", "bf16"]])
+def test_train_air_pr_runs(tmp_path, monkeypatch, flags):
+    import train_air_pr as entry
+    monkeypatch.chdir(tmp_path)
+    step = entry.main(flags + ["-r", str(tmp_path / "res"), "-k", "p", "--iterations", "21",
+                               "--synth-per-count", "40"])
+    assert step == 21
+    text = open(glob.glob(str(tmp_path / "res_(p)" / "logfile*.log"))[0]).read()
+    assert "step:    20\t" in text and "num_margin" in text and "TotLoss" in text
+    assert "test:final\tprecision" in text and "training has ended" in text
