@@ -28,6 +28,7 @@ HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFLOPS = 157.3
 BF16_MFMA_PEAK_TFLOPS = 2500.0
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
+PRECISION = "bf16"  # set from --precision in main()
 
 
 def kernel_work(name, B, C2=2500, H=256, T=3):
@@ -35,8 +36,9 @@ def kernel_work(name, B, C2=2500, H=256, T=3):
     peak).  Per-unit figures in DESIGN.md §Roofline."""
     if name == "lstm_x_projection":          # Gx = X Wx, [B,C2] x [C2,4H], fp32 MFMA
         return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", FP32_MFMA_PEAK_TFLOPS
-    if name == "lstm_x_projection_grad":     # dWx = X^T dGsum, fp32 MFMA
-        return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", FP32_MFMA_PEAK_TFLOPS
+    if name == "lstm_x_projection_grad":     # dWx = X^T dGsum (bf16 MFMA in the bf16 config)
+        peak = BF16_MFMA_PEAK_TFLOPS if PRECISION == "bf16" else FP32_MFMA_PEAK_TFLOPS
+        return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", peak
     if name == "stn_vae_step":               # SURVEY §8 D.3: 30,024 B per image-step
         return "hbm", B * 30024 / 1e9, "GB/s", HBM_PEAK_GBS
     return None
@@ -176,6 +178,8 @@ def cpu_baseline(seconds: float):
 
 def main():
     args = parse()
+    global PRECISION
+    PRECISION = args.precision
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -59,10 +59,12 @@ int mog_stn_forward(const float* U, int N, int Hin, int Win, const float* theta,
 /* Gradient of transformer() (TF GatherV2 grad = UnsortedSegmentSum + the
  * affine-grid chain): G [N, Hout*Wout] upstream, scaled per image by gscale[n]
  * (may be NULL).  Writes dU [N, Hin*Win] (may be NULL), dtheta [N, 6] (may be
- * NULL) and dot[n] = sum_p G[n,p] * out[n,p] (may be NULL). */
+ * NULL) and dot[n] = sum_p G[n,p] * out[n,p] (may be NULL).  u_period /
+ * g_period > 0: image n reads U / G row n % period (all loop steps of a batch
+ * in one launch against the shared canvas input or canvas gradient). */
 int mog_stn_backward(const float* U, int N, int Hin, int Win, const float* theta, int Hout,
                      int Wout, const float* G, const float* gscale, float* dU, float* dtheta,
-                     float* dot, void* stream);
+                     float* dot, int u_period, int g_period, void* stream);
 
 /* ---- LSTM cell (TF-1.12 BasicLSTMCell, air_model.py:454-456,812-815) -----
  * G [B, 4H] gate pre-activations (i,j,f,o) WITHOUT bias when `bias` != NULL. */
@@ -87,7 +89,7 @@ int mog_air_step_forward(int B, int HS, int HZ, int step, int train, int use_num
                          int* digits, int* live, float* rec, float* theta_fwd,
                          float* theta_back, float* scale_out, float* shift_out,
                          float* zprob_out, float* zkl_out, float* skl_out, float* shkl_out,
-                         float* zmask, float* zval, void* stream);
+                         float* zmask, float* zval, float* zc, void* stream);
 /* Backward of the above: writes dout [5][B, 2] and dhid [5][B, HS] (head
  * strides dout_hs / dhid_hs elements). */
 int mog_air_step_backward(int B, int HS, int train, int use_num_prior, float temperature,

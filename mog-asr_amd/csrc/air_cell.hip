@@ -144,6 +144,7 @@ struct StepFwdIO {
   float* shkl_out;         // [B]
   float* zmask;            // [B] active (canvas mask)
   float* zval;             // [B] z_pres value (canvas coefficient)
+  float* zc;               // [B] active ? z : 0 (STN-write backward scale; may be null)
 };
 
 // 8 lanes per image: lanes 0..6 each evaluate one head-output fma chain
@@ -238,6 +239,7 @@ __global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp,
   r[R_ACT * B + b] = act ? 1.0f : 0.0f;
   r[R_LIVE * B + b] = live ? 1.0f : 0.0f;
   r[R_ZC * B + b] = act ? z : 0.0f;
+  if (io.zc) io.zc[b] = act ? z : 0.0f;
 }
 
 struct StepBwdIO {
@@ -565,7 +567,7 @@ extern "C" int mog_air_step_forward(
     const float* eps_scale, const float* eps_shift, const float* u, float* stop, float* runloss,
     int* digits, int* live, float* rec, float* theta_fwd, float* theta_back, float* scale_out,
     float* shift_out, float* zprob_out, float* zkl_out, float* skl_out, float* shkl_out,
-    float* zmask, float* zval, void* stream) {
+    float* zmask, float* zval, float* zc, void* stream) {
   MOG_CHECK_ARG(B >= 0 && hid && w2 && b2 && eps_scale && eps_shift && u && stop && runloss);
   MOG_CHECK_ARG(digits && live && rec && theta_fwd && theta_back && scale_out && shift_out);
   MOG_CHECK_ARG(zprob_out && zkl_out && skl_out && shkl_out && zmask && zval);
@@ -582,7 +584,7 @@ extern "C" int mog_air_step_forward(
   }
   StepFwdIO io{eps_scale, eps_shift, u,       stop,     runloss,  digits,    live,
                rec,       theta_fwd, theta_back, scale_out, shift_out, zprob_out, zkl_out,
-               skl_out,   shkl_out,  zmask,   zval};
+               skl_out,   shkl_out,  zmask,   zval,     zc};
   step_fwd_kernel<<<mog_cdiv(B, 32), 256, 0, mog_stream(stream)>>>(c, hp, io);
   MOG_LAUNCH_RET();
 }

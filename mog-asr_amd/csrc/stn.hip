@@ -225,7 +225,7 @@ __host__ __device__ inline int stn_bwd_slice(int Hin, int Win, int Hout, int Wou
 __global__ __launch_bounds__(256) void stn_bwd_kernel(
     const float* __restrict__ U, int N, int Hin, int Win, const float* __restrict__ theta,
     int Hout, int Wout, const float* __restrict__ G, const float* __restrict__ gscale, float* dU,
-    float* dtheta, float* dot, long long* ts) {
+    float* dtheta, float* dot, int u_period, int g_period, long long* ts) {
 #pragma clang fp contract(off)
   extern __shared__ float smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void stn_bwd_kernel(
   float4* coltab = reinterpret_cast<float4*>(sg + ((P + 3) & ~3));
   float4* rowtab = sdu ? coltab + 64 : reinterpret_cast<float4*>(sU + hw4 * (want_dU ? 2 : 1));
   int2* vrange = reinterpret_cast<int2*>(rowtab + 64);
-  const float* Un = U + (size_t)n * HWin;
+  const float* Un = U + (size_t)(u_period > 0 ? n % u_period : n) * HWin;
   if ((HWin & 3) == 0) {
     const floatx4* src = reinterpret_cast<const floatx4*>(Un);
     for (int q = lane; q < HWin / 4; q += 64) reinterpret_cast<floatx4*>(sU)[q] = src[q];
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256) void stn_bwd_kernel(
   const float sc = gscale ? gscale[n] : 1.0f;
   const bool grads = sc != 0.0f && (want_dU || dtheta != nullptr);
   float a[7] = {0, 0, 0, 0, 0, 0, 0};
-  const float* Gn = G + (size_t)n * P;
+  const float* Gn = G + (size_t)(g_period > 0 ? n % g_period : n) * P;
   const int mode = __builtin_amdgcn_readfirstlane((sep ? 1 : 0) | (sdu ? 2 : 0) | (want_dU ? 4 : 0));
   if (mode == 3 || mode == 7)
     bwd_pixels<true, 1>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, sD, sg, coltab, rowtab, a);
@@ -388,8 +388,10 @@ extern "C" int mog_stn_forward(const float* U, int N, int Hin, int Win, const fl
 
 extern "C" int mog_stn_backward(const float* U, int N, int Hin, int Win, const float* theta,
                                 int Hout, int Wout, const float* G, const float* gscale,
-                                float* dU, float* dtheta, float* dot, void* stream) {
+                                float* dU, float* dtheta, float* dot, int u_period, int g_period,
+                                void* stream) {
   MOG_CHECK_ARG(U && theta && G && N >= 0 && Hin > 0 && Win > 0 && Hout > 0 && Wout > 0);
+  MOG_CHECK_ARG(u_period >= 0 && g_period >= 0);
   MOG_CHECK_ARG(Hin * Win <= 16384);
   if (N == 0) return 0;
   const size_t slice = (size_t)stn_bwd_slice(Hin, Win, Hout, Wout, dU != nullptr);
@@ -411,7 +413,7 @@ extern "C" int mog_stn_backward(const float* U, int N, int Hin, int Win, const f
   }
   stn_bwd_kernel<<<mog_cdiv(N, wpb), 64 * wpb, slice * sizeof(float) * wpb,
                    mog_stream(stream)>>>(U, N, Hin, Win, theta, Hout, Wout, G, gscale, dU, dtheta,
-                                         dot, ts);
+                                         dot, u_period, g_period, ts);
   if (ts) {
     std::vector<long long> h((size_t)N * 8);
     (void)hipStreamSynchronize(mog_stream(stream));

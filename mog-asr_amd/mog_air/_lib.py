@@ -25,11 +25,11 @@ _SIGS = {
     "mog_gemm_f32": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, I, P],
     "mog_gemm_f32_kseg": [I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "mog_stn_forward": [P, I, I, I, P, I, I, P, P, P, I, P],
-    "mog_stn_backward": [P, I, I, I, P, I, I, P, P, P, P, P, P],
+    "mog_stn_backward": [P, I, I, I, P, I, I, P, P, P, P, P, I, I, P],
     "mog_lstm_cell_forward": [P, P, P, P, P, I, I, P],
     "mog_lstm_cell_backward": [P, P, P, P, P, P, P, P, P, I, I, P],
     "mog_air_step_forward": [I, I, I, I, I, I, F, F, F, F, F, F, F, F, F, F, P, P, P, P, P, P,
-                             P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+                             P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "mog_air_step_backward": [I, I, I, I, F, F, F, F, F, F, F, F, P, P, P, P, P, P, P, P, P,
                               L, P, L, P],
     "mog_vae_sample_forward": [I, I, F, F, F, P, P, P, P, P, I, P, P, P, P],

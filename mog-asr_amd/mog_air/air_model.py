@@ -106,6 +106,7 @@ class _Workspace:
         self.shift = e(T, B, 2)
         self.zprob, self.zkl, self.skl, self.shkl = e(T, B), e(T, B), e(T, B), e(T, B)
         self.zmask, self.zval, self.vkl = e(T, B), e(T, B), e(T, B)
+        self.zc = e(T, B)
         self.bf16 = m.precision == "bf16"
         self.mu, self.lv, self.z = e(T, B, Z), e(T, B, Z), e(T, B, Z)
         self.r = e(T, B, W2)
@@ -165,6 +166,10 @@ class _Workspace:
             self.dmu, self.dlv = e(T, B, Z), e(T, B, Z)
             self.da2, self.da1 = e(T, B, R2), e(T, B, R1)
         self.dth_f, self.dth_b, self.dot = e(B, 6), e(B, 6), e(B)
+        # all loop steps at once (AIR: only the LSTM chain is sequential)
+        self.dr_all, self.dg_all = e(T, B, W2), e(T, B, W2)
+        self.dz_all, self.tmp_a2_all = e(T, B, Z), e(T, B, R2)
+        self.dth_f_all, self.dth_b_all, self.dot_all = e(T, B, 6), e(T, B, 6), e(T, B)
         self.dout = e(5, T, B, 2)
         self.dhid = e(5, T, B, HS)
         self.dh = e(T, B, H)
@@ -402,7 +407,8 @@ class AIRModel:
                       dp(ws.eps_shift[t]), dp(ws.u[t]), dp(ws.stop), dp(ws.runloss),
                       dp(ws.digits), dp(ws.live), dp(rec), dp(ws.th_f[t]), dp(ws.th_b[t]),
                       dp(ws.scale[t]), dp(ws.shift[t]), dp(ws.zprob[t]), dp(ws.zkl[t]),
-                      dp(ws.skl[t]), dp(ws.shkl[t]), dp(ws.zmask[t]), dp(ws.zval[t]), s)
+                      dp(ws.skl[t]), dp(ws.shkl[t]), dp(ws.zmask[t]), dp(ws.zval[t]),
+                      dp(ws.zc[t]), s)
             if self.fused_step:
                 with self._timed("stn_vae_step"):
                     self._step_fused(X, ws, t, float(lik_std))
@@ -449,53 +455,52 @@ class AIRModel:
 
     # ---------------------------------------------------------- backward ---
     def _backward(self, X: torch.Tensor, ws: _Workspace) -> None:
+        """Every loop step's glimpse-path backward (STN write, VAE, STN read,
+        heads) depends only on that step's records and dL/dcanvas, so it runs
+        once over all T*B rows; only the LSTM chain is sequential."""
         B, T, H = ws.B, self.max_steps, self.rnn_units
-        C, W, C2, W2 = self.canvas_size, self.windows_size, self.C2, self.W2
-        Z = self.vae_latent_dimensions
-        R1, R2 = self.vae_recognition_units
-        G1, G2 = self.vae_generative_units
+        C, W, C2 = self.canvas_size, self.windows_size, self.C2
         HS = self.scale_hidden_units
+        TB = T * B
         s = stream_ptr()
         st = self.params
         st.grad.zero_()
         K = self._P("rnn/basic_lstm_cell/kernel")
         bK = self._P("rnn/basic_lstm_cell/bias")
         Wh = K[C2:]
-        vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
         w1 = [self._P(h + "/hidden/weights") for h in self._HEADS]
         w2 = [self._P(h + "/output/weights") for h in self._HEADS]
         w2a = _lib.ptr_array([dp(x) for x in w2])
         gscale = 1.0 / (B * self.grad_world)
         prior_lo = self.hyper("z_pres_prior_log_odds")
         temperature = self.hyper("z_pres_temperature")
-        ws.dh[T - 1].zero_()
-        ws.dGsum.zero_()
-        for t in reversed(range(T)):
-            rec = ws.rec[t]
-            # STN write backward: dr, dtheta_back, dot = <dcanvas, w>
-            ops.stn_backward(ws.r[t], ws.th_b[t], (C, C), ws.dcanvas, gscale=rec[R_ZC],
-                             dU=ws.dr, dtheta=ws.dth_b, dot=ws.dot, want_dot=True)
-            if self.precision == "bf16":
-                self._vae_backward_bf16(ws, t, gscale)
-            else:
-                self._vae_backward_fp32(ws, t, gscale)
-            # STN read backward: dtheta only (the canvas input has no gradient)
-            ops.stn_backward(X, ws.th_f[t], (W, W), ws.dg, want_dU=False, dtheta=ws.dth_f)
+        # STN write backward of all steps against the shared canvas gradient
+        ops.stn_backward(ws.r.view(TB, -1), ws.th_b, (C, C), ws.dcanvas, gscale=ws.zc, dU=ws.dr_all,
+                         dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True, n=TB)
+        if self.precision == "bf16":
+            self._vae_backward_bf16_all(ws, gscale)
+        else:
+            self._vae_backward_fp32_all(ws, gscale)
+        # STN read backward of all steps against the shared input canvas
+        ops.stn_backward(X, ws.th_f, (W, W), ws.dg_all, want_dU=False, dtheta=ws.dth_f_all,
+                         n=TB)
+        for t in range(T):
             hid_t = [ws.hid[z, t] for z in range(5)]
-            dhid_t = [ws.dhid[z, t] for z in range(5)]
             _lib.call("mog_air_step_backward", B, HS, int(self.train),
                       int(self.marginal is not None), temperature, prior_lo,
                       float(self.marginal[t]) if self.marginal is not None else 0.0,
                       float(self.scale_prior_mean), float(self.scale_prior_variance),
                       float(self.shift_prior_mean), float(self.shift_prior_variance),
-                      float(gscale), dp(rec), dp(ws.eps_scale[t]), dp(ws.eps_shift[t]),
-                      dp(ws.dth_f), dp(ws.dth_b), dp(ws.dot),
+                      float(gscale), dp(ws.rec[t]), dp(ws.eps_scale[t]), dp(ws.eps_shift[t]),
+                      dp(ws.dth_f_all[t]), dp(ws.dth_b_all[t]), dp(ws.dot_all[t]),
                       _lib.ptr_array([dp(x) for x in hid_t]), w2a, dp(ws.dout[0, t]),
                       T * B * 2, dp(ws.dhid[0, t]), T * B * HS, s)
-            # dh[t] += sum_z dhid_z W1_z^T: one chain over K = 5 * HS (no atomics)
-            _lib.call("mog_gemm_f32_kseg", 5, _lib.ptr_array([dp(x) for x in dhid_t]),
-                      _lib.ptr_array([dp(x) for x in w1]), dp(ws.dh[t]), None, dp(ws.dh[t]),
-                      B, H, HS, HS, HS, H, 0, 1, 0, s)
+        # dh[t] = sum_z dhid_z W1_z^T for every step: one chain over K = 5 * HS
+        _lib.call("mog_gemm_f32_kseg", 5, _lib.ptr_array([dp(ws.dhid[z]) for z in range(5)]),
+                  _lib.ptr_array([dp(x) for x in w1]), dp(ws.dh), None, None, TB, H, HS, HS, HS,
+                  H, 0, 1, 0, s)
+        ws.dGsum.zero_()
+        for t in reversed(range(T)):
             dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
             _lib.call("mog_lstm_cell_backward", dp(ws.Gx if t == 0 else ws.G[t]),
                       dp(bK) if t == 0 else None, dp(ws.c[t - 1]) if t > 0 else None,
@@ -503,8 +508,57 @@ class AIRModel:
                       dp(ws.dGsum), B, H, s)
             if t > 0:
                 gemm([ws.dG[t]], [Wh], [ws.dh[t - 1]], B, H, 4 * H, 4 * H, 4 * H, H,
-                     transB=True)
+                     transB=True, Cin=[ws.dh[t - 1]])
         self._weight_grads(X, ws)
+
+    def _vae_backward_fp32_all(self, ws, gscale):
+        TB = ws.B * self.max_steps
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
+        s = stream_ptr()
+        _lib.call("mog_sigmoid_backward", dp(ws.r), dp(ws.dr_all), dp(ws.dm), TB * W2, 0, s)
+        gemm([ws.dm], [vw["gen_mean"]], [ws.dd2], TB, G2, W2, W2, W2, G2,
+             transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d2pre], ldaux=G2)
+        gemm([ws.dd2], [vw["generative_2"]], [ws.dd1], TB, G1, G2, G2, G2, G1,
+             transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d1pre], ldaux=G1)
+        gemm([ws.dd1], [vw["generative_1"]], [ws.dz_all], TB, Z, G1, G1, G1, Z, transB=True)
+        _lib.call("mog_vae_sample_backward", TB, Z, float(self.vae_prior_mean),
+                  float(self.vae_prior_variance), float(gscale), dp(ws.mu), dp(ws.lv),
+                  dp(ws.eps_z), dp(ws.dz_all), dp(ws.zmask), dp(ws.dmu), dp(ws.dlv), None, None,
+                  0, s)
+        gemm([ws.dmu], [vw["rec_mean"]], [ws.tmp_a2_all], TB, R2, Z, Z, Z, R2, transB=True)
+        gemm([ws.dlv], [vw["rec_log_variance"]], [ws.da2], TB, R2, Z, Z, Z, R2,
+             transB=True, epi=EPI_SOFTPLUS_BWD, Cin=[ws.tmp_a2_all], aux=[ws.a2pre], ldaux=R2)
+        gemm([ws.da2], [vw["recognition_2"]], [ws.da1], TB, R1, R2, R2, R2, R1,
+             transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.a1pre], ldaux=R1)
+        gemm([ws.da1], [vw["recognition_1"]], [ws.dg_all], TB, W2, R1, R1, R1, W2, transB=True)
+
+    def _vae_backward_bf16_all(self, ws, gscale):
+        from .ops import BF_SOFTPLUS_BWD, BF_STORE, gemm_bf16
+        TB = ws.B * self.max_steps
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        Zp = self._pad8(Z)
+        wn = self._wn
+        s = stream_ptr()
+        _lib.call("mog_sigmoid_backward", dp(ws.r), dp(ws.dr_all), dp(ws.dmb), TB * W2, 1, s)
+        gemm_bf16([ws.dmb], [wn["gen_mean"]], [ws.dd2b], TB, G2, W2, W2, W2, G2,
+                  epi=BF_SOFTPLUS_BWD, aux=[ws.d2b], ldaux=G2)
+        gemm_bf16([ws.dd2b], [wn["generative_2"]], [ws.dd1b], TB, G1, G2, G2, G2, G1,
+                  epi=BF_SOFTPLUS_BWD, aux=[ws.d1b], ldaux=G1)
+        gemm_bf16([ws.dd1b], [wn["generative_1"]], [ws.dz_all], TB, Z, G1, G1, G1, Z,
+                  epi=BF_STORE)
+        _lib.call("mog_vae_sample_backward", TB, Z, float(self.vae_prior_mean),
+                  float(self.vae_prior_variance), float(gscale), dp(ws.mu), dp(ws.lv),
+                  dp(ws.eps_z), dp(ws.dz_all), dp(ws.zmask), None, None, dp(ws.dmub),
+                  dp(ws.dlvb), Zp, s)
+        gemm_bf16([ws.dmub], [wn["rec_mean"]], [ws.tmp_a2_all], TB, R2, Zp, Zp, Zp, R2,
+                  epi=BF_STORE)
+        gemm_bf16([ws.dlvb], [wn["rec_log_variance"]], [ws.da2b], TB, R2, Zp, Zp, Zp, R2,
+                  epi=BF_SOFTPLUS_BWD, Cin=[ws.tmp_a2_all], aux=[ws.a2b], ldaux=R2)
+        gemm_bf16([ws.da2b], [wn["recognition_2"]], [ws.da1b], TB, R1, R2, R2, R2, R1,
+                  epi=BF_SOFTPLUS_BWD, aux=[ws.a1b], ldaux=R1)
+        gemm_bf16([ws.da1b], [wn["recognition_1"]], [ws.dg_all], TB, W2, R1, R1, R1, W2,
+                  epi=BF_STORE)
 
     # ------------------------------------------------------ glimpse VAE ----
     def _vae_dims(self):
@@ -755,7 +809,25 @@ class AIRModel:
             self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
         # bias gradient = colsum(sum_t dG_t) = colsum(dGsum), fused here
         with self._timed("lstm_x_projection_grad"):
-            self._dw(X, ws.dGsum, gK[:C2], B, C2, 4 * H, C2, 4 * H, gbK)
+            if self.precision == "bf16":
+                # bf16 configuration: X^T dGsum on bf16 operands (fp32 accumulate);
+                # the forward x-projection stays fp32 (bit-exact counts)
+                self._x_grad_bf16(X, ws, gK[:C2], gbK)
+            else:
+                self._dw(X, ws.dGsum, gK[:C2], B, C2, 4 * H, C2, 4 * H, gbK)
+
+    def _x_grad_bf16(self, X, ws, out, bias_out):
+        B, H, C2 = ws.B, self.rnn_units, self.C2
+        C2p = self._pad8(C2)
+        if getattr(ws, "Xb", None) is None:
+            bf = dict(device=self.device, dtype=torch.bfloat16)
+            ws.Xb = torch.zeros((B, C2p), **bf)
+            ws.dGsumb = torch.empty((B, 4 * H), **bf)
+        srcs = _lib.ptr_array([dp(X), dp(ws.dGsum)])
+        dsts = _lib.ptr_array([dp(ws.Xb), dp(ws.dGsumb)])
+        dims = (ctypes.c_int * 14)(B, C2, C2, B, C2p, C2p, 0, B, 4 * H, 4 * H, B, 4 * H, 4 * H, 0)
+        _lib.call("mog_cvt_bf16_batch", 2, srcs, dsts, dims, stream_ptr())
+        self._dw_bf16(ws.Xb, ws.dGsumb, out, B, C2, 4 * H, C2p, 4 * H, bias_out)
 
     # ------------------------------------------------------------- API ----
     def _prep(self, images, targets):

