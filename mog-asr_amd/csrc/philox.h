@@ -27,15 +27,15 @@ __device__ __forceinline__ void mog_philox_quad(uint64_t seed, uint64_t ctr, boo
     k1 += 0xBB67AE85u;
   }
   if (normal) {
+    // Box-Muller on the hardware transcendentals: v_log_f32 (log2), v_sqrt_f32
+    // and v_sin/v_cos_f32, whose argument is in revolutions (sin(2 pi u2)).
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const float u1 = ((float)(c[2 * h] >> 8) + 1.0f) * 5.9604644775390625e-08f;  // (0,1]
       const float u2 = (float)(c[2 * h + 1] >> 8) * 5.9604644775390625e-08f;        // [0,1)
-      const float r = sqrtf(-2.0f * logf(u1));
-      float sn, cs;
-      sincosf(6.2831853071795865f * u2, &sn, &cs);
-      v[2 * h] = r * cs;
-      v[2 * h + 1] = r * sn;
+      const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+      v[2 * h] = r * __builtin_amdgcn_cosf(u2);
+      v[2 * h + 1] = r * __builtin_amdgcn_sinf(u2);
     }
   } else {
 #pragma unroll

@@ -98,6 +98,14 @@ struct StepArgs {
   long long* tstamp;        // profiling aid: per-block phase timestamps (or null)
 };
 
+// Workgroup barrier for LDS hand-offs only: unlike __syncthreads() it does not
+// drain the wave's global stores (activation flushes, canvas parts), which stay
+// in flight across phases.  The one global hand-off (r, go layer -> STN write)
+// waits for its stores explicitly.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ float softplus_fast(float v) {
   return v > -MOG_SOFTPLUS_T ? v : (v < MOG_SOFTPLUS_T ? __expf(v) : __logf(__expf(v) + 1.0f));
 }
@@ -195,7 +203,7 @@ __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf
         if (K0 + D + d < KS) step(K0 + D + d, q[d]);
     }
   }
-  if constexpr (SYNC) __syncthreads();
+  if constexpr (SYNC) lds_barrier();
   if (!on) return;
 #pragma unroll
   for (int c = 0; c < TPW; ++c) {
@@ -259,6 +267,7 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
   __bf16* sD1 = reinterpret_cast<__bf16*>(sHb);
   float* sR = reinterpret_cast<float*>(arena);
   float2* tabW = reinterpret_cast<float2*>(arena + OFF_TABW);
+  STAMP(11);
 
   for (int i = tid; i < MB * 12; i += NTHR) {
     const int m = i / 12, k = i % 12;
@@ -271,18 +280,72 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
     smask[tid] = act;
     szv[tid] = act ? p.zval[b0 + tid] : 0.0f;
   }
-  __syncthreads();
-  if (tid < MB)
-    ssep[tid] = (stn_separable(&sth[tid][0]) ? 1 : 0) |
-                (stn_separable(&sth[tid][6]) && C <= CTAB_MAX ? 2 : 0);
+  lds_barrier();
+  bool sep_f = true;
+  if (tid < MB) {
+    sep_f = stn_separable(&sth[tid][0]);
+    ssep[tid] = (sep_f ? 1 : 0) | (stn_separable(&sth[tid][6]) && C <= CTAB_MAX ? 2 : 0);
+  }
   build_tables(tabR, sth, 0, MB, 0, C, C, 28, 28);
-  __syncthreads();
+  const bool all_sep = __syncthreads_and(sep_f) != 0;  // (no global stores issued yet)
   STAMP(0);
 
   // ---- 1. STN read (transformer.py:18-175): glimpse -> LDS bf16 ---------
-  // Half-wave per glimpse row (lane = column), eight rows per pass so 32
-  // gathers per lane are in flight.
-  if (p.phases & 1) {
+  // Half-wave per glimpse row (lane = column).  Axis-aligned transforms (every
+  // AIR theta): 14 rows per pass, 56 gathers per lane in flight, the bilinear
+  // weights re-read from the LDS axis tables once the gathers have landed
+  // (only the gathered values are live across the wait).  General affine
+  // transforms: eight rows per pass with per-sample geometry.
+  if ((p.phases & 1) && all_sep) {
+    // half-wave hw owns images 2hw and 2hw+1 (its row entries are broadcast
+    // LDS reads, the column pair per lane is fixed per image); 14 rows per
+    // pass, gathers through a buffer descriptor over this block's images
+    // (32-bit offsets).
+    static_assert(MB == 32 && NTHR == 512, "two images per half-wave");
+    const int hw = tid >> 5, j = tid & 31, jc = min(j, 27);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(p.x) + (size_t)b0 * C2, 0, nb * C2 * 4, 0x00020000);
+    const int C4 = C * 4;
+#pragma unroll 1
+    for (int h = 0; h < 4; ++h) {
+      const int m = 2 * hw + (h >> 1), i0 = (h & 1) * 14;
+      const int mc = m < nb ? m : 0;
+      const float2* tr = tabR + mc * TABR;
+      const float2 cx = tr[jc];
+      const int xo = mc * C2 * 4;
+      const int xa = xo + axis_lo(cx) * 4, xb = xo + axis_hi(cx) * 4;
+      float I[14][4];
+#pragma unroll
+      for (int u = 0; u < 14; ++u) {
+        const float2 cy = tr[28 + i0 + u];
+        const int ya = __mul24(axis_lo(cy), C4), yb = __mul24(axis_hi(cy), C4);
+        I[u][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xa + ya, 0, 0));
+        I[u][1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xa + yb, 0, 0));
+        I[u][2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xb + ya, 0, 0));
+        I[u][3] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xb + yb, 0, 0));
+      }
+      asm volatile("" ::: "memory");  // re-read the tables below instead of keeping them live
+      const float2 cx2 = tr[jc];
+      const float4 ex = axis4(cx2, 1);
+      const bool xlive = m < nb && axis_lo(cx2) != axis_hi(cx2);
+      // branch-free: every lane samples; lanes 28..31 store into the unused
+      // row padding [800, 804) (beyond the GEMM's k extent)
+      __bf16* dst = sG + m * SG + (j < 28 ? i0 * 28 + j : KG + j - 28);
+      const int ustep = j < 28 ? 28 : 0;
+#pragma unroll
+      for (int u = 0; u < 14; ++u) {
+        const float2 cy = tr[28 + i0 + u];
+        const float4 ey = axis4(cy, C);
+        const bool live = xlive || (m < nb && axis_lo(cy) != axis_hi(cy));  // not both axes dead
+        const float sv = sample4(ex, ey, I[u][0], I[u][1], I[u][2], I[u][3]);
+        dst[u * ustep] = (__bf16)(live ? sv : 0.0f);
+      }
+    }
+    for (int i = tid; i < MB * (KG - W2); i += NTHR) {  // zero k padding
+      const int m = i / (KG - W2);
+      sG[m * SG + W2 + (i - m * (KG - W2))] = (__bf16)0.0f;
+    }
+  } else if (p.phases & 1) {
     constexpr int UR = 8;
     const int hw = tid >> 5, j = tid & 31;
     for (int rr0 = hw; rr0 < MB * 28; rr0 += 16 * UR) {
@@ -330,7 +393,7 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
       sG[m * SG + W2 + (i - m * (KG - W2))] = (__bf16)0.0f;
     }
   }
-  __syncthreads();
+  lds_barrier();
   STAMP(1);
   if (p.phases & 16) flush_rows(sG, SG, p.gb + (size_t)b0 * W2, W2, W2, nb);
 
@@ -343,7 +406,7 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
       });
     });
   }
-  __syncthreads();
+  lds_barrier();
   STAMP(2);
   if (p.phases & 16) flush_rows(sA1, S512, p.a1b + (size_t)b0 * 512, 512, 512, nb);
   // ---- 3. a2 = softplus(a1 W2 + b2)  [MB x 256] -> H ----------------------
@@ -355,7 +418,7 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
       });
     });
   }
-  __syncthreads();
+  lds_barrier();
   STAMP(3);
   if (p.phases & 16) flush_rows(sA2, S256, p.a2b + (size_t)b0 * 256, 256, 256, nb);
   // ---- 4. mu | lv = a2 W + b  [MB x 50] fp32 -> A (waves 0-3 | 4-7) ------
@@ -369,7 +432,7 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
       epi_rows(ct, a, 50, [&](int m, int n, float v) { sLv[m * 50 + n] = v + bl[n]; });
     });
   }
-  __syncthreads();
+  lds_barrier();
   STAMP(4);
   // ---- 5. z = mu + eps sqrt(exp(lv)); VAE KL -> runloss (vae.py:27-30) ---
   for (int i = tid; i < MB * 64; i += NTHR) {
@@ -390,7 +453,7 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
     }
     sZ[m * SZ + k] = (__bf16)zv;
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < nb) {  // sequential KL sum per image (k order, as vae_sample_fwd_kernel)
     const int m = tid;
     float t[50];
@@ -413,7 +476,7 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
       });
     });
   }
-  __syncthreads();
+  lds_barrier();
   STAMP(6);
   if (p.phases & 16) flush_rows(sD1, S256, p.d1b + (size_t)b0 * 256, 256, 256, nb);
   // ---- 7. d2 = softplus(d1 Wg2 + b)  [MB x 512] -> A ----------------------
@@ -425,7 +488,7 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
       });
     });
   }
-  __syncthreads();
+  lds_barrier();
   STAMP(7);
   if (p.phases & 16) flush_rows(sD2, S512, p.d2b + (size_t)b0 * 512, 512, 512, nb);
   // ---- 8. r = sigmoid(d2 Wgo + b + std eps)  [MB x 784] fp32 -> HBM -------
@@ -475,7 +538,7 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
     dense_tiles<512, 1, false>(sD2, S512, p.wt[6], 48, 0, 1, epi);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // r stores done before other waves read it
-  __syncthreads();
+  lds_barrier();
   STAMP(8);
   STAMP(9);
   // ---- 9. STN write (air_model.py:580-588): this step's canvas part -------
@@ -495,7 +558,7 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
         for (int i = tid; i < nh * (W2 / 4); i += NTHR) dst[i] = src[i];
       }
       if (C <= CTAB_MAX) build_tables(tabW, sth, h0, nh, 6, 28, 28, C, C);
-      __syncthreads();
+      lds_barrier();
       for (int mm = wv; mm < nh; mm += NW) {
         const int m = h0 + mm;
         float* om = p.part + (size_t)(b0 + m) * C2;
@@ -528,8 +591,19 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
           }
           for (int bb = 0; bb < QB; bb += NBW) {
             const int b = bb + bs;
-            if (!ln || b >= QB) continue;
-            const float4 ey0 = axis4(trow[2 * b], 28), ey1 = axis4(trow[2 * b + 1], 28);
+            const bool on = ln && b < QB;
+            const float4 ey0 = axis4(trow[on ? 2 * b : 0], 28), ey1 = axis4(trow[on ? 2 * b + 1 : 0], 28);
+            // A row whose clipped corner rows coincide samples exactly +0 at
+            // every column (the y weights are exact negatives on one source
+            // row, so the four products cancel pairwise in summation order):
+            // bands where the whole wave sees only such rows store zeros.
+            const bool rows_live = on && (__float_as_int(ey0.x) != __float_as_int(ey0.y) ||
+                                          __float_as_int(ey1.x) != __float_as_int(ey1.y));
+            if (__builtin_amdgcn_ballot_w64(rows_live) == 0) {
+              if (on) om4[b * QB + k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+              continue;
+            }
+            if (!on) continue;
             float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -562,11 +636,11 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
   }
   if (p.tstamp) {
-    __syncthreads();
+    lds_barrier();
     STAMP(10);
   }
 }
@@ -630,15 +704,17 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
     (void)hipMemcpy(h.data(), tbuf, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
     static const char* names[10] = {"stn_read", "L1", "L2", "mu_lv", "sample",
                                     "g1", "g2", "go", "-", "write"};
-    double acc[11] = {0};
+    double acc[11] = {0}, pro = 0;
     long long t0 = h[0], t1 = h[10];
     for (unsigned b = 0; b < nblk; ++b) {
       for (int k = 0; k < 10; ++k) acc[k] += (double)(h[b * 16 + k + 1] - h[b * 16 + k]);
       acc[10] += (double)(h[b * 16 + 10] - h[b * 16]);
+      pro += (double)(h[b * 16] - h[b * 16 + 11]);
       t0 = std::min(t0, h[b * 16]);
       t1 = std::max(t1, h[b * 16 + 10]);
     }
-    fprintf(stderr, "stn_vae_step phases (us, mean over %u blocks; 100 MHz clock):", nblk);
+    fprintf(stderr, "stn_vae_step phases (us, mean over %u blocks; 100 MHz clock): prologue %.2f",
+            nblk, pro / nblk / 100.0);
     for (int k = 0; k < 10; ++k) fprintf(stderr, " %s %.2f", names[k], acc[k] / nblk / 100.0);
     fprintf(stderr, " | block %.2f | span %.2f\n", acc[10] / nblk / 100.0, (t1 - t0) / 100.0);
   }

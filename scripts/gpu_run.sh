@@ -15,6 +15,7 @@ run() {
   tail -n 5 "gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
+nc=0
 for step in "$@"; do
   case "$step" in
     pytest) run pytest 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
@@ -26,6 +27,6 @@ for step in "$@"; do
     pmc) rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
          run pmcf 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --roofline-launches 3
          run pmcw 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --roofline-launches 3 ;;
-    *) run custom 600 bash -c "$step" ;;
+    *) nc=$((nc + 1)); run custom$nc 600 bash -c "$step" ;;
   esac
 done
