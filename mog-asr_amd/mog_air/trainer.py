@@ -58,9 +58,68 @@ def add_common_args(parser, reader_threads: int):
 
 def select_gpu(gpu: str) -> None:
     """-gpu N (training_air_original.py:64-65): must run before the HIP runtime
-    starts; HIP_VISIBLE_DEVICES is the ROCm spelling of CUDA_VISIBLE_DEVICES."""
+    starts; HIP_VISIBLE_DEVICES is the ROCm spelling of CUDA_VISIBLE_DEVICES.
+    Under torch.distributed.run (WORLD_SIZE > 1) each rank takes the GPU of
+    its LOCAL_RANK instead (distributed_setup)."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return
     if 0 <= int(gpu) <= 7:
         os.environ["HIP_VISIBLE_DEVICES"] = str(gpu)
+
+
+class Dist:
+    """Data-parallel context of one trainer process: rank,
+    world, the contiguous shard of each global batch this rank trains on."""
+
+    def __init__(self, rank: int = 0, world: int = 1):
+        self.rank, self.world = rank, world
+
+    @property
+    def main(self) -> bool:
+        return self.rank == 0
+
+    def shard(self, x, k):
+        if self.world == 1:
+            return x, k
+        from .parallel import shard
+        lo, hi = shard(len(k), self.rank, self.world)
+        return x[lo:hi], k[lo:hi]
+
+    def mean(self, values, device):
+        """Mean over ranks of a few host scalars (one small all-reduce)."""
+        if self.world == 1:
+            return list(values)
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor(list(values), dtype=torch.float64, device=device)
+        dist.all_reduce(t)
+        return (t / self.world).tolist()
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+
+def distributed_setup(args) -> Dist:
+    """One process per GPU under torch.distributed.run: RCCL ("nccl") process
+    group, device = cuda:LOCAL_RANK (written into args.device)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1:
+        return Dist()
+    import torch
+    import torch.distributed as dist
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    args.device = "cuda:%d" % local
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device(args.device))
+    return Dist(dist.get_rank(), world)
+
+
+def attach_data_parallel(train_model, ctx: Dist) -> None:
+    if ctx.world > 1:
+        from .parallel import attach
+        attach(train_model)
 
 
 def dataset_files(args, entry: str):
@@ -78,14 +137,17 @@ def dataset_files(args, entry: str):
             os.path.join(folder, f"test{name}.tfrecords"), canvas, name, digits)
 
 
-def results_folder(args, entry: str, name: str) -> str:
+def results_folder(args, entry: str, name: str, main: bool = True) -> str:
     """training_air_original.py:93-115: default name, -k suffix, -o overwrite
-    or the next free _N suffix; creates models/, summary/, source/."""
+    or the next free _N suffix; creates models/, summary/, source/ (rank 0
+    only when data parallel — the other ranks write nothing)."""
     if args.results_folder == "Not Valid":
         args.results_folder = "./results/{time}-({file}_{data})_(train.{train}_test.{test})".format(
             file=entry, train=name.replace("_", "."), test=name.replace("_", "."),
             time=time.strftime("%Y-%m-%d-%H-%M"), data=args.data)
     args.results_folder += "_({})".format(args.key)
+    if not main:
+        return args.results_folder
     if os.path.exists(args.results_folder):
         if args.overwrite_results:
             shutil.rmtree(args.results_folder, ignore_errors=True)
@@ -100,15 +162,19 @@ def results_folder(args, entry: str, name: str) -> str:
     return args.results_folder
 
 
-def build_logger(folder: str, args) -> logging.Logger:
+def build_logger(folder: str, args, main: bool = True) -> logging.Logger:
     """utils/checkpoints.py:31-63: console + results-folder log file, then the
-    sorted configurable parameters between '#' rules."""
+    sorted configurable parameters between '#' rules (rank 0 only when data
+    parallel; the other ranks log nothing)."""
     fmt = "%(asctime)s;%(levelname)s|%(message)s"
     log = logging.getLogger("mog_air")
     log.setLevel(logging.INFO)
     log.propagate = False
     for h in list(log.handlers):
         log.removeHandler(h)
+    if not main:
+        log.addHandler(logging.NullHandler())
+        return log
     sh = logging.StreamHandler()
     sh.setFormatter(logging.Formatter(fmt, "%H-%M-%S"))
     log.addHandler(sh)
@@ -217,7 +283,7 @@ def run_test(test_model, test, canvas: int, batch: int):
 
 
 def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, models_folder,
-               extra_log=None):
+               extra_log=None, ctx: Optional[Dist] = None):
     """The iteration loop of training_air_original.py:226-503 (logging every
     20, testing every 200, parameters every 10,000 iterations; the final
     test when the input runs out)."""
@@ -231,7 +297,11 @@ def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, mod
 
     def test_and_log(tag):
         nonlocal update_flag
+        if not ctx.main:
+            ctx.barrier()
+            return 0.0, 0.0, 0.0, 0.0
         tl, ta, tm, sc, sh, nd = run_test(test_model, test, canvas, args.test_batch)
+        ctx.barrier()
         log.info("iteration {}\ttest loss {:.3f}\ttest accuracy {:.2f}, test mse {:.3f}".format(
             tag, tl, ta, tm))
         p, r, gt_iou, det_iou, g_iou = evaluation(test[3], test[4], sh, sc, nd, csize=canvas)
@@ -242,15 +312,15 @@ def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, mod
     log.info("Training...\n")
     try:
         while True:
-            if step % SAVE_PARAMS_EACH_ITERATIONS == 0:
+            if step % SAVE_PARAMS_EACH_ITERATIONS == 0 and ctx.main:
                 saver.save(train_model.params, step)
-            x, k = batcher.next_batch()
+            x, k = ctx.shard(*batcher.next_batch())
             loss, acc, mse, step = train_model.step(x, k)
             if extra_log is not None:
                 extra_log(train_model, step)
             hist.append([loss, acc, mse])
             if step % LOG_EACH_ITERATION == 0:
-                l0, l1, l2 = np.mean(hist[-LOG_EACH_ITERATION:], axis=0)
+                l0, l1, l2 = ctx.mean(np.mean(hist[-LOG_EACH_ITERATION:], axis=0), args.device)
                 log.info("iteration {}\ttrain loss {:.3f}\ttrain accuracy {:.2f}, "
                          "train mse {:.3f}".format(step, l0, l1, l2))
                 if l0 < min_loss:
@@ -273,12 +343,14 @@ def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, mod
 TESET_EACH_ITERATION = 200  # (sic) train_air_pr.py:31
 
 
-def train_loop_asr(args, train_model, test_model, tr_x, tr_k, test, canvas, log, models_folder):
+def train_loop_asr(args, train_model, test_model, tr_x, tr_k, test, canvas, log, models_folder,
+                   ctx: Optional[Dist] = None):
     """The iteration loop of train_air_pr.py:284-400: every step fetches the
     model's log variables; every 20 iterations their means are logged, every
     200 the test model runs on the test set (log variables + detection
     metrics); parameters are saved every 10,000 iterations; the final test
-    when the input runs out."""
+    when the input runs out.  Data parallel as train_loop."""
+    ctx = ctx or Dist()
     batcher = records.ShuffleBatcher(tr_x, tr_k, BATCH_SIZE, EPOCHS,
                                      min_after_dequeue=min(10000, len(tr_k)))
     saver = Saver(models_folder, "air-model")
@@ -289,7 +361,11 @@ def train_loop_asr(args, train_model, test_model, tr_x, tr_k, test, canvas, log,
 
     def test_and_log(tag):
         nonlocal update_flag
+        if not ctx.main:
+            ctx.barrier()
+            return
         tl, ta, tm, sc, sh, nd = run_test(test_model, test, canvas, args.test_batch)
+        ctx.barrier()
         p, r, gt_iou, det_iou, g_iou = evaluation(test[3], test[4], sh, sc, nd, csize=canvas)
         log.info("test:{}\tprecision:{}\trecall:{}\tgtIoU:{:.4f}\tdetectionIoU:{:.4f}"
                  "\tglobal_iou:{:.4f}".format(tag, p, r, gt_iou, det_iou, g_iou))
@@ -304,15 +380,16 @@ def train_loop_asr(args, train_model, test_model, tr_x, tr_k, test, canvas, log,
     log.info("Training...\n")
     try:
         while True:
-            if step % SAVE_PARAMS_EACH_ITERATIONS == 0:
+            if step % SAVE_PARAMS_EACH_ITERATIONS == 0 and ctx.main:
                 saver.save(train_model.params, step)
-            x, k = batcher.next_batch()
+            x, k = ctx.shard(*batcher.next_batch())
             _, _, _, step = train_model.step(x, k)
             for n, v in train_model.log_variables.items():
                 logged.setdefault(n, []).append(v)
             if step % LOG_EACH_ITERATION == 0:
                 line = "step:{:6d}\t".format(step)
-                for n, v in logged.items():
+                means = ctx.mean([np.mean(v) for v in logged.values()], args.device)
+                for (n, _), v in zip(logged.items(), means):
                     if n == "TotLoss" and np.mean(v) < min_loss:
                         min_loss, update_flag = float(np.mean(v)), True
                     line += "{}:{:.4f}\t".format(n, np.mean(v))

@@ -25,7 +25,14 @@ def _logit8(p):
 
 
 def asr_forward(cfg: AsrConfig, P, noise, images, targets=None, canvas_cotangent=None,
-                fixed_steps=True):
+                fixed_steps=True, live_reduce=None, zsum_reduce=None, global_batch=None):
+    """``live_reduce(local_any) -> global_any`` and ``zsum_reduce(local [T] sum)
+    -> global [T] sum`` restate one data-parallel shard: the
+    loop predicate is global over the batch (air_number_bbox_location.py:386-390)
+    and the margin uses the batch-mean z_pres probabilities (:982-998) of
+    ``global_batch`` images; the returned loss is this shard's share
+    (B_local / global_batch of its mean) plus the full margin, so the sum of
+    the shards' gradients is the full-batch gradient."""
     dt = images.dtype
     B, T, H, Z = cfg.batch, cfg.max_steps, cfg.rnn_units, cfg.vae_latent_dimensions
     C, W = cfg.canvas_size, cfg.windows_size
@@ -61,6 +68,8 @@ def asr_forward(cfg: AsrConfig, P, noise, images, targets=None, canvas_cotangent
     steps = 0
     for t in range(T):
         live = bool((stop < thr).any())
+        if live_reduce is not None:
+            live = bool(live_reduce(live))
         if not live:
             if not fixed_steps:
                 break
@@ -162,12 +171,17 @@ def asr_forward(cfg: AsrConfig, P, noise, images, targets=None, canvas_cotangent
         cons = list(cfg.constrains_num)
         obj = torch.tensor([[1.0 if t < k else 0.0 for t in range(Tx)] for k in cons], dtype=dt)
         mo = obj.mean(0)
-        pm = S["zprob"].mean(0)
+        if zsum_reduce is None:
+            pm = S["zprob"].mean(0)
+        else:  # global value, gradient through this shard's own terms only
+            zl = S["zprob"].sum(0)
+            zg = torch.as_tensor(zsum_reduce(zl.detach().clone()), dtype=dt)
+            pm = (zl + (zg - zl.detach())) / float(global_batch or B)
         margin = (_sce(mo, _logit8(pm)) * cfg.constrains_margin_gamma).sum()
         ce = _sce(obj[None], _logit8(S["zprob"])[:, None, :]).sum(2)
         elem = ce.min(1).values * cfg.constrains_num_element_gamma
     loss_b = elbo + pr + elem
-    loss = loss_b.mean() + margin
+    loss = loss_b.mean() * (B / float(global_batch or B)) + margin
     if canvas_cotangent is not None:
         loss = loss + (canvas_cotangent * canvas).sum()
     return {"loss": loss, "loss_b": loss_b, "kl": kl, "pr": pr, "T": Tx, "digits": digits, "canvas": canvas,

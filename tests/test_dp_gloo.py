@@ -67,3 +67,43 @@ def test_dp_gloo_world2_matches_full_batch(tmp_path):
     P, nz, x, k = dp_worker.inputs()
     full = dp_worker.grads(P, nz, x, k, 0, dp_worker.B, 1.0)
     np.testing.assert_allclose(reduced, full.numpy(), rtol=1e-9, atol=1e-12)
+
+
+def _run_world(args):
+    port = _free_port()
+    procs = []
+    for r in range(WORLD):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                   WORLD_SIZE=str(WORLD), OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py")] + args,
+                                      env=env))
+    try:
+        rcs = [p.wait(timeout=240) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0] * WORLD
+
+
+@pytest.mark.timeout(300)
+def test_dp_gloo_world2_asr_matches_full_batch(tmp_path):
+    """AIR-ASR: with the hooks parallel.attach installs — MAX
+    of each step's live flag, SUM of the per-step z_pres probability sums — the
+    shards' summed gradient, summed loss and executed step count equal the
+    full batch's (each rank's loss is its share of the mean plus the global
+    margin, so the summed loss holds the margin world times).  The config is
+    chosen so that the shards alone would exit after 3 and 2 steps."""
+    out = str(tmp_path / "asr.npz")
+    _run_world([out, "asr"])
+    r = np.load(out)
+    cfg, P, nz, x, G = dp_worker.asr_inputs()
+    g_full, loss_full, T_full = dp_worker.asr_grads(cfg, P, nz, x, G, 0, cfg.batch)
+    assert int(r["T"][0]) == T_full
+    np.testing.assert_allclose(r["g"], g_full.numpy(), rtol=1e-9, atol=1e-12)
+    # every rank adds the (global) margin once: sum = full loss + (world - 1) margin
+    from oracle import asr_torch as st
+    Pt = {n: torch.tensor(v, dtype=torch.float64) for n, v in P.items()}
+    margin = float(st.asr_forward(cfg, Pt, nz, torch.tensor(x, dtype=torch.float64),
+                                  canvas_cotangent=torch.tensor(G))["margin"])
+    assert abs(float(r["loss"][0]) - (loss_full + (WORLD - 1) * margin)) < 1e-8 * max(1.0, abs(loss_full))

@@ -48,11 +48,17 @@ def main(argv=None):
     else:
         size_min, size_max = (12, 15) if "bbox" in args.dig_surfix else (20, 25)
     print(size_min, size_max)
-    folder = trainer.results_folder(args, "train_air_pr.py", name)
-    log = trainer.build_logger(folder, args)
-    trainer.copy_sources(folder, [ROOT, os.path.join(ROOT, "mog-asr_amd", "mog_air")])
+    ctx = trainer.distributed_setup(args)  # one process per GPU under torch.distributed.run
+    folder = trainer.results_folder(args, "train_air_pr.py", name, main=ctx.main)
+    log = trainer.build_logger(folder, args, main=ctx.main)
+    if ctx.main:
+        trainer.copy_sources(folder, [ROOT, os.path.join(ROOT, "mog-asr_amd", "mog_air")])
     log.info("Creating input pipeline...")
+    if not ctx.main:
+        ctx.barrier()  # rank 0 writes synthetic data first when asked to
     tr_x, tr_k, test = trainer.load_data(args, train_file, test_file, digits, log)
+    if ctx.main:
+        ctx.barrier()
 
     models = []
     for i in range(2):
@@ -73,11 +79,13 @@ def main(argv=None):
             constrains_bbox_gamma=args.gamma_bbox, constrains_sharesize_gamma=args.gamma_size,
             constrains_area_gamma=args.gamma_area, constrains_area_minmax=[size_min, size_max],
             fix_steps=digits[0] if len(digits) == 1 else None, annealing_schedules={},
-            device=args.device, seed=1235, precision=args.precision))
+            device=args.device, seed=1235, precision=args.precision,
+            grad_world=ctx.world if i == 0 else 1))
     train_model, test_model = models
+    trainer.attach_data_parallel(train_model, ctx)
     log.info("Initializing variables...")
     return trainer.train_loop_asr(args, train_model, test_model, tr_x, tr_k, test, canvas, log,
-                                  os.path.join(folder, "models"))
+                                  os.path.join(folder, "models"), ctx=ctx)
 
 
 if __name__ == "__main__":

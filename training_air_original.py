@@ -34,12 +34,18 @@ def main(argv=None):
     from mog_air.air_model import AIRModel
 
     train_file, test_file, canvas, name, digits = trainer.dataset_files(args, "training_air_original.py")
-    folder = trainer.results_folder(args, "training_air_original.py", name)
-    log = trainer.build_logger(folder, args)
-    trainer.copy_sources(folder, [ROOT, os.path.join(ROOT, "mog-asr_amd", "mog_air")])
+    ctx = trainer.distributed_setup(args)  # one process per GPU under torch.distributed.run
+    folder = trainer.results_folder(args, "training_air_original.py", name, main=ctx.main)
+    log = trainer.build_logger(folder, args, main=ctx.main)
+    if ctx.main:
+        trainer.copy_sources(folder, [ROOT, os.path.join(ROOT, "mog-asr_amd", "mog_air")])
 
     log.info("Creating input pipeline...")
+    if not ctx.main:
+        ctx.barrier()  # rank 0 writes synthetic data first when asked to
     tr_x, tr_k, test = trainer.load_data(args, train_file, test_file, digits, log)
+    if ctx.main:
+        ctx.barrier()
 
     models = []
     for i in range(2):
@@ -59,11 +65,13 @@ def main(argv=None):
                 "init": 10000.0, "min": 0.000000001, "factor": 0.1, "iters": 3000,
                 "staircase": False, "log": True}},
             num_prior=digits if args.add_prior else None,
-            device=args.device, seed=1235, precision=args.precision))
+            device=args.device, seed=1235, precision=args.precision,
+            grad_world=ctx.world if i == 0 else 1))
     train_model, test_model = models
+    trainer.attach_data_parallel(train_model, ctx)
     log.info("Initializing variables...")
     return trainer.train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log,
-                              os.path.join(folder, "models"))
+                              os.path.join(folder, "models"), ctx=ctx)
 
 
 if __name__ == "__main__":
