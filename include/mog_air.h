@@ -111,8 +111,10 @@ int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, float v_plv, co
  * log-variance 256->50, z = mu + eps*sqrt(exp(lv)), generative 50->256->512
  * softplus, r = sigmoid(512->784 + std*eps_x)), the VAE KL into runloss under
  * `mask` (air_model.py:718-736), and this step's canvas contribution
- * canvas_part = mask ? zval * STN(r, theta_b) : 0 for every pixel
- * (air_model.py:580-588, 665-675; summed in step order by mog_recon_loss).
+ * canvas_part = mask ? zval * STN(r, theta_b) : 0 (air_model.py:580-588,
+ * 665-675; summed in step order by mog_recon_loss).  Only the rows that can be
+ * nonzero are stored: part_rows[b] = lo | hi << 16 records the stored row range
+ * [lo, hi) of image b (0 for an inactive image); every other pixel is +0.
  * wt[7] are the bf16 W^T packs in B-fragment order (mog_cvt_bf16_batch
  * transpose 2) in the order recognition_1, recognition_2, rec_mean, rec_log_variance,
  * generative_1, generative_2, gen_mean; bias[7] fp32 likewise.  eps_x: read
@@ -129,7 +131,8 @@ int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int Z, int G1,
                              const float* eps_x, int eps_gen, unsigned long long eps_seed,
                              unsigned long long eps_offset, const void* const* wt,
                              const float* const* bias, float lik_std, float v_pm, float v_pv,
-                             float v_plv, float* canvas_part, float* runloss, float* vkl, void* gb,
+                             float v_plv, float* canvas_part, int* part_rows, float* runloss,
+                             float* vkl, void* gb,
                              void* a1b, void* a2b, float* mu, float* lv, float* z, void* zb,
                              void* d1b, void* d2b, float* r, void* stream);
 
@@ -173,9 +176,11 @@ int mog_cvt_bf16_batch(int njobs, const float* const* src, void* const* dst, con
 /* With nparts == 0 the canvas [B, C2] is read.  With nparts > 0 it is the
  * step-ordered sum of the per-step contributions parts[t] (stride part_stride
  * elements; written by mog_stn_vae_step_forward) and is stored to `canvas`
- * when that is non-NULL. */
+ * when that is non-NULL.  part_rows (may be NULL: parts fully stored) [nparts,
+ * B]: rows [lo, hi) = (v & 0xffff, v >> 16) of part t / image b that were
+ * stored, the part being +0 elsewhere (C = canvas side, C*C == C2). */
 int mog_recon_loss(const float* x, float* canvas, const float* parts, int nparts,
-                   long part_stride, const float* runloss, const int* digits,
+                   long part_stride, const int* part_rows, int C, const float* runloss, const int* digits,
                    const int* targets, int B, int C2, float grad_scale, float* recon,
                    float* bce, float* mse, float* loss, float* acc, float* dcanvas,
                    void* stream);

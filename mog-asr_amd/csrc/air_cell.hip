@@ -429,11 +429,16 @@ __device__ __forceinline__ void recon_pixel(float c, float xv, float grad_scale,
 // One block per image, four pixels per thread-iteration (16-byte accesses).
 // With nparts > 0 the canvas is the step-ordered sum of the per-step
 // contributions ((p0 + p1) + p2 ..., the accumulation order of
-// air_model.py:665-675) and is written to canvas_out when given.
+// air_model.py:665-675) and is written to canvas_out when given.  With
+// part_rows, part t of image b holds only rows [lo, hi) (part_rows[t*B + b] =
+// lo | hi << 16, row ranges aligned so that no 4-pixel group straddles them)
+// and is +0 elsewhere: those pixels are never read and +0 is added instead,
+// which leaves the sum bit-identical.
 template <bool VEC>
 __global__ __launch_bounds__(256) void recon_loss_kernel(
     const float* __restrict__ x, const float* __restrict__ canvas_in,
-    const float* __restrict__ parts, int nparts, long part_stride, float* canvas_out,
+    const float* __restrict__ parts, int nparts, long part_stride,
+    const int* __restrict__ part_rows, int B, int C, float* canvas_out,
     const float* __restrict__ runloss, const int* __restrict__ digits,
     const int* __restrict__ targets, int C2, float grad_scale, float* recon, float* bce_out,
     float* mse_out, float* loss_out, float* acc_out, float* dcanvas) {
@@ -444,12 +449,18 @@ __global__ __launch_bounds__(256) void recon_loss_kernel(
   float bce = 0.0f, mse = 0.0f;
   constexpr int V = VEC ? 4 : 1;
   typedef float vec __attribute__((ext_vector_type(V)));
+  auto part = [&](int t, int p) -> vec {  // part t's pixels p..p+V-1 (+0 where not stored)
+    vec v = 0.0f;
+    const int pr = part_rows ? part_rows[(size_t)t * B + b] : 0;
+    if (!part_rows || (p >= (pr & 0xffff) * C && p < (pr >> 16) * C))
+      v = *reinterpret_cast<const vec*>(parts + t * part_stride + base + p);
+    return v;
+  };
   for (int p = threadIdx.x * V; p < C2; p += 256 * V) {
     vec c;
     if (nparts > 0) {
-      c = *reinterpret_cast<const vec*>(parts + base + p);
-      for (int t = 1; t < nparts; ++t)
-        c = c + *reinterpret_cast<const vec*>(parts + t * part_stride + base + p);
+      c = part(0, p);
+      for (int t = 1; t < nparts; ++t) c = c + part(t, p);
       if (canvas_out) *reinterpret_cast<vec*>(canvas_out + base + p) = c;
     } else {
       c = *reinterpret_cast<const vec*>(canvas_in + base + p);
@@ -659,21 +670,24 @@ extern "C" int mog_sigmoid_backward(const float* r, const float* dr, void* dm, l
 }
 
 extern "C" int mog_recon_loss(const float* x, float* canvas, const float* parts, int nparts,
-                              long part_stride, const float* runloss, const int* digits,
+                              long part_stride, const int* part_rows, int C,
+                              const float* runloss, const int* digits,
                               const int* targets, int B, int C2, float grad_scale, float* recon,
                               float* bce, float* mse, float* loss, float* acc, float* dcanvas,
                               void* stream) {
   MOG_CHECK_ARG(x && runloss && digits && bce && mse && loss && B >= 0 && C2 > 0);
-  MOG_CHECK_ARG(nparts >= 0 && (nparts > 0 ? parts != nullptr && part_stride >= (long)B * C2
-                                           : canvas != nullptr));
+  MOG_CHECK_ARG(nparts >= 0 &&
+                (nparts > 0 ? parts != nullptr && part_stride >= (long)B * C2
+                            : canvas != nullptr));
+  MOG_CHECK_ARG(!part_rows || (nparts > 0 && C > 0 && C * C == C2 && (C2 % 4 != 0 || C % 2 == 0)));
   if (B == 0) return 0;
   if (C2 % 4 == 0)
     recon_loss_kernel<true><<<B, 256, 0, mog_stream(stream)>>>(
-        x, canvas, parts, nparts, part_stride, canvas, runloss, digits, targets, C2, grad_scale,
+        x, canvas, parts, nparts, part_stride, part_rows, B, C, canvas, runloss, digits, targets, C2, grad_scale,
         recon, bce, mse, loss, acc, dcanvas);
   else
     recon_loss_kernel<false><<<B, 256, 0, mog_stream(stream)>>>(
-        x, canvas, parts, nparts, part_stride, canvas, runloss, digits, targets, C2, grad_scale,
+        x, canvas, parts, nparts, part_stride, part_rows, B, C, canvas, runloss, digits, targets, C2, grad_scale,
         recon, bce, mse, loss, acc, dcanvas);
   MOG_LAUNCH_RET();
 }

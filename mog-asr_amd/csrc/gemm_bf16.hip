@@ -16,6 +16,7 @@
 // prefetch of tile i+2 while tile i is multiplied and tile i+1 is written to
 // the other stage — one barrier per k-iteration.  Workgroup ids are remapped
 // so that the workgroups sharing an A row-panel run on one XCD (shared L2).
+#include "bf16_epi.h"
 #include "mog_common.h"
 
 namespace {
@@ -265,12 +266,11 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
           v = v * sg;
         } else {
           if (bias != nullptr) v = v + bias[col];
-          if (EPI == B_SOFTPLUS)  // TF thresholds, log(exp(x) + 1) between them
-            v = v > -MOG_SOFTPLUS_T ? v : (v < MOG_SOFTPLUS_T ? __expf(v) : __logf(__expf(v) + 1.0f));
+          if (EPI == B_SOFTPLUS) v = mog_softplus_hw(v);
           if (EPI == B_SIGMOID_NOISE) {
             const float y = __builtin_fmaf(
                 reinterpret_cast<const float*>(aux)[(size_t)row * D.ldaux + col], D.aux_scale, v);
-            v = 1.0f / (1.0f + __expf(-y));
+            v = mog_sigmoid_hw(y);
           }
         }
         if (D.out_bf16) reinterpret_cast<__bf16*>(Cv)[o] = (__bf16)v;

@@ -3,32 +3,39 @@
 // vae.py:5-48, transformer.py:18-175).  This is the kernel SURVEY.md §8 D.3
 // prices at 30,024 algorithmic HBM bytes per image-step.
 //
-// One workgroup = 8 waves = MB (32) images, two workgroups per CU (70.5 KB of
-// LDS each), so one workgroup's gathers and stores overlap the other's MFMA
-// phases.  Activations stay in LDS between the six dense layers (bf16, rows
-// padded against bank conflicts), reusing one region: a layer whose output
-// lands on its own input waits for the whole workgroup after its k loop.  The
-// bf16 weights (W^T in MFMA B-fragment order: one 1-KiB contiguous wave load
-// per fragment) stream from L2 straight into the MFMA B operand (four k-steps
-// of register prefetch); the A operand is read from LDS with ds_read_b128.
-// Activations the backward needs (glimpse, softplus outputs, mu/logvar/z, r)
-// are flushed to HBM with 16-byte stores.  The output layer's tiles are
-// transposed through LDS so that the bias + noise + sigmoid epilogue works on
-// four consecutive pixels (one Philox quad of eps_x) and r leaves with 16-byte
-// stores; the STN write then stages r back from L2 sixteen images at a time
-// and stores this step's canvas contribution z * w (0 where inactive or where
-// the sample is exactly +0, i.e. x0 == x1 && y0 == y1); mog_recon_loss sums
-// the parts in step order, so the canvas is bit-identical to the running
-// accumulation of air_model.py:665-675 and this kernel never waits on a
-// canvas read.
+// One workgroup = 16 waves = M = 16*MT images per CU (MT = 8: 128 images;
+// MT = 4 / 2 for batches too small to give every CU 128).  Sixteen waves
+// (four per SIMD) keep enough weight loads, gathers and stores in flight.  The bf16 weights
+// (W^T in MFMA B-fragment order: one 1-KiB contiguous wave load per fragment)
+// stream from L2 straight into the MFMA B operand, so the L2 -> CU weight
+// traffic per image is 2.2 MB / M: the tile height M is what keeps the dense
+// layers off the L2 bandwidth roof.  A workgroup never holds its whole glimpse
+// (M x 800 bf16 would not fit): the STN read is pipelined k-step by k-step into
+// the recognition layer -- the gathers of k-step ks+2 are in flight while the
+// MFMAs of k-step ks run, samples for k-step ks+1 land in a two-slab LDS ring,
+// and each slab is flushed to HBM as the saved glimpse.  The other layers keep
+// their activations in one LDS arena (bf16, rows padded against bank
+// conflicts; a layer whose output lands on its own input waits for the whole
+// workgroup after its k loop).  Activations the backward needs (glimpse,
+// softplus outputs, mu/logvar/z, r) are flushed with 16-byte stores.  The
+// output layer's accumulator quads are transposed across lanes (DPP) so a lane
+// owns four consecutive pixels -- one Philox quad of eps_x, one 16-byte store
+// of r; the STN write stages r back M/4 images at a time and stores, per image,
+// only the band-aligned rows of this step's canvas contribution z * w that can
+// be nonzero (part_rows records them); mog_recon_loss sums the parts in step
+// order, so the canvas is bit-identical to the running accumulation of
+// air_model.py:665-675 and this kernel never waits on a canvas read.
 //
 // Precision: bf16 MFMA operands, fp32 accumulation and epilogues with
 // hardware transcendentals (the bf16 configuration, BASELINE configs[1]).
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
+#include "bf16_epi.h"
 #include "philox.h"
 #include "stn_geom.h"
 
@@ -36,35 +43,59 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+template <int V>
+using IC = std::integral_constant<int, V>;
 
-constexpr int MB = 32;        // images per workgroup
-constexpr int NW = 8;         // waves per workgroup
-constexpr int NTHR = NW * 64;
+// waves per workgroup: a kernel template parameter NW, 16 (one workgroup per
+// CU) or 8 (two per CU)
 constexpr int W2 = 784;       // 28 x 28 glimpse
-constexpr int KG = 800;       // glimpse k extent padded to a multiple of 32 (25 k-steps)
-constexpr int SG = KG + 8;    // LDS row strides (bf16), +16 B against bank conflicts
-constexpr int S512 = 512 + 8, S256 = 256 + 8, SZ = 64 + 8;
-// One LDS arena: region A [0, A_BYTES) then region H [A_BYTES, ARENA).
-//   A: glimpse [32][808] -> a1 [32][520] -> mu | lv | kl fp32, z bf16 -> d2
-//      [32][520] (+ the output layer's transpose scratch behind it)
-//   H: read tables -> a2 [32][264] -> d1 [32][264]
-//   A+H: r staging for 16 images [16][784] fp32 + their write tables
-constexpr int A_BYTES = MB * SG * 2;                     // 51,712
-constexpr int H_BYTES = MB * S256 * 2;                   // 16,896
-constexpr int ARENA = A_BYTES + H_BYTES;                 // 68,608
-constexpr int TABR = 28 + 28;                            // read tables: 28 columns + 28 rows
-constexpr int OFF_MU = 0, OFF_LV = MB * 50 * 4, OFF_KL = 2 * MB * 50 * 4, OFF_Z = 3 * MB * 50 * 4;
-constexpr int OFF_XP = MB * S512 * 2;                    // transpose scratch behind d2
-constexpr int XP_STRIDE = 20;                            // floats per scratch row (conflict-free)
-constexpr int XP_WAVE = 32 * XP_STRIDE * 4;              // 2,560 B per wave
-constexpr int RH = 16;                                   // images per r-staging half
-constexpr int OFF_TABW = RH * W2 * 4;                    // 50,176
-constexpr int CTAB_MAX = 64;                             // write tables for canvases up to 64 x 64
-static_assert(MB * TABR * 8 <= H_BYTES, "read tables");
-static_assert(OFF_Z + MB * SZ * 2 <= A_BYTES, "mu/lv/kl/z");
-static_assert(MB * S512 * 2 <= A_BYTES && MB * S256 * 2 <= H_BYTES, "activations");
-static_assert(OFF_XP + NW * XP_WAVE <= ARENA, "transpose scratch");
-static_assert(OFF_TABW + RH * 2 * CTAB_MAX * 8 <= ARENA, "write tables");
+constexpr int KS1 = 25;       // recognition-layer k-steps (k padded to 800)
+constexpr int S512 = 512 + 8, S256 = 256 + 8, SZ = 64 + 8;  // LDS row strides (bf16)
+constexpr int KG = 5;          // recognition k-steps per glimpse slab (one barrier per slab)
+constexpr int NG = KS1 / KG;   // slabs
+constexpr int SK = 32 * KG + 8;  // slab row stride (bf16)
+static_assert(KS1 % KG == 0, "slabs");
+constexpr int TABR = 56;      // read-table entries per image: 28 columns, then 28 rows
+constexpr int CTAB_MAX = 64;  // write tables for canvases up to 64 x 64
+
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+// f(IC<K>{}), f(IC<K+1>{}) ... f(IC<N-1>{}): a fully unrolled loop whose index
+// is a compile-time constant in every copy (the waitcnt pass then knows
+// exactly which loads are still in flight; at a rolled loop's header it
+// falls back to waiting for all of them)
+template <int K, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (K < N) {
+    f(IC<K>{});
+    static_for<K + 1, N>(f);
+  }
+}
+
+// LDS arena layout (bytes) for M = 16*MT images.
+//   read:   tables [M][56] float4 at 0, glimpse slabs 3 x [M][SK] bf16 behind them
+//   then:   a1 [M][S512] at 0 -> a2 [M][S256] at 0 (in place), mu | lv fp32 behind a2
+//   sample: kl [M][50] fp32 at 0, z [M][SZ] bf16 behind it, d1 [M][S256] at A2
+//   then:   d2 [M][S512] at 0 (in place over d1)
+//   write:  r staging [RH][784] fp32 at 0, write tables [RH][2C] float4 behind
+template <int MT>
+struct Lay {
+  static constexpr int M = 16 * MT;
+  static constexpr int A1 = M * S512 * 2;
+  static constexpr int TAB = M * TABR * 16;
+  static constexpr int KB = M * SK * 2;  // one glimpse slab (KG k-steps)
+  static constexpr int A2 = M * S256 * 2;
+  static constexpr int OFF_MU = A2, OFF_LV = A2 + M * 50 * 4;
+  static constexpr int OFF_KL = 0, OFF_Z = M * 50 * 4;
+  static constexpr int OFF_D1 = A2;
+  static constexpr int RH = M / 4;  // images per r-staging group
+  static constexpr int OFF_TABW = RH * W2 * 4;
+  static constexpr int ARENA =
+      cmax(cmax(A1, TAB + 3 * KB), cmax(OFF_D1 + A2, cmax(OFF_LV + M * 50 * 4, OFF_TABW + RH * 2 * CTAB_MAX * 16)));
+  static_assert(OFF_Z + M * SZ * 2 <= A2, "kl / z behind a2");
+  static_assert(OFF_LV + M * 50 * 4 <= OFF_D1 + A2, "mu / lv");
+};
 
 struct StepArgs {
   const float* x;            // [B, C*C] canvas input
@@ -79,7 +110,8 @@ struct StepArgs {
   const __bf16* wt[7];       // W^T in B-fragment order: r1 [512][800], r2 [256][512],
                              // mu, lv [64][256], g1 [256][64], g2 [512][256], go [784][512]
   const float* bias[7];
-  float* part;               // [B, C*C] this step's canvas contribution (written)
+  float* part;               // [B, C*C] this step's canvas contribution (rows in part_rows)
+  int* part_rows;            // [B] rows [lo, hi) of part that were stored: lo | hi << 16
   float* runloss;            // [B]
   float* vkl;                // [B]
   __bf16* gb;                // [B, 784]   saved for the backward
@@ -100,18 +132,76 @@ struct StepArgs {
 
 // Workgroup barrier for LDS hand-offs only: unlike __syncthreads() it does not
 // drain the wave's global stores (activation flushes, canvas parts), which stay
-// in flight across phases.  The one global hand-off (r, go layer -> STN write)
-// waits for its stores explicitly.
+// in flight across phases.  The one global hand-off (r, output layer -> STN
+// write) waits for its stores explicitly.
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-__device__ __forceinline__ float softplus_fast(float v) {
-  return v > -MOG_SOFTPLUS_T ? v : (v < MOG_SOFTPLUS_T ? __expf(v) : __logf(__expf(v) + 1.0f));
+
+// value of lane (lane ^ 1) / (lane ^ 2) of the same quad
+__device__ __forceinline__ float quad_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float quad_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+
+// 4 x 4 transpose inside lane quads (two DPP exchanges): on entry lane
+// (li = lane & 15, g = lane >> 4) holds an MFMA 16 x 16 accumulator's rows
+// g*4 + r, r < 4, of column li; on exit it holds row g*4 + (li & 3) at the
+// four consecutive columns (li & ~3) + r.
+__device__ __forceinline__ floatx4 quad_transpose(const floatx4& a) {
+  const int e = threadIdx.x & 3;
+  float r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3];
+  {
+    const bool hi = (e & 2) != 0;
+    const float t0 = quad_xor2(hi ? r0 : r2), t1 = quad_xor2(hi ? r1 : r3);
+    if (hi) { r0 = t0; r1 = t1; } else { r2 = t0; r3 = t1; }
+  }
+  {
+    const bool od = (e & 1) != 0;
+    const float t0 = quad_xor1(od ? r0 : r1), t1 = quad_xor1(od ? r2 : r3);
+    if (od) { r0 = t0; r2 = t1; } else { r1 = t0; r3 = t1; }
+  }
+  return floatx4{r0, r1, r2, r3};
+}
+
+// Weight fragments (1 KiB per wave per k-step) through a buffer descriptor:
+// the per-lane offset is fixed per column tile and the k-step goes into the
+// scalar offset, so a fragment load costs no vector ALU address arithmetic.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t weight_rsrc(const __bf16* W) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(W), 0, 0x7ffffff0, 0x00020000);
+}
+__device__ __forceinline__ bf16x8 load_frag(__amdgpu_buffer_rsrc_t r, int voff, int ks) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, ks * 1024, 0);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// bias[n0 .. n0+3] (0 past N)
+__device__ __forceinline__ floatx4 load_bias4(const float* __restrict__ bias, int n0, int N) {
+  if (n0 + 4 <= N) {
+    const float4 b = *reinterpret_cast<const float4*>(bias + n0);
+    return floatx4{b.x, b.y, b.z, b.w};
+  }
+  floatx4 b;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) b[k] = n0 + k < N ? bias[n0 + k] : 0.0f;
+  return b;
+}
+
+// softplus of v + b as four bf16 -> one 8-byte LDS store
+__device__ __forceinline__ void store_softplus4(__bf16* dst, const floatx4& v, const floatx4& b) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  bf16x4 o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o[k] = (__bf16)mog_softplus_hw(v[k] + b[k]);
+  *reinterpret_cast<bf16x4*>(dst) = o;
 }
 
 // Axis tables of `nimg` images' transforms (th at sth[m0 + m][th_off]):
 // tab[m*per + n], n < Wout columns then Hout rows, as {coordinate, lo | hi<<16}.
+template <int NTHR>
 __device__ __forceinline__ void build_tables(float2* tab, const float (*sth)[12], int m0, int nimg,
                                              int th_off, int Hin, int Win, int Hout, int Wout) {
   const int per = Wout + Hout;
@@ -123,53 +213,71 @@ __device__ __forceinline__ void build_tables(float2* tab, const float (*sth)[12]
   }
 }
 
-// Column tiles tile_base + (w + nw*c + rot) % (nw*TPW) of one dense layer
-// over the MB rows held in LDS, for waves wbase .. wbase+nw-1.  A: LDS
-// [MB][lda] bf16, zero-padded to K.  W: the layer's W^T in B-fragment order
-// (mog_cvt_bf16_batch transpose 2; N padded to 16, K to 32, zeros outside),
-// so each B fragment is one 1-KiB contiguous wave load streamed from L2
-// straight into the MFMA, with a register prefetch ring of D k-steps (rolled,
-// branch-free body so the compiler keeps the distance; the ragged tail is
-// peeled at compile time).  SYNC: the whole workgroup meets after the k loop
-// (the epilogue overwrites A; requires nw == NW).  epi(ct, acc[2][4] per tile).
-template <int K, int TPW, bool SYNC, class Epi>
+// Expanded axis tables (axis4: {lo*scale, hi*scale (int bits), hi - c, c - lo})
+// of `nimg` images' transforms: Wout column entries (scale 1), then Hout row
+// entries (scale Win).
+template <int NTHR>
+__device__ __forceinline__ void build_tables4(float4* tab, const float (*sth)[12], int m0, int nimg,
+                                              int th_off, int Hin, int Win, int Hout, int Wout) {
+  const int per = Wout + Hout;
+  for (int i = threadIdx.x; i < nimg * per; i += NTHR) {
+    const int m = i / per, n = i - (i / per) * per;
+    const float* th = &sth[m0 + m][th_off];
+    tab[i] = n < Wout ? axis4(axis_col(th, Hin, Win, Hout, Wout, n), 1)
+                      : axis4(axis_row(th, Hin, Win, Hout, Wout, n - Wout), Win);
+  }
+}
+
+// Column tiles tile_base + (w + nw*c + rot) % (nw*TPW) of one dense layer over
+// the M = 16*MT rows held in LDS, for waves wbase .. wbase+nw-1.  A: LDS
+// [M][lda] bf16, zero-padded to K.  W: the layer's W^T in B-fragment order
+// (mog_cvt_bf16_batch transpose 2; N padded to 16, K to 32, zeros outside), so
+// each B fragment is one 1-KiB contiguous wave load streamed from L2 straight
+// into the MFMA, with a register prefetch ring of D k-steps (rolled,
+// branch-free body; the ragged tail is peeled at compile time).  SYNC: the
+// whole workgroup meets after the k loop (the epilogue overwrites A; requires
+// nw == NW).  Epilogue per 16 x 16 accumulator tile, quad-transposed:
+// epi(m, n0, v, b) with v = row m's columns n0 .. n0+3 and b = their biases
+// (loaded before the k loop; 0 at or past N).
+template <int MT, int K, int TPW, int D, bool SYNC, class Epi>
 __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf16* __restrict__ W,
-                                            int tile_base, int wbase, int nw, Epi epi) {
+                                            const float* __restrict__ bias, int N, int tile_base,
+                                            int wbase, int nw, Epi epi) {
   constexpr int KS = K / 32;
   static_assert(K % 32 == 0, "K padding");
   const int rot = (int)(blockIdx.x >> 3);  // spread the CUs of one XCD over the weight columns
   const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) - wbase;
   const bool on = w >= 0 && w < nw;
   const int li = lane & 15, g = lane >> 4;
-  int ct[TPW];
-  const bf16x8* wf[TPW];
+  int ct[TPW], wo[TPW];
+  const __amdgpu_buffer_rsrc_t wr = weight_rsrc(W);
 #pragma unroll
   for (int c = 0; c < TPW; ++c) {
     ct[c] = tile_base + (w + nw * c + rot) % (nw * TPW);
-    wf[c] = reinterpret_cast<const bf16x8*>(W) + (size_t)ct[c] * KS * 64 + lane;
+    wo[c] = (ct[c] * KS * 64 + lane) * 16;
   }
-  floatx4 acc[2][TPW];
+  floatx4 bq[TPW];
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+  for (int c = 0; c < TPW; ++c) bq[c] = on ? load_bias4(bias, ct[c] * 16 + (li & ~3), N) : floatx4{};
+  floatx4 acc[MT][TPW];
+#pragma unroll
+  for (int rt = 0; rt < MT; ++rt)
 #pragma unroll
     for (int c = 0; c < TPW; ++c) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
   auto loadB = [&](int ks, bf16x8* b) {
 #pragma unroll
-    for (int c = 0; c < TPW; ++c) b[c] = wf[c][ks * 64];
+    for (int c = 0; c < TPW; ++c) b[c] = load_frag(wr, wo[c], ks);
   };
   auto step = [&](int ks, const bf16x8* b) {
     const int k = ks * 32 + 8 * g;
-    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&A[li * lda + k]);
-    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&A[(16 + li) * lda + k]);
 #pragma unroll
-    for (int c = 0; c < TPW; ++c) {
-      acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b[c], acc[0][c], 0, 0, 0);
-      acc[1][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b[c], acc[1][c], 0, 0, 0);
+    for (int rt = 0; rt < MT; ++rt) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&A[(rt * 16 + li) * lda + k]);
+#pragma unroll
+      for (int c = 0; c < TPW; ++c)
+        acc[rt][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[c], acc[rt][c], 0, 0, 0);
     }
   };
-  // ring depth: four k-steps of B fragments in flight, two for four-tile waves
-  // (register budget of two workgroups per CU)
-  constexpr int D = TPW >= 4 ? 2 : 4;
   if (on) {
     if constexpr (KS < D) {
       bf16x8 q[TPW];
@@ -206,27 +314,45 @@ __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf
   if constexpr (SYNC) lds_barrier();
   if (!on) return;
 #pragma unroll
-  for (int c = 0; c < TPW; ++c) {
-    floatx4 a[2] = {acc[0][c], acc[1][c]};
-    epi(ct[c], a);
-  }
+  for (int c = 0; c < TPW; ++c)
+#pragma unroll
+    for (int rt = 0; rt < MT; ++rt)
+      epi(rt * 16 + g * 4 + (li & 3), ct[c] * 16 + (li & ~3), quad_transpose(acc[rt][c]), bq[c]);
 }
 
-// element-wise epilogue into an LDS tile: out[row][col] = f(acc, col) for the
-// lane's 8 accumulators of column tile ct (rows rt*16 + g*4 + r, col ct*16 + li)
-template <class F>
-__device__ __forceinline__ void epi_rows(int ct, const floatx4* a, int N, F f) {
-  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
-  const int col = ct * 16 + li;
-  if (col >= N) return;
+// One column tile `ct` of a dense layer split by rows: wave w < MT computes
+// row tile w (for a last, odd column tile that would otherwise leave seven
+// waves idle).
+template <int MT, int K, class Epi>
+__device__ __forceinline__ void dense_rowsplit(const __bf16* A, int lda, const __bf16* __restrict__ W,
+                                               const float* __restrict__ bias, int N, int ct,
+                                               Epi epi) {
+  constexpr int KS = K / 32, D = 4;
+  static_assert(KS % D == 0, "ring");
+  const int lane = threadIdx.x & 63, rt = threadIdx.x >> 6;
+  if (rt >= MT) return;
+  const int li = lane & 15, g = lane >> 4;
+  const floatx4 bq = load_bias4(bias, ct * 16 + (li & ~3), N);
+  const __amdgpu_buffer_rsrc_t wr = weight_rsrc(W);
+  const int wo = (ct * KS * 64 + lane) * 16;
+  floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 q[D];
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+  for (int d = 0; d < D; ++d) q[d] = load_frag(wr, wo, d);
+#pragma unroll 1
+  for (int ks = 0; ks < KS; ks += D) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) f(rt * 16 + g * 4 + r, col, a[rt][r]);
+    for (int d = 0; d < D; ++d) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&A[(rt * 16 + li) * lda + (ks + d) * 32 + 8 * g]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, q[d], acc, 0, 0, 0);
+      q[d] = load_frag(wr, wo, min(ks + d + D, KS - 1));
+    }
+  }
+  epi(rt * 16 + g * 4 + (li & 3), ct * 16 + (li & ~3), quad_transpose(acc), bq);
 }
 
 // LDS tile [nb][lds] -> HBM rows [nb][ldg] with 16-byte stores (ncols * sizeof(T) % 16 == 0).
-template <class T>
+template <int NTHR, class T>
 __device__ __forceinline__ void flush_rows(const T* s, int lds, T* g, int ldg, int ncols, int nb) {
   constexpr int V = 16 / sizeof(T);
   const int cpr = ncols / V;
@@ -240,218 +366,348 @@ __device__ __forceinline__ void flush_rows(const T* s, int lds, T* g, int ldg, i
 #define STAMP(k) \
   if (p.tstamp && threadIdx.x == 0) p.tstamp[blockIdx.x * 16 + (k)] = wall_clock64()
 
-__global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) {
+// Column entry of the STN read in pair form: the two corner columns lo, hi
+// (hi == lo + 1, or lo == hi when clipped) are always inside the pixel pair
+// (xb, xb + 1), xb = min(lo, Win - 2), which one 8-byte load per corner row
+// fetches: {xb * 4 (byte offset), lo != xb | (hi != xb) << 1 (int bits),
+// hi - c, c - lo}.  Corner values: U[y][lo] = pair[flag0], U[y][hi] = pair[flag1];
+// lo == hi exactly when the two flags agree.
+__device__ __forceinline__ float4 col_pair4(float2 e, int Win) {
+  const int lo = axis_lo(e), hi = axis_hi(e), xb = min(lo, Win - 2);
+  return make_float4(__int_as_float(xb * 4), __int_as_float((lo != xb ? 1 : 0) | (hi != xb ? 2 : 0)),
+                     (float)hi - e.x, e.x - (float)lo);
+}
+
+// Glimpse sample geometry (transformer.py:48-116) for glimpse pixel k < 800 of
+// image m: column entry in pair form (col_pair4), row entry {lo, hi (byte
+// offsets, int bits), hi - c, c - lo}: from the LDS tables (axis-aligned
+// transforms) or per sample.
+template <bool SEP>
+__device__ __forceinline__ void glimpse_geom(const float4* tabR, const float* th, int m, int k, int C,
+                                             float4& ex, float4& ey) {
+  const int i = min(k / 28, 27), j = k - (k / 28) * 28;
+  if constexpr (SEP) {
+    ex = tabR[m * TABR + j];
+    ey = tabR[m * TABR + 28 + i];
+  } else {
+    const Tap t = stn_tap(th, C, C, mog_linspace(j, 28), mog_linspace(i, 28));
+    ex = col_pair4(make_float2(t.x, __int_as_float((int)t.x0f | ((int)t.x1f << 16))), C);
+    ey = make_float4(__int_as_float((int)t.y0f * C * 4), __int_as_float((int)t.y1f * C * 4),
+                     t.y1f - t.y, t.y - t.y0f);
+  }
+}
+
+// STN read pipelined into the recognition layer a1 = softplus(g W1 + b1),
+// with the workgroup split by role: waves 8-15 (samplers) gather and sample
+// the glimpse, waves 0-7 (MFMA waves, four of the 32 column tiles each) run
+// the MFMAs, so the sampling VALU work and the matrix work overlap.  The
+// glimpse passes through a ring of three LDS slabs of KG k-steps (KG*32
+// pixels of all M images): while the MFMA waves consume slab g, the samplers
+// fill slab g+1 and flush slab g-1 to HBM (the saved glimpse); one workgroup
+// barrier per slab.  The samplers' gathers run LA k-steps ahead of the
+// samples (HBM latency).  A sampler lane samples pixel 32ks + (lane&31) of its
+// wave's images sw*M/8 + 2u + (lane>>5), u < M/16.
+template <int MT, int NW, bool SEP>
+__device__ __forceinline__ void read_recognition(const StepArgs& p, unsigned char* arena,
+                                                 const float (*sth)[12], int b0, int nb,
+                                                 floatx4 (&acc)[MT][64 / NW], int (&ct)[64 / NW],
+                                                 floatx4 (&b1q)[64 / NW]) {
+  using Ly = Lay<MT>;
+  constexpr int M = Ly::M;
+  constexpr int NTHR = NW * 64;
+  constexpr int TW = 64 / NW;          // recognition column tiles per MFMA wave (32 over NW/2)
+  constexpr int NU = M / NW;           // gather instructions (two images each) per sampler lane
+  constexpr int DB = NW == 16 ? 2 : 1; // weight-fragment ring depth (register budget)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const bool sampler = wv >= NW / 2;
+  const int li = lane & 15, g = lane >> 4;
+  const int C = p.C, C2 = C * C;
+  const float4* tabR = reinterpret_cast<const float4*>(arena);
+  const bool rd = (p.phases & 1) != 0, mm = (p.phases & 2) != 0;
+  auto opaque = [](int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+  if (sampler) {
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(p.x) + (size_t)b0 * C2, 0, nb * C2 * 4, 0x00020000);
+    const int kk = lane & 31;
+    const int mw = (wv - NW / 2) * (2 * M / NW) + (lane >> 5);
+    // Per-lane LDS bases made opaque to the compiler, so that image u of the
+    // lane (mw + 2u) is a small immediate offset from them instead of one
+    // materialized address register per u (the arena is larger than the 64 KiB
+    // reach of a DS instruction's offset field).
+    const int tabo = mw * TABR * 16;                       // the lane's first table
+    const int kbo = Ly::TAB + (mw * SK + kk) * 2;          // its first sample in slab 0
+    constexpr int LA = 3;
+    float I[LA][NU][4];
+    auto gather = [&](int ks, float (&I)[NU][4]) {
+      const int k = 32 * ks + kk;
+      const int i = min(k / 28, 27), j = k - (k / 28) * 28;
+      const float4* tc = reinterpret_cast<const float4*>(arena + opaque(tabo + j * 16));
+      const float4* tr = reinterpret_cast<const float4*>(arena + opaque(tabo + (28 + i) * 16));
+      int xo = mw * C2 * 4;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int m = mw + 2 * u;
+        float4 ex, ey;
+        if constexpr (SEP) {
+          ex = tc[2 * u * TABR];
+          ey = tr[2 * u * TABR];
+        } else {
+          glimpse_geom<false>(tabR, sth[m], m, k, C, ex, ey);
+        }
+        const int xb = __float_as_int(ex.x) + xo;
+        const u32x2 r0 = __builtin_amdgcn_raw_buffer_load_b64(xr, xb + __float_as_int(ey.x), 0, 0);
+        const u32x2 r1 = __builtin_amdgcn_raw_buffer_load_b64(xr, xb + __float_as_int(ey.y), 0, 0);
+        I[u][0] = __uint_as_float(r0[0]);
+        I[u][1] = __uint_as_float(r0[1]);
+        I[u][2] = __uint_as_float(r1[0]);
+        I[u][3] = __uint_as_float(r1[1]);
+        xo += 2 * C2 * 4;
+      }
+    };
+    auto sample = [&](int ks, const float (&I)[NU][4]) {
+      const int k = 32 * ks + kk;
+      const int i = min(k / 28, 27), j = k - (k / 28) * 28;
+      asm volatile("" ::: "memory");  // re-read the tables instead of keeping them live
+      const float4* tc = reinterpret_cast<const float4*>(arena + opaque(tabo + j * 16));
+      const float4* tr = reinterpret_cast<const float4*>(arena + opaque(tabo + (28 + i) * 16));
+      const int grp = ks / KG;
+      __bf16* kd = reinterpret_cast<__bf16*>(
+          arena + opaque(kbo + (grp % 3) * Ly::KB + (ks - grp * KG) * 64));
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int m = mw + 2 * u;
+        float4 ex, ey;
+        if constexpr (SEP) {
+          ex = tc[2 * u * TABR];
+          ey = tr[2 * u * TABR];
+        } else {
+          glimpse_geom<false>(tabR, sth[m], m, k, C, ex, ey);
+        }
+        // corners from the two pairs (rows y0: I[u][0..1], y1: I[u][2..3])
+        const int fl = __float_as_int(ex.y);
+        const float Ia = (fl & 1) ? I[u][1] : I[u][0], Ib = (fl & 1) ? I[u][3] : I[u][2];
+        const float Ic = (fl & 2) ? I[u][1] : I[u][0], Id = (fl & 2) ? I[u][3] : I[u][2];
+        // dead: corners coincide on both axes (flags agree, rows equal).
+        // Evaluated with bitwise ops: short-circuit forms made the compiler
+        // branch around a separate LDS load of the row entry.
+        const int xlive = (fl ^ (fl >> 1)) & 1;
+        const int ylive = __float_as_int(ey.x) != __float_as_int(ey.y) ? 1 : 0;
+        const int live = (int)rd & (int)(k < W2) & (int)(m < nb) & (xlive | ylive);
+        const float v = sample4(ex, ey, Ia, Ib, Ic, Id);
+        kd[2 * u * SK] = (__bf16)(live ? v : 0.0f);
+      }
+    };
+    // glimpse slab grp -> gb[:, 160grp ..] (16-byte pieces inside the 784 columns)
+    auto flush = [&](int grp) {
+      if (!(p.phases & 16)) return;
+      const __bf16* kb = reinterpret_cast<const __bf16*>(arena + Ly::TAB + (grp % 3) * Ly::KB);
+      constexpr int CPR = KG * 4;  // 16-byte pieces per slab row
+      for (int i = tid - NTHR / 2; i < M * CPR; i += NTHR / 2) {
+        const int m = i / CPR, c = i - (i / CPR) * CPR, k = 32 * KG * grp + 8 * c;
+        if (m < nb && k < W2)
+          *reinterpret_cast<u32x4*>(p.gb + (size_t)(b0 + m) * W2 + k) =
+              *reinterpret_cast<const u32x4*>(kb + m * SK + 8 * c);
+      }
+    };
+    // k-step ks uses gather register set ks % LA; the sample loop is unrolled
+    // by LA so the set index is a compile-time constant
+#pragma unroll
+    for (int k = 0; k < LA; ++k)
+      if (rd) gather(k, I[k]);
+    static_for<0, KS1>([&](auto kc) {
+      constexpr int ks = decltype(kc)::value;
+      sample(ks, I[ks % LA]);
+      if constexpr (ks + LA < KS1)
+        if (rd) gather(ks + LA, I[ks % LA]);
+      if constexpr (ks % KG == KG - 1) {  // slab complete
+        if constexpr (ks >= 2 * KG - 1) flush(ks / KG - 1);
+        lds_barrier();
+      }
+    });
+    flush(NG - 1);
+    lds_barrier();
+  } else {
+    // MFMA waves: column tiles (wv + (NW/2) c + rot) % 32, c < TW
+    const int rot = (int)(blockIdx.x >> 3);
+    const __amdgpu_buffer_rsrc_t wr = weight_rsrc(p.wt[0]);
+    int wo[TW];
+#pragma unroll
+    for (int c = 0; c < TW; ++c) {
+      ct[c] = (wv + (NW / 2) * c + rot) % 32;
+      wo[c] = (ct[c] * KS1 * 64 + lane) * 16;
+    }
+    bf16x8 q[DB][TW];
+    auto loadB = [&](int ks, bf16x8* b) {
+#pragma unroll
+      for (int c = 0; c < TW; ++c) b[c] = load_frag(wr, wo[c], ks);
+    };
+    const int kao = Ly::TAB + (li * SK + 8 * g) * 2;
+    auto mfma = [&](int ks, const bf16x8* b) {
+      if (!mm) return;
+      const int grp = ks / KG;
+      const __bf16* ka = reinterpret_cast<const __bf16*>(
+          arena + opaque(kao + (grp % 3) * Ly::KB + (ks - grp * KG) * 64));
+#pragma unroll
+      for (int rt = 0; rt < MT; ++rt) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&ka[rt * 16 * SK]);
+#pragma unroll
+        for (int c = 0; c < TW; ++c)
+          acc[rt][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[c], acc[rt][c], 0, 0, 0);
+      }
+    };
+#pragma unroll
+    for (int rt = 0; rt < MT; ++rt)
+#pragma unroll
+      for (int c = 0; c < TW; ++c) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < DB; ++d) loadB(d, q[d]);
+    lds_barrier();  // slab 0 filled
+    static_for<0, KS1>([&](auto kc) {
+      constexpr int ks = decltype(kc)::value;
+      mfma(ks, q[ks % DB]);
+      if constexpr (ks + DB < KS1) loadB(ks + DB, q[ks % DB]);
+      if constexpr (ks % KG == KG - 1) lds_barrier();  // slab consumed / next slab filled
+    });
+#pragma unroll
+    for (int c = 0; c < TW; ++c) b1q[c] = load_bias4(p.bias[0], ct[c] * 16 + (li & ~3), 512);
+  }
+}
+
+template <int MT, int NW, int OCC>
+__global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) {
 #pragma clang fp contract(off)
-  __shared__ __attribute__((aligned(16))) unsigned char arena[ARENA];
-  __shared__ float sth[MB][12];
-  __shared__ float szv[MB];
-  __shared__ int smask[MB];
-  __shared__ int ssep[MB];  // bit 0: theta_f axis-aligned, bit 1: theta_b (and tables fit)
+  using Ly = Lay<MT>;
+  constexpr int M = Ly::M;
+  constexpr int NTHR = NW * 64;
+  constexpr int TW = 64 / NW;  // recognition column tiles per MFMA wave
+  static_assert(MT <= NW && (NW == 8 || NW == 16), "shape");
+  __shared__ __attribute__((aligned(16))) unsigned char arena[Ly::ARENA];
+  __shared__ float sth[M][12];
+  __shared__ float szv[M];
+  __shared__ int smask[M];
+  __shared__ int ssep[M];  // bit 0: theta_f axis-aligned, bit 1: theta_b (and tables fit)
   const int tid = threadIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
-  const int b0 = blockIdx.x * MB;
-  const int nb = min(MB, p.B - b0);
+  const int b0 = blockIdx.x * M;
+  const int nb = min(M, p.B - b0);
   const int C = p.C, C2 = C * C;
-  unsigned char* sA = arena;
-  unsigned char* sHb = arena + A_BYTES;
-  __bf16* sG = reinterpret_cast<__bf16*>(sA);
-  __bf16* sA1 = reinterpret_cast<__bf16*>(sA);
-  __bf16* sD2 = reinterpret_cast<__bf16*>(sA);
-  float* sMu = reinterpret_cast<float*>(sA + OFF_MU);
-  float* sLv = reinterpret_cast<float*>(sA + OFF_LV);
-  float* sKl = reinterpret_cast<float*>(sA + OFF_KL);
-  __bf16* sZ = reinterpret_cast<__bf16*>(sA + OFF_Z);
-  float2* tabR = reinterpret_cast<float2*>(sHb);
-  __bf16* sA2 = reinterpret_cast<__bf16*>(sHb);
-  __bf16* sD1 = reinterpret_cast<__bf16*>(sHb);
-  float* sR = reinterpret_cast<float*>(arena);
-  float2* tabW = reinterpret_cast<float2*>(arena + OFF_TABW);
   STAMP(11);
 
-  for (int i = tid; i < MB * 12; i += NTHR) {
+  for (int i = tid; i < M * 12; i += NTHR) {
     const int m = i / 12, k = i % 12;
     float v = 0.0f;
     if (m < nb) v = k < 6 ? p.theta_f[(size_t)(b0 + m) * 6 + k] : p.theta_b[(size_t)(b0 + m) * 6 + k - 6];
     sth[m][k] = v;
   }
-  if (tid < MB) {
+  if (tid < M) {
     const bool act = tid < nb && p.mask[b0 + tid] != 0.0f;
     smask[tid] = act;
     szv[tid] = act ? p.zval[b0 + tid] : 0.0f;
   }
   lds_barrier();
   bool sep_f = true;
-  if (tid < MB) {
+  if (tid < M) {
     sep_f = stn_separable(&sth[tid][0]);
     ssep[tid] = (sep_f ? 1 : 0) | (stn_separable(&sth[tid][6]) && C <= CTAB_MAX ? 2 : 0);
   }
-  build_tables(tabR, sth, 0, MB, 0, C, C, 28, 28);
+  {  // read tables: column entries in pair form, row entries {lo, hi byte offsets, hi - c, c - lo}
+    float4* tabR = reinterpret_cast<float4*>(arena);
+    for (int i = tid; i < M * TABR; i += NTHR) {
+      const int m = i / TABR, n = i - (i / TABR) * TABR;
+      const float* th = sth[m];
+      tabR[i] = n < 28 ? col_pair4(axis_col(th, C, C, 28, 28, n), C)
+                       : axis4(axis_row(th, C, C, 28, 28, n - 28), 4 * C);
+    }
+  }
   const bool all_sep = __syncthreads_and(sep_f) != 0;  // (no global stores issued yet)
   STAMP(0);
 
-  // ---- 1. STN read (transformer.py:18-175): glimpse -> LDS bf16 ---------
-  // Half-wave per glimpse row (lane = column).  Axis-aligned transforms (every
-  // AIR theta): 14 rows per pass, 56 gathers per lane in flight, the bilinear
-  // weights re-read from the LDS axis tables once the gathers have landed
-  // (only the gathered values are live across the wait).  General affine
-  // transforms: eight rows per pass with per-sample geometry.
-  if ((p.phases & 1) && all_sep) {
-    // half-wave hw owns images 2hw and 2hw+1 (its row entries are broadcast
-    // LDS reads, the column pair per lane is fixed per image); 14 rows per
-    // pass, gathers through a buffer descriptor over this block's images
-    // (32-bit offsets).
-    static_assert(MB == 32 && NTHR == 512, "two images per half-wave");
-    const int hw = tid >> 5, j = tid & 31, jc = min(j, 27);
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(p.x) + (size_t)b0 * C2, 0, nb * C2 * 4, 0x00020000);
-    const int C4 = C * 4;
-#pragma unroll 1
-    for (int h = 0; h < 4; ++h) {
-      const int m = 2 * hw + (h >> 1), i0 = (h & 1) * 14;
-      const int mc = m < nb ? m : 0;
-      const float2* tr = tabR + mc * TABR;
-      const float2 cx = tr[jc];
-      const int xo = mc * C2 * 4;
-      const int xa = xo + axis_lo(cx) * 4, xb = xo + axis_hi(cx) * 4;
-      float I[14][4];
+  // ---- 1+2. STN read (transformer.py:18-175) -> a1 = softplus(g W1 + b1) --
+  {
+    floatx4 acc[MT][TW];
+    int ct[TW];
+    floatx4 b1q[TW];
+    if (all_sep) read_recognition<MT, NW, true>(p, arena, sth, b0, nb, acc, ct, b1q);
+    else read_recognition<MT, NW, false>(p, arena, sth, b0, nb, acc, ct, b1q);
+    STAMP(1);
+    __bf16* sA1 = reinterpret_cast<__bf16*>(arena);
+    const int li = lane & 15, g = lane >> 4;
+    if (wv < NW / 2) {  // the MFMA waves hold the layer
 #pragma unroll
-      for (int u = 0; u < 14; ++u) {
-        const float2 cy = tr[28 + i0 + u];
-        const int ya = __mul24(axis_lo(cy), C4), yb = __mul24(axis_hi(cy), C4);
-        I[u][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xa + ya, 0, 0));
-        I[u][1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xa + yb, 0, 0));
-        I[u][2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xb + ya, 0, 0));
-        I[u][3] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xb + yb, 0, 0));
-      }
-      asm volatile("" ::: "memory");  // re-read the tables below instead of keeping them live
-      const float2 cx2 = tr[jc];
-      const float4 ex = axis4(cx2, 1);
-      const bool xlive = m < nb && axis_lo(cx2) != axis_hi(cx2);
-      // branch-free: every lane samples; lanes 28..31 store into the unused
-      // row padding [800, 804) (beyond the GEMM's k extent)
-      __bf16* dst = sG + m * SG + (j < 28 ? i0 * 28 + j : KG + j - 28);
-      const int ustep = j < 28 ? 28 : 0;
+      for (int c = 0; c < TW; ++c) {
+        const int n0 = ct[c] * 16 + (li & ~3);
 #pragma unroll
-      for (int u = 0; u < 14; ++u) {
-        const float2 cy = tr[28 + i0 + u];
-        const float4 ey = axis4(cy, C);
-        const bool live = xlive || (m < nb && axis_lo(cy) != axis_hi(cy));  // not both axes dead
-        const float sv = sample4(ex, ey, I[u][0], I[u][1], I[u][2], I[u][3]);
-        dst[u * ustep] = (__bf16)(live ? sv : 0.0f);
+        for (int rt = 0; rt < MT; ++rt)
+          store_softplus4(sA1 + (rt * 16 + g * 4 + (li & 3)) * S512 + n0, quad_transpose(acc[rt][c]),
+                          b1q[c]);
       }
     }
-    for (int i = tid; i < MB * (KG - W2); i += NTHR) {  // zero k padding
-      const int m = i / (KG - W2);
-      sG[m * SG + W2 + (i - m * (KG - W2))] = (__bf16)0.0f;
-    }
-  } else if (p.phases & 1) {
-    constexpr int UR = 8;
-    const int hw = tid >> 5, j = tid & 31;
-    for (int rr0 = hw; rr0 < MB * 28; rr0 += 16 * UR) {
-      float I[UR][4];
-      float4 ex[UR], ey[UR];
-      bool live[UR];
-#pragma unroll
-      for (int u = 0; u < UR; ++u) {
-        const int rr = rr0 + 16 * u;
-        const int m = rr / 28, i = rr - (rr / 28) * 28;
-        live[u] = rr < MB * 28 && m < nb && j < 28;
-        const int mc = live[u] ? m : 0, jc = min(j, 27);
-        const float* U = p.x + (size_t)(b0 + mc) * C2;
-        if (ssep[mc] & 1) {
-          ex[u] = axis4(tabR[mc * TABR + jc], 1);
-          ey[u] = axis4(tabR[mc * TABR + 28 + i], C);
-        } else {  // general affine transform: per-sample geometry
-          const Tap t = stn_tap(sth[mc], C, C, mog_linspace(jc, 28), mog_linspace(i, 28));
-          ex[u] = make_float4(__int_as_float((int)t.x0f), __int_as_float((int)t.x1f),
-                              t.x1f - t.x, t.x - t.x0f);
-          ey[u] = make_float4(__int_as_float((int)t.y0f * C), __int_as_float((int)t.y1f * C),
-                              t.y1f - t.y, t.y - t.y0f);
-        }
-        live[u] = live[u] && !axis4_dead(ex[u], ey[u]);
-        const int x0 = __float_as_int(ex[u].x), x1 = __float_as_int(ex[u].y);
-        const int y0 = __float_as_int(ey[u].x), y1 = __float_as_int(ey[u].y);
-        // unpredicated (all indices are valid clipped corners of a real
-        // image) so the waitcnt pass keeps the 32 gathers in flight
-        I[u][0] = U[y0 + x0];
-        I[u][1] = U[y1 + x0];
-        I[u][2] = U[y0 + x1];
-        I[u][3] = U[y1 + x1];
-      }
-#pragma unroll
-      for (int u = 0; u < UR; ++u) {
-        const int rr = rr0 + 16 * u;
-        if (rr >= MB * 28 || j >= 28) continue;
-        const int m = rr / 28, i = rr - (rr / 28) * 28;
-        const float v = live[u] ? sample4(ex[u], ey[u], I[u][0], I[u][1], I[u][2], I[u][3]) : 0.0f;
-        sG[m * SG + i * 28 + j] = (__bf16)v;
-      }
-    }
-    for (int i = tid; i < MB * (KG - W2); i += NTHR) {  // zero k padding
-      const int m = i / (KG - W2);
-      sG[m * SG + W2 + (i - m * (KG - W2))] = (__bf16)0.0f;
-    }
-  }
-  lds_barrier();
-  STAMP(1);
-  if (p.phases & 16) flush_rows(sG, SG, p.gb + (size_t)b0 * W2, W2, W2, nb);
-
-  // ---- 2. a1 = softplus(g W1 + b1)  [MB x 512], over the glimpse ----------
-  if (p.phases & 2) {
-    const float* bias = p.bias[0];
-    dense_tiles<KG, 4, true>(sG, SG, p.wt[0], 0, 0, NW, [&](int ct, const floatx4* a) {
-      epi_rows(ct, a, 512, [&](int m, int n, float v) {
-        sA1[m * S512 + n] = (__bf16)softplus_fast(v + bias[n]);
-      });
-    });
   }
   lds_barrier();
   STAMP(2);
-  if (p.phases & 16) flush_rows(sA1, S512, p.a1b + (size_t)b0 * 512, 512, 512, nb);
-  // ---- 3. a2 = softplus(a1 W2 + b2)  [MB x 256] -> H ----------------------
+  __bf16* sA1 = reinterpret_cast<__bf16*>(arena);
+  __bf16* sA2 = sA1;
+  if (p.phases & 16) flush_rows<NTHR>(sA1, S512, p.a1b + (size_t)b0 * 512, 512, 512, nb);
+  // ---- 3. a2 = softplus(a1 W2 + b2)  [M x 256], in place ------------------
   if (p.phases & 2) {
-    const float* bias = p.bias[1];
-    dense_tiles<512, 2, false>(sA1, S512, p.wt[1], 0, 0, NW, [&](int ct, const floatx4* a) {
-      epi_rows(ct, a, 256, [&](int m, int n, float v) {
-        sA2[m * S256 + n] = (__bf16)softplus_fast(v + bias[n]);
-      });
-    });
+    dense_tiles<MT, 512, 16 / NW, 4, true>(sA1, S512, p.wt[1], p.bias[1], 256, 0, 0, NW,
+                                     [&](int m, int n0, const floatx4& v, const floatx4& b) {
+                                       store_softplus4(sA2 + m * S256 + n0, v, b);
+                                     });
   }
   lds_barrier();
   STAMP(3);
-  if (p.phases & 16) flush_rows(sA2, S256, p.a2b + (size_t)b0 * 256, 256, 256, nb);
-  // ---- 4. mu | lv = a2 W + b  [MB x 50] fp32 -> A (waves 0-3 | 4-7) ------
+  if (p.phases & 16) flush_rows<NTHR>(sA2, S256, p.a2b + (size_t)b0 * 256, 256, 256, nb);
+  // ---- 4. mu | lv = a2 W + b  [M x 50] fp32 (waves 0-3 | 4-7) -------------
+  float* sMu = reinterpret_cast<float*>(arena + Ly::OFF_MU);
+  float* sLv = reinterpret_cast<float*>(arena + Ly::OFF_LV);
   if (p.phases & 2) {
-    const float* bm = p.bias[2];
-    dense_tiles<256, 1, false>(sA2, S256, p.wt[2], 0, 0, 4, [&](int ct, const floatx4* a) {
-      epi_rows(ct, a, 50, [&](int m, int n, float v) { sMu[m * 50 + n] = v + bm[n]; });
-    });
-    const float* bl = p.bias[3];
-    dense_tiles<256, 1, false>(sA2, S256, p.wt[3], 0, 4, 4, [&](int ct, const floatx4* a) {
-      epi_rows(ct, a, 50, [&](int m, int n, float v) { sLv[m * 50 + n] = v + bl[n]; });
-    });
+    auto epi_f32 = [&](float* dst) {
+      return [dst](int m, int n0, const floatx4& v, const floatx4& b) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (n0 + k < 50) dst[m * 50 + n0 + k] = v[k] + b[k];
+      };
+    };
+    dense_tiles<MT, 256, 1, 4, false>(sA2, S256, p.wt[2], p.bias[2], 50, 0, 0, 4, epi_f32(sMu));
+    dense_tiles<MT, 256, 1, 4, false>(sA2, S256, p.wt[3], p.bias[3], 50, 0, 4, 4, epi_f32(sLv));
   }
   lds_barrier();
   STAMP(4);
   // ---- 5. z = mu + eps sqrt(exp(lv)); VAE KL -> runloss (vae.py:27-30) ---
-  for (int i = tid; i < MB * 64; i += NTHR) {
-    const int m = i >> 6, k = i & 63;
-    float zv = 0.0f;
-    if (k < 50 && m < nb) {
-      const size_t o = (size_t)(b0 + m) * 50 + k;
-      const float l = sLv[m * 50 + k];
-      const float mv = sMu[m * 50 + k];
-      const float var = mog_expf(l);
-      zv = mv + p.eps_z[o] * sqrtf(var);
-      p.mu[o] = mv;
-      p.lv[o] = l;
-      p.z[o] = zv;
-      p.zb[(size_t)(b0 + m) * 56 + k] = (__bf16)zv;
-      const float d = mv - p.v_pm;
-      sKl[m * 50 + k] = (((p.v_plv - l) - 1.0f) + var / p.v_pv) + (d * d) / p.v_pv;
+  float* sKl = reinterpret_cast<float*>(arena + Ly::OFF_KL);
+  __bf16* sZ = reinterpret_cast<__bf16*>(arena + Ly::OFF_Z);
+  {
+    constexpr int NS = M * 64 / NTHR;
+    float ez[NS];
+#pragma unroll
+    for (int it = 0; it < NS; ++it) {
+      const int i = tid + it * NTHR, m = i >> 6, k = i & 63;
+      ez[it] = (k < 50 && m < nb) ? p.eps_z[(size_t)(b0 + m) * 50 + k] : 0.0f;
     }
-    sZ[m * SZ + k] = (__bf16)zv;
+#pragma unroll
+    for (int it = 0; it < NS; ++it) {
+      const int i = tid + it * NTHR, m = i >> 6, k = i & 63;
+      float zv = 0.0f;
+      if (k < 50 && m < nb) {
+        const size_t o = (size_t)(b0 + m) * 50 + k;
+        const float l = sLv[m * 50 + k];
+        const float mv = sMu[m * 50 + k];
+        const float var = mog_expf(l);
+        zv = mv + ez[it] * sqrtf(var);
+        p.mu[o] = mv;
+        p.lv[o] = l;
+        p.z[o] = zv;
+        p.zb[(size_t)(b0 + m) * 56 + k] = (__bf16)zv;
+        const float d = mv - p.v_pm;
+        sKl[m * 50 + k] = (((p.v_plv - l) - 1.0f) + var / p.v_pv) + (d * d) / p.v_pv;
+      }
+      sZ[m * SZ + k] = (__bf16)zv;
+    }
   }
   lds_barrier();
   if (tid < nb) {  // sequential KL sum per image (k order, as vae_sample_fwd_kernel)
@@ -467,98 +723,102 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
     if (smask[m]) p.runloss[b0 + m] = p.runloss[b0 + m] + vkl;
   }
   STAMP(5);
-  // ---- 6. d1 = softplus(z Wg1 + b)  [MB x 256] -> H -----------------------
+  // ---- 6. d1 = softplus(z Wg1 + b)  [M x 256] (over mu | lv) ---------------
+  __bf16* sD1 = reinterpret_cast<__bf16*>(arena + Ly::OFF_D1);
   if (p.phases & 2) {
-    const float* bias = p.bias[4];
-    dense_tiles<64, 2, false>(sZ, SZ, p.wt[4], 0, 0, NW, [&](int ct, const floatx4* a) {
-      epi_rows(ct, a, 256, [&](int m, int n, float v) {
-        sD1[m * S256 + n] = (__bf16)softplus_fast(v + bias[n]);
-      });
-    });
+    dense_tiles<MT, 64, 16 / NW, 2, false>(sZ, SZ, p.wt[4], p.bias[4], 256, 0, 0, NW,
+                                     [&](int m, int n0, const floatx4& v, const floatx4& b) {
+                                       store_softplus4(sD1 + m * S256 + n0, v, b);
+                                     });
   }
   lds_barrier();
   STAMP(6);
-  if (p.phases & 16) flush_rows(sD1, S256, p.d1b + (size_t)b0 * 256, 256, 256, nb);
-  // ---- 7. d2 = softplus(d1 Wg2 + b)  [MB x 512] -> A ----------------------
+  if (p.phases & 16) flush_rows<NTHR>(sD1, S256, p.d1b + (size_t)b0 * 256, 256, 256, nb);
+  // ---- 7. d2 = softplus(d1 Wg2 + b)  [M x 512] at 0 (in place over d1) -----
+  __bf16* sD2 = reinterpret_cast<__bf16*>(arena);
   if (p.phases & 2) {
-    const float* bias = p.bias[5];
-    dense_tiles<256, 4, false>(sD1, S256, p.wt[5], 0, 0, NW, [&](int ct, const floatx4* a) {
-      epi_rows(ct, a, 512, [&](int m, int n, float v) {
-        sD2[m * S512 + n] = (__bf16)softplus_fast(v + bias[n]);
-      });
-    });
+    dense_tiles<MT, 256, 32 / NW, NW / 4, true>(sD1, S256, p.wt[5], p.bias[5], 512, 0, 0, NW,
+                                     [&](int m, int n0, const floatx4& v, const floatx4& b) {
+                                       store_softplus4(sD2 + m * S512 + n0, v, b);
+                                     });
   }
   lds_barrier();
   STAMP(7);
-  if (p.phases & 16) flush_rows(sD2, S512, p.d2b + (size_t)b0 * 512, 512, 512, nb);
-  // ---- 8. r = sigmoid(d2 Wgo + b + std eps)  [MB x 784] fp32 -> HBM -------
-  // Each 32 x 16 accumulator tile goes through the wave's LDS scratch so that
-  // a lane owns four consecutive pixels of one row: one Philox quad of eps_x
-  // (generated in-kernel exactly as mog_rng_fill would, or loaded), one
-  // 16-byte store of r.  49 column tiles: 32 (4 per wave) + 16 (2) + 1 (wave 0).
+  if (p.phases & 16) flush_rows<NTHR>(sD2, S512, p.d2b + (size_t)b0 * 512, 512, 512, nb);
+  // ---- 8. r = sigmoid(d2 Wgo + b + std eps)  [M x 784] fp32 -> HBM ----------
+  // The 4 x 4 accumulator quads are transposed across lanes (two DPP quad
+  // exchanges) so that a lane owns four consecutive pixels of one row: one
+  // Philox quad of eps_x (generated in-kernel exactly as mog_rng_fill would,
+  // or loaded), one 16-byte store of r.  49 column tiles: 32 (2 per wave) + 16
+  // (1 per wave) + 1 split over the row tiles.
   if (p.phases & 2) {
-    const float* bias = p.bias[6];
     const float sd = p.lik_std;
-    float* xp = reinterpret_cast<float*>(arena + OFF_XP + wv * XP_WAVE);
-    auto epi = [&](int ct, const floatx4* a) {
-      const int li = lane & 15, g = lane >> 4;
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) xp[(rt * 16 + g * 4 + r) * XP_STRIDE + li] = a[rt][r];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const int cq = lane & 3, n = ct * 16 + 4 * cq;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int m = h * 16 + (lane >> 2);
-        const float4 v = *reinterpret_cast<const float4*>(&xp[m * XP_STRIDE + 4 * cq]);
-        if (m < nb && n < W2) {
-          float e[4];
-          const size_t q = (size_t)(b0 + m) * (W2 / 4) + (n >> 2);
-          if (p.eps_gen) {
-            mog_philox_quad(p.eps_seed, p.eps_offset + q, true, e);
-          } else {
-            const float4 e4 = reinterpret_cast<const float4*>(p.eps_x)[q];
-            e[0] = e4.x; e[1] = e4.y; e[2] = e4.z; e[3] = e4.w;
-          }
-          const float vv[4] = {v.x, v.y, v.z, v.w};
-          float o[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float y = __builtin_fmaf(e[k], sd, vv[k] + bias[n + k]);
-            o[k] = 1.0f / (1.0f + __expf(-y));
-          }
-          reinterpret_cast<float4*>(p.r)[q] = make_float4(o[0], o[1], o[2], o[3]);
+    auto epi = [&](int m, int n, const floatx4& v, const floatx4& b) {
+      if (m < nb) {
+        float ev[4];
+        const size_t q = (size_t)(b0 + m) * (W2 / 4) + (n >> 2);
+        if (p.eps_gen) {
+          mog_philox_quad(p.eps_seed, p.eps_offset + q, true, ev);
+        } else {
+          const float4 e4 = reinterpret_cast<const float4*>(p.eps_x)[q];
+          ev[0] = e4.x; ev[1] = e4.y; ev[2] = e4.z; ev[3] = e4.w;
         }
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float y = __builtin_fmaf(ev[k], sd, v[k] + b[k]);
+          o[k] = mog_sigmoid_hw(y);
+        }
+        reinterpret_cast<float4*>(p.r)[q] = make_float4(o[0], o[1], o[2], o[3]);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // scratch reads before the next tile
     };
-    dense_tiles<512, 4, false>(sD2, S512, p.wt[6], 0, 0, NW, epi);
-    dense_tiles<512, 2, false>(sD2, S512, p.wt[6], 32, 0, NW, epi);
-    dense_tiles<512, 1, false>(sD2, S512, p.wt[6], 48, 0, 1, epi);
+    dense_tiles<MT, 512, 32 / NW, NW / 4, false>(sD2, S512, p.wt[6], p.bias[6], W2, 0, 0, NW, epi);
+    dense_tiles<MT, 512, 16 / NW, 4, false>(sD2, S512, p.wt[6], p.bias[6], W2, 32, 0, NW, epi);
+    dense_rowsplit<MT, 512>(sD2, S512, p.wt[6], p.bias[6], W2, 48, epi);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // r stores done before other waves read it
   lds_barrier();
   STAMP(8);
   STAMP(9);
   // ---- 9. STN write (air_model.py:580-588): this step's canvas part -------
-  // part = active ? z * w : 0 for every pixel (write-only; mog_recon_loss sums
-  // the parts in step order).  r is staged back from L2 sixteen images at a
-  // time; one wave per image; each lane produces four consecutive canvas
-  // pixels (flat order) and stores them with one 16-byte store.  Dead samples
-  // (clipped corners coincide on both axes) are exactly +0 and are selected,
-  // not branched.
+  // part = active ? z * w : 0 (mog_recon_loss sums the parts in step order).
+  // r is staged back RH images at a time; one wave per image; each lane
+  // produces four consecutive canvas pixels (flat order) and stores them with
+  // one 16-byte store.  Only rows whose clipped corner rows differ can be
+  // nonzero; the band-aligned range of them is stored and recorded.  Dead
+  // samples (clipped corners coincide on both axes) are exactly +0 and are
+  // selected, not branched.
   if (p.phases & 8) {
+    constexpr int RH = Ly::RH;
+    float* sR = reinterpret_cast<float*>(arena);
+    float4* tabW = reinterpret_cast<float4*>(arena + Ly::OFF_TABW);
     const bool vec = (C2 & 3) == 0;  // even C: 16-byte aligned image rows of parts
+    // r of the next group is fetched into registers while this group computes
+    constexpr int NL = (RH * (W2 / 4) + NTHR - 1) / NTHR;
+    float4 tmp[NL];
+    auto fetch = [&](int h0) {
+      const int nh = min(RH, nb - h0);
+      const float4* src = reinterpret_cast<const float4*>(p.r + (size_t)(b0 + h0) * W2);
+#pragma unroll
+      for (int it = 0; it < NL; ++it) {
+        const int i = tid + it * NTHR;
+        if (i < nh * (W2 / 4)) tmp[it] = src[i];
+      }
+    };
+    fetch(0);
     for (int h0 = 0; h0 < nb; h0 += RH) {
       const int nh = min(RH, nb - h0);
       {
-        const float4* src = reinterpret_cast<const float4*>(p.r + (size_t)(b0 + h0) * W2);
         float4* dst = reinterpret_cast<float4*>(sR);
-        for (int i = tid; i < nh * (W2 / 4); i += NTHR) dst[i] = src[i];
+#pragma unroll
+        for (int it = 0; it < NL; ++it) {
+          const int i = tid + it * NTHR;
+          if (i < nh * (W2 / 4)) dst[i] = tmp[it];
+        }
       }
-      if (C <= CTAB_MAX) build_tables(tabW, sth, h0, nh, 6, 28, 28, C, C);
+      if (C <= CTAB_MAX) build_tables4<NTHR>(tabW, sth, h0, nh, 6, 28, 28, C, C);
       lds_barrier();
+      if (h0 + RH < nb) fetch(h0 + RH);
       for (int mm = wv; mm < nh; mm += NW) {
         const int m = h0 + mm;
         float* om = p.part + (size_t)(b0 + m) * C2;
@@ -566,57 +826,48 @@ __global__ __launch_bounds__(NTHR, 4) void stn_vae_step_bf16_kernel(StepArgs p) 
         const float* U = sR + mm * W2;
         const bool act = smask[m] != 0, tab = (ssep[m] & 2) != 0;
         const float zn = szv[m];
-        const float2* tcol = tabW + mm * 2 * C;
-        const float2* trow = tcol + C;
-        if (!act) {  // inactive: the whole part is +0
-          const int nq = vec ? C2 / 4 : C2;
-          for (int q = lane; q < nq; q += 64) {
-            if (vec) om4[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            else om[q] = 0.0f;
-          }
-        } else if (tab && vec && C <= 128) {
-          // Two-row bands of C/2 16-byte quads: a lane keeps the same four
-          // columns (its x entries stay in registers) across every band and
-          // reads only the two row entries per band.
-          const int QB = C >> 1, NBW = 64 / QB;
-          const bool ln = lane < NBW * QB;
-          const int k = ln ? lane % QB : 0, bs = lane / QB;
-          float4 ex[4];
-          bool br[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int pp = 4 * k + e;
-            br[e] = pp >= C;
-            ex[e] = axis4(tcol[br[e] ? pp - C : pp], 1);
-          }
-          for (int bb = 0; bb < QB; bb += NBW) {
-            const int b = bb + bs;
-            const bool on = ln && b < QB;
-            const float4 ey0 = axis4(trow[on ? 2 * b : 0], 28), ey1 = axis4(trow[on ? 2 * b + 1 : 0], 28);
-            // A row whose clipped corner rows coincide samples exactly +0 at
-            // every column (the y weights are exact negatives on one source
-            // row, so the four products cancel pairwise in summation order):
-            // bands where the whole wave sees only such rows store zeros.
-            const bool rows_live = on && (__float_as_int(ey0.x) != __float_as_int(ey0.y) ||
-                                          __float_as_int(ey1.x) != __float_as_int(ey1.y));
-            if (__builtin_amdgcn_ballot_w64(rows_live) == 0) {
-              if (on) om4[b * QB + k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-              continue;
-            }
-            if (!on) continue;
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float4 ey = br[e] ? ey1 : ey0;
-              const int x0 = __float_as_int(ex[e].x), x1 = __float_as_int(ex[e].y);
-              const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
-              const float sv = zn * sample4(ex[e], ey, U[y0 + x0], U[y1 + x0], U[y0 + x1],
-                                            U[y1 + x1]);
-              v[e] = axis4_dead(ex[e], ey) ? 0.0f : sv;
-            }
-            om4[b * QB + k] = make_float4(v[0], v[1], v[2], v[3]);
+        const float4* tcol = tabW + mm * 2 * C;
+        const float4* trow = tcol + C;
+        if (!act) {  // inactive: the whole part is +0 -- nothing stored
+          if (lane == 0) p.part_rows[b0 + m] = 0;
+        } else if (tab && vec && C <= CTAB_MAX) {
+          // Only rows whose clipped corner rows differ can be nonzero (a row
+          // with coinciding corner rows samples exactly +0 at every column:
+          // the y weights are exact negatives on one source row, and within
+          // a live row no sample is dead): store the even-aligned range
+          // [rlo, rhi) of such rows and record it.
+          const float4 el = trow[lane < C ? lane : 0];
+          const unsigned long long lm =
+              __builtin_amdgcn_ballot_w64(lane < C && __float_as_int(el.x) != __float_as_int(el.y));
+          const int rlo = lm ? (__builtin_ctzll(lm) & ~1) : 0;
+          const int rhi = lm ? min(C, (64 - __builtin_clzll(lm) + 1) & ~1) : 0;
+          if (lane == 0) p.part_rows[b0 + m] = rlo | (rhi << 16);
+          // Pixel pairs of the range, flattened over the wave: a lane reads
+          // its row entry and two column entries, gathers 8 corners from the
+          // staged r, computes both samples with packed fp32 ops (the same
+          // products and summation order as sample4, per pixel) and stores
+          // 8 bytes.
+          const int PR = C >> 1;  // pairs per row
+          const int np = (rhi - rlo) * PR;
+          typedef float f2 __attribute__((ext_vector_type(2)));
+          for (int idx = lane; idx < np; idx += 64) {
+            const int rr = idx / PR, pr = idx - rr * PR;
+            const int row = rlo + rr;
+            const float4 ey = trow[row];
+            const float4 e0 = tcol[2 * pr], e1 = tcol[2 * pr + 1];
+            const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
+            const int a0 = __float_as_int(e0.x), c0 = __float_as_int(e0.y);
+            const int a1 = __float_as_int(e1.x), c1 = __float_as_int(e1.y);
+            const f2 Ia = {U[y0 + a0], U[y0 + a1]}, Ib = {U[y1 + a0], U[y1 + a1]};
+            const f2 Ic = {U[y0 + c0], U[y0 + c1]}, Id = {U[y1 + c0], U[y1 + c1]};
+            const f2 xz = {e0.z, e1.z}, xw = {e0.w, e1.w};
+            const f2 wa = xz * ey.z, wb = xz * ey.w, wc = xw * ey.z, wd = xw * ey.w;
+            const f2 sv = ((wa * Ia + wb * Ib) + wc * Ic) + wd * Id;
+            const f2 v = zn * sv;
+            *reinterpret_cast<f2*>(om + row * C + 2 * pr) = v;
           }
         } else {  // general transform or odd C: per-pixel geometry, flat order
+          if (lane == 0) p.part_rows[b0 + m] = C << 16;
           const int nq = vec ? C2 / 4 : C2;
           const int per = vec ? 4 : 1;
           for (int q = lane; q < nq; q += 64) {
@@ -656,14 +907,14 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
                                         unsigned long long eps_offset, const void* const* wt,
                                         const float* const* bias, float lik_std, float v_pm,
                                         float v_pv, float v_plv, float* canvas_part,
-                                        float* runloss, float* vkl, void* gb, void* a1b,
-                                        void* a2b, float* mu, float* lv, float* z, void* zb,
-                                        void* d1b, void* d2b, float* r, void* stream) {
-  MOG_CHECK_ARG(B >= 0 && C > 0 && C * C <= 16384);
+                                        int* part_rows, float* runloss, float* vkl, void* gb,
+                                        void* a1b, void* a2b, float* mu, float* lv, float* z,
+                                        void* zb, void* d1b, void* d2b, float* r, void* stream) {
+  MOG_CHECK_ARG(B >= 0 && C >= 2 && C * C <= 16384);
   // the tile shapes are compiled for the reference's default VAE
   MOG_CHECK_ARG(W == 28 && R1 == 512 && R2 == 256 && Z == 50 && G1 == 256 && G2 == 512);
   MOG_CHECK_ARG(x && theta_f && theta_b && mask && zval && eps_z && (eps_x || eps_gen) && wt && bias);
-  MOG_CHECK_ARG(canvas_part && runloss && vkl && gb && a1b && a2b && mu && lv && z && zb);
+  MOG_CHECK_ARG(canvas_part && part_rows && runloss && vkl && gb && a1b && a2b && mu && lv && z && zb);
   MOG_CHECK_ARG(d1b && d2b && r);
   if (B == 0) return 0;
   StepArgs p;
@@ -675,7 +926,7 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
     p.wt[i] = reinterpret_cast<const __bf16*>(wt[i]);
     p.bias[i] = bias[i];
   }
-  p.part = canvas_part; p.runloss = runloss; p.vkl = vkl;
+  p.part = canvas_part; p.part_rows = part_rows; p.runloss = runloss; p.vkl = vkl;
   p.gb = reinterpret_cast<__bf16*>(gb); p.a1b = reinterpret_cast<__bf16*>(a1b);
   p.a2b = reinterpret_cast<__bf16*>(a2b); p.mu = mu; p.lv = lv; p.z = z;
   p.zb = reinterpret_cast<__bf16*>(zb); p.d1b = reinterpret_cast<__bf16*>(d1b);
@@ -683,11 +934,21 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   const char* ph = getenv("MOG_VS_PHASES");
   p.phases = ph ? atoi(ph) : 31;
   p.B = B; p.C = C; p.lik_std = lik_std; p.v_pm = v_pm; p.v_pv = v_pv; p.v_plv = v_plv;
+  // Tile height: 64 images per workgroup (one per CU) once the batch gives
+  // every CU at least one such tile, else 32 so small batches still spread
+  // over the chip (two 8-wave workgroups per CU).  MOG_VS_MT overrides: 4 =
+  // 64 images x 16 waves, 2 = 32 images x 8 waves, 3 = 32 images x 16 waves.
+  int mt = B >= 256 * 64 ? 4 : 2;
+  if (const char* e = getenv("MOG_VS_MT")) {
+    const int v = atoi(e);
+    if (v == 2 || v == 3 || v == 4) mt = v;
+  }
+  const int M = 16 * (mt == 3 ? 2 : mt);
   // MOG_VS_TIMING=1 (profiling aid): per-phase durations, averaged over
   // blocks, printed to stderr (synchronizes the stream)
   static long long* tbuf = nullptr;
   static size_t tcap = 0;
-  const unsigned nblk = mog_cdiv(B, MB);
+  const unsigned nblk = mog_cdiv(B, M);
   p.tstamp = nullptr;
   if (getenv("MOG_VS_TIMING")) {
     if (tcap < (size_t)nblk * 16) {
@@ -697,12 +958,15 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
     }
     p.tstamp = tbuf;
   }
-  stn_vae_step_bf16_kernel<<<nblk, NTHR, 0, mog_stream(stream)>>>(p);
+  hipStream_t s = mog_stream(stream);
+  if (mt == 4) stn_vae_step_kernel<4, 16, 4><<<nblk, 1024, 0, s>>>(p);
+  else if (mt == 2) stn_vae_step_kernel<2, 8, 4><<<nblk, 512, 0, s>>>(p);
+  else stn_vae_step_kernel<2, 16, 4><<<nblk, 1024, 0, s>>>(p);
   if (p.tstamp) {
     std::vector<long long> h((size_t)nblk * 16);
-    (void)hipStreamSynchronize(mog_stream(stream));
+    (void)hipStreamSynchronize(s);
     (void)hipMemcpy(h.data(), tbuf, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
-    static const char* names[10] = {"stn_read", "L1", "L2", "mu_lv", "sample",
+    static const char* names[10] = {"read+L1", "L1epi", "L2", "mu_lv", "sample",
                                     "g1", "g2", "go", "-", "write"};
     double acc[11] = {0}, pro = 0;
     long long t0 = h[0], t1 = h[10];
@@ -713,8 +977,8 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
       t0 = std::min(t0, h[b * 16]);
       t1 = std::max(t1, h[b * 16 + 10]);
     }
-    fprintf(stderr, "stn_vae_step phases (us, mean over %u blocks; 100 MHz clock): prologue %.2f",
-            nblk, pro / nblk / 100.0);
+    fprintf(stderr, "stn_vae_step M=%d phases (us, mean over %u blocks; 100 MHz clock): prologue %.2f",
+            M, nblk, pro / nblk / 100.0);
     for (int k = 0; k < 10; ++k) fprintf(stderr, " %s %.2f", names[k], acc[k] / nblk / 100.0);
     fprintf(stderr, " | block %.2f | span %.2f\n", acc[10] / nblk / 100.0, (t1 - t0) / 100.0);
   }

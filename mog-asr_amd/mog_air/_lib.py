@@ -33,13 +33,13 @@ _SIGS = {
     "mog_air_step_backward": [I, I, I, I, F, F, F, F, F, F, F, F, P, P, P, P, P, P, P, P, P,
                               L, P, L, P],
     "mog_vae_sample_forward": [I, I, F, F, F, P, P, P, P, P, I, P, P, P, P],
-    "mog_stn_vae_step_forward": [I] * 8 + [P] * 7 + [I, ULL, ULL] + [P] * 2 + [F] * 4 + [P] * 14,
+    "mog_stn_vae_step_forward": [I] * 8 + [P] * 7 + [I, ULL, ULL] + [P] * 2 + [F] * 4 + [P] * 15,
     "mog_vae_sample_backward": [I, I, F, F, F, P, P, P, P, P, P, P, P, P, I, P],
     "mog_sigmoid_backward": [P, P, P, L, I, P],
     "mog_gemm_bf16": [I, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, I, P],
     "mog_cvt_bf16": [P, I, I, I, P, I, I, I, I, P],
     "mog_cvt_bf16_batch": [I, P, P, P, P],
-    "mog_recon_loss": [P, P, P, I, L, P, P, P, I, I, F, P, P, P, P, P, P, P],
+    "mog_recon_loss": [P, P, P, I, L, P, I, P, P, P, I, I, F, P, P, P, P, P, P, P],
     "mog_batch_mean": [P, P, P, P, I, P, P],
     "mog_colsum_add": [P, I, I, I, P, P],
     "mog_add": [P, P, P, L, P],

@@ -126,6 +126,8 @@ class _Workspace:
         self.canvas = e(B, C2)
         # fused bf16 step: per-step canvas contributions, summed by the loss kernel
         self.cparts = e(T, B, C2) if m.fused_step else None
+        self.prows = (torch.empty((T, B), device=dev, dtype=torch.int32)
+                      if m.fused_step else None)
         self.stop, self.runloss = e(B), e(B)
         self.digits = torch.empty(B, device=dev, dtype=torch.int32)
         self.live = torch.empty(T + 1, device=dev, dtype=torch.int32)
@@ -435,7 +437,8 @@ class AIRModel:
         gscale = 1.0 / (B * self.grad_world)
         canvas_ptr = dp(ws.canvas) if (outputs or parts is None) else None
         _lib.call("mog_recon_loss", dp(X), canvas_ptr, dp(parts),
-                  self.max_steps if parts is not None else 0, B * C2, dp(ws.runloss),
+                  self.max_steps if parts is not None else 0, B * C2, dp(ws.prows),
+                  self.canvas_size, dp(ws.runloss),
                   dp(ws.digits), dp(targets), B, C2, float(gscale),
                   dp(ws.recon) if outputs else None, dp(ws.bce), dp(ws.mse),
                   dp(ws.loss_b), dp(ws.acc_b) if targets is not None else None,
@@ -699,7 +702,8 @@ class AIRModel:
                   dp(ws.zval[t]), dp(ws.eps_z[t]), dp(ws.eps_x[t]), int(gen),
                   self.noise_seed & (2 ** 64 - 1), off & (2 ** 64 - 1), wt, bias, lik_std,
                   float(self.vae_prior_mean), float(self.vae_prior_variance),
-                  self.vae_prior_log_variance, dp(ws.cparts[t]), dp(ws.runloss), dp(ws.vkl[t]),
+                  self.vae_prior_log_variance, dp(ws.cparts[t]), dp(ws.prows[t]),
+                  dp(ws.runloss), dp(ws.vkl[t]),
                   dp(ws.gb[t]), dp(ws.a1b[t]), dp(ws.a2b[t]), dp(ws.mu[t]), dp(ws.lv[t]),
                   dp(ws.z[t]), dp(ws.zb[t]), dp(ws.d1b[t]), dp(ws.d2b[t]), dp(ws.r[t]),
                   stream_ptr())

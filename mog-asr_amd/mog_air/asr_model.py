@@ -357,7 +357,7 @@ class AIRModel(_AirBase):
         gscale = 1.0 / (B * self.grad_world)
         canvas_ptr = dp(ws.canvas) if (outputs or parts is None) else None
         _lib.call("mog_recon_loss", dp(X), canvas_ptr, dp(parts), T if parts is not None else 0,
-                  B * C2, dp(ws.klsum), dp(ws.digits), dp(targets), B, C2, float(gscale),
+                  B * C2, dp(ws.prows), self.canvas_size, dp(ws.klsum), dp(ws.digits), dp(targets), B, C2, float(gscale),
                   dp(ws.recon) if outputs else None, dp(ws.bce), dp(ws.mse), dp(ws.loss_b),
                   dp(ws.acc_b) if targets is not None else None,
                   dp(ws.dcanvas) if need_grad else None, s)
