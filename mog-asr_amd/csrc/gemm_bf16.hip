@@ -378,34 +378,36 @@ struct CvtBatch {
   const float* src[CVT_MAX];
   __bf16* dst[CVT_MAX];
   int d[CVT_MAX][7];  // src_rows, src_cols, ld_src, rows, cols, ld_dst, transpose
-  long start[CVT_MAX + 1];
+  int count[CVT_MAX];  // rows * cols of each job (< 2^31)
   int n;
 };
 
+// One grid row (blockIdx.y) per job, 32-bit index arithmetic throughout (every
+// pack is far below 2^31 elements; 64-bit divisions per element cost more than
+// the copy itself).
 __global__ __launch_bounds__(256) void cvt_bf16_batch_kernel(CvtBatch b) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= b.start[b.n]) return;
-  int j = 0;
-  while (i >= b.start[j + 1]) ++j;
+  const int j = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= b.count[j]) return;
   const int* d = b.d[j];
-  const long e = i - b.start[j];
+  const float* src = b.src[j];
   if (d[6] == 2) {
     // MFMA B-fragment order of W^T (vae_step.hip): element e = ((ct * KS + ks)
     // * 64 + lane) * 8 + q holds W^T[ct*16 + lane%16][ks*32 + 8*(lane/16) + q],
     // so one 16-B-per-lane wave load is 1 KiB contiguous
-    const int q = (int)(e & 7), l = (int)((e >> 3) & 63);
-    const long f = e >> 9;                       // ct * KS + ks
-    const int KS = d[4] / 32;
-    const int ct = (int)(f / KS), ks = (int)(f - (long)ct * KS);
+    const int q = e & 7, l = (e >> 3) & 63;
+    const int f = e >> 9;                        // ct * KS + ks
+    const int KS = d[4] >> 5;
+    const int ct = f / KS, ks = f - ct * KS;
     const int n = ct * 16 + (l & 15), k = ks * 32 + 8 * (l >> 4) + q;
-    const float v = (k < d[0] && n < d[1]) ? b.src[j][(size_t)k * d[2] + n] : 0.0f;
+    const float v = (k < d[0] && n < d[1]) ? src[k * d[2] + n] : 0.0f;
     b.dst[j][e] = (__bf16)v;
     return;
   }
-  const int r = e / d[4], c = e - (long)r * d[4];
+  const int r = e / d[4], c = e - r * d[4];
   const int sr = d[6] ? c : r, sc = d[6] ? r : c;
-  const float v = (sr < d[0] && sc < d[1]) ? b.src[j][(size_t)sr * d[2] + sc] : 0.0f;
-  b.dst[j][(size_t)r * d[5] + c] = (__bf16)v;
+  const float v = (sr < d[0] && sc < d[1]) ? src[sr * d[2] + sc] : 0.0f;
+  b.dst[j][r * d[5] + c] = (__bf16)v;
 }
 }  // namespace
 
@@ -414,16 +416,21 @@ extern "C" int mog_cvt_bf16_batch(int njobs, const float* const* src, void* cons
   MOG_CHECK_ARG(njobs >= 0 && njobs <= CVT_MAX && (njobs == 0 || (src && dst && dims)));
   CvtBatch b;
   b.n = njobs;
-  b.start[0] = 0;
+  long mx = 0;
   for (int j = 0; j < njobs; ++j) {
     MOG_CHECK_ARG(src[j] && dst[j] && dims[7 * j + 3] >= 0 && dims[7 * j + 4] >= 0);
+    const long cnt = (long)dims[7 * j + 3] * dims[7 * j + 4];
+    const long lds = (long)dims[7 * j + 5] * (dims[7 * j + 6] == 2 ? 1 : dims[7 * j + 3]);
+    const long lsrc = (long)dims[7 * j + 0] * dims[7 * j + 2];
+    MOG_CHECK_ARG(cnt < (1L << 31) && lds < (1L << 31) && lsrc < (1L << 31));
     b.src[j] = src[j];
     b.dst[j] = reinterpret_cast<__bf16*>(dst[j]);
     for (int k = 0; k < 7; ++k) b.d[j][k] = dims[7 * j + k];
-    b.start[j + 1] = b.start[j] + (long)dims[7 * j + 3] * dims[7 * j + 4];
+    b.count[j] = (int)cnt;
+    mx = cnt > mx ? cnt : mx;
   }
-  if (njobs == 0 || b.start[njobs] == 0) return 0;
-  cvt_bf16_batch_kernel<<<mog_cdiv(b.start[njobs], 256), 256, 0, mog_stream(stream)>>>(b);
+  if (njobs == 0 || mx == 0) return 0;
+  cvt_bf16_batch_kernel<<<dim3(mog_cdiv(mx, 256), njobs), 256, 0, mog_stream(stream)>>>(b);
   MOG_LAUNCH_RET();
 }
 

@@ -938,7 +938,7 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   // every CU at least one such tile, else 32 so small batches still spread
   // over the chip (two 8-wave workgroups per CU).  MOG_VS_MT overrides: 4 =
   // 64 images x 16 waves, 2 = 32 images x 8 waves, 3 = 32 images x 16 waves.
-  int mt = B >= 256 * 64 ? 4 : 2;
+  int mt = B >= 256 * 64 ? 4 : 3;
   if (const char* e = getenv("MOG_VS_MT")) {
     const int v = atoi(e);
     if (v == 2 || v == 3 || v == 4) mt = v;
