@@ -412,6 +412,7 @@ __device__ __forceinline__ void read_recognition(const StepArgs& p, unsigned cha
                                                  const float (*sth)[12], int b0, int nb,
                                                  floatx4 (&acc)[MT][64 / NW], int (&ct)[64 / NW],
                                                  floatx4 (&b1q)[64 / NW]) {
+#pragma clang fp contract(off)
   using Ly = Lay<MT>;
   constexpr int M = Ly::M;
   constexpr int NTHR = NW * 64;

@@ -49,11 +49,12 @@ def main():
                     "gfx950 FETCH_SIZE halving corrected; averaged over the largest-fetch "
                     "dispatch of the tagged kernel symbol per train step"}
     jobs = [(tag, sym, None) for tag, sym in TAGS.items()]
-    # the fused step kernel runs at the bench batch (8192: 256 workgroups of
-    # 512 threads) and in the stand-alone north-star roofline run (65,536)
+    # the fused step kernel runs at the bench batch (8192: 256 workgroups of 32
+    # images x 1024 threads) and in the stand-alone north-star roofline run
+    # (65,536: 1024 workgroups of 64 images x 1024 threads)
     jobs = [j for j in jobs if j[0] != "stn_vae_step"] + [
-        ("stn_vae_step", "stn_vae_step", 8192 // 32 * 512),
-        ("stn_vae_step_b65536", "stn_vae_step", 65536 // 32 * 512)]
+        ("stn_vae_step", "stn_vae_step", 8192 // 32 * 1024),
+        ("stn_vae_step_b65536", "stn_vae_step", 65536 // 64 * 1024)]
     for tag, sym, grid in jobs:
         fv, wv = per_kernel(fetch, sym, grid), per_kernel(write, sym, grid)
         if not fv or not wv:
