@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import Dict, Optional
 
 import numpy as np
@@ -741,7 +742,8 @@ class AIRModel:
         big = M >= 128 and N >= 128
         tiles = ((M + 127) // 128) * ((N + 127) // 128) if big else \
             ((M + 63) // 64) * ((N + 63) // 64)
-        splitk = max(1, min(K // 512, (1024 + tiles - 1) // tiles))
+        target = int(os.environ.get("MOG_DW_TARGET", "256"))
+        splitk = max(1, min(K // 512, (target + tiles - 1) // tiles))
         gemm_bf16([X], [dY], [out], M, N, K, lda, ldb, N, tn=True, epi=BF_ATOMIC,
                   splitk=splitk, colsum=[bias_out])
 
