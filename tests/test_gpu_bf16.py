@@ -201,3 +201,27 @@ def test_fused_step_inkernel_noise_matches_filled_noise():
         a, b = getattr(mf._ws, name), getattr(mu._ws, name)
         assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
                            b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32)), name
+
+
+@pytest.mark.parametrize("variant", ["2", "3", "4"])
+def test_fused_step_tile_variants_bitwise(variant, monkeypatch):
+    """Every compiled tile shape of vae_step.hip (MOG_VS_MT: 32 images x 8
+    waves, 32 x 16, 64 x 16 -- the last the B >= 16,384 default) against the
+    unfused sequence, bit for bit, with a ragged last workgroup (batch 150);
+    also exercises the row-range canvas parts through mog_recon_loss."""
+    monkeypatch.setenv("MOG_VS_MT", variant)
+    cfg, P, nz, x, k = _setup(batch=150, seed=8)
+    noise = {n: torch.as_tensor(v).to(DEV) for n, v in nz.items()}
+    mf = _model(cfg, P, "tv%s" % variant, fused=True)
+    mu = _model(cfg, P, "tvu%s" % variant, fused=False)
+    mf.infer(x, k, noise=noise)
+    mu.infer(x, k, noise=noise)
+    torch.cuda.synchronize()
+    for name in ("canvas", "runloss", "vkl", "gb", "a1b", "d2b", "r"):
+        a, b = getattr(mf._ws, name), getattr(mu._ws, name)
+        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
+                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32)), name
+    rows = mf._ws.prows.cpu().numpy()
+    lo, hi = rows & 0xffff, rows >> 16
+    assert (lo % 2 == 0).all() and (lo <= hi).all() and (hi <= 50).all()
+    assert mf.loss == mu.loss
