@@ -193,9 +193,7 @@ __device__ __forceinline__ void bwd_pixels(const float* th, int Hin, int Win, in
         const bool use = valid && grads && !degen && g0 != 0.0f;
         const float g = use ? g0 : 0.0f;  // value and gradients exactly 0 where !use
         const float ax = ex.z, bx = ex.w, ay = ey.z, by = ey.w;
-        if (DU == 1) {
-          if (valid) sg[ic * Wout + j] = g;
-        } else if (DU == 2 && use) {
+        if (DU == 2 && use) {
           atomicAdd(&sD[y0 + x0], ax * ay * g);
           atomicAdd(&sD[y1 + x0], ax * by * g);
           atomicAdd(&sD[y0 + x1], bx * ay * g);
@@ -218,11 +216,11 @@ __host__ __device__ inline int stn_bwd_slice(int Hin, int Win, int Hout, int Wou
   const int hw4 = (Hin * Win + 3) & ~3;
   const int atomic_l = hw4 * (dU ? 2 : 1) + 4 * Hout;
   const int sep_l = ((hw4 > ((Hout * Win + 3) & ~3)) ? hw4 : ((Hout * Win + 3) & ~3)) +
-                    ((Hout * Wout + 3) & ~3) + 4 * 64 + 4 * 64 + 2 * 64;
+                    4 * 64 + 4 * 64 + 2 * 64;
   return dU && atomic_l < sep_l ? sep_l : atomic_l;
 }
 
-__global__ __launch_bounds__(256) void stn_bwd_kernel(
+__global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
     const float* __restrict__ U, int N, int Hin, int Win, const float* __restrict__ theta,
     int Hout, int Wout, const float* __restrict__ G, const float* __restrict__ gscale, float* dU,
     float* dtheta, float* dot, int u_period, int g_period, long long* ts) {
@@ -249,7 +247,7 @@ __global__ __launch_bounds__(256) void stn_bwd_kernel(
   float* sD = sU + hw4;
   float* sT = sU;
   float* sg = sU + max(hw4, (Hout * Win + 3) & ~3);
-  float4* coltab = reinterpret_cast<float4*>(sg + ((P + 3) & ~3));
+  float4* coltab = reinterpret_cast<float4*>(sg);
   float4* rowtab = sdu ? coltab + 64 : reinterpret_cast<float4*>(sU + hw4 * (want_dU ? 2 : 1));
   int2* vrange = reinterpret_cast<int2*>(rowtab + 64);
   const float* Un = U + (size_t)(u_period > 0 ? n % u_period : n) * HWin;
@@ -325,23 +323,47 @@ __global__ __launch_bounds__(256) void stn_bwd_kernel(
       if (lane == 0) vrange[v] = make_int2(lo, hi);
     }
     // T[i][u] = sum_j g[i][j] * (x0(j) == u ? x1 - x : x - x0)   (U is dead: T reuses it)
-    // j outer, the lane's rows inner: the row reads are independent (ILP)
+    // j outer, the lane's rows inner: the row reads are independent (ILP).
+    // g is recomputed from the (L1/L2-resident) cotangent exactly as the pixel
+    // loop forms it -- g = G * sc where the sample is not degenerate, else 0;
+    // the columns of [jlo, jhi] are never degenerate, so only the row test
+    // remains -- instead of being staged in LDS (a 10 KB tile per wave that
+    // held the kernel to two waves per SIMD).
     if (ul < Win) {
       constexpr int RMAX = 32;  // rows per lane (ceil(Hout / rpi) <= 32, see sdu)
-      float acc[RMAX];
-#pragma unroll
-      for (int r = 0; r < RMAX; ++r) acc[r] = 0.0f;
+      constexpr int RC = 16;    // rows per chunk (register budget: occupancy)
       const int nr = (Hout - half + rpi - 1) / rpi;
-      for (int j = jlo; j <= jhi; ++j) {
-        const float4 e = coltab[j];
-        const float w = __float_as_int(e.x) == ul ? e.z : e.w;
+      // the cotangent through a buffer descriptor: 32-bit offsets, no 64-bit
+      // address registers per load
+      const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(Gn), 0, P * 4, 0x00020000);
+#pragma unroll 1
+      for (int r0 = 0; r0 < RMAX; r0 += RC) {
+        if (r0 >= nr) break;
+        float acc[RC];
+        unsigned ylive = 0;  // bit r: the lane's row r0 + r has distinct corner rows
 #pragma unroll
-        for (int r = 0; r < RMAX; ++r)  // unpredicated (clamped row): reads stay in flight
-          acc[r] += sg[min(half + rpi * r, Hout - 1) * Wout + j] * w;
+        for (int r = 0; r < RC; ++r) {
+          acc[r] = 0.0f;
+          const float4 e = rowtab[min(half + rpi * (r0 + r), Hout - 1)];
+          ylive |= (__float_as_int(e.x) != __float_as_int(e.y) ? 1u : 0u) << r;
+        }
+        for (int j = jlo; j <= jhi; ++j) {
+          const float4 e = coltab[j];
+          const float w = __float_as_int(e.x) == ul ? e.z : e.w;
+#pragma unroll
+          for (int r = 0; r < RC; ++r) {  // unpredicated (clamped row): loads stay in flight
+            const float g0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                 gr, (min(half + rpi * (r0 + r), Hout - 1) * Wout + j) * 4, 0, 0)) *
+                             sc;
+            const float g = ((ylive >> r) & 1u) && grads && g0 != 0.0f ? g0 : 0.0f;
+            acc[r] += g * w;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < RC; ++r)
+          if (r0 + r < nr) sT[(half + rpi * (r0 + r)) * Win + ul] = acc[r];
       }
-#pragma unroll
-      for (int r = 0; r < RMAX; ++r)
-        if (r < nr) sT[(half + rpi * r) * Win + ul] = acc[r];
     }
     wave_sync();
     TS(3);
