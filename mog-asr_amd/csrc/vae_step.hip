@@ -91,8 +91,10 @@ struct Lay {
   static constexpr int OFF_D1 = A2;
   static constexpr int RH = M / 4;  // images per r-staging group
   static constexpr int OFF_TABW = RH * W2 * 4;
-  static constexpr int ARENA =
+  static constexpr int ARENA0 =
       cmax(cmax(A1, TAB + 3 * KB), cmax(OFF_D1 + A2, cmax(OFF_LV + M * 50 * 4, OFF_TABW + RH * 2 * CTAB_MAX * 16)));
+  static constexpr int OFF_EZ = ARENA0;        // eps_z [M][50] fp32, staged in the prologue
+  static constexpr int ARENA = ARENA0 + M * 50 * 4;
   static_assert(OFF_Z + M * SZ * 2 <= A2, "kl / z behind a2");
   static_assert(OFF_LV + M * 50 * 4 <= OFF_D1 + A2, "mu / lv");
 };
@@ -624,6 +626,15 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
                        : axis4(axis_row(th, C, C, 28, 28, n - 28), 4 * C);
     }
   }
+  {  // eps_z of the tile -> LDS (contiguous [nb][50] rows, 16-byte loads), used in the sample phase
+    float* sEz = reinterpret_cast<float*>(arena + Ly::OFF_EZ);
+    const float4* src = reinterpret_cast<const float4*>(p.eps_z + (size_t)b0 * 50);
+    const bool al = ((reinterpret_cast<size_t>(p.eps_z) & 15) == 0);
+    if (al)
+      for (int i = tid; i < nb * 50 / 4; i += NTHR) reinterpret_cast<float4*>(sEz)[i] = src[i];
+    for (int i = (al ? nb * 50 / 4 * 4 : 0) + tid; i < nb * 50; i += NTHR)
+      sEz[i] = p.eps_z[(size_t)b0 * 50 + i];
+  }
   const bool all_sep = __syncthreads_and(sep_f) != 0;  // (no global stores issued yet)
   STAMP(0);
 
@@ -684,11 +695,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   __bf16* sZ = reinterpret_cast<__bf16*>(arena + Ly::OFF_Z);
   {
     constexpr int NS = M * 64 / NTHR;
+    const float* sEz = reinterpret_cast<const float*>(arena + Ly::OFF_EZ);
     float ez[NS];
 #pragma unroll
     for (int it = 0; it < NS; ++it) {
       const int i = tid + it * NTHR, m = i >> 6, k = i & 63;
-      ez[it] = (k < 50 && m < nb) ? p.eps_z[(size_t)(b0 + m) * 50 + k] : 0.0f;
+      ez[it] = (k < 50 && m < nb) ? sEz[m * 50 + k] : 0.0f;
     }
 #pragma unroll
     for (int it = 0; it < NS; ++it) {
