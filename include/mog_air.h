@@ -65,6 +65,13 @@ int mog_stn_forward(const float* U, int N, int Hin, int Win, const float* theta,
 int mog_stn_backward(const float* U, int N, int Hin, int Win, const float* theta, int Hout,
                      int Wout, const float* G, const float* gscale, float* dU, float* dtheta,
                      float* dot, int u_period, int g_period, void* stream);
+/* The same with the glimpse gradient taken through the VAE output sigmoid
+ * (vae.py:44-46, TF SigmoidGrad): dm[n] = bf16((dU[n] * U[n]) * (1 - U[n])), U
+ * being the sigmoid output r, written instead of dU (u_period must be 0). */
+int mog_stn_backward_sigmoid_bf16(const float* U, int N, int Hin, int Win, const float* theta,
+                                  int Hout, int Wout, const float* G, const float* gscale,
+                                  void* dm, float* dtheta, float* dot, int u_period, int g_period,
+                                  void* stream);
 
 /* ---- LSTM cell (TF-1.12 BasicLSTMCell, air_model.py:454-456,812-815) -----
  * G [B, 4H] gate pre-activations (i,j,f,o) WITHOUT bias when `bias` != NULL. */

@@ -404,6 +404,27 @@ __global__ __launch_bounds__(256) void cvt_bf16_batch_kernel(CvtBatch b) {
     b.dst[j][e] = (__bf16)v;
     return;
   }
+  if (d[6] == 0 && (d[4] & 7) == 0 && (d[5] & 7) == 0) {
+    // plain copy, 8 consecutive destination columns per thread (one 16-byte
+    // store; two 16-byte loads where the source row is aligned and in range)
+    const int e8 = e * 8;
+    if (e8 >= b.count[j]) return;
+    const int r = e8 / d[4], c = e8 - r * d[4];
+    typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+    bf16x8_t o;
+    const float* sp = src + r * d[2] + c;
+    if (r < d[0] && c + 8 <= d[1] && ((d[2] & 3) == 0) && ((reinterpret_cast<size_t>(src) & 15) == 0)) {
+      const float4 a0 = reinterpret_cast<const float4*>(sp)[0];
+      const float4 a1 = reinterpret_cast<const float4*>(sp)[1];
+      o[0] = (__bf16)a0.x; o[1] = (__bf16)a0.y; o[2] = (__bf16)a0.z; o[3] = (__bf16)a0.w;
+      o[4] = (__bf16)a1.x; o[5] = (__bf16)a1.y; o[6] = (__bf16)a1.z; o[7] = (__bf16)a1.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = (__bf16)((r < d[0] && c + q < d[1]) ? sp[q] : 0.0f);
+    }
+    *reinterpret_cast<bf16x8_t*>(b.dst[j] + r * d[5] + c) = o;
+    return;
+  }
   const int r = e / d[4], c = e - r * d[4];
   const int sr = d[6] ? c : r, sc = d[6] ? r : c;
   const float v = (sr < d[0] && sc < d[1]) ? src[sr * d[2] + sc] : 0.0f;
@@ -427,7 +448,10 @@ extern "C" int mog_cvt_bf16_batch(int njobs, const float* const* src, void* cons
     b.dst[j] = reinterpret_cast<__bf16*>(dst[j]);
     for (int k = 0; k < 7; ++k) b.d[j][k] = dims[7 * j + k];
     b.count[j] = (int)cnt;
-    mx = cnt > mx ? cnt : mx;
+    // threads: one per element, or one per 8 for the vectorized plain copy
+    const bool v8 = dims[7 * j + 6] == 0 && (dims[7 * j + 4] & 7) == 0 && (dims[7 * j + 5] & 7) == 0;
+    const long thr = v8 ? (cnt + 7) / 8 : cnt;
+    mx = thr > mx ? thr : mx;
   }
   if (njobs == 0 || mx == 0) return 0;
   cvt_bf16_batch_kernel<<<dim3(mog_cdiv(mx, 256), njobs), 256, 0, mog_stream(stream)>>>(b);

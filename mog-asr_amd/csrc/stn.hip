@@ -223,7 +223,7 @@ __host__ __device__ inline int stn_bwd_slice(int Hin, int Win, int Hout, int Wou
 __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
     const float* __restrict__ U, int N, int Hin, int Win, const float* __restrict__ theta,
     int Hout, int Wout, const float* __restrict__ G, const float* __restrict__ gscale, float* dU,
-    float* dtheta, float* dot, int u_period, int g_period, long long* ts) {
+    float* dtheta, float* dot, int u_period, int g_period, long long* ts, int du_mode) {
 #pragma clang fp contract(off)
   extern __shared__ float smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -288,7 +288,18 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
   TS(2);
   if (!want_dU) return;
   wave_sync();
+  // du_mode 1: the glimpse gradient leaves through the VAE output sigmoid
+  // (vae.py:44-46; TF SigmoidGrad dm = (dr * r) * (1 - r), r = U) as bf16
   float* dUn = dU + (size_t)n * HWin;
+  __bf16* dMn = reinterpret_cast<__bf16*>(dU) + (size_t)n * HWin;
+  auto put = [&](int idx, float d) {
+    if (du_mode) {
+      const float v = Un[idx];
+      dMn[idx] = (__bf16)((d * v) * (1.0f - v));
+    } else {
+      dUn[idx] = d;
+    }
+  };
   if (sdu) {
     // contiguous index ranges (the maps increase): canvas columns j whose
     // corner pair touches source column u, canvas rows i touching source row v
@@ -376,16 +387,16 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
           const float4 e = rowtab[i];
           acc += sT[i * Win + ul] * (__float_as_int(e.x) == v * Win ? e.z : e.w);
         }
-        dUn[v * Win + ul] = acc;
+        put(v * Win + ul, acc);
       }
     TS(4);
     return;
   }
-  if ((HWin & 3) == 0) {
+  if ((HWin & 3) == 0 && !du_mode) {
     for (int q = lane; q < HWin / 4; q += 64)
       reinterpret_cast<floatx4*>(dUn)[q] = reinterpret_cast<const floatx4*>(sD)[q];
   } else {
-    for (int i = lane; i < HWin; i += 64) dUn[i] = sD[i];
+    for (int i = lane; i < HWin; i += 64) put(i, sD[i]);
   }
 }
 
@@ -408,10 +419,10 @@ extern "C" int mog_stn_forward(const float* U, int N, int Hin, int Win, const fl
   MOG_LAUNCH_RET();
 }
 
-extern "C" int mog_stn_backward(const float* U, int N, int Hin, int Win, const float* theta,
-                                int Hout, int Wout, const float* G, const float* gscale,
-                                float* dU, float* dtheta, float* dot, int u_period, int g_period,
-                                void* stream) {
+static int stn_backward_launch(const float* U, int N, int Hin, int Win, const float* theta,
+                               int Hout, int Wout, const float* G, const float* gscale, float* dU,
+                               float* dtheta, float* dot, int u_period, int g_period, int du_mode,
+                               void* stream) {
   MOG_CHECK_ARG(U && theta && G && N >= 0 && Hin > 0 && Win > 0 && Hout > 0 && Wout > 0);
   MOG_CHECK_ARG(u_period >= 0 && g_period >= 0);
   MOG_CHECK_ARG(Hin * Win <= 16384);
@@ -435,7 +446,7 @@ extern "C" int mog_stn_backward(const float* U, int N, int Hin, int Win, const f
   }
   stn_bwd_kernel<<<mog_cdiv(N, wpb), 64 * wpb, slice * sizeof(float) * wpb,
                    mog_stream(stream)>>>(U, N, Hin, Win, theta, Hout, Wout, G, gscale, dU, dtheta,
-                                         dot, u_period, g_period, ts);
+                                         dot, u_period, g_period, ts, du_mode);
   if (ts) {
     std::vector<long long> h((size_t)N * 8);
     (void)hipStreamSynchronize(mog_stream(stream));
@@ -458,4 +469,23 @@ extern "C" int mog_stn_backward(const float* U, int N, int Hin, int Win, const f
             (t1 - t0) / 100.0);
   }
   MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_stn_backward(const float* U, int N, int Hin, int Win, const float* theta,
+                                int Hout, int Wout, const float* G, const float* gscale,
+                                float* dU, float* dtheta, float* dot, int u_period, int g_period,
+                                void* stream) {
+  return stn_backward_launch(U, N, Hin, Win, theta, Hout, Wout, G, gscale, dU, dtheta, dot,
+                             u_period, g_period, 0, stream);
+}
+
+extern "C" int mog_stn_backward_sigmoid_bf16(const float* U, int N, int Hin, int Win,
+                                             const float* theta, int Hout, int Wout,
+                                             const float* G, const float* gscale, void* dm,
+                                             float* dtheta, float* dot, int u_period, int g_period,
+                                             void* stream) {
+  MOG_CHECK_ARG(dm != nullptr && u_period == 0);
+  return stn_backward_launch(U, N, Hin, Win, theta, Hout, Wout, G, gscale,
+                             reinterpret_cast<float*>(dm), dtheta, dot, u_period, g_period, 1,
+                             stream);
 }

@@ -479,8 +479,15 @@ class AIRModel:
         prior_lo = self.hyper("z_pres_prior_log_odds")
         temperature = self.hyper("z_pres_temperature")
         # STN write backward of all steps against the shared canvas gradient
-        ops.stn_backward(ws.r.view(TB, -1), ws.th_b, (C, C), ws.dcanvas, gscale=ws.zc, dU=ws.dr_all,
-                         dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True, n=TB)
+        if self.precision == "bf16":
+            # dr leaves through the output sigmoid as bf16 straight from the kernel
+            ops.stn_backward(ws.r.view(TB, -1), ws.th_b, (C, C), ws.dcanvas, gscale=ws.zc,
+                             dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True, n=TB,
+                             dm_bf16=ws.dmb.view(TB, -1))
+        else:
+            ops.stn_backward(ws.r.view(TB, -1), ws.th_b, (C, C), ws.dcanvas, gscale=ws.zc,
+                             dU=ws.dr_all, dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True,
+                             n=TB)
         if self.precision == "bf16":
             self._vae_backward_bf16_all(ws, gscale)
         else:
@@ -544,7 +551,7 @@ class AIRModel:
         Zp = self._pad8(Z)
         wn = self._wn
         s = stream_ptr()
-        _lib.call("mog_sigmoid_backward", dp(ws.r), dp(ws.dr_all), dp(ws.dmb), TB * W2, 1, s)
+        # dmb = bf16(SigmoidGrad(r, dr)) was written by the STN write backward
         gemm_bf16([ws.dmb], [wn["gen_mean"]], [ws.dd2b], TB, G2, W2, W2, W2, G2,
                   epi=BF_SOFTPLUS_BWD, aux=[ws.d2b], ldaux=G2)
         gemm_bf16([ws.dd2b], [wn["generative_2"]], [ws.dd1b], TB, G1, G2, G2, G2, G1,

@@ -126,10 +126,16 @@ def cvt_bf16(src: torch.Tensor, dst: torch.Tensor, transpose: bool) -> None:
 
 def stn_backward(U: torch.Tensor, theta: torch.Tensor, out_hw, G: torch.Tensor,
                  gscale: Optional[torch.Tensor] = None, want_dU=True, want_dtheta=True,
-                 want_dot=False, dU=None, dtheta=None, dot=None, n: Optional[int] = None):
+                 want_dot=False, dU=None, dtheta=None, dot=None, n: Optional[int] = None,
+                 dm_bf16: Optional[torch.Tensor] = None):
     """Gradient of transformer().  ``n`` images (default U's); when U or G
     holds fewer rows than ``n``, image i reads row i % rows (several loop
-    steps of one batch against the shared canvas or canvas gradient)."""
+    steps of one batch against the shared canvas or canvas gradient).
+
+    ``dm_bf16`` (bf16 [N, Hin*Win], U = the VAE output sigmoid r): the input
+    gradient is taken on through the sigmoid (vae.py:44-46) and stored as
+    bf16 there instead of dU -- bit-identical to dU followed by
+    mog_sigmoid_backward(out_bf16=1)."""
     _chk(U, "U")
     _chk(G, "G")
     if U.dim() == 3:
@@ -141,6 +147,18 @@ def stn_backward(U: torch.Tensor, theta: torch.Tensor, out_hw, G: torch.Tensor,
     N = NU if n is None else int(n)
     assert N % NU == 0 and N % NG == 0 and theta.numel() == 6 * N
     dev = U.device
+    if dm_bf16 is not None:
+        assert want_dU and dU is None and NU == N
+        assert dm_bf16.dtype == torch.bfloat16 and dm_bf16.numel() >= N * Hin * Win
+        _chk(dm_bf16, "dm_bf16", torch.bfloat16)
+        if want_dtheta and dtheta is None:
+            dtheta = torch.empty((N, 6), device=dev, dtype=torch.float32)
+        if want_dot and dot is None:
+            dot = torch.empty((N,), device=dev, dtype=torch.float32)
+        _lib.call("mog_stn_backward_sigmoid_bf16", dp(U), N, Hin, Win, dp(theta), Ho, Wo, dp(G),
+                  dp(gscale), dp(dm_bf16), dp(dtheta if want_dtheta else None),
+                  dp(dot if want_dot else None), 0, NG if NG < N else 0, stream_ptr())
+        return dm_bf16, dtheta, dot
     if want_dU and dU is None:
         dU = torch.empty((N, Hin * Win), device=dev, dtype=torch.float32)
     if want_dtheta and dtheta is None:

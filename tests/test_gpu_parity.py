@@ -160,6 +160,36 @@ def test_stn_backward_vs_autograd(sep, src, dst):
                                atol=1e-3)
 
 
+@pytest.mark.parametrize("sep", [True, False])
+def test_stn_backward_sigmoid_bf16_matches_unfused(sep):
+    """The write backward with the output-sigmoid gradient folded in (bf16
+    dm straight from the kernel) is bit-identical to dU followed by
+    mog_sigmoid_backward; dtheta / dot are unchanged."""
+    from mog_air import _lib, ops
+    from mog_air.ops import dp, stream_ptr
+    rng = np.random.default_rng(31)
+    N, W, C = 40, 28, 50
+    r = rng.uniform(size=(N, W * W)).astype(np.float32)
+    s = rng.uniform(0.2, 0.9, N)
+    t = rng.uniform(-0.8, 0.8, (N, 2))
+    sh = np.zeros(N) if sep else rng.uniform(-0.2, 0.2, N)
+    thb = np.stack([1 / s, sh, -t[:, 0] / s, -sh, 1 / s, -t[:, 1] / s], 1)
+    G = rng.standard_normal((N // 2, C * C))  # shared cotangent (g_period)
+    gs = rng.uniform(size=N)
+    gs[3] = 0.0
+    dU, dth, dot = ops.stn_backward(_cuda(r), _cuda(thb), (C, C), _cuda(G), gscale=_cuda(gs),
+                                    want_dot=True, n=N)
+    ref = torch.empty((N, W * W), device=DEV, dtype=torch.bfloat16)
+    _lib.call("mog_sigmoid_backward", dp(_cuda(r)), dp(dU), dp(ref), N * W * W, 1,
+              stream_ptr())
+    dm = torch.full((N, W * W), float("nan"), device=DEV, dtype=torch.bfloat16)
+    _, dth2, dot2 = ops.stn_backward(_cuda(r), _cuda(thb), (C, C), _cuda(G), gscale=_cuda(gs),
+                                     want_dot=True, n=N, dm_bf16=dm)
+    torch.cuda.synchronize()
+    assert torch.equal(dm.view(torch.int16), ref.view(torch.int16))
+    assert torch.equal(dth2, dth) and torch.equal(dot2, dot)
+
+
 def _setup(batch=16, seed=0, train=True, T=3, num_prior=None, bias_scale=0.05):
     cfg = ao.AirConfig(batch=batch, max_steps=T, train=train, num_prior=num_prior,
                        scale_prior_variance=0.05, z_pres_prior_log_odds=-0.01)
