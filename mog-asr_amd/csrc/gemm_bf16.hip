@@ -16,6 +16,8 @@
 // prefetch of tile i+2 while tile i is multiplied and tile i+1 is written to
 // the other stage — one barrier per k-iteration.  Workgroup ids are remapped
 // so that the workgroups sharing an A row-panel run on one XCD (shared L2).
+#include <cstdlib>
+
 #include "bf16_epi.h"
 #include "mog_common.h"
 
@@ -345,9 +347,12 @@ extern "C" int mog_gemm_bf16(int batch, const void* const* A, const void* const*
   D.splitk = splitk; D.kchunk = 0; D.out_bf16 = out_bf16; D.aux_scale = aux_scale;
   D.nx = D.ny = 1;
   hipStream_t s = mog_stream(stream);
-  // 128x128 only when it still gives >= 2 workgroups per CU (2 x 256 CUs)
+  // 128x128 only when it still gives >= 2 workgroups per CU (2 x 256 CUs);
+  // MOG_BF16_BIG_NT / MOG_BF16_BIG_TN override the workgroup threshold
   const long big = (long)mog_cdiv(M, 128) * mog_cdiv(N, 128) * batch * splitk;
-  if (M >= 128 && N >= 128 && big >= 512)
+  long thr = 512;
+  if (const char* e = getenv(tn ? "MOG_BF16_BIG_TN" : "MOG_BF16_BIG_NT")) thr = atol(e);
+  if (M >= 128 && N >= 128 && big >= thr)
     launch_tile<128, 128>(tn != 0, epi, s, P, D, batch);
   else
     launch_tile<64, 64>(tn != 0, epi, s, P, D, batch);

@@ -78,7 +78,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 //   then:   a1 [M][S512] at 0 -> a2 [M][S256] at 0 (in place), mu | lv fp32 behind a2
 //   sample: kl [M][50] fp32 at 0, z [M][SZ] bf16 behind it, d1 [M][S256] at A2
 //   then:   d2 [M][S512] at 0 (in place over d1)
-//   write:  r staging [RH][784] fp32 at 0, write tables [RH][2C] float4 behind
+//   write:  one slot per wave at wv * WSLOT: r [784] fp32, write tables [2C] float4
 template <int MT>
 struct Lay {
   static constexpr int M = 16 * MT;
@@ -89,10 +89,10 @@ struct Lay {
   static constexpr int OFF_MU = A2, OFF_LV = A2 + M * 50 * 4;
   static constexpr int OFF_KL = 0, OFF_Z = M * 50 * 4;
   static constexpr int OFF_D1 = A2;
-  static constexpr int RH = M / 4;  // images per r-staging group
-  static constexpr int OFF_TABW = RH * W2 * 4;
+  // STN write: one slot per wave (r of one image + its 2C write tables)
+  static constexpr int WSLOT = W2 * 4 + 2 * CTAB_MAX * 16;
   static constexpr int ARENA0 =
-      cmax(cmax(A1, TAB + 3 * KB), cmax(OFF_D1 + A2, cmax(OFF_LV + M * 50 * 4, OFF_TABW + RH * 2 * CTAB_MAX * 16)));
+      cmax(cmax(A1, TAB + 3 * KB), cmax(OFF_D1 + A2, cmax(OFF_LV + M * 50 * 4, 16 * WSLOT)));
   static constexpr int OFF_EZ = ARENA0;        // eps_z [M][50] fp32, staged in the prologue
   static constexpr int ARENA = ARENA0 + M * 50 * 4;
   static_assert(OFF_Z + M * SZ * 2 <= A2, "kl / z behind a2");
@@ -138,6 +138,13 @@ struct StepArgs {
 // write) waits for its stores explicitly.
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+// wave-local LDS ordering (a wave's DS operations complete in order; this
+// keeps the compiler from moving LDS accesses across the point)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 
@@ -212,21 +219,6 @@ __device__ __forceinline__ void build_tables(float2* tab, const float (*sth)[12]
     const float* th = &sth[m0 + m][th_off];
     tab[i] = n < Wout ? axis_col(th, Hin, Win, Hout, Wout, n)
                       : axis_row(th, Hin, Win, Hout, Wout, n - Wout);
-  }
-}
-
-// Expanded axis tables (axis4: {lo*scale, hi*scale (int bits), hi - c, c - lo})
-// of `nimg` images' transforms: Wout column entries (scale 1), then Hout row
-// entries (scale Win).
-template <int NTHR>
-__device__ __forceinline__ void build_tables4(float4* tab, const float (*sth)[12], int m0, int nimg,
-                                              int th_off, int Hin, int Win, int Hout, int Wout) {
-  const int per = Wout + Hout;
-  for (int i = threadIdx.x; i < nimg * per; i += NTHR) {
-    const int m = i / per, n = i - (i / per) * per;
-    const float* th = &sth[m0 + m][th_off];
-    tab[i] = n < Wout ? axis4(axis_col(th, Hin, Win, Hout, Wout, n), 1)
-                      : axis4(axis_row(th, Hin, Win, Hout, Wout, n - Wout), Win);
   }
 }
 
@@ -795,112 +787,122 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   STAMP(9);
   // ---- 9. STN write (air_model.py:580-588): this step's canvas part -------
   // part = active ? z * w : 0 (mog_recon_loss sums the parts in step order).
-  // r is staged back RH images at a time; one wave per image; each lane
-  // produces four consecutive canvas pixels (flat order) and stores them with
-  // one 16-byte store.  Only rows whose clipped corner rows differ can be
-  // nonzero; the band-aligned range of them is stored and recorded.  Dead
-  // samples (clipped corners coincide on both axes) are exactly +0 and are
-  // selected, not branched.
+  // r is staged back one image per wave into the wave's LDS slot; the lanes
+  // walk the image's pixel pairs and store 8 bytes each.  Only rows whose
+  // clipped corner rows differ can be nonzero; the even-aligned range of them
+  // is stored and recorded.
   if (p.phases & 8) {
-    constexpr int RH = Ly::RH;
-    float* sR = reinterpret_cast<float*>(arena);
-    float4* tabW = reinterpret_cast<float4*>(arena + Ly::OFF_TABW);
+    // Wave-private: wave wv writes images wv, wv + NW, ... from its own LDS
+    // slot (r of one image + its write tables); the next image's r is
+    // fetched into registers while the current one is computed, and the
+    // waves meet no workgroup barrier, so their memory and VALU phases drift
+    // apart and overlap.
     const bool vec = (C2 & 3) == 0;  // even C: 16-byte aligned image rows of parts
-    // r of the next group is fetched into registers while this group computes
-    constexpr int NL = (RH * (W2 / 4) + NTHR - 1) / NTHR;
-    float4 tmp[NL];
-    auto fetch = [&](int h0) {
-      const int nh = min(RH, nb - h0);
-      const float4* src = reinterpret_cast<const float4*>(p.r + (size_t)(b0 + h0) * W2);
+    unsigned char* slot = arena + wv * Ly::WSLOT;
+    float* sRw = reinterpret_cast<float*>(slot);
+    float4* tabw = reinterpret_cast<float4*>(slot + W2 * 4);
+    constexpr int NQ = (W2 / 4 + 63) / 64;
+    float4 tmp[NQ];
+    auto fetch = [&](int m) {
+      const float4* src = reinterpret_cast<const float4*>(p.r + (size_t)(b0 + m) * W2);
 #pragma unroll
-      for (int it = 0; it < NL; ++it) {
-        const int i = tid + it * NTHR;
-        if (i < nh * (W2 / 4)) tmp[it] = src[i];
+      for (int it = 0; it < NQ; ++it) {
+        const int i = lane + it * 64;
+        if (i < W2 / 4) tmp[it] = src[i];
       }
     };
-    fetch(0);
-    for (int h0 = 0; h0 < nb; h0 += RH) {
-      const int nh = min(RH, nb - h0);
-      {
-        float4* dst = reinterpret_cast<float4*>(sR);
+    if (wv < nb) fetch(wv);
+    for (int m = wv; m < nb; m += NW) {
 #pragma unroll
-        for (int it = 0; it < NL; ++it) {
-          const int i = tid + it * NTHR;
-          if (i < nh * (W2 / 4)) dst[i] = tmp[it];
-        }
+      for (int it = 0; it < NQ; ++it) {
+        const int i = lane + it * 64;
+        if (i < W2 / 4) reinterpret_cast<float4*>(sRw)[i] = tmp[it];
       }
-      if (C <= CTAB_MAX) build_tables4<NTHR>(tabW, sth, h0, nh, 6, 28, 28, C, C);
-      lds_barrier();
-      if (h0 + RH < nb) fetch(h0 + RH);
-      for (int mm = wv; mm < nh; mm += NW) {
-        const int m = h0 + mm;
-        float* om = p.part + (size_t)(b0 + m) * C2;
-        float4* om4 = reinterpret_cast<float4*>(om);
-        const float* U = sR + mm * W2;
-        const bool act = smask[m] != 0, tab = (ssep[m] & 2) != 0;
-        const float zn = szv[m];
-        const float4* tcol = tabW + mm * 2 * C;
-        const float4* trow = tcol + C;
-        if (!act) {  // inactive: the whole part is +0 -- nothing stored
-          if (lane == 0) p.part_rows[b0 + m] = 0;
-        } else if (tab && vec && C <= CTAB_MAX) {
-          // Only rows whose clipped corner rows differ can be nonzero (a row
-          // with coinciding corner rows samples exactly +0 at every column:
-          // the y weights are exact negatives on one source row, and within
-          // a live row no sample is dead): store the even-aligned range
-          // [rlo, rhi) of such rows and record it.
-          const float4 el = trow[lane < C ? lane : 0];
-          const unsigned long long lm =
-              __builtin_amdgcn_ballot_w64(lane < C && __float_as_int(el.x) != __float_as_int(el.y));
-          const int rlo = lm ? (__builtin_ctzll(lm) & ~1) : 0;
-          const int rhi = lm ? min(C, (64 - __builtin_clzll(lm) + 1) & ~1) : 0;
-          if (lane == 0) p.part_rows[b0 + m] = rlo | (rhi << 16);
-          // Pixel pairs of the range, flattened over the wave: a lane reads
-          // its row entry and two column entries, gathers 8 corners from the
-          // staged r, computes both samples with packed fp32 ops (the same
-          // products and summation order as sample4, per pixel) and stores
-          // 8 bytes.
-          const int PR = C >> 1;  // pairs per row
-          const int np = (rhi - rlo) * PR;
-          typedef float f2 __attribute__((ext_vector_type(2)));
-          for (int idx = lane; idx < np; idx += 64) {
-            const int rr = idx / PR, pr = idx - rr * PR;
-            const int row = rlo + rr;
-            const float4 ey = trow[row];
-            const float4 e0 = tcol[2 * pr], e1 = tcol[2 * pr + 1];
-            const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
-            const int a0 = __float_as_int(e0.x), c0 = __float_as_int(e0.y);
-            const int a1 = __float_as_int(e1.x), c1 = __float_as_int(e1.y);
-            const f2 Ia = {U[y0 + a0], U[y0 + a1]}, Ib = {U[y1 + a0], U[y1 + a1]};
-            const f2 Ic = {U[y0 + c0], U[y0 + c1]}, Id = {U[y1 + c0], U[y1 + c1]};
-            const f2 xz = {e0.z, e1.z}, xw = {e0.w, e1.w};
-            const f2 wa = xz * ey.z, wb = xz * ey.w, wc = xw * ey.z, wd = xw * ey.w;
-            const f2 sv = ((wa * Ia + wb * Ib) + wc * Ic) + wd * Id;
-            const f2 v = zn * sv;
-            *reinterpret_cast<f2*>(om + row * C + 2 * pr) = v;
+      if (C <= CTAB_MAX)
+        for (int i = lane; i < 2 * C; i += 64)
+          tabw[i] = i < C ? axis4(axis_col(&sth[m][6], 28, 28, C, C, i), 4)
+                          : axis4(axis_row(&sth[m][6], 28, 28, C, C, i - C), 4 * 28);
+      wave_lds_sync();
+      if (m + NW < nb) fetch(m + NW);
+      float* om = p.part + (size_t)(b0 + m) * C2;
+      float4* om4 = reinterpret_cast<float4*>(om);
+      const float* U = sRw;
+      const float4* tcol = tabw;
+      const float4* trow = tabw + C;
+      const bool act = smask[m] != 0, tab = (ssep[m] & 2) != 0;
+      const float zn = szv[m];
+      if (!act) {  // inactive: the whole part is +0 -- nothing stored
+        if (lane == 0) p.part_rows[b0 + m] = 0;
+      } else if (tab && vec && C <= CTAB_MAX) {
+        // Only rows whose clipped corner rows differ can be nonzero (a row
+        // with coinciding corner rows samples exactly +0 at every column:
+        // the y weights are exact negatives on one source row, and within
+        // a live row no sample is dead): store the even-aligned range
+        // [rlo, rhi) of such rows and record it.
+        const float4 el = trow[lane < C ? lane : 0];
+        const unsigned long long lm =
+            __builtin_amdgcn_ballot_w64(lane < C && __float_as_int(el.x) != __float_as_int(el.y));
+        const int rlo = lm ? (__builtin_ctzll(lm) & ~1) : 0;
+        const int rhi = lm ? min(C, (64 - __builtin_clzll(lm) + 1) & ~1) : 0;
+        if (lane == 0) p.part_rows[b0 + m] = rlo | (rhi << 16);
+        // Pixel pairs of the range, flattened over the wave: a lane reads
+        // its row entry and two column entries, gathers 8 corners from the
+        // staged r, computes both samples with packed fp32 ops (the same
+        // products and summation order as sample4, per pixel) and stores
+        // 8 bytes.
+        // The pair index idx = rr * PR + pr is walked incrementally (no
+        // per-iteration division) and the store address is linear in it:
+        // row * C + 2 pr = rlo * C + 2 idx.
+        const int PR = C >> 1;  // pairs per row
+        const int np = (rhi - rlo) * PR;
+        const int dq = 64 / PR, dr = 64 - dq * PR;
+        int rr = lane / PR, pr = lane - (lane / PR) * PR;
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const char* Ub = reinterpret_cast<const char*>(sRw);
+        auto ld = [Ub](int a, int b) { return *reinterpret_cast<const float*>(Ub + a + b); };
+        f2* dst = reinterpret_cast<f2*>(om + rlo * C) + lane;
+#pragma unroll 2
+        for (int idx = lane; idx < np; idx += 64) {
+          const float4 ey = trow[rlo + rr];
+          const float4 e0 = tcol[2 * pr], e1 = tcol[2 * pr + 1];
+          const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
+          const int a0 = __float_as_int(e0.x), c0 = __float_as_int(e0.y);
+          const int a1 = __float_as_int(e1.x), c1 = __float_as_int(e1.y);
+          const f2 Ia = {ld(y0, a0), ld(y0, a1)}, Ib = {ld(y1, a0), ld(y1, a1)};
+          const f2 Ic = {ld(y0, c0), ld(y0, c1)}, Id = {ld(y1, c0), ld(y1, c1)};
+          const f2 xz = {e0.z, e1.z}, xw = {e0.w, e1.w};
+          const f2 wa = xz * ey.z, wb = xz * ey.w, wc = xw * ey.z, wd = xw * ey.w;
+          const f2 sv = ((wa * Ia + wb * Ib) + wc * Ic) + wd * Id;
+          *dst = zn * sv;
+          dst += 64;
+          pr += dr;
+          rr += dq;
+          if (pr >= PR) {
+            pr -= PR;
+            ++rr;
           }
-        } else {  // general transform or odd C: per-pixel geometry, flat order
-          if (lane == 0) p.part_rows[b0 + m] = C << 16;
-          const int nq = vec ? C2 / 4 : C2;
-          const int per = vec ? 4 : 1;
-          for (int q = lane; q < nq; q += 64) {
-            float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            int pix = q * per;
-            int i = pix / C, j = pix - (pix / C) * C;
+        }
+      } else {  // general transform or odd C: per-pixel geometry, flat order
+        if (lane == 0) p.part_rows[b0 + m] = C << 16;
+        const int nq = vec ? C2 / 4 : C2;
+        const int per = vec ? 4 : 1;
+        for (int q = lane; q < nq; q += 64) {
+          float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+          int pix = q * per;
+          int i = pix / C, j = pix - (pix / C) * C;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              if (e < per) {
-                const Tap t = stn_tap(&sth[m][6], 28, 28, mog_linspace(j, C), mog_linspace(i, C));
-                v[e] = t.dead ? 0.0f : zn * tap_value(t, U);
-                if (++j == C) { j = 0; ++i; }
-              }
+          for (int e = 0; e < 4; ++e) {
+            if (e < per) {
+              const Tap t = stn_tap(&sth[m][6], 28, 28, mog_linspace(j, C), mog_linspace(i, C));
+              v[e] = t.dead ? 0.0f : zn * tap_value(t, U);
+              if (++j == C) { j = 0; ++i; }
             }
-            if (vec) om4[q] = make_float4(v[0], v[1], v[2], v[3]);
-            else om[q] = v[0];
           }
+          if (vec) om4[q] = make_float4(v[0], v[1], v[2], v[3]);
+          else om[q] = v[0];
         }
       }
-      lds_barrier();
+      wave_lds_sync();  // the slot is rewritten for the next image
     }
   }
   if (p.tstamp) {

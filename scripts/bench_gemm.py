@@ -42,6 +42,26 @@ def main():
         print(f"{name:10s} M={M} N={N} K={K}: store {t_store:7.1f}us ({flop/t_store/1e6:6.0f} TF) "
               f"softplus {t_sp:7.1f}us  hipBLASLt {t_ref:7.1f}us ({flop/t_ref/1e6:6.0f} TF)")
     # TN weight gradient
+    if os.environ.get("GEMM_TN_ONLY"):
+        shapes_tn = (("dW1", 3 * B, 784, 512), ("dWgo", 3 * B, 512, 784),
+                     ("dWx", B, 2504, 1024), ("dW2", 3 * B, 512, 256))
+        for name, K, M, N in shapes_tn:
+            X = torch.randn(K, M, device=dev).to(torch.bfloat16)
+            dY = torch.randn(K, N, device=dev).to(torch.bfloat16)
+            out = torch.zeros(M, N, device=dev)
+            flop = 2.0 * M * N * K
+            for thr in ("512", "1"):
+                os.environ["MOG_BF16_BIG_TN"] = thr
+                for sk in (1, 2, 4, 8, 16):
+                    if K // sk < 512:
+                        continue
+                    t = timeit(lambda: ops.gemm_bf16([X], [dY], [out], M, N, K, M, N, N,
+                                                     tn=True, epi=ops.BF_ATOMIC, splitk=sk))
+                    print(f"{name} thr={thr} splitk={sk}: {t:7.1f}us ({flop/t/1e6:6.0f} TF)",
+                          flush=True)
+            t_ref = timeit(lambda: torch.matmul(X.t(), dY))
+            print(f"{name} hipBLASLt {t_ref:7.1f}us ({flop/t_ref/1e6:6.0f} TF)", flush=True)
+        return
     for name, K, M, N in (("dW1", 3 * B, 784, 512), ("dWgo", 3 * B, 512, 784)):
         X = torch.randn(K, M, device=dev).to(torch.bfloat16)
         dY = torch.randn(K, N, device=dev).to(torch.bfloat16)

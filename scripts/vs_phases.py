@@ -22,7 +22,8 @@ def main():
     m.step(x, k)
     torch.cuda.synchronize()
     ws = m._ws
-    for mask in (31, 1, 2, 8, 16, 0):
+    masks = [int(v) for v in os.environ.get("VS_MASKS", "31,1,2,8,16,0").split(",")]
+    for mask in masks:
         os.environ["MOG_VS_PHASES"] = str(mask)
         for _ in range(3):
             m._step_fused(x, ws, 0, 0.3)
