@@ -123,6 +123,18 @@ __device__ __forceinline__ void bwd_pixels(const float* th, int Hin, int Win, in
   // Wout <= 32: two output rows per pass (lane halves), else one
   const int cw = Wout <= 32 ? 32 : 64, rp = 64 / cw;
   const int sub = lane / cw, jl = lane - sub * cw;
+  // SEP: only the rows whose clipped corner rows differ are walked.  A row
+  // with y0 == y1 samples exactly +0 (its y weights are exact negatives on one
+  // source row) and is degenerate, so it adds exactly nothing to dtheta or to
+  // dot for a finite cotangent; those rows are a prefix and a suffix (the
+  // row map increases).
+  int ilo = 0, ihi = Hout;
+  if (SEP) {
+    const unsigned long long lm = __builtin_amdgcn_ballot_w64(
+        lane < Hout && __float_as_int(ry.x) != __float_as_int(ry.y));
+    ilo = lm ? (__builtin_ctzll(lm) / rp) * rp : 0;
+    ihi = lm ? 64 - __builtin_clzll(lm) : 0;
+  }
   for (int j0 = 0; j0 < Wout; j0 += cw) {
     const int j = j0 + jl;
     const bool jv = j < Wout;
@@ -137,8 +149,8 @@ __device__ __forceinline__ void bwd_pixels(const float* th, int Hin, int Win, in
     constexpr int BR = 4;  // passes per batch
     float gq[BR], gn[BR];
 #pragma unroll
-    for (int u = 0; u < BR; ++u) gn[u] = Gn[min(sub + rp * u, Hout - 1) * Wout + jc];
-    for (int i0 = 0; i0 < Hout; i0 += rp * BR) {
+    for (int u = 0; u < BR; ++u) gn[u] = Gn[min(ilo + sub + rp * u, Hout - 1) * Wout + jc];
+    for (int i0 = ilo; i0 < ihi; i0 += rp * BR) {
 #pragma unroll
       for (int u = 0; u < BR; ++u) gq[u] = gn[u];
 #pragma unroll
