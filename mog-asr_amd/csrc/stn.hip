@@ -352,10 +352,19 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
     // the columns of [jlo, jhi] are never degenerate, so only the row test
     // remains -- instead of being staged in LDS (a 10 KB tile per wave that
     // held the kernel to two waves per SIMD).
+    // The rows with y0 == y1 (a prefix and a suffix) are never read by the dU
+    // pass (no row range includes them): T is formed for the live rows only.
+    // (Ballot over the whole wave, before the lane test below.)
+    const unsigned long long lmr = __builtin_amdgcn_ballot_w64(
+        lane < Hout && __float_as_int(rowtab[min(lane, Hout - 1)].x) !=
+                           __float_as_int(rowtab[min(lane, Hout - 1)].y));
+    const int tlo = lmr ? (__builtin_ctzll(lmr) / rpi) * rpi : Hout;
+    const int thi = lmr ? 64 - __builtin_clzll(lmr) : Hout;
     if (ul < Win) {
       constexpr int RMAX = 32;  // rows per lane (ceil(Hout / rpi) <= 32, see sdu)
       constexpr int RC = 16;    // rows per chunk (register budget: occupancy)
-      const int nr = (Hout - half + rpi - 1) / rpi;
+      const int rb = tlo + half;  // the lane's first row
+      const int nr = rb < thi ? (thi - rb + rpi - 1) / rpi : 0;
       // the cotangent through a buffer descriptor: 32-bit offsets, no 64-bit
       // address registers per load
       const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
@@ -368,7 +377,7 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
 #pragma unroll
         for (int r = 0; r < RC; ++r) {
           acc[r] = 0.0f;
-          const float4 e = rowtab[min(half + rpi * (r0 + r), Hout - 1)];
+          const float4 e = rowtab[min(rb + rpi * (r0 + r), Hout - 1)];
           ylive |= (__float_as_int(e.x) != __float_as_int(e.y) ? 1u : 0u) << r;
         }
         for (int j = jlo; j <= jhi; ++j) {
@@ -377,7 +386,7 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
 #pragma unroll
           for (int r = 0; r < RC; ++r) {  // unpredicated (clamped row): loads stay in flight
             const float g0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                 gr, (min(half + rpi * (r0 + r), Hout - 1) * Wout + j) * 4, 0, 0)) *
+                                 gr, (min(rb + rpi * (r0 + r), Hout - 1) * Wout + j) * 4, 0, 0)) *
                              sc;
             const float g = ((ylive >> r) & 1u) && grads && g0 != 0.0f ? g0 : 0.0f;
             acc[r] += g * w;
@@ -385,7 +394,7 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
         }
 #pragma unroll
         for (int r = 0; r < RC; ++r)
-          if (r0 + r < nr) sT[(half + rpi * (r0 + r)) * Win + ul] = acc[r];
+          if (r0 + r < nr) sT[(rb + rpi * (r0 + r)) * Win + ul] = acc[r];
       }
     }
     wave_sync();
