@@ -779,7 +779,8 @@ class AIRModel:
             X, dY, out = [X], [dY], [out]
             bias_out = None if bias_out is None else [bias_out]
         tiles = ((M + 63) // 64) * ((N + 63) // 64) * len(out)
-        splitk = max(1, min(K // 256, (2048 + tiles - 1) // tiles))
+        target = int(os.environ.get("MOG_DW32_TARGET", "2048"))
+        splitk = max(1, min(K // 256, (target + tiles - 1) // tiles))
         gemm(X, dY, out, M, N, K, lda, ldb, N, transA=True, epi=EPI_ATOMIC,
              splitk=splitk, colsum=bias_out)
 
