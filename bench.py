@@ -1,15 +1,30 @@
 """AIR train-step throughput on MI355X (BASELINE.json metric):
 images/sec/node for the AIR train step, Multi-MNIST-like 50x50 synthetic
 canvases, max_steps = 3 (all 3 steps always computed), data-parallel over N
-GPUs (one process per GPU, RCCL all-reduce of the flat gradient buffer).
+GPUs (one process per GPU, RCCL all-reduce of the gradient in buckets
+overlapped with the backward).
 
 A step = forward (LSTM, heads, STN read, glimpse VAE, STN write, canvas) +
 backward + gradient all-reduce + per-tensor clip + TF Adam, on one batch of
 synthetic input already resident in HBM.  Prints ONE JSON line on rank 0.
+
+Headline ``value``: the train step at the REFERENCE's precision (fp32
+arithmetic throughout, air/vae.py:5-48, air/air_model.py:533-588), per-GPU
+batch 8192 (the batch configs[1] is quoted on).  Extra keys on the same line
+(rank 0, N = 1 only): ``configs_1_bf16`` (configs[1] itself: bf16 VAE, fp32
+elsewhere), ``config_1_batch64_fp32`` (the reference's own batch of 64),
+``fused_step_roofline`` / ``fused_step_roofline_c64`` (the north-star fused
+STN-read -> VAE -> STN-write kernel at B = 65,536, C = 50 and 64),
+``roofline`` (dominant kernel of the headline step) and ``cpu_baseline``.
+
+``python bench.py --gpus N`` without a torch.distributed launcher starts the
+N ranks itself (fresh child processes, before anything touches the GPU).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,62 +43,127 @@ HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFLOPS = 157.3
 BF16_MFMA_PEAK_TFLOPS = 2500.0
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
-PRECISION = "bf16"  # set from --precision in main()
 
 
-def kernel_work(name, B, C2=2500, H=256, T=3):
+def fused_bytes_per_image_step(C2: int, x_bytes: int = 4) -> int:
+    """read x, read+write the running canvas (fp32), 24 B of
+    per-image scalars: 30,024 B at C = 50, 49,176 B at C = 64."""
+    return C2 * x_bytes + 2 * C2 * 4 + 24
+
+
+def kernel_work(name, B, precision, C2=2500, H=256, T=3):
     """Algorithmic work per launch of a tagged kernel: (bound, amount, unit,
-    peak).  Per-unit figures in DESIGN.md §Roofline."""
+    peak).  Per-unit figures in DESIGN.md §4.1."""
     if name == "lstm_x_projection":          # Gx = X Wx, [B,C2] x [C2,4H], fp32 MFMA
         return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", FP32_MFMA_PEAK_TFLOPS
     if name == "lstm_x_projection_grad":     # dWx = X^T dGsum (bf16 MFMA in the bf16 config)
-        peak = BF16_MFMA_PEAK_TFLOPS if PRECISION == "bf16" else FP32_MFMA_PEAK_TFLOPS
+        peak = BF16_MFMA_PEAK_TFLOPS if precision == "bf16" else FP32_MFMA_PEAK_TFLOPS
         return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", peak
-    if name == "stn_vae_step":               # SURVEY §8 D.3: 30,024 B per image-step
-        return "hbm", B * 30024 / 1e9, "GB/s", HBM_PEAK_GBS
+    if name == "stn_vae_step":
+        return "hbm", B * fused_bytes_per_image_step(C2) / 1e9, "GB/s", HBM_PEAK_GBS
     return None
 
 
-def roofline(events, B):
+def pmc_traffic(tag):
+    try:
+        with open(PMC_SUMMARY) as f:
+            return json.load(f).get(tag, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def roofline(events, B, precision):
     """Dominant tagged kernel (largest total time in the timed region)."""
     best = None
     for name, evs in events.items():
         durs = [a.elapsed_time(b) * 1e-3 for a, b in evs]  # seconds
         tot = sum(durs)
-        if kernel_work(name, B) is None:
+        if kernel_work(name, B, precision) is None:
             continue
         if best is None or tot > best[1]:
             best = (name, tot, durs)
     if best is None:
         return None
     name, tot, durs = best
-    bound, amount, unit, peak = kernel_work(name, B)
+    bound, amount, unit, peak = kernel_work(name, B, precision)
     avg = tot / len(durs)
     achieved = amount / avg
-    traffic = None
-    try:
-        with open(PMC_SUMMARY) as f:
-            pmc = json.load(f)
-        traffic = pmc.get(name, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
     return {"kernel": name, "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
-            "frac": achieved / peak, "traffic": traffic, "launches": len(durs),
-            "avg_launch_us": avg * 1e6}
+            "frac": achieved / peak, "traffic": pmc_traffic(f"{name}_{precision}_b{B}"),
+            "launches": len(durs), "avg_launch_us": avg * 1e6,
+            "algorithmic_per_launch": amount * 1e12 if bound == "mfma" else amount * 1e9,
+            "algorithmic_unit": "flop" if bound == "mfma" else "bytes"}
 
 
-def fused_step_roofline(batch: int, launches: int, dev):
+def synthetic(batch, seed, canvas=50):
+    """Multi-MNIST-like canvases: 1-3 glyphs of side
+    U{17..23} (scaled with the canvas), ~35 % inked at U(0,1), < 0.05 -> 0."""
+    rng = np.random.default_rng(seed)
+    imgs = np.zeros((batch, canvas, canvas), np.float32)
+    ks = rng.integers(1, 4, size=batch)
+    lo, hi = (17, 24) if canvas == 50 else (22, 31)
+    for b in range(batch):
+        for _ in range(ks[b]):
+            s = int(rng.integers(lo, hi))
+            y, x = (int(v) for v in rng.integers(0, canvas - s + 1, 2))
+            g = rng.uniform(0, 1, (s, s)).astype(np.float32)
+            g = np.where(rng.uniform(size=(s, s)) < 0.35, g, 0.0)
+            imgs[b, y:y + s, x:x + s] += np.where(g >= 0.05, g, 0.0)
+    return np.clip(imgs, 0, 1).reshape(batch, canvas * canvas), ks.astype(np.int32)
+
+
+def make_model(precision, dev, world, rank, scope, canvas=50):
+    from mog_air.air_model import AIRModel
+    return AIRModel(max_steps=3, max_digits=3, rnn_units=256, canvas_size=canvas, windows_size=28,
+                    scale_prior_mean=-1.0, scale_prior_variance=0.05,
+                    vae_likelihood_std=0.3, z_pres_prior_log_odds=-0.01,
+                    z_pres_temperature=1.0, stopping_threshold=0.99, learning_rate=1e-4,
+                    gradient_clipping_norm=1.0, cnn=False, train=True, scope=scope,
+                    annealing_schedules={"z_pres_prior_log_odds": {
+                        "init": 10000.0, "min": 1e-9, "factor": 0.1, "iters": 3000,
+                        "staircase": False, "log": True}},
+                    device=dev, seed=1235, noise_seed=1235 + rank, grad_world=world,
+                    precision=precision)
+
+
+def timed_train(precision, B, steps, warmup, dev, world=1, rank=0, events=False, scope="bench"):
+    """Time `steps` train steps of batch B per rank (after `warmup`); returns
+    (seconds, model).  Barrier + synchronize on both sides; the caller takes
+    the max over ranks."""
+    model = make_model(precision, dev, world, rank, scope)
+    if world > 1:
+        from mog_air import parallel
+        parallel.attach(model)  # bucketed RCCL all-reduce overlapped with the backward
+    x, k = synthetic(B, 1234 + rank)
+    X = torch.from_numpy(x).to(dev)
+    K = torch.from_numpy(k).to(dev)
+    for _ in range(warmup):
+        model.train_step_async(X, K, global_batch=B * world)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    model.kernel_events = {} if events else None
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        model.train_step_async(X, K, global_batch=B * world)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, model
+
+
+def fused_step_roofline(batch: int, launches: int, dev, canvas: int = 50):
     """North-star measurement (BASELINE.json): the fused STN-read -> glimpse VAE
     -> STN-write step kernel alone at `batch` images on this GPU, inputs
     resident in HBM (theta / masks from one forward pass of a bf16 model on
     the same synthetic canvases).  Timed with HIP events on the stream the
-    kernel is launched on; algorithmic bytes per image-step = 30,024
-    (SURVEY.md §8 D.3)."""
-    from mog_air.air_model import AIRModel
-    m = AIRModel(max_steps=3, cnn=False, train=True, device=dev, precision="bf16",
-                 scale_prior_variance=0.05, z_pres_prior_log_odds=-0.01,
-                 scope="roofline%d" % batch, seed=77, noise_seed=78)
-    x, k = synthetic(batch, 4321)
+    kernel is launched on; algorithmic bytes per image-step from SURVEY.md §8
+    D.3 (30,024 at C = 50, 49,176 at C = 64)."""
+    m = make_model("bf16", dev, 1, 0, "roofline%d_%d" % (batch, canvas), canvas=canvas)
+    m.noise_seed = 78
+    x, k = synthetic(batch, 4321, canvas)
     X = torch.from_numpy(x).to(dev)
     K = torch.from_numpy(k).to(dev)
     m.infer(X, K)
@@ -103,17 +183,14 @@ def fused_step_roofline(batch: int, launches: int, dev):
     torch.cuda.synchronize()
     durs = [a.elapsed_time(b) * 1e-3 for a, b in evs]
     avg = sum(durs) / len(durs)
-    achieved = batch * 30024 / 1e9 / avg
-    traffic = None
-    try:
-        with open(PMC_SUMMARY) as f:
-            traffic = json.load(f).get("stn_vae_step_b%d" % batch, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
-    out = {"kernel": "stn_vae_step", "batch": batch, "bound": "hbm", "achieved": achieved,
-           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-           "traffic": traffic, "launches": launches, "avg_launch_us": avg * 1e6,
-           "algorithmic_bytes_per_launch": batch * 30024}
+    per = fused_bytes_per_image_step(canvas * canvas)
+    achieved = batch * per / 1e9 / avg
+    tag = "stn_vae_step_b%d" % batch + ("" if canvas == 50 else "_c%d" % canvas)
+    out = {"kernel": "stn_vae_step", "batch": batch, "canvas": canvas, "bound": "hbm",
+           "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(tag), "launches": launches,
+           "avg_launch_us": avg * 1e6, "algorithmic_bytes_per_launch": batch * per,
+           "algorithmic_bytes_per_image_step": per}
     del m, ws
     torch.cuda.empty_cache()
     return out
@@ -125,36 +202,57 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8192, help="per-GPU batch (configs[1])")
-    ap.add_argument("--max-steps", type=int, default=3)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="fp32", choices=["bf16", "fp32"],
+                    help="headline precision (fp32 = the reference's arithmetic)")
+    ap.add_argument("--extras", type=int, default=1,
+                    help="N = 1: also time configs[1] (bf16), batch 64, the fused-step rooflines")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--roofline-batch", type=int, default=65536,
-                    help="batch of the stand-alone fused-step roofline run (0: skip)")
+                    help="batch of the stand-alone fused-step roofline runs (0: skip)")
     ap.add_argument("--roofline-launches", type=int, default=30)
     return ap.parse_args()
 
 
-def synthetic(batch, seed):
-    rng = np.random.default_rng(seed)
-    imgs = np.zeros((batch, 50, 50), np.float32)
-    ks = rng.integers(1, 4, size=batch)
-    for b in range(batch):
-        for _ in range(ks[b]):
-            s = int(rng.integers(17, 24))
-            y, x = (int(v) for v in rng.integers(0, 50 - s + 1, 2))
-            g = rng.uniform(0, 1, (s, s)).astype(np.float32)
-            g = np.where(rng.uniform(size=(s, s)) < 0.35, g, 0.0)
-            imgs[b, y:y + s, x:x + s] += np.where(g >= 0.05, g, 0.0)
-    return np.clip(imgs, 0, 1).reshape(batch, 2500), ks.astype(np.int32)
+def physical_cores():
+    """(threads to use, physical cores of the node, logical CPUs available):
+    one thread per physical core this process may run on, capped by the
+    cgroup CPU quota when there is one."""
+    cpus = sorted(os.sched_getaffinity(0))
+    cores = set()
+    for c in cpus:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            with open(base + "core_id") as f1, open(base + "physical_package_id") as f2:
+                cores.add((f2.read().strip(), f1.read().strip()))
+        except OSError:
+            cores.add(("?", str(c)))
+    node = set()
+    for c in range(os.cpu_count() or 1):
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            with open(base + "core_id") as f1, open(base + "physical_package_id") as f2:
+                node.add((f2.read().strip(), f1.read().strip()))
+        except OSError:
+            node.add(("?", str(c)))
+    use = len(cores)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+        if q != "max":
+            use = max(1, min(use, int(int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    return use, len(node), len(cpus)
 
 
 def cpu_baseline(seconds: float):
-    """CPU restatement (oracle/air_torch.py, fp32), batch 64, T=3, on this host."""
+    """CPU restatement (oracle/air_torch.py, fp32), batch 64, T=3, on this
+    host, one torch thread per available physical core."""
     from oracle import air_oracle as ao
     from oracle import air_torch as at
-    cores = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(cores)
+    use, node_cores, logical = physical_cores()
+    torch.set_num_threads(use)
     cfg = ao.AirConfig(batch=64, max_steps=3, scale_prior_variance=0.05)
     P = at.to_torch(ao.init_params(cfg), dtype=torch.float32, requires_grad=True)
     m = {k: torch.zeros_like(v) for k, v in P.items()}
@@ -171,15 +269,34 @@ def cpu_baseline(seconds: float):
         times.append(time.perf_counter() - t0)
         it += 1
     med = float(np.median(times[2:] if len(times) > 4 else times))
-    return {"value": 64.0 / med, "unit": "images/sec", "cores": cores, "kind": "port",
+    return {"value": 64.0 / med, "unit": "images/sec", "cores": use, "kind": "port",
+            "node_physical_cores": node_cores, "logical_cpus_available": logical,
             "sample": f"{len(times)} train steps of batch 64 (T=3) of the fp32 torch CPU "
-                      f"restatement (not TF-1.12); median step {med * 1e3:.1f} ms"}
+                      f"restatement (not TF-1.12), {use} threads; median step "
+                      f"{med * 1e3:.1f} ms"}
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` outside torch.distributed.run: start N ranks as
+    fresh processes (this parent never touches the GPU) and return the
+    worst exit code.  Rank r drives GPU r."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable] + sys.argv, env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
 
 
 def main():
     args = parse()
-    global PRECISION
-    PRECISION = args.precision
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -189,41 +306,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
-    from mog_air.air_model import AIRModel
 
-    B, T = args.batch, args.max_steps
-    model = AIRModel(max_steps=T, max_digits=T, rnn_units=256, canvas_size=50, windows_size=28,
-                     scale_prior_mean=-1.0, scale_prior_variance=0.05,
-                     vae_likelihood_std=0.3, z_pres_prior_log_odds=-0.01,
-                     z_pres_temperature=1.0, stopping_threshold=0.99, learning_rate=1e-4,
-                     gradient_clipping_norm=1.0, cnn=False, train=True, scope="bench",
-                     annealing_schedules={"z_pres_prior_log_odds": {
-                         "init": 10000.0, "min": 1e-9, "factor": 0.1, "iters": 3000,
-                         "staircase": False, "log": True}},
-                     device=dev, seed=1235, noise_seed=1235 + rank, grad_world=world,
-                     precision=args.precision)
-    if world > 1:
-        from mog_air import parallel
-        parallel.attach(model)  # one RCCL all-reduce of the flat gradient per step
-    x, k = synthetic(B, 1234 + rank)
-    X = torch.from_numpy(x).to(dev)
-    K = torch.from_numpy(k).to(dev)
-    for _ in range(args.warmup):
-        model.train_step_async(X, K)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    model.kernel_events = {}
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        model.train_step_async(X, K)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    roof = roofline(model.kernel_events, B)
+    B, T = args.batch, 3
+    el, model = timed_train(args.precision, B, args.steps, args.warmup, dev, world, rank,
+                            events=True)
+    roof = roofline(model.kernel_events, B, args.precision)
     model.kernel_events = None
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
@@ -231,6 +318,8 @@ def main():
         el = float(t.item())
     executed = model.executed_steps
     loss = model.loss
+    del model
+    torch.cuda.empty_cache()
     ms = el / args.steps * 1e3
     value = B * world * args.steps / el
     if rank == 0:
@@ -239,19 +328,39 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.precision, "data": "synthetic",
-            "config": {"workload": "AIR baseline train step (configs[1] batch)",
+            "config": {"workload": "AIR baseline train step (training_air_original.py AIRModel, "
+                                   f"{args.precision}), per-GPU batch {B} (configs[1] batch)",
                        "model": "AIR (LSTM 256, VAE 784-512-256-50, heads 64)",
                        "global_batch": B * world, "per_gpu_batch": B, "canvas": "50x50",
                        "max_steps": T, "data_dependent_steps_would_be": executed,
                        "parallelism": f"dp{world}", "loss_last": loss},
             "roofline": roof,
         }
-        if args.roofline_batch > 0 and world == 1 and args.precision == "bf16":
-            out["fused_step_roofline"] = fused_step_roofline(args.roofline_batch,
-                                                             args.roofline_launches, dev)
+        if world == 1 and args.extras:
+            if args.precision != "bf16":
+                el2, m2 = timed_train("bf16", B, 10, 3, dev, scope="bench_bf16", events=True)
+                out["configs_1_bf16"] = {
+                    "value": B * 10 / el2, "unit": "images/sec", "ms_per_step": el2 / 10 * 1e3,
+                    "dtype": "bf16", "batch": B, "steps": 10,
+                    "workload": "configs[1]: bf16 VAE GEMM operands/activations (fp32 "
+                                "accumulate), fused STN+VAE step kernel, LSTM/heads/STN/loss "
+                                "fp32", "roofline": roofline(m2.kernel_events, B, "bf16")}
+                del m2
+            el3, m3 = timed_train("fp32", 64, 50, 5, dev, scope="bench_b64")
+            out["config_1_batch64_fp32"] = {
+                "value": 64 * 50 / el3, "unit": "images/sec", "ms_per_step": el3 / 50 * 1e3,
+                "dtype": "fp32", "batch": 64, "steps": 50,
+                "workload": "configs[0] shape (the reference's batch of 64) on one MI355X"}
+            del m3
+            torch.cuda.empty_cache()
+            if args.roofline_batch > 0:
+                out["fused_step_roofline"] = fused_step_roofline(args.roofline_batch,
+                                                                 args.roofline_launches, dev)
+                out["fused_step_roofline_c64"] = fused_step_roofline(
+                    args.roofline_batch, args.roofline_launches, dev, canvas=64)
         if args.cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -202,7 +202,8 @@ int mog_add(const float* a, const float* b, float* out, long n, void* stream);
  * Per-tensor inf/nan -> 0, clip_by_norm(clip), TF ApplyAdam with lr_t given.
  * off/len: tensor table; block_tensor/block_start: block -> (tensor, first
  * element), chunks of mog_optim_chunk_elems() elements; all device arrays.
- * sumsq [n_tensors] must be zero on entry. */
+ * sumsq [n_tensors] must be zero on entry; sumsq == NULL skips the NaN/Inf
+ * zeroing and the clip (gradient_clipping_norm=None, air_model.py:948). */
 int mog_optim_chunk_elems(void);
 int mog_clip_adam(float* params, float* grads, float* m, float* v, const long* off,
                   const long* len, const int* block_tensor, const long* block_start,

@@ -122,7 +122,9 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
       } else {
         const int k = q / (BM / 8), mc = (q % (BM / 8)) * 8;
         const int gk = k0 + k, gm = m0 + mc;
-        ra[i] = (gk < kend && gm < D.lda)
+        // gm < M (not < lda): a caller may offset A to a column window
+        // (row chunks of a weight gradient); 8-wide loads stay inside the row
+        ra[i] = (gk < kend && gm < M)
                     ? *reinterpret_cast<const u32x4*>(A + (size_t)gk * D.lda + gm) : zero4;
       }
     }

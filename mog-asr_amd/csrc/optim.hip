@@ -50,12 +50,15 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* p, const float* g
   const long base = off[ti], n = len[ti];
   const long c0 = block_start[blockIdx.x];
   const long c1 = min(n, c0 + CHUNK);
-  const float l2 = sumsq[ti];
+  // sumsq == nullptr: gradient_clipping_norm=None -- no sanitize, no clip
+  // (air_model.py:948 skips both), plain ApplyAdam
+  const bool clipped = sumsq != nullptr;
+  const float l2 = clipped ? sumsq[ti] : 0.0f;
   const float norm = l2 > 0.0f ? sqrtf(l2) : l2;
   const float denom = fmaxf(norm, clip);
   for (long i = c0 + threadIdx.x; i < c1; i += 256) {
     const long k = base + i;
-    const float gc = (g[k] * clip) / denom;
+    const float gc = clipped ? (g[k] * clip) / denom : g[k];
     float mm = m[k], vv = v[k];
     mm = mm + (gc - mm) * (1.0f - b1);
     vv = vv + (gc * gc - vv) * (1.0f - b2);
@@ -69,17 +72,19 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* p, const float* g
 
 extern "C" int mog_optim_chunk_elems(void) { return CHUNK; }
 
-// `sumsq` must be zeroed by the caller (it is an in/out accumulator).
+// `sumsq` must be zeroed by the caller (it is an in/out accumulator); a null
+// `sumsq` skips the NaN/Inf zeroing and the clip (gradient_clipping_norm=None).
 extern "C" int mog_clip_adam(float* params, float* grads, float* m, float* v, const long* off,
                              const long* len, const int* block_tensor, const long* block_start,
                              int nblocks, float* sumsq, float clip, float lr_t, float beta1,
                              float beta2, float eps, void* stream) {
-  MOG_CHECK_ARG(params && grads && m && v && off && len && block_tensor && block_start && sumsq);
+  MOG_CHECK_ARG(params && grads && m && v && off && len && block_tensor && block_start);
   MOG_CHECK_ARG(nblocks >= 0);
   if (nblocks == 0) return 0;
   hipStream_t s = mog_stream(stream);
-  sanitize_sumsq_kernel<<<nblocks, 256, 0, s>>>(grads, off, len, block_tensor, block_start,
-                                                sumsq);
+  if (sumsq != nullptr)
+    sanitize_sumsq_kernel<<<nblocks, 256, 0, s>>>(grads, off, len, block_tensor, block_start,
+                                                  sumsq);
   clip_adam_kernel<<<nblocks, 256, 0, s>>>(params, grads, m, v, off, len, block_tensor,
                                            block_start, sumsq, clip, lr_t, beta1, beta2, eps);
   MOG_LAUNCH_RET();

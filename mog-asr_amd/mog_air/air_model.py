@@ -306,6 +306,34 @@ class AIRModel:
     def global_step(self) -> int:
         return self.params.global_step
 
+    # Data parallelism (parallel.attach): the loss is the mean over the GLOBAL
+    # batch, so each rank scales its loss gradient by 1/B_global and the SUM
+    # all-reduce of the shards' gradients is the full-batch gradient even for
+    # unequal shards.  B_global defaults to B_local * grad_world; the trainer
+    # passes the true global batch of each step (global_batch=...).
+    _global_batch: Optional[int] = None
+
+    def _gscale(self, B: int) -> float:
+        gb = self._global_batch if self._global_batch is not None else B * self.grad_world
+        return 1.0 / float(gb)
+
+    # set by parallel.attach: bucketed async SUM all-reduce of params.grad
+    # (launch(view) as buckets become final during the backward, wait() before
+    # the optimizer) and, for the data-dependent loop exit, a MAX all-reduce of
+    # each step's live flag (only where the exit changes the loss: ``-ap``)
+    grad_reducer = None
+    live_hook = None
+
+    def _reduce_bucket(self, lo: int, hi: int) -> None:
+        if self.grad_reducer is not None:
+            self.grad_reducer.launch(self.params.grad[lo:hi])
+
+    def _bucket_split(self) -> int:
+        """Flat offset where the glimpse-side variables (heads, VAE) start:
+        [0, split) is the LSTM kernel + bias, [split, total) everything else
+        (params.param_specs order)."""
+        return self.params.offsets[self._SCOPE_PREFIX + "scale/mean/hidden/weights"]
+
     def hyper(self, name: str) -> float:
         """Current value of a possibly-annealed hyper-parameter, evaluated at
         the pre-increment global step (as in the reference forward pass)."""
@@ -412,6 +440,8 @@ class AIRModel:
                       dp(ws.scale[t]), dp(ws.shift[t]), dp(ws.zprob[t]), dp(ws.zkl[t]),
                       dp(ws.skl[t]), dp(ws.shkl[t]), dp(ws.zmask[t]), dp(ws.zval[t]),
                       dp(ws.zc[t]), s)
+            if self.live_hook is not None:
+                self.live_hook(ws.live, t)
             if self.fused_step:
                 with self._timed("stn_vae_step"):
                     self._step_fused(X, ws, t, float(lik_std))
@@ -435,7 +465,7 @@ class AIRModel:
         parts = ws.cparts
         self._loss_inputs = (X, targets)
         ws.materialized = bool(outputs)
-        gscale = 1.0 / (B * self.grad_world)
+        gscale = self._gscale(B)
         canvas_ptr = dp(ws.canvas) if (outputs or parts is None) else None
         _lib.call("mog_recon_loss", dp(X), canvas_ptr, dp(parts),
                   self.max_steps if parts is not None else 0, B * C2, dp(ws.prows),
@@ -475,7 +505,7 @@ class AIRModel:
         w1 = [self._P(h + "/hidden/weights") for h in self._HEADS]
         w2 = [self._P(h + "/output/weights") for h in self._HEADS]
         w2a = _lib.ptr_array([dp(x) for x in w2])
-        gscale = 1.0 / (B * self.grad_world)
+        gscale = self._gscale(B)
         prior_lo = self.hyper("z_pres_prior_log_odds")
         temperature = self.hyper("z_pres_temperature")
         # STN write backward of all steps against the shared canvas gradient
@@ -510,6 +540,11 @@ class AIRModel:
         _lib.call("mog_gemm_f32_kseg", 5, _lib.ptr_array([dp(ws.dhid[z]) for z in range(5)]),
                   _lib.ptr_array([dp(x) for x in w1]), dp(ws.dh), None, None, TB, H, HS, HS, HS,
                   H, 0, 1, 0, s)
+        # the heads' and the VAE's weight gradients are final here: their
+        # all-reduce bucket runs while the LSTM chain below computes
+        self._weight_grads_glimpse(ws)
+        split = self._bucket_split()
+        self._reduce_bucket(split, self.params.total)
         ws.dGsum.zero_()
         for t in reversed(range(T)):
             dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
@@ -520,7 +555,7 @@ class AIRModel:
             if t > 0:
                 gemm([ws.dG[t]], [Wh], [ws.dh[t - 1]], B, H, 4 * H, 4 * H, 4 * H, H,
                      transB=True, Cin=[ws.dh[t - 1]])
-        self._weight_grads(X, ws)
+        self._weight_grads_lstm(X, ws)
 
     def _vae_backward_fp32_all(self, ws, gscale):
         TB = ws.B * self.max_steps
@@ -797,13 +832,10 @@ class AIRModel:
         self._dw(ws.d1, ws.dd2, g("generative_2"), TB, G1, G2, G1, G2, gb("generative_2"))
         self._dw(ws.d2, ws.dm, g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
 
-    def _weight_grads(self, X, ws):
-        B, T, H = ws.B, self.max_steps, self.rnn_units
-        C2, W2, Z = self.C2, self.W2, self.vae_latent_dimensions
-        R1, R2 = self.vae_recognition_units
-        G1, G2 = self.vae_generative_units
-        HS = self.scale_hidden_units
-        TB = T * B
+    def _weight_grads_glimpse(self, ws):
+        """Weight gradients of the VAE and the five heads (every loop step at
+        once, K = T*B rows)."""
+        H, HS, TB = self.rnn_units, self.scale_hidden_units, ws.B * self.max_steps
         if self.precision == "bf16":
             self._vae_weight_grads_bf16(ws)
         else:
@@ -817,31 +849,55 @@ class AIRModel:
             self._dw([ws.hid[zi] for zi, _ in sel], [ws.dout[zi] for zi, _ in sel],
                      [self._G(h + "/output/weights") for _, h in sel], TB, HS, k, HS, 2,
                      [self._G(h + "/output/biases") for _, h in sel])
+
+    # rows of the x-part of the LSTM kernel gradient per all-reduce bucket
+    # (multiple of the 64-row GEMM tile; data parallel only)
+    X_GRAD_CHUNK = 640
+
+    def _weight_grads_lstm(self, X, ws):
+        """LSTM kernel / bias gradients.  Data parallel: the x-part X^T dGsum
+        (2500 x 1024, 10 MB) is produced in row chunks, each handed to the
+        all-reduce as soon as it is final, so the collective of chunk i runs
+        under the GEMM of chunk i+1; the recurrent rows and the bias go last."""
+        B, T, H, C2 = ws.B, self.max_steps, self.rnn_units, self.C2
         gK = self._G("rnn/basic_lstm_cell/kernel")
         gbK = self._G("rnn/basic_lstm_cell/bias")
         if T > 1:
             self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
-        # bias gradient = colsum(sum_t dG_t) = colsum(dGsum), fused here
+        chunk = self.X_GRAD_CHUNK if self.grad_reducer is not None else C2
+        base = self.params.offsets[self._SCOPE_PREFIX + "rnn/basic_lstm_cell/kernel"]
+        # bias gradient = colsum(sum_t dG_t) = colsum(dGsum), fused into chunk 0
+        m_last = 0
         with self._timed("lstm_x_projection_grad"):
-            if self.precision == "bf16":
-                # bf16 configuration: X^T dGsum on bf16 operands (fp32 accumulate);
-                # the forward x-projection stays fp32 (bit-exact counts)
-                self._x_grad_bf16(X, ws, gK[:C2], gbK)
-            else:
-                self._dw(X, ws.dGsum, gK[:C2], B, C2, 4 * H, C2, 4 * H, gbK)
+            for m0 in range(0, C2, chunk):
+                m_last = m0
+                m1 = min(C2, m0 + chunk)
+                bias = gbK if m0 == 0 else None
+                if self.precision == "bf16":
+                    # bf16 configuration: X^T dGsum on bf16 operands (fp32
+                    # accumulate); the forward x-projection stays fp32
+                    self._x_grad_bf16(X, ws, gK, bias, m0, m1)
+                else:
+                    self._dw(X[:, m0:], ws.dGsum, gK[m0:m1], B, m1 - m0, 4 * H, C2, 4 * H, bias)
+                if m1 < C2:
+                    self._reduce_bucket(base + m0 * 4 * H, base + m1 * 4 * H)
+        self._reduce_bucket(base + m_last * 4 * H, self._bucket_split())
 
-    def _x_grad_bf16(self, X, ws, out, bias_out):
+    def _x_grad_bf16(self, X, ws, gK, bias_out, m0, m1):
         B, H, C2 = ws.B, self.rnn_units, self.C2
         C2p = self._pad8(C2)
-        if getattr(ws, "Xb", None) is None:
-            bf = dict(device=self.device, dtype=torch.bfloat16)
-            ws.Xb = torch.zeros((B, C2p), **bf)
-            ws.dGsumb = torch.empty((B, 4 * H), **bf)
-        srcs = _lib.ptr_array([dp(X), dp(ws.dGsum)])
-        dsts = _lib.ptr_array([dp(ws.Xb), dp(ws.dGsumb)])
-        dims = (ctypes.c_int * 14)(B, C2, C2, B, C2p, C2p, 0, B, 4 * H, 4 * H, B, 4 * H, 4 * H, 0)
-        _lib.call("mog_cvt_bf16_batch", 2, srcs, dsts, dims, stream_ptr())
-        self._dw_bf16(ws.Xb, ws.dGsumb, out, B, C2, 4 * H, C2p, 4 * H, bias_out)
+        if m0 == 0:
+            if getattr(ws, "Xb", None) is None:
+                bf = dict(device=self.device, dtype=torch.bfloat16)
+                ws.Xb = torch.zeros((B, C2p), **bf)
+                ws.dGsumb = torch.empty((B, 4 * H), **bf)
+            srcs = _lib.ptr_array([dp(X), dp(ws.dGsum)])
+            dsts = _lib.ptr_array([dp(ws.Xb), dp(ws.dGsumb)])
+            dims = (ctypes.c_int * 14)(B, C2, C2, B, C2p, C2p, 0, B, 4 * H, 4 * H, B, 4 * H,
+                                       4 * H, 0)
+            _lib.call("mog_cvt_bf16_batch", 2, srcs, dsts, dims, stream_ptr())
+        self._dw_bf16(ws.Xb[:, m0:], ws.dGsumb, gK[m0:m1], B, m1 - m0, 4 * H, C2p, 4 * H,
+                      bias_out)
 
     # ------------------------------------------------------------- API ----
     def _prep(self, images, targets):
@@ -852,44 +908,50 @@ class AIRModel:
             tg = torch.as_tensor(targets).to(self.device, torch.int32).contiguous()
         return X, tg
 
-    def train_step_async(self, images, targets=None, noise=None) -> None:
-        """One train step (forward, backward, [all-reduce hook], clip, Adam)
-        with no host synchronisation."""
+    def train_step_async(self, images, targets=None, noise=None,
+                         global_batch: Optional[int] = None) -> None:
+        """One train step (forward, backward, [bucketed all-reduce], clip,
+        Adam) with no host synchronisation.  ``global_batch``: images over all
+        data-parallel ranks this step (default: local batch x grad_world)."""
         if not self.train:
             raise RuntimeError("train_step on a model built with train=False")
         X, tg = self._prep(images, targets)
         ws = self._workspace(X.shape[0])
         ws.alloc_backward(self)
         self._fill_noise(ws, noise)
+        self._global_batch = global_batch
         self._forward(X, tg, ws, need_grad=True, outputs=False)
         self._backward(X, ws)
-        if self.grad_hook is not None:
-            self.grad_hook(self.params.grad)
+        if self.grad_reducer is not None:
+            self.grad_reducer.wait()
         self.params.apply_adam(self.hyper("learning_rate"), self.gradient_clipping_norm)
         self.params.global_step += 1
         self._X = X
 
-    grad_hook = None  # e.g. data-parallel all-reduce of params.grad (SUM)
-
-    def step(self, images, targets=None, noise=None):
+    def step(self, images, targets=None, noise=None, global_batch: Optional[int] = None):
         """``sess.run([training, loss, accuracy, mse_loss, global_step])``
         (training_air_original.py:304-310)."""
-        self.train_step_async(images, targets, noise)
+        self.train_step_async(images, targets, noise, global_batch)
         m = self._ws.means.detach().cpu().numpy()
         return float(m[0]), float(m[1]), float(m[2]), self.params.global_step
 
-    def compute_gradients(self, images, targets=None, noise=None, canvas_cotangent=None):
-        """Forward + backward only (no optimizer update); returns the gradient
-        dict.  ``canvas_cotangent`` [B, C*C] replaces dL/dcanvas of the BCE
-        term (used by the gradient parity tests)."""
+    def compute_gradients(self, images, targets=None, noise=None, canvas_cotangent=None,
+                          global_batch: Optional[int] = None):
+        """Forward + backward (+ the data-parallel all-reduce when attached),
+        no optimizer update; returns the gradient dict.  ``canvas_cotangent``
+        [B, C*C] replaces dL/dcanvas of the BCE term (used by the gradient
+        parity tests)."""
         X, tg = self._prep(images, targets)
         ws = self._workspace(X.shape[0])
         ws.alloc_backward(self)
         self._fill_noise(ws, noise)
+        self._global_batch = global_batch
         self._forward(X, tg, ws, need_grad=True)
         if canvas_cotangent is not None:
             ws.dcanvas.copy_(torch.as_tensor(canvas_cotangent, dtype=torch.float32))
         self._backward(X, ws)
+        if self.grad_reducer is not None:
+            self.grad_reducer.wait()
         return self.params.grad_dict()
 
     def infer(self, images, targets=None, noise=None):

@@ -221,7 +221,6 @@ class AIRModel(_AirBase):
 
     # zsum_hook / live_hook: data-parallel collectives (parallel.attach)
     zsum_hook = None
-    live_hook = None
 
     def _workspace(self, B):
         if self._ws is None or self._ws.B != B:
@@ -354,7 +353,7 @@ class AIRModel(_AirBase):
         parts = ws.cparts
         self._loss_inputs = (X, targets)
         ws.materialized = bool(outputs)
-        gscale = 1.0 / (B * self.grad_world)
+        gscale = self._gscale(B)
         canvas_ptr = dp(ws.canvas) if (outputs or parts is None) else None
         _lib.call("mog_recon_loss", dp(X), canvas_ptr, dp(parts), T if parts is not None else 0,
                   B * C2, dp(ws.prows), self.canvas_size, dp(ws.klsum), dp(ws.digits), dp(targets), B, C2, float(gscale),
@@ -362,7 +361,7 @@ class AIRModel(_AirBase):
                   dp(ws.acc_b) if targets is not None else None,
                   dp(ws.dcanvas) if need_grad else None, s)
         _lib.call("mog_asr_finalize", B, T, self.canvas_size, len(self.constrains_num),
-                  self._cons_arr, g, float(1.0 / (B * self.grad_world)), dp(ws.arec),
+                  self._cons_arr, g, float(self._gscale(B)), dp(ws.arec),
                   dp(ws.live), dp(ws.zsum), dp(ws.pr), dp(ws.loss_b), dp(ws.element),
                   dp(ws.margin), s)
         _lib.call("mog_batch_mean", dp(ws.loss_b), dp(ws.acc_b) if targets is not None else None,
@@ -384,7 +383,7 @@ class AIRModel(_AirBase):
         Ki = self._N("infer_rnn_running/kernel")
         Kg = self._N("gen_rnn_running/kernel")
         KU = Z + 3 + H
-        gscale = 1.0 / (B * self.grad_world)
+        gscale = self._gscale(B)
         fix = -1 if self.fix_steps is None else int(self.fix_steps)
         w20 = self._w20()
         ws.dh.zero_()
@@ -445,6 +444,7 @@ class AIRModel(_AirBase):
                           dp(ws.dz_carry), dp(ws.dss_carry), dp(ws.dh[t - 1]),
                           dp(ws.dhg[t - 1]), s)
         self._weight_grads(X, ws)
+        self._reduce_bucket(0, self.params.total)
 
     def _weight_grads(self, X, ws):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
@@ -458,7 +458,7 @@ class AIRModel(_AirBase):
         gKi, gKg = G("infer_rnn_running/kernel"), G("gen_rnn_running/kernel")
         # LSTMCells: x rows from sum_t dG (the x input is loop-invariant)
         if self.precision == "bf16":
-            self._x_grad_bf16(X, ws, gKi[:C2], G("infer_rnn_running/bias"))
+            self._x_grad_bf16(X, ws, gKi, G("infer_rnn_running/bias"), 0, C2)
         else:
             self._dw(X, ws.dGsum, gKi[:C2], B, C2, 4 * H, C2, 4 * H, G("infer_rnn_running/bias"))
         self._dw(ws.U, ws.dG, gKi[C2:], TB, KU, 4 * H, LU, 4 * H)

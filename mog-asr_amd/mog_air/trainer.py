@@ -79,6 +79,7 @@ class Dist:
         return self.rank == 0
 
     def shard(self, x, k):
+        """This rank's contiguous part of a global batch."""
         if self.world == 1:
             return x, k
         from .parallel import shard
@@ -287,6 +288,7 @@ def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, mod
     """The iteration loop of training_air_original.py:226-503 (logging every
     20, testing every 200, parameters every 10,000 iterations; the final
     test when the input runs out)."""
+    ctx = ctx or Dist()
     batcher = records.ShuffleBatcher(tr_x, tr_k, BATCH_SIZE, EPOCHS,
                                      min_after_dequeue=min(10000, len(tr_k)))
     saver = Saver(models_folder, "air-model")
@@ -305,8 +307,11 @@ def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, mod
         log.info("iteration {}\ttest loss {:.3f}\ttest accuracy {:.2f}, test mse {:.3f}".format(
             tag, tl, ta, tm))
         p, r, gt_iou, det_iou, g_iou = evaluation(test[3], test[4], sh, sc, nd, csize=canvas)
+        # integer steps are padded to 6 as training_air_original.py:357 does
+        # ('final' is printed as is)
+        step_tag = "{:6d}".format(tag) if isinstance(tag, int) else tag
         log.info("test:{}\tprecision:{}\trecall:{}\tgtIoU:{:.4f}\tdetectionIoU:{:.4f}"
-                 "\tglobaliou:{:.4f}".format(tag, p, r, gt_iou, det_iou, g_iou))
+                 "\tglobaliou:{:.4f}".format(step_tag, p, r, gt_iou, det_iou, g_iou))
         return tl, ta, tm, g_iou
 
     log.info("Training...\n")
@@ -314,8 +319,9 @@ def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, mod
         while True:
             if step % SAVE_PARAMS_EACH_ITERATIONS == 0 and ctx.main:
                 saver.save(train_model.params, step)
-            x, k = ctx.shard(*batcher.next_batch())
-            loss, acc, mse, step = train_model.step(x, k)
+            xg, kg = batcher.next_batch()
+            x, k = ctx.shard(xg, kg)
+            loss, acc, mse, step = train_model.step(x, k, global_batch=len(kg))
             if extra_log is not None:
                 extra_log(train_model, step)
             hist.append([loss, acc, mse])
@@ -367,13 +373,13 @@ def train_loop_asr(args, train_model, test_model, tr_x, tr_k, test, canvas, log,
         tl, ta, tm, sc, sh, nd = run_test(test_model, test, canvas, args.test_batch)
         ctx.barrier()
         p, r, gt_iou, det_iou, g_iou = evaluation(test[3], test[4], sh, sc, nd, csize=canvas)
-        log.info("test:{}\tprecision:{}\trecall:{}\tgtIoU:{:.4f}\tdetectionIoU:{:.4f}"
+        log.info("test:{:6d}\tprecision:{}\trecall:{}\tgtIoU:{:.4f}\tdetectionIoU:{:.4f}"
                  "\tglobal_iou:{:.4f}".format(tag, p, r, gt_iou, det_iou, g_iou))
         lv = test_model.log_variables
         if update_flag:
             update_flag = False
             best[:] = [lv["elbo"], lv["accu"], lv["mse"], g_iou]
-        log.info("test:{}\t".format(tag) +
+        log.info("test:{:6d}\t".format(tag) +
                  "".join("{}:{:.4f}\t".format(n, v) for n, v in lv.items()))
         log.info("Current Best: elbo:{}\taccu:{}\tmse:{}\tiou:{}".format(*best))
 
@@ -382,8 +388,9 @@ def train_loop_asr(args, train_model, test_model, tr_x, tr_k, test, canvas, log,
         while True:
             if step % SAVE_PARAMS_EACH_ITERATIONS == 0 and ctx.main:
                 saver.save(train_model.params, step)
-            x, k = ctx.shard(*batcher.next_batch())
-            _, _, _, step = train_model.step(x, k)
+            xg, kg = batcher.next_batch()
+            x, k = ctx.shard(xg, kg)
+            _, _, _, step = train_model.step(x, k, global_batch=len(kg))
             for n, v in train_model.log_variables.items():
                 logged.setdefault(n, []).append(v)
             if step % LOG_EACH_ITERATION == 0:
@@ -400,7 +407,7 @@ def train_loop_asr(args, train_model, test_model, tr_x, tr_k, test, canvas, log,
             if args.iterations and step >= args.iterations:
                 raise StopIteration
     except StopIteration:
-        test_and_log("final")
+        test_and_log(step)  # the reference logs the step here too (train_air_pr.py:426-430)
         log.info("Final Best: elbo:{}\taccu:{}\tmse:{}\tiou:{}".format(*best))
         log.info("\ntraining has ended\n")
     return step

@@ -39,6 +39,9 @@ CASES = {
     # test model (rounded z_pres), 6 steps as the entry points, -ap prior
     "air_fwd_test_ap_b5": dict(cfg=dict(batch=5, max_steps=6, train=False, num_prior=(1, 3)),
                                pseed=21, nseed=22, xseed=23),
+    # Multi-dSprites canvas (configs[3]: C = 64, multi_dsprites.py:391-392), train model
+    "air_fwd_train_c64_b4": dict(cfg=dict(batch=4, max_steps=3, train=True, canvas_size=64),
+                                 pseed=41, nseed=42, xseed=43, side=(22, 30)),
 }
 
 
@@ -46,7 +49,8 @@ def make_forward(name, spec):
     cfg = ao.AirConfig(scale_prior_variance=0.05, z_pres_prior_log_odds=-0.01, **spec["cfg"])
     P = ao.init_params(cfg, seed=spec["pseed"], bias_scale=0.05)
     nz = ao.make_noise(cfg, seed=spec["nseed"])
-    x, k = ao.synthetic_canvases(cfg.batch, seed=spec["xseed"])
+    x, k = ao.synthetic_canvases(cfg.batch, canvas=cfg.canvas_size, seed=spec["xseed"],
+                                 side=spec.get("side", (17, 23)))
     ref = ao.forward(cfg, P, nz, x, k)
     out = {"x": x, "targets": k, "param_seed": spec["pseed"], "param_checksum": param_checksum(P),
            "T": ref["T"], "loss_mean": ref["loss_mean"], "accuracy": ref["accuracy"]}

@@ -3,11 +3,14 @@ MI355X_MICROARCH.md §HBM prescribes) into profiles/pmc_summary.json.
 
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports exactly half
 of the bytes of a wide (16 B/lane) coalesced read, so it is doubled; WRITE_SIZE
-is exact for 16 B/lane stores.  Both counters are in KiB.
+is exact for 16 B/lane stores and float atomics.  Both counters are in KiB.
 
-Tag -> kernel selection: the tagged launch is the dispatch of the named kernel
-symbol with the largest FETCH_SIZE in each train step (the x-projection GEMM
-shares its template instantiation with the smaller recurrent GEMMs).
+Tag -> dispatch selection: the kernel symbol AND the launch grid (total
+work-items) of the launch bench.py times, then, among those dispatches, the
+ones with the largest FETCH_SIZE (the x-projection shares symbol and grid
+with the two smaller recurrent GEMMs of the same step).  The grids below are
+those of the bench workloads: per-GPU batch 8192 (fp32 headline, bf16
+configs[1]) and the stand-alone fused-step roofline runs at 65,536.
 
 usage: python scripts/pmc_summary.py <fetch_dir> <write_dir> [out.json]
 """
@@ -17,10 +20,32 @@ import json
 import os
 import sys
 
+B = 8192
+
+
+def _ceil(a, b):
+    return (a + b - 1) // b
+
+
+def _x_grad_grid_fp32(B, C2=2500, N=1024, target=2048):
+    """gemm_f32 transA split-K launch of dWx (air_model._dw, launch_tile)."""
+    tiles = _ceil(C2, 64) * _ceil(N, 64)
+    splitk = max(1, min(B // 256, _ceil(target, tiles)))
+    kchunk = _ceil(_ceil(B, splitk), 16) * 16
+    return tiles * _ceil(B, kchunk) * 256
+
+
+# tag -> (kernel symbol substring, grid work-items)
 TAGS = {
-    "lstm_x_projection": "gemm_f32_kernel<128, 128, false, false, 0>",
-    "lstm_x_projection_grad": "gemm_f32_kernel<64, 64, true, false, 5>",
-    "stn_vae_step": "stn_vae_step",
+    "lstm_x_projection_fp32_b%d" % B: ("gemm_f32_kernel<128, 128, false, false, 0>",
+                                       (1024 // 128) * (B // 128) * 256),
+    "lstm_x_projection_grad_fp32_b%d" % B: ("gemm_f32_kernel<64, 64, true, false, 5>",
+                                            _x_grad_grid_fp32(B)),
+    "lstm_x_projection_bf16_b%d" % B: ("gemm_f32_kernel<128, 128, false, false, 0>",
+                                       (1024 // 128) * (B // 128) * 256),
+    "stn_vae_step_bf16_b%d" % B: ("stn_vae_step", B // 32 * 1024),
+    "stn_vae_step_b65536": ("stn_vae_step", 65536 // 64 * 1024),
+    "stn_vae_step_b65536_c64": ("stn_vae_step", 65536 // 64 * 1024),
 }
 
 
@@ -34,46 +59,42 @@ def load(d, counter):
     return rows
 
 
-def per_kernel(rows, symbol, grid=None):
-    vals = [(int(r["Dispatch_Id"]), float(r["Counter_Value"])) for r in rows
-            if symbol in r["Kernel_Name"]
-            and (grid is None or int(float(r.get("Grid_Size", -1))) == grid)]
-    return sorted(vals)
+def per_kernel(rows, symbol, grid):
+    return sorted((int(r["Dispatch_Id"]), float(r["Counter_Value"]), r) for r in rows
+                  if symbol in r["Kernel_Name"] and int(float(r.get("Grid_Size", -1))) == grid)
 
 
 def main():
     fdir, wdir = sys.argv[1], sys.argv[2]
     out = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_summary.json"
     fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
-    res = {"_note": "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024, "
-                    "gfx950 FETCH_SIZE halving corrected; averaged over the largest-fetch "
-                    "dispatch of the tagged kernel symbol per train step"}
-    jobs = [(tag, sym, None) for tag, sym in TAGS.items()]
-    # the fused step kernel runs at the bench batch (8192: 256 workgroups of 32
-    # images x 1024 threads) and in the stand-alone north-star roofline run
-    # (65,536: 1024 workgroups of 64 images x 1024 threads)
-    jobs = [j for j in jobs if j[0] != "stn_vae_step"] + [
-        ("stn_vae_step", "stn_vae_step", 8192 // 32 * 1024),
-        ("stn_vae_step_b65536", "stn_vae_step", 65536 // 64 * 1024)]
-    for tag, sym, grid in jobs:
+    res = {"_note": "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024 (gfx950 "
+                    "FETCH_SIZE halving corrected), averaged over the dispatches of the tagged "
+                    "kernel symbol with the bench launch's grid and >= 0.5x the largest fetch"}
+    for tag, (sym, grid) in TAGS.items():
         fv, wv = per_kernel(fetch, sym, grid), per_kernel(write, sym, grid)
         if not fv or not wv:
             continue
-        fmax = max(v for _, v in fv)
-        fsel = [v for _, v in fv if v >= 0.5 * fmax]
-        wmax = max(v for _, v in wv)
-        wsel = [v for _, v in wv if v >= 0.5 * wmax] if tag.endswith("grad") else \
-            [v for (i, v) in wv][:len(fsel)]
-        # pair write dispatches with the selected fetch dispatches by order
-        fids = [i for i, v in fv if v >= 0.5 * fmax]
-        wmap = dict(wv)
-        wsel = [wmap.get(i) for i in fids if wmap.get(i) is not None] or wsel
-        fk = sum(fsel) / len(fsel)
+        fmax = max(v for _, v, _ in fv)
+        fsel = [(i, v) for i, v, _ in fv if v >= 0.5 * fmax]
+        # fused-step runs at C = 50 and C = 64 share symbol and grid: the
+        # C = 64 run comes second in the bench (dispatch order)
+        if tag.startswith("stn_vae_step_b65536"):
+            half = len(fsel) // 2
+            fsel = fsel[half:] if tag.endswith("_c64") else fsel[:half]
+            if not fsel:
+                continue
+        ids = [i for i, _ in fsel]
+        wmap = {i: v for i, v, _ in wv}
+        wsel = [wmap[i] for i in ids if i in wmap]
+        if not wsel:  # separate passes: dispatch ids do not line up, pair by order
+            wsel = [v for _, v, _ in wv][:len(fsel)]
+        fk = sum(v for _, v in fsel) / len(fsel)
         wk = sum(wsel) / len(wsel)
-        res[tag] = {"kernel_symbol": sym, "grid_threads": grid, "fetch_kib": fk, "write_kib": wk,
-                    "dispatches": len(fsel),
+        res[tag] = {"kernel_symbol": sym, "grid_threads": grid, "fetch_kib": fk,
+                    "write_kib": wk, "dispatches": len(fsel),
                     "hbm_bytes_per_launch": (2.0 * fk + wk) * 1024.0}
-    os.makedirs(os.path.dirname(out), exist_ok=True)
+    os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))

@@ -109,7 +109,8 @@ def asr_main(out_path):
         return zs
 
     g, loss, T = asr_grads(cfg, P, nz, x, G, lo, hi, live_reduce, zsum_reduce)
-    m.grad_hook(g)
+    m.grad_reducer.launch(g)
+    m.grad_reducer.wait()
     lt = torch.tensor([loss], dtype=torch.float64)
     dist.all_reduce(lt)  # shard losses add up to the full-batch loss (margin counted per rank)
     if rank == 0:

@@ -1,0 +1,124 @@
+"""One rank of tests/test_gpu_dp.py: the HIP AIR / AIR-ASR model on cuda:0
+with a gloo process group (several ranks share the one GPU of a test box;
+the RCCL path is the same code with backend "nccl").  Each rank runs its
+contiguous shard of the batch through ``compute_gradients`` with
+``parallel.attach`` installed (bucketed async all-reduce, global loop
+predicate, ASR batch-mean hook) and saves what it saw.
+
+usage: gpu_dp_worker.py <out_prefix> air|asr"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "mog-asr_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from mog_air import parallel  # noqa: E402
+
+DEV = "cuda:0"
+
+
+def air_case():
+    from oracle import air_oracle as ao
+    cfg = ao.AirConfig(batch=13, max_steps=3, train=True, num_prior=(1, 3),
+                       scale_prior_variance=0.05, z_pres_prior_log_odds=-0.01)
+    P = ao.init_params(cfg, seed=71, bias_scale=0.05)
+    nz = ao.make_noise(cfg, seed=72)
+    x, k = ao.synthetic_canvases(cfg.batch, seed=73)
+    G = (np.random.default_rng(74).standard_normal((cfg.batch, 2500)) * 0.01).astype(np.float32)
+    return cfg, P, nz, x, k, G
+
+
+def air_model(cfg, P, world, scope):
+    from mog_air.air_model import AIRModel
+    m = AIRModel(max_steps=cfg.max_steps, canvas_size=cfg.canvas_size,
+                 scale_prior_variance=cfg.scale_prior_variance,
+                 z_pres_prior_log_odds=cfg.z_pres_prior_log_odds,
+                 z_pres_temperature=cfg.z_pres_temperature,
+                 stopping_threshold=cfg.stopping_threshold,
+                 vae_likelihood_std=cfg.vae_likelihood_std, learning_rate=1e-4,
+                 gradient_clipping_norm=1.0, cnn=False, train=True, num_prior=cfg.num_prior,
+                 scope=scope, device=DEV, grad_world=world)
+    m.params.load_dict(P)
+    return m
+
+
+def asr_case():
+    from oracle import air_oracle as ao
+    from oracle import asr_oracle as so
+    cfg = so.AsrConfig(batch=11, max_steps=4, constrains_num=(1, 3), constrains_num_gamma=0.5,
+                       constrains_margin_gamma=100.0, constrains_num_element_gamma=10.0,
+                       constrains_bbox_gamma=1.0, constrains_sharesize_gamma=0.3,
+                       constrains_area_gamma=0.2, constrains_area_minmax=(17.0, 23.0),
+                       stopping_threshold=0.5, z_pres_temperature=1.0)
+    P = so.init_params(cfg, seed=81, bias_scale=0.05)
+    nz = so.make_noise(cfg, seed=82)
+    x, k = ao.synthetic_canvases(cfg.batch, seed=83)
+    G = (np.random.default_rng(84).standard_normal((cfg.batch, 2500)) * 0.01).astype(np.float32)
+    return cfg, P, nz, x, k, G
+
+
+def asr_model(cfg, P, world, scope):
+    from mog_air.asr_model import AIRModel
+    m = AIRModel(max_steps=cfg.max_steps, max_digits=cfg.max_steps, canvas_size=cfg.canvas_size,
+                 vae_likelihood_std=cfg.vae_likelihood_std, z_pres_prior_log_odds=-0.01,
+                 z_pres_temperature=cfg.z_pres_temperature,
+                 stopping_threshold=cfg.stopping_threshold, learning_rate=1e-4,
+                 gradient_clipping_norm=1.0, cnn=False, train=True, scope=scope,
+                 constrains_num=list(cfg.constrains_num),
+                 constrains_num_gamma=cfg.constrains_num_gamma,
+                 constrains_margin_gamma=cfg.constrains_margin_gamma,
+                 constrains_num_element_gamma=cfg.constrains_num_element_gamma,
+                 constrains_bbox_gamma=cfg.constrains_bbox_gamma,
+                 constrains_sharesize_gamma=cfg.constrains_sharesize_gamma,
+                 constrains_area_gamma=cfg.constrains_area_gamma,
+                 constrains_area_minmax=list(cfg.constrains_area_minmax),
+                 fix_steps=cfg.fix_steps, device=DEV, grad_world=world)
+    m.params.load_dict(P)
+    return m
+
+
+def run(kind, lo, hi, world, scope, attach=True):
+    """compute_gradients on images [lo, hi) of the case; returns a dict."""
+    cfg, P, nz, x, k, G = air_case() if kind == "air" else asr_case()
+    m = (air_model if kind == "air" else asr_model)(cfg, P, world, scope)
+    reducer = None
+    if attach and world > 1:
+        reducer = parallel.attach(m, global_steps=True)
+        reducer.log = []
+    noise = {n: torch.as_tensor(np.ascontiguousarray(v[:, lo:hi])).to(DEV) for n, v in nz.items()}
+    grads = m.compute_gradients(x[lo:hi], k[lo:hi], noise=noise,
+                                canvas_cotangent=torch.as_tensor(G[lo:hi]).to(DEV),
+                                global_batch=cfg.batch)
+    names = sorted(grads)
+    out = {"g": np.concatenate([grads[n].reshape(-1) for n in names]),
+           "T": np.array([m.executed_steps]),
+           "digits": m.rec_num_digits.cpu().numpy(),
+           "loss_b": m.per_image_loss.cpu().numpy(),
+           "mean": np.array([m.loss])}
+    if reducer is not None:
+        out["buckets"] = np.array(reducer.log)
+    if kind == "asr":
+        out["margin"] = m._ws.margin.cpu().numpy()
+    return out
+
+
+def main():
+    prefix, kind = sys.argv[1], sys.argv[2]
+    dist.init_process_group("gloo")
+    try:
+        rank, world = dist.get_rank(), dist.get_world_size()
+        n = 13 if kind == "air" else 11
+        lo, hi = parallel.shard(n, rank, world)
+        res = run(kind, lo, hi, world, scope=f"dp_{kind}_{rank}")
+        np.savez(f"{prefix}_{rank}.npz", lo=np.array([lo]), hi=np.array([hi]), **res)
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -46,7 +46,7 @@ def _load(path):
 
 
 def test_golden_files_present():
-    assert len(FWD) >= 2 and os.path.exists(os.path.join(GOLD, "air_adam_step_b4.npz"))
+    assert len(FWD) >= 3 and os.path.exists(os.path.join(GOLD, "air_adam_step_b4.npz"))
 
 
 @pytest.mark.parametrize("path", FWD, ids=os.path.basename)
@@ -91,7 +91,7 @@ def test_torch_oracle_reproduces_golden_adam_step():
 
 def _gpu_model(cfg, P, scope, precision="fp32"):
     from mog_air.air_model import AIRModel
-    m = AIRModel(max_steps=cfg.max_steps, scale_prior_variance=0.05,
+    m = AIRModel(max_steps=cfg.max_steps, canvas_size=cfg.canvas_size, scale_prior_variance=0.05,
                  z_pres_prior_log_odds=-0.01, learning_rate=1e-4, gradient_clipping_norm=1.0,
                  cnn=False, train=cfg.train, scope=scope, device="cuda:0",
                  num_prior=list(cfg.num_prior) if cfg.num_prior else None, precision=precision)
@@ -118,9 +118,9 @@ def test_hip_reproduces_golden_forward(path):
     np.testing.assert_array_equal(m.rec_num_digits.cpu().numpy(), g["out_digits"])
     np.testing.assert_allclose(m.per_image_loss.cpu().numpy(), g["out_loss"], rtol=1e-5)
     # batch-mean -ELBO: 1e-3 absolute or, for losses in the
-    # thousands, the same 1e-6 relative the block-tree BCE sum allows
+    # thousands (fp32 ulp 5e-4 at 6,000), the per-image 1e-5 relative bar
     ref = float(g["loss_mean"])
-    assert abs(m.loss - ref) <= max(1e-3, 1e-6 * abs(ref))
+    assert abs(m.loss - ref) <= max(1e-3, 1e-5 * abs(ref))
 
 
 @pytest.mark.gpu

@@ -38,4 +38,6 @@ def test_train_air_pr_runs(tmp_path, monkeypatch, flags):
     assert step == 21
     text = open(glob.glob(str(tmp_path / "res_(p)" / "logfile*.log"))[0]).read()
     assert "step:    20\t" in text and "num_margin" in text and "TotLoss" in text
-    assert "test:final\tprecision" in text and "training has ended" in text
+    # the ASR trainer logs its final test under the step number
+    # (train_air_pr.py:426-430), unlike training_air_original.py's 'final'
+    assert "test:    21\tprecision" in text and "training has ended" in text

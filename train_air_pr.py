@@ -80,6 +80,7 @@ def main(argv=None):
             constrains_area_gamma=args.gamma_area, constrains_area_minmax=[size_min, size_max],
             fix_steps=digits[0] if len(digits) == 1 else None, annealing_schedules={},
             device=args.device, seed=1235, precision=args.precision,
+            noise_seed=1235 + ctx.rank,  # independent Monte-Carlo noise per rank
             grad_world=ctx.world if i == 0 else 1))
     train_model, test_model = models
     trainer.attach_data_parallel(train_model, ctx)

@@ -66,6 +66,7 @@ def main(argv=None):
                 "staircase": False, "log": True}},
             num_prior=digits if args.add_prior else None,
             device=args.device, seed=1235, precision=args.precision,
+            noise_seed=1235 + ctx.rank,  # independent Monte-Carlo noise per rank
             grad_world=ctx.world if i == 0 else 1))
     train_model, test_model = models
     trainer.attach_data_parallel(train_model, ctx)
