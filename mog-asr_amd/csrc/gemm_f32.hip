@@ -11,8 +11,10 @@
 // contrib/layers fully_connected as used at vae.py:18-41, air_model.py:462-499).
 //
 // Tiles: 64x64 or 128x128 per 256-thread workgroup (2x2 waves, each wave
-// (BM/2)x(BN/2) of 16x16 MFMA tiles), BK = 16, register-staged double
-// buffering (next tile's global loads in flight during the MFMAs).
+// (BM/2)x(BN/2) of 16x16 MFMA tiles), BK = 16, operands through raw buffer
+// descriptors, register-staged double buffering (next tile's global loads in
+// flight during the MFMAs), k-permuted LDS rows read as one ds_read_b128 per
+// fragment per k-tile.
 //
 // Weight-gradient form: transA + EPI_ATOMIC + split-K computes dW += X^T dY;
 // when `colsum` is given the workgroups of the first M-tile row also add the
@@ -21,6 +23,10 @@
 //
 // Replaces the TF-1.12 MatMul / BiasAdd / Softplus / Relu / Sigmoid op groups
 // of the hot path (SURVEY.md §2 table "TF op group on the hot path").
+#include <cstdlib>
+#include <cstring>
+#include <type_traits>
+
 #include "mog_common.h"
 
 namespace {
@@ -52,7 +58,30 @@ struct GemmDims {
   float aux_scale;
 };
 
-constexpr int BK = 16, PADF = 16;
+// LDS image of a BK-deep slice of an operand: one row of Lay<BK>::S floats
+// per m (A) or n (B).  The BK k values of a row are stored PERMUTED: k =
+// 4 kk + g lives in 4-float chunk ci = g (BK/16) + kk / 4 (XOR-swizzled by the
+// row), position kk % 4, so lane (row, g) of a 16x16x4 MFMA fragment reads four
+// consecutive k-steps with ONE ds_read_b128.  Strides / swizzles were searched
+// to be conflict-free for those reads and for the tile writes under the gfx950
+// LDS lane grouping (MI355X_MICROARCH.md §LDS): BK = 16 -> S = 24, no
+// swizzle; BK = 32 -> S = 48, chunk ^= row & 7.
+template <int BK>
+struct Lay;
+template <>
+struct Lay<16> {
+  static constexpr int S = 24;
+  __device__ static __forceinline__ int sw(int) { return 0; }
+};
+template <>
+struct Lay<32> {
+  static constexpr int S = 48;
+  __device__ static __forceinline__ int sw(int row) { return row & 7; }
+};
+template <int BK>
+__device__ __forceinline__ int lpos(int row, int g, int kk) {  // float index of (row, k = 4 kk + g)
+  return row * Lay<BK>::S + 4 * ((g * (BK / 16) + (kk >> 2)) ^ Lay<BK>::sw(row)) + (kk & 3);
+}
 
 // bijective XCD-grouping remap of the linear workgroup id (guide §5, T1):
 // consecutive ids (same A row-panel, neighbouring N tiles) share one XCD's L2
@@ -61,22 +90,104 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-template <int BM, int BN, bool TA, bool TB, int EPI>
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frsrc(const float* p, long elems) {
+  // raw buffer over [p, p + elems): loads past the end return 0 (no fault)
+  const long bytes = elems * 4;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0,
+                                           (int)(bytes < 0x7ffffff0L ? bytes : 0x7ffffff0L),
+                                           0x00020000);
+}
+
+// One operand tile (ROWS x BK) moving global -> registers -> LDS, through a
+// raw buffer descriptor (32-bit offsets; rows past the operand's extent read
+// 0).  Interior k-tiles (`full`) load without per-element checks; only the
+// ragged last k-tile of a split masks k >= kend.
+//   KC (k-contiguous in memory: A [M][K], B^T [N][K]): float4 loads along k,
+//     four ds_write_b32 into the permuted row.
+//   otherwise (row-contiguous: A^T [K][M], B [K][N]): per (row, g) BK/4 dword
+//     loads at k = g, 4+g, 8+g, ... (coalesced over rows across lanes), one
+//     ds_write_b128 per four of them.
+template <int ROWS, bool KC, int BK>
+struct TileIO {
+  static constexpr int KK = BK / 4;
+  static constexpr int NV = ROWS * BK / 1024;  // KC: float4 per thread
+  static constexpr int NP = ROWS * 4 / 256;    // row-contiguous: (row, g) pairs per thread
+  static constexpr int NR = KC ? NV * 4 : NP * KK;
+  float r[NR];
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, int ld, int r0, int k0,
+                                       int kend, bool vec, bool full, int t) {
+    if constexpr (KC) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int q = t + 256 * i;
+        const int row = q / KK, c = q % KK;  // KK float4 chunks per BK-deep row
+        const int gk = k0 + 4 * c;
+        const int off = ((r0 + row) * ld + gk) * 4;
+        if (full && vec) {
+          const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r[4 * i + j] = __uint_as_float(v[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float v =
+                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * j, 0, 0));
+            r[4 * i + j] = (full || gk + j < kend) ? v : 0.0f;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int q = t + 256 * i;
+        const int row = q % ROWS, g = q / ROWS;  // lanes run along the contiguous rows
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          const int gk = k0 + 4 * kk + g;
+          const float v = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(rs, (gk * ld + r0 + row) * 4, 0, 0));
+          r[KK * i + kk] = (full || gk < kend) ? v : 0.0f;
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float* S, int t) const {
+    if constexpr (KC) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int q = t + 256 * i;
+        const int row = q / KK, c = q % KK;  // chunk c holds kk = c for g = 0..3
+#pragma unroll
+        for (int g = 0; g < 4; ++g) S[lpos<BK>(row, g, c)] = r[4 * i + g];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int q = t + 256 * i;
+        const int row = q % ROWS, g = q / ROWS;
+#pragma unroll
+        for (int h = 0; h < KK / 4; ++h)
+          *reinterpret_cast<floatx4*>(&S[lpos<BK>(row, g, 4 * h)]) =
+              floatx4{r[KK * i + 4 * h], r[KK * i + 4 * h + 1], r[KK * i + 4 * h + 2],
+                      r[KK * i + 4 * h + 3]};
+      }
+    }
+  }
+};
+
+template <int BM, int BN, int BK, int PF, bool TA, bool TB, int EPI, bool KSEG>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
 #pragma clang fp contract(off)
-  constexpr int MI = BM / 32, NI = BN / 32;     // 16x16 tiles per wave
-  constexpr int NA = BM * BK / 1024, NB = BN * BK / 1024;  // float4 loads per thread
-  constexpr int CPR = BK / 4;                              // float4 chunks per k-row
-  constexpr int LDA_S = BM + PADF, LDB_S = BN + PADF;
-  constexpr int STAGE = BK * (LDA_S + LDB_S);
-  // two pipeline stages in ONE shared array: [stage][A: BK x LDA_S | B: BK x LDB_S]
+  constexpr int MI = BM / 32, NI = BN / 32;     // 16x16 tiles per wave (2x2 waves)
+  constexpr int KK = BK / 4;                    // MFMA k-steps per tile
+  constexpr int A_SZ = BM * Lay<BK>::S, STAGE = (BM + BN) * Lay<BK>::S;
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
   const int nwg = gridDim.x * gridDim.y * gridDim.z;
   const int wg = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nwg);
   const int bx = wg % D.nx, by = (wg / D.nx) % D.ny, bz = wg / (D.nx * D.ny);
   const int z = bz / D.splitk, ks = bz - z * D.splitk;
-  const float* __restrict__ A = P.A[z];
-  const float* __restrict__ Bm = P.B[z];
   const int m0 = by * BM, n0 = bx * BN;
   const int kbeg = ks * D.kchunk;
   const int kend = min(D.K, kbeg + D.kchunk);
@@ -104,142 +215,100 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
         acc[mi][ni][r] = v;
       }
 
-  float ra[NA][4], rb[NB][4];
-  auto load_tiles = [&](int k0) {
-    const float* __restrict__ Aq = A;
-    const float* __restrict__ Bq = Bm;
-    int koff = 0;
-    if (D.kseg > 0) {  // a BK tile never straddles two segments (kseg % BK == 0)
+  // operand extents (elements) behind the buffer descriptors: A rows < M
+  // (TA: k rows < K of lda), B likewise; per K-segment when KSEG
+  const int ka = KSEG ? D.kseg : D.K;
+  const long extA = TA ? (long)(ka - 1) * D.lda + M : (long)(M - 1) * D.lda + ka;
+  const long extB = TB ? (long)(N - 1) * D.ldb + ka : (long)(ka - 1) * D.ldb + N;
+  __amdgpu_buffer_rsrc_t ra = frsrc(P.A[KSEG ? 0 : z], extA);
+  __amdgpu_buffer_rsrc_t rb = frsrc(P.B[KSEG ? 0 : z], extB);
+  int seg = 0;
+
+  // PF register sets of staged tiles: tile j+1 is loaded PF iterations
+  // before it is written to LDS (PF = 2 hides an HBM miss behind two k-tiles)
+  TileIO<BM, !TA, BK> ta[PF];
+  TileIO<BN, TB, BK> tb[PF];
+  auto load_tiles = [&](int k0, TileIO<BM, !TA, BK>& A_, TileIO<BN, TB, BK>& B_) {
+    int kl = k0, kl_end = kend;
+    if (KSEG) {  // a BK tile never straddles two segments (kseg % BK == 0)
       const int sg = k0 / D.kseg;
-      Aq = P.A[sg];
-      Bq = P.B[sg];
-      koff = sg * D.kseg;
-    }
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int q = t + 256 * i;
-      if (!TA) {
-        const int row = q / CPR, kc = (q % CPR) * 4;
-        const int gm = m0 + row, gk = k0 + kc;
-        if (D.vecA && gm < M && gk + 3 < kend) {
-          const float4 v = *reinterpret_cast<const float4*>(Aq + (size_t)gm * D.lda + (gk - koff));
-          ra[i][0] = v.x; ra[i][1] = v.y; ra[i][2] = v.z; ra[i][3] = v.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            ra[i][j] = (gm < M && gk + j < kend) ? Aq[(size_t)gm * D.lda + (gk - koff) + j] : 0.0f;
-        }
-      } else {
-        const int k = q / (BM / 4), mc = (q % (BM / 4)) * 4;
-        const int gk = k0 + k, gm = m0 + mc;
-        if (D.vecA && gk < kend && gm + 3 < M) {
-          const float4 v = *reinterpret_cast<const float4*>(Aq + (size_t)(gk - koff) * D.lda + gm);
-          ra[i][0] = v.x; ra[i][1] = v.y; ra[i][2] = v.z; ra[i][3] = v.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            ra[i][j] = (gk < kend && gm + j < M) ? Aq[(size_t)(gk - koff) * D.lda + gm + j] : 0.0f;
-        }
+      if (sg != seg) {
+        seg = sg;
+        ra = frsrc(P.A[sg], extA);
+        rb = frsrc(P.B[sg], extB);
       }
+      kl = k0 - sg * D.kseg;
+      kl_end = kend - sg * D.kseg;
     }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int q = t + 256 * i;
-      if (!TB) {
-        const int k = q / (BN / 4), nc = (q % (BN / 4)) * 4;
-        const int gk = k0 + k, gn = n0 + nc;
-        if (D.vecB && gk < kend && gn + 3 < N) {
-          const float4 v = *reinterpret_cast<const float4*>(Bq + (size_t)(gk - koff) * D.ldb + gn);
-          rb[i][0] = v.x; rb[i][1] = v.y; rb[i][2] = v.z; rb[i][3] = v.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            rb[i][j] = (gk < kend && gn + j < N) ? Bq[(size_t)(gk - koff) * D.ldb + gn + j] : 0.0f;
-        }
-      } else {
-        const int n = q / CPR, kc = (q % CPR) * 4;
-        const int gn = n0 + n, gk = k0 + kc;
-        if (D.vecB && gn < N && gk + 3 < kend) {
-          const float4 v = *reinterpret_cast<const float4*>(Bq + (size_t)gn * D.ldb + (gk - koff));
-          rb[i][0] = v.x; rb[i][1] = v.y; rb[i][2] = v.z; rb[i][3] = v.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            rb[i][j] = (gn < N && gk + j < kend) ? Bq[(size_t)gn * D.ldb + (gk - koff) + j] : 0.0f;
-        }
-      }
-    }
+    const bool full = k0 + BK <= kend;
+    A_.load(ra, D.lda, m0, kl, kl_end, D.vecA, full, t);
+    B_.load(rb, D.ldb, n0, kl, kl_end, D.vecB, full, t);
   };
-  auto store_tiles = [&](int stage) {
+  auto store_tiles = [&](int stage, const TileIO<BM, !TA, BK>& A_,
+                         const TileIO<BN, TB, BK>& B_) {
     float* As = lds + stage * STAGE;
-    float* Bs = As + BK * LDA_S;
+    A_.store(As, t);
+    B_.store(As + A_SZ, t);
+  };
+  const int fr = lane & 15, fg = lane >> 4;
+  floatx4 fa[MI][KK / 4], fb[NI][KK / 4];
+  auto read_frags = [&](int stage) {
+    const float* As = lds + stage * STAGE;
+    const float* Bs = As + A_SZ;
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int q = t + 256 * i;
-      if (!TA) {
-        const int row = q / CPR, kc = (q % CPR) * 4;
+    for (int h = 0; h < KK / 4; ++h) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) As[(kc + j) * LDA_S + row] = ra[i][j];
-      } else {
-        const int k = q / (BM / 4), mc = (q % (BM / 4)) * 4;
-        *reinterpret_cast<floatx4*>(&As[k * LDA_S + mc]) =
-            floatx4{ra[i][0], ra[i][1], ra[i][2], ra[i][3]};
-      }
+      for (int mi = 0; mi < MI; ++mi)
+        fa[mi][h] = *reinterpret_cast<const floatx4*>(&As[lpos<BK>(wm + mi * 16 + fr, fg, 4 * h)]);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+        fb[ni][h] = *reinterpret_cast<const floatx4*>(&Bs[lpos<BK>(wn + ni * 16 + fr, fg, 4 * h)]);
     }
+    if (do_cs) {
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int q = t + 256 * i;
-      if (!TB) {
-        const int k = q / (BN / 4), nc = (q % (BN / 4)) * 4;
-        *reinterpret_cast<floatx4*>(&Bs[k * LDB_S + nc]) =
-            floatx4{rb[i][0], rb[i][1], rb[i][2], rb[i][3]};
-      } else {
-        const int n = q / CPR, kc = (q % CPR) * 4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) Bs[(kc + j) * LDB_S + n] = rb[i][j];
-      }
+      for (int k = 0; k < BK; ++k) cs += Bs[t * Lay<BK>::S + k];
     }
   };
-  auto compute = [&](int stage) {
-    const float* As = lds + stage * STAGE;
-    const float* Bs = As + BK * LDA_S;
+  auto mfmas = [&]() {
+    // k = 4 kk + g: MFMA kk consumes k-slots 4kk..4kk+3 in order -> one
+    // k-ordered fma chain per output element
 #pragma unroll
-    for (int kk = 0; kk < BK / 4; ++kk) {
-      const int k = kk * 4 + (lane >> 4);
-      float a[MI], b[NI];
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) a[mi] = As[k * LDA_S + wm + mi * 16 + (lane & 15)];
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) b[ni] = Bs[k * LDB_S + wn + ni * 16 + (lane & 15)];
+    for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-    }
-    if (do_cs) {
-#pragma unroll
-      for (int k = 0; k < BK; ++k) cs += Bs[k * LDB_S + t];
-    }
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              fa[mi][kk >> 2][kk & 3], fb[ni][kk >> 2][kk & 3], acc[mi][ni], 0, 0, 0);
   };
 
-  // two-stage pipeline: tile it is multiplied from stage it&1 while tile it+1
-  // is written to the other stage and tile it+2's global loads are in flight;
-  // one barrier per k-tile.  The k order of every fma chain is unchanged.
+  // two LDS stages, PF register sets, one barrier per k-tile: after the
+  // barrier of iteration it the wave reads tile it's fragments (stage it&1),
+  // writes the register set holding tile it+1 (set it % PF) to the other
+  // stage (last read in iteration it-1, before this barrier), re-issues tile
+  // it+1+PF's loads into that set and then runs its MFMAs.  The k order of
+  // every fma chain is unchanged.
   const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
-  if (nk > 0) {
-    load_tiles(kbeg);
-    store_tiles(0);
-    if (nk > 1) load_tiles(kbeg + BK);
+  auto body = [&](int it, auto sc) {
+    constexpr int S = decltype(sc)::value;
     __syncthreads();
-    for (int it = 0; it < nk; ++it) {
-      const int cur = it & 1;
-      compute(cur);
-      if (it + 1 < nk) {
-        store_tiles(cur ^ 1);
-        if (it + 2 < nk) load_tiles(kbeg + (it + 2) * BK);
-      }
-      __syncthreads();
+    read_frags(it & 1);
+    if (it + 1 < nk) {
+      store_tiles((it + 1) & 1, ta[S], tb[S]);
+      if (it + 1 + PF < nk) load_tiles(kbeg + (it + 1 + PF) * BK, ta[S], tb[S]);
+    }
+    mfmas();
+  };
+  if (nk > 0) {
+    load_tiles(kbeg, ta[0], tb[0]);
+    store_tiles(0, ta[0], tb[0]);
+#pragma unroll
+    for (int j = 1; j <= PF; ++j)
+      if (j < nk) load_tiles(kbeg + j * BK, ta[j - 1], tb[j - 1]);
+    for (int it = 0; it < nk; it += PF) {
+      body(it, std::integral_constant<int, 0>{});
+      if constexpr (PF > 1)
+        if (it + 1 < nk) body(it + 1, std::integral_constant<int, 1>{});
     }
   }
   if (do_cs && n0 + t < N) atomicAdd(colsum + n0 + t, cs);
@@ -284,24 +353,28 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
       }
 }
 
-template <int BM, int BN, bool TA, bool TB>
+template <int BM, int BN, int BK, int PF, bool TA, bool TB, bool KS>
 void launch_epi(int epi, dim3 g, hipStream_t s, const GemmPtrs& P, const GemmDims& D) {
+#define MOG_GEMM_LAUNCH(E) gemm_f32_kernel<BM, BN, BK, PF, TA, TB, E, KS><<<g, 256, 0, s>>>(P, D)
+  if constexpr (KS) {  // K-segment form: only the plain and the accumulate epilogues
+    if (epi == EPI_ATOMIC) MOG_GEMM_LAUNCH(EPI_ATOMIC);
+    else MOG_GEMM_LAUNCH(EPI_STORE);
+    return;
+  } else {
   switch (epi) {
-    case EPI_STORE: gemm_f32_kernel<BM, BN, TA, TB, EPI_STORE><<<g, 256, 0, s>>>(P, D); break;
-    case EPI_RELU: gemm_f32_kernel<BM, BN, TA, TB, EPI_RELU><<<g, 256, 0, s>>>(P, D); break;
-    case EPI_SOFTPLUS:
-      gemm_f32_kernel<BM, BN, TA, TB, EPI_SOFTPLUS><<<g, 256, 0, s>>>(P, D); break;
-    case EPI_SIGMOID_NOISE:
-      gemm_f32_kernel<BM, BN, TA, TB, EPI_SIGMOID_NOISE><<<g, 256, 0, s>>>(P, D); break;
-    case EPI_SOFTPLUS_BWD:
-      gemm_f32_kernel<BM, BN, TA, TB, EPI_SOFTPLUS_BWD><<<g, 256, 0, s>>>(P, D); break;
-    case EPI_ATOMIC: gemm_f32_kernel<BM, BN, TA, TB, EPI_ATOMIC><<<g, 256, 0, s>>>(P, D); break;
-    case EPI_RELU_BWD:
-      gemm_f32_kernel<BM, BN, TA, TB, EPI_RELU_BWD><<<g, 256, 0, s>>>(P, D); break;
+    case EPI_STORE: MOG_GEMM_LAUNCH(EPI_STORE); break;
+    case EPI_RELU: MOG_GEMM_LAUNCH(EPI_RELU); break;
+    case EPI_SOFTPLUS: MOG_GEMM_LAUNCH(EPI_SOFTPLUS); break;
+    case EPI_SIGMOID_NOISE: MOG_GEMM_LAUNCH(EPI_SIGMOID_NOISE); break;
+    case EPI_SOFTPLUS_BWD: MOG_GEMM_LAUNCH(EPI_SOFTPLUS_BWD); break;
+    case EPI_ATOMIC: MOG_GEMM_LAUNCH(EPI_ATOMIC); break;
+    case EPI_RELU_BWD: MOG_GEMM_LAUNCH(EPI_RELU_BWD); break;
   }
+  }
+#undef MOG_GEMM_LAUNCH
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int BK, int PF>
 void launch_tile(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, GemmDims D,
                  int batch) {
   int kchunk = (D.K + D.splitk - 1) / D.splitk;
@@ -313,10 +386,31 @@ void launch_tile(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, Ge
   D.nx = mog_cdiv(D.N, BN);
   D.ny = mog_cdiv(D.M, BM);
   dim3 g(D.nx, D.ny, batch * D.splitk);
-  if (!ta && !tb) launch_epi<BM, BN, false, false>(epi, g, s, P, D);
-  else if (!ta && tb) launch_epi<BM, BN, false, true>(epi, g, s, P, D);
-  else if (ta && !tb) launch_epi<BM, BN, true, false>(epi, g, s, P, D);
-  else launch_epi<BM, BN, true, true>(epi, g, s, P, D);
+  if (D.kseg > 0) {  // heads' dh = sum_z dhid_z W1_z^T (NT form only)
+    if (!ta && tb) launch_epi<BM, BN, BK, PF, false, true, true>(epi, g, s, P, D);
+    else launch_epi<BM, BN, BK, PF, false, false, true>(epi, g, s, P, D);
+    return;
+  }
+  if (!ta && !tb) launch_epi<BM, BN, BK, PF, false, false, false>(epi, g, s, P, D);
+  else if (!ta && tb) launch_epi<BM, BN, BK, PF, false, true, false>(epi, g, s, P, D);
+  else if (ta && !tb) launch_epi<BM, BN, BK, PF, true, false, false>(epi, g, s, P, D);
+  else launch_epi<BM, BN, BK, PF, true, true, false>(epi, g, s, P, D);
+}
+
+// Tile shape (measured on MI355X, scripts/bench_gemm_f32.py):
+// 64x64 (2x2 waves of 32x32) wins on every train-step shape except the long-K
+// x-projection (K = 2500), where 128x128 keeps more MFMAs per barrier and
+// still gives every CU two workgroups.  Measured and not kept: BK = 32 (-5..-25 %
+// on every shape), a second register prefetch set (PF = 2: within +-2 %),
+// 128x64 / 64x128 tiles.  MOG_GEMM_TILE ("64" / "128") forces a tile.
+void launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, const GemmDims& D,
+                 int batch) {
+  static const char* force = getenv("MOG_GEMM_TILE");
+  const long big = (long)mog_cdiv(D.M, 128) * mog_cdiv(D.N, 128) * batch * D.splitk;
+  bool b128 = !ta && D.K >= 2048 && D.M >= 128 && D.N >= 128 && big >= 512;
+  if (force != nullptr) b128 = atoi(force) == 128;
+  if (b128) launch_tile<128, 128, 16, 1>(ta, tb, epi, s, P, D, batch);
+  else launch_tile<64, 64, 16, 1>(ta, tb, epi, s, P, D, batch);
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -356,6 +450,10 @@ extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const
         MOG_CHECK_ARG(P.aux[i] != nullptr);
     }
   }
+  // operands are addressed through raw buffer descriptors (32-bit byte offsets)
+  const long extA = transA ? (long)(K - 1) * lda + M : (long)(M - 1) * lda + K;
+  const long extB = transB ? (long)(N - 1) * ldb + K : (long)(K - 1) * ldb + N;
+  MOG_CHECK_ARG(extA * 4 < 0x7ffffff0L && extB * 4 < 0x7ffffff0L);
   GemmDims D;
   D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc; D.ldaux = ldaux;
   D.aux_scale = aux_scale;
@@ -364,16 +462,7 @@ extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const
   D.splitk = splitk;
   D.kchunk = 0;
   D.kseg = 0;
-  hipStream_t s = mog_stream(stream);
-  // 128x128 tiles once both output dims fill them and the grid still covers
-  // the chip (>= 512 workgroups); 64x64 otherwise.
-  // (measured: 128x128 is on par for the large NN GEMMs and slower for the
-  // split-K weight-gradient form, so the transposed-A form stays on 64x64)
-  const long big_tiles = (long)mog_cdiv(M, 128) * mog_cdiv(N, 128) * batch * splitk;
-  if (!transA && M >= 128 && N >= 128 && big_tiles >= 512)
-    launch_tile<128, 128>(transA, transB, epi, s, P, D, batch);
-  else
-    launch_tile<64, 64>(transA, transB, epi, s, P, D, batch);
+  launch_auto(transA, transB, epi, mog_stream(stream), P, D, batch);
   MOG_LAUNCH_RET();
 }
 
@@ -385,9 +474,10 @@ extern "C" int mog_gemm_f32_kseg(int nseg, const float* const* A, const float* c
                                  float* C, const float* bias, const float* Cin, int M, int N,
                                  int kseg, int lda, int ldb, int ldc, int transA, int transB,
                                  int epi, void* stream) {
-  MOG_CHECK_ARG(nseg >= 1 && nseg <= MAXB && kseg > 0 && kseg % BK == 0);
+  MOG_CHECK_ARG(nseg >= 1 && nseg <= MAXB && kseg > 0 && kseg % 16 == 0);
   MOG_CHECK_ARG(M >= 0 && N >= 0 && A && B && C);
   MOG_CHECK_ARG(epi == EPI_STORE || epi == EPI_ATOMIC);
+  MOG_CHECK_ARG(!transA);
   if (M == 0 || N == 0) return 0;
   GemmPtrs P = {};
   bool va = true, vb = true;
@@ -409,6 +499,6 @@ extern "C" int mog_gemm_f32_kseg(int nseg, const float* const* A, const float* c
   D.splitk = 1;
   D.kchunk = 0;
   D.kseg = kseg;
-  launch_tile<64, 64>(transA, transB, epi, mog_stream(stream), P, D, 1);
+  launch_auto(transA, transB, epi, mog_stream(stream), P, D, 1);
   MOG_LAUNCH_RET();
 }
