@@ -79,7 +79,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 //   sample: kl [M][50] fp32 at 0, z [M][SZ] bf16 behind it, d1 [M][S256] at A2
 //   then:   d2 [M][S512] at 0 (in place over d1)
 //   write:  one slot per wave at wv * WSLOT: r [784] fp32, write tables [2C] float4
-template <int MT>
+template <int MT, int NW>
 struct Lay {
   static constexpr int M = 16 * MT;
   static constexpr int A1 = M * S512 * 2;
@@ -92,7 +92,7 @@ struct Lay {
   // STN write: one slot per wave (r of one image + its 2C write tables)
   static constexpr int WSLOT = W2 * 4 + 2 * CTAB_MAX * 16;
   static constexpr int ARENA0 =
-      cmax(cmax(A1, TAB + 3 * KB), cmax(OFF_D1 + A2, cmax(OFF_LV + M * 50 * 4, 16 * WSLOT)));
+      cmax(cmax(A1, TAB + 3 * KB), cmax(OFF_D1 + A2, cmax(OFF_LV + M * 50 * 4, NW * WSLOT)));
   static constexpr int OFF_EZ = ARENA0;        // eps_z [M][50] fp32, staged in the prologue
   static constexpr int ARENA = ARENA0 + M * 50 * 4;
   static_assert(OFF_Z + M * SZ * 2 <= A2, "kl / z behind a2");
@@ -407,7 +407,7 @@ __device__ __forceinline__ void read_recognition(const StepArgs& p, unsigned cha
                                                  floatx4 (&acc)[MT][64 / NW], int (&ct)[64 / NW],
                                                  floatx4 (&b1q)[64 / NW]) {
 #pragma clang fp contract(off)
-  using Ly = Lay<MT>;
+  using Ly = Lay<MT, NW>;
   constexpr int M = Ly::M;
   constexpr int NTHR = NW * 64;
   constexpr int TW = 64 / NW;          // recognition column tiles per MFMA wave (32 over NW/2)
@@ -574,7 +574,7 @@ __device__ __forceinline__ void read_recognition(const StepArgs& p, unsigned cha
 template <int MT, int NW, int OCC>
 __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) {
 #pragma clang fp contract(off)
-  using Ly = Lay<MT>;
+  using Ly = Lay<MT, NW>;
   constexpr int M = Ly::M;
   constexpr int NTHR = NW * 64;
   constexpr int TW = 64 / NW;  // recognition column tiles per MFMA wave

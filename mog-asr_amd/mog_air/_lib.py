@@ -99,3 +99,51 @@ def call(name: str, *args) -> None:
 
 def ptr_array(ptrs) -> ctypes.Array:
     return (ctypes.c_void_p * len(ptrs))(*ptrs)
+
+
+# ---- PyTorch custom operators (csrc/torch_ops.cpp) --------------------------
+TORCH_OPS_PATH = os.path.join(_HERE, "_lib", "libmog_air_torch.so")
+_torch_ops_loaded = False
+
+
+def build_torch_ops(verbose: bool = False) -> str:
+    """Compile csrc/torch_ops.cpp (TORCH_LIBRARY_FRAGMENT(mog_air) over the C
+    ABI) against this torch and libmog_air.so into mog_air/_lib/
+    libmog_air_torch.so (in-tree, so it travels with the tree)."""
+    import shutil
+
+    import torch
+    from torch.utils import cpp_extension
+    load()  # libmog_air.so mapped first (the extension links it by soname)
+    pkg = os.path.normpath(os.path.join(_HERE, ".."))
+    bdir = os.path.join(pkg, "build", "torch_ops")
+    os.makedirs(bdir, exist_ok=True)
+    cpp_extension.load(
+        name="libmog_air_torch", sources=[os.path.join(pkg, "csrc", "torch_ops.cpp")],
+        extra_include_paths=[os.path.dirname(HEADER_PATH), "/opt/rocm/include"],
+        extra_cflags=["-O2", "-D__HIP_PLATFORM_AMD__"],
+        # libmog_air.so: resolved by its soname once load() has mapped it
+        # (runpath kept as a fallback); c10_hip for the current-stream query
+        extra_ldflags=["-L" + os.path.dirname(LIB_PATH), "-lmog_air",
+                       "-L" + os.path.join(os.path.dirname(torch.__file__), "lib"), "-lc10_hip",
+                       "-Wl,-rpath," + os.path.dirname(LIB_PATH)],
+        build_directory=bdir, is_python_module=False, verbose=verbose)
+    # cpp_extension.load registered the ops from the build copy already
+    global _torch_ops_loaded
+    _torch_ops_loaded = True
+    shutil.copy2(os.path.join(bdir, "libmog_air_torch.so"), TORCH_OPS_PATH)
+    return TORCH_OPS_PATH
+
+
+def load_torch_ops() -> None:
+    """Register torch.ops.mog_air.* (fails loudly when the extension is
+    missing: there is no fallback path)."""
+    global _torch_ops_loaded
+    if _torch_ops_loaded:
+        return
+    load()
+    if not os.path.exists(TORCH_OPS_PATH):
+        raise MogError(f"{TORCH_OPS_PATH} not built (run __graft_entry__.build())")
+    import torch
+    torch.ops.load_library(TORCH_OPS_PATH)
+    _torch_ops_loaded = True

@@ -20,7 +20,6 @@ No host synchronisation happens inside a train step.
 """
 from __future__ import annotations
 
-import ctypes
 import math
 import os
 from typing import Dict, Optional
@@ -33,6 +32,8 @@ from . import ops
 from .ops import (EPI_ATOMIC, EPI_RELU, EPI_SIGMOID_NOISE, EPI_SOFTPLUS, EPI_SOFTPLUS_BWD,
                   EPI_STORE, dp, gemm, stream_ptr)
 from .params import ParamStore, param_specs
+
+_ops = ops._ops  # torch.ops.mog_air (csrc/torch_ops.cpp)
 
 # step-record slots (air_cell.hip enum)
 R_SM, R_SLV, R_HM0, R_HM1, R_HLV0, R_HLV1, R_LO, R_S, R_TX, R_TY, R_Y, R_Z = range(12)
@@ -217,7 +218,7 @@ class AIRModel:
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         if self.device.type != "cuda":
             raise RuntimeError("AIRModel runs on a HIP device only (no CPU fallback)")
-        _lib.load()
+        _lib.load_torch_ops()
         self.input_images = input_images
         self.target_num_digits = target_num_digits
         self.max_steps, self.max_digits = int(max_steps), max_digits
@@ -390,7 +391,6 @@ class AIRModel:
         R1, R2 = self.vae_recognition_units
         G1, G2 = self.vae_generative_units
         HS = self.scale_hidden_units
-        s = stream_ptr()
         K = self._P("rnn/basic_lstm_cell/kernel")
         bK = self._P("rnn/basic_lstm_cell/bias")
         Wx, Wh = K[:C2], K[C2:]
@@ -414,32 +414,25 @@ class AIRModel:
         b2 = [self._P(h + "/output/biases") for h in self._HEADS]
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
         vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
-        w2a = _lib.ptr_array([dp(x) for x in w2])
-        b2a = _lib.ptr_array([dp(x) for x in b2])
         for t in range(T):
             if t == 0:
-                _lib.call("mog_lstm_cell_forward", dp(ws.Gx), dp(bK), None, dp(ws.c[0]),
-                          dp(ws.h[0]), B, H, s)
+                _ops.lstm_cell_forward_(ws.Gx, bK, None, ws.c[0], ws.h[0], B, H)
             else:
                 gemm([ws.h[t - 1]], [Wh], [ws.G[t]], B, 4 * H, H, H, 4 * H, 4 * H, bias=[bK],
                      Cin=[ws.Gx])
-                _lib.call("mog_lstm_cell_forward", dp(ws.G[t]), None, dp(ws.c[t - 1]),
-                          dp(ws.c[t]), dp(ws.h[t]), B, H, s)
+                _ops.lstm_cell_forward_(ws.G[t], None, ws.c[t - 1], ws.c[t], ws.h[t], B, H)
             hid_t = [ws.hid[z, t] for z in range(5)]
             gemm([ws.h[t]] * 5, w1, hid_t, B, HS, H, H, HS, HS, epi=EPI_RELU, bias=b1)
             bias_t = float(self.marginal[t]) if self.marginal is not None else 0.0
             rec = ws.rec[t]
-            _lib.call("mog_air_step_forward", B, HS, HS, t, int(self.train),
-                      int(self.marginal is not None), thr, temperature, prior_lo, bias_t,
-                      float(self.scale_prior_mean), float(self.scale_prior_variance),
-                      self.scale_prior_log_variance, float(self.shift_prior_mean),
-                      float(self.shift_prior_variance), self.shift_prior_log_variance,
-                      _lib.ptr_array([dp(x) for x in hid_t]), w2a, b2a, dp(ws.eps_scale[t]),
-                      dp(ws.eps_shift[t]), dp(ws.u[t]), dp(ws.stop), dp(ws.runloss),
-                      dp(ws.digits), dp(ws.live), dp(rec), dp(ws.th_f[t]), dp(ws.th_b[t]),
-                      dp(ws.scale[t]), dp(ws.shift[t]), dp(ws.zprob[t]), dp(ws.zkl[t]),
-                      dp(ws.skl[t]), dp(ws.shkl[t]), dp(ws.zmask[t]), dp(ws.zval[t]),
-                      dp(ws.zc[t]), s)
+            _ops.air_step_forward_(
+                B, HS, HS, t, self.train, self.marginal is not None, thr, temperature, prior_lo,
+                bias_t, float(self.scale_prior_mean), float(self.scale_prior_variance),
+                self.scale_prior_log_variance, float(self.shift_prior_mean),
+                float(self.shift_prior_variance), self.shift_prior_log_variance, hid_t, w2, b2,
+                ws.eps_scale[t], ws.eps_shift[t], ws.u[t], ws.stop, ws.runloss, ws.digits,
+                ws.live, rec, ws.th_f[t], ws.th_b[t], ws.scale[t], ws.shift[t], ws.zprob[t],
+                ws.zkl[t], ws.skl[t], ws.shkl[t], ws.zmask[t], ws.zval[t], ws.zc[t])
             if self.live_hook is not None:
                 self.live_hook(ws.live, t)
             if self.fused_step:
@@ -461,21 +454,19 @@ class AIRModel:
         outputs=False (train steps) the clipped reconstruction and, in the
         fused configuration, the summed canvas are not stored; the
         ``reconstruction`` / ``canvas`` accessors materialize them on demand."""
-        B, C2, s = ws.B, self.C2, stream_ptr()
+        B, C2 = ws.B, self.C2
         parts = ws.cparts
         self._loss_inputs = (X, targets)
         ws.materialized = bool(outputs)
         gscale = self._gscale(B)
-        canvas_ptr = dp(ws.canvas) if (outputs or parts is None) else None
-        _lib.call("mog_recon_loss", dp(X), canvas_ptr, dp(parts),
-                  self.max_steps if parts is not None else 0, B * C2, dp(ws.prows),
-                  self.canvas_size, dp(ws.runloss),
-                  dp(ws.digits), dp(targets), B, C2, float(gscale),
-                  dp(ws.recon) if outputs else None, dp(ws.bce), dp(ws.mse),
-                  dp(ws.loss_b), dp(ws.acc_b) if targets is not None else None,
-                  dp(ws.dcanvas) if need_grad else None, s)
-        _lib.call("mog_batch_mean", dp(ws.loss_b), dp(ws.acc_b) if targets is not None else None,
-                  dp(ws.mse), None, B, dp(ws.means), s)
+        canvas = ws.canvas if (outputs or parts is None) else None
+        _ops.recon_loss_(X, canvas, parts, self.max_steps if parts is not None else 0, B * C2,
+                         ws.prows, self.canvas_size, ws.runloss, ws.digits, targets, B, C2,
+                         float(gscale), ws.recon if outputs else None, ws.bce, ws.mse, ws.loss_b,
+                         ws.acc_b if targets is not None else None,
+                         ws.dcanvas if need_grad else None)
+        _ops.batch_mean_(ws.loss_b, ws.acc_b if targets is not None else None, ws.mse, None, B,
+                         ws.means)
         self._outputs_ready = True
 
     def _materialize(self):
@@ -496,7 +487,6 @@ class AIRModel:
         C, W, C2 = self.canvas_size, self.windows_size, self.C2
         HS = self.scale_hidden_units
         TB = T * B
-        s = stream_ptr()
         st = self.params
         st.grad.zero_()
         K = self._P("rnn/basic_lstm_cell/kernel")
@@ -504,7 +494,6 @@ class AIRModel:
         Wh = K[C2:]
         w1 = [self._P(h + "/hidden/weights") for h in self._HEADS]
         w2 = [self._P(h + "/output/weights") for h in self._HEADS]
-        w2a = _lib.ptr_array([dp(x) for x in w2])
         gscale = self._gscale(B)
         prior_lo = self.hyper("z_pres_prior_log_odds")
         temperature = self.hyper("z_pres_temperature")
@@ -527,19 +516,16 @@ class AIRModel:
                          n=TB)
         for t in range(T):
             hid_t = [ws.hid[z, t] for z in range(5)]
-            _lib.call("mog_air_step_backward", B, HS, int(self.train),
-                      int(self.marginal is not None), temperature, prior_lo,
-                      float(self.marginal[t]) if self.marginal is not None else 0.0,
-                      float(self.scale_prior_mean), float(self.scale_prior_variance),
-                      float(self.shift_prior_mean), float(self.shift_prior_variance),
-                      float(gscale), dp(ws.rec[t]), dp(ws.eps_scale[t]), dp(ws.eps_shift[t]),
-                      dp(ws.dth_f_all[t]), dp(ws.dth_b_all[t]), dp(ws.dot_all[t]),
-                      _lib.ptr_array([dp(x) for x in hid_t]), w2a, dp(ws.dout[0, t]),
-                      T * B * 2, dp(ws.dhid[0, t]), T * B * HS, s)
+            _ops.air_step_backward_(
+                B, HS, self.train, self.marginal is not None, temperature, prior_lo,
+                float(self.marginal[t]) if self.marginal is not None else 0.0,
+                float(self.scale_prior_mean), float(self.scale_prior_variance),
+                float(self.shift_prior_mean), float(self.shift_prior_variance), float(gscale),
+                ws.rec[t], ws.eps_scale[t], ws.eps_shift[t], ws.dth_f_all[t], ws.dth_b_all[t],
+                ws.dot_all[t], hid_t, w2, ws.dout[0, t], T * B * 2, ws.dhid[0, t], T * B * HS)
         # dh[t] = sum_z dhid_z W1_z^T for every step: one chain over K = 5 * HS
-        _lib.call("mog_gemm_f32_kseg", 5, _lib.ptr_array([dp(ws.dhid[z]) for z in range(5)]),
-                  _lib.ptr_array([dp(x) for x in w1]), dp(ws.dh), None, None, TB, H, HS, HS, HS,
-                  H, 0, 1, 0, s)
+        ops.gemm_kseg([ws.dhid[z] for z in range(5)], w1, ws.dh, TB, H, HS, HS, HS, H,
+                      transB=True)
         # the heads' and the VAE's weight gradients are final here: their
         # all-reduce bucket runs while the LSTM chain below computes
         self._weight_grads_glimpse(ws)
@@ -548,10 +534,9 @@ class AIRModel:
         ws.dGsum.zero_()
         for t in reversed(range(T)):
             dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
-            _lib.call("mog_lstm_cell_backward", dp(ws.Gx if t == 0 else ws.G[t]),
-                      dp(bK) if t == 0 else None, dp(ws.c[t - 1]) if t > 0 else None,
-                      dp(ws.c[t]), dp(ws.dh[t]), dp(dc_in), dp(ws.dG[t]), dp(ws.dc[t % 2]),
-                      dp(ws.dGsum), B, H, s)
+            _ops.lstm_cell_backward_(ws.Gx if t == 0 else ws.G[t], bK if t == 0 else None,
+                                     ws.c[t - 1] if t > 0 else None, ws.c[t], ws.dh[t], dc_in,
+                                     ws.dG[t], ws.dc[t % 2], ws.dGsum, B, H)
             if t > 0:
                 gemm([ws.dG[t]], [Wh], [ws.dh[t - 1]], B, H, 4 * H, 4 * H, 4 * H, H,
                      transB=True, Cin=[ws.dh[t - 1]])
@@ -561,17 +546,15 @@ class AIRModel:
         TB = ws.B * self.max_steps
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
-        s = stream_ptr()
-        _lib.call("mog_sigmoid_backward", dp(ws.r), dp(ws.dr_all), dp(ws.dm), TB * W2, 0, s)
+        _ops.sigmoid_backward_(ws.r, ws.dr_all, ws.dm, TB * W2)
         gemm([ws.dm], [vw["gen_mean"]], [ws.dd2], TB, G2, W2, W2, W2, G2,
              transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d2pre], ldaux=G2)
         gemm([ws.dd2], [vw["generative_2"]], [ws.dd1], TB, G1, G2, G2, G2, G1,
              transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d1pre], ldaux=G1)
         gemm([ws.dd1], [vw["generative_1"]], [ws.dz_all], TB, Z, G1, G1, G1, Z, transB=True)
-        _lib.call("mog_vae_sample_backward", TB, Z, float(self.vae_prior_mean),
-                  float(self.vae_prior_variance), float(gscale), dp(ws.mu), dp(ws.lv),
-                  dp(ws.eps_z), dp(ws.dz_all), dp(ws.zmask), dp(ws.dmu), dp(ws.dlv), None, None,
-                  0, s)
+        _ops.vae_sample_backward_(TB, Z, float(self.vae_prior_mean),
+                                  float(self.vae_prior_variance), float(gscale), ws.mu, ws.lv,
+                                  ws.eps_z, ws.dz_all, ws.zmask, ws.dmu, ws.dlv, None, None, 0)
         gemm([ws.dmu], [vw["rec_mean"]], [ws.tmp_a2_all], TB, R2, Z, Z, Z, R2, transB=True)
         gemm([ws.dlv], [vw["rec_log_variance"]], [ws.da2], TB, R2, Z, Z, Z, R2,
              transB=True, epi=EPI_SOFTPLUS_BWD, Cin=[ws.tmp_a2_all], aux=[ws.a2pre], ldaux=R2)
@@ -585,7 +568,6 @@ class AIRModel:
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         Zp = self._pad8(Z)
         wn = self._wn
-        s = stream_ptr()
         # dmb = bf16(SigmoidGrad(r, dr)) was written by the STN write backward
         gemm_bf16([ws.dmb], [wn["gen_mean"]], [ws.dd2b], TB, G2, W2, W2, W2, G2,
                   epi=BF_SOFTPLUS_BWD, aux=[ws.d2b], ldaux=G2)
@@ -593,10 +575,9 @@ class AIRModel:
                   epi=BF_SOFTPLUS_BWD, aux=[ws.d1b], ldaux=G1)
         gemm_bf16([ws.dd1b], [wn["generative_1"]], [ws.dz_all], TB, Z, G1, G1, G1, Z,
                   epi=BF_STORE)
-        _lib.call("mog_vae_sample_backward", TB, Z, float(self.vae_prior_mean),
-                  float(self.vae_prior_variance), float(gscale), dp(ws.mu), dp(ws.lv),
-                  dp(ws.eps_z), dp(ws.dz_all), dp(ws.zmask), None, None, dp(ws.dmub),
-                  dp(ws.dlvb), Zp, s)
+        _ops.vae_sample_backward_(TB, Z, float(self.vae_prior_mean),
+                                  float(self.vae_prior_variance), float(gscale), ws.mu, ws.lv,
+                                  ws.eps_z, ws.dz_all, ws.zmask, None, None, ws.dmub, ws.dlvb, Zp)
         gemm_bf16([ws.dmub], [wn["rec_mean"]], [ws.tmp_a2_all], TB, R2, Zp, Zp, Zp, R2,
                   epi=BF_STORE)
         gemm_bf16([ws.dlvb], [wn["rec_log_variance"]], [ws.da2b], TB, R2, Zp, Zp, Zp, R2,
@@ -635,11 +616,10 @@ class AIRModel:
              aux=[ws.eps_x[t]], ldaux=W2, aux_scale=lik_std)
 
     def _vae_sample_fwd(self, ws, t, zb, ldzb):
-        _lib.call("mog_vae_sample_forward", ws.B, self.vae_latent_dimensions,
-                  float(self.vae_prior_mean), float(self.vae_prior_variance),
-                  self.vae_prior_log_variance, dp(ws.mu[t]), dp(ws.lv[t]), dp(ws.eps_z[t]),
-                  dp(ws.z[t]), dp(zb), ldzb, dp(ws.zmask[t]), dp(ws.runloss), dp(ws.vkl[t]),
-                  stream_ptr())
+        _ops.vae_sample_forward_(ws.B, self.vae_latent_dimensions, float(self.vae_prior_mean),
+                                 float(self.vae_prior_variance), self.vae_prior_log_variance,
+                                 ws.mu[t], ws.lv[t], ws.eps_z[t], ws.z[t], zb, ldzb,
+                                 ws.zmask[t], ws.runloss, ws.vkl[t])
 
     def _dz_hook(self, ws, t):
         """Extra gradient reaching the latent z of step t before the sample
@@ -650,18 +630,17 @@ class AIRModel:
         B = ws.B
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
-        s = stream_ptr()
-        _lib.call("mog_sigmoid_backward", dp(ws.r[t]), dp(ws.dr), dp(ws.dm[t]), B * W2, 0, s)
+        _ops.sigmoid_backward_(ws.r[t], ws.dr, ws.dm[t], B * W2)
         gemm([ws.dm[t]], [vw["gen_mean"]], [ws.dd2[t]], B, G2, W2, W2, W2, G2,
              transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d2pre[t]], ldaux=G2)
         gemm([ws.dd2[t]], [vw["generative_2"]], [ws.dd1[t]], B, G1, G2, G2, G2, G1,
              transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d1pre[t]], ldaux=G1)
         gemm([ws.dd1[t]], [vw["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z, transB=True)
         self._dz_hook(ws, t)
-        _lib.call("mog_vae_sample_backward", B, Z, float(self.vae_prior_mean),
-                  float(self.vae_prior_variance), float(gscale), dp(ws.mu[t]), dp(ws.lv[t]),
-                  dp(ws.eps_z[t]), dp(ws.dz), dp(ws.zmask[t]), dp(ws.dmu[t]), dp(ws.dlv[t]),
-                  None, None, 0, s)
+        _ops.vae_sample_backward_(B, Z, float(self.vae_prior_mean),
+                                  float(self.vae_prior_variance), float(gscale), ws.mu[t],
+                                  ws.lv[t], ws.eps_z[t], ws.dz, ws.zmask[t], ws.dmu[t], ws.dlv[t],
+                                  None, None, 0)
         gemm([ws.dmu[t]], [vw["rec_mean"]], [ws.tmp_a2], B, R2, Z, Z, Z, R2, transB=True)
         gemm([ws.dlv[t]], [vw["rec_log_variance"]], [ws.da2[t]], B, R2, Z, Z, Z, R2,
              transB=True, epi=EPI_SOFTPLUS_BWD, Cin=[ws.tmp_a2], aux=[ws.a2pre[t]], ldaux=R2)
@@ -698,12 +677,11 @@ class AIRModel:
                 else:
                     wt = self._wt[n] = torch.zeros((O, self._pad8(I)), **bf)
                     fwd, fdims = wt, [I, O, O, O, wt.shape[1], wt.shape[1], 1]
-                srcs += [dp(w), dp(w)]
-                dsts += [dp(fwd), dp(wn)]
+                srcs += [w, w]
+                dsts += [fwd, wn]
                 dims += fdims + [I, O, O, I, wn.shape[1], wn.shape[1], 0]
-            self._pack_args = (len(srcs), _lib.ptr_array(srcs), _lib.ptr_array(dsts),
-                               (ctypes.c_int * len(dims))(*dims))
-        _lib.call("mog_cvt_bf16_batch", *self._pack_args, stream_ptr())
+            self._pack_args = (srcs, dsts, dims)
+        _ops.cvt_bf16_batch_(*self._pack_args)
         self._pack_version = self.params.version
 
     def _vae_forward_bf16(self, X, ws, t, lik_std):
@@ -736,20 +714,19 @@ class AIRModel:
         (vae_step.hip; same arithmetic as the unfused bf16 sequence)."""
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         self._pack_bf16()
-        wt = _lib.ptr_array([dp(self._wf[n]) for n in self._VAE])
+        if self.windows_size != 28 or (R1, R2, Z, G1, G2) != (512, 256, 50, 256, 512):
+            raise ValueError("the fused step kernel is compiled for the reference VAE shape")
+        wt = [self._wf[n] for n in self._VAE]
         gen = getattr(ws, "eps_x_offset", None) is not None
         off = ws.eps_x_offset + t * ws.B * (W2 // 4) if gen else 0
-        bias = _lib.ptr_array([dp(self._P("vae/" + n + "/biases")) for n in self._VAE])
-        _lib.call("mog_stn_vae_step_forward", ws.B, self.canvas_size, self.windows_size, R1, R2,
-                  Z, G1, G2, dp(X), dp(ws.th_f[t]), dp(ws.th_b[t]), dp(ws.zmask[t]),
-                  dp(ws.zval[t]), dp(ws.eps_z[t]), dp(ws.eps_x[t]), int(gen),
-                  self.noise_seed & (2 ** 64 - 1), off & (2 ** 64 - 1), wt, bias, lik_std,
-                  float(self.vae_prior_mean), float(self.vae_prior_variance),
-                  self.vae_prior_log_variance, dp(ws.cparts[t]), dp(ws.prows[t]),
-                  dp(ws.runloss), dp(ws.vkl[t]),
-                  dp(ws.gb[t]), dp(ws.a1b[t]), dp(ws.a2b[t]), dp(ws.mu[t]), dp(ws.lv[t]),
-                  dp(ws.z[t]), dp(ws.zb[t]), dp(ws.d1b[t]), dp(ws.d2b[t]), dp(ws.r[t]),
-                  stream_ptr())
+        bias = [self._P("vae/" + n + "/biases") for n in self._VAE]
+        _ops.stn_vae_step_(ws.B, self.canvas_size, X, ws.th_f[t], ws.th_b[t], ws.zmask[t],
+                           ws.zval[t], ws.eps_z[t], ws.eps_x[t], ops._i64(self.noise_seed),
+                           ops._i64(off), gen, wt, bias, lik_std, float(self.vae_prior_mean),
+                           float(self.vae_prior_variance), self.vae_prior_log_variance,
+                           ws.cparts[t], ws.prows[t], ws.runloss, ws.vkl[t], ws.gb[t],
+                           ws.a1b[t], ws.a2b[t], ws.mu[t], ws.lv[t], ws.z[t], ws.zb[t],
+                           ws.d1b[t], ws.d2b[t], ws.r[t])
 
     def _vae_backward_bf16(self, ws, t, gscale):
         from .ops import BF_SOFTPLUS_BWD, BF_STORE, gemm_bf16
@@ -757,8 +734,7 @@ class AIRModel:
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         Zp = self._pad8(Z)
         wn = self._wn
-        s = stream_ptr()
-        _lib.call("mog_sigmoid_backward", dp(ws.r[t]), dp(ws.dr), dp(ws.dmb[t]), B * W2, 1, s)
+        _ops.sigmoid_backward_(ws.r[t], ws.dr, ws.dmb[t], B * W2)
         gemm_bf16([ws.dmb[t]], [wn["gen_mean"]], [ws.dd2b[t]], B, G2, W2, W2, W2, G2,
                   epi=BF_SOFTPLUS_BWD, aux=[ws.d2b[t]], ldaux=G2)
         gemm_bf16([ws.dd2b[t]], [wn["generative_2"]], [ws.dd1b[t]], B, G1, G2, G2, G2, G1,
@@ -766,10 +742,10 @@ class AIRModel:
         gemm_bf16([ws.dd1b[t]], [wn["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z,
                   epi=BF_STORE)
         self._dz_hook(ws, t)
-        _lib.call("mog_vae_sample_backward", B, Z, float(self.vae_prior_mean),
-                  float(self.vae_prior_variance), float(gscale), dp(ws.mu[t]), dp(ws.lv[t]),
-                  dp(ws.eps_z[t]), dp(ws.dz), dp(ws.zmask[t]), None, None, dp(ws.dmub[t]),
-                  dp(ws.dlvb[t]), Zp, s)
+        _ops.vae_sample_backward_(B, Z, float(self.vae_prior_mean),
+                                  float(self.vae_prior_variance), float(gscale), ws.mu[t],
+                                  ws.lv[t], ws.eps_z[t], ws.dz, ws.zmask[t], None, None,
+                                  ws.dmub[t], ws.dlvb[t], Zp)
         gemm_bf16([ws.dmub[t]], [wn["rec_mean"]], [ws.tmp_a2], B, R2, Zp, Zp, Zp, R2,
                   epi=BF_STORE)
         gemm_bf16([ws.dlvb[t]], [wn["rec_log_variance"]], [ws.da2b[t]], B, R2, Zp, Zp, Zp, R2,
@@ -891,11 +867,8 @@ class AIRModel:
                 bf = dict(device=self.device, dtype=torch.bfloat16)
                 ws.Xb = torch.zeros((B, C2p), **bf)
                 ws.dGsumb = torch.empty((B, 4 * H), **bf)
-            srcs = _lib.ptr_array([dp(X), dp(ws.dGsum)])
-            dsts = _lib.ptr_array([dp(ws.Xb), dp(ws.dGsumb)])
-            dims = (ctypes.c_int * 14)(B, C2, C2, B, C2p, C2p, 0, B, 4 * H, 4 * H, B, 4 * H,
-                                       4 * H, 0)
-            _lib.call("mog_cvt_bf16_batch", 2, srcs, dsts, dims, stream_ptr())
+            _ops.cvt_bf16_batch_([X, ws.dGsum], [ws.Xb, ws.dGsumb],
+                                 [B, C2, C2, B, C2p, C2p, 0, B, 4 * H, 4 * H, B, 4 * H, 4 * H, 0])
         self._dw_bf16(ws.Xb[:, m0:], ws.dGsumb, gK[m0:m1], B, m1 - m0, 4 * H, C2p, 4 * H,
                       bias_out)
 

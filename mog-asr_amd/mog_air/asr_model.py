@@ -31,6 +31,8 @@ from . import _lib, ops
 from .air_model import AIRModel as _AirBase
 from .air_model import _SCOPES, _Workspace, _f32log, annealed_value
 from .ops import EPI_RELU, EPI_STORE, dp, gemm, stream_ptr
+
+_ops = ops._ops  # torch.ops.mog_air (csrc/torch_ops.cpp)
 from .params import ParamStore
 
 # asr_cell.hip record slots
@@ -305,11 +307,11 @@ class AIRModel(_AirBase):
             KU = Z + 3 + H
             gemm([ws.U[t]], [Ki[C2:]], [ws.G[t]], B, 4 * H, KU, LU, 4 * H, 4 * H, bias=[bi],
                  Cin=[ws.Gx])
-            _lib.call("mog_lstm_cell_forward", dp(ws.G[t]), None,
-                      dp(ws.c[t - 1]) if prev else None, dp(ws.c[t]), dp(ws.h[t]), B, H, s)
+            _ops.lstm_cell_forward_(ws.G[t], None, ws.c[t - 1] if prev else None, ws.c[t],
+                                    ws.h[t], B, H)
             gemm([ws.Ug[t]], [Kg], [ws.Gg[t]], B, 4 * H, KU, LU, 4 * H, 4 * H, bias=[bg])
-            _lib.call("mog_lstm_cell_forward", dp(ws.Gg[t]), None,
-                      dp(ws.cg[t - 1]) if prev else None, dp(ws.cg[t]), dp(ws.hg[t]), B, H, s)
+            _ops.lstm_cell_forward_(ws.Gg[t], None, ws.cg[t - 1] if prev else None, ws.cg[t],
+                                    ws.hg[t], B, H)
             hid = [ws.hid8[k, t] for k in range(8)]
             gemm([ws.h[t]] * 3, relu_w, hid[0:3], B, 64, H, H, 64, 64, epi=EPI_RELU, bias=relu_b)
             gemm([ws.hg[t]] * 2, gen_w, hid[3:5], B, 64, H, H, 64, 64, epi=EPI_RELU, bias=gen_b)
@@ -354,18 +356,18 @@ class AIRModel(_AirBase):
         self._loss_inputs = (X, targets)
         ws.materialized = bool(outputs)
         gscale = self._gscale(B)
-        canvas_ptr = dp(ws.canvas) if (outputs or parts is None) else None
-        _lib.call("mog_recon_loss", dp(X), canvas_ptr, dp(parts), T if parts is not None else 0,
-                  B * C2, dp(ws.prows), self.canvas_size, dp(ws.klsum), dp(ws.digits), dp(targets), B, C2, float(gscale),
-                  dp(ws.recon) if outputs else None, dp(ws.bce), dp(ws.mse), dp(ws.loss_b),
-                  dp(ws.acc_b) if targets is not None else None,
-                  dp(ws.dcanvas) if need_grad else None, s)
+        _ops.recon_loss_(X, ws.canvas if (outputs or parts is None) else None, parts,
+                         T if parts is not None else 0, B * C2, ws.prows, self.canvas_size,
+                         ws.klsum, ws.digits, targets, B, C2, float(gscale),
+                         ws.recon if outputs else None, ws.bce, ws.mse, ws.loss_b,
+                         ws.acc_b if targets is not None else None,
+                         ws.dcanvas if need_grad else None)
         _lib.call("mog_asr_finalize", B, T, self.canvas_size, len(self.constrains_num),
                   self._cons_arr, g, float(self._gscale(B)), dp(ws.arec),
                   dp(ws.live), dp(ws.zsum), dp(ws.pr), dp(ws.loss_b), dp(ws.element),
                   dp(ws.margin), s)
-        _lib.call("mog_batch_mean", dp(ws.loss_b), dp(ws.acc_b) if targets is not None else None,
-                  dp(ws.mse), None, B, dp(ws.means), s)
+        _ops.batch_mean_(ws.loss_b, ws.acc_b if targets is not None else None, ws.mse, None, B,
+                         ws.means)
         _lib.call("mog_add", dp(ws.means), dp(ws.margin), dp(ws.means), 1, s)
         self._outputs_ready = True
 
@@ -418,24 +420,19 @@ class AIRModel(_AirBase):
                       _lib.ptr_array([dp(x) if (k != 5 or fix < 0) else None
                                       for k, x in enumerate(dpre)]), s)
             # dh[t] += the five heads reading h_t; dhg[t] += the generative shift heads
-            _lib.call("mog_gemm_f32_kseg", 5,
-                      _lib.ptr_array([dp(dpre[k]) for k in (0, 1, 2, 6, 7)]),
-                      _lib.ptr_array([dp(x) for x in head_w]), dp(ws.dh[t]), None, dp(ws.dh[t]),
-                      B, H, 64, 64, 64, H, 0, 1, 0, s)
-            _lib.call("mog_gemm_f32_kseg", 2, _lib.ptr_array([dp(dpre[3]), dp(dpre[4])]),
-                      _lib.ptr_array([dp(x) for x in gen_w]), dp(ws.dhg[t]), None,
-                      dp(ws.dhg[t]), B, H, 64, 64, 64, H, 0, 1, 0, s)
+            ops.gemm_kseg([dpre[k] for k in (0, 1, 2, 6, 7)], head_w, ws.dh[t], B, H, 64, 64, 64,
+                          H, transB=True, Cin=ws.dh[t])
+            ops.gemm_kseg([dpre[3], dpre[4]], gen_w, ws.dhg[t], B, H, 64, 64, 64, H, transB=True,
+                          Cin=ws.dhg[t])
             if fix < 0 and t > 0:  # the prior at step t reads hg_{t-1}
                 gemm([dpre[5]], [self._N("z_pres/prior/dense/kernel")], [ws.dhg[t - 1]], B, H,
                      64, 64, 64, H, transB=True, Cin=[ws.dhg[t - 1]])
             dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
-            _lib.call("mog_lstm_cell_backward", dp(ws.G[t]), None,
-                      dp(ws.c[t - 1]) if t > 0 else None, dp(ws.c[t]), dp(ws.dh[t]), dp(dc_in),
-                      dp(ws.dG[t]), dp(ws.dc[t % 2]), dp(ws.dGsum), B, H, s)
+            _ops.lstm_cell_backward_(ws.G[t], None, ws.c[t - 1] if t > 0 else None, ws.c[t],
+                                     ws.dh[t], dc_in, ws.dG[t], ws.dc[t % 2], ws.dGsum, B, H)
             dcg_in = ws.dcg[(t + 1) % 2] if t < T - 1 else None
-            _lib.call("mog_lstm_cell_backward", dp(ws.Gg[t]), None,
-                      dp(ws.cg[t - 1]) if t > 0 else None, dp(ws.cg[t]), dp(ws.dhg[t]),
-                      dp(dcg_in), dp(ws.dGg[t]), dp(ws.dcg[t % 2]), dp(ws.dGgsum), B, H, s)
+            _ops.lstm_cell_backward_(ws.Gg[t], None, ws.cg[t - 1] if t > 0 else None, ws.cg[t],
+                                     ws.dhg[t], dcg_in, ws.dGg[t], ws.dcg[t % 2], ws.dGgsum, B, H)
             if t > 0:
                 gemm([ws.dG[t]], [Ki[C2:]], [ws.dU], B, KU, 4 * H, 4 * H, 4 * H, LU,
                      transB=True)

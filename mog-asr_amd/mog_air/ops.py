@@ -1,9 +1,10 @@
 """Typed wrappers of the HIP entry points over torch device tensors.
 
-torch supplies device memory and the current HIP stream only; every
-computation below is a launch of libmog_air.so.  Arguments are validated
-here (device, dtype, contiguity, shape) before any launch, so a shape error
-never reaches a kernel."""
+Every launch goes through the PyTorch-ROCm custom operators torch.ops.mog_air.*
+(csrc/torch_ops.cpp, a TORCH_LIBRARY fragment over the C ABI of libmog_air.so)
+on torch's current HIP stream.  Arguments are validated here (device, dtype,
+contiguity, shape) before any launch, so a shape error never reaches a
+kernel."""
 from __future__ import annotations
 
 from typing import Optional, Sequence
@@ -11,6 +12,9 @@ from typing import Optional, Sequence
 import torch
 
 from . import _lib
+
+_lib.load_torch_ops()
+_ops = torch.ops.mog_air
 
 EPI_STORE, EPI_RELU, EPI_SOFTPLUS, EPI_SIGMOID_NOISE = 0, 1, 2, 3
 EPI_SOFTPLUS_BWD, EPI_ATOMIC, EPI_RELU_BWD = 4, 5, 6
@@ -35,6 +39,10 @@ def _chk(t: torch.Tensor, name: str, dtype=torch.float32):
         raise ValueError(f"{name} must be contiguous")
 
 
+def _opt_list(xs):
+    return [] if xs is None else list(xs)
+
+
 def gemm(A: Sequence[torch.Tensor], B: Sequence[torch.Tensor], C: Sequence[torch.Tensor],
          M: int, N: int, K: int, lda: int, ldb: int, ldc: int, transA=False, transB=False,
          epi=EPI_STORE, bias=None, Cin=None, Cpre=None, aux=None, ldaux=0,
@@ -43,15 +51,17 @@ def gemm(A: Sequence[torch.Tensor], B: Sequence[torch.Tensor], C: Sequence[torch
     tensors (or views) whose data_ptr is the matrix origin."""
     nb = len(C)
     assert len(A) == nb and len(B) == nb and 1 <= nb <= 8
+    _ops.gemm_f32_(list(A), list(B), list(C), _opt_list(bias), _opt_list(Cin), _opt_list(Cpre),
+                   _opt_list(aux), _opt_list(colsum), M, N, K, lda, ldb, ldc, ldaux,
+                   bool(transA), bool(transB), epi, float(aux_scale), int(splitk))
 
-    def arr(xs):
-        if xs is None:
-            return None
-        return _lib.ptr_array([dp(x) for x in xs])
 
-    _lib.call("mog_gemm_f32", nb, arr(A), arr(B), arr(C), arr(bias), arr(Cin), arr(Cpre),
-              arr(aux), arr(colsum), M, N, K, lda, ldb, ldc, ldaux, int(transA), int(transB),
-              epi, float(aux_scale), int(splitk), stream_ptr())
+def gemm_kseg(A: Sequence[torch.Tensor], B: Sequence[torch.Tensor], C: torch.Tensor, M: int,
+              N: int, kseg: int, lda: int, ldb: int, ldc: int, transB=False, Cin=None,
+              epi=EPI_STORE) -> None:
+    """C = sum_s A_s op(B_s) as ONE k-ordered chain (mog_gemm_f32_kseg)."""
+    _ops.gemm_f32_kseg_(list(A), list(B), C, None, Cin, M, N, kseg, lda, ldb, ldc, False,
+                        bool(transB), epi)
 
 
 def dense(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor,
@@ -89,8 +99,7 @@ def stn_forward(U: torch.Tensor, theta: torch.Tensor, out_hw, out: Optional[torc
         mode = 1
     else:
         mode = 2 if out.dtype == torch.bfloat16 else 0
-    _lib.call("mog_stn_forward", dp(U), N, Hin, Win, dp(theta), Ho, Wo, dp(out), dp(z), dp(mask),
-              mode, stream_ptr())
+    _ops.stn_forward_(U, N, Hin, Win, theta, Ho, Wo, out, z, mask, mode)
     return out
 
 
@@ -103,16 +112,9 @@ def gemm_bf16(A, B, C, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, tn=
     """Batched bf16-operand MFMA GEMM (see mog_gemm_bf16); output dtype is C's."""
     nb = len(C)
     assert len(A) == nb and len(B) == nb and 1 <= nb <= 8
-    out_bf16 = C[0].dtype == torch.bfloat16
-
-    def arr(xs):
-        if xs is None:
-            return None
-        return _lib.ptr_array([dp(x) for x in xs])
-
-    _lib.call("mog_gemm_bf16", nb, arr(A), arr(B), arr(C), arr(bias), arr(Cin), arr(aux),
-              arr(colsum), M, N, K, lda, ldb, ldc, ldaux, int(tn), epi, int(out_bf16),
-              float(aux_scale), int(splitk), stream_ptr())
+    _ops.gemm_bf16_(list(A), list(B), list(C), _opt_list(bias), _opt_list(Cin), _opt_list(aux),
+                    _opt_list(colsum), M, N, K, lda, ldb, ldc, ldaux, bool(tn), epi,
+                    float(aux_scale), int(splitk))
 
 
 def cvt_bf16(src: torch.Tensor, dst: torch.Tensor, transpose: bool) -> None:
@@ -155,9 +157,9 @@ def stn_backward(U: torch.Tensor, theta: torch.Tensor, out_hw, G: torch.Tensor,
             dtheta = torch.empty((N, 6), device=dev, dtype=torch.float32)
         if want_dot and dot is None:
             dot = torch.empty((N,), device=dev, dtype=torch.float32)
-        _lib.call("mog_stn_backward_sigmoid_bf16", dp(U), N, Hin, Win, dp(theta), Ho, Wo, dp(G),
-                  dp(gscale), dp(dm_bf16), dp(dtheta if want_dtheta else None),
-                  dp(dot if want_dot else None), 0, NG if NG < N else 0, stream_ptr())
+        _ops.stn_backward_sigmoid_bf16_(U, N, Hin, Win, theta, Ho, Wo, G, gscale, dm_bf16,
+                                        dtheta if want_dtheta else None,
+                                        dot if want_dot else None, NG if NG < N else 0)
         return dm_bf16, dtheta, dot
     if want_dU and dU is None:
         dU = torch.empty((N, Hin * Win), device=dev, dtype=torch.float32)
@@ -165,10 +167,9 @@ def stn_backward(U: torch.Tensor, theta: torch.Tensor, out_hw, G: torch.Tensor,
         dtheta = torch.empty((N, 6), device=dev, dtype=torch.float32)
     if want_dot and dot is None:
         dot = torch.empty((N,), device=dev, dtype=torch.float32)
-    _lib.call("mog_stn_backward", dp(U), N, Hin, Win, dp(theta), Ho, Wo, dp(G), dp(gscale),
-              dp(dU if want_dU else None), dp(dtheta if want_dtheta else None),
-              dp(dot if want_dot else None), NU if NU < N else 0, NG if NG < N else 0,
-              stream_ptr())
+    _ops.stn_backward_(U, N, Hin, Win, theta, Ho, Wo, G, gscale, dU if want_dU else None,
+                       dtheta if want_dtheta else None, dot if want_dot else None,
+                       NU if NU < N else 0, NG if NG < N else 0)
     return dU, dtheta, dot
 
 
@@ -176,7 +177,12 @@ def colsum_add(X: torch.Tensor, R: int, N: int, ld: int, out: torch.Tensor) -> N
     _lib.call("mog_colsum_add", dp(X), R, N, ld, dp(out), stream_ptr())
 
 
+def _i64(v: int) -> int:
+    """a 64-bit counter / seed as the signed int64 of an op schema's `int`"""
+    v &= 2 ** 64 - 1
+    return v - 2 ** 64 if v >= 2 ** 63 else v
+
+
 def rng_fill(out: torch.Tensor, seed: int, offset: int, normal: bool) -> None:
     _chk(out, "out")
-    _lib.call("mog_rng_fill", dp(out), out.numel(), seed & (2 ** 64 - 1),
-              offset & (2 ** 64 - 1), int(normal), stream_ptr())
+    _ops.rng_fill_(out, _i64(seed), _i64(offset), bool(normal))

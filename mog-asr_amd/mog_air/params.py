@@ -150,19 +150,18 @@ class ParamStore:
         """TF AdamOptimizer.apply_gradients after the reference's per-tensor
         sanitize + clip_by_norm (air_model.py:944-999).  beta powers are fp32
         variables starting at beta (t = 1) and multiplied after each update."""
-        from .ops import stream_ptr
+        from . import ops  # noqa: F401  (registers torch.ops.mog_air)
         lr_t = np.float32(lr) * np.sqrt(np.float32(1) - self.beta2_power,
                                         dtype=np.float32) / (np.float32(1) - self.beta1_power)
         # clip None (gradient_clipping_norm=None): the reference applies the
         # gradients as they are, without NaN/Inf zeroing (air_model.py:948)
         if clip is not None:
             self.sumsq.zero_()
-        _lib.call("mog_clip_adam", self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(),
-                  self.v.data_ptr(), self.t_off.data_ptr(), self.t_len.data_ptr(),
-                  self.t_bt.data_ptr(), self.t_bs.data_ptr(), self.n_blocks,
-                  self.sumsq.data_ptr() if clip is not None else None,
-                  float(clip) if clip is not None else 0.0, float(lr_t), float(beta1),
-                  float(beta2), float(eps), stream_ptr())
+        torch.ops.mog_air.clip_adam_(self.flat, self.grad, self.m, self.v, self.t_off, self.t_len,
+                                     self.t_bt, self.t_bs, self.n_blocks,
+                                     self.sumsq if clip is not None else None,
+                                     float(clip) if clip is not None else 0.0, float(lr_t),
+                                     float(beta1), float(beta2), float(eps))
         self.beta1_power = np.float32(self.beta1_power * np.float32(beta1))
         self.beta2_power = np.float32(self.beta2_power * np.float32(beta2))
         self.adam_t += 1

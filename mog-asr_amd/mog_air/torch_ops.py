@@ -1,8 +1,9 @@
-"""PyTorch-ROCm custom ops over the HIP kernels: the
-``mog_air::`` operator namespace, so the hot-path pieces are callable (and
-differentiable) from ordinary torch code the way the reference's TF graph
-uses transformer() / vae() / BasicLSTMCell / AdamOptimizer.  Each op launches
-the same HIP kernel the AIRModel host drives through the C ABI, on torch's
+"""Differentiable PyTorch-ROCm custom ops over the HIP kernels:
+functional ``mog_air::`` operators with autograd, so the hot-path pieces are
+callable from ordinary torch code the way the reference's TF graph uses
+transformer() / vae() / BasicLSTMCell / AdamOptimizer.  Every op is a
+composition of the launch-level C++ operators of csrc/torch_ops.cpp
+(torch.ops.mog_air.*_ -- the same launches the AIRModel schedules), on torch's
 current HIP stream; there is no CPU implementation (a CPU tensor raises).
 
     import mog_air.torch_ops                          # registers the ops
@@ -14,16 +15,26 @@ Ops (reference counterpart):
   stn_accumulate_(canvas[N,C*C], U, theta, z[N], mask[N]) (in place)  air_model.py:580-588,665-675
   lstm_cell(G[B,4H], c_prev[B,H]) -> (c, h)                         BasicLSTMCell gates
   dense(x, W, b, act) -> act(x W + b)  act: 0 none, 1 relu, 2 softplus  fully_connected
+  glimpse_vae(g[B,784], W[7], b[7], eps_z, eps_x, lik_std)            vae.py:5-48 (fp32)
+      -> [r, mu, logvar, z, *saved]   differentiable in g, W, b through r, mu, logvar, z
+  stn_vae_step(x[B,C*C], theta_f, theta_b, z_pres[B], mask[B], eps_z, eps_x, W[7], b[7],
+               lik_std) -> [canvas_part[B,C*C], r, mu, logvar, z, vae_kl, *saved]
+      the fused bf16 STN-read -> VAE -> STN-write step (air_model.py:523-588, vae.py:5-48);
+      differentiable in theta_f, theta_b, z_pres, W, b through canvas_part
   tf_adam_clip_(flat params, grads, m, v, lr, clip, beta1, beta2, eps, step)  air_model.py:941-999
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import List, Tuple
 
+import numpy as np
 import torch
 
 from . import _lib, ops
-from .ops import EPI_RELU, EPI_SOFTPLUS, EPI_STORE, dp, stream_ptr
+from .ops import (BF_ATOMIC, BF_SOFTPLUS_BWD, BF_STORE, EPI_ATOMIC, EPI_RELU, EPI_SIGMOID_NOISE,
+                  EPI_SOFTPLUS, EPI_SOFTPLUS_BWD, EPI_STORE, gemm, gemm_bf16)
+
+_ops = ops._ops
 
 
 def _need_hip(*ts):
@@ -40,8 +51,7 @@ def stn(U: torch.Tensor, theta: torch.Tensor, Hout: int, Wout: int) -> torch.Ten
     _need_hip(U, theta)
     N, Hin, Win = U.shape
     out = torch.empty((N, Hout * Wout), device=U.device, dtype=torch.float32)
-    _lib.call("mog_stn_forward", dp(U), N, Hin, Win, dp(theta), Hout, Wout, dp(out), None, None,
-              0, stream_ptr())
+    _ops.stn_forward_(U, N, Hin, Win, theta, Hout, Wout, out, None, None, 0)
     return out.view(N, Hout, Wout)
 
 
@@ -86,8 +96,7 @@ def stn_accumulate_(canvas: torch.Tensor, U: torch.Tensor, theta: torch.Tensor, 
     N, Hin, Win = U.shape
     C2 = canvas.shape[1]
     C = int(round(C2 ** 0.5))
-    _lib.call("mog_stn_forward", dp(U), N, Hin, Win, dp(theta), C, C, dp(canvas), dp(z),
-              dp(mask), 1, stream_ptr())
+    _ops.stn_forward_(U, N, Hin, Win, theta, C, C, canvas, z, mask, 1)
 
 
 # ----------------------------------------------------------------- LSTM ----
@@ -97,7 +106,7 @@ def lstm_cell(G: torch.Tensor, c_prev: torch.Tensor) -> Tuple[torch.Tensor, torc
     B, H = c_prev.shape
     c = torch.empty_like(c_prev)
     h = torch.empty_like(c_prev)
-    _lib.call("mog_lstm_cell_forward", dp(G), None, dp(c_prev), dp(c), dp(h), B, H, stream_ptr())
+    _ops.lstm_cell_forward_(G, None, c_prev, c, h, B, H)
     return c, h
 
 
@@ -113,8 +122,7 @@ def lstm_cell_backward(G: torch.Tensor, c_prev: torch.Tensor, c: torch.Tensor, d
     B, H = c_prev.shape
     dG = torch.empty_like(G)
     dc_prev = torch.empty_like(c_prev)
-    _lib.call("mog_lstm_cell_backward", dp(G), None, dp(c_prev), dp(c), dp(dh), dp(dc), dp(dG),
-              dp(dc_prev), None, B, H, stream_ptr())
+    _ops.lstm_cell_backward_(G, None, c_prev, c, dh, dc, dG, dc_prev, None, B, H)
     return dG, dc_prev
 
 
@@ -149,13 +157,247 @@ def dense(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, act: int) -> torch.
     N = W.shape[1]
     out = torch.empty((M, N), device=x.device, dtype=torch.float32)
     epi = {0: EPI_STORE, 1: EPI_RELU, 2: EPI_SOFTPLUS}[int(act)]
-    ops.gemm([x], [W], [out], M, N, K, K, N, N, epi=epi, bias=[b])
+    gemm([x], [W], [out], M, N, K, K, N, N, epi=epi, bias=[b])
     return out
 
 
 @dense.register_fake
 def _(x, W, b, act):
     return x.new_empty((x.shape[0], W.shape[1]))
+
+
+# ------------------------------------------------------------ glimpse VAE ----
+_VAE_SHAPES = ((784, 512), (512, 256), (256, 50), (256, 50), (50, 256), (256, 512), (512, 784))
+
+
+def _check_vae(weights, biases):
+    if len(weights) != 7 or len(biases) != 7:
+        raise ValueError("7 VAE layers: recognition_1, recognition_2, rec_mean, "
+                         "rec_log_variance, generative_1, generative_2, gen_mean")
+    for w, b, s in zip(weights, biases, _VAE_SHAPES):
+        if tuple(w.shape) != s or tuple(b.shape) != (s[1],):
+            raise ValueError(f"VAE layer shape {tuple(w.shape)} / {tuple(b.shape)}, expected {s}")
+    _need_hip(*weights, *biases)
+
+
+@torch.library.custom_op("mog_air::glimpse_vae", mutates_args=())
+def glimpse_vae(g: torch.Tensor, weights: List[torch.Tensor], biases: List[torch.Tensor],
+                eps_z: torch.Tensor, eps_x: torch.Tensor, lik_std: float
+                ) -> List[torch.Tensor]:
+    """vae() of air/vae.py:5-48 in fp32 (the reference's precision): every
+    dense layer one k-ordered fma chain, TF softplus / sigmoid epilogues,
+    z = mu + eps_z sqrt(exp(logvar)), r = sigmoid(gen_mean + lik_std eps_x).
+    Returns [r, mu, logvar, z] and the saved pre- / post-activations (a1pre,
+    a1, a2pre, a2, d1pre, d1, d2pre, d2) the backward uses."""
+    _need_hip(g, eps_z, eps_x)
+    _check_vae(weights, biases)
+    B = g.shape[0]
+    e = lambda n: torch.empty((B, n), device=g.device, dtype=torch.float32)  # noqa: E731
+    a1p, a1, a2p, a2 = e(512), e(512), e(256), e(256)
+    mu, lv, z = e(50), e(50), e(50)
+    d1p, d1, d2p, d2, r = e(256), e(256), e(512), e(512), e(784)
+    W, b = weights, biases
+    gemm([g], [W[0]], [a1], B, 512, 784, 784, 512, 512, epi=EPI_SOFTPLUS, bias=[b[0]], Cpre=[a1p])
+    gemm([a1], [W[1]], [a2], B, 256, 512, 512, 256, 256, epi=EPI_SOFTPLUS, bias=[b[1]],
+         Cpre=[a2p])
+    gemm([a2, a2], [W[2], W[3]], [mu, lv], B, 50, 256, 256, 50, 50, bias=[b[2], b[3]])
+    zero = torch.zeros(B, device=g.device, dtype=torch.float32)
+    _ops.vae_sample_forward_(B, 50, 0.0, 1.0, 0.0, mu, lv, eps_z, z, None, 0, zero, zero.clone(),
+                             zero.clone())
+    gemm([z], [W[4]], [d1], B, 256, 50, 50, 256, 256, epi=EPI_SOFTPLUS, bias=[b[4]], Cpre=[d1p])
+    gemm([d1], [W[5]], [d2], B, 512, 256, 256, 512, 512, epi=EPI_SOFTPLUS, bias=[b[5]],
+         Cpre=[d2p])
+    gemm([d2], [W[6]], [r], B, 784, 512, 512, 784, 784, epi=EPI_SIGMOID_NOISE, bias=[b[6]],
+         aux=[eps_x], ldaux=784, aux_scale=float(lik_std))
+    return [r, mu, lv, z, a1p, a1, a2p, a2, d1p, d1, d2p, d2]
+
+
+@glimpse_vae.register_fake
+def _(g, weights, biases, eps_z, eps_x, lik_std):
+    B = g.shape[0]
+    e = lambda n: g.new_empty((B, n))  # noqa: E731
+    return [e(784), e(50), e(50), e(50), e(512), e(512), e(256), e(256), e(256), e(256), e(512),
+            e(512)]
+
+
+def _gv_setup(ctx, inputs, output):
+    g, weights, biases, eps_z, eps_x, lik_std = inputs
+    ctx.save_for_backward(g, eps_z, *output, *weights)
+
+
+def _gv_bwd(ctx, grads):
+    g, eps_z, r, mu, lv, z, a1p, a1, a2p, a2, d1p, d1, d2p, d2, *W = ctx.saved_tensors
+    dr, dmu, dlv, dz = grads[:4]
+    B, dev = g.shape[0], g.device
+    e = lambda *s: torch.empty(s, device=dev, dtype=torch.float32)  # noqa: E731
+    zeros = lambda *s: torch.zeros(s, device=dev, dtype=torch.float32)  # noqa: E731
+    dr = zeros(B, 784) if dr is None else dr.contiguous()
+    dm, dd2, dd1, dzt = e(B, 784), e(B, 512), e(B, 256), e(B, 50)
+    _ops.sigmoid_backward_(r, dr, dm, B * 784)
+    gemm([dm], [W[6]], [dd2], B, 512, 784, 784, 784, 512, transB=True, epi=EPI_SOFTPLUS_BWD,
+         aux=[d2p], ldaux=512)
+    gemm([dd2], [W[5]], [dd1], B, 256, 512, 512, 512, 256, transB=True, epi=EPI_SOFTPLUS_BWD,
+         aux=[d1p], ldaux=256)
+    gemm([dd1], [W[4]], [dzt], B, 50, 256, 256, 256, 50, transB=True)
+    if dz is not None:
+        _ops.add_(dzt, dz.contiguous(), dzt, B * 50)
+    dmut, dlvt = e(B, 50), e(B, 50)
+    zero = torch.zeros(B, device=dev, dtype=torch.float32)
+    _ops.vae_sample_backward_(B, 50, 0.0, 1.0, 0.0, mu, lv, eps_z, dzt, zero, dmut, dlvt, None,
+                              None, 0)
+    if dmu is not None:
+        _ops.add_(dmut, dmu.contiguous(), dmut, B * 50)
+    if dlv is not None:
+        _ops.add_(dlvt, dlv.contiguous(), dlvt, B * 50)
+    tmp, da2, da1, dg = e(B, 256), e(B, 256), e(B, 512), e(B, 784)
+    gemm([dmut], [W[2]], [tmp], B, 256, 50, 50, 50, 256, transB=True)
+    gemm([dlvt], [W[3]], [da2], B, 256, 50, 50, 50, 256, transB=True, epi=EPI_SOFTPLUS_BWD,
+         Cin=[tmp], aux=[a2p], ldaux=256)
+    gemm([da2], [W[1]], [da1], B, 512, 256, 256, 256, 512, transB=True, epi=EPI_SOFTPLUS_BWD,
+         aux=[a1p], ldaux=512)
+    gemm([da1], [W[0]], [dg], B, 784, 512, 512, 512, 784, transB=True)
+    # weight / bias gradients: dW = X^T dY (fp32 atomics), db = colsum(dY)
+    xs = (g, a1, a2, a2, z, d1, d2)
+    dys = (da1, da2, dmut, dlvt, dd1, dd2, dm)
+    gW = [zeros(*w.shape) for w in W]
+    gb = [zeros(w.shape[1]) for w in W]
+    for x, dy, gw, gbi in zip(xs, dys, gW, gb):
+        K, M = x.shape
+        N = dy.shape[1]
+        gemm([x], [dy], [gw], M, N, K, M, N, N, transA=True, epi=EPI_ATOMIC, colsum=[gbi])
+    return dg, gW, gb, None, None, None
+
+
+glimpse_vae.register_autograd(_gv_bwd, setup_context=_gv_setup)
+
+
+# -------------------------------------- fused STN read -> VAE -> STN write ----
+def _pack_vae_bf16(weights):
+    """bf16 packs of the 7 VAE matrices: W^T in MFMA B-fragment order (the
+    fused kernel's operand, mog_cvt_bf16_batch transpose 2) and W [in][out8]
+    (the backward GEMMs' dX operand), one batched launch."""
+    dev = weights[0].device
+    bf = dict(device=dev, dtype=torch.bfloat16)
+    wf, wn, srcs, dsts, dims = [], [], [], [], []
+    for w in weights:
+        I, O = w.shape
+        Np, Kp = (O + 15) // 16 * 16, (I + 31) // 32 * 32
+        f = torch.zeros((Np, Kp), **bf)
+        n = torch.zeros((I, (O + 7) // 8 * 8), **bf)
+        wf.append(f)
+        wn.append(n)
+        srcs += [w, w]
+        dsts += [f, n]
+        dims += [I, O, O, Np, Kp, Kp, 2, I, O, O, I, n.shape[1], n.shape[1], 0]
+    _ops.cvt_bf16_batch_(srcs, dsts, dims)
+    return wf, wn
+
+
+@torch.library.custom_op("mog_air::stn_vae_step", mutates_args=())
+def stn_vae_step(x: torch.Tensor, theta_f: torch.Tensor, theta_b: torch.Tensor,
+                 z_pres: torch.Tensor, mask: torch.Tensor, eps_z: torch.Tensor,
+                 eps_x: torch.Tensor, weights: List[torch.Tensor], biases: List[torch.Tensor],
+                 lik_std: float) -> List[torch.Tensor]:
+    """One loop step's glimpse path (air_model.py:523-588, vae.py:5-48) in the
+    fused bf16 kernel (vae_step.hip), functional form: canvas_part =
+    mask ? z_pres * STN(r, theta_b) : 0 over the C x C canvas, and r, mu,
+    logvar, z, vae_kl (the per-image VAE KL of vae.py:27-30), then the saved
+    bf16 activations (g, a1, a2, z, d1, d2) of the backward."""
+    _need_hip(x, theta_f, theta_b, z_pres, mask, eps_z, eps_x)
+    _check_vae(weights, biases)
+    B, C2 = x.shape
+    C = int(round(C2 ** 0.5))
+    dev = x.device
+    f32 = dict(device=dev, dtype=torch.float32)
+    bf = dict(device=dev, dtype=torch.bfloat16)
+    wf, _ = _pack_vae_bf16(weights)
+    part = torch.zeros((B, C2), **f32)
+    rows = torch.empty(B, device=dev, dtype=torch.int32)
+    runloss, vkl = torch.zeros(B, **f32), torch.empty(B, **f32)
+    gb, a1b, a2b = torch.empty((B, 784), **bf), torch.empty((B, 512), **bf), torch.empty((B, 256), **bf)
+    zb = torch.zeros((B, 56), **bf)
+    d1b, d2b = torch.empty((B, 256), **bf), torch.empty((B, 512), **bf)
+    mu, lv, z = torch.empty((B, 50), **f32), torch.empty((B, 50), **f32), torch.empty((B, 50), **f32)
+    r = torch.empty((B, 784), **f32)
+    _ops.stn_vae_step_(B, C, x, theta_f, theta_b, mask, z_pres, eps_z, eps_x, 0, 0, False, wf,
+                       list(biases), float(lik_std), 0.0, 1.0, 0.0, part, rows, runloss, vkl, gb,
+                       a1b, a2b, mu, lv, z, zb, d1b, d2b, r)
+    return [part, r, mu, lv, z, vkl, gb, a1b, a2b, zb, d1b, d2b]
+
+
+@stn_vae_step.register_fake
+def _(x, theta_f, theta_b, z_pres, mask, eps_z, eps_x, weights, biases, lik_std):
+    B, C2 = x.shape
+    f = lambda *s: x.new_empty(s)  # noqa: E731
+    b = lambda *s: x.new_empty(s, dtype=torch.bfloat16)  # noqa: E731
+    return [f(B, C2), f(B, 784), f(B, 50), f(B, 50), f(B, 50), f(B), b(B, 784), b(B, 512),
+            b(B, 256), b(B, 56), b(B, 256), b(B, 512)]
+
+
+def _svs_setup(ctx, inputs, output):
+    x, theta_f, theta_b, z_pres, mask, eps_z, eps_x, weights, biases, lik_std = inputs
+    part, r, mu, lv, z, vkl, gb, a1b, a2b, zb, d1b, d2b = output
+    ctx.save_for_backward(x, theta_f, theta_b, z_pres, mask, eps_z, r, mu, lv, gb, a1b, a2b, zb,
+                          d1b, d2b, *weights)
+
+
+def _svs_bwd(ctx, grads):
+    """Gradient from canvas_part (the other outputs are treated as
+    non-differentiable here): STN write backward with the output sigmoid
+    folded (bf16 dm), the bf16 VAE backward GEMM chain, the STN read backward
+    for d theta_f, and fp32 weight / bias gradients (split-K atomics)."""
+    (x, theta_f, theta_b, z_pres, mask, eps_z, r, mu, lv, gb, a1b, a2b, zb, d1b, d2b,
+     *W) = ctx.saved_tensors
+    dpart = grads[0]
+    B, C2 = x.shape
+    C = int(round(C2 ** 0.5))
+    dev = x.device
+    f32 = dict(device=dev, dtype=torch.float32)
+    bf = dict(device=dev, dtype=torch.bfloat16)
+    zeros = lambda *s: torch.zeros(s, **f32)  # noqa: E731
+    if dpart is None:
+        dpart = zeros(B, C2)
+    _, wn = _pack_vae_bf16(W)
+    zc = z_pres * (mask != 0).to(torch.float32)
+    dmb = torch.empty((B, 784), **bf)
+    dth_b, dot = torch.empty((B, 6), **f32), torch.empty(B, **f32)
+    ops.stn_backward(r, theta_b, (C, C), dpart.contiguous(), gscale=zc.contiguous(), want_dot=True,
+                     dtheta=dth_b, dot=dot, dm_bf16=dmb)
+    dd2b, dd1b = torch.empty((B, 512), **bf), torch.empty((B, 256), **bf)
+    dz = torch.empty((B, 50), **f32)
+    gemm_bf16([dmb], [wn[6]], [dd2b], B, 512, 784, 784, 784, 512, epi=BF_SOFTPLUS_BWD, aux=[d2b],
+              ldaux=512)
+    gemm_bf16([dd2b], [wn[5]], [dd1b], B, 256, 512, 512, 512, 256, epi=BF_SOFTPLUS_BWD,
+              aux=[d1b], ldaux=256)
+    gemm_bf16([dd1b], [wn[4]], [dz], B, 50, 256, 256, 256, 50, epi=BF_STORE)
+    dmub, dlvb = torch.zeros((B, 56), **bf), torch.zeros((B, 56), **bf)
+    _ops.vae_sample_backward_(B, 50, 0.0, 1.0, 0.0, mu, lv, eps_z, dz, torch.zeros(B, **f32),
+                              None, None, dmub, dlvb, 56)
+    tmp, da2b, da1b = torch.empty((B, 256), **f32), torch.empty((B, 256), **bf), \
+        torch.empty((B, 512), **bf)
+    dg = torch.empty((B, 784), **f32)
+    gemm_bf16([dmub], [wn[2]], [tmp], B, 256, 56, 56, 56, 256, epi=BF_STORE)
+    gemm_bf16([dlvb], [wn[3]], [da2b], B, 256, 56, 56, 56, 256, epi=BF_SOFTPLUS_BWD, Cin=[tmp],
+              aux=[a2b], ldaux=256)
+    gemm_bf16([da2b], [wn[1]], [da1b], B, 512, 256, 256, 256, 512, epi=BF_SOFTPLUS_BWD,
+              aux=[a1b], ldaux=512)
+    gemm_bf16([da1b], [wn[0]], [dg], B, 784, 512, 512, 512, 784, epi=BF_STORE)
+    dth_f = torch.empty((B, 6), **f32)
+    ops.stn_backward(x, theta_f, (28, 28), dg, want_dU=False, dtheta=dth_f)
+    xs = (gb, a1b, a2b, a2b, zb, d1b, d2b)
+    dys = (da1b, da2b, dmub, dlvb, dd1b, dd2b, dmb)
+    lds = (784, 512, 256, 256, 56, 256, 512)
+    ldy = (512, 256, 56, 56, 256, 512, 784)
+    gW = [zeros(*w.shape) for w in W]
+    gbias = [zeros(w.shape[1]) for w in W]
+    for xq, dy, gw, gbi, la, lb in zip(xs, dys, gW, gbias, lds, ldy):
+        M, N = gw.shape
+        gemm_bf16([xq], [dy], [gw], M, N, B, la, lb, N, tn=True, epi=BF_ATOMIC, colsum=[gbi])
+    dz_pres = dot * (mask != 0).to(torch.float32)
+    return None, dth_f, dth_b, dz_pres, None, None, None, gW, gbias, None
+
+
+stn_vae_step.register_autograd(_svs_bwd, setup_context=_svs_setup)
 
 
 # ----------------------------------------------------------- optimizer ----
@@ -175,12 +417,10 @@ def tf_adam_clip_(params: torch.Tensor, grads: torch.Tensor, m: torch.Tensor, v:
     bt = torch.zeros(nblk, device=dev, dtype=torch.int32)
     bs = torch.arange(nblk, device=dev, dtype=torch.int64) * chunk
     sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
-    import numpy as np
     f = np.float32
     b1p, b2p = f(1), f(1)
     for _ in range(int(step)):  # TF keeps the beta powers as fp32 variables
         b1p, b2p = f(b1p * f(beta1)), f(b2p * f(beta2))
     lr_t = f(lr) * np.sqrt(f(1) - b2p, dtype=np.float32) / (f(1) - b1p)
-    _lib.call("mog_clip_adam", dp(params), dp(grads), dp(m), dp(v), dp(off), dp(ln), dp(bt),
-              dp(bs), nblk, dp(sumsq), float(clip), float(lr_t), float(beta1), float(beta2),
-              float(eps), stream_ptr())
+    _ops.clip_adam_(params, grads, m, v, off, ln, bt, bs, nblk, sumsq, float(clip), float(lr_t),
+                    float(beta1), float(beta2), float(eps))

@@ -37,6 +37,23 @@ def test_all_headers_symbols_exported():
             assert hasattr(lib, name), (fn, name)
 
 
+def test_torch_ops_extension_registers_every_launch_op():
+    """csrc/torch_ops.cpp: the TORCH_LIBRARY fragment loads on a CPU host and
+    registers the launch-level ops the AIRModel dispatches through; a CPU
+    tensor finds no kernel (no CPU fallback)."""
+    from mog_air import _lib
+    _lib.load_torch_ops()
+    names = ("gemm_f32_", "gemm_f32_kseg_", "gemm_bf16_", "cvt_bf16_batch_", "stn_forward_",
+             "stn_backward_", "stn_backward_sigmoid_bf16_", "lstm_cell_forward_",
+             "lstm_cell_backward_", "air_step_forward_", "air_step_backward_",
+             "vae_sample_forward_", "vae_sample_backward_", "sigmoid_backward_", "stn_vae_step_",
+             "recon_loss_", "batch_mean_", "clip_adam_", "add_", "rng_fill_")
+    for n in names:
+        getattr(torch.ops.mog_air, n).default  # schema registered
+    with pytest.raises(NotImplementedError):
+        torch.ops.mog_air.rng_fill_(torch.zeros(4), 1, 0, True)
+
+
 def test_host_only_entry_point():
     from mog_air import _lib
     assert _lib.load().mog_optim_chunk_elems() == 4096
