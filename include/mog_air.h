@@ -72,6 +72,11 @@ int mog_stn_backward_sigmoid_bf16(const float* U, int N, int Hin, int Win, const
                                   int Hout, int Wout, const float* G, const float* gscale,
                                   void* dm, float* dtheta, float* dot, int u_period, int g_period,
                                   void* stream);
+/* The same with dm in fp32 (the reference-precision train step). */
+int mog_stn_backward_sigmoid_f32(const float* U, int N, int Hin, int Win, const float* theta,
+                                 int Hout, int Wout, const float* G, const float* gscale, float* dm,
+                                 float* dtheta, float* dot, int u_period, int g_period,
+                                 void* stream);
 
 /* ---- LSTM cell (TF-1.12 BasicLSTMCell, air_model.py:454-456,812-815) -----
  * G [B, 4H] gate pre-activations (i,j,f,o) WITHOUT bias when `bias` != NULL. */

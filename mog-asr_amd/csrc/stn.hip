@@ -238,16 +238,20 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
     float* dtheta, float* dot, int u_period, int g_period, long long* ts, int du_mode) {
 #pragma clang fp contract(off)
   extern __shared__ float smem[];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // wave-uniform image index (readfirstlane): the cotangent's buffer
+  // descriptor below is then provably uniform -- otherwise hipcc wraps every
+  // buffer load of the T pass in a waterfall loop and serialises them
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int n = blockIdx.x * (blockDim.x >> 6) + wv;
   if (n >= N) return;  // no workgroup barriers below
 #define TS(k) if (ts && lane == 0) ts[(size_t)n * 8 + (k)] = wall_clock64()
   TS(0);
   const int HWin = Hin * Win, P = Hout * Wout;
   const bool want_dU = dU != nullptr;
-  float th[6];
+  float th[6];  // wave-uniform (scalar registers): the branches below are uniform
 #pragma unroll
-  for (int k = 0; k < 6; ++k) th[k] = theta[n * 6 + k];
+  for (int k = 0; k < 6; ++k)
+    th[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(theta[n * 6 + k])));
   const bool sep = stn_separable(th) && Hin < 32768 && Win < 32768 && Hout <= 64;
   // separable dU (no atomics): axis-aligned, increasing maps, extents <= 64
   const bool sdu = want_dU && sep && th[0] > 0.0f && th[4] > 0.0f && Hin <= 64 && Win <= 64 &&
@@ -300,14 +304,17 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
   TS(2);
   if (!want_dU) return;
   wave_sync();
-  // du_mode 1: the glimpse gradient leaves through the VAE output sigmoid
-  // (vae.py:44-46; TF SigmoidGrad dm = (dr * r) * (1 - r), r = U) as bf16
+  // du_mode 1 / 2: the glimpse gradient leaves through the VAE output
+  // sigmoid (vae.py:44-46; TF SigmoidGrad dm = (dr * r) * (1 - r), r = U) as
+  // bf16 / fp32 -- bit-identical to dU followed by mog_sigmoid_backward
   float* dUn = dU + (size_t)n * HWin;
   __bf16* dMn = reinterpret_cast<__bf16*>(dU) + (size_t)n * HWin;
   auto put = [&](int idx, float d) {
     if (du_mode) {
       const float v = Un[idx];
-      dMn[idx] = (__bf16)((d * v) * (1.0f - v));
+      const float m = (d * v) * (1.0f - v);
+      if (du_mode == 1) dMn[idx] = (__bf16)m;
+      else dUn[idx] = m;
     } else {
       dUn[idx] = d;
     }
@@ -358,6 +365,15 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
     const unsigned long long lmr = __builtin_amdgcn_ballot_w64(
         lane < Hout && __float_as_int(rowtab[min(lane, Hout - 1)].x) !=
                            __float_as_int(rowtab[min(lane, Hout - 1)].y));
+    // the cotangent through a buffer descriptor (built in uniform control flow
+    // from uniform values, so it lives in SGPRs: no waterfall loop per load):
+    // 32-bit offsets, no 64-bit address registers per load
+    const unsigned long long gp = reinterpret_cast<unsigned long long>(Gn);
+    const unsigned glo = __builtin_amdgcn_readfirstlane((unsigned)gp);
+    const unsigned ghi = __builtin_amdgcn_readfirstlane((unsigned)(gp >> 32));
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<float*>(((unsigned long long)ghi << 32) | glo), 0,
+        __builtin_amdgcn_readfirstlane(P * 4), 0x00020000);
     const int tlo = lmr ? (__builtin_ctzll(lmr) / rpi) * rpi : Hout;
     const int thi = lmr ? 64 - __builtin_clzll(lmr) : Hout;
     if (ul < Win) {
@@ -365,10 +381,7 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
       constexpr int RC = 16;    // rows per chunk (register budget: occupancy)
       const int rb = tlo + half;  // the lane's first row
       const int nr = rb < thi ? (thi - rb + rpi - 1) / rpi : 0;
-      // the cotangent through a buffer descriptor: 32-bit offsets, no 64-bit
-      // address registers per load
-      const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<float*>(Gn), 0, P * 4, 0x00020000);
+
 #pragma unroll 1
       for (int r0 = 0; r0 < RMAX; r0 += RC) {
         if (r0 >= nr) break;
@@ -509,4 +522,14 @@ extern "C" int mog_stn_backward_sigmoid_bf16(const float* U, int N, int Hin, int
   return stn_backward_launch(U, N, Hin, Win, theta, Hout, Wout, G, gscale,
                              reinterpret_cast<float*>(dm), dtheta, dot, u_period, g_period, 1,
                              stream);
+}
+
+extern "C" int mog_stn_backward_sigmoid_f32(const float* U, int N, int Hin, int Win,
+                                            const float* theta, int Hout, int Wout,
+                                            const float* G, const float* gscale, float* dm,
+                                            float* dtheta, float* dot, int u_period, int g_period,
+                                            void* stream) {
+  MOG_CHECK_ARG(dm != nullptr && u_period == 0);
+  return stn_backward_launch(U, N, Hin, Win, theta, Hout, Wout, G, gscale, dm, dtheta, dot,
+                             u_period, g_period, 2, stream);
 }

@@ -123,14 +123,20 @@ void stn_backward_(const Tensor& U, int64_t N, int64_t Hin, int64_t Win, const T
         "stn_backward_");
 }
 
-void stn_backward_sigmoid_bf16_(const Tensor& U, int64_t N, int64_t Hin, int64_t Win,
+void stn_backward_sigmoid_(const Tensor& U, int64_t N, int64_t Hin, int64_t Win,
                                 const Tensor& theta, int64_t Hout, int64_t Wout, const Tensor& G,
                                 const optional<Tensor>& gscale, Tensor dm,
                                 const optional<Tensor>& dtheta, const optional<Tensor>& dot,
                                 int64_t g_period) {
-  check(mog_stn_backward_sigmoid_bf16(f(U), N, Hin, Win, f(theta), Hout, Wout, f(G), f(gscale),
-                                      p(dm), f(dtheta), f(dot), 0, g_period, stream()),
-        "stn_backward_sigmoid_bf16_");
+  // dm bf16 (configs[1]) or fp32 (reference precision)
+  if (dm.scalar_type() == at::kBFloat16)
+    check(mog_stn_backward_sigmoid_bf16(f(U), N, Hin, Win, f(theta), Hout, Wout, f(G), f(gscale),
+                                        p(dm), f(dtheta), f(dot), 0, g_period, stream()),
+          "stn_backward_sigmoid_");
+  else
+    check(mog_stn_backward_sigmoid_f32(f(U), N, Hin, Win, f(theta), Hout, Wout, f(G), f(gscale),
+                                       f(dm), f(dtheta), f(dot), 0, g_period, stream()),
+          "stn_backward_sigmoid_");
 }
 
 // ----------------------------------------------------------------- LSTM ----
@@ -296,7 +302,7 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "Tensor G, Tensor? gscale, Tensor? dU, Tensor? dtheta, Tensor? dot, int u_period, "
       "int g_period) -> ()");
   m.def(
-      "stn_backward_sigmoid_bf16_(Tensor U, int N, int Hin, int Win, Tensor theta, int Hout, "
+      "stn_backward_sigmoid_(Tensor U, int N, int Hin, int Win, Tensor theta, int Hout, "
       "int Wout, Tensor G, Tensor? gscale, Tensor(a!) dm, Tensor? dtheta, Tensor? dot, "
       "int g_period) -> ()");
   m.def(
@@ -358,7 +364,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("cvt_bf16_batch_", &cvt_bf16_batch_);
   m.impl("stn_forward_", &stn_forward_);
   m.impl("stn_backward_", &stn_backward_);
-  m.impl("stn_backward_sigmoid_bf16_", &stn_backward_sigmoid_bf16_);
+  m.impl("stn_backward_sigmoid_", &stn_backward_sigmoid_);
   m.impl("lstm_cell_forward_", &lstm_cell_forward_);
   m.impl("lstm_cell_backward_", &lstm_cell_backward_);
   m.impl("air_step_forward_", &air_step_forward_);

@@ -27,6 +27,7 @@ _SIGS = {
     "mog_stn_forward": [P, I, I, I, P, I, I, P, P, P, I, P],
     "mog_stn_backward": [P, I, I, I, P, I, I, P, P, P, P, P, I, I, P],
     "mog_stn_backward_sigmoid_bf16": [P, I, I, I, P, I, I, P, P, P, P, P, I, I, P],
+    "mog_stn_backward_sigmoid_f32": [P, I, I, I, P, I, I, P, P, P, P, P, I, I, P],
     "mog_lstm_cell_forward": [P, P, P, P, P, I, I, P],
     "mog_lstm_cell_backward": [P, P, P, P, P, P, P, P, P, I, I, P],
     "mog_air_step_forward": [I, I, I, I, I, I, F, F, F, F, F, F, F, F, F, F, P, P, P, P, P, P,

@@ -503,10 +503,10 @@ class AIRModel:
             ops.stn_backward(ws.r.view(TB, -1), ws.th_b, (C, C), ws.dcanvas, gscale=ws.zc,
                              dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True, n=TB,
                              dm_bf16=ws.dmb.view(TB, -1))
-        else:
+        else:  # fp32 dm through the output sigmoid, likewise
             ops.stn_backward(ws.r.view(TB, -1), ws.th_b, (C, C), ws.dcanvas, gscale=ws.zc,
-                             dU=ws.dr_all, dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True,
-                             n=TB)
+                             dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True, n=TB,
+                             dm=ws.dm.view(TB, -1))
         if self.precision == "bf16":
             self._vae_backward_bf16_all(ws, gscale)
         else:
@@ -546,7 +546,7 @@ class AIRModel:
         TB = ws.B * self.max_steps
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
-        _ops.sigmoid_backward_(ws.r, ws.dr_all, ws.dm, TB * W2)
+        # dm = SigmoidGrad(r, dr) was written by the STN write backward
         gemm([ws.dm], [vw["gen_mean"]], [ws.dd2], TB, G2, W2, W2, W2, G2,
              transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d2pre], ldaux=G2)
         gemm([ws.dd2], [vw["generative_2"]], [ws.dd1], TB, G1, G2, G2, G2, G1,

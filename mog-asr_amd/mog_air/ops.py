@@ -129,17 +129,19 @@ def cvt_bf16(src: torch.Tensor, dst: torch.Tensor, transpose: bool) -> None:
 def stn_backward(U: torch.Tensor, theta: torch.Tensor, out_hw, G: torch.Tensor,
                  gscale: Optional[torch.Tensor] = None, want_dU=True, want_dtheta=True,
                  want_dot=False, dU=None, dtheta=None, dot=None, n: Optional[int] = None,
-                 dm_bf16: Optional[torch.Tensor] = None):
+                 dm: Optional[torch.Tensor] = None, dm_bf16: Optional[torch.Tensor] = None):
     """Gradient of transformer().  ``n`` images (default U's); when U or G
     holds fewer rows than ``n``, image i reads row i % rows (several loop
     steps of one batch against the shared canvas or canvas gradient).
 
-    ``dm_bf16`` (bf16 [N, Hin*Win], U = the VAE output sigmoid r): the input
-    gradient is taken on through the sigmoid (vae.py:44-46) and stored as
-    bf16 there instead of dU -- bit-identical to dU followed by
-    mog_sigmoid_backward(out_bf16=1)."""
+    ``dm`` (bf16 or fp32 [N, Hin*Win], U = the VAE output sigmoid r): the
+    input gradient is taken on through the sigmoid (vae.py:44-46) and stored
+    there instead of dU -- bit-identical to dU followed by
+    mog_sigmoid_backward.  (``dm_bf16``: the same, kept as an alias.)"""
     _chk(U, "U")
     _chk(G, "G")
+    if dm is None:
+        dm = dm_bf16
     if U.dim() == 3:
         Hin, Win = U.shape[1], U.shape[2]
     else:
@@ -149,18 +151,18 @@ def stn_backward(U: torch.Tensor, theta: torch.Tensor, out_hw, G: torch.Tensor,
     N = NU if n is None else int(n)
     assert N % NU == 0 and N % NG == 0 and theta.numel() == 6 * N
     dev = U.device
-    if dm_bf16 is not None:
+    if dm is not None:
         assert want_dU and dU is None and NU == N
-        assert dm_bf16.dtype == torch.bfloat16 and dm_bf16.numel() >= N * Hin * Win
-        _chk(dm_bf16, "dm_bf16", torch.bfloat16)
+        assert dm.numel() >= N * Hin * Win
+        _chk(dm, "dm", dm.dtype if dm.dtype in (torch.bfloat16, torch.float32) else None)
         if want_dtheta and dtheta is None:
             dtheta = torch.empty((N, 6), device=dev, dtype=torch.float32)
         if want_dot and dot is None:
             dot = torch.empty((N,), device=dev, dtype=torch.float32)
-        _ops.stn_backward_sigmoid_bf16_(U, N, Hin, Win, theta, Ho, Wo, G, gscale, dm_bf16,
-                                        dtheta if want_dtheta else None,
-                                        dot if want_dot else None, NG if NG < N else 0)
-        return dm_bf16, dtheta, dot
+        _ops.stn_backward_sigmoid_(U, N, Hin, Win, theta, Ho, Wo, G, gscale, dm,
+                                   dtheta if want_dtheta else None, dot if want_dot else None,
+                                   NG if NG < N else 0)
+        return dm, dtheta, dot
     if want_dU and dU is None:
         dU = torch.empty((N, Hin * Win), device=dev, dtype=torch.float32)
     if want_dtheta and dtheta is None:

@@ -160,10 +160,11 @@ def test_stn_backward_vs_autograd(sep, src, dst):
                                atol=1e-3)
 
 
-@pytest.mark.parametrize("sep", [True, False])
-def test_stn_backward_sigmoid_bf16_matches_unfused(sep):
-    """The write backward with the output-sigmoid gradient folded in (bf16
-    dm straight from the kernel) is bit-identical to dU followed by
+@pytest.mark.parametrize("sep,dt", [(True, torch.bfloat16), (False, torch.bfloat16),
+                                    (True, torch.float32), (False, torch.float32)])
+def test_stn_backward_sigmoid_bf16_matches_unfused(sep, dt):
+    """The write backward with the output-sigmoid gradient folded in (bf16 or
+    fp32 dm straight from the kernel) is bit-identical to dU followed by
     mog_sigmoid_backward; dtheta / dot are unchanged."""
     from mog_air import _lib, ops
     from mog_air.ops import dp, stream_ptr
@@ -179,14 +180,15 @@ def test_stn_backward_sigmoid_bf16_matches_unfused(sep):
     gs[3] = 0.0
     dU, dth, dot = ops.stn_backward(_cuda(r), _cuda(thb), (C, C), _cuda(G), gscale=_cuda(gs),
                                     want_dot=True, n=N)
-    ref = torch.empty((N, W * W), device=DEV, dtype=torch.bfloat16)
-    _lib.call("mog_sigmoid_backward", dp(_cuda(r)), dp(dU), dp(ref), N * W * W, 1,
-              stream_ptr())
-    dm = torch.full((N, W * W), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ref = torch.empty((N, W * W), device=DEV, dtype=dt)
+    _lib.call("mog_sigmoid_backward", dp(_cuda(r)), dp(dU), dp(ref), N * W * W,
+              int(dt == torch.bfloat16), stream_ptr())
+    dm = torch.full((N, W * W), float("nan"), device=DEV, dtype=dt)
     _, dth2, dot2 = ops.stn_backward(_cuda(r), _cuda(thb), (C, C), _cuda(G), gscale=_cuda(gs),
-                                     want_dot=True, n=N, dm_bf16=dm)
+                                     want_dot=True, n=N, dm=dm)
     torch.cuda.synchronize()
-    assert torch.equal(dm.view(torch.int16), ref.view(torch.int16))
+    iv = torch.int16 if dt == torch.bfloat16 else torch.int32
+    assert torch.equal(dm.view(iv), ref.view(iv))
     assert torch.equal(dth2, dth) and torch.equal(dot2, dot)
 
 

@@ -44,7 +44,7 @@ def test_torch_ops_extension_registers_every_launch_op():
     from mog_air import _lib
     _lib.load_torch_ops()
     names = ("gemm_f32_", "gemm_f32_kseg_", "gemm_bf16_", "cvt_bf16_batch_", "stn_forward_",
-             "stn_backward_", "stn_backward_sigmoid_bf16_", "lstm_cell_forward_",
+             "stn_backward_", "stn_backward_sigmoid_", "lstm_cell_forward_",
              "lstm_cell_backward_", "air_step_forward_", "air_step_backward_",
              "vae_sample_forward_", "vae_sample_backward_", "sigmoid_backward_", "stn_vae_step_",
              "recon_loss_", "batch_mean_", "clip_adam_", "add_", "rng_fill_")
