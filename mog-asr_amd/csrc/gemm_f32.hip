@@ -109,6 +109,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t frsrc(const float* p, long ele
 //   otherwise (row-contiguous: A^T [K][M], B [K][N]): per (row, g) BK/4 dword
 //     loads at k = g, 4+g, 8+g, ... (coalesced over rows across lanes), one
 //     ds_write_b128 per four of them.
+// Elements masked off (k >= kend of a split-K chunk, still inside the
+// operand) are read at an offset past every descriptor's extent, so the
+// hardware returns 0: the mask is applied to the address, never to the loaded
+// value, and nothing waits for a load before its k-tile is written to LDS.
+constexpr int OOB = 0x7ffffff0;
+
 template <int ROWS, bool KC, int BK>
 struct TileIO {
   static constexpr int KK = BK / 4;
@@ -131,11 +137,9 @@ struct TileIO {
           for (int j = 0; j < 4; ++j) r[4 * i + j] = __uint_as_float(v[j]);
         } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float v =
-                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * j, 0, 0));
-            r[4 * i + j] = (full || gk + j < kend) ? v : 0.0f;
-          }
+          for (int j = 0; j < 4; ++j)
+            r[4 * i + j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                rs, (full || gk + j < kend) ? off + 4 * j : OOB, 0, 0));
         }
       }
     } else {
@@ -146,9 +150,8 @@ struct TileIO {
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk) {
           const int gk = k0 + 4 * kk + g;
-          const float v = __uint_as_float(
-              __builtin_amdgcn_raw_buffer_load_b32(rs, (gk * ld + r0 + row) * 4, 0, 0));
-          r[KK * i + kk] = (full || gk < kend) ? v : 0.0f;
+          r[KK * i + kk] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+              rs, (full || gk < kend) ? (gk * ld + r0 + row) * 4 : OOB, 0, 0));
         }
       }
     }
@@ -176,6 +179,54 @@ struct TileIO {
     }
   }
 };
+
+// Epilogue of one wave's (16 MI) x (16 NI) accumulator block at output rows
+// r0 + ..., columns c0 + ... (16x16 MFMA layout: lane (li, g) holds rows
+// 4g .. 4g+3 of column li of each tile).
+template <int MI, int NI, int EPI>
+__device__ __forceinline__ void store_tile(const floatx4 (&acc)[MI][NI], const GemmPtrs& P,
+                                           const GemmDims& D, int z, int r0, int c0, int lane) {
+#pragma clang fp contract(off)
+  const int M = D.M, N = D.N;
+  float* C = P.C[z];
+  const float* bias = P.bias[z];
+  const float* aux = P.aux[z];
+  float* Cpre = P.Cpre[z];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + mi * 16 + (lane >> 4) * 4 + r;
+        const int col = c0 + ni * 16 + (lane & 15);
+        if (row >= M || col >= N) continue;
+        const size_t o = (size_t)row * D.ldc + col;
+        float v = acc[mi][ni][r];
+        if (EPI == EPI_ATOMIC) {
+          atomicAdd(C + o, v);
+          continue;
+        }
+        if (EPI == EPI_SOFTPLUS_BWD) {
+          C[o] = v * mog_sigmoidf(aux[(size_t)row * D.ldaux + col]);
+          continue;
+        }
+        if (EPI == EPI_RELU_BWD) {
+          C[o] = aux[(size_t)row * D.ldaux + col] > 0.0f ? v : 0.0f;
+          continue;
+        }
+        if (bias != nullptr) v = v + bias[col];
+        if (EPI == EPI_STORE) {
+          C[o] = v;
+        } else {
+          if (Cpre != nullptr) Cpre[o] = v;
+          if (EPI == EPI_RELU) C[o] = v > 0.0f ? v : 0.0f;
+          if (EPI == EPI_SOFTPLUS) C[o] = mog_softplusf(v);
+          if (EPI == EPI_SIGMOID_NOISE)
+            C[o] = mog_sigmoidf(v + aux[(size_t)row * D.ldaux + col] * D.aux_scale);
+        }
+      }
+}
 
 template <int BM, int BN, int BK, int PF, bool TA, bool TB, int EPI, bool KSEG>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
@@ -313,44 +364,226 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
   }
   if (do_cs && n0 + t < N) atomicAdd(colsum + n0 + t, cs);
 
-  float* C = P.C[z];
-  const float* bias = P.bias[z];
-  const float* aux = P.aux[z];
-  float* Cpre = P.Cpre[z];
+  store_tile<MI, NI, EPI>(acc, P, D, z, m0 + wm, n0 + wn, lane);
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA form: operand k-tiles go global -> LDS by buffer_load_dwordx4 ... lds
+// (no register staging, no LDS store instructions), NS stages deep, with the
+// DMA of tile it+NS-1 issued right after the barrier of iteration it and a
+// counted vmcnt keeping NS-2 tiles in flight across every barrier.  A DMA
+// wave-instruction writes 64 x 16 B lane-linearly, so the LDS images are laid
+// out by choosing each lane's SOURCE address (MI355X guide §5 rule 21):
+//   KC image (operand k-contiguous: A [M][K], B^T [N][K]): ROWS rows of 16 k;
+//     16-B chunk c of row r holds k = 4 (c ^ kcs(r)) .. +3 (one instruction
+//     fills 16 rows, 64 B of each);
+//   RC image (operand row-contiguous: A^T [K][M], B [K][N]): 16 k-rows of
+//     ROWS floats; element n of k-row k sits at n ^ ((k & 1) << 4).
+// A fragment element (row, k = 4 kk + g) is one ds_read_b32: conflict-free on
+// RC images, 2-way on KC images (the minimum for 4-B reads of a 16-float row).
+// The MFMA sequence, and so every fma chain, is the register-staged kernel's.
+// KC chunk swizzle: BK = 16 -> 4 chunks per row, (r >> 1) & 3; BK = 32 -> 8
+// chunks, r & 7 (both the 2-way minimum for 4-B reads)
+template <int BK>
+__device__ __forceinline__ int kcs(int r) {
+  return BK == 16 ? (r >> 1) & 3 : r & 7;
+}
+
+template <int ROWS, bool KC, int BK>
+struct DmaOperand {
+  static constexpr int NQ = ROWS * BK * 4 / 1024;  // 1-KiB DMA instructions per k-tile
+  static constexpr int NWQ = NQ / 4;               // per wave
+  static constexpr int CPR = BK / 4;               // KC: 16-B chunks per row
+  static_assert(NQ % 4 == 0, "four waves share a tile's DMAs");
+  int voff[NWQ];  // this lane's source byte offset at k0 = 0
+  int kof[NWQ];   // its k within the tile (KC: first of its 4; RC: its k-row)
+  __device__ __forceinline__ void init(int w, int lane, int r0, int ld) {
+#pragma unroll
+    for (int j = 0; j < NWQ; ++j) {
+      const int q = w + 4 * j;
+      if constexpr (KC) {
+        const int row = (64 / CPR) * q + lane / CPR;
+        const int kc = 4 * ((lane % CPR) ^ kcs<BK>(row));
+        voff[j] = ((r0 + row) * ld + kc) * 4;
+        kof[j] = kc;
+      } else {
+        constexpr int PER = ROWS / 4;  // 16-B chunks per k-row
+        const int k = q * (256 / ROWS) + lane / PER;
+        const int n = (4 * (lane % PER)) ^ ((k & 1) << 4);
+        voff[j] = (k * ld + r0 + n) * 4;
+        kof[j] = k;
+      }
+    }
+  }
+  // this wave's DMAs of the k-tile at k0 into `img`; k >= kend reads 0
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, float* img, int w, int k0,
+                                        int kend, bool full, int ld) const {
+#pragma unroll
+    for (int j = 0; j < NWQ; ++j) {
+      int o = voff[j] + (KC ? k0 * 4 : k0 * ld * 4);
+      if (!full && k0 + kof[j] >= kend) o = OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(img + (w + 4 * j) * 256), 16, o, 0, 0, 0);
+    }
+  }
+  // image index of element (row, k = 4 kk + g)
+  __device__ static __forceinline__ int at(int row, int kk, int g) {
+    if constexpr (KC) return row * BK + 4 * (kk ^ kcs<BK>(row)) + g;
+    else return (4 * kk + g) * ROWS + (row ^ ((g & 1) << 4));
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int BK, int NS, bool TA, bool TB, int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_f32_dma_kernel(GemmPtrs P, GemmDims D) {
+#pragma clang fp contract(off)
+  constexpr int MI = BM / 32, NI = BN / 32, KK = BK / 4;
+  constexpr int A_SZ = BM * BK, STAGE = (BM + BN) * BK;  // floats
+  using OpA = DmaOperand<BM, !TA, BK>;
+  using OpB = DmaOperand<BN, TB, BK>;
+  constexpr int DPT = OpA::NWQ + OpB::NWQ;  // DMA instructions per wave per k-tile
+  __shared__ __attribute__((aligned(1024))) float lds[NS * STAGE];
+  const int nwg = gridDim.x * gridDim.y * gridDim.z;
+  const int wg = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nwg);
+  const int bx = wg % D.nx, by = (wg / D.nx) % D.ny, bz = wg / (D.nx * D.ny);
+  const int z = bz / D.splitk, ks = bz - z * D.splitk;
+  const int m0 = by * BM, n0 = bx * BN;
+  const int kbeg = ks * D.kchunk;
+  const int kend = min(D.K, kbeg + D.kchunk);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
+  const int M = D.M, N = D.N;
+  float* colsum = P.colsum[z];
+  const bool do_cs = colsum != nullptr && by == 0 && t < BN;
+  float cs = 0.0f;
+
+  floatx4 acc[MI][NI];
+  const float* Cin = P.Cin[z];
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm + mi * 16 + (lane >> 4) * 4 + r;
-        const int col = n0 + wn + ni * 16 + (lane & 15);
-        if (row >= M || col >= N) continue;
-        const size_t o = (size_t)row * D.ldc + col;
-        float v = acc[mi][ni][r];
-        if (EPI == EPI_ATOMIC) {
-          atomicAdd(C + o, v);
-          continue;
+        float v = 0.0f;
+        if (Cin != nullptr && ks == 0) {
+          const int row = m0 + wm + mi * 16 + (lane >> 4) * 4 + r;
+          const int col = n0 + wn + ni * 16 + (lane & 15);
+          if (row < M && col < N) v = Cin[(size_t)row * D.ldc + col];
         }
-        if (EPI == EPI_SOFTPLUS_BWD) {
-          C[o] = v * mog_sigmoidf(aux[(size_t)row * D.ldaux + col]);
-          continue;
-        }
-        if (EPI == EPI_RELU_BWD) {
-          C[o] = aux[(size_t)row * D.ldaux + col] > 0.0f ? v : 0.0f;
-          continue;
-        }
-        if (bias != nullptr) v = v + bias[col];
-        if (EPI == EPI_STORE) {
-          C[o] = v;
-        } else {
-          if (Cpre != nullptr) Cpre[o] = v;
-          if (EPI == EPI_RELU) C[o] = v > 0.0f ? v : 0.0f;
-          if (EPI == EPI_SOFTPLUS) C[o] = mog_softplusf(v);
-          if (EPI == EPI_SIGMOID_NOISE)
-            C[o] = mog_sigmoidf(v + aux[(size_t)row * D.ldaux + col] * D.aux_scale);
-        }
+        acc[mi][ni][r] = v;
       }
+
+  const long extA = TA ? (long)(D.K - 1) * D.lda + M : (long)(M - 1) * D.lda + D.K;
+  const long extB = TB ? (long)(N - 1) * D.ldb + D.K : (long)(D.K - 1) * D.ldb + N;
+  const __amdgpu_buffer_rsrc_t ra = frsrc(P.A[z], extA);
+  const __amdgpu_buffer_rsrc_t rb = frsrc(P.B[z], extB);
+  OpA da;
+  OpB db;
+  da.init(w, lane, m0, D.lda);
+  db.init(w, lane, n0, D.ldb);
+
+  const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
+  auto issue = [&](int j, int stage) {
+    const int k0 = kbeg + j * BK;
+    const bool full = k0 + BK <= kend;
+    float* st = lds + stage * STAGE;
+    da.issue(ra, st, w, k0, kend, full, D.lda);
+    db.issue(rb, st + A_SZ, w, k0, kend, full, D.ldb);
+  };
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < nk) issue(j, j);
+
+  const int fr = lane & 15, fg = lane >> 4;
+  // fragment registers: FP = 2 sets (tile it+1's fragments are read from LDS
+  // while tile it's MFMAs run), FP = 1 set (read after the barrier)
+  constexpr int FP = NS >= 4 ? 2 : 1;
+  float fa[FP][KK][MI], fb[FP][KK][NI];
+  auto read_frags = [&](int stage, auto fs) {
+    constexpr int F = decltype(fs)::value;
+    const float* As = lds + stage * STAGE;
+    const float* Bs = As + A_SZ;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) fa[F][kk][mi] = As[OpA::at(wm + mi * 16 + fr, kk, fg)];
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) fb[F][kk][ni] = Bs[OpB::at(wn + ni * 16 + fr, kk, fg)];
+    }
+    if constexpr (!TB) {
+      if (do_cs) {
+#pragma unroll
+        for (int k = 0; k < BK; ++k) cs += Bs[k * BN + (t ^ ((k & 1) << 4))];
+      }
+    }
+  };
+  auto mfmas = [&](auto fs) {
+    constexpr int F = decltype(fs)::value;
+    // k = 4 kk + g: MFMA kk consumes k-slots 4kk..4kk+3 in order
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[F][kk][mi], fb[F][kk][ni],
+                                                             acc[mi][ni], 0, 0, 0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  auto next = [](int s) { return s == NS - 1 ? 0 : s + 1; };
+  if constexpr (FP == 1) {
+    int st = 0;  // stage of tile it
+    for (int it = 0; it < nk; ++it) {
+      // this wave's DMAs of tile it have landed (NS-2 later tiles may stay in
+      // flight), then every wave's have, and every wave is done reading the
+      // stage the next DMA overwrites (tile it-1's)
+      if (it + NS - 2 < nk) wait_vm<DPT * (NS - 2)>();
+      else wait_vm<0>();
+      asm volatile("s_barrier" ::: "memory");
+      if (it + NS - 1 < nk) issue(it + NS - 1, st == 0 ? NS - 1 : st - 1);
+      read_frags(st, I0{});
+      mfmas(I0{});
+      st = next(st);
+    }
+  } else {
+    // iteration it: tile it+1 has landed everywhere (NS-3 later tiles stay in
+    // flight); tile it's fragments are in registers (read in iteration
+    // it-1); the DMA of tile it+NS-1 overwrites tile it-1's stage, whose
+    // fragment reads every wave completed before this barrier
+    if (nk > 0) {
+      if (NS - 2 < nk) wait_vm<DPT * (NS - 2)>();
+      else wait_vm<0>();
+      asm volatile("s_barrier" ::: "memory");
+      read_frags(0, I0{});
+    }
+    int st = 0;
+    auto body = [&](int it, auto fs) {
+      constexpr int F = decltype(fs)::value;
+      if (it + 1 < nk) {
+        if (it + NS - 2 < nk) wait_vm<DPT * (NS - 3)>();
+        else wait_vm<0>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (it + NS - 1 < nk) issue(it + NS - 1, st == 0 ? NS - 1 : st - 1);
+      if (it + 1 < nk) read_frags(next(st), std::integral_constant<int, 1 - F>{});
+      mfmas(fs);
+      st = next(st);
+    };
+    for (int it = 0; it < nk; it += 2) {
+      body(it, I0{});
+      if (it + 1 < nk) body(it + 1, I1{});
+    }
+  }
+  if (do_cs && n0 + t < N) atomicAdd(colsum + n0 + t, cs);
+
+  store_tile<MI, NI, EPI>(acc, P, D, z, m0 + wm, n0 + wn, lane);
 }
 
 template <int BM, int BN, int BK, int PF, bool TA, bool TB, bool KS>
@@ -397,18 +630,77 @@ void launch_tile(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, Ge
   else launch_epi<BM, BN, BK, PF, true, true, false>(epi, g, s, P, D);
 }
 
+template <int BM, int BN, int BK, int NS, bool TA, bool TB>
+void launch_dma_epi(int epi, dim3 g, hipStream_t s, const GemmPtrs& P, const GemmDims& D) {
+#define MOG_GEMM_LAUNCH(E) gemm_f32_dma_kernel<BM, BN, BK, NS, TA, TB, E><<<g, 256, 0, s>>>(P, D)
+  switch (epi) {
+    case EPI_STORE: MOG_GEMM_LAUNCH(EPI_STORE); break;
+    case EPI_RELU: MOG_GEMM_LAUNCH(EPI_RELU); break;
+    case EPI_SOFTPLUS: MOG_GEMM_LAUNCH(EPI_SOFTPLUS); break;
+    case EPI_SIGMOID_NOISE: MOG_GEMM_LAUNCH(EPI_SIGMOID_NOISE); break;
+    case EPI_SOFTPLUS_BWD: MOG_GEMM_LAUNCH(EPI_SOFTPLUS_BWD); break;
+    case EPI_ATOMIC: MOG_GEMM_LAUNCH(EPI_ATOMIC); break;
+    case EPI_RELU_BWD: MOG_GEMM_LAUNCH(EPI_RELU_BWD); break;
+  }
+#undef MOG_GEMM_LAUNCH
+}
+
+template <int BM, int BN, int BK, int NS>
+void launch_dma(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, GemmDims D,
+                int batch) {
+  int kchunk = (D.K + D.splitk - 1) / D.splitk;
+  kchunk = ((kchunk + BK - 1) / BK) * BK;
+  if (kchunk == 0) kchunk = BK;
+  D.kchunk = kchunk;
+  D.splitk = (D.K + kchunk - 1) / kchunk;
+  if (D.splitk < 1) D.splitk = 1;
+  D.nx = mog_cdiv(D.N, BN);
+  D.ny = mog_cdiv(D.M, BM);
+  dim3 g(D.nx, D.ny, batch * D.splitk);
+  if (!ta && !tb) launch_dma_epi<BM, BN, BK, NS, false, false>(epi, g, s, P, D);
+  else if (!ta && tb) launch_dma_epi<BM, BN, BK, NS, false, true>(epi, g, s, P, D);
+  else if (ta && !tb) launch_dma_epi<BM, BN, BK, NS, true, false>(epi, g, s, P, D);
+  else launch_dma_epi<BM, BN, BK, NS, true, true>(epi, g, s, P, D);
+}
+
 // Tile shape (measured on MI355X, scripts/bench_gemm_f32.py):
 // 64x64 (2x2 waves of 32x32) wins on every train-step shape except the long-K
 // x-projection (K = 2500), where 128x128 keeps more MFMAs per barrier and
-// still gives every CU two workgroups.  Measured and not kept: BK = 32 (-5..-25 %
-// on every shape), a second register prefetch set (PF = 2: within +-2 %),
-// 128x64 / 64x128 tiles.  MOG_GEMM_TILE ("64" / "128") forces a tile.
+// still gives every CU two workgroups.  Operands that allow it go through the
+// LDS-DMA kernel (x-projection 457 -> 379 us, its gradient 385 -> 369 us,
+// the dh GEMM 65 -> 49 us against register staging); register staging
+// remains for unaligned / K % 4 operands and K segments.  Measured and not
+// kept: BK = 32 (register staging -5..-25 %, LDS-DMA -3..-20 % on most
+// shapes), 128x64 / 64x128 tiles, a 3-stage register pipeline with fragment
+// prefetch (1 wave per SIMD at 128x128).  MOG_GEMM_TILE ("64" / "128")
+// forces a tile, MOG_GEMM_DMA=0 the register-staged kernel.
 void launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, const GemmDims& D,
                  int batch) {
   static const char* force = getenv("MOG_GEMM_TILE");
   const long big = (long)mog_cdiv(D.M, 128) * mog_cdiv(D.N, 128) * batch * D.splitk;
   bool b128 = !ta && D.K >= 2048 && D.M >= 128 && D.N >= 128 && big >= 512;
   if (force != nullptr) b128 = atoi(force) == 128;
+  // LDS-DMA form: 16-B source chunks must be aligned and lie wholly inside or
+  // outside the k range and the operand's last row (K % 4 for k-contiguous
+  // operands, M / N % 4 for row-contiguous ones); no K segments; the fused
+  // bias-gradient column sum only from a row-contiguous B
+  static const char* dma_env = getenv("MOG_GEMM_DMA");
+  const bool dma = (dma_env == nullptr || atoi(dma_env) != 0) && D.kseg == 0 && D.vecA &&
+                   D.vecB && (ta ? D.M % 4 == 0 : D.K % 4 == 0) &&
+                   (tb ? D.K % 4 == 0 : D.N % 4 == 0) && !(tb && P.colsum[0] != nullptr);
+  if (dma) {
+    // stages (measured, scripts/bench_gemm_f32.py): 4 with fragment
+    // double-buffering for the split-K weight gradients (transA), 3 for the
+    // rest, where a fifth/sixth workgroup per CU beats the deeper pipeline
+    if (b128) {
+      if (ta) launch_dma<128, 128, 16, 4>(ta, tb, epi, s, P, D, batch);
+      else launch_dma<128, 128, 16, 3>(ta, tb, epi, s, P, D, batch);
+    } else {
+      if (ta) launch_dma<64, 64, 16, 4>(ta, tb, epi, s, P, D, batch);
+      else launch_dma<64, 64, 16, 3>(ta, tb, epi, s, P, D, batch);
+    }
+    return;
+  }
   if (b128) launch_tile<128, 128, 16, 1>(ta, tb, epi, s, P, D, batch);
   else launch_tile<64, 64, 16, 1>(ta, tb, epi, s, P, D, batch);
 }
