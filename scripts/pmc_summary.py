@@ -37,11 +37,11 @@ def _x_grad_grid_fp32(B, C2=2500, N=1024, target=2048):
 
 # tag -> (kernel symbol substring, grid work-items)
 TAGS = {
-    "lstm_x_projection_fp32_b%d" % B: ("gemm_f32_kernel<128, 128, 16, 1, false, false, 0, false>",
+    "lstm_x_projection_fp32_b%d" % B: ("gemm_f32_dma_kernel<128, 128, 16, 3, false, false, 0>",
                                        (1024 // 128) * (B // 128) * 256),
-    "lstm_x_projection_grad_fp32_b%d" % B: ("gemm_f32_kernel<64, 64, 16, 1, true, false, 5, false>",
+    "lstm_x_projection_grad_fp32_b%d" % B: ("gemm_f32_dma_kernel<64, 64, 16, 4, true, false, 5>",
                                             _x_grad_grid_fp32(B)),
-    "lstm_x_projection_bf16_b%d" % B: ("gemm_f32_kernel<128, 128, 16, 1, false, false, 0, false>",
+    "lstm_x_projection_bf16_b%d" % B: ("gemm_f32_dma_kernel<128, 128, 16, 3, false, false, 0>",
                                        (1024 // 128) * (B // 128) * 256),
     "stn_vae_step_bf16_b%d" % B: ("stn_vae_step", B // 32 * 1024),
     "stn_vae_step_b65536": ("stn_vae_step", 65536 // 64 * 1024),
