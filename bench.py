@@ -61,6 +61,8 @@ def kernel_work(name, B, precision, C2=2500, H=256, T=3):
         return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", peak
     if name == "stn_vae_step":
         return "hbm", B * fused_bytes_per_image_step(C2) / 1e9, "GB/s", HBM_PEAK_GBS
+    if name == "stn_vae_step_all":           # all T steps' rows in one launch
+        return "hbm", T * B * fused_bytes_per_image_step(C2) / 1e9, "GB/s", HBM_PEAK_GBS
     return None
 
 

@@ -91,7 +91,8 @@ int mog_lstm_cell_backward(const float* G, const float* bias, const float* c_pre
  * :552-577 (theta^-1), :590-663 (concrete z_pres, KL, stop/digits),
  * :677-705 (scale/shift KLs), loop predicate :428-432 via live[step+1].
  * hid/w2/b2: HOST arrays of 5 device pointers (scale-mean, scale-logvar,
- * shift-mean, shift-logvar, z_pres log-odds). rec: [16, B] saved records. */
+ * shift-mean, shift-logvar, z_pres log-odds). rec: [17, B] saved records
+ * (slot 16: the z_pres KL term this step added to runloss, for mog_air_runloss). */
 int mog_air_step_forward(int B, int HS, int HZ, int step, int train, int use_num_prior,
                          float thr, float temperature, float prior_lo, float prior_bias,
                          float s_pm, float s_pv, float s_plv, float h_pm, float h_pv, float h_plv,
@@ -113,10 +114,20 @@ int mog_air_step_backward(int B, int HS, int train, int use_num_prior, float tem
                           long dhid_hs, void* stream);
 
 /* ---- VAE latent sample + KL (air/vae.py:27-30, air_model.py:718-736) ----
- * z_bf16 (may be NULL): bf16 copy of z with row stride ld_zb (GEMM operand). */
+ * z_bf16 (may be NULL): bf16 copy of z with row stride ld_zb (GEMM operand).
+ * runloss may be NULL (vkl only; mog_air_runloss adds it later). */
 int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, float v_plv, const float* mu,
                            const float* lv, const float* eps, float* z, void* z_bf16, int ld_zb,
                            const float* act, float* runloss, float* vkl, void* stream);
+/* Per-image running loss of T steps replayed from the records in the order the
+ * loop accumulates it (air_model.py:622-736: per step the z_pres term, then,
+ * for an active image, scale KL, shift KL, VAE KL), starting from +0:
+ * bit-identical to accumulating step by step.  rec: [T][rec_step_stride]
+ * (mog_air_step_forward records), skl/shkl/vkl: [T, B].  Lets the VAE of all
+ * T steps run after the recurrent loop as one set of launches over T*B rows
+ * (AIR: the VAE output never feeds the recurrence). */
+int mog_air_runloss(int T, int B, const float* rec, long rec_step_stride, const float* skl,
+                    const float* shkl, const float* vkl, float* runloss, void* stream);
 /* ---- fused per-object step, bf16 configuration ----
  * One launch per loop step: glimpse = STN(x, theta_f) (transformer.py:18-175),
  * the glimpse VAE (vae.py:5-48: recognition 784->512->256 softplus, mean /
@@ -136,7 +147,10 @@ int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, float v_plv, co
  * backward: gb/a1b/a2b/zb/d1b/d2b (bf16, zb row stride 56), mu/lv/z/r (fp32).
  * Shapes must be the reference defaults (W 28, 512/256, Z 50, 256/512):
  * anything else returns MOG_ERR_INVALID.  Replaces the per-step sequence
- * air_model.py:523-588 (stn_forward + 6 GEMMs + vae_sample + stn accumulate). */
+ * air_model.py:523-588 (stn_forward + 6 GEMMs + vae_sample + stn accumulate).
+ * x_period > 0 (all T steps in one launch: B = T * x_period rows, row b reads
+ * image x[b % x_period]) requires x_period % 64 == 0 and runloss == NULL;
+ * x_period <= 0 means B. */
 int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int Z, int G1, int G2,
                              const float* x, const float* theta_f, const float* theta_b,
                              const float* mask, const float* zval, const float* eps_z,
@@ -146,7 +160,7 @@ int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int Z, int G1,
                              float v_plv, float* canvas_part, int* part_rows, float* runloss,
                              float* vkl, void* gb,
                              void* a1b, void* a2b, float* mu, float* lv, float* z, void* zb,
-                             void* d1b, void* d2b, float* r, void* stream);
+                             void* d1b, void* d2b, float* r, int x_period, void* stream);
 
 /* dmu/dlv fp32 [B,Z] and/or bf16 copies with row stride ld_b (any may be NULL,
  * but one complete pair must be given). */

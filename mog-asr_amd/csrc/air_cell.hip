@@ -85,7 +85,7 @@ struct StepCfg {
 // record slots [NREC][B] per step
 enum {
   R_SM, R_SLV, R_HM0, R_HM1, R_HLV0, R_HLV1, R_LO, R_S, R_TX, R_TY, R_Y, R_Z,
-  R_ACT_OLD, R_ACT, R_LIVE, R_ZC, R_NREC
+  R_ACT_OLD, R_ACT, R_LIVE, R_ZC, R_ZTERM, R_NREC
 };
 
 struct HeadPtrs {
@@ -204,7 +204,9 @@ __global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp,
   const float stop_old = io.stop[b];
   const bool act_old = stop_old < cfg.thr;
   float rl = io.runloss[b];
-  if (live) rl = rl + (act_old ? zkl : kl_end);
+  // the z_pres term this step adds (recorded: mog_air_runloss replays the sum)
+  const float zterm = live ? (act_old ? zkl : kl_end) : 0.0f;
+  if (live) rl = rl + zterm;
   io.zkl_out[b] = zkl;
 
   // stopping sum, digit count, live flag for the next step (:428-432, :659-663)
@@ -239,6 +241,7 @@ __global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp,
   r[R_ACT * B + b] = act ? 1.0f : 0.0f;
   r[R_LIVE * B + b] = live ? 1.0f : 0.0f;
   r[R_ZC * B + b] = act ? z : 0.0f;
+  r[R_ZTERM * B + b] = zterm;
   if (io.zc) io.zc[b] = act ? z : 0.0f;
 }
 
@@ -372,7 +375,32 @@ __global__ __launch_bounds__(256) void vae_sample_fwd_kernel(VaeCfg c, const flo
   for (int q = 0; q < c.Z; ++q) sum = sum + terms[w][q];
   const float vkl = 0.5f * sum;
   vkl_out[b] = vkl;
-  if (act[b] != 0.0f) runloss[b] = runloss[b] + vkl;
+  if (runloss && act[b] != 0.0f) runloss[b] = runloss[b] + vkl;
+}
+
+// Per-image running loss of all T steps replayed from the step records in the
+// order the step kernels accumulate it (step_fwd_kernel, then the VAE KL):
+// for the VAE of every step run after the loop (AIR, all T*B rows at once).
+__global__ __launch_bounds__(256) void runloss_kernel(int T, int B, const float* __restrict__ rec,
+                                                      long rstride, const float* __restrict__ skl,
+                                                      const float* __restrict__ shkl,
+                                                      const float* __restrict__ vkl,
+                                                      float* runloss) {
+#pragma clang fp contract(off)
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  float rl = 0.0f;
+  for (int t = 0; t < T; ++t) {
+    const float* r = rec + t * rstride;
+    rl = rl + r[R_ZTERM * B + b];
+    if (r[R_ACT * B + b] != 0.0f) {
+      const size_t i = (size_t)t * B + b;
+      rl = rl + skl[i];
+      rl = rl + shkl[i];
+      rl = rl + vkl[i];
+    }
+  }
+  runloss[b] = rl;
 }
 
 __global__ __launch_bounds__(256) void vae_sample_bwd_kernel(VaeCfg c, const float* mu,
@@ -634,12 +662,23 @@ extern "C" int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, floa
                                       const float* mu, const float* lv, const float* eps,
                                       float* z, void* z_bf16, int ld_zb, const float* act,
                                       float* runloss, float* vkl, void* stream) {
-  MOG_CHECK_ARG(B >= 0 && Z > 0 && Z <= 64 && mu && lv && eps && z && act && runloss && vkl);
+  MOG_CHECK_ARG(B >= 0 && Z > 0 && Z <= 64 && mu && lv && eps && z && act && vkl);
   MOG_CHECK_ARG(!z_bf16 || ld_zb >= Z);
   if (B == 0) return 0;
   VaeCfg c{B, Z, v_pm, v_pv, v_plv, 0.0f};
   vae_sample_fwd_kernel<<<mog_cdiv(B, 4), 256, 0, mog_stream(stream)>>>(
       c, mu, lv, eps, z, reinterpret_cast<__bf16*>(z_bf16), ld_zb, act, runloss, vkl);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_air_runloss(int T, int B, const float* rec, long rec_step_stride,
+                               const float* skl, const float* shkl, const float* vkl,
+                               float* runloss, void* stream) {
+  MOG_CHECK_ARG(T >= 1 && B >= 0 && rec && skl && shkl && vkl && runloss);
+  MOG_CHECK_ARG(rec_step_stride >= (long)R_NREC * B);
+  if (B == 0) return 0;
+  runloss_kernel<<<mog_cdiv(B, 256), 256, 0, mog_stream(stream)>>>(T, B, rec, rec_step_stride,
+                                                                   skl, shkl, vkl, runloss);
   MOG_LAUNCH_RET();
 }
 

@@ -223,6 +223,79 @@ __device__ __forceinline__ void bwd_pixels(const float* th, int Hin, int Win, in
   }
 }
 
+// Axis-aligned transform, 32 < Wout <= 64 (one output row per pass: the STN
+// write backward, canvas -> glimpse): every live cotangent row of the lane's
+// column is loaded up front into registers gv[] (one memory latency per
+// image instead of one per 4-row batch), the row bodies then run from
+// registers, and gv[] stays live for the separable dU pass (lanes exchange
+// it with ds_bpermute, no second read of the cotangent).  The per-row body,
+// its order and its masks are bwd_pixels<true, DU>'s.
+constexpr int GV = 64;  // rows held per lane (Hout <= 64)
+template <int DU>
+__device__ __forceinline__ void bwd_rows_reg(const float* th, int Hin, int Win, int Hout,
+                                             int Wout, const float* __restrict__ Gn, float sc,
+                                             bool grads, bool want_dot, const float* sU,
+                                             float4* coltab, const float4* rowtab, float* a,
+                                             float (&gv)[GV], int& ilo_out, int& ihi_out) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const float wm2 = ((float)Win - 1.001f) / 2.0f;
+  const float hm2 = ((float)Hin - 1.001f) / 2.0f;
+  const float ystep = Hout > 1 ? 2.0f / (float)(Hout - 1) : 0.0f;
+  const float4 ry = rowtab[min(lane, Hout - 1)];
+  const unsigned long long lm = __builtin_amdgcn_ballot_w64(
+      lane < Hout && __float_as_int(ry.x) != __float_as_int(ry.y));
+  const int ilo = lm ? __builtin_ctzll(lm) : 0;
+  const int ihi = lm ? 64 - __builtin_clzll(lm) : 0;
+  ilo_out = ilo;
+  ihi_out = ihi;
+  const int j = lane;
+  const bool jv = j < Wout;
+  const int jc = jv ? j : Wout - 1;
+  const float xt = mog_linspace(jc, Wout);
+  const float4 ex = axis4(axis_col(th, Hin, Win, Hout, Wout, jc), 1);
+  if (DU == 1 && jv) coltab[j] = ex;
+  // all live rows' cotangent (clamped rows: unpredicated loads), 16 per chunk
+#pragma unroll
+  for (int c = 0; c < GV / 16; ++c) {
+    if (16 * c < ihi - ilo) {
+#pragma unroll
+      for (int r = 16 * c; r < 16 * c + 16; ++r) gv[r] = Gn[min(ilo + r, Hout - 1) * Wout + jc];
+    }
+  }
+  const int x0 = __float_as_int(ex.x), x1 = __float_as_int(ex.y);
+  const float ax = ex.z, bx = ex.w;
+  float sdx = 0.0f, sdy = 0.0f;
+#pragma unroll
+  for (int r = 0; r < GV; ++r) {
+    const int i = ilo + r;
+    if (i >= ihi) break;
+    const float yt = Hout == 1 ? -1.0f : (i == Hout - 1 ? 1.0f : -1.0f + ystep * (float)i);
+    const float4 ey = make_float4(
+        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.x), i)),
+        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.y), i)),
+        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.z), i)),
+        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.w), i)));
+    const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
+    const bool dead = x0 == x1 && y0 == y1;
+    const bool degen = x0 == x1 || y0 == y1;
+    const float Ia = sU[y0 + x0], Ib = sU[y1 + x0], Ic = sU[y0 + x1], Id = sU[y1 + x1];
+    const float gout = gv[r];
+    const float pv = gout * sample4(ex, ey, Ia, Ib, Ic, Id);
+    a[6] += (want_dot && jv && !dead) ? pv : 0.0f;
+    const float g0 = gout * sc;
+    const bool use = jv && grads && !degen && g0 != 0.0f;
+    const float g = use ? g0 : 0.0f;
+    const float ay = ey.z, by = ey.w;
+    const float dx = g * (ay * (Ic - Ia) + by * (Id - Ib)) * wm2;
+    const float dy = g * (ax * (Ib - Ia) + bx * (Id - Ic)) * hm2;
+    sdx += dx; a[1] += dx * yt;
+    sdy += dy; a[4] += dy * yt;
+  }
+  a[0] += sdx * xt; a[2] += sdx;
+  a[3] += sdy * xt; a[5] += sdy;
+}
+
 // floats of one wave's LDS slice (max over the atomic and separable layouts)
 __host__ __device__ inline int stn_bwd_slice(int Hin, int Win, int Hout, int Wout, bool dU) {
   const int hw4 = (Hin * Win + 3) & ~3;
@@ -284,7 +357,18 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
   float a[7] = {0, 0, 0, 0, 0, 0, 0};
   const float* Gn = G + (size_t)(g_period > 0 ? n % g_period : n) * P;
   const int mode = __builtin_amdgcn_readfirstlane((sep ? 1 : 0) | (sdu ? 2 : 0) | (want_dU ? 4 : 0));
-  if (mode == 3 || mode == 7)
+  // rows in registers: axis-aligned, one output row per pass, separable or no dU
+  const bool regs = sep && Wout > 32 && Wout <= 64 && (mode == 1 || mode == 3 || mode == 7);
+  float gv[GV];
+  int rlo = 0, rhi = 0;
+  if (regs) {
+    if (mode == 1)
+      bwd_rows_reg<0>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, coltab, rowtab,
+                      a, gv, rlo, rhi);
+    else
+      bwd_rows_reg<1>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, coltab, rowtab,
+                      a, gv, rlo, rhi);
+  } else if (mode == 3 || mode == 7)
     bwd_pixels<true, 1>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, sD, sg, coltab, rowtab, a);
   else if (mode == 5)
     bwd_pixels<true, 2>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, sD, sg, coltab, rowtab, a);
@@ -376,6 +460,47 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
         __builtin_amdgcn_readfirstlane(P * 4), 0x00020000);
     const int tlo = lmr ? (__builtin_ctzll(lmr) / rpi) * rpi : Hout;
     const int thi = lmr ? 64 - __builtin_clzll(lmr) : Hout;
+    if (regs) {
+      // T[i][u] = sum_{j = jlo(u)..jhi(u)} g[i][j] w_j(u), j ascending (the order
+      // of the loop below); lane j's g[i][j] arrives by ds_bpermute, so every
+      // lane takes part in each exchange and lanes u >= Win discard theirs.
+      // The live rows [rlo, rhi) are exactly [tlo, thi) for one row per pass.
+      constexpr int JM = 8;  // canvas columns per source column (<= 8: scale <= ~2)
+      const bool uact = ul < Win && half == 0;
+      const int nj = uact ? jhi - jlo + 1 : 0;
+      int jmax = nj;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) jmax = max(jmax, __shfl_xor(jmax, o, 64));
+      jmax = __builtin_amdgcn_readfirstlane(jmax);
+      if (jmax <= JM) {
+        float wj[JM];
+        int src[JM];
+#pragma unroll
+        for (int d = 0; d < JM; ++d) {
+          const int jj = min(jlo + d, Wout - 1);
+          const float4 e = coltab[max(jj, 0)];
+          wj[d] = d < nj ? (__float_as_int(e.x) == ul ? e.z : e.w) : 0.0f;
+          src[d] = max(jj, 0) * 4;
+        }
+#pragma unroll
+        for (int r = 0; r < GV; ++r) {
+          if (rlo + r >= rhi) break;
+          const float g0 = gv[r] * sc;
+          const float gt = grads && g0 != 0.0f ? g0 : 0.0f;
+          float acc = 0.0f;
+#pragma unroll
+          for (int d = 0; d < JM; ++d) {
+            if (d >= jmax) break;
+            const float gj = __int_as_float(__builtin_amdgcn_ds_bpermute(src[d], __float_as_int(gt)));
+            if (d < nj) acc += gj * wj[d];
+          }
+          if (uact) sT[(rlo + r) * Win + ul] = acc;
+        }
+        wave_sync();
+        TS(3);
+        goto du_pass;
+      }
+    }
     if (ul < Win) {
       constexpr int RMAX = 32;  // rows per lane (ceil(Hout / rpi) <= 32, see sdu)
       constexpr int RC = 16;    // rows per chunk (register budget: occupancy)
@@ -412,6 +537,7 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
     }
     wave_sync();
     TS(3);
+  du_pass:
     // dU[v][u] = sum_i T[i][u] * (y0(i) == v ? y1 - y : y - y0)
     if (ul < Win)
       for (int v = half; v < Hin; v += rpi) {

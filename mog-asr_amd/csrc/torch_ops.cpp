@@ -198,10 +198,17 @@ void air_step_backward_(int64_t B, int64_t HS, bool train, bool use_num_prior,
 void vae_sample_forward_(int64_t B, int64_t Z, double v_pm, double v_pv, double v_plv,
                          const Tensor& mu, const Tensor& lv, const Tensor& eps, Tensor z,
                          const optional<Tensor>& z_bf16, int64_t ld_zb, const Tensor& act,
-                         Tensor runloss, Tensor vkl) {
+                         const optional<Tensor>& runloss, Tensor vkl) {
   check(mog_vae_sample_forward(B, Z, v_pm, v_pv, v_plv, f(mu), f(lv), f(eps), f(z), p(z_bf16),
                                ld_zb, f(act), f(runloss), f(vkl), stream()),
         "vae_sample_forward_");
+}
+
+void air_runloss_(int64_t T, int64_t B, const Tensor& rec, int64_t rec_step_stride,
+                  const Tensor& skl, const Tensor& shkl, const Tensor& vkl, Tensor runloss) {
+  check(mog_air_runloss(T, B, f(rec), rec_step_stride, f(skl), f(shkl), f(vkl), f(runloss),
+                        stream()),
+        "air_runloss_");
 }
 
 void vae_sample_backward_(int64_t B, int64_t Z, double v_pm, double v_pv, double grad_scale,
@@ -224,8 +231,9 @@ void stn_vae_step_(int64_t B, int64_t C, const Tensor& x, const Tensor& theta_f,
                    const Tensor& eps_z, const optional<Tensor>& eps_x, int64_t eps_seed,
                    int64_t eps_offset, bool eps_gen, at::TensorList wt, at::TensorList bias,
                    double lik_std, double v_pm, double v_pv, double v_plv, Tensor canvas_part,
-                   Tensor part_rows, Tensor runloss, Tensor vkl, Tensor gb, Tensor a1b, Tensor a2b,
-                   Tensor mu, Tensor lv, Tensor z, Tensor zb, Tensor d1b, Tensor d2b, Tensor r) {
+                   Tensor part_rows, const optional<Tensor>& runloss, Tensor vkl, Tensor gb,
+                   Tensor a1b, Tensor a2b, Tensor mu, Tensor lv, Tensor z, Tensor zb, Tensor d1b,
+                   Tensor d2b, Tensor r, int64_t x_period) {
   auto w = ptrs(wt), b = ptrs(bias);
   TORCH_CHECK(w.size() == 7 && b.size() == 7, "stn_vae_step_: 7 VAE layers");
   check(mog_stn_vae_step_forward(B, C, 28, 512, 256, 50, 256, 512, f(x), f(theta_f), f(theta_b),
@@ -234,7 +242,7 @@ void stn_vae_step_(int64_t B, int64_t C, const Tensor& x, const Tensor& theta_f,
                                  arr<void>(w), arr<float>(b), lik_std, v_pm, v_pv, v_plv,
                                  f(canvas_part), static_cast<int*>(p(part_rows)), f(runloss),
                                  f(vkl), p(gb), p(a1b), p(a2b), f(mu), f(lv), f(z), p(zb), p(d1b),
-                                 p(d2b), f(r), stream()),
+                                 p(d2b), f(r), x_period, stream()),
         "stn_vae_step_");
 }
 
@@ -329,7 +337,10 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
   m.def(
       "vae_sample_forward_(int B, int Z, float v_pm, float v_pv, float v_plv, Tensor mu, "
       "Tensor lv, Tensor eps, Tensor(a!) z, Tensor? z_bf16, int ld_zb, Tensor act, "
-      "Tensor(b!) runloss, Tensor(c!) vkl) -> ()");
+      "Tensor(b!)? runloss, Tensor(c!) vkl) -> ()");
+  m.def(
+      "air_runloss_(int T, int B, Tensor rec, int rec_step_stride, Tensor skl, Tensor shkl, "
+      "Tensor vkl, Tensor(a!) runloss) -> ()");
   m.def(
       "vae_sample_backward_(int B, int Z, float v_pm, float v_pv, float grad_scale, Tensor mu, "
       "Tensor lv, Tensor eps, Tensor dz, Tensor act, Tensor? dmu, Tensor? dlv, Tensor? dmu_bf16, "
@@ -339,9 +350,10 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "stn_vae_step_(int B, int C, Tensor x, Tensor theta_f, Tensor theta_b, Tensor mask, "
       "Tensor zval, Tensor eps_z, Tensor? eps_x, int eps_seed, int eps_offset, bool eps_gen, "
       "Tensor[] wt, Tensor[] bias, float lik_std, float v_pm, float v_pv, float v_plv, "
-      "Tensor(a!) canvas_part, Tensor(b!) part_rows, Tensor(c!) runloss, Tensor(d!) vkl, "
+      "Tensor(a!) canvas_part, Tensor(b!) part_rows, Tensor(c!)? runloss, Tensor(d!) vkl, "
       "Tensor(e!) gb, Tensor(f!) a1b, Tensor(g!) a2b, Tensor(h!) mu, Tensor(i!) lv, "
-      "Tensor(j!) z, Tensor(k!) zb, Tensor(l!) d1b, Tensor(m!) d2b, Tensor(n!) r) -> ()");
+      "Tensor(j!) z, Tensor(k!) zb, Tensor(l!) d1b, Tensor(m!) d2b, Tensor(n!) r, "
+      "int x_period=0) -> ()");
   m.def(
       "recon_loss_(Tensor x, Tensor? canvas, Tensor? parts, int nparts, int part_stride, "
       "Tensor? part_rows, int C, Tensor runloss, Tensor digits, Tensor? targets, int B, int C2, "
@@ -371,6 +383,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("air_step_backward_", &air_step_backward_);
   m.impl("vae_sample_forward_", &vae_sample_forward_);
   m.impl("vae_sample_backward_", &vae_sample_backward_);
+  m.impl("air_runloss_", &air_runloss_);
   m.impl("sigmoid_backward_", &sigmoid_backward_);
   m.impl("stn_vae_step_", &stn_vae_step_);
   m.impl("recon_loss_", &recon_loss_);

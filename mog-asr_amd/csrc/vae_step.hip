@@ -127,6 +127,7 @@ struct StepArgs {
   __bf16* d2b;               // [B, 512]
   float* r;                  // [B, 784]
   int B, C;
+  int x_period;             // image of row b is x[b % x_period] (all T steps in one launch)
   float lik_std, v_pm, v_pv, v_plv;
   int phases;               // profiling aid: bit mask of the phases to run (all by default)
   long long* tstamp;        // profiling aid: per-block phase timestamps (or null)
@@ -425,7 +426,7 @@ __device__ __forceinline__ void read_recognition(const StepArgs& p, unsigned cha
   };
   if (sampler) {
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(p.x) + (size_t)b0 * C2, 0, nb * C2 * 4, 0x00020000);
+        const_cast<float*>(p.x) + (size_t)(b0 % p.x_period) * C2, 0, nb * C2 * 4, 0x00020000);
     const int kk = lane & 31;
     const int mw = (wv - NW / 2) * (2 * M / NW) + (lane >> 5);
     // Per-lane LDS bases made opaque to the compiler, so that image u of the
@@ -725,7 +726,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
     for (int k = 0; k < 50; ++k) sum = sum + t[k];
     const float vkl = 0.5f * sum;
     p.vkl[b0 + m] = vkl;
-    if (smask[m]) p.runloss[b0 + m] = p.runloss[b0 + m] + vkl;
+    if (p.runloss && smask[m]) p.runloss[b0 + m] = p.runloss[b0 + m] + vkl;
   }
   STAMP(5);
   // ---- 6. d1 = softplus(z Wg1 + b)  [M x 256] (over mu | lv) ---------------
@@ -924,12 +925,13 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
                                         float v_pv, float v_plv, float* canvas_part,
                                         int* part_rows, float* runloss, float* vkl, void* gb,
                                         void* a1b, void* a2b, float* mu, float* lv, float* z,
-                                        void* zb, void* d1b, void* d2b, float* r, void* stream) {
+                                        void* zb, void* d1b, void* d2b, float* r, int x_period,
+                                        void* stream) {
   MOG_CHECK_ARG(B >= 0 && C >= 2 && C * C <= 16384);
   // the tile shapes are compiled for the reference's default VAE
   MOG_CHECK_ARG(W == 28 && R1 == 512 && R2 == 256 && Z == 50 && G1 == 256 && G2 == 512);
   MOG_CHECK_ARG(x && theta_f && theta_b && mask && zval && eps_z && (eps_x || eps_gen) && wt && bias);
-  MOG_CHECK_ARG(canvas_part && part_rows && runloss && vkl && gb && a1b && a2b && mu && lv && z && zb);
+  MOG_CHECK_ARG(canvas_part && part_rows && vkl && gb && a1b && a2b && mu && lv && z && zb);
   MOG_CHECK_ARG(d1b && d2b && r);
   if (B == 0) return 0;
   StepArgs p;
@@ -949,6 +951,7 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   const char* ph = getenv("MOG_VS_PHASES");
   p.phases = ph ? atoi(ph) : 31;
   p.B = B; p.C = C; p.lik_std = lik_std; p.v_pm = v_pm; p.v_pv = v_pv; p.v_plv = v_plv;
+  p.x_period = x_period > 0 ? x_period : B;
   // Tile height: 64 images per workgroup (one per CU) once the batch gives
   // every CU at least one such tile, else 32 so small batches still spread
   // over the chip (two 8-wave workgroups per CU).  MOG_VS_MT overrides: 4 =
@@ -959,6 +962,10 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
     if (v == 2 || v == 3 || v == 4) mt = v;
   }
   const int M = 16 * (mt == 3 ? 2 : mt);
+  // a tile must not straddle two periods of x (one descriptor per tile);
+  // several steps' rows in one launch also rule out the running loss
+  // (rows of one image would race on it: mog_air_runloss replays it)
+  MOG_CHECK_ARG(p.x_period == B || (p.x_period % M == 0 && !runloss));
   // MOG_VS_TIMING=1 (profiling aid): per-phase durations, averaged over
   // blocks, printed to stderr (synchronizes the stream)
   static long long* tbuf = nullptr;

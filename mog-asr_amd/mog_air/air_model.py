@@ -37,7 +37,7 @@ _ops = ops._ops  # torch.ops.mog_air (csrc/torch_ops.cpp)
 
 # step-record slots (air_cell.hip enum)
 R_SM, R_SLV, R_HM0, R_HM1, R_HLV0, R_HLV1, R_LO, R_S, R_TX, R_TY, R_Y, R_Z = range(12)
-R_ACT_OLD, R_ACT, R_LIVE, R_ZC, R_NREC = 12, 13, 14, 15, 16
+R_ACT_OLD, R_ACT, R_LIVE, R_ZC, R_ZTERM, R_NREC = 12, 13, 14, 15, 16, 17
 
 _SCOPES: Dict[str, ParamStore] = {}
 
@@ -200,7 +200,8 @@ class AIRModel:
                  cnn=True, cnn_filters=8, num_summary_images=60, train=False, reuse=False,
                  scope="air", annealing_schedules=None, generation_batch_size=64,
                  num_prior=None, *, device=None, seed: int = 1235, noise_seed: int = 1235,
-                 grad_world: int = 1, precision: str = "fp32", fused_step: bool = True):
+                 grad_world: int = 1, precision: str = "fp32", fused_step: bool = True,
+                 batch_vae: bool = True):
         if precision not in ("fp32", "bf16"):
             raise ValueError("precision must be 'fp32' (bit-exact parity) or 'bf16'")
         self.precision = precision
@@ -209,6 +210,8 @@ class AIRModel:
         self.fused_step = bool(fused_step) and precision == "bf16" and (
             windows_size == 28 and tuple(vae_recognition_units) == (512, 256)
             and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512))
+        # the glimpse VAE of all T steps after the loop, over T*B rows (AIR)
+        self.batch_vae = bool(batch_vae)
         if cnn:
             raise NotImplementedError(
                 "cnn=True (air_model.py:763-810) is outside the hot-path scope; the entry "
@@ -405,6 +408,7 @@ class AIRModel:
         temperature = self.hyper("z_pres_temperature")
         thr = self.hyper("stopping_threshold")
         lik_std = self.hyper("vae_likelihood_std")
+        batched = self._batched_vae(B)
         # hoisted x-projection of the LSTM input (input is loop-invariant in AIR)
         with self._timed("lstm_x_projection"):
             gemm([X], [Wx], [ws.Gx], B, 4 * H, C2, C2, 4 * H, 4 * H)
@@ -435,6 +439,8 @@ class AIRModel:
                 ws.zkl[t], ws.skl[t], ws.shkl[t], ws.zmask[t], ws.zval[t], ws.zc[t])
             if self.live_hook is not None:
                 self.live_hook(ws.live, t)
+            if batched:
+                continue
             if self.fused_step:
                 with self._timed("stn_vae_step"):
                     self._step_fused(X, ws, t, float(lik_std))
@@ -447,7 +453,96 @@ class AIRModel:
             # STN write + masked canvas accumulation (air_model.py:580-588, 665-675)
             ops.stn_forward(ws.r[t], ws.th_b[t], (C, C), out=ws.canvas, z=ws.zval[t],
                             mask=ws.zmask[t], accumulate=True)
+        if batched:
+            self._vae_forward_all(X, ws, float(lik_std))
+            # the running loss in the loop's order (z_pres term, scale, shift
+            # and VAE KLs per step), replayed from the step records
+            _ops.air_runloss_(T, B, ws.rec, R_NREC * B, ws.skl, ws.shkl, ws.vkl, ws.runloss)
         self._forward_loss(X, targets, ws, need_grad, outputs)
+
+    def _batched_vae(self, B: int) -> bool:
+        """AIR's VAE output never feeds the recurrence (the LSTM input is the
+        image alone, air_model.py:454-456), so the glimpse VAE of every step
+        can run after the loop over all T*B rows at once: taller GEMMs and one
+        fused launch instead of T.  Rows of one image stay independent, so
+        every output is bit-identical to the per-step schedule; the canvas is
+        still accumulated in step order.  Tiles of the fused kernel must not
+        straddle two steps (B % 64)."""
+        return self.batch_vae and B % 64 == 0
+
+    def _vae_forward_all(self, X, ws, lik_std):
+        B, T, C, W = ws.B, self.max_steps, self.canvas_size, self.windows_size
+        TB = T * B
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        if self.fused_step:
+            self._pack_bf16()
+            if self.windows_size != 28 or (R1, R2, Z, G1, G2) != (512, 256, 50, 256, 512):
+                raise ValueError("the fused step kernel is compiled for the reference VAE shape")
+            wt = [self._wf[n] for n in self._VAE]
+            gen = getattr(ws, "eps_x_offset", None) is not None
+            off = ws.eps_x_offset if gen else 0
+            bias = [self._P("vae/" + n + "/biases") for n in self._VAE]
+            with self._timed("stn_vae_step_all"):
+                _ops.stn_vae_step_(TB, C, X, ws.th_f, ws.th_b, ws.zmask, ws.zval, ws.eps_z,
+                                   ws.eps_x, ops._i64(self.noise_seed), ops._i64(off), gen, wt,
+                                   bias, lik_std, float(self.vae_prior_mean),
+                                   float(self.vae_prior_variance), self.vae_prior_log_variance,
+                                   ws.cparts, ws.prows, None, ws.vkl, ws.gb, ws.a1b, ws.a2b,
+                                   ws.mu, ws.lv, ws.z, ws.zb, ws.d1b, ws.d2b, ws.r, B)
+            return
+        v = lambda a: a.view(TB, -1)  # noqa: E731
+        vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
+        if self.precision == "bf16":
+            from .ops import BF_SIGMOID_NOISE, BF_SOFTPLUS, BF_STORE, gemm_bf16
+            Zp = self._pad8(Z)
+            self._pack_bf16()
+            wt = self._wt
+            for t in range(T):
+                ops.stn_forward(X, ws.th_f[t], (W, W), out=ws.gb[t])
+            gemm_bf16([v(ws.gb)], [wt["recognition_1"]], [v(ws.a1b)], TB, R1, W2, W2, W2, R1,
+                      epi=BF_SOFTPLUS, bias=[vb["recognition_1"]])
+            gemm_bf16([v(ws.a1b)], [wt["recognition_2"]], [v(ws.a2b)], TB, R2, R1, R1, R1, R2,
+                      epi=BF_SOFTPLUS, bias=[vb["recognition_2"]])
+            gemm_bf16([v(ws.a2b), v(ws.a2b)], [wt["rec_mean"], wt["rec_log_variance"]],
+                      [v(ws.mu), v(ws.lv)], TB, Z, R2, R2, R2, Z, epi=BF_STORE,
+                      bias=[vb["rec_mean"], vb["rec_log_variance"]])
+            self._vae_sample_fwd_all(ws, v(ws.zb), Zp)
+            gemm_bf16([v(ws.zb)], [wt["generative_1"]], [v(ws.d1b)], TB, G1, Zp, Zp, Zp, G1,
+                      epi=BF_SOFTPLUS, bias=[vb["generative_1"]])
+            gemm_bf16([v(ws.d1b)], [wt["generative_2"]], [v(ws.d2b)], TB, G2, G1, G1, G1, G2,
+                      epi=BF_SOFTPLUS, bias=[vb["generative_2"]])
+            gemm_bf16([v(ws.d2b)], [wt["gen_mean"]], [v(ws.r)], TB, W2, G2, G2, G2, W2,
+                      epi=BF_SIGMOID_NOISE, bias=[vb["gen_mean"]], aux=[v(ws.eps_x)], ldaux=W2,
+                      aux_scale=lik_std)
+        else:
+            vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
+            for t in range(T):
+                ops.stn_forward(X, ws.th_f[t], (W, W), out=ws.g[t])
+            gemm([v(ws.g)], [vw["recognition_1"]], [v(ws.a1)], TB, R1, W2, W2, R1, R1,
+                 epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]], Cpre=[v(ws.a1pre)])
+            gemm([v(ws.a1)], [vw["recognition_2"]], [v(ws.a2)], TB, R2, R1, R1, R2, R2,
+                 epi=EPI_SOFTPLUS, bias=[vb["recognition_2"]], Cpre=[v(ws.a2pre)])
+            gemm([v(ws.a2), v(ws.a2)], [vw["rec_mean"], vw["rec_log_variance"]],
+                 [v(ws.mu), v(ws.lv)], TB, Z, R2, R2, Z, Z,
+                 bias=[vb["rec_mean"], vb["rec_log_variance"]])
+            self._vae_sample_fwd_all(ws, None, 0)
+            gemm([v(ws.z)], [vw["generative_1"]], [v(ws.d1)], TB, G1, Z, Z, G1, G1,
+                 epi=EPI_SOFTPLUS, bias=[vb["generative_1"]], Cpre=[v(ws.d1pre)])
+            gemm([v(ws.d1)], [vw["generative_2"]], [v(ws.d2)], TB, G2, G1, G1, G2, G2,
+                 epi=EPI_SOFTPLUS, bias=[vb["generative_2"]], Cpre=[v(ws.d2pre)])
+            gemm([v(ws.d2)], [vw["gen_mean"]], [v(ws.r)], TB, W2, G2, G2, W2, W2,
+                 epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]], Cpre=[v(ws.mpre)],
+                 aux=[v(ws.eps_x)], ldaux=W2, aux_scale=lik_std)
+        # STN write + masked canvas accumulation, in step order
+        for t in range(T):
+            ops.stn_forward(ws.r[t], ws.th_b[t], (C, C), out=ws.canvas, z=ws.zval[t],
+                            mask=ws.zmask[t], accumulate=True)
+
+    def _vae_sample_fwd_all(self, ws, zb, ldzb):
+        TB = ws.B * self.max_steps
+        _ops.vae_sample_forward_(TB, self.vae_latent_dimensions, float(self.vae_prior_mean),
+                                 float(self.vae_prior_variance), self.vae_prior_log_variance,
+                                 ws.mu, ws.lv, ws.eps_z, ws.z, zb, ldzb, ws.zmask, None, ws.vkl)
 
     def _forward_loss(self, X, targets, ws, need_grad, outputs=True):
         """reconstruction loss (air_model.py:866-900) + batch means.  With

@@ -199,7 +199,7 @@ def test_stn_vae_step_op_matches_c_abi_bitwise():
               dp(thb), dp(mask), dp(zp), dp(ez), dp(ex), 0, 0, 0,
               _lib.ptr_array([dp(w) for w in wf]), _lib.ptr_array([dp(t) for t in b]), 0.3, 0.0,
               1.0, 0.0, dp(part), dp(rows), dp(runloss), dp(vkl), dp(gb), dp(a1b), dp(a2b),
-              dp(mu), dp(lv), dp(z), dp(zb), dp(d1b), dp(d2b), dp(r),
+              dp(mu), dp(lv), dp(z), dp(zb), dp(d1b), dp(d2b), dp(r), 0,
               torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     for i, (a, e) in enumerate(zip(out, ref)):
