@@ -231,31 +231,28 @@ __device__ __forceinline__ void bwd_pixels(const float* th, int Hin, int Win, in
 // it with ds_bpermute, no second read of the cotangent).  The per-row body,
 // its order and its masks are bwd_pixels<true, DU>'s.
 constexpr int GV = 64;  // rows held per lane (Hout <= 64)
-template <int DU>
-__device__ __forceinline__ void bwd_rows_reg(const float* th, int Hin, int Win, int Hout,
-                                             int Wout, const float* __restrict__ Gn, float sc,
-                                             bool grads, bool want_dot, const float* sU,
-                                             float4* coltab, const float4* rowtab, float* a,
-                                             float (&gv)[GV], int& ilo_out, int& ihi_out) {
-#pragma clang fp contract(off)
+
+// Row geometry of the lane's output row (lane i -> row i) and the live row
+// range [ilo, ihi): rows whose clipped corner rows differ (a prefix and a
+// suffix of the rows are degenerate; they add exactly nothing).
+__device__ __forceinline__ float4 live_rows(const float* th, int Hin, int Win, int Hout, int Wout,
+                                            int& ilo, int& ihi) {
   const int lane = threadIdx.x & 63;
-  const float wm2 = ((float)Win - 1.001f) / 2.0f;
-  const float hm2 = ((float)Hin - 1.001f) / 2.0f;
-  const float ystep = Hout > 1 ? 2.0f / (float)(Hout - 1) : 0.0f;
-  const float4 ry = rowtab[min(lane, Hout - 1)];
+  const float4 ry = axis4(axis_row(th, Hin, Win, Hout, Wout, min(lane, Hout - 1)), Win);
   const unsigned long long lm = __builtin_amdgcn_ballot_w64(
       lane < Hout && __float_as_int(ry.x) != __float_as_int(ry.y));
-  const int ilo = lm ? __builtin_ctzll(lm) : 0;
-  const int ihi = lm ? 64 - __builtin_clzll(lm) : 0;
-  ilo_out = ilo;
-  ihi_out = ihi;
-  const int j = lane;
-  const bool jv = j < Wout;
-  const int jc = jv ? j : Wout - 1;
-  const float xt = mog_linspace(jc, Wout);
-  const float4 ex = axis4(axis_col(th, Hin, Win, Hout, Wout, jc), 1);
-  if (DU == 1 && jv) coltab[j] = ex;
-  // all live rows' cotangent (clamped rows: unpredicated loads), 16 per chunk
+  ilo = lm ? __builtin_ctzll(lm) : 0;
+  ihi = lm ? 64 - __builtin_clzll(lm) : 0;
+  return ry;
+}
+
+// all live cotangent rows of the lane's column into gv[] (clamped rows:
+// unpredicated loads, 16 per chunk), issued before the image is staged so
+// the two latencies overlap
+__device__ __forceinline__ void load_rows(const float* __restrict__ Gn, int Hout, int Wout, int ilo,
+                                          int ihi, float (&gv)[GV]) {
+  const int lane = threadIdx.x & 63;
+  const int jc = lane < Wout ? lane : Wout - 1;
 #pragma unroll
   for (int c = 0; c < GV / 16; ++c) {
     if (16 * c < ihi - ilo) {
@@ -263,6 +260,24 @@ __device__ __forceinline__ void bwd_rows_reg(const float* th, int Hin, int Win, 
       for (int r = 16 * c; r < 16 * c + 16; ++r) gv[r] = Gn[min(ilo + r, Hout - 1) * Wout + jc];
     }
   }
+}
+
+template <int DU>
+__device__ __forceinline__ void bwd_rows_reg(const float* th, int Hin, int Win, int Hout,
+                                             int Wout, float sc, bool grads, bool want_dot,
+                                             const float* sU, float4* coltab, const float4 ry,
+                                             int ilo, int ihi, float* a, const float (&gv)[GV]) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const float wm2 = ((float)Win - 1.001f) / 2.0f;
+  const float hm2 = ((float)Hin - 1.001f) / 2.0f;
+  const float ystep = Hout > 1 ? 2.0f / (float)(Hout - 1) : 0.0f;
+  const int j = lane;
+  const bool jv = j < Wout;
+  const int jc = jv ? j : Wout - 1;
+  const float xt = mog_linspace(jc, Wout);
+  const float4 ex = axis4(axis_col(th, Hin, Win, Hout, Wout, jc), 1);
+  if (DU == 1 && jv) coltab[j] = ex;
   const int x0 = __float_as_int(ex.x), x1 = __float_as_int(ex.y);
   const float ax = ex.z, bx = ex.w;
   float sdx = 0.0f, sdy = 0.0f;
@@ -305,30 +320,20 @@ __host__ __device__ inline int stn_bwd_slice(int Hin, int Win, int Hout, int Wou
   return dU && atomic_l < sep_l ? sep_l : atomic_l;
 }
 
-__global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
-    const float* __restrict__ U, int N, int Hin, int Win, const float* __restrict__ theta,
-    int Hout, int Wout, const float* __restrict__ G, const float* __restrict__ gscale, float* dU,
-    float* dtheta, float* dot, int u_period, int g_period, long long* ts, int du_mode) {
+#define TS(k) if (ts && lane == 0) ts[(size_t)n * 8 + (k)] = wall_clock64()
+// One image of stn_bwd_kernel.  REGS: the rows-in-registers form (see
+// bwd_rows_reg), a separate instantiation so the other forms' register
+// allocation never sees its 64 cotangent registers.
+template <bool REGS>
+__device__ __forceinline__ void stn_bwd_image(
+    const float* __restrict__ U, int Hin, int Win, const float* th, int Hout, int Wout,
+    const float* __restrict__ G, const float* __restrict__ gscale, float* dU, float* dtheta,
+    float* dot, int u_period, int g_period, long long* ts, int du_mode, int n, int lane, int wv,
+    bool sep, bool sdu) {
 #pragma clang fp contract(off)
   extern __shared__ float smem[];
-  // wave-uniform image index (readfirstlane): the cotangent's buffer
-  // descriptor below is then provably uniform -- otherwise hipcc wraps every
-  // buffer load of the T pass in a waterfall loop and serialises them
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int n = blockIdx.x * (blockDim.x >> 6) + wv;
-  if (n >= N) return;  // no workgroup barriers below
-#define TS(k) if (ts && lane == 0) ts[(size_t)n * 8 + (k)] = wall_clock64()
-  TS(0);
   const int HWin = Hin * Win, P = Hout * Wout;
   const bool want_dU = dU != nullptr;
-  float th[6];  // wave-uniform (scalar registers): the branches below are uniform
-#pragma unroll
-  for (int k = 0; k < 6; ++k)
-    th[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(theta[n * 6 + k])));
-  const bool sep = stn_separable(th) && Hin < 32768 && Win < 32768 && Hout <= 64;
-  // separable dU (no atomics): axis-aligned, increasing maps, extents <= 64
-  const bool sdu = want_dU && sep && th[0] > 0.0f && th[4] > 0.0f && Hin <= 64 && Win <= 64 &&
-                   Hout <= (Win <= 32 ? 64 : 32) && Wout <= 64;
   const int slice = stn_bwd_slice(Hin, Win, Hout, Wout, want_dU);
   const int hw4 = (HWin + 3) & ~3;
   float* sU = smem + wv * slice;
@@ -340,7 +345,28 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
   float4* rowtab = sdu ? coltab + 64 : reinterpret_cast<float4*>(sU + hw4 * (want_dU ? 2 : 1));
   int2* vrange = reinterpret_cast<int2*>(rowtab + 64);
   const float* Un = U + (size_t)(u_period > 0 ? n % u_period : n) * HWin;
-  if ((HWin & 3) == 0) {
+  const float* Gn = G + (size_t)(g_period > 0 ? n % g_period : n) * P;
+  // rows in registers: axis-aligned, one output row per pass, separable or no
+  // dU, image staged by 16-byte loads (the write backward, canvas <- glimpse)
+  const int mode = __builtin_amdgcn_readfirstlane((sep ? 1 : 0) | (sdu ? 2 : 0) | (want_dU ? 4 : 0));
+  constexpr bool regs = REGS;
+  float gv[GV];
+  int rlo = 0, rhi = 0;
+  float4 ry = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (regs) {
+    // image -> registers, cotangent rows -> registers, then image -> LDS: the
+    // write to LDS waits only for the image loads (issued first)
+    const floatx4* src = reinterpret_cast<const floatx4*>(Un);
+    floatx4 us[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) us[k] = src[min(lane + 64 * k, HWin / 4 - 1)];
+    ry = live_rows(th, Hin, Win, Hout, Wout, rlo, rhi);
+    load_rows(Gn, Hout, Wout, rlo, rhi, gv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (lane + 64 * k < HWin / 4) reinterpret_cast<floatx4*>(sU)[lane + 64 * k] = us[k];
+    if (lane < Hout) rowtab[lane] = ry;
+  } else if ((HWin & 3) == 0) {
     const floatx4* src = reinterpret_cast<const floatx4*>(Un);
     for (int q = lane; q < HWin / 4; q += 64) reinterpret_cast<floatx4*>(sU)[q] = src[q];
   } else {
@@ -348,26 +374,20 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
   }
   if (want_dU && !sdu)
     for (int i = lane; i < HWin; i += 64) sD[i] = 0.0f;
-  if (sep)  // row geometry once per image (lane i -> row i)
+  if (sep && !regs)  // row geometry once per image (lane i -> row i)
     for (int i = lane; i < Hout; i += 64) rowtab[i] = axis4(axis_row(th, Hin, Win, Hout, Wout, i), Win);
   wave_sync();
   TS(1);
   const float sc = gscale ? gscale[n] : 1.0f;
   const bool grads = sc != 0.0f && (want_dU || dtheta != nullptr);
   float a[7] = {0, 0, 0, 0, 0, 0, 0};
-  const float* Gn = G + (size_t)(g_period > 0 ? n % g_period : n) * P;
-  const int mode = __builtin_amdgcn_readfirstlane((sep ? 1 : 0) | (sdu ? 2 : 0) | (want_dU ? 4 : 0));
-  // rows in registers: axis-aligned, one output row per pass, separable or no dU
-  const bool regs = sep && Wout > 32 && Wout <= 64 && (mode == 1 || mode == 3 || mode == 7);
-  float gv[GV];
-  int rlo = 0, rhi = 0;
   if (regs) {
     if (mode == 1)
-      bwd_rows_reg<0>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, coltab, rowtab,
-                      a, gv, rlo, rhi);
+      bwd_rows_reg<0>(th, Hin, Win, Hout, Wout, sc, grads, dot != nullptr, sU, coltab, ry, rlo,
+                      rhi, a, gv);
     else
-      bwd_rows_reg<1>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, coltab, rowtab,
-                      a, gv, rlo, rhi);
+      bwd_rows_reg<1>(th, Hin, Win, Hout, Wout, sc, grads, dot != nullptr, sU, coltab, ry, rlo,
+                      rhi, a, gv);
   } else if (mode == 3 || mode == 7)
     bwd_pixels<true, 1>(th, Hin, Win, Hout, Wout, Gn, sc, grads, dot != nullptr, sU, sD, sg, coltab, rowtab, a);
   else if (mode == 5)
@@ -393,6 +413,15 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
   // bf16 / fp32 -- bit-identical to dU followed by mog_sigmoid_backward
   float* dUn = dU + (size_t)n * HWin;
   __bf16* dMn = reinterpret_cast<__bf16*>(dU) + (size_t)n * HWin;
+  auto put_u = [&](int idx, float d, float v) {
+    if (du_mode) {
+      const float m = (d * v) * (1.0f - v);
+      if (du_mode == 1) dMn[idx] = (__bf16)m;
+      else dUn[idx] = m;
+    } else {
+      dUn[idx] = d;
+    }
+  };
   auto put = [&](int idx, float d) {
     if (du_mode) {
       const float v = Un[idx];
@@ -425,6 +454,9 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
     }
     const int cwi = Win <= 32 ? 32 : 64, rpi = 64 / cwi;
     const int ul = lane % cwi, half = lane / cwi;
+    constexpr int UV = 32;
+    const bool upre = du_mode != 0 && rpi * UV >= Hin;
+    float uv[UV];
     int jlo = 0, jhi = -1;
     for (int u = 0; u < Win; ++u) {
       const int lo = __popcll(__ballot(x1l < u));
@@ -538,8 +570,31 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
     wave_sync();
     TS(3);
   du_pass:
+    // the output sigmoid's r = U at the lane's dU outputs, all loaded up
+    // front (the T pass overwrote the staged image): one memory latency
+    // instead of one dependent round trip per output
+    if (upre) {
+#pragma unroll
+      for (int k = 0; k < UV; ++k)
+        uv[k] = Un[min(half + rpi * k, Hin - 1) * Win + min(ul, Win - 1)];
+    }
     // dU[v][u] = sum_i T[i][u] * (y0(i) == v ? y1 - y : y - y0)
-    if (ul < Win)
+    if (upre) {
+      if (ul < Win) {
+#pragma unroll
+        for (int k = 0; k < UV; ++k) {
+          const int v = half + rpi * k;
+          if (v >= Hin) break;
+          const int2 r = vrange[v];
+          float acc = 0.0f;
+          for (int i = r.x; i <= r.y; ++i) {
+            const float4 e = rowtab[i];
+            acc += sT[i * Win + ul] * (__float_as_int(e.x) == v * Win ? e.z : e.w);
+          }
+          put_u(v * Win + ul, acc, uv[k]);
+        }
+      }
+    } else if (ul < Win)
       for (int v = half; v < Hin; v += rpi) {
         const int2 r = vrange[v];
         float acc = 0.0f;
@@ -558,6 +613,39 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
   } else {
     for (int i = lane; i < HWin; i += 64) put(i, sD[i]);
   }
+}
+
+__global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
+    const float* __restrict__ U, int N, int Hin, int Win, const float* __restrict__ theta,
+    int Hout, int Wout, const float* __restrict__ G, const float* __restrict__ gscale, float* dU,
+    float* dtheta, float* dot, int u_period, int g_period, long long* ts, int du_mode) {
+#pragma clang fp contract(off)
+  // wave-uniform image index (readfirstlane): the cotangent's buffer
+  // descriptor below is then provably uniform -- otherwise hipcc wraps every
+  // buffer load of the T pass in a waterfall loop and serialises them
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n = blockIdx.x * (blockDim.x >> 6) + wv;
+  if (n >= N) return;  // no workgroup barriers below
+  TS(0);
+  const int HWin = Hin * Win;
+  const bool want_dU = dU != nullptr;
+  float th[6];  // wave-uniform (scalar registers): the branches below are uniform
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    th[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(theta[n * 6 + k])));
+  const bool sep = stn_separable(th) && Hin < 32768 && Win < 32768 && Hout <= 64;
+  // separable dU (no atomics): axis-aligned, increasing maps, extents <= 64
+  const bool sdu = want_dU && sep && th[0] > 0.0f && th[4] > 0.0f && Hin <= 64 && Win <= 64 &&
+                   Hout <= (Win <= 32 ? 64 : 32) && Wout <= 64;
+  const int mode = (sep ? 1 : 0) | (sdu ? 2 : 0) | (want_dU ? 4 : 0);
+  const bool regs = sep && Wout > 32 && Wout <= 64 && (HWin & 3) == 0 && HWin <= 1024 &&
+                    (mode == 1 || mode == 3 || mode == 7);
+  if (regs)
+    stn_bwd_image<true>(U, Hin, Win, th, Hout, Wout, G, gscale, dU, dtheta, dot, u_period,
+                        g_period, ts, du_mode, n, lane, wv, sep, sdu);
+  else
+    stn_bwd_image<false>(U, Hin, Win, th, Hout, Wout, G, gscale, dU, dtheta, dot, u_period,
+                         g_period, ts, du_mode, n, lane, wv, sep, sdu);
 }
 
 }  // namespace
