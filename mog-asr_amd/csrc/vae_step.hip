@@ -778,8 +778,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
         reinterpret_cast<float4*>(p.r)[q] = make_float4(o[0], o[1], o[2], o[3]);
       }
     };
-    dense_tiles<MT, 512, 32 / NW, NW / 4, false>(sD2, S512, p.wt[6], p.bias[6], W2, 0, 0, NW, epi);
-    dense_tiles<MT, 512, 16 / NW, 4, false>(sD2, S512, p.wt[6], p.bias[6], W2, 32, 0, NW, epi);
+    dense_tiles<MT, 512, 32 / NW, 8, false>(sD2, S512, p.wt[6], p.bias[6], W2, 0, 0, NW, epi);
+    dense_tiles<MT, 512, 16 / NW, 8, false>(sD2, S512, p.wt[6], p.bias[6], W2, 32, 0, NW, epi);
     dense_rowsplit<MT, 512>(sD2, S512, p.wt[6], p.bias[6], W2, 48, epi);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // r stores done before other waves read it
