@@ -55,6 +55,7 @@ struct GemmPtrs {
 struct GemmDims {
   int M, N, K, lda, ldb, ldc, ldaux, splitk, kchunk, vecA, vecB, nx, ny;
   int kseg;  // > 0: K is nseg segments of kseg, segment s read from A[s] / B[s]
+  int vecC;  // C / Cpre / aux 16-byte aligned with ldc, ldaux % 4 == 0 (row-staged epilogue)
   float aux_scale;
 };
 
@@ -226,6 +227,96 @@ __device__ __forceinline__ void store_tile(const floatx4 (&acc)[MI][NI], const G
             C[o] = mog_sigmoidf(v + aux[(size_t)row * D.ldaux + col] * D.aux_scale);
         }
       }
+}
+
+// Epilogue of the whole BM x BN workgroup tile staged through LDS (the k
+// loop's stage buffers, free by now): the waves' 16x16 accumulator layout
+// (a store instruction writes 64-byte row pieces) is re-read as whole rows,
+// so every store / aux load / atomic instruction covers full 256-byte row
+// segments.  Elementwise math identical to store_tile.
+template <int BM, int BN, int EPI>
+__device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[BM / 32][BN / 32],
+                                                float* sC, const GemmPtrs& P, const GemmDims& D,
+                                                int z, int m0, int n0, int wm, int wn) {
+#pragma clang fp contract(off)
+  constexpr int MI = BM / 32, NI = BN / 32, LDC = BN + 4;
+  const int t = threadIdx.x, lane = t & 63;
+  __syncthreads();  // every wave is done with the stage buffers
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        sC[(wm + mi * 16 + (lane >> 4) * 4 + r) * LDC + wn + ni * 16 + (lane & 15)] =
+            acc[mi][ni][r];
+  __syncthreads();
+  const int M = D.M, N = D.N;
+  float* C = P.C[z];
+  if constexpr (EPI == EPI_ATOMIC) {
+    // one element per lane: a wave-instruction adds 64 consecutive columns
+    for (int q = t; q < BM * BN; q += 256) {
+      const int row = q / BN, col = q - row * BN;
+      if (m0 + row < M && n0 + col < N)
+        atomicAdd(C + (size_t)(m0 + row) * D.ldc + n0 + col, sC[row * LDC + col]);
+    }
+  } else {
+    const float* bias = P.bias[z];
+    const float* aux = P.aux[z];
+    float* Cpre = P.Cpre[z];
+    constexpr int C4 = BN / 4;
+    constexpr bool HAS_PRE = EPI == EPI_RELU || EPI == EPI_SOFTPLUS || EPI == EPI_SIGMOID_NOISE;
+    constexpr bool HAS_AUX = EPI == EPI_SOFTPLUS_BWD || EPI == EPI_RELU_BWD ||
+                             EPI == EPI_SIGMOID_NOISE;
+    for (int q = t; q < BM * C4; q += 256) {
+      const int row = q / C4, c4 = q - row * C4;
+      const int grow = m0 + row, gcol = n0 + 4 * c4;
+      if (grow >= M || gcol >= N) continue;
+      const bool full = gcol + 4 <= N;
+      const float4 a4 = *reinterpret_cast<const float4*>(&sC[row * LDC + 4 * c4]);
+      const float v[4] = {a4.x, a4.y, a4.z, a4.w};
+      float x[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (HAS_AUX) {
+        const float* ar = aux + (size_t)grow * D.ldaux + gcol;
+        if (full) {
+          const float4 x4 = *reinterpret_cast<const float4*>(ar);
+          x[0] = x4.x; x[1] = x4.y; x[2] = x4.z; x[3] = x4.w;
+        } else {
+          for (int e = 0; e < 4; ++e) x[e] = gcol + e < N ? ar[e] : 0.0f;
+        }
+      }
+      float o[4], pre[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float w = v[e];
+        pre[e] = w;
+        if (EPI == EPI_SOFTPLUS_BWD) {
+          o[e] = w * mog_sigmoidf(x[e]);
+        } else if (EPI == EPI_RELU_BWD) {
+          o[e] = x[e] > 0.0f ? w : 0.0f;
+        } else {
+          if (bias != nullptr) w = w + bias[min(gcol + e, N - 1)];
+          pre[e] = w;
+          if (EPI == EPI_STORE) o[e] = w;
+          if (EPI == EPI_RELU) o[e] = w > 0.0f ? w : 0.0f;
+          if (EPI == EPI_SOFTPLUS) o[e] = mog_softplusf(w);
+          if (EPI == EPI_SIGMOID_NOISE) o[e] = mog_sigmoidf(w + x[e] * D.aux_scale);
+        }
+      }
+      float* cr = C + (size_t)grow * D.ldc + gcol;
+      float* pr = (HAS_PRE && Cpre) ? Cpre + (size_t)grow * D.ldc + gcol : nullptr;
+      if (full) {
+        *reinterpret_cast<float4*>(cr) = make_float4(o[0], o[1], o[2], o[3]);
+        if (pr) *reinterpret_cast<float4*>(pr) = make_float4(pre[0], pre[1], pre[2], pre[3]);
+      } else {
+        for (int e = 0; e < 4; ++e)
+          if (gcol + e < N) {
+            cr[e] = o[e];
+            if (pr) pr[e] = pre[e];
+          }
+      }
+    }
+  }
 }
 
 template <int BM, int BN, int BK, int PF, bool TA, bool TB, int EPI, bool KSEG>
@@ -583,6 +674,12 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_dma_kernel(GemmPtrs P, GemmDi
   }
   if (do_cs && n0 + t < N) atomicAdd(colsum + n0 + t, cs);
 
+  if constexpr (BM * (BN + 4) <= NS * STAGE) {
+    if (D.vecC) {
+      store_tile_rows<BM, BN, EPI>(acc, lds, P, D, z, m0, n0, wm, wn);
+      return;
+    }
+  }
   store_tile<MI, NI, EPI>(acc, P, D, z, m0 + wm, n0 + wn, lane);
 }
 
@@ -751,6 +848,11 @@ extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const
   D.aux_scale = aux_scale;
   D.vecA = va && (lda % 4 == 0);
   D.vecB = vb && (ldb % 4 == 0);
+  bool vc = ldc % 4 == 0 && (ldaux % 4 == 0 || aux == nullptr);
+  for (int i = 0; i < batch; ++i)
+    vc = vc && aligned16(P.C[i]) && (!P.Cpre[i] || aligned16(P.Cpre[i])) &&
+         (!P.aux[i] || aligned16(P.aux[i]));
+  D.vecC = vc;
   D.splitk = splitk;
   D.kchunk = 0;
   D.kseg = 0;
@@ -788,6 +890,7 @@ extern "C" int mog_gemm_f32_kseg(int nseg, const float* const* A, const float* c
   D.aux_scale = 0.0f;
   D.vecA = va && (lda % 4 == 0);
   D.vecB = vb && (ldb % 4 == 0);
+  D.vecC = 0;
   D.splitk = 1;
   D.kchunk = 0;
   D.kseg = kseg;

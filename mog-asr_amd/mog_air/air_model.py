@@ -124,7 +124,6 @@ class _Workspace:
             self.a2pre, self.a2 = e(T, B, R2), e(T, B, R2)
             self.d1pre, self.d1 = e(T, B, G1), e(T, B, G1)
             self.d2pre, self.d2 = e(T, B, G2), e(T, B, G2)
-            self.mpre = e(T, B, W2)
         self.canvas = e(B, C2)
         # fused bf16 step: per-step canvas contributions, summed by the loss kernel
         self.cparts = e(T, B, C2) if m.fused_step else None
@@ -531,7 +530,7 @@ class AIRModel:
             gemm([v(ws.d1)], [vw["generative_2"]], [v(ws.d2)], TB, G2, G1, G1, G2, G2,
                  epi=EPI_SOFTPLUS, bias=[vb["generative_2"]], Cpre=[v(ws.d2pre)])
             gemm([v(ws.d2)], [vw["gen_mean"]], [v(ws.r)], TB, W2, G2, G2, W2, W2,
-                 epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]], Cpre=[v(ws.mpre)],
+                 epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]],
                  aux=[v(ws.eps_x)], ldaux=W2, aux_scale=lik_std)
         # STN write + masked canvas accumulation, in step order
         for t in range(T):
@@ -707,7 +706,7 @@ class AIRModel:
         gemm([ws.d1[t]], [vw["generative_2"]], [ws.d2[t]], B, G2, G1, G1, G2, G2,
              epi=EPI_SOFTPLUS, bias=[vb["generative_2"]], Cpre=[ws.d2pre[t]])
         gemm([ws.d2[t]], [vw["gen_mean"]], [ws.r[t]], B, W2, G2, G2, W2, W2,
-             epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]], Cpre=[ws.mpre[t]],
+             epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]],
              aux=[ws.eps_x[t]], ldaux=W2, aux_scale=lik_std)
 
     def _vae_sample_fwd(self, ws, t, zb, ldzb):
