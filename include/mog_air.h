@@ -55,6 +55,15 @@ int mog_gemm_f32_kseg(int nseg, const float* const* A, const float* const* B, fl
 int mog_stn_forward(const float* U, int N, int Hin, int Win, const float* theta, int Hout,
                     int Wout, void* out, const float* z, const float* mask, int mode,
                     void* stream);
+/* STN write of N images into per-image canvas parts (mode-1 semantics without
+ * the read-modify-write): parts[n] = mask[n] ? z[n] * STN(U[n], theta[n]) : 0,
+ * stored only on the rows part_rows[n] = lo | hi << 16 (even bounds; rows
+ * outside are exactly +0 for axis-aligned theta; all rows otherwise; 0 for an
+ * inactive image).  mog_recon_loss sums T such part sets in step order
+ * (air_model.py:580-588, 665-675), bit-identical to accumulating. */
+int mog_stn_write_parts(const float* U, int N, int Hin, int Win, const float* theta, int Hout,
+                        int Wout, const float* z, const float* mask, float* parts,
+                        int* part_rows, void* stream);
 
 /* Gradient of transformer() (TF GatherV2 grad = UnsortedSegmentSum + the
  * affine-grid chain): G [N, Hout*Wout] upstream, scaled per image by gscale[n]

@@ -89,6 +89,64 @@ __global__ __launch_bounds__(256) void stn_fwd_kernel(const float* __restrict__ 
   }
 }
 
+// STN write of one image into its canvas part (the fp32 counterpart of the
+// fused step kernel's write phase): part = mask ? z * STN(U, theta) : 0,
+// stored only on the rows whose clipped corner rows differ (the others are
+// exactly +0: their y weights cancel on one source row), widened to even
+// bounds; part_rows[n] = lo | hi << 16 records them (0: inactive image, nothing
+// stored).  mog_recon_loss sums the parts in step order, bit-identical to the
+// running canvas accumulation (mode 1 above), so all T steps' writes run as
+// one launch and the canvas is never read-modified-written.
+__global__ __launch_bounds__(256) void stn_part_kernel(const float* __restrict__ U, int Hin,
+                                                       int Win, const float* __restrict__ theta,
+                                                       int Hout, int Wout, float* parts,
+                                                       int* part_rows, const float* __restrict__ z,
+                                                       const float* __restrict__ mask) {
+#pragma clang fp contract(off)
+  __shared__ int srange;
+  const int n = blockIdx.x;
+  const int P = Hout * Wout;
+  if (!(mask[n] != 0.0f)) {
+    if (threadIdx.x == 0) part_rows[n] = 0;
+    return;
+  }
+  float th[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) th[k] = theta[n * 6 + k];
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    int lo = 0, hi = Hout;
+    if (stn_separable(th) && Hout <= 64 && (Hout & 1) == 0) {
+      const float2 e = axis_row(th, Hin, Win, Hout, Wout, min(lane, Hout - 1));
+      const unsigned long long lm =
+          __builtin_amdgcn_ballot_w64(lane < Hout && axis_lo(e) != axis_hi(e));
+      lo = lm ? (__builtin_ctzll(lm) & ~1) : 0;
+      hi = lm ? min(Hout, (64 - __builtin_clzll(lm) + 1) & ~1) : 0;
+    }
+    if (lane == 0) {
+      srange = lo | (hi << 16);
+      part_rows[n] = lo | (hi << 16);
+    }
+  }
+  __syncthreads();
+  const int lo = srange & 0xffff, hi = srange >> 16;
+  const float* Un = U + (size_t)n * Hin * Win;
+  const float zn = z[n];
+  const RowMap rm = row_map(Wout);
+  const int w = threadIdx.x >> 6;
+  float* out = parts + (size_t)n * P;
+  for (int j0 = 0; j0 < Wout; j0 += rm.cw) {
+    const int j = j0 + rm.j;
+    if (j >= Wout) continue;
+    const float xt = mog_linspace(j, Wout);
+    for (int i = lo + w * rm.rw + rm.sub; i < hi; i += 4 * rm.rw) {
+      const float yt = mog_linspace(i, Hout);
+      const Tap s = stn_tap(th, Hin, Win, xt, yt);
+      out[i * Wout + j] = s.dead ? 0.0f : zn * tap_value(s, Un);
+    }
+  }
+}
+
 // Backward, one wave per image (no workgroup barriers): lanes walk output
 // columns (the column geometry stays in registers), the wave walks output
 // rows with the cotangent rows prefetched one batch ahead.  The source image
@@ -649,6 +707,17 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
 }
 
 }  // namespace
+
+extern "C" int mog_stn_write_parts(const float* U, int N, int Hin, int Win, const float* theta,
+                                   int Hout, int Wout, const float* z, const float* mask,
+                                   float* parts, int* part_rows, void* stream) {
+  MOG_CHECK_ARG(U && theta && z && mask && parts && part_rows && N >= 0);
+  MOG_CHECK_ARG(Hin > 0 && Win > 0 && Hout > 0 && Wout > 0 && Hout < 65536);
+  if (N == 0) return 0;
+  stn_part_kernel<<<N, 256, 0, mog_stream(stream)>>>(U, Hin, Win, theta, Hout, Wout, parts,
+                                                      part_rows, z, mask);
+  MOG_LAUNCH_RET();
+}
 
 // transformer(U, theta, out_size) forward; see include/mog_air.h
 extern "C" int mog_stn_forward(const float* U, int N, int Hin, int Win, const float* theta,

@@ -194,6 +194,14 @@ void air_step_backward_(int64_t B, int64_t HS, bool train, bool use_num_prior,
         "air_step_backward_");
 }
 
+void stn_write_parts_(const Tensor& U, int64_t N, int64_t Hin, int64_t Win, const Tensor& theta,
+                      int64_t Hout, int64_t Wout, const Tensor& z, const Tensor& mask, Tensor parts,
+                      Tensor part_rows) {
+  check(mog_stn_write_parts(f(U), N, Hin, Win, f(theta), Hout, Wout, f(z), f(mask), f(parts),
+                            static_cast<int*>(p(part_rows)), stream()),
+        "stn_write_parts_");
+}
+
 // ------------------------------------------------------------ glimpse VAE ----
 void vae_sample_forward_(int64_t B, int64_t Z, double v_pm, double v_pv, double v_plv,
                          const Tensor& mu, const Tensor& lv, const Tensor& eps, Tensor z,
@@ -335,6 +343,9 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "Tensor dtheta_back, Tensor dot, Tensor[] hid, Tensor[] w2, Tensor(a!) dout, int dout_hs, "
       "Tensor(b!) dhid, int dhid_hs) -> ()");
   m.def(
+      "stn_write_parts_(Tensor U, int N, int Hin, int Win, Tensor theta, int Hout, int Wout, "
+      "Tensor z, Tensor mask, Tensor(a!) parts, Tensor(b!) part_rows) -> ()");
+  m.def(
       "vae_sample_forward_(int B, int Z, float v_pm, float v_pv, float v_plv, Tensor mu, "
       "Tensor lv, Tensor eps, Tensor(a!) z, Tensor? z_bf16, int ld_zb, Tensor act, "
       "Tensor(b!)? runloss, Tensor(c!) vkl) -> ()");
@@ -384,6 +395,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("vae_sample_forward_", &vae_sample_forward_);
   m.impl("vae_sample_backward_", &vae_sample_backward_);
   m.impl("air_runloss_", &air_runloss_);
+  m.impl("stn_write_parts_", &stn_write_parts_);
   m.impl("sigmoid_backward_", &sigmoid_backward_);
   m.impl("stn_vae_step_", &stn_vae_step_);
   m.impl("recon_loss_", &recon_loss_);

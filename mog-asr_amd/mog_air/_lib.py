@@ -38,6 +38,7 @@ _SIGS = {
     "mog_stn_vae_step_forward": ([I] * 8 + [P] * 7 + [I, ULL, ULL] + [P] * 2 + [F] * 4 + [P] * 14
                                  + [I, P]),
     "mog_air_runloss": [I, I, P, L, P, P, P, P, P],
+    "mog_stn_write_parts": [P, I, I, I, P, I, I, P, P, P, P, P],
     "mog_vae_sample_backward": [I, I, F, F, F, P, P, P, P, P, P, P, P, P, I, P],
     "mog_sigmoid_backward": [P, P, P, L, I, P],
     "mog_gemm_bf16": [I, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, I, P],

@@ -126,9 +126,9 @@ class _Workspace:
             self.d2pre, self.d2 = e(T, B, G2), e(T, B, G2)
         self.canvas = e(B, C2)
         # fused bf16 step: per-step canvas contributions, summed by the loss kernel
-        self.cparts = e(T, B, C2) if m.fused_step else None
-        self.prows = (torch.empty((T, B), device=dev, dtype=torch.int32)
-                      if m.fused_step else None)
+        parts = m._parts_layout(B)
+        self.cparts = e(T, B, C2) if parts else None
+        self.prows = torch.empty((T, B), device=dev, dtype=torch.int32) if parts else None
         self.stop, self.runloss = e(B), e(B)
         self.digits = torch.empty(B, device=dev, dtype=torch.int32)
         self.live = torch.empty(T + 1, device=dev, dtype=torch.int32)
@@ -396,7 +396,7 @@ class AIRModel:
         K = self._P("rnn/basic_lstm_cell/kernel")
         bK = self._P("rnn/basic_lstm_cell/bias")
         Wx, Wh = K[:C2], K[C2:]
-        if not self.fused_step:  # fused: the loss kernel writes the canvas
+        if ws.cparts is None:  # parts: the loss kernel sums them into the canvas
             ws.canvas.zero_()
         ws.stop.zero_()
         ws.runloss.zero_()
@@ -458,6 +458,12 @@ class AIRModel:
             # and VAE KLs per step), replayed from the step records
             _ops.air_runloss_(T, B, ws.rec, R_NREC * B, ws.skl, ws.shkl, ws.vkl, ws.runloss)
         self._forward_loss(X, targets, ws, need_grad, outputs)
+
+    def _parts_layout(self, B: int) -> bool:
+        """Per-step canvas parts [T, B, C*C] (+ stored row ranges) summed in
+        step order by the loss kernel, instead of one running canvas: the
+        fused step kernel and the all-steps STN write."""
+        return self.fused_step or self._batched_vae(B)
 
     def _batched_vae(self, B: int) -> bool:
         """AIR's VAE output never feeds the recurrence (the LSTM input is the
@@ -532,10 +538,10 @@ class AIRModel:
             gemm([v(ws.d2)], [vw["gen_mean"]], [v(ws.r)], TB, W2, G2, G2, W2, W2,
                  epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]],
                  aux=[v(ws.eps_x)], ldaux=W2, aux_scale=lik_std)
-        # STN write + masked canvas accumulation, in step order
-        for t in range(T):
-            ops.stn_forward(ws.r[t], ws.th_b[t], (C, C), out=ws.canvas, z=ws.zval[t],
-                            mask=ws.zmask[t], accumulate=True)
+        # STN write of every step into its canvas part (air_model.py:580-588);
+        # the loss kernel adds the parts in step order (:665-675)
+        _ops.stn_write_parts_(v(ws.r), TB, W, W, ws.th_b, C, C, ws.zval, ws.zmask, ws.cparts,
+                              ws.prows)
 
     def _vae_sample_fwd_all(self, ws, zb, ldzb):
         TB = ws.B * self.max_steps

@@ -268,6 +268,9 @@ class AIRModel(_AirBase):
         super()._fill_noise(ws, None)
 
     # ---------------------------------------------------------- forward ---
+    def _parts_layout(self, B: int) -> bool:
+        return self.fused_step
+
     def _forward(self, X, targets, ws, need_grad, outputs=True):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
         C, W, C2 = self.canvas_size, self.windows_size, self.C2
@@ -275,7 +278,7 @@ class AIRModel(_AirBase):
         Ki = self._N("infer_rnn_running/kernel")
         Kg = self._N("gen_rnn_running/kernel")
         bi, bg = self._N("infer_rnn_running/bias"), self._N("gen_rnn_running/bias")
-        if not self.fused_step:
+        if ws.cparts is None:
             ws.canvas.zero_()
         ws.stop.zero_()
         ws.runloss.zero_()

@@ -58,12 +58,15 @@ def test_batched_vae_matches_per_step_bitwise(precision, fused):
     torch.cuda.synchronize()
     names = ["runloss", "vkl", "mu", "lv", "z", "r", "zval", "zmask", "loss_b"]
     names += ["gb", "a1b", "a2b", "zb", "d1b", "d2b"] if precision == "bf16" else \
-        ["g", "a1", "a2", "d1", "d2", "a1pre", "d2pre", "canvas"]
+        ["g", "a1", "a2", "d1", "d2", "a1pre", "d2pre"]
     for n in names:
         assert torch.equal(_bits(getattr(mb._ws, n)), _bits(getattr(ms._ws, n))), n
-    if fused:  # parts are stored only inside part_rows; the summed canvas is the check
+    if fused:
         assert torch.equal(mb._ws.prows, ms._ws.prows)
-        assert torch.equal(_bits(mb.canvas), _bits(ms.canvas))
+    # parts are stored only inside part_rows: the summed canvas is the check
+    # (-0 vs +0 allowed: the loss kernel starts from the first part, the
+    # running accumulation from +0)
+    np.testing.assert_array_equal(mb.canvas.cpu().numpy(), ms.canvas.cpu().numpy())
     assert mb.loss == ms.loss
     for n in gb:
         np.testing.assert_array_equal(gb[n], gs[n], err_msg=n)
