@@ -339,10 +339,13 @@ __device__ __forceinline__ void bwd_rows_reg(const float* th, int Hin, int Win, 
   const int x0 = __float_as_int(ex.x), x1 = __float_as_int(ex.y);
   const float ax = ex.z, bx = ex.w;
   float sdx = 0.0f, sdy = 0.0f;
+  // rows in groups of four: one uniform branch per group, so the four rows'
+  // LDS gathers are in flight together (rows past ihi are clamped and masked)
 #pragma unroll
   for (int r = 0; r < GV; ++r) {
-    const int i = ilo + r;
-    if (i >= ihi) break;
+    if (r % 4 == 0 && ilo + r >= ihi) break;
+    const bool rv = ilo + r < ihi;
+    const int i = min(ilo + r, ihi - 1);
     const float yt = Hout == 1 ? -1.0f : (i == Hout - 1 ? 1.0f : -1.0f + ystep * (float)i);
     const float4 ey = make_float4(
         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry.x), i)),
@@ -355,9 +358,9 @@ __device__ __forceinline__ void bwd_rows_reg(const float* th, int Hin, int Win, 
     const float Ia = sU[y0 + x0], Ib = sU[y1 + x0], Ic = sU[y0 + x1], Id = sU[y1 + x1];
     const float gout = gv[r];
     const float pv = gout * sample4(ex, ey, Ia, Ib, Ic, Id);
-    a[6] += (want_dot && jv && !dead) ? pv : 0.0f;
+    a[6] += (want_dot && jv && rv && !dead) ? pv : 0.0f;
     const float g0 = gout * sc;
-    const bool use = jv && grads && !degen && g0 != 0.0f;
+    const bool use = jv && rv && grads && !degen && g0 != 0.0f;
     const float g = use ? g0 : 0.0f;
     const float ay = ey.z, by = ey.w;
     const float dx = g * (ay * (Ic - Ia) + by * (Id - Ib)) * wm2;
@@ -572,9 +575,12 @@ __device__ __forceinline__ void stn_bwd_image(
           wj[d] = d < nj ? (__float_as_int(e.x) == ul ? e.z : e.w) : 0.0f;
           src[d] = max(jj, 0) * 4;
         }
+        // rows in groups of four (one uniform branch per group): the group's
+        // exchanges are in flight together
 #pragma unroll
         for (int r = 0; r < GV; ++r) {
-          if (rlo + r >= rhi) break;
+          if (r % 4 == 0 && rlo + r >= rhi) break;
+          const bool rv = rlo + r < rhi;
           const float g0 = gv[r] * sc;
           const float gt = grads && g0 != 0.0f ? g0 : 0.0f;
           float acc = 0.0f;
@@ -584,7 +590,7 @@ __device__ __forceinline__ void stn_bwd_image(
             const float gj = __int_as_float(__builtin_amdgcn_ds_bpermute(src[d], __float_as_int(gt)));
             if (d < nj) acc += gj * wj[d];
           }
-          if (uact) sT[(rlo + r) * Win + ul] = acc;
+          if (uact && rv) sT[(rlo + r) * Win + ul] = acc;
         }
         wave_sync();
         TS(3);
