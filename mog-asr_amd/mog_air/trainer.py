@@ -5,9 +5,11 @@ the reference's logging / testing / checkpoint cadence, and the end-of-data
 (OutOfRangeError) epilogue — training_air_original.py:18-503 and
 train_air_pr.py:18-400 restated around ``AIRModel.step`` / ``infer``.
 
-Out of scope: TensorBoard summaries and PNG dumps — the
-reference writes them from the test model every 500 iterations; here the
-iteration numbers where they would be written are logged instead.
+Image grids (training_air_original.py:368-411, :445-490): every
+IMAGE_SAVE_ITERATION iterations and at the end, the test model's
+reconstruction / misclassified / generation grids are written as PNG files
+under summary/ (``mog_air.visualize``).  TensorBoard event files are out of
+scope.
 """
 from __future__ import annotations
 
@@ -28,6 +30,8 @@ EPOCHS = 300
 BATCH_SIZE = 64
 LOG_EACH_ITERATION = 20
 TEST_EACH_ITERATION = 200
+IMAGE_SAVE_ITERATION = 500  # training_air_original.py:31
+NUM_IMAGES_TO_SAVE = 60     # :43
 SAVE_PARAMS_EACH_ITERATIONS = 10000
 
 
@@ -54,6 +58,8 @@ def add_common_args(parser, reader_threads: int):
                         help="images per object count when the dataset files are absent")
     parser.add_argument("--write-synthetic", type=int, choices=[0, 1], default=0)
     parser.add_argument("--device", default="cuda:0")
+    parser.add_argument("--no-images", action="store_true",
+                        help="skip the PNG grids (training_air_original.py:368-411)")
 
 
 def select_gpu(gpu: str) -> None:
@@ -314,6 +320,17 @@ def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, mod
                  "\tglobaliou:{:.4f}".format(step_tag, p, r, gt_iou, det_iou, g_iou))
         return tl, ta, tm, g_iou
 
+    summary_folder = os.path.join(os.path.dirname(os.path.normpath(models_folder)), "summary")
+    digits = [int(c) for c in getattr(args, "dig_num", "")]
+    vis_n = args.test_batch if getattr(args, "test_batch", 0) > 0 else len(test[1])
+
+    def save_images(tag, generations=True):
+        if not ctx.main or getattr(args, "no_images", False):
+            return
+        from .visualize import save_visualizations
+        save_visualizations(test_model, test[0][:vis_n], test[1][:vis_n], summary_folder, tag,
+                            digits=digits, num=NUM_IMAGES_TO_SAVE, generations=generations)
+
     log.info("Training...\n")
     try:
         while True:
@@ -337,10 +354,13 @@ def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, mod
                     update_flag = False
                     best = [tl, ta, tm, g_iou]
                 log.info("Current Best: elbo:{}\taccu:{}\tmse:{}\tiou:{}".format(*best))
+            if step % IMAGE_SAVE_ITERATION == 0:
+                save_images(step)
             if args.iterations and step >= args.iterations:
                 raise StopIteration
     except StopIteration:
         test_and_log("final")
+        save_images("final")
         log.info("Final Best: elbo:{}\taccu:{}\tmse:{}\tiou:{}".format(*best))
         log.info("\ntraining has ended\n")
     return step
@@ -383,6 +403,18 @@ def train_loop_asr(args, train_model, test_model, tr_x, tr_k, test, canvas, log,
                  "".join("{}:{:.4f}\t".format(n, v) for n, v in lv.items()))
         log.info("Current Best: elbo:{}\taccu:{}\tmse:{}\tiou:{}".format(*best))
 
+    summary_folder = os.path.join(os.path.dirname(os.path.normpath(models_folder)), "summary")
+    vis_n = args.test_batch if getattr(args, "test_batch", 0) > 0 else len(test[1])
+
+    def save_images(tag):
+        # train_air_pr.py:362-389 (the ASR generation grids need the
+        # generative LSTM prior, not part of this build)
+        if not ctx.main or getattr(args, "no_images", False):
+            return
+        from .visualize import save_visualizations
+        save_visualizations(test_model, test[0][:vis_n], test[1][:vis_n], summary_folder, tag,
+                            num=NUM_IMAGES_TO_SAVE, generations=False)
+
     log.info("Training...\n")
     try:
         while True:
@@ -404,10 +436,13 @@ def train_loop_asr(args, train_model, test_model, tr_x, tr_k, test, canvas, log,
                 logged = {}
             if step % TESET_EACH_ITERATION == 0:
                 test_and_log(step)
+            if step % IMAGE_SAVE_ITERATION == 0:
+                save_images(step)
             if args.iterations and step >= args.iterations:
                 raise StopIteration
     except StopIteration:
         test_and_log(step)  # the reference logs the step here too (train_air_pr.py:426-430)
+        save_images("final")
         log.info("Final Best: elbo:{}\taccu:{}\tmse:{}\tiou:{}".format(*best))
         log.info("\ntraining has ended\n")
     return step
