@@ -789,7 +789,17 @@ void launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, co
     // stages (measured, scripts/bench_gemm_f32.py): 4 with fragment
     // double-buffering for the split-K weight gradients (transA), 3 for the
     // rest, where a fifth/sixth workgroup per CU beats the deeper pipeline
-    if (b128) {
+    // 128x64 (4 waves of 64x32: twice the MFMAs per barrier of 64x64, still
+    // >= 3 workgroups per CU) for the tall non-transposed-A GEMMs: the
+    // T*B-row forward layers and input gradients, the recurrent GEMM
+    // (scripts/bench_gemm_f32.py: dX 196 -> 188 / 190 -> 182 us, recurrent
+    // 54 -> 48 us; N = 256 layers and split-K weight gradients lose)
+    bool t12864 = !ta && !b128 && D.N >= 512 && (long)D.M * D.N >= 8192L * 1024;
+    if (force != nullptr) t12864 = atoi(force) == 12864;
+    if (t12864) {
+      if (ta) launch_dma<128, 64, 16, 4>(ta, tb, epi, s, P, D, batch);
+      else launch_dma<128, 64, 16, 3>(ta, tb, epi, s, P, D, batch);
+    } else if (b128) {
       if (ta) launch_dma<128, 128, 16, 4>(ta, tb, epi, s, P, D, batch);
       else launch_dma<128, 128, 16, 3>(ta, tb, epi, s, P, D, batch);
     } else {
