@@ -611,6 +611,12 @@ class AIRModel:
             self._vae_backward_bf16_all(ws, gscale)
         else:
             self._vae_backward_fp32_all(ws, gscale)
+        # The VAE weight gradients need only the activations and the VAE input
+        # gradients, final here: they run on a second stream (MFMA-bound
+        # split-K GEMMs) under the latency-bound STN read backward, the heads
+        # and the LSTM chain below; the main stream joins before the bucket
+        # all-reduce / the optimizer.
+        vae_done = self._vae_weight_grads_async(ws)
         # STN read backward of all steps against the shared input canvas
         ops.stn_backward(X, ws.th_f, (W, W), ws.dg_all, want_dU=False, dtheta=ws.dth_f_all,
                          n=TB)
@@ -628,7 +634,8 @@ class AIRModel:
                       transB=True)
         # the heads' and the VAE's weight gradients are final here: their
         # all-reduce bucket runs while the LSTM chain below computes
-        self._weight_grads_glimpse(ws)
+        self._weight_grads_heads(ws)
+        torch.cuda.current_stream().wait_event(vae_done)
         split = self._bucket_split()
         self._reduce_bucket(split, self.params.total)
         ws.dGsum.zero_()
@@ -911,11 +918,33 @@ class AIRModel:
     def _weight_grads_glimpse(self, ws):
         """Weight gradients of the VAE and the five heads (every loop step at
         once, K = T*B rows)."""
-        H, HS, TB = self.rnn_units, self.scale_hidden_units, ws.B * self.max_steps
         if self.precision == "bf16":
             self._vae_weight_grads_bf16(ws)
         else:
             self._vae_weight_grads_fp32(ws)
+        self._weight_grads_heads(ws)
+
+    def _vae_weight_grads_async(self, ws):
+        """The VAE weight gradients on the side stream (ordered after
+        everything issued so far on the current stream); returns the event
+        that marks their completion."""
+        main = torch.cuda.current_stream()
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        self._side.wait_event(ready)
+        with torch.cuda.stream(self._side):
+            if self.precision == "bf16":
+                self._vae_weight_grads_bf16(ws)
+            else:
+                self._vae_weight_grads_fp32(ws)
+            done = torch.cuda.Event()
+            done.record(self._side)
+        return done
+
+    def _weight_grads_heads(self, ws):
+        H, HS, TB = self.rnn_units, self.scale_hidden_units, ws.B * self.max_steps
         heads = list(enumerate(self._HEADS))
         self._dw([ws.h] * 5, [ws.dhid[zi] for zi, _ in heads],
                  [self._G(h + "/hidden/weights") for _, h in heads], TB, H, HS, H, HS,
