@@ -209,7 +209,9 @@ class AIRModel:
         self.fused_step = bool(fused_step) and precision == "bf16" and (
             windows_size == 28 and tuple(vae_recognition_units) == (512, 256)
             and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512))
-        # the glimpse VAE of all T steps after the loop, over T*B rows (AIR)
+        # the glimpse VAE of all T steps after the loop, over T*B rows (AIR).
+        # (Measured and not kept: step 0's VAE on a second stream under the
+        # rest of the recurrent loop -- no gain at B = 8192, slower at 64.)
         self.batch_vae = bool(batch_vae)
         if cnn:
             raise NotImplementedError(
@@ -475,34 +477,38 @@ class AIRModel:
         straddle two steps (B % 64)."""
         return self.batch_vae and B % 64 == 0
 
-    def _vae_forward_all(self, X, ws, lik_std):
-        B, T, C, W = ws.B, self.max_steps, self.canvas_size, self.windows_size
-        TB = T * B
+    def _vae_forward_all(self, X, ws, lik_std, t0=0, t1=None):
+        """The glimpse VAE (STN read -> VAE -> STN write into the canvas
+        parts) of loop steps [t0, t1) as one set of launches over their rows."""
+        B, C, W = ws.B, self.canvas_size, self.windows_size
+        t1 = self.max_steps if t1 is None else t1
+        T, TB = t1 - t0, (t1 - t0) * B
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        r_ = lambda a: a[t0:t1]  # noqa: E731
         if self.fused_step:
             self._pack_bf16()
             if self.windows_size != 28 or (R1, R2, Z, G1, G2) != (512, 256, 50, 256, 512):
                 raise ValueError("the fused step kernel is compiled for the reference VAE shape")
             wt = [self._wf[n] for n in self._VAE]
             gen = getattr(ws, "eps_x_offset", None) is not None
-            off = ws.eps_x_offset if gen else 0
+            off = ws.eps_x_offset + t0 * B * (W2 // 4) if gen else 0
             bias = [self._P("vae/" + n + "/biases") for n in self._VAE]
-            with self._timed("stn_vae_step_all"):
-                _ops.stn_vae_step_(TB, C, X, ws.th_f, ws.th_b, ws.zmask, ws.zval, ws.eps_z,
-                                   ws.eps_x, ops._i64(self.noise_seed), ops._i64(off), gen, wt,
-                                   bias, lik_std, float(self.vae_prior_mean),
-                                   float(self.vae_prior_variance), self.vae_prior_log_variance,
-                                   ws.cparts, ws.prows, None, ws.vkl, ws.gb, ws.a1b, ws.a2b,
-                                   ws.mu, ws.lv, ws.z, ws.zb, ws.d1b, ws.d2b, ws.r, B)
+            _ops.stn_vae_step_(TB, C, X, r_(ws.th_f), r_(ws.th_b), r_(ws.zmask), r_(ws.zval),
+                               r_(ws.eps_z), r_(ws.eps_x), ops._i64(self.noise_seed),
+                               ops._i64(off), gen, wt, bias, lik_std, float(self.vae_prior_mean),
+                               float(self.vae_prior_variance), self.vae_prior_log_variance,
+                               r_(ws.cparts), r_(ws.prows), None, r_(ws.vkl), r_(ws.gb),
+                               r_(ws.a1b), r_(ws.a2b), r_(ws.mu), r_(ws.lv), r_(ws.z), r_(ws.zb),
+                               r_(ws.d1b), r_(ws.d2b), r_(ws.r), B)
             return
-        v = lambda a: a.view(TB, -1)  # noqa: E731
+        v = lambda a: a[t0:t1].reshape(TB, -1)  # noqa: E731
         vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
         if self.precision == "bf16":
             from .ops import BF_SIGMOID_NOISE, BF_SOFTPLUS, BF_STORE, gemm_bf16
             Zp = self._pad8(Z)
             self._pack_bf16()
             wt = self._wt
-            for t in range(T):
+            for t in range(t0, t1):
                 ops.stn_forward(X, ws.th_f[t], (W, W), out=ws.gb[t])
             gemm_bf16([v(ws.gb)], [wt["recognition_1"]], [v(ws.a1b)], TB, R1, W2, W2, W2, R1,
                       epi=BF_SOFTPLUS, bias=[vb["recognition_1"]])
@@ -511,7 +517,7 @@ class AIRModel:
             gemm_bf16([v(ws.a2b), v(ws.a2b)], [wt["rec_mean"], wt["rec_log_variance"]],
                       [v(ws.mu), v(ws.lv)], TB, Z, R2, R2, R2, Z, epi=BF_STORE,
                       bias=[vb["rec_mean"], vb["rec_log_variance"]])
-            self._vae_sample_fwd_all(ws, v(ws.zb), Zp)
+            self._vae_sample_fwd_all(ws, v(ws.zb), Zp, t0, t1)
             gemm_bf16([v(ws.zb)], [wt["generative_1"]], [v(ws.d1b)], TB, G1, Zp, Zp, Zp, G1,
                       epi=BF_SOFTPLUS, bias=[vb["generative_1"]])
             gemm_bf16([v(ws.d1b)], [wt["generative_2"]], [v(ws.d2b)], TB, G2, G1, G1, G1, G2,
@@ -521,7 +527,7 @@ class AIRModel:
                       aux_scale=lik_std)
         else:
             vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
-            for t in range(T):
+            for t in range(t0, t1):
                 ops.stn_forward(X, ws.th_f[t], (W, W), out=ws.g[t])
             gemm([v(ws.g)], [vw["recognition_1"]], [v(ws.a1)], TB, R1, W2, W2, R1, R1,
                  epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]], Cpre=[v(ws.a1pre)])
@@ -530,7 +536,7 @@ class AIRModel:
             gemm([v(ws.a2), v(ws.a2)], [vw["rec_mean"], vw["rec_log_variance"]],
                  [v(ws.mu), v(ws.lv)], TB, Z, R2, R2, Z, Z,
                  bias=[vb["rec_mean"], vb["rec_log_variance"]])
-            self._vae_sample_fwd_all(ws, None, 0)
+            self._vae_sample_fwd_all(ws, None, 0, t0, t1)
             gemm([v(ws.z)], [vw["generative_1"]], [v(ws.d1)], TB, G1, Z, Z, G1, G1,
                  epi=EPI_SOFTPLUS, bias=[vb["generative_1"]], Cpre=[v(ws.d1pre)])
             gemm([v(ws.d1)], [vw["generative_2"]], [v(ws.d2)], TB, G2, G1, G1, G2, G2,
@@ -540,14 +546,17 @@ class AIRModel:
                  aux=[v(ws.eps_x)], ldaux=W2, aux_scale=lik_std)
         # STN write of every step into its canvas part (air_model.py:580-588);
         # the loss kernel adds the parts in step order (:665-675)
-        _ops.stn_write_parts_(v(ws.r), TB, W, W, ws.th_b, C, C, ws.zval, ws.zmask, ws.cparts,
-                              ws.prows)
+        _ops.stn_write_parts_(v(ws.r), TB, W, W, r_(ws.th_b), C, C, r_(ws.zval), r_(ws.zmask),
+                              r_(ws.cparts), r_(ws.prows))
 
-    def _vae_sample_fwd_all(self, ws, zb, ldzb):
-        TB = ws.B * self.max_steps
+    def _vae_sample_fwd_all(self, ws, zb, ldzb, t0=0, t1=None):
+        t1 = self.max_steps if t1 is None else t1
+        TB = ws.B * (t1 - t0)
+        r_ = lambda a: a[t0:t1]  # noqa: E731
         _ops.vae_sample_forward_(TB, self.vae_latent_dimensions, float(self.vae_prior_mean),
                                  float(self.vae_prior_variance), self.vae_prior_log_variance,
-                                 ws.mu, ws.lv, ws.eps_z, ws.z, zb, ldzb, ws.zmask, None, ws.vkl)
+                                 r_(ws.mu), r_(ws.lv), r_(ws.eps_z), r_(ws.z), zb, ldzb,
+                                 r_(ws.zmask), None, r_(ws.vkl))
 
     def _forward_loss(self, X, targets, ws, need_grad, outputs=True):
         """reconstruction loss (air_model.py:866-900) + batch means.  With
@@ -924,23 +933,26 @@ class AIRModel:
             self._vae_weight_grads_fp32(ws)
         self._weight_grads_heads(ws)
 
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
     def _vae_weight_grads_async(self, ws):
         """The VAE weight gradients on the side stream (ordered after
         everything issued so far on the current stream); returns the event
         that marks their completion."""
-        main = torch.cuda.current_stream()
-        if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(device=self.device)
+        main, side = torch.cuda.current_stream(), self._side_stream()
         ready = torch.cuda.Event()
         ready.record(main)
-        self._side.wait_event(ready)
-        with torch.cuda.stream(self._side):
+        side.wait_event(ready)
+        with torch.cuda.stream(side):
             if self.precision == "bf16":
                 self._vae_weight_grads_bf16(ws)
             else:
                 self._vae_weight_grads_fp32(ws)
             done = torch.cuda.Event()
-            done.record(self._side)
+            done.record(side)
         return done
 
     def _weight_grads_heads(self, ws):
