@@ -13,7 +13,8 @@ arithmetic throughout, air/vae.py:5-48, air/air_model.py:533-588), per-GPU
 batch 8192 (the batch configs[1] is quoted on).  Extra keys on the same line
 (rank 0, N = 1 only): ``configs_1_bf16`` (configs[1] itself: bf16 VAE, fp32
 elsewhere), ``config_1_batch64_fp32`` (the reference's own batch of 64),
-``fused_step_roofline`` / ``fused_step_roofline_c64`` (the north-star fused
+``fp32_step_roofline`` (the same step at reference precision against the fp32
+MFMA roof), ``fused_step_roofline`` / ``fused_step_roofline_c64`` (the north-star fused
 STN-read -> VAE -> STN-write kernel at B = 65,536, C = 50 and 64),
 ``roofline`` (dominant kernel of the headline step) and ``cpu_baseline``.
 
@@ -198,6 +199,55 @@ def fused_step_roofline(batch: int, launches: int, dev, canvas: int = 50):
     return out
 
 
+def vae_chain_flops_per_image(W2=784, R1=512, R2=256, Z=50, G1=256, G2=512) -> float:
+    """Dense-layer flops of one glimpse VAE pass (vae.py:5-48): 2.21 MFLOP."""
+    return 2.0 * (W2 * R1 + R1 * R2 + 2 * R2 * Z + Z * G1 + G1 * G2 + G2 * W2)
+
+
+def fp32_step_roofline(batch: int, launches: int, dev):
+    """SURVEY §8 D.3's fp32 step (STN read -> glimpse VAE -> STN write at
+    reference precision) at `batch` images, priced against the fp32 MFMA roof
+    (batch x 2.21 MFLOP; >= 919 us at 65,536).  This build runs it unfused: the
+    STN read, seven bit-exact fp32 GEMMs with fused epilogues, the latent
+    sample and the STN write into canvas parts (AIRModel._vae_forward_all,
+    one step over `batch` rows); timed with HIP events on the launch stream."""
+    from mog_air.air_model import AIRModel
+    m = AIRModel(max_steps=1, max_digits=1, canvas_size=50, scale_prior_variance=0.05,
+                 z_pres_prior_log_odds=-0.01, learning_rate=1e-4, gradient_clipping_norm=1.0,
+                 cnn=False, train=True, scope="fp32roof%d" % batch, device=dev,
+                 precision="fp32", seed=1235, noise_seed=79)
+    x, k = synthetic(batch, 4322, 50)
+    X = torch.from_numpy(x).to(dev)
+    K = torch.from_numpy(k).to(dev)
+    m.infer(X, K)
+    ws = m._ws
+    assert m._batched_vae(batch)
+    for _ in range(2):
+        m._vae_forward_all(X, ws, 0.3)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    evs = []
+    for _ in range(launches):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        m._vae_forward_all(X, ws, 0.3)
+        e1.record(s)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    avg = sum(a.elapsed_time(b) * 1e-3 for a, b in evs) / len(evs)
+    flop = batch * vae_chain_flops_per_image()
+    out = {"kernel": "fp32 STN read + VAE GEMM chain + STN write (unfused, bit-exact)",
+           "batch": batch, "bound": "mfma", "achieved": flop / avg / 1e12,
+           "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": flop / avg / 1e12 / FP32_MFMA_PEAK_TFLOPS, "launches": launches,
+           "avg_chain_us": avg * 1e6, "roof_us": flop / FP32_MFMA_PEAK_TFLOPS / 1e6,
+           "flop_per_image": vae_chain_flops_per_image()}
+    del m, ws
+    torch.cuda.empty_cache()
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -360,6 +410,8 @@ def main():
                                                                  args.roofline_launches, dev)
                 out["fused_step_roofline_c64"] = fused_step_roofline(
                     args.roofline_batch, args.roofline_launches, dev, canvas=64)
+                out["fp32_step_roofline"] = fp32_step_roofline(args.roofline_batch,
+                                                               args.roofline_launches, dev)
         if args.cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out), flush=True)
