@@ -113,10 +113,13 @@ int mog_air_step_forward(int B, int HS, int HZ, int step, int train, int use_num
                          float* zprob_out, float* zkl_out, float* skl_out, float* shkl_out,
                          float* zmask, float* zval, float* zc, void* stream);
 /* Backward of the above: writes dout [5][B, 2] and dhid [5][B, HS] (head
- * strides dout_hs / dhid_hs elements). */
+ * strides dout_hs / dhid_hs elements).  The KL terms this step added to the
+ * running loss are weighted by dloss[b] (the loss's cotangent per image), or by
+ * the scalar grad_scale when dloss is NULL (a batch-mean loss: 1 / B). */
 int mog_air_step_backward(int B, int HS, int train, int use_num_prior, float temperature,
                           float prior_lo, float prior_bias, float s_pm, float s_pv, float h_pm,
-                          float h_pv, float grad_scale, const float* rec, const float* eps_scale,
+                          float h_pv, float grad_scale, const float* dloss, const float* rec,
+                          const float* eps_scale,
                           const float* eps_shift, const float* dtheta_fwd,
                           const float* dtheta_back, const float* dot, const float* const* hid,
                           const float* const* w2, float* dout, long dout_hs, float* dhid,

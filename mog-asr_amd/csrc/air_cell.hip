@@ -252,6 +252,7 @@ struct StepBwdIO {
   const float* dtheta_fwd;  // [B,6] from STN-read backward
   const float* dtheta_back; // [B,6] from STN-write backward (already z*active scaled)
   const float* dot;         // [B] sum_p dcanvas*w  (canvas -> z_pres)
+  const float* dloss;       // [B] per-image cotangent of the running loss (or null: grad_scale)
   float* dout;              // [5][B, 2] grads wrt head outputs, head stride dout_hs
   long dout_hs;
 };
@@ -268,7 +269,7 @@ __global__ __launch_bounds__(256) void step_bwd_kernel(StepCfg cfg, StepBwdIO io
   const float ty = r[R_TY * B + b], y = r[R_Y * B + b], z = r[R_Z * B + b];
   const bool act_old = r[R_ACT_OLD * B + b] != 0.0f, act = r[R_ACT * B + b] != 0.0f;
   const bool live = r[R_LIVE * B + b] != 0.0f;
-  const float gL = cfg.grad_scale;
+  const float gL = io.dloss ? io.dloss[b] : cfg.grad_scale;
   const float T = cfg.temperature;
 
   // theta gradients -> (s, tx, ty)
@@ -655,8 +656,9 @@ extern "C" int mog_air_step_forward(
 extern "C" int mog_air_step_backward(int B, int HS, int train, int use_num_prior,
                                      float temperature, float prior_lo, float prior_bias,
                                      float s_pm, float s_pv, float h_pm, float h_pv,
-                                     float grad_scale, const float* rec, const float* eps_scale,
-                                     const float* eps_shift, const float* dtheta_fwd,
+                                     float grad_scale, const float* dloss, const float* rec,
+                                     const float* eps_scale, const float* eps_shift,
+                                     const float* dtheta_fwd,
                                      const float* dtheta_back, const float* dot,
                                      const float* const* hid, const float* const* w2,
                                      float* dout, long dout_hs, float* dhid, long dhid_hs,
@@ -669,7 +671,7 @@ extern "C" int mog_air_step_backward(int B, int HS, int train, int use_num_prior
   c.step = 0; c.thr = 0.0f; c.temperature = temperature; c.prior_lo = prior_lo;
   c.prior_bias = prior_bias; c.s_pm = s_pm; c.s_pv = s_pv; c.s_plv = 0.0f; c.h_pm = h_pm;
   c.h_pv = h_pv; c.h_plv = 0.0f; c.grad_scale = grad_scale;
-  StepBwdIO io{rec, eps_scale, eps_shift, dtheta_fwd, dtheta_back, dot, dout, dout_hs};
+  StepBwdIO io{rec, eps_scale, eps_shift, dtheta_fwd, dtheta_back, dot, dloss, dout, dout_hs};
   hipStream_t s = mog_stream(stream);
   step_bwd_kernel<<<mog_cdiv(B, 256), 256, 0, s>>>(c, io);
   HeadPtrs hp;

@@ -181,14 +181,15 @@ void air_step_forward_(int64_t B, int64_t HS, int64_t HZ, int64_t step, bool tra
 void air_step_backward_(int64_t B, int64_t HS, bool train, bool use_num_prior,
                         double temperature, double prior_lo, double prior_bias, double s_pm,
                         double s_pv, double h_pm, double h_pv, double grad_scale,
-                        const Tensor& rec, const Tensor& eps_scale, const Tensor& eps_shift,
+                        const optional<Tensor>& dloss, const Tensor& rec, const Tensor& eps_scale, const Tensor& eps_shift,
                         const Tensor& dtheta_fwd, const Tensor& dtheta_back, const Tensor& dot,
                         at::TensorList hid, at::TensorList w2, Tensor dout, int64_t dout_hs,
                         Tensor dhid, int64_t dhid_hs) {
   auto h = ptrs(hid), w = ptrs(w2);
   TORCH_CHECK(h.size() == 5 && w.size() == 5, "air_step_backward_: 5 heads");
   check(mog_air_step_backward(B, HS, train, use_num_prior, temperature, prior_lo, prior_bias, s_pm,
-                              s_pv, h_pm, h_pv, grad_scale, f(rec), f(eps_scale), f(eps_shift),
+                              s_pv, h_pm, h_pv, grad_scale, f(dloss), f(rec),
+                              f(eps_scale), f(eps_shift),
                               f(dtheta_fwd), f(dtheta_back), f(dot), arr<float>(h), arr<float>(w),
                               f(dout), dout_hs, f(dhid), dhid_hs, stream()),
         "air_step_backward_");
@@ -339,7 +340,8 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
   m.def(
       "air_step_backward_(int B, int HS, bool train, bool use_num_prior, float temperature, "
       "float prior_lo, float prior_bias, float s_pm, float s_pv, float h_pm, float h_pv, "
-      "float grad_scale, Tensor rec, Tensor eps_scale, Tensor eps_shift, Tensor dtheta_fwd, "
+      "float grad_scale, Tensor? dloss, Tensor rec, Tensor eps_scale, Tensor eps_shift, "
+      "Tensor dtheta_fwd, "
       "Tensor dtheta_back, Tensor dot, Tensor[] hid, Tensor[] w2, Tensor(a!) dout, int dout_hs, "
       "Tensor(b!) dhid, int dhid_hs) -> ()");
   m.def(

@@ -636,7 +636,7 @@ class AIRModel:
                 float(self.marginal[t]) if self.marginal is not None else 0.0,
                 float(self.scale_prior_mean), float(self.scale_prior_variance),
                 float(self.shift_prior_mean), float(self.shift_prior_variance), float(gscale),
-                ws.rec[t], ws.eps_scale[t], ws.eps_shift[t], ws.dth_f_all[t], ws.dth_b_all[t],
+                None, ws.rec[t], ws.eps_scale[t], ws.eps_shift[t], ws.dth_f_all[t], ws.dth_b_all[t],
                 ws.dot_all[t], hid_t, w2, ws.dout[0, t], T * B * 2, ws.dhid[0, t], T * B * HS)
         # dh[t] = sum_z dhid_z W1_z^T for every step: one chain over K = 5 * HS
         ops.gemm_kseg([ws.dhid[z] for z in range(5)], w1, ws.dh, TB, H, HS, HS, HS, H,

@@ -21,6 +21,10 @@ Ops (reference counterpart):
                lik_std) -> [canvas_part[B,C*C], r, mu, logvar, z, vae_kl, *saved]
       the fused bf16 STN-read -> VAE -> STN-write step (air_model.py:523-588, vae.py:5-48);
       differentiable in theta_f, theta_b, z_pres, W, b through canvas_part
+  air_step(h[B,H], W1[5], b1[5], W2[5], b2[5], eps_scale, eps_shift, u, stop, runloss, digits,
+           live, cfg[10], train, use_num_prior) -> [theta_f, theta_b, zc, zmask, runloss, ...]
+      one loop step's five heads + concrete z_pres + KLs (air_model.py:458-520, 552-705);
+      differentiable in h, W1, b1, W2, b2 through theta_f, theta_b, zc and runloss
   tf_adam_clip_(flat params, grads, m, v, lr, clip, beta1, beta2, eps, step)  air_model.py:941-999
 """
 from __future__ import annotations
@@ -31,6 +35,7 @@ import numpy as np
 import torch
 
 from . import _lib, ops
+from .air_model import R_NREC
 from .ops import (BF_ATOMIC, BF_SOFTPLUS_BWD, BF_STORE, EPI_ATOMIC, EPI_RELU, EPI_SIGMOID_NOISE,
                   EPI_SOFTPLUS, EPI_SOFTPLUS_BWD, EPI_STORE, gemm, gemm_bf16)
 
@@ -398,6 +403,118 @@ def _svs_bwd(ctx, grads):
 
 
 stn_vae_step.register_autograd(_svs_bwd, setup_context=_svs_setup)
+
+
+# ------------------------------------------- heads + concrete z_pres step ----
+# cfg order of air_step (floats): stopping threshold, concrete temperature,
+# z_pres prior log-odds, its per-step bias (num prior), scale prior mean /
+# variance / log-variance, shift prior mean / variance / log-variance
+AIR_STEP_CFG = ("thr", "temperature", "prior_lo", "prior_bias", "s_pm", "s_pv", "s_plv", "h_pm",
+                "h_pv", "h_plv")
+
+
+@torch.library.custom_op("mog_air::air_step", mutates_args=())
+def air_step(h: torch.Tensor, W1: List[torch.Tensor], b1: List[torch.Tensor],
+             W2: List[torch.Tensor], b2: List[torch.Tensor], eps_scale: torch.Tensor,
+             eps_shift: torch.Tensor, u: torch.Tensor, stop: torch.Tensor, runloss: torch.Tensor,
+             digits: torch.Tensor, live: torch.Tensor, cfg: List[float], train: bool,
+             use_num_prior: bool) -> List[torch.Tensor]:
+    """One loop step's heads and concrete z_pres (SURVEY §8 B heads_fwd +
+    concrete_fwd; air_model.py:458-520 heads, scale / shift sampling and theta,
+    :552-577 theta^-1, :590-663 concrete z_pres and its KL, :677-705 scale /
+    shift KLs): the five ReLU hidden layers in one batched launch, then the
+    step kernel.  h [B,H] is the LSTM output; W1/b1 [H,HS]/[HS] and W2/b2
+    [HS,k]/[k] are the five heads (scale-mean, scale-logvar, shift-mean,
+    shift-logvar, z_pres log-odds; k = 2 for the shift heads).  State in:
+    stop / runloss [B] f32, digits [B] int32, live [1] int32 (is step t live).
+    Returns [theta_f, theta_b, zc, zmask, runloss, stop, digits, live, zprob,
+    scale, shift, zkl, skl, shkl, rec, hid]: zc = active ? z_pres : 0 is the
+    canvas coefficient.  Differentiable in h, W1, b1, W2, b2 (and runloss)
+    through theta_f, theta_b, zc and runloss; the discrete state and the
+    reporting outputs carry no gradient."""
+    _need_hip(h, eps_scale, eps_shift, u, stop, runloss, *W1, *b1, *W2, *b2)
+    if len(W1) != 5 or len(b1) != 5 or len(W2) != 5 or len(b2) != 5 or len(cfg) != 10:
+        raise ValueError("air_step takes five heads and ten cfg floats")
+    if digits.dtype != torch.int32 or live.dtype != torch.int32 or live.numel() != 1:
+        raise ValueError("air_step: digits [B] and live [1] are int32")
+    B, H = h.shape
+    HS = W1[0].shape[1]
+    dev = h.device
+    f32 = dict(device=dev, dtype=torch.float32)
+    hid = torch.empty((5, B, HS), **f32)
+    gemm([h] * 5, list(W1), [hid[z] for z in range(5)], B, HS, H, H, HS, HS, epi=EPI_RELU,
+         bias=list(b1))
+    stop_o, rl_o, dig_o = stop.clone(), runloss.clone(), digits.clone()
+    live_o = torch.zeros(2, device=dev, dtype=torch.int32)
+    live_o[:1] = live
+    rec = torch.empty((R_NREC, B), **f32)
+    th_f, th_b = torch.empty((B, 6), **f32), torch.empty((B, 6), **f32)
+    e = lambda *sh: torch.empty(sh, **f32)  # noqa: E731
+    scale, shift, zprob, zkl, skl, shkl = e(B), e(B, 2), e(B), e(B), e(B), e(B)
+    zmask, zval, zc = e(B), e(B), e(B)
+    thr, temp, plo, pb, s_pm, s_pv, s_plv, h_pm, h_pv, h_plv = (float(c) for c in cfg)
+    _ops.air_step_forward_(B, HS, HS, 0, train, use_num_prior, thr, temp, plo, pb, s_pm, s_pv,
+                           s_plv, h_pm, h_pv, h_plv, [hid[z] for z in range(5)], list(W2),
+                           list(b2), eps_scale, eps_shift, u, stop_o, rl_o, dig_o, live_o, rec,
+                           th_f, th_b, scale, shift, zprob, zkl, skl, shkl, zmask, zval, zc)
+    return [th_f, th_b, zc, zmask, rl_o, stop_o, dig_o, live_o[1:].clone(), zprob, scale, shift,
+            zkl, skl, shkl, rec, hid]
+
+
+@air_step.register_fake
+def _(h, W1, b1, W2, b2, eps_scale, eps_shift, u, stop, runloss, digits, live, cfg, train,
+      use_num_prior):
+    B, HS = h.shape[0], W1[0].shape[1]
+    n = lambda *sh: h.new_empty(sh)  # noqa: E731
+    return [n(B, 6), n(B, 6), n(B), n(B), n(B), n(B), digits.new_empty(B), live.new_empty(1),
+            n(B), n(B), n(B, 2), n(B), n(B), n(B), n(R_NREC, B), n(5, B, HS)]
+
+
+def _as_setup(ctx, inputs, output):
+    h, W1, b1, W2, b2, eps_scale, eps_shift, u, stop, runloss, digits, live, cfg, train, \
+        use_num_prior = inputs
+    ctx.cfg, ctx.train, ctx.use_num_prior = list(cfg), train, use_num_prior
+    ctx.ks = [w.shape[1] for w in W2]
+    ctx.save_for_backward(h, eps_scale, eps_shift, output[14], output[15], *W1, *W2)
+    ctx.set_materialize_grads(False)
+
+
+def _as_bwd(ctx, grads):
+    """mog_air_step_backward with the per-image cotangent of the running loss
+    (dloss) weighting this step's KL terms, then the heads: dh = sum_z dhid_z
+    W1_z^T (one k-ordered chain), dW1 / db1 = h^T dhid, dW2 / db2 = hid^T dout
+    (split-K atomics with fused column sums)."""
+    h, eps_scale, eps_shift, rec, hid, *W = ctx.saved_tensors
+    W1, W2 = W[:5], W[5:]
+    B, H = h.shape
+    HS = hid.shape[2]
+    f32 = dict(device=h.device, dtype=torch.float32)
+    zeros = lambda *s: torch.zeros(s, **f32)  # noqa: E731
+    g = lambda i, *s: zeros(*s) if grads[i] is None else grads[i].contiguous()  # noqa: E731
+    dth_f, dth_b, dzc, drl = g(0, B, 6), g(1, B, 6), g(2, B), g(4, B)
+    thr, temp, plo, pb, s_pm, s_pv, s_plv, h_pm, h_pv, h_plv = (float(c) for c in ctx.cfg)
+    dout, dhid = torch.empty((5, B, 2), **f32), torch.empty((5, B, HS), **f32)
+    hid_l = [hid[z] for z in range(5)]
+    _ops.air_step_backward_(B, HS, ctx.train, ctx.use_num_prior, temp, plo, pb, s_pm, s_pv, h_pm,
+                            h_pv, 0.0, drl, rec, eps_scale, eps_shift, dth_f, dth_b, dzc, hid_l,
+                            list(W2), dout[0], B * 2, dhid[0], B * HS)
+    dh = torch.empty((B, H), **f32)
+    ops.gemm_kseg([dhid[z] for z in range(5)], list(W1), dh, B, H, HS, HS, HS, H, transB=True)
+    gW1, gb1 = [zeros(H, HS) for _ in range(5)], [zeros(HS) for _ in range(5)]
+    splitk = max(1, B // 256)
+    gemm([h] * 5, [dhid[z] for z in range(5)], gW1, H, HS, B, H, HS, HS, transA=True,
+         epi=EPI_ATOMIC, splitk=splitk, colsum=gb1)
+    gW2, gb2 = [zeros(HS, k) for k in ctx.ks], [zeros(k) for k in ctx.ks]
+    for k in (1, 2):
+        sel = [z for z in range(5) if ctx.ks[z] == k]
+        if sel:
+            gemm([hid[z] for z in sel], [dout[z] for z in sel], [gW2[z] for z in sel], HS, k, B,
+                 HS, 2, k, transA=True, epi=EPI_ATOMIC, splitk=splitk,
+                 colsum=[gb2[z] for z in sel])
+    return (dh, gW1, gb1, gW2, gb2, None, None, None, None, drl, None, None, None, None, None)
+
+
+air_step.register_autograd(_as_bwd, setup_context=_as_setup)
 
 
 # ----------------------------------------------------------- optimizer ----

@@ -269,3 +269,185 @@ def test_air_model_dispatches_through_torch_ops():
                   "mog_air.stn_backward_sigmoid_"} if prec == "bf16"
                  else {"mog_air.stn_forward_", "mog_air.vae_sample_forward_"})
         assert want <= rec.names, sorted(want - rec.names)
+
+
+# ------------------------------------------------ heads + concrete step op ----
+_STEP_CFG = [0.99, 1.0, -2.0, 0.3, -1.0, 0.05, float(np.log(0.05)), 0.0, 1.0, 0.0]
+
+
+def _air_step_inputs(seed, B=96, H=256, HS=64):
+    rng = np.random.default_rng(seed)
+    t = lambda a: torch.tensor(np.asarray(a, np.float32), device=DEV)  # noqa: E731
+    h = t(rng.standard_normal((B, H)) * 0.5)
+    W1 = [t(rng.standard_normal((H, HS)) * 0.08) for _ in range(5)]
+    b1 = [t(rng.standard_normal(HS) * 0.05) for _ in range(5)]
+    ks = (1, 1, 2, 2, 1)
+    W2 = [t(rng.standard_normal((HS, k)) * 0.1) for k in ks]
+    b2 = [t(rng.standard_normal(k) * 0.1) for k in ks]
+    es, eh = t(rng.standard_normal(B)), t(rng.standard_normal((B, 2)))
+    u = t(rng.uniform(0.05, 0.95, B))
+    stop = t(rng.choice([0.0, 0.4, 1.5], B))
+    rl = t(rng.standard_normal(B))
+    dig = torch.tensor(rng.integers(0, 3, B).astype(np.int32), device=DEV)
+    live = torch.ones(1, device=DEV, dtype=torch.int32)
+    return h, W1, b1, W2, b2, es, eh, u, stop, rl, dig, live
+
+
+def _step_c_abi(h, W1, b1, W2, b2, es, eh, u, stop, rl, dig, live, cfg, num_prior):
+    """The AIRModel's launch sequence for one step (hidden GEMM + step kernel)."""
+    from mog_air import ops
+    from mog_air.air_model import R_NREC
+    B, H = h.shape
+    HS = W1[0].shape[1]
+    e = lambda *s: torch.empty(s, device=DEV)  # noqa: E731
+    hid = e(5, B, HS)
+    ops.gemm([h] * 5, W1, [hid[z] for z in range(5)], B, HS, H, H, HS, HS, epi=ops.EPI_RELU,
+             bias=b1)
+    st, r, d = stop.clone(), rl.clone(), dig.clone()
+    lv = torch.zeros(2, device=DEV, dtype=torch.int32)
+    lv[0] = live[0]
+    outs = dict(rec=e(R_NREC, B), th_f=e(B, 6), th_b=e(B, 6), scale=e(B), shift=e(B, 2),
+                zprob=e(B), zkl=e(B), skl=e(B), shkl=e(B), zmask=e(B), zval=e(B), zc=e(B))
+    torch.ops.mog_air.air_step_forward_(
+        B, HS, HS, 0, True, num_prior, *cfg, [hid[z] for z in range(5)], W2, b2, es, eh, u, st, r,
+        d, lv, outs["rec"], outs["th_f"], outs["th_b"], outs["scale"], outs["shift"],
+        outs["zprob"], outs["zkl"], outs["skl"], outs["shkl"], outs["zmask"], outs["zval"],
+        outs["zc"])
+    outs.update(hid=hid, stop=st, runloss=r, digits=d, live=lv[1:])
+    return outs
+
+
+def _step64(h, W1, b1, W2, b2, es, eh, u, stop, rl, cfg, num_prior):
+    """float64 torch restatement of one step (air_model.py:458-520, 552-705)."""
+    thr, T, plo, pb, s_pm, s_pv, s_plv, h_pm, h_pv, h_plv = cfg
+    hid = [torch.relu(h @ W1[z] + b1[z]) for z in range(5)]
+    o = [hid[z] @ W2[z] + b2[z] for z in range(5)]
+    sm, slv, lo, hm, hv = o[0][:, 0], o[1][:, 0], o[4][:, 0], o[2], o[3]
+    s = torch.sigmoid(sm + es * torch.sqrt(torch.exp(slv)))
+    tt = torch.tanh(hm + eh * torch.sqrt(torch.exp(hv)))
+    tx, ty = tt[:, 0], tt[:, 1]
+    zero = torch.zeros_like(s)
+    thf = torch.stack([s, zero, tx, zero, s, ty], 1)
+    thb = torch.stack([1 / s, zero, -tx / s, zero, 1 / s, -ty / s], 1)
+    y = (lo + (torch.log(u + 1e-9) - torch.log((1 - u) + 1e-9))) / T
+    z = torch.sigmoid(y)
+    zkl = at.concrete_kl(y, plo + pb, T, lo, T)
+    kl_end = at.concrete_kl(y, -100.0, T, lo, T) if num_prior else zero
+    act = (stop + (1 - z.detach())) < thr
+    skl = 0.5 * ((((s_plv - slv) - 1) + torch.exp(slv) / s_pv) + (sm - s_pm) ** 2 / s_pv)
+    g = lambda m, v: (((h_plv - v) - 1) + torch.exp(v) / h_pv) + (m - h_pm) ** 2 / h_pv  # noqa
+    shkl = 0.5 * (g(hm[:, 0], hv[:, 0]) + g(hm[:, 1], hv[:, 1]))
+    rl_out = rl + torch.where(stop < thr, zkl, kl_end) + torch.where(act, skl + shkl, zero)
+    return thf, thb, torch.where(act, z, zero), rl_out, act
+
+
+@pytest.mark.parametrize("num_prior", [False, True])
+def test_air_step_op_matches_c_abi_bitwise(num_prior):
+    """torch.ops.mog_air.air_step (heads + concrete z_pres step) against the
+    AIRModel's C-ABI launch sequence: every output bitwise; its autograd
+    against mog_air_step_backward with the scalar grad_scale (dh bitwise,
+    the split-K weight gradients to fp32 rounding)."""
+    from mog_air import ops
+    ins = _air_step_inputs(5 + num_prior)
+    h, W1, b1, W2, b2, es, eh, u, stop, rl, dig, live = ins
+    ref = _step_c_abi(*ins, _STEP_CFG, num_prior)
+    hq = h.clone().requires_grad_()
+    W1q = [w.clone().requires_grad_() for w in W1]
+    W2q = [w.clone().requires_grad_() for w in W2]
+    b1q = [w.clone().requires_grad_() for w in b1]
+    b2q = [w.clone().requires_grad_() for w in b2]
+    out = torch.ops.mog_air.air_step(hq, W1q, b1q, W2q, b2q, es, eh, u, stop, rl, dig, live,
+                                     _STEP_CFG, True, num_prior)
+    names = ["th_f", "th_b", "zc", "zmask", "runloss", "stop", "digits", "live", "zprob", "scale",
+             "shift", "zkl", "skl", "shkl", "rec", "hid"]
+    for n, o in zip(names, out):
+        np.testing.assert_array_equal(o.detach().cpu().numpy(), ref[n].cpu().numpy(), err_msg=n)
+    B = h.shape[0]
+    rng = np.random.default_rng(9)
+    Gf = torch.tensor(rng.standard_normal((B, 6)).astype(np.float32), device=DEV)
+    Gb = torch.tensor(rng.standard_normal((B, 6)).astype(np.float32), device=DEV)
+    Gz = torch.tensor(rng.standard_normal(B).astype(np.float32), device=DEV)
+    gs = 1.0 / B
+    loss = (out[0] * Gf).sum() + (out[1] * Gb).sum() + (out[2] * Gz).sum() + out[4].sum() * gs
+    grads = torch.autograd.grad(loss, [hq, *W1q, *b1q, *W2q, *b2q])
+    HS = W1[0].shape[1]
+    dout, dhid = torch.empty((5, B, 2), device=DEV), torch.empty((5, B, HS), device=DEV)
+    thr, T, plo, pb, s_pm, s_pv, s_plv, h_pm, h_pv, h_plv = _STEP_CFG
+    hid_l = [ref["hid"][z] for z in range(5)]
+    torch.ops.mog_air.air_step_backward_(B, HS, True, num_prior, T, plo, pb, s_pm, s_pv, h_pm,
+                                         h_pv, gs, None, ref["rec"], es, eh, Gf, Gb, Gz, hid_l,
+                                         W2, dout[0], B * 2, dhid[0], B * HS)
+    dh = torch.empty_like(h)
+    ops.gemm_kseg([dhid[z] for z in range(5)], W1, dh, B, h.shape[1], HS, HS, HS, h.shape[1],
+                  transB=True)
+    np.testing.assert_array_equal(grads[0].cpu().numpy(), dh.cpu().numpy())
+    for z in range(5):
+        np.testing.assert_allclose(grads[1 + z].cpu().numpy(),
+                                   (h.T @ dhid[z]).cpu().numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(grads[11 + z].cpu().numpy(),
+                                   (ref["hid"][z].T @ dout[z][:, :W2[z].shape[1]]).cpu().numpy(),
+                                   rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(grads[16 + z].cpu().numpy(),
+                                   dout[z][:, :W2[z].shape[1]].sum(0).cpu().numpy(),
+                                   rtol=1e-4, atol=1e-6)
+
+
+def test_air_step_op_autograd_vs_float64():
+    """Per-image running-loss cotangents (dloss) included: gradients of the op
+    against float64 autograd of the restated step."""
+    ins = _air_step_inputs(11)
+    h, W1, b1, W2, b2, es, eh, u, stop, rl, dig, live = ins
+    req = lambda ts: [t.clone().requires_grad_() for t in ts]  # noqa: E731
+    hq, W1q, b1q, W2q, b2q = req([h])[0], req(W1), req(b1), req(W2), req(b2)
+    out = torch.ops.mog_air.air_step(hq, W1q, b1q, W2q, b2q, es, eh, u, stop, rl, dig, live,
+                                     _STEP_CFG, True, True)
+    B = h.shape[0]
+    rng = np.random.default_rng(12)
+    G = [torch.tensor(rng.standard_normal(s).astype(np.float32), device=DEV)
+         for s in ((B, 6), (B, 6), (B,), (B,))]
+    loss = sum((o * g).sum() for o, g in zip((out[0], out[1], out[2], out[4]), G))
+    grads = torch.autograd.grad(loss, [hq, *W1q, *b1q, *W2q, *b2q])
+    d = lambda ts: [t.detach().cpu().double().requires_grad_() for t in ts]  # noqa: E731
+    h6, W16, b16, W26, b26 = d([h])[0], d(W1), d(b1), d(W2), d(b2)
+    c = lambda t: t.cpu().double()  # noqa: E731
+    thf, thb, zc, rlo, act = _step64(h6, W16, b16, W26, b26, c(es), c(eh), c(u), c(stop), c(rl),
+                                     _STEP_CFG, True)
+    np.testing.assert_array_equal(act.numpy(), out[3].detach().cpu().numpy() != 0)
+    np.testing.assert_allclose(out[4].detach().cpu().numpy(), rlo.detach().numpy(), rtol=1e-4,
+                               atol=1e-4)
+    l64 = sum((o * c(g)).sum() for o, g in zip((thf, thb, zc, rlo), G))
+    g64 = torch.autograd.grad(l64, [h6, *W16, *b16, *W26, *b26])
+    for i, (a, b) in enumerate(zip(grads, g64)):
+        bn = b.numpy()
+        tol = 2e-3 * max(1.0, float(np.abs(bn).max()))
+        np.testing.assert_allclose(a.cpu().numpy(), bn, rtol=2e-3, atol=tol, err_msg=str(i))
+
+
+def test_air_step_backward_per_image_dloss():
+    """mog_air_step_backward's dloss: each image's head-output gradient equals
+    the one a uniform grad_scale of that image's value gives (bitwise)."""
+    ins = _air_step_inputs(13)
+    h, W1, b1, W2, b2, es, eh, u, stop, rl, dig, live = ins
+    ref = _step_c_abi(*ins, _STEP_CFG, True)
+    B, HS = h.shape[0], W1[0].shape[1]
+    rng = np.random.default_rng(14)
+    Gf = torch.tensor(rng.standard_normal((B, 6)).astype(np.float32), device=DEV)
+    Gb = torch.tensor(rng.standard_normal((B, 6)).astype(np.float32), device=DEV)
+    Gz = torch.tensor(rng.standard_normal(B).astype(np.float32), device=DEV)
+    thr, T, plo, pb, s_pm, s_pv, s_plv, h_pm, h_pv, h_plv = _STEP_CFG
+    hid_l = [ref["hid"][z] for z in range(5)]
+
+    def run(gs, dl):
+        dout, dhid = torch.empty((5, B, 2), device=DEV), torch.empty((5, B, HS), device=DEV)
+        torch.ops.mog_air.air_step_backward_(B, HS, True, True, T, plo, pb, s_pm, s_pv, h_pm,
+                                             h_pv, gs, dl, ref["rec"], es, eh, Gf, Gb, Gz, hid_l,
+                                             W2, dout[0], B * 2, dhid[0], B * HS)
+        return dout.cpu().numpy(), dhid.cpu().numpy()
+
+    odd = np.arange(B) % 2 == 1
+    dl = torch.tensor(np.where(odd, 2.0, 0.5).astype(np.float32), device=DEV)
+    mix = run(0.0, dl)
+    for v, rows in ((0.5, ~odd), (2.0, odd)):
+        uni = run(v, None)
+        for a, b in zip(mix, uni):
+            np.testing.assert_array_equal(a[:, rows], b[:, rows])

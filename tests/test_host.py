@@ -54,6 +54,22 @@ def test_torch_ops_extension_registers_every_launch_op():
         torch.ops.mog_air.rng_fill_(torch.zeros(4), 1, 0, True)
 
 
+def test_functional_ops_registered_and_refuse_cpu():
+    """mog_air/torch_ops.py: the differentiable functional ops are registered
+    on import and raise on CPU tensors (no CPU implementation)."""
+    import mog_air.torch_ops  # noqa: F401
+    for n in ("stn", "stn_backward", "lstm_cell", "dense", "glimpse_vae", "stn_vae_step",
+              "air_step", "tf_adam_clip_"):
+        getattr(torch.ops.mog_air, n).default
+    z = torch.zeros(4, 8)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        torch.ops.mog_air.air_step(z, [torch.zeros(8, 2)] * 5, [torch.zeros(2)] * 5,
+                                   [torch.zeros(2, 1)] * 5, [torch.zeros(1)] * 5, torch.zeros(4),
+                                   torch.zeros(4, 2), torch.zeros(4), torch.zeros(4),
+                                   torch.zeros(4), torch.zeros(4, dtype=torch.int32),
+                                   torch.ones(1, dtype=torch.int32), [0.0] * 10, True, False)
+
+
 def test_host_only_entry_point():
     from mog_air import _lib
     assert _lib.load().mog_optim_chunk_elems() == 4096
