@@ -15,7 +15,8 @@ batch 8192 (the batch configs[1] is quoted on).  Extra keys on the same line
 elsewhere), ``config_1_batch64_fp32`` (the reference's own batch of 64),
 ``fp32_step_roofline`` (the same step at reference precision against the fp32
 MFMA roof), ``fused_step_roofline`` / ``fused_step_roofline_c64`` (the north-star fused
-STN-read -> VAE -> STN-write kernel at B = 65,536, C = 50 and 64),
+STN-read -> VAE -> STN-write kernel at B = 65,536, C = 50 and 64, training form),
+``fused_step_roofline_fwd`` (its forward-only form, C = 50),
 ``roofline`` (dominant kernel of the headline step) and ``cpu_baseline``.
 
 ``python bench.py --gpus N`` without a torch.distributed launcher starts the
@@ -157,14 +158,16 @@ def timed_train(precision, B, steps, warmup, dev, world=1, rank=0, events=False,
     return time.perf_counter() - t0, model
 
 
-def fused_step_roofline(batch: int, launches: int, dev, canvas: int = 50):
+def fused_step_roofline(batch: int, launches: int, dev, canvas: int = 50, save: bool = True):
     """North-star measurement (BASELINE.json): the fused STN-read -> glimpse VAE
     -> STN-write step kernel alone at `batch` images on this GPU, inputs
     resident in HBM (theta / masks from one forward pass of a bf16 model on
     the same synthetic canvases).  Timed with HIP events on the stream the
     kernel is launched on; algorithmic bytes per image-step from SURVEY.md §8
-    D.3 (30,024 at C = 50, 49,176 at C = 64)."""
-    m = make_model("bf16", dev, 1, 0, "roofline%d_%d" % (batch, canvas), canvas=canvas)
+    D.3 (30,024 at C = 50, 49,176 at C = 64).  save=True: the training form,
+    which also writes the backward's saved activations (SAVED_BYTES per
+    image-step on top); save=False: the forward-only form (evaluation)."""
+    m = make_model("bf16", dev, 1, 0, "roofline%d_%d_%d" % (batch, canvas, save), canvas=canvas)
     m.noise_seed = 78
     x, k = synthetic(batch, 4321, canvas)
     X = torch.from_numpy(x).to(dev)
@@ -172,7 +175,7 @@ def fused_step_roofline(batch: int, launches: int, dev, canvas: int = 50):
     m.infer(X, K)
     ws = m._ws
     for t in range(3):
-        m._step_fused(X, ws, t, 0.3)
+        m._step_fused(X, ws, t, 0.3, save=save)
     torch.cuda.synchronize()
     s = torch.cuda.current_stream()
     evs = []
@@ -180,7 +183,7 @@ def fused_step_roofline(batch: int, launches: int, dev, canvas: int = 50):
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(s)
-        m._step_fused(X, ws, i % 3, 0.3)
+        m._step_fused(X, ws, i % 3, 0.3, save=save)
         e1.record(s)
         evs.append((e0, e1))
     torch.cuda.synchronize()
@@ -188,15 +191,24 @@ def fused_step_roofline(batch: int, launches: int, dev, canvas: int = 50):
     avg = sum(durs) / len(durs)
     per = fused_bytes_per_image_step(canvas * canvas)
     achieved = batch * per / 1e9 / avg
-    tag = "stn_vae_step_b%d" % batch + ("" if canvas == 50 else "_c%d" % canvas)
-    out = {"kernel": "stn_vae_step", "batch": batch, "canvas": canvas, "bound": "hbm",
+    tag = "stn_vae_step_b%d" % batch + ("" if canvas == 50 else "_c%d" % canvas) + \
+        ("" if save else "_fwd")
+    out = {"kernel": "stn_vae_step", "mode": "train" if save else "forward-only",
+           "batch": batch, "canvas": canvas, "bound": "hbm",
            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(tag), "launches": launches,
            "avg_launch_us": avg * 1e6, "algorithmic_bytes_per_launch": batch * per,
            "algorithmic_bytes_per_image_step": per}
+    if save:
+        out["saved_activation_bytes_per_image_step"] = SAVED_BYTES
     del m, ws
     torch.cuda.empty_cache()
     return out
+
+
+# bytes per image-step of the backward's saved activations the training form
+# also writes: glimpse, a1, a2, d1, d2 (bf16), mu / logvar (fp32), z bf16 copy
+SAVED_BYTES = 2 * (784 + 512 + 256 + 256 + 512) + 4 * 2 * 50 + 2 * 56
 
 
 def vae_chain_flops_per_image(W2=784, R1=512, R2=256, Z=50, G1=256, G2=512) -> float:
@@ -410,6 +422,8 @@ def main():
                                                                  args.roofline_launches, dev)
                 out["fused_step_roofline_c64"] = fused_step_roofline(
                     args.roofline_batch, args.roofline_launches, dev, canvas=64)
+                out["fused_step_roofline_fwd"] = fused_step_roofline(
+                    args.roofline_batch, args.roofline_launches, dev, save=False)
                 out["fp32_step_roofline"] = fp32_step_roofline(args.roofline_batch,
                                                                args.roofline_launches, dev)
         if args.cpu_baseline and world == 1:

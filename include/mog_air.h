@@ -156,7 +156,10 @@ int mog_air_runloss(int T, int B, const float* rec, long rec_step_stride, const 
  * from `eps_x` [B,784] when eps_gen == 0; otherwise generated in-kernel as the
  * Philox normals mog_rng_fill(eps_x, B*784, eps_seed, eps_offset, 1) would
  * have written (bit-identical; eps_x may then be NULL).  Saved for the
- * backward: gb/a1b/a2b/zb/d1b/d2b (bf16, zb row stride 56), mu/lv/z/r (fp32).
+ * backward: gb/a1b/a2b/zb/d1b/d2b (bf16, zb row stride 56), mu/lv/z (fp32) --
+ * all of them but z NULL for a forward-only step (evaluation / inference: the
+ * kernel then moves only the step's own bytes; z, the reported latents, is
+ * written when given); r (fp32) is always written.
  * Shapes must be the reference defaults (W 28, 512/256, Z 50, 256/512):
  * anything else returns MOG_ERR_INVALID.  Replaces the per-step sequence
  * air_model.py:523-588 (stn_forward + 6 GEMMs + vae_sample + stn accumulate).

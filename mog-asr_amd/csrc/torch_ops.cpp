@@ -240,9 +240,12 @@ void stn_vae_step_(int64_t B, int64_t C, const Tensor& x, const Tensor& theta_f,
                    const Tensor& eps_z, const optional<Tensor>& eps_x, int64_t eps_seed,
                    int64_t eps_offset, bool eps_gen, at::TensorList wt, at::TensorList bias,
                    double lik_std, double v_pm, double v_pv, double v_plv, Tensor canvas_part,
-                   Tensor part_rows, const optional<Tensor>& runloss, Tensor vkl, Tensor gb,
-                   Tensor a1b, Tensor a2b, Tensor mu, Tensor lv, Tensor z, Tensor zb, Tensor d1b,
-                   Tensor d2b, Tensor r, int64_t x_period) {
+                   Tensor part_rows, const optional<Tensor>& runloss, Tensor vkl,
+                   const optional<Tensor>& gb, const optional<Tensor>& a1b,
+                   const optional<Tensor>& a2b, const optional<Tensor>& mu,
+                   const optional<Tensor>& lv, const optional<Tensor>& z,
+                   const optional<Tensor>& zb, const optional<Tensor>& d1b,
+                   const optional<Tensor>& d2b, Tensor r, int64_t x_period) {
   auto w = ptrs(wt), b = ptrs(bias);
   TORCH_CHECK(w.size() == 7 && b.size() == 7, "stn_vae_step_: 7 VAE layers");
   check(mog_stn_vae_step_forward(B, C, 28, 512, 256, 50, 256, 512, f(x), f(theta_f), f(theta_b),
@@ -364,8 +367,8 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "Tensor zval, Tensor eps_z, Tensor? eps_x, int eps_seed, int eps_offset, bool eps_gen, "
       "Tensor[] wt, Tensor[] bias, float lik_std, float v_pm, float v_pv, float v_plv, "
       "Tensor(a!) canvas_part, Tensor(b!) part_rows, Tensor(c!)? runloss, Tensor(d!) vkl, "
-      "Tensor(e!) gb, Tensor(f!) a1b, Tensor(g!) a2b, Tensor(h!) mu, Tensor(i!) lv, "
-      "Tensor(j!) z, Tensor(k!) zb, Tensor(l!) d1b, Tensor(m!) d2b, Tensor(n!) r, "
+      "Tensor(e!)? gb, Tensor(f!)? a1b, Tensor(g!)? a2b, Tensor(h!)? mu, Tensor(i!)? lv, "
+      "Tensor(j!)? z, Tensor(k!)? zb, Tensor(l!)? d1b, Tensor(m!)? d2b, Tensor(n!) r, "
       "int x_period=0) -> ()");
   m.def(
       "recon_loss_(Tensor x, Tensor? canvas, Tensor? parts, int nparts, int part_stride, "

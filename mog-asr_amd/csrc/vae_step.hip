@@ -705,10 +705,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
         const float mv = sMu[m * 50 + k];
         const float var = mog_expf(l);
         zv = mv + ez[it] * sqrtf(var);
-        p.mu[o] = mv;
-        p.lv[o] = l;
-        p.z[o] = zv;
-        p.zb[(size_t)(b0 + m) * 56 + k] = (__bf16)zv;
+        if (p.z) p.z[o] = zv;  // the latents (also a reported output)
+        if (p.phases & 16) {   // saved for the backward
+          p.mu[o] = mv;
+          p.lv[o] = l;
+          p.zb[(size_t)(b0 + m) * 56 + k] = (__bf16)zv;
+        }
         const float d = mv - p.v_pm;
         sKl[m * 50 + k] = (((p.v_plv - l) - 1.0f) + var / p.v_pv) + (d * d) / p.v_pv;
       }
@@ -931,8 +933,11 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   // the tile shapes are compiled for the reference's default VAE
   MOG_CHECK_ARG(W == 28 && R1 == 512 && R2 == 256 && Z == 50 && G1 == 256 && G2 == 512);
   MOG_CHECK_ARG(x && theta_f && theta_b && mask && zval && eps_z && (eps_x || eps_gen) && wt && bias);
-  MOG_CHECK_ARG(canvas_part && part_rows && vkl && gb && a1b && a2b && mu && lv && z && zb);
-  MOG_CHECK_ARG(d1b && d2b && r);
+  MOG_CHECK_ARG(canvas_part && part_rows && vkl && r);
+  // the saved activations: all given (train) or all NULL (forward only)
+  const bool save = gb != nullptr;
+  MOG_CHECK_ARG(save == (a1b && a2b && mu && lv && z && zb && d1b && d2b));
+  MOG_CHECK_ARG(save || !(a1b || a2b || mu || lv || zb || d1b || d2b));
   if (B == 0) return 0;
   StepArgs p;
   p.x = x; p.theta_f = theta_f; p.theta_b = theta_b; p.mask = mask; p.zval = zval;
@@ -950,6 +955,7 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   p.d2b = reinterpret_cast<__bf16*>(d2b); p.r = r;
   const char* ph = getenv("MOG_VS_PHASES");
   p.phases = ph ? atoi(ph) : 31;
+  if (!save) p.phases &= ~16;
   p.B = B; p.C = C; p.lik_std = lik_std; p.v_pm = v_pm; p.v_pv = v_pv; p.v_plv = v_plv;
   p.x_period = x_period > 0 ? x_period : B;
   // Tile height: 64 images per workgroup (one per CU) once the batch gives

@@ -444,7 +444,7 @@ class AIRModel:
                 continue
             if self.fused_step:
                 with self._timed("stn_vae_step"):
-                    self._step_fused(X, ws, t, float(lik_std))
+                    self._step_fused(X, ws, t, float(lik_std), save=need_grad)
                 continue
             # STN read -> glimpse VAE (air_model.py:523-550, vae.py:5-48)
             if self.precision == "bf16":
@@ -455,7 +455,7 @@ class AIRModel:
             ops.stn_forward(ws.r[t], ws.th_b[t], (C, C), out=ws.canvas, z=ws.zval[t],
                             mask=ws.zmask[t], accumulate=True)
         if batched:
-            self._vae_forward_all(X, ws, float(lik_std))
+            self._vae_forward_all(X, ws, float(lik_std), save=need_grad)
             # the running loss in the loop's order (z_pres term, scale, shift
             # and VAE KLs per step), replayed from the step records
             _ops.air_runloss_(T, B, ws.rec, R_NREC * B, ws.skl, ws.shkl, ws.vkl, ws.runloss)
@@ -477,9 +477,11 @@ class AIRModel:
         straddle two steps (B % 64)."""
         return self.batch_vae and B % 64 == 0
 
-    def _vae_forward_all(self, X, ws, lik_std, t0=0, t1=None):
+    def _vae_forward_all(self, X, ws, lik_std, t0=0, t1=None, save=True):
         """The glimpse VAE (STN read -> VAE -> STN write into the canvas
-        parts) of loop steps [t0, t1) as one set of launches over their rows."""
+        parts) of loop steps [t0, t1) as one set of launches over their rows.
+        save=False: no backward follows (the fused kernel skips the saved
+        activations)."""
         B, C, W = ws.B, self.canvas_size, self.windows_size
         t1 = self.max_steps if t1 is None else t1
         T, TB = t1 - t0, (t1 - t0) * B
@@ -493,13 +495,16 @@ class AIRModel:
             gen = getattr(ws, "eps_x_offset", None) is not None
             off = ws.eps_x_offset + t0 * B * (W2 // 4) if gen else 0
             bias = [self._P("vae/" + n + "/biases") for n in self._VAE]
+            # forward only (no backward follows): the backward's saved
+            # activations are not written (vae_step.hip moves its own bytes)
+            sv = r_ if save else (lambda a: None)  # noqa: E731
             _ops.stn_vae_step_(TB, C, X, r_(ws.th_f), r_(ws.th_b), r_(ws.zmask), r_(ws.zval),
                                r_(ws.eps_z), r_(ws.eps_x), ops._i64(self.noise_seed),
                                ops._i64(off), gen, wt, bias, lik_std, float(self.vae_prior_mean),
                                float(self.vae_prior_variance), self.vae_prior_log_variance,
-                               r_(ws.cparts), r_(ws.prows), None, r_(ws.vkl), r_(ws.gb),
-                               r_(ws.a1b), r_(ws.a2b), r_(ws.mu), r_(ws.lv), r_(ws.z), r_(ws.zb),
-                               r_(ws.d1b), r_(ws.d2b), r_(ws.r), B)
+                               r_(ws.cparts), r_(ws.prows), None, r_(ws.vkl), sv(ws.gb),
+                               sv(ws.a1b), sv(ws.a2b), sv(ws.mu), sv(ws.lv), r_(ws.z), sv(ws.zb),
+                               sv(ws.d1b), sv(ws.d2b), r_(ws.r), B)
             return
         v = lambda a: a[t0:t1].reshape(TB, -1)  # noqa: E731
         vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
@@ -825,9 +830,10 @@ class AIRModel:
                   epi=BF_SIGMOID_NOISE, bias=[vb["gen_mean"]], aux=[ws.eps_x[t]], ldaux=W2,
                   aux_scale=lik_std)
 
-    def _step_fused(self, X, ws, t, lik_std):
+    def _step_fused(self, X, ws, t, lik_std, save=True):
         """STN read + VAE + latent sample/KL + STN write-accumulate in one launch
-        (vae_step.hip; same arithmetic as the unfused bf16 sequence)."""
+        (vae_step.hip; same arithmetic as the unfused bf16 sequence).
+        save=False: forward only, the backward's activations are not written."""
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         self._pack_bf16()
         if self.windows_size != 28 or (R1, R2, Z, G1, G2) != (512, 256, 50, 256, 512):
@@ -840,9 +846,10 @@ class AIRModel:
                            ws.zval[t], ws.eps_z[t], ws.eps_x[t], ops._i64(self.noise_seed),
                            ops._i64(off), gen, wt, bias, lik_std, float(self.vae_prior_mean),
                            float(self.vae_prior_variance), self.vae_prior_log_variance,
-                           ws.cparts[t], ws.prows[t], ws.runloss, ws.vkl[t], ws.gb[t],
-                           ws.a1b[t], ws.a2b[t], ws.mu[t], ws.lv[t], ws.z[t], ws.zb[t],
-                           ws.d1b[t], ws.d2b[t], ws.r[t])
+                           ws.cparts[t], ws.prows[t], ws.runloss, ws.vkl[t],
+                           *(a[t] if save else None for a in (ws.gb, ws.a1b, ws.a2b, ws.mu, ws.lv)),
+                           ws.z[t], ws.zb[t] if save else None, ws.d1b[t] if save else None,
+                           ws.d2b[t] if save else None, ws.r[t])
 
     def _vae_backward_bf16(self, ws, t, gscale):
         from .ops import BF_SOFTPLUS_BWD, BF_STORE, gemm_bf16

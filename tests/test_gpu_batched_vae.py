@@ -86,3 +86,33 @@ def test_batched_vae_fp32_bit_exact_vs_oracle(num_prior):
     np.testing.assert_array_equal(m.vae_kls.cpu().numpy(), ro["vae_kl"].T)
     np.testing.assert_array_equal(m.canvas.cpu().numpy(), ro["canvas"])
     np.testing.assert_allclose(m.per_image_loss.cpu().numpy(), ro["loss"], rtol=1e-5)
+
+
+def test_fused_forward_only_matches_training_form_bitwise():
+    """The fused step kernel without the backward's saved activations (the
+    forward-only form infer() runs) writes the same canvas parts, row ranges,
+    VAE KL, r and latents as the training form and leaves the saved buffers
+    untouched."""
+    cfg, P, nz, x, k = _setup(batch=128, seed=4)
+    m = _model(cfg, P, "bv_fwd", "bf16", True, True)
+    X = torch.as_tensor(x).to(DEV)
+    m.infer(X, torch.as_tensor(k).to(DEV))
+    ws = m._ws
+    outs = ("cparts", "prows", "vkl", "r", "z")
+    saved = ("gb", "a1b", "a2b", "mu", "lv", "zb", "d1b", "d2b")
+
+    def run(save):
+        for n in outs:
+            getattr(ws, n).zero_()
+        for n in saved:
+            getattr(ws, n).fill_(7.0)
+        m._vae_forward_all(X, ws, 0.3, save=save)
+        torch.cuda.synchronize()
+        return {n: getattr(ws, n).clone() for n in outs + saved}
+
+    tr, fw = run(True), run(False)
+    for n in outs:
+        assert torch.equal(_bits(tr[n]), _bits(fw[n])), n
+    for n in saved:
+        assert bool((fw[n] == 7.0).all()), n
+        assert not bool((tr[n] == 7.0).all()), n

@@ -165,8 +165,11 @@ def test_fused_step_matches_unfused_bitwise(batch):
     mf = _model(cfg, P, "fused%d" % batch, fused=True)
     mu = _model(cfg, P, "unfused%d" % batch, fused=False)
     assert mf.fused_step and not mu.fused_step
-    mf.infer(x, k, noise=noise)
-    mu.infer(x, k, noise=noise)
+    # the training form (saved activations written; infer() runs the
+    # forward-only form, test_gpu_batched_vae.py pins the two together)
+    G = torch.zeros((batch, cfg.canvas_size ** 2), device=DEV)
+    mf.compute_gradients(x, k, noise=noise, canvas_cotangent=G)
+    mu.compute_gradients(x, k, noise=noise, canvas_cotangent=G)
     torch.cuda.synchronize()
     for name in ("canvas", "runloss", "vkl", "gb", "a1b", "a2b", "mu", "lv", "z", "zb", "d1b",
                  "d2b", "r"):
@@ -195,8 +198,8 @@ def test_fused_step_inkernel_noise_matches_filled_noise():
     mf = _model(cfg, P, "pfused", fused=True)
     mu = _model(cfg, P, "punfused", fused=False)
     mf.noise_seed = mu.noise_seed = 4242
-    mf.infer(x, k)
-    mu.infer(x, k)
+    mf.compute_gradients(x, k)  # the training form: saved activations written
+    mu.compute_gradients(x, k)
     torch.cuda.synchronize()
     assert mf._ws.eps_x_offset is not None and mu._ws.eps_x_offset is None
     for name in ("canvas", "runloss", "vkl", "r", "z", "d2b"):
@@ -216,8 +219,8 @@ def test_fused_step_tile_variants_bitwise(variant, monkeypatch):
     noise = {n: torch.as_tensor(v).to(DEV) for n, v in nz.items()}
     mf = _model(cfg, P, "tv%s" % variant, fused=True)
     mu = _model(cfg, P, "tvu%s" % variant, fused=False)
-    mf.infer(x, k, noise=noise)
-    mu.infer(x, k, noise=noise)
+    mf.compute_gradients(x, k, noise=noise)  # the training form: saved activations written
+    mu.compute_gradients(x, k, noise=noise)
     torch.cuda.synchronize()
     for name in ("canvas", "runloss", "vkl", "gb", "a1b", "d2b", "r"):
         a, b = getattr(mf._ws, name), getattr(mu._ws, name)

@@ -104,8 +104,8 @@ def test_bf16_fused_step_c64_matches_unfused_bitwise(variant, monkeypatch):
     mf = _model(cfg, P, "c64f%s" % variant, precision="bf16", fused=True)
     mu = _model(cfg, P, "c64u%s" % variant, precision="bf16", fused=False)
     assert mf.fused_step and not mu.fused_step
-    mf.infer(x, k, noise=noise)
-    mu.infer(x, k, noise=noise)
+    mf.compute_gradients(x, k, noise=noise)  # the training form: saved activations written
+    mu.compute_gradients(x, k, noise=noise)
     torch.cuda.synchronize()
     for name in ("canvas", "runloss", "vkl", "gb", "a1b", "a2b", "mu", "lv", "z", "zb", "d1b",
                  "d2b", "r"):
