@@ -184,7 +184,19 @@ struct TileIO {
 // Epilogue of one wave's (16 MI) x (16 NI) accumulator block at output rows
 // r0 + ..., columns c0 + ... (16x16 MFMA layout: lane (li, g) holds rows
 // 4g .. 4g+3 of column li of each tile).
-template <int MI, int NI, int EPI>
+// RA / RB: the LDS-DMA kernel's remapped fragments (row-contiguous operands
+// read as one vector per k-step, gemm_f32_dma_kernel): accumulator row i of
+// tile mi is output row MI i + mi, column j of tile ni is column NI j + ni.
+template <int MI, int NI, bool RA, bool RB>
+__device__ __forceinline__ int acc_row(int mi, int i) {
+  return RA ? MI * i + mi : mi * 16 + i;
+}
+template <int MI, int NI, bool RA, bool RB>
+__device__ __forceinline__ int acc_col(int ni, int j) {
+  return RB ? NI * j + ni : ni * 16 + j;
+}
+
+template <int MI, int NI, int EPI, bool RA = false, bool RB = false>
 __device__ __forceinline__ void store_tile(const floatx4 (&acc)[MI][NI], const GemmPtrs& P,
                                            const GemmDims& D, int z, int r0, int c0, int lane) {
 #pragma clang fp contract(off)
@@ -199,8 +211,8 @@ __device__ __forceinline__ void store_tile(const floatx4 (&acc)[MI][NI], const G
     for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = r0 + mi * 16 + (lane >> 4) * 4 + r;
-        const int col = c0 + ni * 16 + (lane & 15);
+        const int row = r0 + acc_row<MI, NI, RA, RB>(mi, (lane >> 4) * 4 + r);
+        const int col = c0 + acc_col<MI, NI, RA, RB>(ni, lane & 15);
         if (row >= M || col >= N) continue;
         const size_t o = (size_t)row * D.ldc + col;
         float v = acc[mi][ni][r];
@@ -234,7 +246,7 @@ __device__ __forceinline__ void store_tile(const floatx4 (&acc)[MI][NI], const G
 // (a store instruction writes 64-byte row pieces) is re-read as whole rows,
 // so every store / aux load / atomic instruction covers full 256-byte row
 // segments.  Elementwise math identical to store_tile.
-template <int BM, int BN, int EPI>
+template <int BM, int BN, int EPI, bool RA = false, bool RB = false>
 __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[BM / 32][BN / 32],
                                                 float* sC, const GemmPtrs& P, const GemmDims& D,
                                                 int z, int m0, int n0, int wm, int wn) {
@@ -248,8 +260,8 @@ __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[BM / 32][BN
     for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        sC[(wm + mi * 16 + (lane >> 4) * 4 + r) * LDC + wn + ni * 16 + (lane & 15)] =
-            acc[mi][ni][r];
+        sC[(wm + acc_row<MI, NI, RA, RB>(mi, (lane >> 4) * 4 + r)) * LDC + wn +
+           acc_col<MI, NI, RA, RB>(ni, lane & 15)] = acc[mi][ni][r];
   __syncthreads();
   const int M = D.M, N = D.N;
   float* C = P.C[z];
@@ -469,9 +481,17 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
 //     16-B chunk c of row r holds k = 4 (c ^ kcs(r)) .. +3 (one instruction
 //     fills 16 rows, 64 B of each);
 //   RC image (operand row-contiguous: A^T [K][M], B [K][N]): 16 k-rows of
-//     ROWS floats; element n of k-row k sits at n ^ ((k & 1) << 4).
-// A fragment element (row, k = 4 kk + g) is one ds_read_b32: conflict-free on
-// RC images, 2-way on KC images (the minimum for 4-B reads of a 16-float row).
+//     ROWS floats; element n of k-row k sits at n ^ rcs(k).
+// KC fragments: element (row, k = 4 kk + g) is one ds_read_b32 (2-way, the
+// minimum for 4-B reads of a 16-float row).  RC fragments are REMAPPED: the
+// wave's (16 MI) rows are assigned so that lane (fr, g) owns rows
+// w0 + MI fr .. + MI - 1, which sit side by side in the k-row: one ds_read_b64
+// (MI = 2) / ds_read_b128 (MI = 4) per k-step instead of MI ds_read_b32 (those
+// run at half the LDS rate, gfx950 LDS table of MI355X_MICROARCH.md); the
+// epilogue maps accumulator rows back (acc_row / acc_col).  rcs() makes the
+// vector reads conflict-free under the b64 (2 x 32 lanes) / b128 (4 x 16
+// lanes) lane groups: 64-float rows swap their halves on odd k, 128-float rows
+// need no swizzle.  The k order of every MFMA chain is unchanged.
 // The MFMA sequence, and so every fma chain, is the register-staged kernel's.
 // KC chunk swizzle: BK = 16 -> 4 chunks per row, (r >> 1) & 3; BK = 32 -> 8
 // chunks, r & 7 (both the 2-way minimum for 4-B reads)
@@ -486,6 +506,9 @@ struct DmaOperand {
   static constexpr int NWQ = NQ / 4;               // per wave
   static constexpr int CPR = BK / 4;               // KC: 16-B chunks per row
   static_assert(NQ % 4 == 0, "four waves share a tile's DMAs");
+  static_assert(KC || ROWS == 64 || ROWS == 128, "RC swizzle");
+  // RC: float offset XOR of k-row k
+  __device__ static __forceinline__ int rcs(int k) { return ROWS == 64 ? (k & 1) << 5 : 0; }
   int voff[NWQ];  // this lane's source byte offset at k0 = 0
   int kof[NWQ];   // its k within the tile (KC: first of its 4; RC: its k-row)
   __device__ __forceinline__ void init(int w, int lane, int r0, int ld) {
@@ -500,7 +523,7 @@ struct DmaOperand {
       } else {
         constexpr int PER = ROWS / 4;  // 16-B chunks per k-row
         const int k = q * (256 / ROWS) + lane / PER;
-        const int n = (4 * (lane % PER)) ^ ((k & 1) << 4);
+        const int n = (4 * (lane % PER)) ^ rcs(k);
         voff[j] = (k * ld + r0 + n) * 4;
         kof[j] = k;
       }
@@ -520,7 +543,7 @@ struct DmaOperand {
   // image index of element (row, k = 4 kk + g)
   __device__ static __forceinline__ int at(int row, int kk, int g) {
     if constexpr (KC) return row * BK + 4 * (kk ^ kcs<BK>(row)) + g;
-    else return (4 * kk + g) * ROWS + (row ^ ((g & 1) << 4));
+    else return (4 * kk + g) * ROWS + (row ^ rcs(g));
   }
 };
 
@@ -536,8 +559,13 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_dma_kernel(GemmPtrs P, GemmDi
   constexpr int A_SZ = BM * BK, STAGE = (BM + BN) * BK;  // floats
   using OpA = DmaOperand<BM, !TA, BK>;
   using OpB = DmaOperand<BN, TB, BK>;
+  constexpr bool RA = TA, RB = !TB;  // row-contiguous operands: remapped vector fragments
+  typedef float fva __attribute__((ext_vector_type(MI)));
+  typedef float fvb __attribute__((ext_vector_type(NI)));
   constexpr int DPT = OpA::NWQ + OpB::NWQ;  // DMA instructions per wave per k-tile
-  __shared__ __attribute__((aligned(1024))) float lds[NS * STAGE];
+  // the stage buffers, reused by the row-staged epilogue
+  constexpr int LDS_F = NS * STAGE > BM * (BN + 4) ? NS * STAGE : BM * (BN + 4);
+  __shared__ __attribute__((aligned(1024))) float lds[LDS_F];
   const int nwg = gridDim.x * gridDim.y * gridDim.z;
   const int wg = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nwg);
   const int bx = wg % D.nx, by = (wg / D.nx) % D.ny, bz = wg / (D.nx * D.ny);
@@ -563,8 +591,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_dma_kernel(GemmPtrs P, GemmDi
       for (int r = 0; r < 4; ++r) {
         float v = 0.0f;
         if (Cin != nullptr && ks == 0) {
-          const int row = m0 + wm + mi * 16 + (lane >> 4) * 4 + r;
-          const int col = n0 + wn + ni * 16 + (lane & 15);
+          const int row = m0 + wm + acc_row<MI, NI, RA, RB>(mi, (lane >> 4) * 4 + r);
+          const int col = n0 + wn + acc_col<MI, NI, RA, RB>(ni, lane & 15);
           if (row < M && col < N) v = Cin[(size_t)row * D.ldc + col];
         }
         acc[mi][ni][r] = v;
@@ -602,15 +630,27 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_dma_kernel(GemmPtrs P, GemmDi
     const float* Bs = As + A_SZ;
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
+      if constexpr (RA) {
+        const fva v = *reinterpret_cast<const fva*>(&As[OpA::at(wm + MI * fr, kk, fg)]);
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) fa[F][kk][mi] = As[OpA::at(wm + mi * 16 + fr, kk, fg)];
+        for (int mi = 0; mi < MI; ++mi) fa[F][kk][mi] = v[mi];
+      } else {
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) fb[F][kk][ni] = Bs[OpB::at(wn + ni * 16 + fr, kk, fg)];
+        for (int mi = 0; mi < MI; ++mi) fa[F][kk][mi] = As[OpA::at(wm + mi * 16 + fr, kk, fg)];
+      }
+      if constexpr (RB) {
+        const fvb v = *reinterpret_cast<const fvb*>(&Bs[OpB::at(wn + NI * fr, kk, fg)]);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) fb[F][kk][ni] = v[ni];
+      } else {
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) fb[F][kk][ni] = Bs[OpB::at(wn + ni * 16 + fr, kk, fg)];
+      }
     }
     if constexpr (!TB) {
       if (do_cs) {
 #pragma unroll
-        for (int k = 0; k < BK; ++k) cs += Bs[k * BN + (t ^ ((k & 1) << 4))];
+        for (int k = 0; k < BK; ++k) cs += Bs[k * BN + (t ^ OpB::rcs(k))];
       }
     }
   };
@@ -674,13 +714,11 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_dma_kernel(GemmPtrs P, GemmDi
   }
   if (do_cs && n0 + t < N) atomicAdd(colsum + n0 + t, cs);
 
-  if constexpr (BM * (BN + 4) <= NS * STAGE) {
-    if (D.vecC) {
-      store_tile_rows<BM, BN, EPI>(acc, lds, P, D, z, m0, n0, wm, wn);
-      return;
-    }
+  if (D.vecC) {
+    store_tile_rows<BM, BN, EPI, RA, RB>(acc, lds, P, D, z, m0, n0, wm, wn);
+    return;
   }
-  store_tile<MI, NI, EPI>(acc, P, D, z, m0 + wm, n0 + wn, lane);
+  store_tile<MI, NI, EPI, RA, RB>(acc, P, D, z, m0 + wm, n0 + wn, lane);
 }
 
 template <int BM, int BN, int BK, int PF, bool TA, bool TB, bool KS>
