@@ -399,13 +399,14 @@ __global__ __launch_bounds__(256) void cvt_bf16_batch_kernel(CvtBatch b) {
   const int* d = b.d[j];
   const float* src = b.src[j];
   if (d[6] == 2) {
-    // MFMA B-fragment order of W^T (vae_step.hip): element e = ((ct * KS + ks)
-    // * 64 + lane) * 8 + q holds W^T[ct*16 + lane%16][ks*32 + 8*(lane/16) + q],
-    // so one 16-B-per-lane wave load is 1 KiB contiguous
+    // MFMA B-fragment order of W^T (vae_step.hip), k-step major: element
+    // e = ((ks * NCT + ct) * 64 + lane) * 8 + q holds
+    // W^T[ct*16 + lane%16][ks*32 + 8*(lane/16) + q], so one 16-B-per-lane wave
+    // load is 1 KiB contiguous and the column tiles of one k-step are adjacent
     const int q = e & 7, l = (e >> 3) & 63;
-    const int f = e >> 9;                        // ct * KS + ks
-    const int KS = d[4] >> 5;
-    const int ct = f / KS, ks = f - ct * KS;
+    const int f = e >> 9;                        // ks * NCT + ct
+    const int NCT = d[3] >> 4;
+    const int ks = f / NCT, ct = f - ks * NCT;
     const int n = ct * 16 + (l & 15), k = ks * 32 + 8 * (l >> 4) + q;
     const float v = (k < d[0] && n < d[1]) ? src[k * d[2] + n] : 0.0f;
     b.dst[j][e] = (__bf16)v;

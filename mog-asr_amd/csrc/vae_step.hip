@@ -180,13 +180,20 @@ __device__ __forceinline__ floatx4 quad_transpose(const floatx4& a) {
 // Weight fragments (1 KiB per wave per k-step) through a buffer descriptor:
 // the per-lane offset is fixed per column tile and the k-step goes into the
 // scalar offset, so a fragment load costs no vector ALU address arithmetic.
+// Layout k-step major (mog_cvt_bf16_batch transpose 2): fragment (ks, ct) at
+// (ks * NCT + ct) KiB, NCT = the layer's 16-column tiles -- the column tiles
+// that the waves and CUs stream at the same k-step are adjacent in memory
+// (spread over the L2 channels) instead of a column tile's K-long run apart.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t weight_rsrc(const __bf16* W) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(W), 0, 0x7ffffff0, 0x00020000);
 }
+__device__ __forceinline__ int frag_voff(int ct, int lane) { return (ct * 64 + lane) * 16; }
+template <int NCT>
 __device__ __forceinline__ bf16x8 load_frag(__amdgpu_buffer_rsrc_t r, int voff, int ks) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, ks * 1024, 0);
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, ks * NCT * 1024, 0);
   return __builtin_bit_cast(bf16x8, v);
 }
+constexpr int nct(int N) { return (N + 15) / 16; }
 
 // bias[n0 .. n0+3] (0 past N)
 __device__ __forceinline__ floatx4 load_bias4(const float* __restrict__ bias, int n0, int N) {
@@ -234,11 +241,11 @@ __device__ __forceinline__ void build_tables(float2* tab, const float (*sth)[12]
 // nw == NW).  Epilogue per 16 x 16 accumulator tile, quad-transposed:
 // epi(m, n0, v, b) with v = row m's columns n0 .. n0+3 and b = their biases
 // (loaded before the k loop; 0 at or past N).
-template <int MT, int K, int TPW, int D, bool SYNC, class Epi>
+template <int MT, int K, int N, int TPW, int D, bool SYNC, class Epi>
 __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf16* __restrict__ W,
-                                            const float* __restrict__ bias, int N, int tile_base,
+                                            const float* __restrict__ bias, int tile_base,
                                             int wbase, int nw, Epi epi) {
-  constexpr int KS = K / 32;
+  constexpr int KS = K / 32, NCT = nct(N);
   static_assert(K % 32 == 0, "K padding");
   const int rot = (int)(blockIdx.x >> 3);  // spread the CUs of one XCD over the weight columns
   const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) - wbase;
@@ -249,7 +256,7 @@ __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf
 #pragma unroll
   for (int c = 0; c < TPW; ++c) {
     ct[c] = tile_base + (w + nw * c + rot) % (nw * TPW);
-    wo[c] = (ct[c] * KS * 64 + lane) * 16;
+    wo[c] = frag_voff(ct[c], lane);
   }
   floatx4 bq[TPW];
 #pragma unroll
@@ -261,7 +268,7 @@ __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf
     for (int c = 0; c < TPW; ++c) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
   auto loadB = [&](int ks, bf16x8* b) {
 #pragma unroll
-    for (int c = 0; c < TPW; ++c) b[c] = load_frag(wr, wo[c], ks);
+    for (int c = 0; c < TPW; ++c) b[c] = load_frag<NCT>(wr, wo[c], ks);
   };
   auto step = [&](int ks, const bf16x8* b) {
     const int k = ks * 32 + 8 * g;
@@ -318,29 +325,28 @@ __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf
 // One column tile `ct` of a dense layer split by rows: wave w < MT computes
 // row tile w (for a last, odd column tile that would otherwise leave seven
 // waves idle).
-template <int MT, int K, class Epi>
+template <int MT, int K, int N, class Epi>
 __device__ __forceinline__ void dense_rowsplit(const __bf16* A, int lda, const __bf16* __restrict__ W,
-                                               const float* __restrict__ bias, int N, int ct,
-                                               Epi epi) {
-  constexpr int KS = K / 32, D = 4;
+                                               const float* __restrict__ bias, int ct, Epi epi) {
+  constexpr int KS = K / 32, D = 4, NCT = nct(N);
   static_assert(KS % D == 0, "ring");
   const int lane = threadIdx.x & 63, rt = threadIdx.x >> 6;
   if (rt >= MT) return;
   const int li = lane & 15, g = lane >> 4;
   const floatx4 bq = load_bias4(bias, ct * 16 + (li & ~3), N);
   const __amdgpu_buffer_rsrc_t wr = weight_rsrc(W);
-  const int wo = (ct * KS * 64 + lane) * 16;
+  const int wo = frag_voff(ct, lane);
   floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
   bf16x8 q[D];
 #pragma unroll
-  for (int d = 0; d < D; ++d) q[d] = load_frag(wr, wo, d);
+  for (int d = 0; d < D; ++d) q[d] = load_frag<NCT>(wr, wo, d);
 #pragma unroll 1
   for (int ks = 0; ks < KS; ks += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const bf16x8 a = *reinterpret_cast<const bf16x8*>(&A[(rt * 16 + li) * lda + (ks + d) * 32 + 8 * g]);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, q[d], acc, 0, 0, 0);
-      q[d] = load_frag(wr, wo, min(ks + d + D, KS - 1));
+      q[d] = load_frag<NCT>(wr, wo, min(ks + d + D, KS - 1));
     }
   }
   epi(rt * 16 + g * 4 + (li & 3), ct * 16 + (li & ~3), quad_transpose(acc), bq);
@@ -533,12 +539,12 @@ __device__ __forceinline__ void read_recognition(const StepArgs& p, unsigned cha
 #pragma unroll
     for (int c = 0; c < TW; ++c) {
       ct[c] = (wv + (NW / 2) * c + rot) % 32;
-      wo[c] = (ct[c] * KS1 * 64 + lane) * 16;
+      wo[c] = frag_voff(ct[c], lane);
     }
     bf16x8 q[DB][TW];
     auto loadB = [&](int ks, bf16x8* b) {
 #pragma unroll
-      for (int c = 0; c < TW; ++c) b[c] = load_frag(wr, wo[c], ks);
+      for (int c = 0; c < TW; ++c) b[c] = load_frag<32>(wr, wo[c], ks);
     };
     const int kao = Ly::TAB + (li * SK + 8 * g) * 2;
     auto mfma = [&](int ks, const bf16x8* b) {
@@ -659,7 +665,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   if (p.phases & 16) flush_rows<NTHR>(sA1, S512, p.a1b + (size_t)b0 * 512, 512, 512, nb);
   // ---- 3. a2 = softplus(a1 W2 + b2)  [M x 256], in place ------------------
   if (p.phases & 2) {
-    dense_tiles<MT, 512, 16 / NW, 4, true>(sA1, S512, p.wt[1], p.bias[1], 256, 0, 0, NW,
+    dense_tiles<MT, 512, 256, 16 / NW, 4, true>(sA1, S512, p.wt[1], p.bias[1], 0, 0, NW,
                                      [&](int m, int n0, const floatx4& v, const floatx4& b) {
                                        store_softplus4(sA2 + m * S256 + n0, v, b);
                                      });
@@ -678,8 +684,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
           if (n0 + k < 50) dst[m * 50 + n0 + k] = v[k] + b[k];
       };
     };
-    dense_tiles<MT, 256, 1, 4, false>(sA2, S256, p.wt[2], p.bias[2], 50, 0, 0, 4, epi_f32(sMu));
-    dense_tiles<MT, 256, 1, 4, false>(sA2, S256, p.wt[3], p.bias[3], 50, 0, 4, 4, epi_f32(sLv));
+    dense_tiles<MT, 256, 50, 1, 4, false>(sA2, S256, p.wt[2], p.bias[2], 0, 0, 4, epi_f32(sMu));
+    dense_tiles<MT, 256, 50, 1, 4, false>(sA2, S256, p.wt[3], p.bias[3], 0, 4, 4, epi_f32(sLv));
   }
   lds_barrier();
   STAMP(4);
@@ -734,7 +740,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   // ---- 6. d1 = softplus(z Wg1 + b)  [M x 256] (over mu | lv) ---------------
   __bf16* sD1 = reinterpret_cast<__bf16*>(arena + Ly::OFF_D1);
   if (p.phases & 2) {
-    dense_tiles<MT, 64, 16 / NW, 2, false>(sZ, SZ, p.wt[4], p.bias[4], 256, 0, 0, NW,
+    dense_tiles<MT, 64, 256, 16 / NW, 2, false>(sZ, SZ, p.wt[4], p.bias[4], 0, 0, NW,
                                      [&](int m, int n0, const floatx4& v, const floatx4& b) {
                                        store_softplus4(sD1 + m * S256 + n0, v, b);
                                      });
@@ -745,7 +751,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   // ---- 7. d2 = softplus(d1 Wg2 + b)  [M x 512] at 0 (in place over d1) -----
   __bf16* sD2 = reinterpret_cast<__bf16*>(arena);
   if (p.phases & 2) {
-    dense_tiles<MT, 256, 32 / NW, NW / 4, true>(sD1, S256, p.wt[5], p.bias[5], 512, 0, 0, NW,
+    dense_tiles<MT, 256, 512, 32 / NW, NW / 4, true>(sD1, S256, p.wt[5], p.bias[5], 0, 0, NW,
                                      [&](int m, int n0, const floatx4& v, const floatx4& b) {
                                        store_softplus4(sD2 + m * S512 + n0, v, b);
                                      });
@@ -780,9 +786,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
         reinterpret_cast<float4*>(p.r)[q] = make_float4(o[0], o[1], o[2], o[3]);
       }
     };
-    dense_tiles<MT, 512, 32 / NW, 8, false>(sD2, S512, p.wt[6], p.bias[6], W2, 0, 0, NW, epi);
-    dense_tiles<MT, 512, 16 / NW, 8, false>(sD2, S512, p.wt[6], p.bias[6], W2, 32, 0, NW, epi);
-    dense_rowsplit<MT, 512>(sD2, S512, p.wt[6], p.bias[6], W2, 48, epi);
+    dense_tiles<MT, 512, W2, 32 / NW, 8, false>(sD2, S512, p.wt[6], p.bias[6], 0, 0, NW, epi);
+    dense_tiles<MT, 512, W2, 16 / NW, 8, false>(sD2, S512, p.wt[6], p.bias[6], 32, 0, NW, epi);
+    dense_rowsplit<MT, 512, W2>(sD2, S512, p.wt[6], p.bias[6], 48, epi);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // r stores done before other waves read it
   lds_barrier();
