@@ -515,7 +515,7 @@ __device__ __forceinline__ void stn_bwd_image(
     }
     const int cwi = Win <= 32 ? 32 : 64, rpi = 64 / cwi;
     const int ul = lane % cwi, half = lane / cwi;
-    constexpr int UV = 32;
+    constexpr int UV = 16;  // dU outputs per lane held up front (Hin <= 16 rpi)
     const bool upre = du_mode != 0 && rpi * UV >= Hin;
     float uv[UV];
     int jlo = 0, jhi = -1;
@@ -575,22 +575,35 @@ __device__ __forceinline__ void stn_bwd_image(
           wj[d] = d < nj ? (__float_as_int(e.x) == ul ? e.z : e.w) : 0.0f;
           src[d] = max(jj, 0) * 4;
         }
-        // rows in groups of four (one uniform branch per group): the group's
-        // exchanges are in flight together
+        // rows in groups of RG (one uniform branch per group), the column
+        // offset d outermost: the group's RG exchanges of one d are
+        // independent and in flight together (per row the sum still runs
+        // over d ascending)
+        constexpr int RG = 8;
 #pragma unroll
-        for (int r = 0; r < GV; ++r) {
-          if (r % 4 == 0 && rlo + r >= rhi) break;
-          const bool rv = rlo + r < rhi;
-          const float g0 = gv[r] * sc;
-          const float gt = grads && g0 != 0.0f ? g0 : 0.0f;
-          float acc = 0.0f;
+        for (int r0 = 0; r0 < GV; r0 += RG) {
+          if (rlo + r0 >= rhi) break;
+          float gt[RG], acc[RG];
+#pragma unroll
+          for (int r = 0; r < RG; ++r) {
+            const float g0 = gv[r0 + r] * sc;
+            gt[r] = grads && g0 != 0.0f ? g0 : 0.0f;
+            acc[r] = 0.0f;
+          }
 #pragma unroll
           for (int d = 0; d < JM; ++d) {
             if (d >= jmax) break;
-            const float gj = __int_as_float(__builtin_amdgcn_ds_bpermute(src[d], __float_as_int(gt)));
-            if (d < nj) acc += gj * wj[d];
+            float gj[RG];
+#pragma unroll
+            for (int r = 0; r < RG; ++r)
+              gj[r] = __int_as_float(__builtin_amdgcn_ds_bpermute(src[d], __float_as_int(gt[r])));
+#pragma unroll
+            for (int r = 0; r < RG; ++r)
+              if (d < nj) acc[r] += gj[r] * wj[d];
           }
-          if (uact && rv) sT[(rlo + r) * Win + ul] = acc;
+#pragma unroll
+          for (int r = 0; r < RG; ++r)
+            if (uact && rlo + r0 + r < rhi) sT[(rlo + r0 + r) * Win + ul] = acc[r];
         }
         wave_sync();
         TS(3);
@@ -645,17 +658,42 @@ __device__ __forceinline__ void stn_bwd_image(
     // dU[v][u] = sum_i T[i][u] * (y0(i) == v ? y1 - y : y - y0)
     if (upre) {
       if (ul < Win) {
+        // outputs in groups of VG, the first IM rows of every range read
+        // together (clamped, masked); longer ranges finish in a loop.  Per
+        // output the sum runs over i ascending, as before.
+        constexpr int VG = 4, IM = 4;
 #pragma unroll
-        for (int k = 0; k < UV; ++k) {
-          const int v = half + rpi * k;
-          if (v >= Hin) break;
-          const int2 r = vrange[v];
-          float acc = 0.0f;
-          for (int i = r.x; i <= r.y; ++i) {
-            const float4 e = rowtab[i];
-            acc += sT[i * Win + ul] * (__float_as_int(e.x) == v * Win ? e.z : e.w);
+        for (int k0 = 0; k0 < UV; k0 += VG) {
+          if (half + rpi * k0 >= Hin) break;
+          int2 rr[VG];
+#pragma unroll
+          for (int q = 0; q < VG; ++q) rr[q] = vrange[min(half + rpi * (k0 + q), Hin - 1)];
+          float tv[VG][IM], wv[VG][IM];
+#pragma unroll
+          for (int q = 0; q < VG; ++q) {
+            const int v = half + rpi * (k0 + q);
+#pragma unroll
+            for (int j = 0; j < IM; ++j) {
+              const int i = max(min(rr[q].x + j, rr[q].y), 0);
+              const float4 e = rowtab[i];
+              tv[q][j] = sT[i * Win + ul];
+              wv[q][j] = __float_as_int(e.x) == v * Win ? e.z : e.w;
+            }
           }
-          put_u(v * Win + ul, acc, uv[k]);
+#pragma unroll
+          for (int q = 0; q < VG; ++q) {
+            const int k = k0 + q, v = half + rpi * k;
+            if (v >= Hin) break;
+            float acc = 0.0f;
+#pragma unroll
+            for (int j = 0; j < IM; ++j)
+              if (rr[q].x + j <= rr[q].y) acc += tv[q][j] * wv[q][j];
+            for (int i = rr[q].x + IM; i <= rr[q].y; ++i) {
+              const float4 e = rowtab[i];
+              acc += sT[i * Win + ul] * (__float_as_int(e.x) == v * Win ? e.z : e.w);
+            }
+            put_u(v * Win + ul, acc, uv[k]);
+          }
         }
       }
     } else if (ul < Win)

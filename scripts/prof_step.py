@@ -24,4 +24,17 @@ for r in rows[a:b]:
 for k, (c, d) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
     print(f"{d:9.1f} us  n={c:3d}  {k}")
 span = (int(rows[b - 1]["End_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
-print(f"sum {tot:.1f} us  span {span:.1f} us")
+# GPU busy time = union of the kernels' intervals (both streams); the rest of
+# the span is idle (launch / host gaps)
+iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows[a:b])
+busy, cur_s, cur_e, gaps = 0, iv[0][0], iv[0][1], []
+for s_, e_ in iv[1:]:
+    if s_ > cur_e:
+        busy += cur_e - cur_s
+        gaps.append((s_ - cur_e) / 1e3)
+        cur_s, cur_e = s_, e_
+    else:
+        cur_e = max(cur_e, e_)
+busy += cur_e - cur_s
+print(f"sum {tot:.1f} us  span {span:.1f} us  busy {busy / 1e3:.1f} us  idle {span - busy / 1e3:.1f} us "
+      f"in {len(gaps)} gaps (largest {sorted(gaps)[-5:] if gaps else []})")
