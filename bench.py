@@ -364,10 +364,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = None
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        # RCCL needs one GPU per rank; more ranks than GPUs (a rehearsal of the
+        # data-parallel path on a one-GPU box) share the devices over gloo
+        ndev = torch.cuda.device_count()
+        backend = os.environ.get("MOG_DP_BACKEND") or ("nccl" if world <= ndev else "gloo")
+        local = local % max(ndev, 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
@@ -388,7 +397,8 @@ def main():
     value = B * world * args.steps / el
     if rank == 0:
         out = {
-            "metric": METRIC, "value": value, "unit": "images/sec", "n_gpus": world,
+            "metric": METRIC, "value": value, "unit": "images/sec",
+            "n_gpus": min(world, torch.cuda.device_count()), "ranks": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.precision, "data": "synthetic",
@@ -397,7 +407,8 @@ def main():
                        "model": "AIR (LSTM 256, VAE 784-512-256-50, heads 64)",
                        "global_batch": B * world, "per_gpu_batch": B, "canvas": "50x50",
                        "max_steps": T, "data_dependent_steps_would_be": executed,
-                       "parallelism": f"dp{world}", "loss_last": loss},
+                       "parallelism": f"dp{world}", "loss_last": loss,
+                       "collective_backend": {"nccl": "rccl"}.get(backend, backend)},
             "roofline": roof,
         }
         if world == 1 and args.extras:
