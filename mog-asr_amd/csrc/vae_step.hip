@@ -195,6 +195,15 @@ __device__ __forceinline__ bf16x8 load_frag(__amdgpu_buffer_rsrc_t r, int voff, 
 }
 constexpr int nct(int N) { return (N + 15) / 16; }
 
+// Streaming stores (saved activations, canvas parts: written once, read by
+// later launches) carry the non-temporal hint so they do not evict the bf16
+// weights, which every tile of every CU re-streams, from the XCD's L2.  r stays
+// a normal store: the STN write phase reads it back.
+template <class T>
+__device__ __forceinline__ void st_stream(T* p, T v) {
+  __builtin_nontemporal_store(v, p);
+}
+
 // bias[n0 .. n0+3] (0 past N)
 __device__ __forceinline__ floatx4 load_bias4(const float* __restrict__ bias, int n0, int N) {
   if (n0 + 4 <= N) {
@@ -359,8 +368,8 @@ __device__ __forceinline__ void flush_rows(const T* s, int lds, T* g, int ldg, i
   const int cpr = ncols / V;
   for (int i = threadIdx.x; i < nb * cpr; i += NTHR) {
     const int m = i / cpr, c = i - (i / cpr) * cpr;
-    *reinterpret_cast<u32x4*>(g + (size_t)m * ldg + c * V) =
-        *reinterpret_cast<const u32x4*>(s + m * lds + c * V);
+    st_stream(reinterpret_cast<u32x4*>(g + (size_t)m * ldg + c * V),
+              *reinterpret_cast<const u32x4*>(s + m * lds + c * V));
   }
 }
 
@@ -510,8 +519,8 @@ __device__ __forceinline__ void read_recognition(const StepArgs& p, unsigned cha
       for (int i = tid - NTHR / 2; i < M * CPR; i += NTHR / 2) {
         const int m = i / CPR, c = i - (i / CPR) * CPR, k = 32 * KG * grp + 8 * c;
         if (m < nb && k < W2)
-          *reinterpret_cast<u32x4*>(p.gb + (size_t)(b0 + m) * W2 + k) =
-              *reinterpret_cast<const u32x4*>(kb + m * SK + 8 * c);
+          st_stream(reinterpret_cast<u32x4*>(p.gb + (size_t)(b0 + m) * W2 + k),
+                    *reinterpret_cast<const u32x4*>(kb + m * SK + 8 * c));
       }
     };
     // k-step ks uses gather register set ks % LA; the sample loop is unrolled
@@ -711,10 +720,10 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
         const float mv = sMu[m * 50 + k];
         const float var = mog_expf(l);
         zv = mv + ez[it] * sqrtf(var);
-        if (p.z) p.z[o] = zv;  // the latents (also a reported output)
+        if (p.z) st_stream(p.z + o, zv);  // the latents (also a reported output)
         if (p.phases & 16) {   // saved for the backward
-          p.mu[o] = mv;
-          p.lv[o] = l;
+          st_stream(p.mu + o, mv);
+          st_stream(p.lv + o, l);
           p.zb[(size_t)(b0 + m) * 56 + k] = (__bf16)zv;
         }
         const float d = mv - p.v_pm;
@@ -882,7 +891,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
           const f2 xz = {e0.z, e1.z}, xw = {e0.w, e1.w};
           const f2 wa = xz * ey.z, wb = xz * ey.w, wc = xw * ey.z, wd = xw * ey.w;
           const f2 sv = ((wa * Ia + wb * Ib) + wc * Ic) + wd * Id;
-          *dst = zn * sv;
+          st_stream(dst, zn * sv);
           dst += 64;
           pr += dr;
           rr += dq;
@@ -907,8 +916,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
               if (++j == C) { j = 0; ++i; }
             }
           }
-          if (vec) om4[q] = make_float4(v[0], v[1], v[2], v[3]);
-          else om[q] = v[0];
+          if (vec) st_stream(reinterpret_cast<floatx4*>(om4 + q), floatx4{v[0], v[1], v[2], v[3]});
+          else st_stream(om + q, v[0]);
         }
       }
       wave_lds_sync();  // the slot is rewritten for the next image
