@@ -150,8 +150,43 @@ def test_bf16_gradients_vs_float64_autograd():
         err = np.linalg.norm(grads[name] - ref) / max(np.linalg.norm(ref), 1e-12)
         if np.linalg.norm(ref) > 1e-6:
             worst = max(worst, err)
-            assert err < 6e-2, (name, err)
+            # measured on MI355X: worst 8.7e-3 over the tensors (batch 16)
+            assert err < 2e-2, (name, err)
     print(f"bf16 worst relative gradient error {worst:.2e}")
+
+
+def test_bf16_lstm_x_weight_gradient_on_its_own():
+    """The largest gradient tensor, the x-part of the LSTM kernel
+    (dWx = X^T sum_t dG_t over 2500 x 1024, air_model.py:454-456), takes bf16
+    operands in the bf16 configuration (fp32 accumulate): checked by itself
+    against float64 autograd on the same inputs, next to its recurrent rows
+    (fp32 in both configurations).  Measured on MI355X (batch 32): x rows
+    3.4e-3 relative, recurrent rows 3.9e-3."""
+    cfg, P, nz, x, k = _setup(batch=32, seed=5)
+    rng = np.random.default_rng(19)
+    Gc = (rng.standard_normal((cfg.batch, 2500)) * 0.01).astype(np.float32)
+    m = _model(cfg, P, "bf16xgrad")
+    grads = m.compute_gradients(x, k, noise={n: torch.as_tensor(v).to(DEV) for n, v in nz.items()},
+                                canvas_cotangent=torch.as_tensor(Gc).to(DEV))
+    Pt = at.to_torch(P, requires_grad=True)
+    out = at.air_forward(cfg, Pt, at.to_torch(nz), torch.tensor(x, dtype=torch.float64),
+                         z_pres_prior_log_odds=cfg.z_pres_prior_log_odds,
+                         canvas_cotangent=torch.tensor(Gc, dtype=torch.float64),
+                         fixed_steps=True)
+    out["loss"].backward()
+    name = next(n for n in Pt if n.endswith("rnn/basic_lstm_cell/kernel"))
+    ref = Pt[name].grad.numpy()
+    got = grads[name]
+    C2 = 2500
+    res = {}
+    for part, sl in (("x", slice(0, C2)), ("h", slice(C2, None))):
+        r, g = ref[sl].ravel(), got[sl].ravel()
+        res[part] = (np.linalg.norm(g - r) / np.linalg.norm(r),
+                     float(r @ g / (np.linalg.norm(r) * np.linalg.norm(g))))
+    print("bf16 LSTM kernel gradient: x rows rel %.2e cos %.8f | h rows rel %.2e cos %.8f"
+          % (res["x"] + res["h"]))
+    assert res["x"][0] < 1e-2 and res["x"][1] > 0.9999, res
+    assert res["h"][0] < 1e-2 and res["h"][1] > 0.9999, res
 
 
 @pytest.mark.parametrize("batch", [100, 257])
