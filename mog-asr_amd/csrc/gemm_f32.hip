@@ -834,6 +834,19 @@ void launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, co
     // 54 -> 48 us; N = 256 layers and split-K weight gradients lose)
     bool t12864 = !ta && !b128 && D.N >= 512 && (long)D.M * D.N >= 8192L * 1024;
     if (force != nullptr) t12864 = atoi(force) == 12864;
+    // 32-deep k-tiles in two stages (the LDS bytes of 16-deep x 4): half the
+    // barriers per MFMA.  Measured (scripts/bench_gemm_f32.py):
+    // faster for the weight gradients (transA, +1..6 %) and the transB input
+    // gradients (dh +15 %), slower for the forward layers (recurrent -18 %,
+    // T*B-row layers -2..5 %).  MOG_GEMM_BK=16|32 forces one depth.
+    static const char* bk_env = getenv("MOG_GEMM_BK");
+    bool bk32 = ta || tb;
+    if (bk_env != nullptr) bk32 = atoi(bk_env) == 32;
+    if (bk32 && !b128) {
+      if (t12864) launch_dma<128, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
+      else launch_dma<64, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
+      return;
+    }
     if (t12864) {
       if (ta) launch_dma<128, 64, 16, 4>(ta, tb, epi, s, P, D, batch);
       else launch_dma<128, 64, 16, 3>(ta, tb, epi, s, P, D, batch);

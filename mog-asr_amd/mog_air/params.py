@@ -55,6 +55,7 @@ class ParamStore:
     def __init__(self, specs, device, seed: int = 1235):
         self.specs = list(specs)
         self.device = device
+        self._views: Dict[Tuple[str, str], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.offsets: Dict[str, int] = {}
         self.shapes: Dict[str, Tuple[int, ...]] = {}
         off = 0
@@ -80,10 +81,20 @@ class ParamStore:
 
     # ------------------------------------------------------------ views ---
     def view(self, name: str, buf: str = "flat") -> torch.Tensor:
+        """View of one variable inside a flat buffer.  Cached per (buffer,
+        name) while the buffer object stays the same: the train step asks for
+        ~100 views per step, and at the reference's batch of 64 the host-side
+        launch sequence, not the GPU, sets the step time."""
         t = getattr(self, buf)
+        key = (buf, name)
+        hit = self._views.get(key)
+        if hit is not None and hit[0] is t:
+            return hit[1]
         o = self.offsets[name]
         shape = self.shapes[name]
-        return t[o:o + int(np.prod(shape))].view(shape)
+        v = t[o:o + int(np.prod(shape))].view(shape)
+        self._views[key] = (t, v)
+        return v
 
     def g(self, name: str) -> torch.Tensor:
         return self.view(name, "grad")

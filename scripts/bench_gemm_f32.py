@@ -19,6 +19,10 @@ SHAPES = [
     ("enc2", B, 256, 512, 0, 0, ops.EPI_SOFTPLUS, 1),
     ("dec2", B, 512, 256, 0, 0, ops.EPI_SOFTPLUS, 1),
     ("genmean", B, 784, 512, 0, 0, ops.EPI_SIGMOID_NOISE, 1),
+    ("enc1_TB", TB, 512, 784, 0, 0, ops.EPI_SOFTPLUS, 1),
+    ("enc2_TB", TB, 256, 512, 0, 0, ops.EPI_SOFTPLUS, 1),
+    ("dec2_TB", TB, 512, 256, 0, 0, ops.EPI_SOFTPLUS, 1),
+    ("genmean_TB", TB, 784, 512, 0, 0, ops.EPI_SIGMOID_NOISE, 1),
     ("dX_dd2", TB, 512, 784, 0, 1, ops.EPI_SOFTPLUS_BWD, 1),
     ("dX_dg", TB, 784, 512, 0, 1, ops.EPI_STORE, 1),
     ("dX_da1", TB, 512, 256, 0, 1, ops.EPI_SOFTPLUS_BWD, 1),
