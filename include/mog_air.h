@@ -113,7 +113,8 @@ int mog_air_step_forward(int B, int HS, int HZ, int step, int train, int use_num
                          float* zprob_out, float* zkl_out, float* skl_out, float* shkl_out,
                          float* zmask, float* zval, float* zc, void* stream);
 /* Backward of the above: writes dout [5][B, 2] and dhid [5][B, HS] (head
- * strides dout_hs / dhid_hs elements).  The KL terms this step added to the
+ * strides dout_hs / dhid_hs elements; dhid_hs == HS means the heads side by
+ * side, [B][5][HS] with rows 5 HS apart).  The KL terms this step added to the
  * running loss are weighted by dloss[b] (the loss's cotangent per image), or by
  * the scalar grad_scale when dloss is NULL (a batch-mean loss: 1 / B). */
 int mog_air_step_backward(int B, int HS, int train, int use_num_prior, float temperature,

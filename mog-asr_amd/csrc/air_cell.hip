@@ -325,6 +325,9 @@ __global__ __launch_bounds__(256) void step_bwd_kernel(StepCfg cfg, StepBwdIO io
 }
 
 // dHh_z[b][l] = relu'(Hh) * sum_c dout_z[b][c] W2_z[l][c]
+// dhid layout: head z at dhid + z * dhid_hs, rows HS apart -- or, when
+// dhid_hs == HS (heads side by side), rows 5 * HS apart: [B][5][HS], so that
+// dh = [dhid_0 .. dhid_4] [W1_0 .. W1_4]^T is one plain GEMM over K = 5 HS
 __global__ __launch_bounds__(256) void heads_hidden_bwd_kernel(HeadPtrs hp, const float* dout,
                                                                long dout_hs, float* dhid,
                                                                long dhid_hs, int B, int HS) {
@@ -333,6 +336,7 @@ __global__ __launch_bounds__(256) void heads_hidden_bwd_kernel(HeadPtrs hp, cons
   const int zh = idx / ((long)B * HS);
   const long rem = idx - (long)zh * B * HS;
   const int b = rem / HS, l = rem - (long)b * HS;
+  const long rs = dhid_hs == HS ? 5L * HS : HS;
   const int k = (zh == 2 || zh == 3) ? 2 : 1;
   const float h = hp.hid[zh][(size_t)b * HS + l];
   float v = 0.0f;
@@ -340,7 +344,7 @@ __global__ __launch_bounds__(256) void heads_hidden_bwd_kernel(HeadPtrs hp, cons
     v = dout[zh * dout_hs + b * 2] * hp.w2[zh][l * k];
     if (k == 2) v += dout[zh * dout_hs + b * 2 + 1] * hp.w2[zh][l * k + 1];
   }
-  dhid[zh * dhid_hs + (long)b * HS + l] = v;
+  dhid[zh * dhid_hs + (long)b * rs + l] = v;
 }
 
 // --------------------------------------------------------- VAE sample ---

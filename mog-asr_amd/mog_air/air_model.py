@@ -174,7 +174,8 @@ class _Workspace:
         self.dz_all, self.tmp_a2_all = e(T, B, Z), e(T, B, R2)
         self.dth_f_all, self.dth_b_all, self.dot_all = e(T, B, 6), e(T, B, 6), e(T, B)
         self.dout = e(5, T, B, 2)
-        self.dhid = e(5, T, B, HS)
+        # heads side by side per row ([T, B, 5, HS]): dh is one GEMM over K = 5 HS
+        self.dhid = e(T, B, 5, HS)
         self.dh = e(T, B, H)
         self.dc = e(2, B, H)
         self.dG = e(T, B, 4 * H)
@@ -642,10 +643,12 @@ class AIRModel:
                 float(self.scale_prior_mean), float(self.scale_prior_variance),
                 float(self.shift_prior_mean), float(self.shift_prior_variance), float(gscale),
                 None, ws.rec[t], ws.eps_scale[t], ws.eps_shift[t], ws.dth_f_all[t], ws.dth_b_all[t],
-                ws.dot_all[t], hid_t, w2, ws.dout[0, t], T * B * 2, ws.dhid[0, t], T * B * HS)
-        # dh[t] = sum_z dhid_z W1_z^T for every step: one chain over K = 5 * HS
-        ops.gemm_kseg([ws.dhid[z] for z in range(5)], w1, ws.dh, TB, H, HS, HS, HS, H,
-                      transB=True)
+                ws.dot_all[t], hid_t, w2, ws.dout[0, t], T * B * 2, ws.dhid[t], HS)
+        # dh[t] = sum_z dhid_z W1_z^T for every step: one plain GEMM over
+        # K = 5 HS ([dhid_0 .. dhid_4] rows against [W1_0 .. W1_4]), the same
+        # k-ordered chain as the per-head sum
+        gemm([ws.dhid], [self._w1cat()], [ws.dh], TB, H, 5 * HS, 5 * HS, 5 * HS, H,
+             transB=True)
         # the heads' and the VAE's weight gradients are final here: their
         # all-reduce bucket runs while the LSTM chain below computes
         self._weight_grads_heads(ws)
@@ -962,11 +965,24 @@ class AIRModel:
             done.record(side)
         return done
 
+    def _w1cat(self):
+        """[W1_0 .. W1_4] side by side ([H, 5 HS]): the B operand of the heads'
+        dh GEMM, refreshed when the parameters change."""
+        if getattr(self, "_w1cat_version", None) != self.params.version:
+            if getattr(self, "_w1cat_buf", None) is None:
+                H, HS = self.rnn_units, self.scale_hidden_units
+                self._w1cat_buf = torch.empty((H, 5 * HS), device=self.device)
+            torch.cat([self._P(h + "/hidden/weights") for h in self._HEADS], dim=1,
+                      out=self._w1cat_buf)
+            self._w1cat_version = self.params.version
+        return self._w1cat_buf
+
     def _weight_grads_heads(self, ws):
         H, HS, TB = self.rnn_units, self.scale_hidden_units, ws.B * self.max_steps
         heads = list(enumerate(self._HEADS))
-        self._dw([ws.h] * 5, [ws.dhid[zi] for zi, _ in heads],
-                 [self._G(h + "/hidden/weights") for _, h in heads], TB, H, HS, H, HS,
+        dhid = ws.dhid.view(TB, 5, HS)
+        self._dw([ws.h] * 5, [dhid[:, zi] for zi, _ in heads],
+                 [self._G(h + "/hidden/weights") for _, h in heads], TB, H, HS, H, 5 * HS,
                  [self._G(h + "/hidden/biases") for _, h in heads])
         for k in (1, 2):
             sel = [(zi, h) for zi, h in heads if (2 if h.startswith("shift") else 1) == k]
