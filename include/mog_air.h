@@ -39,6 +39,16 @@ int mog_gemm_f32(int batch, const float* const* A, const float* const* B, float*
                  const float* const* aux, float* const* colsum, int M, int N, int K, int lda,
                  int ldb, int ldc, int ldaux, int transA, int transB, int epi, float aux_scale,
                  int splitk, void* stream);
+/* C = sigmoid((A B + bias) + scale * eps) for A [M][K] (lda), B [K][N] (ldb):
+ * the VAE output layer (vae.py:44-46) with the likelihood noise eps generated
+ * in the epilogue -- element (m, n) is lane n % 4 of Philox4x32-10 quad
+ * offset + m * N / 4 + n / 4, bit-identical to mog_rng_fill(seed, offset) of
+ * an [M][N] buffer read as the aux operand of epi 3.  N % 4 == 0.  Replaces
+ * TF's random_normal + add + sigmoid of the decoder (air_model.py:548-550). */
+int mog_gemm_f32_sigmoid_philox(const float* A, const float* B, float* C, const float* bias,
+                                int M, int N, int K, int lda, int ldb, int ldc, float scale,
+                                unsigned long long seed, unsigned long long offset,
+                                void* stream);
 /* C = epi(sum_s A_s op(B_s)) as one k-ordered chain over K = nseg * kseg
  * (nseg <= 8, kseg % 16 == 0; segment s from A[s] / B[s]); epi 0 or 5.  The
  * five heads' hidden-state gradient dh = sum_z dhid_z W1_z^T in one launch. */

@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include "mog_common.h"
+#include "philox.h"
 
 namespace {
 
@@ -57,7 +58,17 @@ struct GemmDims {
   int kseg;  // > 0: K is nseg segments of kseg, segment s read from A[s] / B[s]
   int vecC;  // C / Cpre / aux 16-byte aligned with ldc, ldaux % 4 == 0 (row-staged epilogue)
   float aux_scale;
+  // EPI_SIGMOID_NOISE with in-kernel noise (eps_gen): the noise of element
+  // (row, col) is lane col % 4 of Philox quad eps_off + row * N / 4 + col / 4,
+  // bit-identical to mog_rng_fill(seed, eps_off) of a [M][N] buffer
+  int eps_gen;
+  unsigned long long eps_seed, eps_off;
 };
+
+// noise quad of output row `row`, columns col .. col + 3 (col % 4 == 0)
+__device__ __forceinline__ void noise_quad(const GemmDims& D, int row, int col, float v[4]) {
+  mog_philox_quad(D.eps_seed, D.eps_off + (unsigned long long)row * (D.N / 4) + col / 4, true, v);
+}
 
 // LDS image of a BK-deep slice of an operand: one row of Lay<BK>::S floats
 // per m (A) or n (B).  The BK k values of a row are stored PERMUTED: k =
@@ -235,8 +246,17 @@ __device__ __forceinline__ void store_tile(const floatx4 (&acc)[MI][NI], const G
           if (Cpre != nullptr) Cpre[o] = v;
           if (EPI == EPI_RELU) C[o] = v > 0.0f ? v : 0.0f;
           if (EPI == EPI_SOFTPLUS) C[o] = mog_softplusf(v);
-          if (EPI == EPI_SIGMOID_NOISE)
-            C[o] = mog_sigmoidf(v + aux[(size_t)row * D.ldaux + col] * D.aux_scale);
+          if (EPI == EPI_SIGMOID_NOISE) {
+            float nz;
+            if (D.eps_gen) {
+              float q[4];
+              noise_quad(D, row, col & ~3, q);
+              nz = q[col & 3];
+            } else {
+              nz = aux[(size_t)row * D.ldaux + col];
+            }
+            C[o] = mog_sigmoidf(v + nz * D.aux_scale);
+          }
         }
       }
 }
@@ -288,7 +308,9 @@ __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[BM / 32][BN
       const float4 a4 = *reinterpret_cast<const float4*>(&sC[row * LDC + 4 * c4]);
       const float v[4] = {a4.x, a4.y, a4.z, a4.w};
       float x[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (HAS_AUX) {
+      if (EPI == EPI_SIGMOID_NOISE && D.eps_gen) {
+        noise_quad(D, grow, gcol, x);  // N % 4 == 0: the quad lies inside the row
+      } else if constexpr (HAS_AUX) {
         const float* ar = aux + (size_t)grow * D.ldaux + gcol;
         if (full) {
           const float4 x4 = *reinterpret_cast<const float4*>(ar);
@@ -917,7 +939,38 @@ extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const
   D.splitk = splitk;
   D.kchunk = 0;
   D.kseg = 0;
+  D.eps_gen = 0;
+  D.eps_seed = D.eps_off = 0;
   launch_auto(transA, transB, epi, mog_stream(stream), P, D, batch);
+  MOG_LAUNCH_RET();
+}
+
+// C = sigmoid((A B + bias) + scale * eps), eps standard normal from Philox
+// (seed, offset) in [M][N] fill order (vae.py:44-46, air_model.py:548-550 with
+// the noise of mog_rng_fill generated in the epilogue instead of read)
+extern "C" int mog_gemm_f32_sigmoid_philox(const float* A, const float* B, float* C,
+                                           const float* bias, int M, int N, int K, int lda,
+                                           int ldb, int ldc, float scale,
+                                           unsigned long long seed, unsigned long long offset,
+                                           void* stream) {
+  MOG_CHECK_ARG(A && B && C && M >= 0 && N >= 0 && K >= 0 && N % 4 == 0);
+  if (M == 0 || N == 0) return 0;
+  MOG_CHECK_ARG((long)(K - 1) * ldb + N < 0x1ffffffcL && (long)(M - 1) * lda + K < 0x1ffffffcL);
+  GemmPtrs P = {};
+  P.A[0] = A; P.B[0] = B; P.C[0] = C; P.bias[0] = bias;
+  GemmDims D;
+  D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc; D.ldaux = 0;
+  D.aux_scale = scale;
+  D.vecA = aligned16(A) && lda % 4 == 0;
+  D.vecB = aligned16(B) && ldb % 4 == 0;
+  D.vecC = aligned16(C) && ldc % 4 == 0;
+  D.splitk = 1;
+  D.kchunk = 0;
+  D.kseg = 0;
+  D.eps_gen = 1;
+  D.eps_seed = seed;
+  D.eps_off = offset;
+  launch_auto(false, false, EPI_SIGMOID_NOISE, mog_stream(stream), P, D, 1);
   MOG_LAUNCH_RET();
 }
 
@@ -955,6 +1008,8 @@ extern "C" int mog_gemm_f32_kseg(int nseg, const float* const* A, const float* c
   D.splitk = 1;
   D.kchunk = 0;
   D.kseg = kseg;
+  D.eps_gen = 0;
+  D.eps_seed = D.eps_off = 0;
   launch_auto(transA, transB, epi, mog_stream(stream), P, D, 1);
   MOG_LAUNCH_RET();
 }

@@ -74,6 +74,16 @@ void gemm_f32_(at::TensorList A, at::TensorList B, at::TensorList C,
         "gemm_f32_");
 }
 
+void gemm_f32_sigmoid_philox_(const Tensor& A, const Tensor& B, Tensor C,
+                              const optional<Tensor>& bias, int64_t M, int64_t N, int64_t K,
+                              int64_t lda, int64_t ldb, int64_t ldc, double scale, int64_t seed,
+                              int64_t offset) {
+  check(mog_gemm_f32_sigmoid_philox(f(A), f(B), f(C), f(bias), M, N, K, lda, ldb, ldc,
+                                    (float)scale, (unsigned long long)seed,
+                                    (unsigned long long)offset, stream()),
+        "gemm_f32_sigmoid_philox_");
+}
+
 void gemm_f32_kseg_(at::TensorList A, at::TensorList B, Tensor C, const optional<Tensor>& bias,
                     const optional<Tensor>& Cin, int64_t M, int64_t N, int64_t kseg, int64_t lda,
                     int64_t ldb, int64_t ldc, bool transA, bool transB, int64_t epi) {
@@ -307,6 +317,9 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "Tensor?[] Cpre, Tensor?[] aux, Tensor?[] colsum, int M, int N, int K, int lda, int ldb, "
       "int ldc, int ldaux, bool transA, bool transB, int epi, float aux_scale, int splitk) -> ()");
   m.def(
+      "gemm_f32_sigmoid_philox_(Tensor A, Tensor B, Tensor(a!) C, Tensor? bias, int M, int N, "
+      "int K, int lda, int ldb, int ldc, float scale, int seed, int offset) -> ()");
+  m.def(
       "gemm_f32_kseg_(Tensor[] A, Tensor[] B, Tensor(a!) C, Tensor? bias, Tensor? Cin, int M, "
       "int N, int kseg, int lda, int ldb, int ldc, bool transA, bool transB, int epi) -> ()");
   m.def(
@@ -388,6 +401,7 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
 TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("gemm_f32_", &gemm_f32_);
   m.impl("gemm_f32_kseg_", &gemm_f32_kseg_);
+  m.impl("gemm_f32_sigmoid_philox_", &gemm_f32_sigmoid_philox_);
   m.impl("gemm_bf16_", &gemm_bf16_);
   m.impl("cvt_bf16_batch_", &cvt_bf16_batch_);
   m.impl("stn_forward_", &stn_forward_);

@@ -366,6 +366,7 @@ class AIRModel:
             "generative_2", "gen_mean")
 
     def _fill_noise(self, ws: _Workspace, noise: Optional[Dict[str, torch.Tensor]]):
+        ws.eps_x_offset = None  # injected noise: every consumer reads the buffers
         if noise is not None:
             for k in ("eps_scale", "eps_shift", "eps_z", "eps_x", "u"):
                 src = noise[k]
@@ -375,13 +376,13 @@ class AIRModel:
                                      f"expected {tuple(dst.shape)}")
                 dst.copy_(src)
             return
-        ws.eps_x_offset = None
         for k, normal in (("eps_scale", True), ("eps_shift", True), ("eps_z", True),
                           ("eps_x", True), ("u", False)):
             buf = getattr(ws, k)
-            if k == "eps_x" and self.fused_step:
-                # generated inside the fused step kernel from the same Philox
-                # counters (bit-identical to filling the buffer)
+            if k == "eps_x" and self._eps_x_in_kernel(ws.B):
+                # generated inside the fused step kernel / the fp32 output
+                # layer's epilogue from the same Philox counters (bit-identical
+                # to filling the buffer)
                 ws.eps_x_offset = self._noise_ctr
             else:
                 ops.rng_fill(buf, self.noise_seed, self._noise_ctr, normal)
@@ -468,6 +469,12 @@ class AIRModel:
         fused step kernel and the all-steps STN write."""
         return self.fused_step or self._batched_vae(B)
 
+    def _eps_x_in_kernel(self, B: int) -> bool:
+        """The likelihood noise eps_x is generated where it is consumed: in the
+        fused step kernel (bf16) or in the fp32 output layer's epilogue (the
+        batched VAE), never materialised."""
+        return self.fused_step or (self.precision == "fp32" and self._batched_vae(B))
+
     def _batched_vae(self, B: int) -> bool:
         """AIR's VAE output never feeds the recurrence (the LSTM input is the
         image alone, air_model.py:454-456), so the glimpse VAE of every step
@@ -547,9 +554,15 @@ class AIRModel:
                  epi=EPI_SOFTPLUS, bias=[vb["generative_1"]], Cpre=[v(ws.d1pre)])
             gemm([v(ws.d1)], [vw["generative_2"]], [v(ws.d2)], TB, G2, G1, G1, G2, G2,
                  epi=EPI_SOFTPLUS, bias=[vb["generative_2"]], Cpre=[v(ws.d2pre)])
-            gemm([v(ws.d2)], [vw["gen_mean"]], [v(ws.r)], TB, W2, G2, G2, W2, W2,
-                 epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]],
-                 aux=[v(ws.eps_x)], ldaux=W2, aux_scale=lik_std)
+            if ws.eps_x_offset is not None:
+                # eps_x of steps t0.. in the epilogue: [T, B, W2] fill order
+                ops.gemm_sigmoid_philox(v(ws.d2), vw["gen_mean"], v(ws.r), vb["gen_mean"], TB, W2,
+                                        G2, G2, W2, W2, lik_std, self.noise_seed,
+                                        ws.eps_x_offset + t0 * B * W2 // 4)
+            else:
+                gemm([v(ws.d2)], [vw["gen_mean"]], [v(ws.r)], TB, W2, G2, G2, W2, W2,
+                     epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]],
+                     aux=[v(ws.eps_x)], ldaux=W2, aux_scale=lik_std)
         # STN write of every step into its canvas part (air_model.py:580-588);
         # the loss kernel adds the parts in step order (:665-675)
         _ops.stn_write_parts_(v(ws.r), TB, W, W, r_(ws.th_b), C, C, r_(ws.zval), r_(ws.zmask),

@@ -271,6 +271,9 @@ class AIRModel(_AirBase):
     def _parts_layout(self, B: int) -> bool:
         return self.fused_step
 
+    def _eps_x_in_kernel(self, B: int) -> bool:
+        return self.fused_step  # the fp32 ASR VAE runs per step and reads eps_x
+
     def _forward(self, X, targets, ws, need_grad, outputs=True):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
         C, W, C2 = self.canvas_size, self.windows_size, self.C2

@@ -56,6 +56,16 @@ def gemm(A: Sequence[torch.Tensor], B: Sequence[torch.Tensor], C: Sequence[torch
                    bool(transA), bool(transB), epi, float(aux_scale), int(splitk))
 
 
+def gemm_sigmoid_philox(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias, M: int, N: int,
+                        K: int, lda: int, ldb: int, ldc: int, scale: float, seed: int,
+                        offset: int) -> None:
+    """C = sigmoid((A B + bias) + scale * eps), eps generated in the epilogue
+    exactly as rng_fill(seed, offset) of an [M, N] buffer would hold it
+    (mog_gemm_f32_sigmoid_philox)."""
+    _ops.gemm_f32_sigmoid_philox_(A, B, C, bias, M, N, K, lda, ldb, ldc, float(scale),
+                                  _i64(seed), _i64(offset))
+
+
 def gemm_kseg(A: Sequence[torch.Tensor], B: Sequence[torch.Tensor], C: torch.Tensor, M: int,
               N: int, kseg: int, lda: int, ldb: int, ldc: int, transB=False, Cin=None,
               epi=EPI_STORE) -> None:
