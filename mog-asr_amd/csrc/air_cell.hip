@@ -347,6 +347,39 @@ __global__ __launch_bounds__(256) void heads_hidden_bwd_kernel(HeadPtrs hp, cons
   dhid[zh * dhid_hs + (long)b * rs + l] = v;
 }
 
+// The same, four hidden units per thread (HS % 4 == 0, 16-byte aligned rows):
+// one head per grid row (blockIdx.y), 32-bit index math, 16-byte loads of the
+// hidden activations and stores of dhid
+__global__ __launch_bounds__(256) void heads_hidden_bwd4_kernel(HeadPtrs hp, const float* dout,
+                                                                long dout_hs, float* dhid,
+                                                                long dhid_hs, int B, int HS) {
+  const int zh = blockIdx.y;
+  const int hq = HS >> 2;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= B * hq) return;
+  const int b = q / hq, l0 = (q - b * hq) * 4;
+  const int k = (zh == 2 || zh == 3) ? 2 : 1;
+  const float4 h = *reinterpret_cast<const float4*>(hp.hid[zh] + (size_t)b * HS + l0);
+  const float* dz = dout + zh * dout_hs + (size_t)b * 2;
+  const float d0 = dz[0], d1 = k == 2 ? dz[1] : 0.0f;
+  const float* w = hp.w2[zh];
+  const float hv[4] = {h.x, h.y, h.z, h.w};
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int l = l0 + e;
+    float a = 0.0f;
+    if (hv[e] > 0.0f) {
+      a = d0 * w[l * k];
+      if (k == 2) a += d1 * w[l * k + 1];
+    }
+    v[e] = a;
+  }
+  const long rs = dhid_hs == HS ? 5L * HS : HS;
+  *reinterpret_cast<float4*>(dhid + zh * dhid_hs + (size_t)b * rs + l0) =
+      make_float4(v[0], v[1], v[2], v[3]);
+}
+
 // --------------------------------------------------------- VAE sample ---
 struct VaeCfg {
   int B, Z;
@@ -683,8 +716,14 @@ extern "C" int mog_air_step_backward(int B, int HS, int train, int use_num_prior
     MOG_CHECK_ARG(hid[i] && w2[i]);
     hp.hid[i] = hid[i]; hp.w2[i] = w2[i]; hp.b2[i] = nullptr;
   }
-  heads_hidden_bwd_kernel<<<mog_cdiv(5L * B * HS, 256), 256, 0, s>>>(hp, dout, dout_hs, dhid,
-                                                                      dhid_hs, B, HS);
+  bool vec = HS % 4 == 0 && (dhid_hs % 4) == 0 && (reinterpret_cast<uintptr_t>(dhid) & 15) == 0;
+  for (int i = 0; i < 5; ++i) vec = vec && (reinterpret_cast<uintptr_t>(hid[i]) & 15) == 0;
+  if (vec)
+    heads_hidden_bwd4_kernel<<<dim3(mog_cdiv((long)B * (HS / 4), 256), 5), 256, 0, s>>>(
+        hp, dout, dout_hs, dhid, dhid_hs, B, HS);
+  else
+    heads_hidden_bwd_kernel<<<mog_cdiv(5L * B * HS, 256), 256, 0, s>>>(hp, dout, dout_hs, dhid,
+                                                                        dhid_hs, B, HS);
   MOG_LAUNCH_RET();
 }
 
