@@ -130,11 +130,30 @@ def make_model(precision, dev, world, rank, scope, canvas=50):
                     precision=precision)
 
 
-def timed_train(precision, B, steps, warmup, dev, world=1, rank=0, events=False, scope="bench"):
+def make_asr_model(precision, dev, scope, canvas=50):
+    """configs[2]: train_air_pr.py -dn 13 -gm 100 -gne 10 (AIR-ASR with the
+    number regularisers: objects {1, 3}, margin gamma 100, element gamma 10,
+    z_pres temperature 0.1, MAX_STEPS 6; train_air_pr.py:63-82)."""
+    from mog_air.asr_model import AIRModel as AsrModel
+    return AsrModel(None, None, max_steps=6, max_digits=6, rnn_units=256, canvas_size=canvas,
+                    windows_size=28, vae_latent_dimensions=50, vae_recognition_units=(512, 256),
+                    vae_generative_units=(256, 512), fix_scale_distribution=True,
+                    vae_prior_mean=0.0, vae_prior_variance=1.0, vae_likelihood_std=0.0,
+                    scale_hidden_units=64, shift_hidden_units=64, z_pres_hidden_units=64,
+                    z_pres_prior_log_odds=-0.01, z_pres_temperature=0.1, stopping_threshold=0.9,
+                    learning_rate=1e-4, gradient_clipping_norm=1.0, cnn=False, train=True,
+                    scope=scope, constrains_num=[1, 3], constrains_margin_gamma=100.0,
+                    constrains_num_element_gamma=10.0, constrains_area_minmax=[17, 23],
+                    annealing_schedules={}, device=dev, seed=1235, precision=precision)
+
+
+def timed_train(precision, B, steps, warmup, dev, world=1, rank=0, events=False, scope="bench",
+                model=None):
     """Time `steps` train steps of batch B per rank (after `warmup`); returns
     (seconds, model).  Barrier + synchronize on both sides; the caller takes
     the max over ranks."""
-    model = make_model(precision, dev, world, rank, scope)
+    if model is None:
+        model = make_model(precision, dev, world, rank, scope)
     if world > 1:
         from mog_air import parallel
         parallel.attach(model)  # bucketed RCCL all-reduce overlapped with the backward
@@ -421,6 +440,18 @@ def main():
                                 "accumulate), fused STN+VAE step kernel, LSTM/heads/STN/loss "
                                 "fp32", "roofline": roofline(m2.kernel_events, B, "bf16")}
                 del m2
+            for prec in ("fp32", "bf16"):
+                el4, m4 = timed_train(prec, B, 10, 3, dev,
+                                      model=make_asr_model(prec, dev, "bench_asr_" + prec))
+                out["configs_2_asr_" + prec] = {
+                    "value": B * 10 / el4, "unit": "images/sec", "ms_per_step": el4 / 10 * 1e3,
+                    "dtype": prec, "batch": B, "steps": 10, "max_steps": 6,
+                    "executed_steps": m4.executed_steps,
+                    "workload": "configs[2]: AIR-ASR train step (train_air_pr.py -dn 13 -gm 100 "
+                                "-gne 10: number regularisers, learned z_pres prior, "
+                                "MAX_STEPS 6)"}
+                del m4
+            torch.cuda.empty_cache()
             el3, m3 = timed_train("fp32", 64, 50, 5, dev, scope="bench_b64")
             out["config_1_batch64_fp32"] = {
                 "value": 64 * 50 / el3, "unit": "images/sec", "ms_per_step": el3 / 50 * 1e3,

@@ -428,8 +428,21 @@ __device__ __forceinline__ void stn_bwd_image(
       if (lane + 64 * k < HWin / 4) reinterpret_cast<floatx4*>(sU)[lane + 64 * k] = us[k];
     if (lane < Hout) rowtab[lane] = ry;
   } else if ((HWin & 3) == 0) {
+    // axis-aligned without dU (the STN read backward, glimpse <- canvas):
+    // only the source rows between the clipped corner rows of output rows 0
+    // and Hout - 1 (the map is monotonic, so every row's corners lie there)
+    // are staged -- the window's rows, not the whole canvas
+    int q0 = 0, q1 = HWin / 4;
+    if (mode == 1) {
+      const float2 ea = axis_row(th, Hin, Win, Hout, Wout, 0);
+      const float2 eb = axis_row(th, Hin, Win, Hout, Wout, Hout - 1);
+      const int ylo = min(min(axis_lo(ea), axis_hi(ea)), min(axis_lo(eb), axis_hi(eb)));
+      const int yhi = max(max(axis_lo(ea), axis_hi(ea)), max(axis_lo(eb), axis_hi(eb)));
+      q0 = (ylo * Win) >> 2;
+      q1 = min(HWin / 4, ((yhi + 1) * Win + 3) >> 2);
+    }
     const floatx4* src = reinterpret_cast<const floatx4*>(Un);
-    for (int q = lane; q < HWin / 4; q += 64) reinterpret_cast<floatx4*>(sU)[q] = src[q];
+    for (int q = q0 + lane; q < q1; q += 64) reinterpret_cast<floatx4*>(sU)[q] = src[q];
   } else {
     for (int i = lane; i < HWin; i += 64) sU[i] = Un[i];
   }
