@@ -310,12 +310,15 @@ class AIRModel(_AirBase):
             _lib.call("mog_asr_pack", B, Z, H, LU, dp(ws.z[t - 1]) if prev else None,
                       dp(ws.ss[t - 1]) if prev else None, dp(ws.hg[t - 1]) if prev else None,
                       dp(ws.Ug[t]), s)
-            KU = Z + 3 + H
-            gemm([ws.U[t]], [Ki[C2:]], [ws.G[t]], B, 4 * H, KU, LU, 4 * H, 4 * H, bias=[bi],
+            # K = LU: the packed rows end in zeros, so the chain's last terms are
+            # 0 * w (exactly +-0: the sum is unchanged bit for bit) and the
+            # operands are 16-byte rows (LDS-DMA GEMM); the 3 weight rows read
+            # past the U-part are the following variables (finite), in bounds
+            gemm([ws.U[t]], [Ki[C2:]], [ws.G[t]], B, 4 * H, LU, LU, 4 * H, 4 * H, bias=[bi],
                  Cin=[ws.Gx])
             _ops.lstm_cell_forward_(ws.G[t], None, ws.c[t - 1] if prev else None, ws.c[t],
                                     ws.h[t], B, H)
-            gemm([ws.Ug[t]], [Kg], [ws.Gg[t]], B, 4 * H, KU, LU, 4 * H, 4 * H, bias=[bg])
+            gemm([ws.Ug[t]], [Kg], [ws.Gg[t]], B, 4 * H, LU, LU, 4 * H, 4 * H, bias=[bg])
             _ops.lstm_cell_forward_(ws.Gg[t], None, ws.cg[t - 1] if prev else None, ws.cg[t],
                                     ws.hg[t], B, H)
             hid = [ws.hid8[k, t] for k in range(8)]
@@ -440,9 +443,10 @@ class AIRModel(_AirBase):
             _ops.lstm_cell_backward_(ws.Gg[t], None, ws.cg[t - 1] if t > 0 else None, ws.cg[t],
                                      ws.dhg[t], dcg_in, ws.dGg[t], ws.dcg[t % 2], ws.dGgsum, B, H)
             if t > 0:
-                gemm([ws.dG[t]], [Ki[C2:]], [ws.dU], B, KU, 4 * H, 4 * H, 4 * H, LU,
+                # N = LU: the 3 pad columns of dU / dUg are scratch (unpack skips them)
+                gemm([ws.dG[t]], [Ki[C2:]], [ws.dU], B, LU, 4 * H, 4 * H, 4 * H, LU,
                      transB=True)
-                gemm([ws.dGg[t]], [Kg], [ws.dUg], B, KU, 4 * H, 4 * H, 4 * H, LU, transB=True)
+                gemm([ws.dGg[t]], [Kg], [ws.dUg], B, LU, 4 * H, 4 * H, 4 * H, LU, transB=True)
                 _lib.call("mog_asr_unpack", B, Z, H, LU, dp(ws.dU), dp(ws.dUg),
                           dp(ws.dz_carry), dp(ws.dss_carry), dp(ws.dh[t - 1]),
                           dp(ws.dhg[t - 1]), s)
@@ -464,8 +468,11 @@ class AIRModel(_AirBase):
             self._x_grad_bf16(X, ws, gKi, G("infer_rnn_running/bias"), 0, C2)
         else:
             self._dw(X, ws.dGsum, gKi[:C2], B, C2, 4 * H, C2, 4 * H, G("infer_rnn_running/bias"))
-        self._dw(ws.U, ws.dG, gKi[C2:], TB, KU, 4 * H, LU, 4 * H)
-        self._dw(ws.Ug, ws.dGg, gKg, TB, KU, 4 * H, LU, 4 * H, G("gen_rnn_running/bias"))
+        # M = LU (16-byte aligned LDS-DMA operands): the 3 pad rows of U^T are
+        # zero, so their rows of the product are exactly +-0 and the atomics
+        # leave the following variables' gradients unchanged
+        self._dw(ws.U, ws.dG, gKi[C2:], TB, LU, 4 * H, LU, 4 * H)
+        self._dw(ws.Ug, ws.dGg, gKg, TB, LU, 4 * H, LU, 4 * H, G("gen_rnn_running/bias"))
         # hidden layers reading h_t, hg_t, hg_{t-1}
         hs = ("inf_shift/dense", "inf_shift/dense_2", "z_pres/log_odds/dense", "inf_scale/dense",
               "inf_scale/dense_2")
