@@ -27,11 +27,12 @@ def _ceil(a, b):
     return (a + b - 1) // b
 
 
-def _x_grad_grid_fp32(B, C2=2500, N=1024, target=2048):
-    """gemm_f32 transA split-K launch of dWx (air_model._dw, launch_tile)."""
+def _x_grad_grid_fp32(B, C2=2500, N=1024, target=2048, BK=32):
+    """gemm_f32 transA split-K launch of dWx (air_model._dw, launch_dma with
+    32-deep k-tiles for transA)."""
     tiles = _ceil(C2, 64) * _ceil(N, 64)
     splitk = max(1, min(B // 256, _ceil(target, tiles)))
-    kchunk = _ceil(_ceil(B, splitk), 16) * 16
+    kchunk = _ceil(_ceil(B, splitk), BK) * BK
     return tiles * _ceil(B, kchunk) * 256
 
 
@@ -39,7 +40,7 @@ def _x_grad_grid_fp32(B, C2=2500, N=1024, target=2048):
 TAGS = {
     "lstm_x_projection_fp32_b%d" % B: ("gemm_f32_dma_kernel<128, 128, 16, 3, false, false, 0>",
                                        (1024 // 128) * (B // 128) * 256),
-    "lstm_x_projection_grad_fp32_b%d" % B: ("gemm_f32_dma_kernel<64, 64, 16, 4, true, false, 5>",
+    "lstm_x_projection_grad_fp32_b%d" % B: ("gemm_f32_dma_kernel<64, 64, 32, 2, true, false, 5>",
                                             _x_grad_grid_fp32(B)),
     "lstm_x_projection_bf16_b%d" % B: ("gemm_f32_dma_kernel<128, 128, 16, 3, false, false, 0>",
                                        (1024 // 128) * (B // 128) * 256),
