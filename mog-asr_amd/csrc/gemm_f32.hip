@@ -339,14 +339,18 @@ __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[BM / 32][BN
       }
       float* cr = C + (size_t)grow * D.ldc + gcol;
       float* pr = (HAS_PRE && Cpre) ? Cpre + (size_t)grow * D.ldc + gcol : nullptr;
+      // the pre-activation is read only by the backward, long after: stored
+      // non-temporal so it does not displace the next layer's operands
       if (full) {
         *reinterpret_cast<float4*>(cr) = make_float4(o[0], o[1], o[2], o[3]);
-        if (pr) *reinterpret_cast<float4*>(pr) = make_float4(pre[0], pre[1], pre[2], pre[3]);
+        if (pr)
+          __builtin_nontemporal_store(floatx4{pre[0], pre[1], pre[2], pre[3]},
+                                      reinterpret_cast<floatx4*>(pr));
       } else {
         for (int e = 0; e < 4; ++e)
           if (gcol + e < N) {
             cr[e] = o[e];
-            if (pr) pr[e] = pre[e];
+            if (pr) __builtin_nontemporal_store(pre[e], pr + e);
           }
       }
     }
