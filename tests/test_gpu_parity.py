@@ -160,6 +160,33 @@ def test_stn_backward_vs_autograd(sep, src, dst):
                                atol=1e-3)
 
 
+def test_stn_read_backward_dtheta_only():
+    """The STN read backward without dU (canvas -> glimpse, dtheta only: the
+    train step's form) stages only the window's source rows: dtheta must be
+    bit-identical to the form that stages the whole canvas (want_dU), and match
+    float64 autograd -- windows partly outside the canvas, flipped axes and
+    tiny / large scales included."""
+    from mog_air import ops
+    rng = np.random.default_rng(17)
+    N = 48
+    x = rng.uniform(size=(N, 50, 50))
+    s = rng.uniform(0.1, 1.3, N) * np.where(np.arange(N) % 5 == 0, -1.0, 1.0)
+    t = rng.uniform(-1.3, 1.3, (N, 2))
+    th = np.stack([s, 0 * s, t[:, 0], 0 * s, s, t[:, 1]], 1)
+    G = rng.standard_normal((N, 784))
+    _, dth_only, _ = ops.stn_backward(_cuda(x.reshape(N, -1)), _cuda(th), (28, 28), _cuda(G),
+                                      want_dU=False)
+    _, dth_full, _ = ops.stn_backward(_cuda(x.reshape(N, -1)), _cuda(th), (28, 28), _cuda(G))
+    assert torch.equal(dth_only, dth_full)
+    U = torch.tensor(x)
+    TH = torch.tensor(th, requires_grad=True)
+    out = at.transformer(U, TH, (28, 28)).reshape(N, -1)
+    (out * torch.tensor(G)).sum().backward()
+    gt, got = TH.grad.numpy(), dth_only.cpu().numpy()
+    for k in (0, 2, 4, 5):
+        np.testing.assert_allclose(got[:, k], gt[:, k], rtol=1e-3, atol=1e-3)
+
+
 @pytest.mark.parametrize("sep,dt", [(True, torch.bfloat16), (False, torch.bfloat16),
                                     (True, torch.float32), (False, torch.float32)])
 def test_stn_backward_sigmoid_bf16_matches_unfused(sep, dt):
