@@ -367,10 +367,14 @@ def spawn_ranks(n: int) -> int:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     procs = []
+    # more ranks than GPUs (a rehearsal of the data-parallel path on a one-GPU
+    # box): RCCL refuses two ranks on one device, so those ranks use gloo
+    # (device_count() does not initialise the GPU in this parent)
+    extra = {} if n <= torch.cuda.device_count() else {"MOG_DP_BACKEND": "gloo"}
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+                   HSA_ENABLE_IPC_MODE_LEGACY="0", **extra)
         procs.append(subprocess.Popen([sys.executable] + sys.argv, env=env))
     rcs = [p.wait() for p in procs]
     return max(rcs, key=abs)
@@ -386,10 +390,11 @@ def main():
     backend = None
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        # RCCL needs one GPU per rank; more ranks than GPUs (a rehearsal of the
-        # data-parallel path on a one-GPU box) share the devices over gloo
+        # RCCL (one GPU per rank, as torch.distributed.run starts the ranks);
+        # MOG_DP_BACKEND=gloo for ranks sharing a device (spawn_ranks sets it
+        # when asked for more ranks than there are GPUs)
         ndev = torch.cuda.device_count()
-        backend = os.environ.get("MOG_DP_BACKEND") or ("nccl" if world <= ndev else "gloo")
+        backend = os.environ.get("MOG_DP_BACKEND") or "nccl"
         local = local % max(ndev, 1)
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -417,7 +422,8 @@ def main():
     if rank == 0:
         out = {
             "metric": METRIC, "value": value, "unit": "images/sec",
-            "n_gpus": min(world, torch.cuda.device_count()), "ranks": world,
+            "n_gpus": world if backend in (None, "nccl") else min(world, torch.cuda.device_count()),
+            "ranks": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.precision, "data": "synthetic",
