@@ -494,16 +494,23 @@ class AIRModel(_AirBase):
         outs = (("inf_shift/dense_1", 0, 0, 2), ("inf_shift/dense_3", 1, 2, 2),
                 ("z_pres/log_odds/dense_1", 2, 4, 1), ("gen_shift/dense_1", 3, 5, 2),
                 ("gen_shift/dense_3", 4, 7, 2))
-        for n, hk, col, k in outs:
-            self._dw(ws.hid8[hk], d[..., col:], G(n + "/kernel"), TB, 64, k, 64, D_N,
-                     G(n + "/bias"))
+        # grouped by shape, one batched launch per group (each is a tiny
+        # [64 x 1..2] product over K = T*B rows: launch-bound one by one)
+        one = [(ws.hid8[hk], d[..., col:], G(n + "/kernel"), G(n + "/bias"))
+               for n, hk, col, k in outs if k == 1]
+        two = [(ws.hid8[hk], d[..., col:], G(n + "/kernel"), G(n + "/bias"))
+               for n, hk, col, k in outs if k == 2]
         if fix < 0:
-            self._dw(ws.hid8[5], d[..., 9:], G("z_pres/prior/dense_1/kernel"), TB, 64, 1, 64, D_N,
-                     G("z_pres/prior/dense_1/bias"))
-        for n, hk, col in (("inf_scale/dense_1", 6, 10), ("inf_scale/dense_3", 7, 11)):
-            self._dw(ws.hid8[hk], d[..., col:], G(n + "/kernel")[:64], TB, 64, 1, 64, D_N,
-                     G(n + "/bias"))
-            self._dw(ws.ss, d[..., col:], G(n + "/kernel")[64:], TB, 2, 1, 3, D_N)
+            one.append((ws.hid8[5], d[..., 9:], G("z_pres/prior/dense_1/kernel"),
+                        G("z_pres/prior/dense_1/bias")))
+        scl = (("inf_scale/dense_1", 6, 10), ("inf_scale/dense_3", 7, 11))
+        one += [(ws.hid8[hk], d[..., col:], G(n + "/kernel")[:64], G(n + "/bias"))
+                for n, hk, col in scl]
+        for grp, k in ((two, 2), (one, 1)):
+            self._dw([g[0] for g in grp], [g[1] for g in grp], [g[2] for g in grp], TB, 64, k,
+                     64, D_N, [g[3] for g in grp])
+        self._dw([ws.ss] * 2, [d[..., col:] for _, _, col in scl],
+                 [G(n + "/kernel")[64:] for n, _, _ in scl], TB, 2, 1, 3, D_N)
 
     # ------------------------------------------------------- outputs -----
     @property
