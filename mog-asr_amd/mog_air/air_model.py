@@ -941,8 +941,8 @@ class AIRModel:
         gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
         self._dw(ws.g, ws.da1, g("recognition_1"), TB, W2, R1, W2, R1, gb("recognition_1"))
         self._dw(ws.a1, ws.da2, g("recognition_2"), TB, R1, R2, R1, R2, gb("recognition_2"))
-        self._dw(ws.a2, ws.dmu, g("rec_mean"), TB, R2, Z, R2, Z, gb("rec_mean"))
-        self._dw(ws.a2, ws.dlv, g("rec_log_variance"), TB, R2, Z, R2, Z, gb("rec_log_variance"))
+        self._dw([ws.a2] * 2, [ws.dmu, ws.dlv], [g("rec_mean"), g("rec_log_variance")], TB, R2,
+                 Z, R2, Z, [gb("rec_mean"), gb("rec_log_variance")])
         self._dw(ws.z, ws.dd1, g("generative_1"), TB, Z, G1, Z, G1, gb("generative_1"))
         self._dw(ws.d1, ws.dd2, g("generative_2"), TB, G1, G2, G1, G2, gb("generative_2"))
         self._dw(ws.d2, ws.dm, g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
