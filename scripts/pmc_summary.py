@@ -47,7 +47,11 @@ TAGS = {
     "stn_vae_step_bf16_b%d" % B: ("stn_vae_step", B // 32 * 1024),
     "stn_vae_step_b65536": ("stn_vae_step", 65536 // 64 * 1024),
     "stn_vae_step_b65536_c64": ("stn_vae_step", 65536 // 64 * 1024),
+    "stn_vae_step_b65536_fwd": ("stn_vae_step", 65536 // 64 * 1024),
 }
+# bench.py runs the three B = 65,536 fused-step measurements in this order
+# (same symbol and grid): training form at C = 50, at C = 64, forward-only at C = 50
+FUSED_ORDER = ("stn_vae_step_b65536", "stn_vae_step_b65536_c64", "stn_vae_step_b65536_fwd")
 
 
 def load(d, counter):
@@ -78,11 +82,13 @@ def main():
             continue
         fmax = max(v for _, v, _ in fv)
         fsel = [(i, v) for i, v, _ in fv if v >= 0.5 * fmax]
-        # fused-step runs at C = 50 and C = 64 share symbol and grid: the
-        # C = 64 run comes second in the bench (dispatch order)
-        if tag.startswith("stn_vae_step_b65536"):
-            half = len(fsel) // 2
-            fsel = fsel[half:] if tag.endswith("_c64") else fsel[:half]
+        # the three fused-step runs share symbol and grid: equal groups of
+        # dispatches in FUSED_ORDER (dispatch order)
+        if tag in FUSED_ORDER:
+            fsel = [(i, v) for i, v, _ in fv]
+            third = len(fsel) // 3
+            g = FUSED_ORDER.index(tag)
+            fsel = fsel[g * third:(g + 1) * third]
             if not fsel:
                 continue
         ids = [i for i, _ in fsel]
