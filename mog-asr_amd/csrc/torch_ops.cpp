@@ -1,16 +1,22 @@
 // PyTorch-ROCm custom operators over the C ABI of libmog_air.so
 // (include/mog_air.h): TORCH_LIBRARY_FRAGMENT(mog_air) schemas with HIP
 // (dispatch key CUDA on ROCm) implementations, so the Python host drives every
-// hot-path launch through torch.ops.mog_air.* (SURVEY.md §8 B).  Each op takes
-// device tensors (or views: a tensor's data_ptr is the matrix origin) and plain
-// scalars, launches on torch's current HIP stream, and raises (c10::Error ->
-// RuntimeError) when the C ABI rejects an argument.  There is no CPU kernel: a
-// CPU tensor finds no implementation and fails loudly.
+// hot-path launch through torch.ops.mog_air.*  -- the AIR
+// model (air/air_model.py) and the AIR-ASR model
+// (air/air_number_bbox_location.py) alike.  Each op takes device tensors (or
+// views: a tensor's data_ptr is the matrix origin, leading dimensions are
+// explicit) and plain scalars, launches on torch's current HIP stream of the
+// operands' device, and raises (c10::Error -> RuntimeError) when an operand is
+// on the wrong device, has the wrong dtype or is too small for the extent the
+// launch touches, or when the C ABI rejects an argument.  There is no CPU
+// kernel: a CPU tensor finds no implementation and fails loudly.  Every
+// argument an op writes carries a (x!) alias annotation in its schema.
 //
-// The ops are the launch-level (mutating, "out=") form the AIRModel schedules
-// its forward / backward with; differentiable functional ops built on them
+// The ops are the launch-level (mutating, "out=") form the models schedule
+// their forward / backward with; differentiable functional ops built on them
 // live in mog_air/torch_ops.py.
 #include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
@@ -20,36 +26,81 @@
 
 namespace {
 
+using at::ScalarType;
 using at::Tensor;
 using c10::optional;
 using std::vector;
 
-void* stream() { return c10::hip::getCurrentHIPStream().stream(); }
+constexpr ScalarType F32 = at::kFloat, BF16 = at::kBFloat16, I32 = at::kInt;
 
 void check(int rc, const char* name) {
   TORCH_CHECK(rc == 0, "mog_air::", name, " failed: ",
               rc == MOG_ERR_INVALID ? "invalid argument" : "HIP error ", rc);
 }
 
-void* p(const Tensor& t) {
-  TORCH_CHECK(t.is_cuda(), "mog_air ops take HIP device tensors (no CPU implementation)");
-  return t.data_ptr();
-}
-void* p(const optional<Tensor>& t) { return t.has_value() && t->defined() ? p(*t) : nullptr; }
-float* f(const Tensor& t) { return static_cast<float*>(p(t)); }
-float* f(const optional<Tensor>& t) { return static_cast<float*>(p(t)); }
+// Operand validation: every tensor on the op's device (the first checked
+// operand fixes it), of the dtype the C ABI reads, and holding at least
+// `extent` elements from its data_ptr (the span the launch reads or writes).
+struct Op {
+  const char* name;
+  c10::optional<c10::Device> dev;
+  explicit Op(const char* n) : name(n) {}
+  void* need(const Tensor& t, ScalarType st, int64_t extent, const char* arg) {
+    TORCH_CHECK(t.defined(), name, ": ", arg, " is undefined");
+    TORCH_CHECK(t.is_cuda(), name, ": ", arg,
+                " must be a HIP device tensor (there is no CPU implementation)");
+    if (!dev) dev = t.device();
+    TORCH_CHECK(t.device() == *dev, name, ": ", arg, " is on ", t.device(), ", the op on ", *dev);
+    TORCH_CHECK(t.scalar_type() == st, name, ": ", arg, " must be ", st, ", got ",
+                t.scalar_type());
+    if (extent > 0) {
+      const int64_t avail =
+          (int64_t)(t.storage().nbytes() / t.element_size()) - t.storage_offset();
+      TORCH_CHECK(extent <= avail, name, ": ", arg, " holds ", avail,
+                  " elements from its origin, the launch touches ", extent);
+    }
+    return t.data_ptr();
+  }
+  void* need(const optional<Tensor>& t, ScalarType st, int64_t extent, const char* arg) {
+    return t.has_value() && t->defined() ? need(*t, st, extent, arg) : nullptr;
+  }
+  float* f(const Tensor& t, int64_t extent, const char* arg) {
+    return static_cast<float*>(need(t, F32, extent, arg));
+  }
+  float* f(const optional<Tensor>& t, int64_t extent, const char* arg) {
+    return static_cast<float*>(need(t, F32, extent, arg));
+  }
+  int* i(const Tensor& t, int64_t extent, const char* arg) {
+    return static_cast<int*>(need(t, I32, extent, arg));
+  }
+  int* i(const optional<Tensor>& t, int64_t extent, const char* arg) {
+    return static_cast<int*>(need(t, I32, extent, arg));
+  }
+  // device pointer arrays of tensor lists (None entries -> NULL)
+  vector<void*> list(at::TensorList ts, ScalarType st, int64_t extent, const char* arg) {
+    vector<void*> v;
+    for (const auto& t : ts) v.push_back(need(t, st, extent, arg));
+    return v;
+  }
+  vector<void*> list(const c10::List<optional<Tensor>>& ts, ScalarType st, int64_t extent,
+                     const char* arg) {
+    vector<void*> v;
+    for (size_t k = 0; k < ts.size(); ++k)
+      v.push_back(need(static_cast<optional<Tensor>>(ts[k]), st, extent, arg));
+    return v;
+  }
+  // the current HIP stream of the op's device (set by the guard)
+  void* stream() {
+    TORCH_CHECK(dev.has_value(), name, ": no device operand");
+    return c10::hip::getCurrentHIPStream(dev->index()).stream();
+  }
+};
 
-// device pointer arrays of tensor lists (None entries -> NULL)
-vector<void*> ptrs(const at::TensorList& ts) {
-  vector<void*> v;
-  for (const auto& t : ts) v.push_back(p(t));
-  return v;
+// elements spanned by a rows x cols matrix with leading dimension ld
+int64_t mat(int64_t rows, int64_t cols, int64_t ld) {
+  return rows <= 0 || cols <= 0 ? 0 : (rows - 1) * ld + cols;
 }
-vector<void*> ptrs(const c10::List<optional<Tensor>>& ts) {
-  vector<void*> v;
-  for (size_t i = 0; i < ts.size(); ++i) v.push_back(p(static_cast<optional<Tensor>>(ts[i])));
-  return v;
-}
+
 template <class T>
 const T* const* arr(const vector<void*>& v) {
   return v.empty() ? nullptr : reinterpret_cast<const T* const*>(v.data());
@@ -59,6 +110,8 @@ T* const* marr(const vector<void*>& v) {
   return v.empty() ? nullptr : reinterpret_cast<T* const*>(v.data());
 }
 
+#define GUARD(op) const c10::hip::HIPGuardMasqueradingAsCUDA guard_(*op.dev)
+
 // ---------------------------------------------------------------- GEMMs ----
 void gemm_f32_(at::TensorList A, at::TensorList B, at::TensorList C,
                const c10::List<optional<Tensor>>& bias, const c10::List<optional<Tensor>>& Cin,
@@ -66,31 +119,50 @@ void gemm_f32_(at::TensorList A, at::TensorList B, at::TensorList C,
                const c10::List<optional<Tensor>>& colsum, int64_t M, int64_t N, int64_t K,
                int64_t lda, int64_t ldb, int64_t ldc, int64_t ldaux, bool transA, bool transB,
                int64_t epi, double aux_scale, int64_t splitk) {
-  auto a = ptrs(A), b = ptrs(B), c = ptrs(C), bi = ptrs(bias), ci = ptrs(Cin), cp = ptrs(Cpre),
-       ax = ptrs(aux), cs = ptrs(colsum);
+  Op o("gemm_f32_");
+  auto c = o.list(C, F32, mat(M, N, ldc), "C");
+  auto a = o.list(A, F32, transA ? mat(K, M, lda) : mat(M, K, lda), "A");
+  auto b = o.list(B, F32, transB ? mat(N, K, ldb) : mat(K, N, ldb), "B");
+  auto bi = o.list(bias, F32, N, "bias"), ci = o.list(Cin, F32, mat(M, N, ldc), "Cin");
+  auto cp = o.list(Cpre, F32, mat(M, N, ldc), "Cpre"), ax = o.list(aux, F32, mat(M, N, ldaux), "aux");
+  auto cs = o.list(colsum, F32, N, "colsum");
+  GUARD(o);
   check(mog_gemm_f32((int)c.size(), arr<float>(a), arr<float>(b), marr<float>(c), arr<float>(bi),
                      arr<float>(ci), marr<float>(cp), arr<float>(ax), marr<float>(cs), M, N, K, lda,
-                     ldb, ldc, ldaux, transA, transB, epi, (float)aux_scale, splitk, stream()),
-        "gemm_f32_");
+                     ldb, ldc, ldaux, transA, transB, epi, (float)aux_scale, splitk, o.stream()),
+        o.name);
 }
 
 void gemm_f32_sigmoid_philox_(const Tensor& A, const Tensor& B, Tensor C,
                               const optional<Tensor>& bias, int64_t M, int64_t N, int64_t K,
                               int64_t lda, int64_t ldb, int64_t ldc, double scale, int64_t seed,
                               int64_t offset) {
-  check(mog_gemm_f32_sigmoid_philox(f(A), f(B), f(C), f(bias), M, N, K, lda, ldb, ldc,
-                                    (float)scale, (unsigned long long)seed,
-                                    (unsigned long long)offset, stream()),
-        "gemm_f32_sigmoid_philox_");
+  Op o("gemm_f32_sigmoid_philox_");
+  float* c = o.f(C, mat(M, N, ldc), "C");
+  float* a = o.f(A, mat(M, K, lda), "A");
+  float* b = o.f(B, mat(K, N, ldb), "B");
+  float* bi = o.f(bias, N, "bias");
+  GUARD(o);
+  check(mog_gemm_f32_sigmoid_philox(a, b, c, bi, M, N, K, lda, ldb, ldc, (float)scale,
+                                    (unsigned long long)seed, (unsigned long long)offset,
+                                    o.stream()),
+        o.name);
 }
 
 void gemm_f32_kseg_(at::TensorList A, at::TensorList B, Tensor C, const optional<Tensor>& bias,
                     const optional<Tensor>& Cin, int64_t M, int64_t N, int64_t kseg, int64_t lda,
                     int64_t ldb, int64_t ldc, bool transA, bool transB, int64_t epi) {
-  auto a = ptrs(A), b = ptrs(B);
-  check(mog_gemm_f32_kseg((int)a.size(), arr<float>(a), arr<float>(b), f(C), f(bias), f(Cin), M, N,
-                          kseg, lda, ldb, ldc, transA, transB, epi, stream()),
-        "gemm_f32_kseg_");
+  Op o("gemm_f32_kseg_");
+  float* c = o.f(C, mat(M, N, ldc), "C");
+  auto a = o.list(A, F32, transA ? mat(kseg, M, lda) : mat(M, kseg, lda), "A");
+  auto b = o.list(B, F32, transB ? mat(N, kseg, ldb) : mat(kseg, N, ldb), "B");
+  TORCH_CHECK(a.size() == b.size(), o.name, ": as many A as B segments");
+  float* bi = o.f(bias, N, "bias");
+  float* ci = o.f(Cin, mat(M, N, ldc), "Cin");
+  GUARD(o);
+  check(mog_gemm_f32_kseg((int)a.size(), arr<float>(a), arr<float>(b), c, bi, ci, M, N, kseg, lda,
+                          ldb, ldc, transA, transB, epi, o.stream()),
+        o.name);
 }
 
 void gemm_bf16_(at::TensorList A, at::TensorList B, at::TensorList C,
@@ -98,72 +170,144 @@ void gemm_bf16_(at::TensorList A, at::TensorList B, at::TensorList C,
                 const c10::List<optional<Tensor>>& aux, const c10::List<optional<Tensor>>& colsum,
                 int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc,
                 int64_t ldaux, bool tn, int64_t epi, double aux_scale, int64_t splitk) {
-  auto a = ptrs(A), b = ptrs(B), c = ptrs(C), bi = ptrs(bias), ci = ptrs(Cin), ax = ptrs(aux),
-       cs = ptrs(colsum);
-  const bool out_bf16 = C.size() > 0 && C[0].scalar_type() == at::kBFloat16;
+  Op o("gemm_bf16_");
+  TORCH_CHECK(C.size() > 0, o.name, ": no output");
+  const bool out_bf16 = C[0].scalar_type() == BF16;
+  auto c = o.list(C, out_bf16 ? BF16 : F32, mat(M, N, ldc), "C");
+  auto a = o.list(A, BF16, tn ? mat(K, M, lda) : mat(M, K, lda), "A");
+  auto b = o.list(B, BF16, tn ? mat(K, N, ldb) : mat(N, K, ldb), "B");
+  auto bi = o.list(bias, F32, N, "bias"), ci = o.list(Cin, F32, mat(M, N, ldc), "Cin");
+  // aux: the noise (epi 2, fp32) or the softplus output (epi 3, bf16)
+  auto ax = o.list(aux, epi == 3 ? BF16 : F32, mat(M, N, ldaux), "aux");
+  auto cs = o.list(colsum, F32, N, "colsum");
+  GUARD(o);
   check(mog_gemm_bf16((int)c.size(), arr<void>(a), arr<void>(b), marr<void>(c), arr<float>(bi),
                       arr<float>(ci), arr<void>(ax), marr<float>(cs), M, N, K, lda, ldb, ldc,
-                      ldaux, tn, epi, out_bf16, (float)aux_scale, splitk, stream()),
-        "gemm_bf16_");
+                      ldaux, tn, epi, out_bf16, (float)aux_scale, splitk, o.stream()),
+        o.name);
 }
 
 void cvt_bf16_batch_(at::TensorList src, at::TensorList dst, at::IntArrayRef dims) {
-  auto s = ptrs(src), d = ptrs(dst);
+  Op o("cvt_bf16_batch_");
+  TORCH_CHECK(dims.size() == 7 * src.size() && src.size() == dst.size(),
+              o.name, ": 7 dims per job");
+  vector<void*> s, d;
   vector<int> di(dims.begin(), dims.end());
-  TORCH_CHECK(di.size() == 7 * s.size() && s.size() == d.size(), "cvt_bf16_batch_: 7 dims per job");
-  check(mog_cvt_bf16_batch((int)s.size(), arr<float>(s), marr<void>(d), di.data(), stream()),
-        "cvt_bf16_batch_");
+  for (size_t j = 0; j < src.size(); ++j) {
+    const int* q = &di[7 * j];  // src_rows, src_cols, ld_src, rows, cols, ld_dst, transpose
+    s.push_back(o.need(src[j], F32, mat(q[0], q[1], q[2]), "src"));
+    d.push_back(o.need(dst[j], BF16, q[6] == 2 ? (int64_t)q[3] * q[4] : mat(q[3], q[4], q[5]),
+                       "dst"));
+  }
+  GUARD(o);
+  check(mog_cvt_bf16_batch((int)s.size(), arr<float>(s), marr<void>(d), di.data(), o.stream()),
+        o.name);
 }
 
 // ------------------------------------------------------------------ STN ----
 void stn_forward_(const Tensor& U, int64_t N, int64_t Hin, int64_t Win, const Tensor& theta,
                   int64_t Hout, int64_t Wout, Tensor out, const optional<Tensor>& z,
                   const optional<Tensor>& mask, int64_t mode) {
-  check(mog_stn_forward(f(U), N, Hin, Win, f(theta), Hout, Wout, p(out), f(z), f(mask), mode,
-                        stream()),
-        "stn_forward_");
+  Op o("stn_forward_");
+  void* po = o.need(out, mode == 2 ? BF16 : F32, N * Hout * Wout, "out");
+  float* pu = o.f(U, N * Hin * Win, "U");
+  float* pt = o.f(theta, N * 6, "theta");
+  float* pz = o.f(z, N, "z");
+  float* pm = o.f(mask, N, "mask");
+  GUARD(o);
+  check(mog_stn_forward(pu, N, Hin, Win, pt, Hout, Wout, po, pz, pm, mode, o.stream()), o.name);
 }
 
 void stn_backward_(const Tensor& U, int64_t N, int64_t Hin, int64_t Win, const Tensor& theta,
                    int64_t Hout, int64_t Wout, const Tensor& G, const optional<Tensor>& gscale,
                    const optional<Tensor>& dU, const optional<Tensor>& dtheta,
                    const optional<Tensor>& dot, int64_t u_period, int64_t g_period) {
-  check(mog_stn_backward(f(U), N, Hin, Win, f(theta), Hout, Wout, f(G), f(gscale), f(dU),
-                         f(dtheta), f(dot), u_period, g_period, stream()),
-        "stn_backward_");
+  Op o("stn_backward_");
+  float* pu = o.f(U, (u_period > 0 ? u_period : N) * Hin * Win, "U");
+  float* pt = o.f(theta, N * 6, "theta");
+  float* pg = o.f(G, (g_period > 0 ? g_period : N) * Hout * Wout, "G");
+  float* ps = o.f(gscale, N, "gscale");
+  float* pdu = o.f(dU, N * Hin * Win, "dU");
+  float* pdt = o.f(dtheta, N * 6, "dtheta");
+  float* pd = o.f(dot, N, "dot");
+  GUARD(o);
+  check(mog_stn_backward(pu, N, Hin, Win, pt, Hout, Wout, pg, ps, pdu, pdt, pd, u_period,
+                         g_period, o.stream()),
+        o.name);
 }
 
 void stn_backward_sigmoid_(const Tensor& U, int64_t N, int64_t Hin, int64_t Win,
-                                const Tensor& theta, int64_t Hout, int64_t Wout, const Tensor& G,
-                                const optional<Tensor>& gscale, Tensor dm,
-                                const optional<Tensor>& dtheta, const optional<Tensor>& dot,
-                                int64_t g_period) {
+                           const Tensor& theta, int64_t Hout, int64_t Wout, const Tensor& G,
+                           const optional<Tensor>& gscale, Tensor dm,
+                           const optional<Tensor>& dtheta, const optional<Tensor>& dot,
+                           int64_t g_period) {
   // dm bf16 (configs[1]) or fp32 (reference precision)
-  if (dm.scalar_type() == at::kBFloat16)
-    check(mog_stn_backward_sigmoid_bf16(f(U), N, Hin, Win, f(theta), Hout, Wout, f(G), f(gscale),
-                                        p(dm), f(dtheta), f(dot), 0, g_period, stream()),
-          "stn_backward_sigmoid_");
+  Op o("stn_backward_sigmoid_");
+  const bool bf = dm.scalar_type() == BF16;
+  void* pdm = o.need(dm, bf ? BF16 : F32, N * Hin * Win, "dm");
+  float* pu = o.f(U, N * Hin * Win, "U");
+  float* pt = o.f(theta, N * 6, "theta");
+  float* pg = o.f(G, (g_period > 0 ? g_period : N) * Hout * Wout, "G");
+  float* ps = o.f(gscale, N, "gscale");
+  float* pdt = o.f(dtheta, N * 6, "dtheta");
+  float* pd = o.f(dot, N, "dot");
+  GUARD(o);
+  if (bf)
+    check(mog_stn_backward_sigmoid_bf16(pu, N, Hin, Win, pt, Hout, Wout, pg, ps, pdm, pdt, pd, 0,
+                                        g_period, o.stream()),
+          o.name);
   else
-    check(mog_stn_backward_sigmoid_f32(f(U), N, Hin, Win, f(theta), Hout, Wout, f(G), f(gscale),
-                                       f(dm), f(dtheta), f(dot), 0, g_period, stream()),
-          "stn_backward_sigmoid_");
+    check(mog_stn_backward_sigmoid_f32(pu, N, Hin, Win, pt, Hout, Wout, pg, ps,
+                                       static_cast<float*>(pdm), pdt, pd, 0, g_period,
+                                       o.stream()),
+          o.name);
+}
+
+void stn_write_parts_(const Tensor& U, int64_t N, int64_t Hin, int64_t Win, const Tensor& theta,
+                      int64_t Hout, int64_t Wout, const Tensor& z, const Tensor& mask, Tensor parts,
+                      Tensor part_rows) {
+  Op o("stn_write_parts_");
+  float* pp = o.f(parts, N * Hout * Wout, "parts");
+  int* pr = o.i(part_rows, N, "part_rows");
+  float* pu = o.f(U, N * Hin * Win, "U");
+  float* pt = o.f(theta, N * 6, "theta");
+  float* pz = o.f(z, N, "z");
+  float* pm = o.f(mask, N, "mask");
+  GUARD(o);
+  check(mog_stn_write_parts(pu, N, Hin, Win, pt, Hout, Wout, pz, pm, pp, pr, o.stream()), o.name);
 }
 
 // ----------------------------------------------------------------- LSTM ----
 void lstm_cell_forward_(const Tensor& G, const optional<Tensor>& bias,
                         const optional<Tensor>& c_prev, Tensor c_out, Tensor h_out, int64_t B,
                         int64_t H) {
-  check(mog_lstm_cell_forward(f(G), f(bias), f(c_prev), f(c_out), f(h_out), B, H, stream()),
-        "lstm_cell_forward_");
+  Op o("lstm_cell_forward_");
+  float* pc = o.f(c_out, B * H, "c_out");
+  float* ph = o.f(h_out, B * H, "h_out");
+  float* pg = o.f(G, B * 4 * H, "G");
+  float* pb = o.f(bias, 4 * H, "bias");
+  float* pp = o.f(c_prev, B * H, "c_prev");
+  GUARD(o);
+  check(mog_lstm_cell_forward(pg, pb, pp, pc, ph, B, H, o.stream()), o.name);
 }
 
 void lstm_cell_backward_(const Tensor& G, const optional<Tensor>& bias,
                          const optional<Tensor>& c_prev, const Tensor& c_cur, const Tensor& dh,
                          const optional<Tensor>& dc, Tensor dG, Tensor dc_prev,
                          const optional<Tensor>& dGsum, int64_t B, int64_t H) {
-  check(mog_lstm_cell_backward(f(G), f(bias), f(c_prev), f(c_cur), f(dh), f(dc), f(dG),
-                               f(dc_prev), f(dGsum), B, H, stream()),
-        "lstm_cell_backward_");
+  Op o("lstm_cell_backward_");
+  float* pdg = o.f(dG, B * 4 * H, "dG");
+  float* pdcp = o.f(dc_prev, B * H, "dc_prev");
+  float* pg = o.f(G, B * 4 * H, "G");
+  float* pb = o.f(bias, 4 * H, "bias");
+  float* pcp = o.f(c_prev, B * H, "c_prev");
+  float* pcc = o.f(c_cur, B * H, "c_cur");
+  float* pdh = o.f(dh, B * H, "dh");
+  float* pdc = o.f(dc, B * H, "dc");
+  float* pgs = o.f(dGsum, B * 4 * H, "dGsum");
+  GUARD(o);
+  check(mog_lstm_cell_backward(pg, pb, pcp, pcc, pdh, pdc, pdg, pdcp, pgs, B, H, o.stream()),
+        o.name);
 }
 
 // ------------------------------------------------ heads / concrete / masks ----
@@ -176,41 +320,81 @@ void air_step_forward_(int64_t B, int64_t HS, int64_t HZ, int64_t step, bool tra
                        Tensor rec, Tensor theta_fwd, Tensor theta_back, Tensor scale, Tensor shift,
                        Tensor zprob, Tensor zkl, Tensor skl, Tensor shkl, Tensor zmask, Tensor zval,
                        Tensor zc) {
-  auto h = ptrs(hid), w = ptrs(w2), b = ptrs(b2);
-  TORCH_CHECK(h.size() == 5 && w.size() == 5 && b.size() == 5, "air_step_forward_: 5 heads");
+  Op o("air_step_forward_");
+  TORCH_CHECK(hid.size() == 5 && w2.size() == 5 && b2.size() == 5, o.name, ": 5 heads");
+  float* pst = o.f(stop, B, "stop");
+  auto h = o.list(hid, F32, B * HS, "hid"), w = o.list(w2, F32, HS, "w2"),
+       b = o.list(b2, F32, 1, "b2");
+  float* pes = o.f(eps_scale, B, "eps_scale");
+  float* peh = o.f(eps_shift, 2 * B, "eps_shift");
+  float* pu = o.f(u, B, "u");
+  float* prl = o.f(runloss, B, "runloss");
+  int* pd = o.i(digits, B, "digits");
+  int* pl = o.i(live, step + 2, "live");
+  float* pr = o.f(rec, 17 * B, "rec");
+  float* ptf = o.f(theta_fwd, 6 * B, "theta_fwd");
+  float* ptb = o.f(theta_back, 6 * B, "theta_back");
+  float* psc = o.f(scale, B, "scale");
+  float* psh = o.f(shift, 2 * B, "shift");
+  float* pzp = o.f(zprob, B, "zprob");
+  float* pzk = o.f(zkl, B, "zkl");
+  float* psk = o.f(skl, B, "skl");
+  float* phk = o.f(shkl, B, "shkl");
+  float* pzm = o.f(zmask, B, "zmask");
+  float* pzv = o.f(zval, B, "zval");
+  float* pzc = o.f(zc, B, "zc");
+  GUARD(o);
   check(mog_air_step_forward(B, HS, HZ, step, train, use_num_prior, thr, temperature, prior_lo,
                              prior_bias, s_pm, s_pv, s_plv, h_pm, h_pv, h_plv, arr<float>(h),
-                             arr<float>(w), arr<float>(b), f(eps_scale), f(eps_shift), f(u),
-                             f(stop), f(runloss), static_cast<int*>(p(digits)),
-                             static_cast<int*>(p(live)), f(rec), f(theta_fwd), f(theta_back),
-                             f(scale), f(shift), f(zprob), f(zkl), f(skl), f(shkl), f(zmask),
-                             f(zval), f(zc), stream()),
-        "air_step_forward_");
+                             arr<float>(w), arr<float>(b), pes, peh, pu, pst, prl, pd, pl, pr, ptf,
+                             ptb, psc, psh, pzp, pzk, psk, phk, pzm, pzv, pzc, o.stream()),
+        o.name);
 }
 
 void air_step_backward_(int64_t B, int64_t HS, bool train, bool use_num_prior,
                         double temperature, double prior_lo, double prior_bias, double s_pm,
                         double s_pv, double h_pm, double h_pv, double grad_scale,
-                        const optional<Tensor>& dloss, const Tensor& rec, const Tensor& eps_scale, const Tensor& eps_shift,
-                        const Tensor& dtheta_fwd, const Tensor& dtheta_back, const Tensor& dot,
-                        at::TensorList hid, at::TensorList w2, Tensor dout, int64_t dout_hs,
-                        Tensor dhid, int64_t dhid_hs) {
-  auto h = ptrs(hid), w = ptrs(w2);
-  TORCH_CHECK(h.size() == 5 && w.size() == 5, "air_step_backward_: 5 heads");
+                        const optional<Tensor>& dloss, const Tensor& rec, const Tensor& eps_scale,
+                        const Tensor& eps_shift, const Tensor& dtheta_fwd,
+                        const Tensor& dtheta_back, const Tensor& dot, at::TensorList hid,
+                        at::TensorList w2, Tensor dout, int64_t dout_hs, Tensor dhid,
+                        int64_t dhid_hs) {
+  Op o("air_step_backward_");
+  TORCH_CHECK(hid.size() == 5 && w2.size() == 5, o.name, ": 5 heads");
+  float* pdo = o.f(dout, 4 * dout_hs + 2 * B, "dout");
+  float* pdh = o.f(dhid, dhid_hs == HS ? 5 * B * HS : 4 * dhid_hs + B * HS, "dhid");
+  auto h = o.list(hid, F32, B * HS, "hid"), w = o.list(w2, F32, HS, "w2");
+  float* pl = o.f(dloss, B, "dloss");
+  float* pr = o.f(rec, 17 * B, "rec");
+  float* pes = o.f(eps_scale, B, "eps_scale");
+  float* peh = o.f(eps_shift, 2 * B, "eps_shift");
+  float* ptf = o.f(dtheta_fwd, 6 * B, "dtheta_fwd");
+  float* ptb = o.f(dtheta_back, 6 * B, "dtheta_back");
+  float* pd = o.f(dot, B, "dot");
+  GUARD(o);
   check(mog_air_step_backward(B, HS, train, use_num_prior, temperature, prior_lo, prior_bias, s_pm,
-                              s_pv, h_pm, h_pv, grad_scale, f(dloss), f(rec),
-                              f(eps_scale), f(eps_shift),
-                              f(dtheta_fwd), f(dtheta_back), f(dot), arr<float>(h), arr<float>(w),
-                              f(dout), dout_hs, f(dhid), dhid_hs, stream()),
-        "air_step_backward_");
+                              s_pv, h_pm, h_pv, grad_scale, pl, pr, pes, peh, ptf, ptb, pd,
+                              arr<float>(h), arr<float>(w), pdo, dout_hs, pdh, dhid_hs,
+                              o.stream()),
+        o.name);
 }
 
-void stn_write_parts_(const Tensor& U, int64_t N, int64_t Hin, int64_t Win, const Tensor& theta,
-                      int64_t Hout, int64_t Wout, const Tensor& z, const Tensor& mask, Tensor parts,
-                      Tensor part_rows) {
-  check(mog_stn_write_parts(f(U), N, Hin, Win, f(theta), Hout, Wout, f(z), f(mask), f(parts),
-                            static_cast<int*>(p(part_rows)), stream()),
-        "stn_write_parts_");
+void generation_prior_(int64_t G, int64_t Z, double s_pm, double s_plv, double h_pm,
+                       double h_plv, double v_pm, double v_plv, const Tensor& eps_scale,
+                       const Tensor& eps_shift, const Tensor& eps_z, Tensor theta_back,
+                       Tensor scale, Tensor shift, Tensor z) {
+  Op o("generation_prior_");
+  float* ptb = o.f(theta_back, 6 * G, "theta_back");
+  float* psc = o.f(scale, G, "scale");
+  float* psh = o.f(shift, 2 * G, "shift");
+  float* pz = o.f(z, G * Z, "z");
+  float* pes = o.f(eps_scale, G, "eps_scale");
+  float* peh = o.f(eps_shift, 2 * G, "eps_shift");
+  float* pez = o.f(eps_z, G * Z, "eps_z");
+  GUARD(o);
+  check(mog_generation_prior(G, Z, s_pm, s_plv, h_pm, h_plv, v_pm, v_plv, pes, peh, pez, ptb, psc,
+                             psh, pz, o.stream()),
+        o.name);
 }
 
 // ------------------------------------------------------------ glimpse VAE ----
@@ -218,16 +402,31 @@ void vae_sample_forward_(int64_t B, int64_t Z, double v_pm, double v_pv, double 
                          const Tensor& mu, const Tensor& lv, const Tensor& eps, Tensor z,
                          const optional<Tensor>& z_bf16, int64_t ld_zb, const Tensor& act,
                          const optional<Tensor>& runloss, Tensor vkl) {
-  check(mog_vae_sample_forward(B, Z, v_pm, v_pv, v_plv, f(mu), f(lv), f(eps), f(z), p(z_bf16),
-                               ld_zb, f(act), f(runloss), f(vkl), stream()),
-        "vae_sample_forward_");
+  Op o("vae_sample_forward_");
+  float* pz = o.f(z, B * Z, "z");
+  void* pzb = o.need(z_bf16, BF16, mat(B, Z, ld_zb), "z_bf16");
+  float* pm = o.f(mu, B * Z, "mu");
+  float* pl = o.f(lv, B * Z, "lv");
+  float* pe = o.f(eps, B * Z, "eps");
+  float* pa = o.f(act, B, "act");
+  float* prl = o.f(runloss, B, "runloss");
+  float* pk = o.f(vkl, B, "vkl");
+  GUARD(o);
+  check(mog_vae_sample_forward(B, Z, v_pm, v_pv, v_plv, pm, pl, pe, pz, pzb, ld_zb, pa, prl, pk,
+                               o.stream()),
+        o.name);
 }
 
 void air_runloss_(int64_t T, int64_t B, const Tensor& rec, int64_t rec_step_stride,
                   const Tensor& skl, const Tensor& shkl, const Tensor& vkl, Tensor runloss) {
-  check(mog_air_runloss(T, B, f(rec), rec_step_stride, f(skl), f(shkl), f(vkl), f(runloss),
-                        stream()),
-        "air_runloss_");
+  Op o("air_runloss_");
+  float* prl = o.f(runloss, B, "runloss");
+  float* pr = o.f(rec, (T - 1) * rec_step_stride + 17 * B, "rec");
+  float* ps = o.f(skl, T * B, "skl");
+  float* ph = o.f(shkl, T * B, "shkl");
+  float* pv = o.f(vkl, T * B, "vkl");
+  GUARD(o);
+  check(mog_air_runloss(T, B, pr, rec_step_stride, ps, ph, pv, prl, o.stream()), o.name);
 }
 
 void vae_sample_backward_(int64_t B, int64_t Z, double v_pm, double v_pv, double grad_scale,
@@ -235,14 +434,30 @@ void vae_sample_backward_(int64_t B, int64_t Z, double v_pm, double v_pv, double
                           const Tensor& act, const optional<Tensor>& dmu,
                           const optional<Tensor>& dlv, const optional<Tensor>& dmu_bf16,
                           const optional<Tensor>& dlv_bf16, int64_t ld_b) {
-  check(mog_vae_sample_backward(B, Z, v_pm, v_pv, grad_scale, f(mu), f(lv), f(eps), f(dz), f(act),
-                                f(dmu), f(dlv), p(dmu_bf16), p(dlv_bf16), ld_b, stream()),
-        "vae_sample_backward_");
+  Op o("vae_sample_backward_");
+  float* pm = o.f(mu, B * Z, "mu");
+  float* pl = o.f(lv, B * Z, "lv");
+  float* pe = o.f(eps, B * Z, "eps");
+  float* pdz = o.f(dz, B * Z, "dz");
+  float* pa = o.f(act, B, "act");
+  float* pdm = o.f(dmu, B * Z, "dmu");
+  float* pdl = o.f(dlv, B * Z, "dlv");
+  void* pdmb = o.need(dmu_bf16, BF16, mat(B, Z, ld_b), "dmu_bf16");
+  void* pdlb = o.need(dlv_bf16, BF16, mat(B, Z, ld_b), "dlv_bf16");
+  GUARD(o);
+  check(mog_vae_sample_backward(B, Z, v_pm, v_pv, grad_scale, pm, pl, pe, pdz, pa, pdm, pdl, pdmb,
+                                pdlb, ld_b, o.stream()),
+        o.name);
 }
 
 void sigmoid_backward_(const Tensor& r, const Tensor& dr, Tensor dm, int64_t n) {
-  check(mog_sigmoid_backward(f(r), f(dr), p(dm), n, dm.scalar_type() == at::kBFloat16, stream()),
-        "sigmoid_backward_");
+  Op o("sigmoid_backward_");
+  const bool bf = dm.scalar_type() == BF16;
+  void* pdm = o.need(dm, bf ? BF16 : F32, n, "dm");
+  float* pr = o.f(r, n, "r");
+  float* pdr = o.f(dr, n, "dr");
+  GUARD(o);
+  check(mog_sigmoid_backward(pr, pdr, pdm, n, bf, o.stream()), o.name);
 }
 
 void stn_vae_step_(int64_t B, int64_t C, const Tensor& x, const Tensor& theta_f,
@@ -256,16 +471,46 @@ void stn_vae_step_(int64_t B, int64_t C, const Tensor& x, const Tensor& theta_f,
                    const optional<Tensor>& lv, const optional<Tensor>& z,
                    const optional<Tensor>& zb, const optional<Tensor>& d1b,
                    const optional<Tensor>& d2b, Tensor r, int64_t x_period) {
-  auto w = ptrs(wt), b = ptrs(bias);
-  TORCH_CHECK(w.size() == 7 && b.size() == 7, "stn_vae_step_: 7 VAE layers");
-  check(mog_stn_vae_step_forward(B, C, 28, 512, 256, 50, 256, 512, f(x), f(theta_f), f(theta_b),
-                                 f(mask), f(zval), f(eps_z), f(eps_x), eps_gen,
-                                 (unsigned long long)eps_seed, (unsigned long long)eps_offset,
-                                 arr<void>(w), arr<float>(b), lik_std, v_pm, v_pv, v_plv,
-                                 f(canvas_part), static_cast<int*>(p(part_rows)), f(runloss),
-                                 f(vkl), p(gb), p(a1b), p(a2b), f(mu), f(lv), f(z), p(zb), p(d1b),
-                                 p(d2b), f(r), x_period, stream()),
-        "stn_vae_step_");
+  Op o("stn_vae_step_");
+  TORCH_CHECK(wt.size() == 7 && bias.size() == 7, o.name, ": 7 VAE layers");
+  const int64_t C2 = C * C;
+  float* pr = o.f(r, B * 784, "r");
+  // bf16 W^T packs in MFMA B-fragment order: [out padded to 16][in padded to 32]
+  static const int64_t pack[7] = {512 * 800, 256 * 512, 64 * 256, 64 * 256, 256 * 64, 512 * 256,
+                                  784 * 512};
+  static const int64_t nb[7] = {512, 256, 50, 50, 256, 512, 784};
+  vector<void*> w, b;
+  for (int k = 0; k < 7; ++k) {
+    w.push_back(o.need(wt[k], BF16, pack[k], "wt"));
+    b.push_back(o.need(bias[k], F32, nb[k], "bias"));
+  }
+  float* px = o.f(x, (x_period > 0 ? x_period : B) * C2, "x");
+  float* ptf = o.f(theta_f, 6 * B, "theta_f");
+  float* ptb = o.f(theta_b, 6 * B, "theta_b");
+  float* pm = o.f(mask, B, "mask");
+  float* pzv = o.f(zval, B, "zval");
+  float* pez = o.f(eps_z, 50 * B, "eps_z");
+  float* pex = o.f(eps_x, 784 * B, "eps_x");
+  float* pcp = o.f(canvas_part, B * C2, "canvas_part");
+  int* prw = o.i(part_rows, B, "part_rows");
+  float* prl = o.f(runloss, B, "runloss");
+  float* pk = o.f(vkl, B, "vkl");
+  void* pgb = o.need(gb, BF16, B * 784, "gb");
+  void* pa1 = o.need(a1b, BF16, B * 512, "a1b");
+  void* pa2 = o.need(a2b, BF16, B * 256, "a2b");
+  float* pmu = o.f(mu, B * 50, "mu");
+  float* plv = o.f(lv, B * 50, "lv");
+  float* pz = o.f(z, B * 50, "z");
+  void* pzb = o.need(zb, BF16, B * 56, "zb");
+  void* pd1 = o.need(d1b, BF16, B * 256, "d1b");
+  void* pd2 = o.need(d2b, BF16, B * 512, "d2b");
+  GUARD(o);
+  check(mog_stn_vae_step_forward(B, C, 28, 512, 256, 50, 256, 512, px, ptf, ptb, pm, pzv, pez,
+                                 pex, eps_gen, (unsigned long long)eps_seed,
+                                 (unsigned long long)eps_offset, arr<void>(w), arr<float>(b),
+                                 lik_std, v_pm, v_pv, v_plv, pcp, prw, prl, pk, pgb, pa1, pa2, pmu,
+                                 plv, pz, pzb, pd1, pd2, pr, x_period, o.stream()),
+        o.name);
 }
 
 // ------------------------------------------------- loss / optimizer / RNG ----
@@ -275,38 +520,236 @@ void recon_loss_(const Tensor& x, const optional<Tensor>& canvas, const optional
                  int64_t B, int64_t C2, double grad_scale, const optional<Tensor>& recon,
                  Tensor bce, Tensor mse, Tensor loss, const optional<Tensor>& acc,
                  const optional<Tensor>& dcanvas) {
-  check(mog_recon_loss(f(x), f(canvas), f(parts), nparts, part_stride,
-                       static_cast<const int*>(p(part_rows)), C, f(runloss),
-                       static_cast<const int*>(p(digits)), static_cast<const int*>(p(targets)), B,
-                       C2, grad_scale, f(recon), f(bce), f(mse), f(loss), f(acc), f(dcanvas),
-                       stream()),
-        "recon_loss_");
+  Op o("recon_loss_");
+  float* pl = o.f(loss, B, "loss");
+  float* px = o.f(x, B * C2, "x");
+  float* pc = o.f(canvas, B * C2, "canvas");
+  float* pp = o.f(parts, nparts > 0 ? (nparts - 1) * part_stride + B * C2 : 0, "parts");
+  const int* prw = o.i(part_rows, nparts * B, "part_rows");
+  float* prl = o.f(runloss, B, "runloss");
+  const int* pd = o.i(digits, B, "digits");
+  const int* pt = o.i(targets, B, "targets");
+  float* prc = o.f(recon, B * C2, "recon");
+  float* pb = o.f(bce, B, "bce");
+  float* pms = o.f(mse, B, "mse");
+  float* pa = o.f(acc, B, "acc");
+  float* pdc = o.f(dcanvas, B * C2, "dcanvas");
+  GUARD(o);
+  check(mog_recon_loss(px, pc, pp, nparts, part_stride, prw, C, prl, pd, pt, B, C2, grad_scale,
+                       prc, pb, pms, pl, pa, pdc, o.stream()),
+        o.name);
 }
 
 void batch_mean_(const optional<Tensor>& a0, const optional<Tensor>& a1,
                  const optional<Tensor>& a2, const optional<Tensor>& a3, int64_t B, Tensor out) {
-  check(mog_batch_mean(f(a0), f(a1), f(a2), f(a3), B, f(out), stream()), "batch_mean_");
+  Op o("batch_mean_");
+  float* po = o.f(out, 4, "out");
+  float* p0 = o.f(a0, B, "a0");
+  float* p1 = o.f(a1, B, "a1");
+  float* p2 = o.f(a2, B, "a2");
+  float* p3 = o.f(a3, B, "a3");
+  GUARD(o);
+  check(mog_batch_mean(p0, p1, p2, p3, B, po, o.stream()), o.name);
 }
 
 void clip_adam_(Tensor params, Tensor grads, Tensor m, Tensor v, const Tensor& off,
                 const Tensor& len, const Tensor& block_tensor, const Tensor& block_start,
                 int64_t nblocks, const optional<Tensor>& sumsq, double clip, double lr_t,
                 double beta1, double beta2, double eps) {
-  check(mog_clip_adam(f(params), f(grads), f(m), f(v), static_cast<const long*>(p(off)),
-                      static_cast<const long*>(p(len)), static_cast<const int*>(p(block_tensor)),
-                      static_cast<const long*>(p(block_start)), nblocks, f(sumsq), clip, lr_t,
-                      beta1, beta2, eps, stream()),
-        "clip_adam_");
+  // the tensor table lives on the device (off / len / block arrays); the flat
+  // buffers must hold the same number of elements
+  Op o("clip_adam_");
+  const int64_t n = params.numel();
+  float* pp = o.f(params, n, "params");
+  float* pg = o.f(grads, n, "grads");
+  float* pm = o.f(m, n, "m");
+  float* pv = o.f(v, n, "v");
+  TORCH_CHECK(grads.numel() == n && m.numel() == n && v.numel() == n, o.name,
+              ": params / grads / m / v differ in size");
+  auto* poff = static_cast<const long*>(o.need(off, at::kLong, 0, "off"));
+  auto* plen = static_cast<const long*>(o.need(len, at::kLong, 0, "len"));
+  const int* pbt = o.i(block_tensor, nblocks, "block_tensor");
+  auto* pbs = static_cast<const long*>(o.need(block_start, at::kLong, nblocks, "block_start"));
+  float* ps = o.f(sumsq, off.numel(), "sumsq");
+  GUARD(o);
+  check(mog_clip_adam(pp, pg, pm, pv, poff, plen, pbt, pbs, nblocks, ps, clip, lr_t, beta1, beta2,
+                      eps, o.stream()),
+        o.name);
 }
 
 void add_(const Tensor& a, const Tensor& b, Tensor out, int64_t n) {
-  check(mog_add(f(a), f(b), f(out), n, stream()), "add_");
+  Op o("add_");
+  float* po = o.f(out, n, "out");
+  float* pa = o.f(a, n, "a");
+  float* pb = o.f(b, n, "b");
+  GUARD(o);
+  check(mog_add(pa, pb, po, n, o.stream()), o.name);
 }
 
 void rng_fill_(Tensor out, int64_t seed, int64_t offset, bool normal) {
-  check(mog_rng_fill(f(out), out.numel(), (unsigned long long)seed, (unsigned long long)offset,
-                     normal, stream()),
-        "rng_fill_");
+  Op o("rng_fill_");
+  float* po = o.f(out, out.numel(), "out");
+  GUARD(o);
+  check(mog_rng_fill(po, out.numel(), (unsigned long long)seed, (unsigned long long)offset, normal,
+                     o.stream()),
+        o.name);
+}
+
+// ---------------------------------------------- AIR-ASR cells and losses ----
+// (air/air_number_bbox_location.py; records [T][28][B], asr_cell.hip)
+constexpr int64_t ASR_NQ = 28, ASR_DN = 12;
+
+void asr_pack_(int64_t B, int64_t Z, int64_t H, int64_t ld, const optional<Tensor>& z,
+               const optional<Tensor>& ss, const optional<Tensor>& h, Tensor out) {
+  Op o("asr_pack_");
+  float* po = o.f(out, B * ld, "out");
+  float* pz = o.f(z, B * Z, "z");
+  float* ps = o.f(ss, B * 3, "ss");
+  float* ph = o.f(h, B * H, "h");
+  GUARD(o);
+  check(mog_asr_pack(B, Z, H, ld, pz, ps, ph, po, o.stream()), o.name);
+}
+
+void asr_unpack_(int64_t B, int64_t Z, int64_t H, int64_t ld, const Tensor& dU, const Tensor& dUg,
+                 Tensor dz, Tensor dss, Tensor dh, Tensor dhg) {
+  Op o("asr_unpack_");
+  float* pdz = o.f(dz, B * Z, "dz");
+  float* pds = o.f(dss, B * 3, "dss");
+  float* pdh = o.f(dh, B * H, "dh");
+  float* pdg = o.f(dhg, B * H, "dhg");
+  float* pu = o.f(dU, B * ld, "dU");
+  float* pug = o.f(dUg, B * ld, "dUg");
+  GUARD(o);
+  check(mog_asr_unpack(B, Z, H, ld, pu, pug, pdz, pds, pdh, pdg, o.stream()), o.name);
+}
+
+void asr_step_forward_(int64_t B, int64_t step, bool train, int64_t fix_steps, double thr,
+                       double temperature, double s_pm, double s_pv, double s_plv,
+                       double gamma_num, at::TensorList w, const c10::List<optional<Tensor>>& hid,
+                       const Tensor& eps_shift, const Tensor& eps_scale, const Tensor& u,
+                       Tensor stop, Tensor digits, Tensor live, Tensor rec, Tensor theta_fwd,
+                       Tensor theta_back, Tensor ss, Tensor scale, Tensor shift, Tensor zprob,
+                       Tensor zmask, Tensor zval, Tensor zc) {
+  Op o("asr_step_forward_");
+  TORCH_CHECK(w.size() == 20 && hid.size() == 8, o.name, ": 10 output layers, 8 hidden layers");
+  float* pst = o.f(stop, B, "stop");
+  auto pw = o.list(w, F32, 1, "w");
+  auto ph = o.list(hid, F32, B * 64, "hid");
+  float* peh = o.f(eps_shift, 2 * B, "eps_shift");
+  float* pes = o.f(eps_scale, B, "eps_scale");
+  float* pu = o.f(u, B, "u");
+  int* pd = o.i(digits, B, "digits");
+  int* pl = o.i(live, step + 2, "live");
+  float* pr = o.f(rec, ASR_NQ * B, "rec");
+  float* ptf = o.f(theta_fwd, 6 * B, "theta_fwd");
+  float* ptb = o.f(theta_back, 6 * B, "theta_back");
+  float* pss = o.f(ss, 3 * B, "ss");
+  float* psc = o.f(scale, B, "scale");
+  float* psh = o.f(shift, 2 * B, "shift");
+  float* pzp = o.f(zprob, B, "zprob");
+  float* pzm = o.f(zmask, B, "zmask");
+  float* pzv = o.f(zval, B, "zval");
+  float* pzc = o.f(zc, B, "zc");
+  GUARD(o);
+  check(mog_asr_step_forward(B, step, train, fix_steps, thr, temperature, s_pm, s_pv, s_plv,
+                             gamma_num, arr<float>(pw), marr<float>(ph), peh, pes, pu, pst, pd, pl,
+                             pr, ptf, ptb, pss, psc, psh, pzp, pzm, pzv, pzc, o.stream()),
+        o.name);
+}
+
+void asr_terms_(int64_t B, int64_t T, int64_t C, at::IntArrayRef cons, at::ArrayRef<double> gammas,
+                const Tensor& rec, const Tensor& vkl, const Tensor& zmask, const Tensor& live,
+                Tensor klsum, Tensor pr, Tensor area, Tensor out, Tensor size, Tensor overlap,
+                Tensor zsum) {
+  Op o("asr_terms_");
+  TORCH_CHECK(gammas.size() == 8 && !cons.empty() && cons.size() <= 8, o.name,
+              ": 8 gammas, 1..8 counts");
+  vector<int> c(cons.begin(), cons.end());
+  vector<float> g(gammas.begin(), gammas.end());
+  float* pk = o.f(klsum, B, "klsum");
+  float* pp = o.f(pr, B, "pr");
+  float* pa = o.f(area, B, "area");
+  float* pout = o.f(out, B, "out");
+  float* psz = o.f(size, B, "size");
+  float* pov = o.f(overlap, B, "overlap");
+  float* pzs = o.f(zsum, T, "zsum");
+  float* prec = o.f(rec, T * ASR_NQ * B, "rec");
+  float* pv = o.f(vkl, T * B, "vkl");
+  float* pzm = o.f(zmask, T * B, "zmask");
+  const int* pl = o.i(live, T + 1, "live");
+  GUARD(o);
+  check(mog_asr_terms(B, T, C, (int)c.size(), c.data(), g.data(), prec, pv, pzm, pl, pk, pp, pa,
+                      pout, psz, pov, pzs, o.stream()),
+        o.name);
+}
+
+void asr_finalize_(int64_t B, int64_t T, int64_t C, at::IntArrayRef cons,
+                   at::ArrayRef<double> gammas, double inv_batch_global, const Tensor& rec,
+                   const Tensor& live, const Tensor& zsum, const Tensor& pr, Tensor loss,
+                   Tensor element, Tensor margin) {
+  Op o("asr_finalize_");
+  TORCH_CHECK(gammas.size() == 8 && !cons.empty() && cons.size() <= 8, o.name,
+              ": 8 gammas, 1..8 counts");
+  vector<int> c(cons.begin(), cons.end());
+  vector<float> g(gammas.begin(), gammas.end());
+  float* pl = o.f(loss, B, "loss");
+  float* pe = o.f(element, B, "element");
+  float* pm = o.f(margin, 1, "margin");
+  float* prec = o.f(rec, T * ASR_NQ * B, "rec");
+  const int* plv = o.i(live, T + 1, "live");
+  float* pzs = o.f(zsum, T, "zsum");
+  float* pp = o.f(pr, B, "pr");
+  GUARD(o);
+  check(mog_asr_finalize(B, T, C, (int)c.size(), c.data(), g.data(), inv_batch_global, prec, plv,
+                         pzs, pp, pl, pe, pm, o.stream()),
+        o.name);
+}
+
+void asr_terms_backward_(int64_t B, int64_t T, int64_t C, at::IntArrayRef cons,
+                         at::ArrayRef<double> gammas, double grad_scale, double inv_batch_global,
+                         const Tensor& rec, const Tensor& live, const Tensor& zsum, Tensor dreg) {
+  Op o("asr_terms_backward_");
+  TORCH_CHECK(gammas.size() == 8 && !cons.empty() && cons.size() <= 8, o.name,
+              ": 8 gammas, 1..8 counts");
+  vector<int> c(cons.begin(), cons.end());
+  vector<float> g(gammas.begin(), gammas.end());
+  float* pd = o.f(dreg, T * 4 * B, "dreg");
+  float* prec = o.f(rec, T * ASR_NQ * B, "rec");
+  const int* pl = o.i(live, T + 1, "live");
+  float* pzs = o.f(zsum, T, "zsum");
+  GUARD(o);
+  check(mog_asr_terms_backward(B, T, C, (int)c.size(), c.data(), g.data(), grad_scale,
+                               inv_batch_global, prec, pl, pzs, pd, o.stream()),
+        o.name);
+}
+
+void asr_step_backward_(int64_t B, bool train, int64_t fix_steps, double temperature,
+                        double s_pm, double s_pv, double grad_scale, at::TensorList w,
+                        const c10::List<optional<Tensor>>& hid, const Tensor& rec,
+                        const Tensor& eps_shift, const Tensor& eps_scale,
+                        const Tensor& dtheta_fwd, const Tensor& dtheta_back, const Tensor& dot,
+                        const Tensor& dreg, const optional<Tensor>& dss, Tensor douts,
+                        const c10::List<optional<Tensor>>& dpre) {
+  Op o("asr_step_backward_");
+  TORCH_CHECK(w.size() == 20 && hid.size() == 8 && dpre.size() == 8, o.name,
+              ": 10 output layers, 8 hidden layers");
+  float* pdo = o.f(douts, B * ASR_DN, "douts");
+  auto pw = o.list(w, F32, 1, "w");
+  auto ph = o.list(hid, F32, B * 64, "hid");
+  auto pdp = o.list(dpre, F32, B * 64, "dpre");
+  float* prec = o.f(rec, ASR_NQ * B, "rec");
+  float* peh = o.f(eps_shift, 2 * B, "eps_shift");
+  float* pes = o.f(eps_scale, B, "eps_scale");
+  float* ptf = o.f(dtheta_fwd, 6 * B, "dtheta_fwd");
+  float* ptb = o.f(dtheta_back, 6 * B, "dtheta_back");
+  float* pd = o.f(dot, B, "dot");
+  float* pdr = o.f(dreg, 4 * B, "dreg");
+  float* pds = o.f(dss, 3 * B, "dss");
+  GUARD(o);
+  check(mog_asr_step_backward(B, train, fix_steps, temperature, s_pm, s_pv, grad_scale,
+                              arr<float>(pw), marr<float>(ph), prec, peh, pes, ptf, ptb, pd, pdr,
+                              pds, pdo, marr<float>(pdp), o.stream()),
+        o.name);
 }
 
 }  // namespace
@@ -314,8 +757,9 @@ void rng_fill_(Tensor out, int64_t seed, int64_t offset, bool normal) {
 TORCH_LIBRARY_FRAGMENT(mog_air, m) {
   m.def(
       "gemm_f32_(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, Tensor?[] Cin, "
-      "Tensor?[] Cpre, Tensor?[] aux, Tensor?[] colsum, int M, int N, int K, int lda, int ldb, "
-      "int ldc, int ldaux, bool transA, bool transB, int epi, float aux_scale, int splitk) -> ()");
+      "Tensor(b!)?[] Cpre, Tensor?[] aux, Tensor(c!)?[] colsum, int M, int N, int K, int lda, "
+      "int ldb, int ldc, int ldaux, bool transA, bool transB, int epi, float aux_scale, "
+      "int splitk) -> ()");
   m.def(
       "gemm_f32_sigmoid_philox_(Tensor A, Tensor B, Tensor(a!) C, Tensor? bias, int M, int N, "
       "int K, int lda, int ldb, int ldc, float scale, int seed, int offset) -> ()");
@@ -324,7 +768,7 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "int N, int kseg, int lda, int ldb, int ldc, bool transA, bool transB, int epi) -> ()");
   m.def(
       "gemm_bf16_(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, Tensor?[] Cin, "
-      "Tensor?[] aux, Tensor?[] colsum, int M, int N, int K, int lda, int ldb, int ldc, "
+      "Tensor?[] aux, Tensor(b!)?[] colsum, int M, int N, int K, int lda, int ldb, int ldc, "
       "int ldaux, bool tn, int epi, float aux_scale, int splitk) -> ()");
   m.def("cvt_bf16_batch_(Tensor[] src, Tensor(a!)[] dst, int[] dims) -> ()");
   m.def(
@@ -332,18 +776,18 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "Tensor(a!) out, Tensor? z, Tensor? mask, int mode) -> ()");
   m.def(
       "stn_backward_(Tensor U, int N, int Hin, int Win, Tensor theta, int Hout, int Wout, "
-      "Tensor G, Tensor? gscale, Tensor? dU, Tensor? dtheta, Tensor? dot, int u_period, "
-      "int g_period) -> ()");
+      "Tensor G, Tensor? gscale, Tensor(a!)? dU, Tensor(b!)? dtheta, Tensor(c!)? dot, "
+      "int u_period, int g_period) -> ()");
   m.def(
       "stn_backward_sigmoid_(Tensor U, int N, int Hin, int Win, Tensor theta, int Hout, "
-      "int Wout, Tensor G, Tensor? gscale, Tensor(a!) dm, Tensor? dtheta, Tensor? dot, "
+      "int Wout, Tensor G, Tensor? gscale, Tensor(a!) dm, Tensor(b!)? dtheta, Tensor(c!)? dot, "
       "int g_period) -> ()");
   m.def(
       "lstm_cell_forward_(Tensor G, Tensor? bias, Tensor? c_prev, Tensor(a!) c_out, "
       "Tensor(b!) h_out, int B, int H) -> ()");
   m.def(
       "lstm_cell_backward_(Tensor G, Tensor? bias, Tensor? c_prev, Tensor c_cur, Tensor dh, "
-      "Tensor? dc, Tensor(a!) dG, Tensor(b!) dc_prev, Tensor? dGsum, int B, int H) -> ()");
+      "Tensor? dc, Tensor(a!) dG, Tensor(b!) dc_prev, Tensor(c!)? dGsum, int B, int H) -> ()");
   m.def(
       "air_step_forward_(int B, int HS, int HZ, int step, bool train, bool use_num_prior, "
       "float thr, float temperature, float prior_lo, float prior_bias, float s_pm, float s_pv, "
@@ -357,23 +801,26 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "air_step_backward_(int B, int HS, bool train, bool use_num_prior, float temperature, "
       "float prior_lo, float prior_bias, float s_pm, float s_pv, float h_pm, float h_pv, "
       "float grad_scale, Tensor? dloss, Tensor rec, Tensor eps_scale, Tensor eps_shift, "
-      "Tensor dtheta_fwd, "
-      "Tensor dtheta_back, Tensor dot, Tensor[] hid, Tensor[] w2, Tensor(a!) dout, int dout_hs, "
-      "Tensor(b!) dhid, int dhid_hs) -> ()");
+      "Tensor dtheta_fwd, Tensor dtheta_back, Tensor dot, Tensor[] hid, Tensor[] w2, "
+      "Tensor(a!) dout, int dout_hs, Tensor(b!) dhid, int dhid_hs) -> ()");
+  m.def(
+      "generation_prior_(int G, int Z, float s_pm, float s_plv, float h_pm, float h_plv, "
+      "float v_pm, float v_plv, Tensor eps_scale, Tensor eps_shift, Tensor eps_z, "
+      "Tensor(a!) theta_back, Tensor(b!) scale, Tensor(c!) shift, Tensor(d!) z) -> ()");
   m.def(
       "stn_write_parts_(Tensor U, int N, int Hin, int Win, Tensor theta, int Hout, int Wout, "
       "Tensor z, Tensor mask, Tensor(a!) parts, Tensor(b!) part_rows) -> ()");
   m.def(
       "vae_sample_forward_(int B, int Z, float v_pm, float v_pv, float v_plv, Tensor mu, "
-      "Tensor lv, Tensor eps, Tensor(a!) z, Tensor? z_bf16, int ld_zb, Tensor act, "
-      "Tensor(b!)? runloss, Tensor(c!) vkl) -> ()");
+      "Tensor lv, Tensor eps, Tensor(a!) z, Tensor(b!)? z_bf16, int ld_zb, Tensor act, "
+      "Tensor(c!)? runloss, Tensor(d!) vkl) -> ()");
   m.def(
       "air_runloss_(int T, int B, Tensor rec, int rec_step_stride, Tensor skl, Tensor shkl, "
       "Tensor vkl, Tensor(a!) runloss) -> ()");
   m.def(
       "vae_sample_backward_(int B, int Z, float v_pm, float v_pv, float grad_scale, Tensor mu, "
-      "Tensor lv, Tensor eps, Tensor dz, Tensor act, Tensor? dmu, Tensor? dlv, Tensor? dmu_bf16, "
-      "Tensor? dlv_bf16, int ld_b) -> ()");
+      "Tensor lv, Tensor eps, Tensor dz, Tensor act, Tensor(a!)? dmu, Tensor(b!)? dlv, "
+      "Tensor(c!)? dmu_bf16, Tensor(d!)? dlv_bf16, int ld_b) -> ()");
   m.def("sigmoid_backward_(Tensor r, Tensor dr, Tensor(a!) dm, int n) -> ()");
   m.def(
       "stn_vae_step_(int B, int C, Tensor x, Tensor theta_f, Tensor theta_b, Tensor mask, "
@@ -384,18 +831,48 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "Tensor(j!)? z, Tensor(k!)? zb, Tensor(l!)? d1b, Tensor(m!)? d2b, Tensor(n!) r, "
       "int x_period=0) -> ()");
   m.def(
-      "recon_loss_(Tensor x, Tensor? canvas, Tensor? parts, int nparts, int part_stride, "
+      "recon_loss_(Tensor x, Tensor(a!)? canvas, Tensor? parts, int nparts, int part_stride, "
       "Tensor? part_rows, int C, Tensor runloss, Tensor digits, Tensor? targets, int B, int C2, "
-      "float grad_scale, Tensor? recon, Tensor(a!) bce, Tensor(b!) mse, Tensor(c!) loss, "
-      "Tensor? acc, Tensor? dcanvas) -> ()");
+      "float grad_scale, Tensor(b!)? recon, Tensor(c!) bce, Tensor(d!) mse, Tensor(e!) loss, "
+      "Tensor(f!)? acc, Tensor(g!)? dcanvas) -> ()");
   m.def(
       "batch_mean_(Tensor? a0, Tensor? a1, Tensor? a2, Tensor? a3, int B, Tensor(a!) out) -> ()");
   m.def(
       "clip_adam_(Tensor(a!) params, Tensor(b!) grads, Tensor(c!) m, Tensor(d!) v, Tensor off, "
-      "Tensor len, Tensor block_tensor, Tensor block_start, int nblocks, Tensor? sumsq, "
+      "Tensor len, Tensor block_tensor, Tensor block_start, int nblocks, Tensor(e!)? sumsq, "
       "float clip, float lr_t, float beta1, float beta2, float eps) -> ()");
   m.def("add_(Tensor a, Tensor b, Tensor(a!) out, int n) -> ()");
   m.def("rng_fill_(Tensor(a!) out, int seed, int offset, bool normal) -> ()");
+  // AIR-ASR (air_number_bbox_location.py:384-1084)
+  m.def(
+      "asr_pack_(int B, int Z, int H, int ld, Tensor? z, Tensor? ss, Tensor? h, "
+      "Tensor(a!) out) -> ()");
+  m.def(
+      "asr_unpack_(int B, int Z, int H, int ld, Tensor dU, Tensor dUg, Tensor(a!) dz, "
+      "Tensor(b!) dss, Tensor(c!) dh, Tensor(d!) dhg) -> ()");
+  m.def(
+      "asr_step_forward_(int B, int step, bool train, int fix_steps, float thr, "
+      "float temperature, float s_pm, float s_pv, float s_plv, float gamma_num, Tensor[] w, "
+      "Tensor(a!)?[] hid, Tensor eps_shift, Tensor eps_scale, Tensor u, Tensor(b!) stop, "
+      "Tensor(c!) digits, Tensor(d!) live, Tensor(e!) rec, Tensor(f!) theta_fwd, "
+      "Tensor(g!) theta_back, Tensor(h!) ss, Tensor(i!) scale, Tensor(j!) shift, "
+      "Tensor(k!) zprob, Tensor(l!) zmask, Tensor(m!) zval, Tensor(n!) zc) -> ()");
+  m.def(
+      "asr_terms_(int B, int T, int C, int[] cons, float[] gammas, Tensor rec, Tensor vkl, "
+      "Tensor zmask, Tensor live, Tensor(a!) klsum, Tensor(b!) pr, Tensor(c!) area, "
+      "Tensor(d!) out, Tensor(e!) size, Tensor(f!) overlap, Tensor(g!) zsum) -> ()");
+  m.def(
+      "asr_finalize_(int B, int T, int C, int[] cons, float[] gammas, float inv_batch_global, "
+      "Tensor rec, Tensor live, Tensor zsum, Tensor pr, Tensor(a!) loss, Tensor(b!) element, "
+      "Tensor(c!) margin) -> ()");
+  m.def(
+      "asr_terms_backward_(int B, int T, int C, int[] cons, float[] gammas, float grad_scale, "
+      "float inv_batch_global, Tensor rec, Tensor live, Tensor zsum, Tensor(a!) dreg) -> ()");
+  m.def(
+      "asr_step_backward_(int B, bool train, int fix_steps, float temperature, float s_pm, "
+      "float s_pv, float grad_scale, Tensor[] w, Tensor?[] hid, Tensor rec, Tensor eps_shift, "
+      "Tensor eps_scale, Tensor dtheta_fwd, Tensor dtheta_back, Tensor dot, Tensor dreg, "
+      "Tensor? dss, Tensor(a!) douts, Tensor(b!)?[] dpre) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
@@ -411,6 +888,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("lstm_cell_backward_", &lstm_cell_backward_);
   m.impl("air_step_forward_", &air_step_forward_);
   m.impl("air_step_backward_", &air_step_backward_);
+  m.impl("generation_prior_", &generation_prior_);
   m.impl("vae_sample_forward_", &vae_sample_forward_);
   m.impl("vae_sample_backward_", &vae_sample_backward_);
   m.impl("air_runloss_", &air_runloss_);
@@ -422,4 +900,11 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("clip_adam_", &clip_adam_);
   m.impl("add_", &add_);
   m.impl("rng_fill_", &rng_fill_);
+  m.impl("asr_pack_", &asr_pack_);
+  m.impl("asr_unpack_", &asr_unpack_);
+  m.impl("asr_step_forward_", &asr_step_forward_);
+  m.impl("asr_terms_", &asr_terms_);
+  m.impl("asr_finalize_", &asr_finalize_);
+  m.impl("asr_terms_backward_", &asr_terms_backward_);
+  m.impl("asr_step_backward_", &asr_step_backward_);
 }

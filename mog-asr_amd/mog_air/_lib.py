@@ -130,7 +130,7 @@ def build_torch_ops(verbose: bool = False) -> str:
         # libmog_air.so: resolved by its soname once load() has mapped it
         # (runpath kept as a fallback); c10_hip for the current-stream query
         extra_ldflags=["-L" + os.path.dirname(LIB_PATH), "-lmog_air",
-                       "-L" + os.path.join(os.path.dirname(torch.__file__), "lib"), "-lc10_hip",
+                       "-L" + os.path.join(os.path.dirname(torch.__file__), "lib"), "-lc10_hip", "-ltorch_hip",
                        "-Wl,-rpath," + os.path.dirname(LIB_PATH)],
         build_directory=bdir, is_python_module=False, verbose=verbose)
     # cpp_extension.load registered the ops from the build copy already

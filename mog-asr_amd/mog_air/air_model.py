@@ -1130,7 +1130,7 @@ class AIRModel:
         G = int(batch if batch is not None else self.generation_batch_size)
         T, C, W2, Z = int(num_steps), self.canvas_size, self.W2, self.vae_latent_dimensions
         G1, G2 = self.vae_generative_units
-        dev, s = self.device, stream_ptr()
+        dev = self.device
         e = lambda *sh: torch.empty(sh, device=dev, dtype=torch.float32)  # noqa: E731
         eps = {"eps_scale": e(T, G), "eps_shift": e(T, G, 2), "eps_z": e(T, G, Z),
                "eps_x": e(T, G, W2)}
@@ -1149,12 +1149,12 @@ class AIRModel:
         vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
         lik_std = float(self.hyper("vae_likelihood_std"))
         for t in range(T):
-            _lib.call("mog_generation_prior", G, Z, float(self.scale_prior_mean),
-                      self.scale_prior_log_variance, float(self.shift_prior_mean),
-                      self.shift_prior_log_variance, float(self.vae_prior_mean),
-                      self.vae_prior_log_variance, dp(eps["eps_scale"][t]),
-                      dp(eps["eps_shift"][t]), dp(eps["eps_z"][t]), dp(st_back[t]), dp(scale),
-                      dp(shift), dp(z), s)
+            _ops.generation_prior_(G, Z, float(self.scale_prior_mean),
+                                   self.scale_prior_log_variance, float(self.shift_prior_mean),
+                                   self.shift_prior_log_variance, float(self.vae_prior_mean),
+                                   self.vae_prior_log_variance, eps["eps_scale"][t],
+                                   eps["eps_shift"][t], eps["eps_z"][t], st_back[t], scale, shift,
+                                   z)
             gemm([z], [vw["generative_1"]], [d1], G, G1, Z, Z, G1, G1, epi=EPI_SOFTPLUS,
                  bias=[vb["generative_1"]])
             gemm([d1], [vw["generative_2"]], [d2], G, G2, G1, G1, G2, G2, epi=EPI_SOFTPLUS,

@@ -21,7 +21,6 @@ steps at the end, as the reference's TensorArrays are (:917-923).
 """
 from __future__ import annotations
 
-import ctypes
 from typing import Dict, Optional, Sequence
 
 import numpy as np
@@ -30,7 +29,7 @@ import torch
 from . import _lib, ops
 from .air_model import AIRModel as _AirBase
 from .air_model import _SCOPES, _Workspace, _f32log, annealed_value
-from .ops import EPI_RELU, EPI_STORE, dp, gemm, stream_ptr
+from .ops import EPI_RELU, EPI_STORE, gemm
 
 _ops = ops._ops  # torch.ops.mog_air (csrc/torch_ops.cpp)
 from .params import ParamStore
@@ -162,7 +161,7 @@ class AIRModel(_AirBase):
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         if self.device.type != "cuda":
             raise RuntimeError("AIRModel runs on a HIP device only (no CPU fallback)")
-        _lib.load()
+        _lib.load_torch_ops()
         self.input_images, self.target_num_digits = input_images, target_num_digits
         self.max_steps, self.max_digits = int(max_steps), max_digits
         self.rnn_units = int(rnn_units)
@@ -214,12 +213,18 @@ class AIRModel(_AirBase):
             if self.params.specs != specs:
                 raise ValueError("reused scope has different variable shapes")
         else:
-            self.params = ParamStore(specs, self.device, seed=seed)
+            # the LSTM GEMMs run over LU = 312 packed rows (16-byte operand
+            # rows): 3 zero rows behind each LSTM kernel are the rows past its
+            # Z + 3 + H, so no launch reads or accumulates into a neighbour
+            kpad = (LU - (self.vae_latent_dimensions + 3 + self.rnn_units)) * 4 * self.rnn_units
+            self.params = ParamStore(specs, self.device, seed=seed,
+                                     pad={ROOT + "infer_rnn_running/kernel": kpad,
+                                          ROOT + "gen_rnn_running/kernel": kpad})
             _SCOPES[key] = self.params
         self._ws = None
         self._last_T = None
         self._outputs_ready = False
-        self._cons_arr = (ctypes.c_int * len(cons))(*cons)
+        self._cons = [int(c) for c in cons]
 
     # zsum_hook / live_hook: data-parallel collectives (parallel.attach)
     zsum_hook = None
@@ -232,6 +237,21 @@ class AIRModel(_AirBase):
     def _N(self, name):
         return self.params.view(ROOT + name)
 
+    def _Kpad(self, name, buf="flat"):
+        """An LSTM kernel with its zero pad rows: [rows + pad, 4H] (the GEMMs
+        over LU packed rows read / accumulate rows up to C2 + LU)."""
+        key = ("kpad", buf, name)
+        hit = self.params._views.get(key)
+        t = getattr(self.params, buf)
+        if hit is not None and hit[0] is t:
+            return hit[1]
+        o = self.params.offsets[ROOT + name]
+        rows, cols = self.params.shapes[ROOT + name]
+        pad_rows = LU - (self.vae_latent_dimensions + 3 + self.rnn_units)
+        v = t[o:o + (rows + pad_rows) * cols].view(rows + pad_rows, cols)
+        self.params._views[key] = (t, v)
+        return v
+
     def _Ng(self, name):
         return self.params.g(ROOT + name)
 
@@ -240,17 +260,17 @@ class AIRModel(_AirBase):
               "z_pres/prior/dense_1", "z_pres/log_odds/dense_1")
 
     def _w20(self):
-        ptrs = []
+        ts = []
         for n in self._OUT_W:
-            ptrs += [dp(self._N(n + "/kernel")), dp(self._N(n + "/bias"))]
-        return _lib.ptr_array(ptrs)
+            ts += [self._N(n + "/kernel"), self._N(n + "/bias")]
+        return ts
 
     def _gammas(self):
-        g = [self.hyper("constrains_num_gamma"), self.hyper("constrains_margin_gamma"),
-             self.hyper("constrains_num_element_gamma"), self.hyper("constrains_bbox_gamma"),
-             self.hyper("constrains_sharesize_gamma"), self.hyper("constrains_area_gamma"),
-             self.constrains_area_minmax[0], self.constrains_area_minmax[1]]
-        return (ctypes.c_float * 8)(*g)
+        return [float(v) for v in (
+            self.hyper("constrains_num_gamma"), self.hyper("constrains_margin_gamma"),
+            self.hyper("constrains_num_element_gamma"), self.hyper("constrains_bbox_gamma"),
+            self.hyper("constrains_sharesize_gamma"), self.hyper("constrains_area_gamma"),
+            self.constrains_area_minmax[0], self.constrains_area_minmax[1])]
 
     def _fill_noise(self, ws, noise):
         """eps_shift [T,B,2], eps_scale [T,B], eps_z, eps_x, u (injected or
@@ -277,9 +297,8 @@ class AIRModel(_AirBase):
     def _forward(self, X, targets, ws, need_grad, outputs=True):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
         C, W, C2 = self.canvas_size, self.windows_size, self.C2
-        s = stream_ptr()
-        Ki = self._N("infer_rnn_running/kernel")
-        Kg = self._N("gen_rnn_running/kernel")
+        Ki = self._Kpad("infer_rnn_running/kernel")
+        Kg = self._Kpad("gen_rnn_running/kernel")
         bi, bg = self._N("infer_rnn_running/bias"), self._N("gen_rnn_running/bias")
         if ws.cparts is None:
             ws.canvas.zero_()
@@ -304,16 +323,15 @@ class AIRModel(_AirBase):
         sc_w = [self._N("inf_scale/dense/kernel")[:H], self._N("inf_scale/dense_2/kernel")[:H]]
         for t in range(T):
             prev = t > 0
-            _lib.call("mog_asr_pack", B, Z, H, LU, dp(ws.z[t - 1]) if prev else None,
-                      dp(ws.ss[t - 1]) if prev else None, dp(ws.h[t - 1]) if prev else None,
-                      dp(ws.U[t]), s)
-            _lib.call("mog_asr_pack", B, Z, H, LU, dp(ws.z[t - 1]) if prev else None,
-                      dp(ws.ss[t - 1]) if prev else None, dp(ws.hg[t - 1]) if prev else None,
-                      dp(ws.Ug[t]), s)
+            _ops.asr_pack_(B, Z, H, LU, ws.z[t - 1] if prev else None,
+                           ws.ss[t - 1] if prev else None, ws.h[t - 1] if prev else None, ws.U[t])
+            _ops.asr_pack_(B, Z, H, LU, ws.z[t - 1] if prev else None,
+                           ws.ss[t - 1] if prev else None, ws.hg[t - 1] if prev else None,
+                           ws.Ug[t])
             # K = LU: the packed rows end in zeros, so the chain's last terms are
             # 0 * w (exactly +-0: the sum is unchanged bit for bit) and the
-            # operands are 16-byte rows (LDS-DMA GEMM); the 3 weight rows read
-            # past the U-part are the following variables (finite), in bounds
+            # operands are 16-byte rows (LDS-DMA GEMM); the 3 weight rows past
+            # the U-part are the kernels' own zero pad rows (ParamStore pad)
             gemm([ws.U[t]], [Ki[C2:]], [ws.G[t]], B, 4 * H, LU, LU, 4 * H, 4 * H, bias=[bi],
                  Cin=[ws.Gx])
             _ops.lstm_cell_forward_(ws.G[t], None, ws.c[t - 1] if prev else None, ws.c[t],
@@ -328,15 +346,14 @@ class AIRModel(_AirBase):
                 gemm([ws.Ug[t][:, Z + 3:]], [self._N("z_pres/prior/dense/kernel")], [hid[5]], B,
                      64, H, LU, 64, 64, epi=EPI_RELU, bias=[self._N("z_pres/prior/dense/bias")])
             gemm([ws.h[t]] * 2, sc_w, hid[6:8], B, 64, H, H, 64, 64, epi=EPI_STORE)
-            hid_arr = _lib.ptr_array([dp(x) if (k != 5 or fix < 0) else None
-                                      for k, x in enumerate(hid)])
-            _lib.call("mog_asr_step_forward", B, t, int(self.train), fix, thr, temp,
-                      float(self.scale_prior_mean), float(self.scale_prior_variance),
-                      self.scale_prior_log_variance, float(self.hyper("constrains_num_gamma")),
-                      w20, hid_arr, dp(ws.eps_shift[t]), dp(ws.eps_scale[t]), dp(ws.u[t]),
-                      dp(ws.stop), dp(ws.digits), dp(ws.live), dp(ws.arec[t]), dp(ws.th_f[t]),
-                      dp(ws.th_b[t]), dp(ws.ss[t]), dp(ws.scale[t]), dp(ws.shift[t]),
-                      dp(ws.zprob[t]), dp(ws.zmask[t]), dp(ws.zval[t]), dp(ws.zc[t]), s)
+            hid_l = [x if (k != 5 or fix < 0) else None for k, x in enumerate(hid)]
+            _ops.asr_step_forward_(B, t, self.train, fix, thr, temp, float(self.scale_prior_mean),
+                                   float(self.scale_prior_variance), self.scale_prior_log_variance,
+                                   float(self.hyper("constrains_num_gamma")), w20, hid_l,
+                                   ws.eps_shift[t], ws.eps_scale[t], ws.u[t], ws.stop, ws.digits,
+                                   ws.live, ws.arec[t], ws.th_f[t], ws.th_b[t], ws.ss[t],
+                                   ws.scale[t], ws.shift[t], ws.zprob[t], ws.zmask[t], ws.zval[t],
+                                   ws.zc[t])
             if self.live_hook is not None:
                 self.live_hook(ws.live, t)
             if self.fused_step:
@@ -353,12 +370,10 @@ class AIRModel(_AirBase):
     def _forward_loss(self, X, targets, ws, need_grad, outputs=True):
         """elbo (:917-935, recon :937-962) + pr_loss + element + margin
         (:964-1079)."""
-        B, T, C2, s = ws.B, self.max_steps, self.C2, stream_ptr()
+        B, T, C2 = ws.B, self.max_steps, self.C2
         g = self._gammas()
-        _lib.call("mog_asr_terms", B, T, self.canvas_size, len(self.constrains_num),
-                  self._cons_arr, g, dp(ws.arec), dp(ws.vkl), dp(ws.zmask), dp(ws.live),
-                  dp(ws.klsum), dp(ws.pr), dp(ws.area), dp(ws.outl), dp(ws.size), dp(ws.over),
-                  dp(ws.zsum), s)
+        _ops.asr_terms_(B, T, self.canvas_size, self._cons, g, ws.arec, ws.vkl, ws.zmask, ws.live,
+                        ws.klsum, ws.pr, ws.area, ws.outl, ws.size, ws.over, ws.zsum)
         if self.zsum_hook is not None:
             self.zsum_hook(ws.zsum)
         parts = ws.cparts
@@ -371,28 +386,24 @@ class AIRModel(_AirBase):
                          ws.recon if outputs else None, ws.bce, ws.mse, ws.loss_b,
                          ws.acc_b if targets is not None else None,
                          ws.dcanvas if need_grad else None)
-        _lib.call("mog_asr_finalize", B, T, self.canvas_size, len(self.constrains_num),
-                  self._cons_arr, g, float(self._gscale(B)), dp(ws.arec),
-                  dp(ws.live), dp(ws.zsum), dp(ws.pr), dp(ws.loss_b), dp(ws.element),
-                  dp(ws.margin), s)
+        _ops.asr_finalize_(B, T, self.canvas_size, self._cons, g, float(self._gscale(B)), ws.arec,
+                           ws.live, ws.zsum, ws.pr, ws.loss_b, ws.element, ws.margin)
         _ops.batch_mean_(ws.loss_b, ws.acc_b if targets is not None else None, ws.mse, None, B,
                          ws.means)
-        _lib.call("mog_add", dp(ws.means), dp(ws.margin), dp(ws.means), 1, s)
+        _ops.add_(ws.means, ws.margin, ws.means, 1)
         self._outputs_ready = True
 
     # --------------------------------------------------------- backward ---
     def _dz_hook(self, ws, t):
         if t < self.max_steps - 1:
-            _lib.call("mog_add", dp(ws.dz), dp(ws.dz_carry), dp(ws.dz),
-                      ws.B * self.vae_latent_dimensions, stream_ptr())
+            _ops.add_(ws.dz, ws.dz_carry, ws.dz, ws.B * self.vae_latent_dimensions)
 
     def _backward(self, X, ws):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
         C, W, C2 = self.canvas_size, self.windows_size, self.C2
-        s = stream_ptr()
         self.params.grad.zero_()
-        Ki = self._N("infer_rnn_running/kernel")
-        Kg = self._N("gen_rnn_running/kernel")
+        Ki = self._Kpad("infer_rnn_running/kernel")
+        Kg = self._Kpad("gen_rnn_running/kernel")
         KU = Z + 3 + H
         gscale = self._gscale(B)
         fix = -1 if self.fix_steps is None else int(self.fix_steps)
@@ -401,9 +412,8 @@ class AIRModel(_AirBase):
         ws.dhg.zero_()
         ws.dGsum.zero_()
         ws.dGgsum.zero_()
-        _lib.call("mog_asr_terms_backward", B, T, self.canvas_size, len(self.constrains_num),
-                  self._cons_arr, self._gammas(), float(gscale), float(gscale), dp(ws.arec),
-                  dp(ws.live), dp(ws.zsum), dp(ws.dreg), s)
+        _ops.asr_terms_backward_(B, T, self.canvas_size, self._cons, self._gammas(), float(gscale),
+                                 float(gscale), ws.arec, ws.live, ws.zsum, ws.dreg)
         head_w = [self._N(n + "/kernel")[:H] for n in ("inf_shift/dense", "inf_shift/dense_2",
                                                      "z_pres/log_odds/dense", "inf_scale/dense",
                                                      "inf_scale/dense_2")]
@@ -418,16 +428,15 @@ class AIRModel(_AirBase):
             ops.stn_backward(X, ws.th_f[t], (W, W), ws.dg, want_dU=False, dtheta=ws.dth_f)
             hid = [ws.hid8[k, t] for k in range(8)]
             dpre = [ws.dpre[k, t] for k in range(8)]
-            _lib.call("mog_asr_step_backward", B, int(self.train), fix,
-                      float(self.hyper("z_pres_temperature")), float(self.scale_prior_mean),
-                      float(self.scale_prior_variance), float(gscale), w20,
-                      _lib.ptr_array([dp(x) if (k != 5 or fix < 0) else None
-                                      for k, x in enumerate(hid)]),
-                      dp(ws.arec[t]), dp(ws.eps_shift[t]), dp(ws.eps_scale[t]), dp(ws.dth_f),
-                      dp(ws.dth_b), dp(ws.dot), dp(ws.dreg[t]),
-                      dp(ws.dss_carry) if t < T - 1 else None, dp(ws.douts[t]),
-                      _lib.ptr_array([dp(x) if (k != 5 or fix < 0) else None
-                                      for k, x in enumerate(dpre)]), s)
+            _ops.asr_step_backward_(B, self.train, fix, float(self.hyper("z_pres_temperature")),
+                                    float(self.scale_prior_mean),
+                                    float(self.scale_prior_variance), float(gscale), w20,
+                                    [x if (k != 5 or fix < 0) else None for k, x in enumerate(hid)],
+                                    ws.arec[t], ws.eps_shift[t], ws.eps_scale[t], ws.dth_f,
+                                    ws.dth_b, ws.dot, ws.dreg[t],
+                                    ws.dss_carry if t < T - 1 else None, ws.douts[t],
+                                    [x if (k != 5 or fix < 0) else None
+                                     for k, x in enumerate(dpre)])
             # dh[t] += the five heads reading h_t; dhg[t] += the generative shift heads
             ops.gemm_kseg([dpre[k] for k in (0, 1, 2, 6, 7)], head_w, ws.dh[t], B, H, 64, 64, 64,
                           H, transB=True, Cin=ws.dh[t])
@@ -447,9 +456,8 @@ class AIRModel(_AirBase):
                 gemm([ws.dG[t]], [Ki[C2:]], [ws.dU], B, LU, 4 * H, 4 * H, 4 * H, LU,
                      transB=True)
                 gemm([ws.dGg[t]], [Kg], [ws.dUg], B, LU, 4 * H, 4 * H, 4 * H, LU, transB=True)
-                _lib.call("mog_asr_unpack", B, Z, H, LU, dp(ws.dU), dp(ws.dUg),
-                          dp(ws.dz_carry), dp(ws.dss_carry), dp(ws.dh[t - 1]),
-                          dp(ws.dhg[t - 1]), s)
+                _ops.asr_unpack_(B, Z, H, LU, ws.dU, ws.dUg, ws.dz_carry, ws.dss_carry,
+                                 ws.dh[t - 1], ws.dhg[t - 1])
         self._weight_grads(X, ws)
         self._reduce_bucket(0, self.params.total)
 
@@ -462,15 +470,16 @@ class AIRModel(_AirBase):
         else:
             self._vae_weight_grads_fp32(ws)
         G = self._Ng
-        gKi, gKg = G("infer_rnn_running/kernel"), G("gen_rnn_running/kernel")
+        gKi = self._Kpad("infer_rnn_running/kernel", "grad")
+        gKg = self._Kpad("gen_rnn_running/kernel", "grad")
         # LSTMCells: x rows from sum_t dG (the x input is loop-invariant)
         if self.precision == "bf16":
             self._x_grad_bf16(X, ws, gKi, G("infer_rnn_running/bias"), 0, C2)
         else:
             self._dw(X, ws.dGsum, gKi[:C2], B, C2, 4 * H, C2, 4 * H, G("infer_rnn_running/bias"))
-        # M = LU (16-byte aligned LDS-DMA operands): the 3 pad rows of U^T are
-        # zero, so their rows of the product are exactly +-0 and the atomics
-        # leave the following variables' gradients unchanged
+        # M = LU (16-byte aligned LDS-DMA operands): rows Z+3+H.. of the
+        # product land in the kernels' own pad rows (ParamStore pad), never in
+        # a neighbouring variable's gradient
         self._dw(ws.U, ws.dG, gKi[C2:], TB, LU, 4 * H, LU, 4 * H)
         self._dw(ws.Ug, ws.dGg, gKg, TB, LU, 4 * H, LU, 4 * H, G("gen_rnn_running/bias"))
         # hidden layers reading h_t, hg_t, hg_{t-1}

@@ -52,17 +52,22 @@ def param_specs(C2: int, H: int, W2: int, R: Tuple[int, int], G: Tuple[int, int]
 class ParamStore:
     """Flat parameters + grads + Adam state for one scope (shared on reuse)."""
 
-    def __init__(self, specs, device, seed: int = 1235):
+    def __init__(self, specs, device, seed: int = 1235, pad: Dict[str, int] = None):
+        """pad[name]: zero elements kept behind variable `name` (not part of
+        any variable: no view, optimizer entry or checkpoint covers them), for
+        kernels that read / accumulate a few rows past a matrix (the AIR-ASR
+        LSTM kernels at the 16-byte-aligned packed-row count)."""
         self.specs = list(specs)
         self.device = device
         self._views: Dict[Tuple[str, str], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.offsets: Dict[str, int] = {}
         self.shapes: Dict[str, Tuple[int, ...]] = {}
+        pad = dict(pad or {})
         off = 0
         for name, shape in self.specs:
             self.offsets[name] = off
             self.shapes[name] = tuple(shape)
-            n = int(np.prod(shape))
+            n = int(np.prod(shape)) + pad.get(name, 0)
             off += (n + ALIGN - 1) // ALIGN * ALIGN
         self.total = off
         self.n_params = sum(int(np.prod(s)) for _, s in self.specs)

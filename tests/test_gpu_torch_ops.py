@@ -271,6 +271,99 @@ def test_air_model_dispatches_through_torch_ops():
         assert want <= rec.names, sorted(want - rec.names)
 
 
+def test_asr_model_dispatches_through_torch_ops():
+    """Every hot-path launch of an AIR-ASR train step (train_air_pr.py config:
+    learned z_pres prior, number regularisers) goes through torch.ops.mog_air,
+    the ASR cells and structural losses (air_number_bbox_location.py:384-1084)
+    included; no ctypes launch remains on the step."""
+    from torch.utils._python_dispatch import TorchDispatchMode
+
+    from mog_air import _lib
+    from mog_air.asr_model import AIRModel as AsrModel
+
+    class Rec(TorchDispatchMode):
+        def __init__(self):
+            super().__init__()
+            self.names = set()
+
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            self.names.add(str(func.overloadpacket))
+            return func(*args, **(kwargs or {}))
+
+    calls = []
+    real = _lib.call
+    _lib.call = lambda name, *a: (calls.append(name), real(name, *a))[1]
+    try:
+        x, k = ao.synthetic_canvases(32, seed=4)
+        for prec in ("bf16", "fp32"):
+            m = AsrModel(None, None, max_steps=3, max_digits=3, cnn=False, train=True,
+                         scope="asrdisp" + prec, device=DEV, precision=prec,
+                         learning_rate=1e-4, gradient_clipping_norm=1.0,
+                         constrains_num=[1, 3], constrains_margin_gamma=100.0,
+                         constrains_num_element_gamma=10.0, constrains_area_minmax=[17, 23],
+                         z_pres_temperature=0.1, stopping_threshold=0.9)
+            X, K = torch.tensor(x, device=DEV), torch.tensor(k, device=DEV)
+            with Rec() as rec:
+                m.train_step_async(X, K)
+            torch.cuda.synchronize()
+            want = {"mog_air.asr_pack_", "mog_air.asr_step_forward_", "mog_air.asr_terms_",
+                    "mog_air.asr_finalize_", "mog_air.asr_terms_backward_",
+                    "mog_air.asr_step_backward_", "mog_air.asr_unpack_", "mog_air.add_",
+                    "mog_air.gemm_f32_", "mog_air.lstm_cell_forward_", "mog_air.recon_loss_",
+                    "mog_air.lstm_cell_backward_", "mog_air.clip_adam_"}
+            assert want <= rec.names, sorted(want - rec.names)
+    finally:
+        _lib.call = real
+    assert not calls, calls
+
+
+def test_ops_validate_operands():
+    """The launch-level ops reject, before any launch, an operand that is too
+    small for the extent the kernel touches, of the wrong dtype, or on the
+    host (ADVICE: a wrongly shaped tensor must be an error, not an
+    out-of-bounds device write)."""
+    ops = torch.ops.mog_air
+    r = torch.empty(10, device=DEV)
+    with pytest.raises(RuntimeError, match="touches"):
+        ops.add_(r, r, torch.empty(5, device=DEV), 10)
+    with pytest.raises(RuntimeError, match="must be"):
+        ops.add_(r, r.to(torch.bfloat16), torch.empty(10, device=DEV), 10)
+    with pytest.raises((RuntimeError, NotImplementedError)):
+        ops.add_(r.cpu(), r.cpu(), r.cpu(), 10)
+    A = torch.empty((64, 32), device=DEV)
+    with pytest.raises(RuntimeError, match="touches"):  # C needs (64-1)*64+64 elements
+        ops.gemm_f32_([A], [torch.empty((32, 64), device=DEV)], [torch.empty((64, 32), device=DEV)],
+                      [None], [None], [None], [None], [None], 64, 64, 32, 32, 64, 64, 64, False,
+                      False, 0, 0.0, 1)
+
+
+def test_opcheck_launch_level_ops():
+    """torch.library.opcheck on launch-level ops: the schemas' (x!)
+    annotations match what the kernels write (test_schema) and the ops
+    behave under fake / functionalized dispatch."""
+    from torch.library import opcheck
+    ops = torch.ops.mog_air
+    n = 1000
+    a, b = torch.randn(n, device=DEV), torch.randn(n, device=DEV)
+    opcheck(ops.add_.default, (a, b, torch.empty(n, device=DEV), n),
+            test_utils=("test_schema",))
+    opcheck(ops.rng_fill_.default, (torch.empty(n, device=DEV), 7, 0, True),
+            test_utils=("test_schema",))
+    B, Z = 40, 50
+    mu, lv, ep = (torch.randn(B, Z, device=DEV) * 0.3 for _ in range(3))
+    act = torch.ones(B, device=DEV)
+    opcheck(ops.vae_sample_forward_.default,
+            (B, Z, 0.0, 1.0, 0.0, mu, lv, ep, torch.empty(B, Z, device=DEV),
+             torch.zeros(B, 56, device=DEV, dtype=torch.bfloat16), 56, act,
+             torch.zeros(B, device=DEV), torch.empty(B, device=DEV)),
+            test_utils=("test_schema",))
+    G = torch.randn(B, 4 * 256, device=DEV)
+    opcheck(ops.lstm_cell_forward_.default,
+            (G, None, torch.randn(B, 256, device=DEV), torch.empty(B, 256, device=DEV),
+             torch.empty(B, 256, device=DEV), B, 256),
+            test_utils=("test_schema",))
+
+
 # ------------------------------------------------ heads + concrete step op ----
 _STEP_CFG = [0.99, 1.0, -2.0, 0.3, -1.0, 0.05, float(np.log(0.05)), 0.0, 1.0, 0.0]
 

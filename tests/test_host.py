@@ -47,11 +47,29 @@ def test_torch_ops_extension_registers_every_launch_op():
              "stn_backward_", "stn_backward_sigmoid_", "lstm_cell_forward_",
              "lstm_cell_backward_", "air_step_forward_", "air_step_backward_",
              "vae_sample_forward_", "vae_sample_backward_", "sigmoid_backward_", "stn_vae_step_",
-             "recon_loss_", "batch_mean_", "clip_adam_", "add_", "rng_fill_")
+             "recon_loss_", "batch_mean_", "clip_adam_", "add_", "rng_fill_",
+             "generation_prior_", "asr_pack_", "asr_unpack_", "asr_step_forward_", "asr_terms_",
+             "asr_finalize_", "asr_terms_backward_", "asr_step_backward_")
     for n in names:
         getattr(torch.ops.mog_air, n).default  # schema registered
     with pytest.raises(NotImplementedError):
         torch.ops.mog_air.rng_fill_(torch.zeros(4), 1, 0, True)
+    # every argument an op writes is annotated as mutated: no
+    # schema leaves a written tensor unannotated
+    written = {"gemm_f32_": {"C", "Cpre", "colsum"}, "gemm_bf16_": {"C", "colsum"},
+               "stn_backward_": {"dU", "dtheta", "dot"},
+               "stn_backward_sigmoid_": {"dm", "dtheta", "dot"},
+               "lstm_cell_backward_": {"dG", "dc_prev", "dGsum"},
+               "vae_sample_forward_": {"z", "z_bf16", "runloss", "vkl"},
+               "vae_sample_backward_": {"dmu", "dlv", "dmu_bf16", "dlv_bf16"},
+               "recon_loss_": {"canvas", "recon", "bce", "mse", "loss", "acc", "dcanvas"},
+               "clip_adam_": {"params", "grads", "m", "v", "sumsq"},
+               "asr_step_forward_": {"hid", "stop", "digits", "live", "rec"},
+               "asr_step_backward_": {"douts", "dpre"}}
+    for op, args in written.items():
+        sch = getattr(torch.ops.mog_air, op).default._schema
+        mut = {a.name for a in sch.arguments if a.alias_info is not None and a.alias_info.is_write}
+        assert args <= mut, (op, sorted(args - mut))
 
 
 def test_functional_ops_registered_and_refuse_cpu():
