@@ -99,13 +99,18 @@ def roofline(events, B, precision):
             "algorithmic_unit": "flop" if bound == "mfma" else "bytes"}
 
 
-def synthetic(batch, seed, canvas=50):
+def synthetic(batch, seed, canvas=50, counts=None, side=None):
     """Multi-MNIST-like canvases: 1-3 glyphs of side
-    U{17..23} (scaled with the canvas), ~35 % inked at U(0,1), < 0.05 -> 0."""
+    U{17..23} (scaled with the canvas), ~35 % inked at U(0,1), < 0.05 -> 0.
+    counts: objects per image drawn uniformly from this tuple (default 1..3);
+    side: (lo, hi) glyph side, hi exclusive (the bbox datasets: 11..15)."""
     rng = np.random.default_rng(seed)
     imgs = np.zeros((batch, canvas, canvas), np.float32)
-    ks = rng.integers(1, 4, size=batch)
-    lo, hi = (17, 24) if canvas == 50 else (22, 31)
+    if counts is None:
+        ks = rng.integers(1, 4, size=batch)
+    else:
+        ks = np.asarray(counts)[rng.integers(0, len(counts), size=batch)]
+    lo, hi = side if side is not None else ((17, 24) if canvas == 50 else (22, 31))
     for b in range(batch):
         for _ in range(ks[b]):
             s = int(rng.integers(lo, hi))
@@ -130,11 +135,25 @@ def make_model(precision, dev, world, rank, scope, canvas=50):
                     precision=precision)
 
 
-def make_asr_model(precision, dev, scope, canvas=50):
+# configs[4] (train_air_pr.py -dn 3 -ds bbox20k -gb 1 -gs 10 -ga 20,
+# train_air_pr.py:40-61,77-98): three objects of side 11..15, fix_steps 3,
+# bbox / size / area regularisers
+ASR_BBOX = dict(constrains_num=[3], constrains_margin_gamma=0.0,
+                constrains_num_element_gamma=0.0, constrains_bbox_gamma=1.0,
+                constrains_sharesize_gamma=10.0, constrains_area_gamma=20.0,
+                constrains_area_minmax=[11, 15], fix_steps=3)
+ASR_BBOX_DATA = dict(counts=(3,), side=(11, 16))
+
+
+def make_asr_model(precision, dev, scope, canvas=50, world=1, rank=0, cfg=None):
     """configs[2]: train_air_pr.py -dn 13 -gm 100 -gne 10 (AIR-ASR with the
     number regularisers: objects {1, 3}, margin gamma 100, element gamma 10,
-    z_pres temperature 0.1, MAX_STEPS 6; train_air_pr.py:63-82)."""
+    z_pres temperature 0.1, MAX_STEPS 6; train_air_pr.py:63-82); cfg=ASR_BBOX
+    for configs[4]."""
     from mog_air.asr_model import AIRModel as AsrModel
+    kw = dict(constrains_num=[1, 3], constrains_margin_gamma=100.0,
+              constrains_num_element_gamma=10.0, constrains_area_minmax=[17, 23])
+    kw.update(cfg or {})
     return AsrModel(None, None, max_steps=6, max_digits=6, rnn_units=256, canvas_size=canvas,
                     windows_size=28, vae_latent_dimensions=50, vae_recognition_units=(512, 256),
                     vae_generative_units=(256, 512), fix_scale_distribution=True,
@@ -142,22 +161,21 @@ def make_asr_model(precision, dev, scope, canvas=50):
                     scale_hidden_units=64, shift_hidden_units=64, z_pres_hidden_units=64,
                     z_pres_prior_log_odds=-0.01, z_pres_temperature=0.1, stopping_threshold=0.9,
                     learning_rate=1e-4, gradient_clipping_norm=1.0, cnn=False, train=True,
-                    scope=scope, constrains_num=[1, 3], constrains_margin_gamma=100.0,
-                    constrains_num_element_gamma=10.0, constrains_area_minmax=[17, 23],
-                    annealing_schedules={}, device=dev, seed=1235, precision=precision)
+                    scope=scope, annealing_schedules={}, device=dev, seed=1235,
+                    noise_seed=1235 + rank, grad_world=world, precision=precision, **kw)
 
 
 def timed_train(precision, B, steps, warmup, dev, world=1, rank=0, events=False, scope="bench",
-                model=None):
+                model=None, canvas=50, data=None):
     """Time `steps` train steps of batch B per rank (after `warmup`); returns
     (seconds, model).  Barrier + synchronize on both sides; the caller takes
-    the max over ranks."""
+    the max over ranks.  data: synthetic() keywords (counts, side)."""
     if model is None:
-        model = make_model(precision, dev, world, rank, scope)
+        model = make_model(precision, dev, world, rank, scope, canvas=canvas)
     if world > 1:
         from mog_air import parallel
         parallel.attach(model)  # bucketed RCCL all-reduce overlapped with the backward
-    x, k = synthetic(B, 1234 + rank)
+    x, k = synthetic(B, 1234 + rank, canvas, **(data or {}))
     X = torch.from_numpy(x).to(dev)
     K = torch.from_numpy(k).to(dev)
     for _ in range(warmup):
@@ -294,6 +312,10 @@ def parse():
     ap.add_argument("--roofline-batch", type=int, default=65536,
                     help="batch of the stand-alone fused-step roofline runs (0: skip)")
     ap.add_argument("--roofline-launches", type=int, default=30)
+    ap.add_argument("--workload", default="air", choices=["air", "asr_bbox"],
+                    help="air: the BASELINE.json metric (AIR train step); asr_bbox: configs[4] "
+                         "(train_air_pr.py -dn 3 -ds bbox20k -gb 1 -gs 10 -ga 20), the data-"
+                         "parallel ASR-bbox train step")
     return ap.parse_args()
 
 
@@ -405,8 +427,16 @@ def main():
     torch.cuda.set_device(dev)
 
     B, T = args.batch, 3
-    el, model = timed_train(args.precision, B, args.steps, args.warmup, dev, world, rank,
-                            events=True)
+    asr = args.workload == "asr_bbox"
+    if asr:
+        T = 6
+        el, model = timed_train(args.precision, B, args.steps, args.warmup, dev, world, rank,
+                                events=True, data=ASR_BBOX_DATA,
+                                model=make_asr_model(args.precision, dev, "bench_asrbb", world=world,
+                                                     rank=rank, cfg=ASR_BBOX))
+    else:
+        el, model = timed_train(args.precision, B, args.steps, args.warmup, dev, world, rank,
+                                events=True)
     roof = roofline(model.kernel_events, B, args.precision)
     model.kernel_events = None
     if world > 1:
@@ -420,23 +450,32 @@ def main():
     ms = el / args.steps * 1e3
     value = B * world * args.steps / el
     if rank == 0:
+        workload = ("AIR baseline train step (training_air_original.py AIRModel, "
+                    f"{args.precision}), per-GPU batch {B} (configs[1] batch)")
+        model_name = "AIR (LSTM 256, VAE 784-512-256-50, heads 64)"
+        metric = METRIC
+        if asr:
+            metric = ("images/sec/node AIR-ASR bbox train step (configs[4]: train_air_pr.py -dn 3 "
+                      "-ds bbox20k -gb 1 -gs 10 -ga 20), Multi-MNIST 50x50, 1/2/4/8 GPU")
+            workload = ("AIR-ASR train step (air_number_bbox_location.py AIRModel, "
+                        f"{args.precision}): 3 objects of side 11-15, fix_steps 3, bbox / size / "
+                        f"area regularisers, MAX_STEPS 6, per-GPU batch {B}")
+            model_name = "AIR-ASR (inference + generative LSTMCell 256, VAE 784-512-256-50)"
         out = {
-            "metric": METRIC, "value": value, "unit": "images/sec",
+            "metric": metric, "value": value, "unit": "images/sec",
             "n_gpus": world if backend in (None, "nccl") else min(world, torch.cuda.device_count()),
             "ranks": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.precision, "data": "synthetic",
-            "config": {"workload": "AIR baseline train step (training_air_original.py AIRModel, "
-                                   f"{args.precision}), per-GPU batch {B} (configs[1] batch)",
-                       "model": "AIR (LSTM 256, VAE 784-512-256-50, heads 64)",
+            "config": {"workload": workload, "model": model_name,
                        "global_batch": B * world, "per_gpu_batch": B, "canvas": "50x50",
                        "max_steps": T, "data_dependent_steps_would_be": executed,
                        "parallelism": f"dp{world}", "loss_last": loss,
                        "collective_backend": {"nccl": "rccl"}.get(backend, backend)},
             "roofline": roof,
         }
-        if world == 1 and args.extras:
+        if world == 1 and args.extras and not asr:
             if args.precision != "bf16":
                 el2, m2 = timed_train("bf16", B, 10, 3, dev, scope="bench_bf16", events=True)
                 out["configs_1_bf16"] = {
@@ -457,6 +496,26 @@ def main():
                                 "-gne 10: number regularisers, learned z_pres prior, "
                                 "MAX_STEPS 6)"}
                 del m4
+            # configs[2] at the reference's own batch of 64
+            el5, m5 = timed_train("fp32", 64, 30, 5, dev,
+                                  model=make_asr_model("fp32", dev, "bench_asr_b64"))
+            out["configs_2_asr_fp32_b64"] = {
+                "value": 64 * 30 / el5, "unit": "images/sec", "ms_per_step": el5 / 30 * 1e3,
+                "dtype": "fp32", "batch": 64, "steps": 30, "max_steps": 6,
+                "workload": "configs[2] (train_air_pr.py -dn 13 -gm 100 -gne 10) at the "
+                            "reference's batch of 64"}
+            del m5
+            # configs[3]: Multi-dSprites 2-4 objects on 64 x 64 canvases
+            # (multi_dsprites.py:391-392, training_air_original.py -data sprites -dn 24),
+            # bf16 fused step, max_steps 3 as the headline metric
+            el6, m6 = timed_train("bf16", B, 10, 3, dev, scope="bench_c64", canvas=64,
+                                  data=dict(counts=(2, 3, 4)))
+            out["configs_3_dsprites_bf16"] = {
+                "value": B * 10 / el6, "unit": "images/sec", "ms_per_step": el6 / 10 * 1e3,
+                "dtype": "bf16", "batch": B, "steps": 10, "canvas": 64, "max_steps": 3,
+                "workload": "configs[3]: AIR train step on 64x64 Multi-dSprites-like canvases "
+                            "(2-4 objects of side 22-30), bf16 fused step kernel"}
+            del m6
             torch.cuda.empty_cache()
             el3, m3 = timed_train("fp32", 64, 50, 5, dev, scope="bench_b64")
             out["config_1_batch64_fp32"] = {
@@ -474,7 +533,7 @@ def main():
                     args.roofline_batch, args.roofline_launches, dev, save=False)
                 out["fp32_step_roofline"] = fp32_step_roofline(args.roofline_batch,
                                                                args.roofline_launches, dev)
-        if args.cpu_baseline and world == 1:
+        if args.cpu_baseline and world == 1 and not asr:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if world > 1:

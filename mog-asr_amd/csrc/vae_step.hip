@@ -130,6 +130,7 @@ struct StepArgs {
   int x_period;             // image of row b is x[b % x_period] (all T steps in one launch)
   float lik_std, v_pm, v_pv, v_plv;
   int phases;               // profiling aid: bit mask of the phases to run (all by default)
+  int prio;                 // pipelined form: s_setprio of the S | W | M roles (4 bits each)
   long long* tstamp;        // profiling aid: per-block phase timestamps (or null)
 };
 
@@ -1031,6 +1032,12 @@ struct MBar {
 #define PSTAMP(k) \
   if (p.tstamp && (threadIdx.x & 63) == 0) p.tstamp[(size_t)blockIdx.x * 64 + (k)] = wall_clock64()
 
+__device__ __forceinline__ void set_prio(int v) {
+  if (v == 1) __builtin_amdgcn_s_setprio(1);
+  else if (v == 2) __builtin_amdgcn_s_setprio(2);
+  else if (v == 3) __builtin_amdgcn_s_setprio(3);
+}
+
 // ---- S role: the STN read of 8 images (m0 .. m0+7 of the tile) -> gb rows --
 // Lane (kk = lane & 31, h = lane >> 5) samples pixel 32 ks + kk of images
 // m0 + h + 2u, u < 4, gathers LA k-steps ahead (as the lockstep kernel's
@@ -1155,6 +1162,7 @@ __global__ __launch_bounds__(1024, 4) void stn_vae_pipe_kernel(StepArgs p, int n
   if (wv >= P_WS0) {
 #ifndef PIPE_SKIP_S
     // ------------------------------------------------------------ S role --
+    set_prio(p.prio & 15);
     const int sw = wv - P_WS0;
     float4* tab = reinterpret_cast<float4*>(lds + P_OFF_S + sw * P_STAB);
     float* th8 = reinterpret_cast<float*>(lds + P_OFF_S + sw * P_STAB + 8 * TABR * 16);
@@ -1180,6 +1188,7 @@ __global__ __launch_bounds__(1024, 4) void stn_vae_pipe_kernel(StepArgs p, int n
         }
         wave_lds_sync();
         const int tabo = P_OFF_S + sw * P_STAB;
+        if (!(p.phases & 1)) continue;  // profiling aid: no STN read
         // (the general-transform fallback, never taken by AIR's axis-aligned
         // theta, without gather lookahead: it would not fit the registers)
         if (sep) pipe_sample8<true, 3>(p, lds, tabo, th8, gdst, b0, nb, m0, tidv);
@@ -1223,6 +1232,7 @@ __global__ __launch_bounds__(1024, 4) void stn_vae_pipe_kernel(StepArgs p, int n
   if (wv >= P_WW0) {
 #ifndef PIPE_SKIP_W
     // ------------------------------------------------------------ W role --
+    set_prio((p.prio >> 4) & 15);
     const int ww = wv - P_WW0;
     unsigned char* slot = lds + P_OFF_W + ww * Ly::WSLOT;
     float* sRw = reinterpret_cast<float*>(slot);
@@ -1244,7 +1254,7 @@ __global__ __launch_bounds__(1024, 4) void stn_vae_pipe_kernel(StepArgs p, int n
         }
       };
       if (ww < nb) fetch(ww);
-      for (int m = ww; m < nb; m += P_NW) {
+      for (int m = ww; m < nb && (p.phases & 8); m += P_NW) {
         float th[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) th[k] = p.theta_b[(size_t)(b0 + m) * 6 + k];
@@ -1334,6 +1344,7 @@ __global__ __launch_bounds__(1024, 4) void stn_vae_pipe_kernel(StepArgs p, int n
   }
 
   // -------------------------------------------------------------- M role --
+  set_prio((p.prio >> 8) & 15);
   const bool save = p.a1b != nullptr;
   auto opaque = [](int v) {
     asm volatile("" : "+v"(v));
@@ -1597,6 +1608,8 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   const char* ph = getenv("MOG_VS_PHASES");
   p.phases = ph ? atoi(ph) : 31;
   if (!save) p.phases &= ~16;
+  p.prio = 0;
+  if (const char* e = getenv("MOG_VS_PRIO")) p.prio = (int)strtol(e, nullptr, 16);
   p.B = B; p.C = C; p.lik_std = lik_std; p.v_pm = v_pm; p.v_pv = v_pv; p.v_plv = v_plv;
   p.x_period = x_period > 0 ? x_period : B;
   hipStream_t s = mog_stream(stream);

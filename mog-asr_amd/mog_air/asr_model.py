@@ -313,7 +313,8 @@ class AIRModel(_AirBase):
         fix = -1 if self.fix_steps is None else int(self.fix_steps)
         w20 = self._w20()
         # loop-invariant x-projection of the inference LSTM (chain over x first)
-        gemm([X], [Ki[:C2]], [ws.Gx], B, 4 * H, C2, C2, 4 * H, 4 * H)
+        with self._timed("lstm_x_projection"):
+            gemm([X], [Ki[:C2]], [ws.Gx], B, 4 * H, C2, C2, 4 * H, 4 * H)
         relu_w = [self._N(n + "/kernel") for n in ("inf_shift/dense", "inf_shift/dense_2",
                                                    "z_pres/log_odds/dense")]
         relu_b = [self._N(n + "/bias") for n in ("inf_shift/dense", "inf_shift/dense_2",
@@ -473,10 +474,12 @@ class AIRModel(_AirBase):
         gKi = self._Kpad("infer_rnn_running/kernel", "grad")
         gKg = self._Kpad("gen_rnn_running/kernel", "grad")
         # LSTMCells: x rows from sum_t dG (the x input is loop-invariant)
-        if self.precision == "bf16":
-            self._x_grad_bf16(X, ws, gKi, G("infer_rnn_running/bias"), 0, C2)
-        else:
-            self._dw(X, ws.dGsum, gKi[:C2], B, C2, 4 * H, C2, 4 * H, G("infer_rnn_running/bias"))
+        with self._timed("lstm_x_projection_grad"):
+            if self.precision == "bf16":
+                self._x_grad_bf16(X, ws, gKi, G("infer_rnn_running/bias"), 0, C2)
+            else:
+                self._dw(X, ws.dGsum, gKi[:C2], B, C2, 4 * H, C2, 4 * H,
+                         G("infer_rnn_running/bias"))
         # M = LU (16-byte aligned LDS-DMA operands): rows Z+3+H.. of the
         # product land in the kernels' own pad rows (ParamStore pad), never in
         # a neighbouring variable's gradient

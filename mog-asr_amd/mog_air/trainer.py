@@ -92,15 +92,20 @@ class Dist:
         lo, hi = shard(len(k), self.rank, self.world)
         return x[lo:hi], k[lo:hi]
 
-    def mean(self, values, device):
-        """Mean over ranks of a few host scalars (one small all-reduce)."""
+    def mean(self, values, device, weight: float = 1.0):
+        """Weighted mean over ranks of a few host scalars (one small
+        all-reduce): each rank's values are per-image means over its shard, so
+        weighting by the shard size (``weight``) gives the global batch mean
+        even when the shards differ in size (a global batch that does not
+        divide by the world size)."""
         if self.world == 1:
             return list(values)
         import torch
         import torch.distributed as dist
-        t = torch.tensor(list(values), dtype=torch.float64, device=device)
+        t = torch.tensor([float(v) * weight for v in values] + [float(weight)],
+                         dtype=torch.float64, device=device)
         dist.all_reduce(t)
-        return (t / self.world).tolist()
+        return (t[:-1] / t[-1]).tolist()
 
     def barrier(self):
         if self.world > 1:
@@ -324,12 +329,13 @@ def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, mod
     digits = [int(c) for c in getattr(args, "dig_num", "")]
     vis_n = args.test_batch if getattr(args, "test_batch", 0) > 0 else len(test[1])
 
-    def save_images(tag, generations=True):
+    def save_images(tag, generations=True, gen_tag=None):
         if not ctx.main or getattr(args, "no_images", False):
             return
         from .visualize import save_visualizations
         save_visualizations(test_model, test[0][:vis_n], test[1][:vis_n], summary_folder, tag,
-                            digits=digits, num=NUM_IMAGES_TO_SAVE, generations=generations)
+                            digits=digits, num=NUM_IMAGES_TO_SAVE, generations=generations,
+                            gen_tag=gen_tag)
 
     log.info("Training...\n")
     try:
@@ -343,7 +349,8 @@ def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, mod
                 extra_log(train_model, step)
             hist.append([loss, acc, mse])
             if step % LOG_EACH_ITERATION == 0:
-                l0, l1, l2 = ctx.mean(np.mean(hist[-LOG_EACH_ITERATION:], axis=0), args.device)
+                l0, l1, l2 = ctx.mean(np.mean(hist[-LOG_EACH_ITERATION:], axis=0), args.device,
+                                      weight=len(k))
                 log.info("iteration {}\ttrain loss {:.3f}\ttrain accuracy {:.2f}, "
                          "train mse {:.3f}".format(step, l0, l1, l2))
                 if l0 < min_loss:
@@ -360,7 +367,9 @@ def train_loop(args, train_model, test_model, tr_x, tr_k, test, canvas, log, mod
                 raise StopIteration
     except StopIteration:
         test_and_log("final")
-        save_images("final")
+        # the final reconstruction / misclassified grids are tagged 'final',
+        # the final generation grids with the step (training_air_original.py:478-483)
+        save_images("final", gen_tag=step)
         log.info("Final Best: elbo:{}\taccu:{}\tmse:{}\tiou:{}".format(*best))
         log.info("\ntraining has ended\n")
     return step
@@ -427,11 +436,13 @@ def train_loop_asr(args, train_model, test_model, tr_x, tr_k, test, canvas, log,
                 logged.setdefault(n, []).append(v)
             if step % LOG_EACH_ITERATION == 0:
                 line = "step:{:6d}\t".format(step)
-                means = ctx.mean([np.mean(v) for v in logged.values()], args.device)
-                for (n, _), v in zip(logged.items(), means):
-                    if n == "TotLoss" and np.mean(v) < min_loss:
-                        min_loss, update_flag = float(np.mean(v)), True
-                    line += "{}:{:.4f}\t".format(n, np.mean(v))
+                # the global batch's means (shard-size weighted over ranks)
+                means = ctx.mean([np.mean(v) for v in logged.values()], args.device,
+                                 weight=len(k))
+                for n, v in zip(logged, means):
+                    if n == "TotLoss" and v < min_loss:
+                        min_loss, update_flag = float(v), True
+                    line += "{}:{:.4f}\t".format(n, v)
                 log.info(line)
                 logged = {}
             if step % TESET_EACH_ITERATION == 0:

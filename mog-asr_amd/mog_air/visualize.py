@@ -141,10 +141,11 @@ def generation_images(model, num_steps: int, zoom: int = 2):
 
 
 def save_visualizations(model, images, targets, folder: str, tag, digits=(), num: int = 60,
-                        generations: bool = True) -> None:
+                        generations: bool = True, gen_tag=None) -> None:
     """training_air_original.py:368-411 for one test batch: visualize_{tag}.png
     (first ``num``), visualize_{tag}_wrong.png (misclassified, up to 100) and,
-    per digit count i, visualize_gen{tag}_{i}.png / visualize_genbbox{tag}_{i}.png."""
+    per digit count i, visualize_gen{gen_tag}_{i}.png / visualize_genbbox{gen_tag}_{i}.png
+    (gen_tag defaults to tag; the final dump uses the step number there)."""
     model.infer(images, targets)
     allv = reconstruction_images(model, images)
     pile_image(allv[:num], os.path.join(folder, "visualize_{}.png".format(tag)))
@@ -156,5 +157,6 @@ def save_visualizations(model, images, targets, folder: str, tag, digits=(), num
         return
     for i in digits:
         gen, gen_box = generation_images(model, int(i))
-        pile_image(gen, os.path.join(folder, "visualize_gen{}_{}.png".format(tag, i)))
-        pile_image(gen_box, os.path.join(folder, "visualize_genbbox{}_{}.png".format(tag, i)))
+        gt = tag if gen_tag is None else gen_tag
+        pile_image(gen, os.path.join(folder, "visualize_gen{}_{}.png".format(gt, i)))
+        pile_image(gen_box, os.path.join(folder, "visualize_genbbox{}_{}.png".format(gt, i)))

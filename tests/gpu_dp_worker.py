@@ -5,7 +5,12 @@ contiguous shard of the batch through ``compute_gradients`` with
 ``parallel.attach`` installed (bucketed async all-reduce, global loop
 predicate, ASR batch-mean hook) and saves what it saw.
 
-usage: gpu_dp_worker.py <out_prefix> air|asr"""
+Kinds: air / asr (13 / 11 images: odd shards, the per-step VAE path) and
+air64 / air64b (128 images, 64-row shards, fp32 / bf16: the batched T*B-row
+VAE, the VAE weight gradients on the side stream joined before the bucket
+all-reduce -- the configuration bench.py and the trainer run).
+
+usage: gpu_dp_worker.py <out_prefix> air|asr|air64|air64b"""
 import os
 import sys
 
@@ -22,9 +27,12 @@ from mog_air import parallel  # noqa: E402
 DEV = "cuda:0"
 
 
-def air_case():
+BATCH = {"air": 13, "asr": 11, "air64": 128, "air64b": 128}
+
+
+def air_case(batch=13):
     from oracle import air_oracle as ao
-    cfg = ao.AirConfig(batch=13, max_steps=3, train=True, num_prior=(1, 3),
+    cfg = ao.AirConfig(batch=batch, max_steps=3, train=True, num_prior=(1, 3),
                        scale_prior_variance=0.05, z_pres_prior_log_odds=-0.01)
     P = ao.init_params(cfg, seed=71, bias_scale=0.05)
     nz = ao.make_noise(cfg, seed=72)
@@ -33,7 +41,7 @@ def air_case():
     return cfg, P, nz, x, k, G
 
 
-def air_model(cfg, P, world, scope):
+def air_model(cfg, P, world, scope, precision="fp32"):
     from mog_air.air_model import AIRModel
     m = AIRModel(max_steps=cfg.max_steps, canvas_size=cfg.canvas_size,
                  scale_prior_variance=cfg.scale_prior_variance,
@@ -42,7 +50,7 @@ def air_model(cfg, P, world, scope):
                  stopping_threshold=cfg.stopping_threshold,
                  vae_likelihood_std=cfg.vae_likelihood_std, learning_rate=1e-4,
                  gradient_clipping_norm=1.0, cnn=False, train=True, num_prior=cfg.num_prior,
-                 scope=scope, device=DEV, grad_world=world)
+                 scope=scope, device=DEV, grad_world=world, precision=precision)
     m.params.load_dict(P)
     return m
 
@@ -84,8 +92,12 @@ def asr_model(cfg, P, world, scope):
 
 def run(kind, lo, hi, world, scope, attach=True):
     """compute_gradients on images [lo, hi) of the case; returns a dict."""
-    cfg, P, nz, x, k, G = air_case() if kind == "air" else asr_case()
-    m = (air_model if kind == "air" else asr_model)(cfg, P, world, scope)
+    if kind == "asr":
+        cfg, P, nz, x, k, G = asr_case()
+        m = asr_model(cfg, P, world, scope)
+    else:
+        cfg, P, nz, x, k, G = air_case(BATCH[kind])
+        m = air_model(cfg, P, world, scope, "bf16" if kind == "air64b" else "fp32")
     reducer = None
     if attach and world > 1:
         reducer = parallel.attach(m, global_steps=True)
@@ -104,6 +116,7 @@ def run(kind, lo, hi, world, scope, attach=True):
         out["buckets"] = np.array(reducer.log)
     if kind == "asr":
         out["margin"] = m._ws.margin.cpu().numpy()
+    out["batched"] = np.array([int(getattr(m, "_batched_vae", lambda b: False)(hi - lo))])
     return out
 
 
@@ -112,7 +125,7 @@ def main():
     dist.init_process_group("gloo")
     try:
         rank, world = dist.get_rank(), dist.get_world_size()
-        n = 13 if kind == "air" else 11
+        n = BATCH[kind]
         lo, hi = parallel.shard(n, rank, world)
         res = run(kind, lo, hi, world, scope=f"dp_{kind}_{rank}")
         np.savez(f"{prefix}_{rank}.npz", lo=np.array([lo]), hi=np.array([hi]), **res)

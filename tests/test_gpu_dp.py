@@ -59,11 +59,16 @@ def _launch(prefix, kind):
     return [dict(np.load(f"{prefix}_{r}.npz")) for r in range(WORLD)]
 
 
-@pytest.mark.parametrize("kind", ["air", "asr"])
+@pytest.mark.parametrize("kind", ["air", "asr", "air64", "air64b"])
 def test_world2_matches_full_batch(tmp_path, kind):
+    """air64 / air64b: 64-row shards, so every rank takes the batched VAE
+    (T*B rows; bf16: the fused step kernel) with its weight gradients on the
+    side stream, joined before the glimpse bucket's all-reduce."""
     ranks = _launch(str(tmp_path / kind), kind)
-    n = 13 if kind == "air" else 11
+    n = W.BATCH[kind]
     full = W.run(kind, 0, n, 1, scope=f"dp_full_{kind}", attach=False)
+    if kind.startswith("air64"):
+        assert all(int(r["batched"][0]) for r in ranks) and int(full["batched"][0])
     # every rank holds the same reduced gradient
     np.testing.assert_array_equal(ranks[0]["g"], ranks[1]["g"])
     g, ref = ranks[0]["g"], full["g"]
@@ -77,7 +82,7 @@ def test_world2_matches_full_batch(tmp_path, kind):
         np.testing.assert_allclose(r["loss_b"], full["loss_b"][lo:hi], rtol=1e-6)
     # batch mean: the shards' local means weighted by their sizes
     sizes = [int(r["hi"][0] - r["lo"][0]) for r in ranks]
-    if kind == "air":
+    if kind != "asr":
         mean = sum(float(r["mean"][0]) * s for r, s in zip(ranks, sizes)) / n
         assert mean == pytest.approx(float(full["mean"][0]), rel=1e-5)
         # buckets: glimpse block, 3 x-grad chunks, the rest (5 launches)
