@@ -170,14 +170,9 @@ int mog_air_runloss(int T, int B, const float* rec, long rec_step_stride, const 
  * backward: gb/a1b/a2b/zb/d1b/d2b (bf16, zb row stride 56), mu/lv/z (fp32) --
  * a1b/a2b/zb/d1b/d2b/mu/lv NULL for a forward-only step (evaluation /
  * inference; z, the reported latents, is written when given); r (fp32) is
- * always written.  gb may be given in the forward-only form too: it is then
- * the glimpse workspace of the pipelined form (below), and without it a
- * forward-only step runs the lockstep form.
- * Two launch forms, bit-identical: lockstep (workgroups of 32 / 64 images,
- * every phase of a tile in sequence) and pipelined (B >= 64 x #CUs and gb
- * given: one persistent workgroup per CU, waves split into sampler / DMA /
- * MFMA / STN-write roles that run different 64-image tiles concurrently;
- * env MOG_VS_PIPE=0/1 overrides the choice).
+ * always written; in the forward-only form gb is not written either (it may
+ * be NULL).  Workgroups of 64 images (32 below B = 16,384),
+ * every phase of a tile in sequence on the whole CU.
  * Shapes must be the reference defaults (W 28, 512/256, Z 50, 256/512):
  * anything else returns MOG_ERR_INVALID.  Replaces the per-step sequence
  * air_model.py:523-588 (stn_forward + 6 GEMMs + vae_sample + stn accumulate).

@@ -869,7 +869,12 @@ void launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, co
     bool bk32 = ta || tb;
     if (bk_env != nullptr) bk32 = atoi(bk_env) == 32;
     if (bk32 && !b128) {
+      // MOG_GEMM_NS=3|4: deeper 32-deep pipelines (48 / 64 KB per workgroup)
+      static const char* ns_env = getenv("MOG_GEMM_NS");
+      const int ns = ns_env != nullptr ? atoi(ns_env) : 2;
       if (t12864) launch_dma<128, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
+      else if (ns == 4) launch_dma<64, 64, 32, 4>(ta, tb, epi, s, P, D, batch);
+      else if (ns == 3) launch_dma<64, 64, 32, 3>(ta, tb, epi, s, P, D, batch);
       else launch_dma<64, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
       return;
     }

@@ -130,7 +130,6 @@ struct StepArgs {
   int x_period;             // image of row b is x[b % x_period] (all T steps in one launch)
   float lik_std, v_pm, v_pv, v_plv;
   int phases;               // profiling aid: bit mask of the phases to run (all by default)
-  int prio;                 // pipelined form: s_setprio of the S | W | M roles (4 bits each)
   long long* tstamp;        // profiling aid: per-block phase timestamps (or null)
 };
 
@@ -256,11 +255,39 @@ struct LdsBarrier {
 };
 struct NoHook {
   __device__ __forceinline__ void operator()() const {}
+  __device__ __forceinline__ void step() {}
 };
 
-// Bar: the barrier SYNC uses (the whole workgroup, or the MFMA role of the
-// pipelined kernel); Hook: called by every participating wave right after its
-// last read of A (before the epilogue).
+// The LDS -> HBM copy of a saved activation (rows [nb] x NCOL of T, LDS row
+// stride lds) spread over the k loop of the NEXT dense layer: every k-step
+// each thread moves one 16-byte chunk (the waves wait on the weight stream
+// there), finish() moves what is left before that layer overwrites its input.
+template <class T, int NCOL, int NTHR>
+struct RowFlush {
+  static constexpr int V = 16 / sizeof(T), CPR = NCOL / V;
+  const T* s;
+  T* g;
+  int lds, ldg, total, i;
+  __device__ __forceinline__ RowFlush(const T* s_, int lds_, T* g_, int ldg_, int nb, bool on,
+                                      int tid)
+      : s(s_), g(g_), lds(lds_), ldg(ldg_), total(on ? nb * CPR : 0), i(tid) {}
+  __device__ __forceinline__ void step() {
+    if (i < total) {
+      const int m = i / CPR, c = i - (i / CPR) * CPR;
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(s + m * lds + c * V),
+                                  reinterpret_cast<u32x4*>(g + (size_t)m * ldg + c * V));
+      i += NTHR;
+    }
+  }
+  __device__ __forceinline__ void operator()() {
+    while (i < total) step();
+  }
+};
+
+// Bar: the barrier SYNC uses; Hook: step() once per k-step (a RowFlush
+// spreading the previous activation's copy over the k loop), operator() by
+// every participating wave right after its last read of A (before the
+// epilogue).
 template <int MT, int K, int N, int TPW, int D, bool SYNC, class Epi, class Bar = LdsBarrier,
           class Hook = NoHook>
 __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf16* __restrict__ W,
@@ -301,6 +328,7 @@ __device__ __forceinline__ void dense_tiles(const __bf16* A, int lda, const __bf
       for (int c = 0; c < TPW; ++c)
         acc[rt][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[c], acc[rt][c], 0, 0, 0);
     }
+    hook.step();
   };
   if (on) {
     if constexpr (KS < D) {
@@ -376,6 +404,98 @@ __device__ __forceinline__ void dense_rowsplit(const __bf16* A, int lda, const _
   epi(rt * 16 + g * 4 + (li & 3), ct * 16 + (li & ~3), quad_transpose(acc, tid), bq);
 }
 
+// The VAE output layer r = sigmoid(d2 Wgo + b + std * eps_x) (vae.py:44-46)
+// over column tiles tile_base + .. (dense_tiles' assignment, K = 512, N = 784)
+// with the likelihood noise produced INSIDE the k loop: the waves wait on the
+// weight stream there with the VALU idle, so each odd k-step computes one
+// Philox4x32-10 quad of eps_x (or loads the injected one) for an accumulator
+// tile of the lane -- the quads the epilogue needs after the quad transpose
+// (lane row g*4 + (li & 3), columns (li & ~3) .. +3: one quad).  Same
+// counters, same arithmetic as the epilogue form: bit-identical.
+template <int MT, int TPW, int D, class Hook = NoHook>
+__device__ __forceinline__ void dense_out(const __bf16* A, int lda, const StepArgs& p, int tile_base,
+                                          int wbase, int nw, int b0, int nb, int tid,
+                                          Hook hook = Hook{}) {
+#pragma clang fp contract(off)
+  constexpr int K = 512, N = W2, KS = K / 32, NCT = nct(N), NQ = MT * TPW;
+  static_assert(NQ <= KS, "one noise quad per k-step at most");
+  const int rot = (int)(blockIdx.x >> 3);
+  const int lane = tid & 63, w = (tid >> 6) - wbase;
+  const bool on = w >= 0 && w < nw;
+  const int li = lane & 15, g = lane >> 4;
+  int ct[TPW], wo[TPW];
+  const __amdgpu_buffer_rsrc_t wr = weight_rsrc(p.wt[6]);
+#pragma unroll
+  for (int c = 0; c < TPW; ++c) {
+    ct[c] = tile_base + (w + nw * c + rot) % (nw * TPW);
+    wo[c] = frag_voff(ct[c], lane);
+  }
+  floatx4 bq[TPW];
+#pragma unroll
+  for (int c = 0; c < TPW; ++c) bq[c] = on ? load_bias4(p.bias[6], ct[c] * 16 + (li & ~3), N) : floatx4{};
+  floatx4 acc[MT][TPW];
+#pragma unroll
+  for (int rt = 0; rt < MT; ++rt)
+#pragma unroll
+    for (int c = 0; c < TPW; ++c) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float ev[NQ][4];
+  auto noise = [&](int idx) {
+    const int rt = idx / TPW, c = idx - (idx / TPW) * TPW;
+    const int m = rt * 16 + g * 4 + (li & 3), n = ct[c] * 16 + (li & ~3);
+    const size_t q = (size_t)(b0 + m) * (W2 / 4) + (n >> 2);
+    if (p.eps_gen) {
+      mog_philox_quad(p.eps_seed, p.eps_offset + q, true, ev[idx]);
+    } else {
+      const float4 e4 = m < nb ? reinterpret_cast<const float4*>(p.eps_x)[q] : float4{};
+      ev[idx][0] = e4.x; ev[idx][1] = e4.y; ev[idx][2] = e4.z; ev[idx][3] = e4.w;
+    }
+  };
+  if (on) {
+    bf16x8 q[D][TPW];
+    auto loadB = [&](int ks, bf16x8* b) {
+#pragma unroll
+      for (int c = 0; c < TPW; ++c) b[c] = load_frag<NCT>(wr, wo[c], ks);
+    };
+#pragma unroll
+    for (int d = 0; d < D; ++d) loadB(d, q[d]);
+    static_for<0, KS>([&](auto kc) {
+      constexpr int ks = decltype(kc)::value;
+      const int k = ks * 32 + 8 * g;
+#pragma unroll
+      for (int rt = 0; rt < MT; ++rt) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&A[(rt * 16 + li) * lda + k]);
+#pragma unroll
+        for (int c = 0; c < TPW; ++c)
+          acc[rt][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, q[ks % D][c], acc[rt][c], 0, 0, 0);
+      }
+      if constexpr (ks + D < KS) loadB(ks + D, q[ks % D]);
+      if constexpr (ks % (KS / NQ) == KS / NQ - 1) noise(ks / (KS / NQ));
+      if constexpr (ks % 4 == 1) hook.step();  // (the rest of a flush: hook())
+    });
+  }
+  hook();
+  if (!on) return;
+  const float sd = p.lik_std;
+#pragma unroll
+  for (int c = 0; c < TPW; ++c)
+#pragma unroll
+    for (int rt = 0; rt < MT; ++rt) {
+      const int m = rt * 16 + g * 4 + (li & 3), n = ct[c] * 16 + (li & ~3);
+      const floatx4 v = quad_transpose(acc[rt][c], tid);
+      const float* e = ev[rt * TPW + c];
+      if (m < nb) {
+        float o[4];
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) {
+          const float y = __builtin_fmaf(e[kq], sd, v[kq] + bq[c][kq]);
+          o[kq] = mog_sigmoid_hw(y);
+        }
+        reinterpret_cast<float4*>(p.r)[(size_t)(b0 + m) * (W2 / 4) + (n >> 2)] =
+            make_float4(o[0], o[1], o[2], o[3]);
+      }
+    }
+}
+
 // LDS tile [nb][lds] -> HBM rows [nb][ldg] with 16-byte stores (ncols * sizeof(T) % 16 == 0).
 template <int NTHR, class T>
 __device__ __forceinline__ void flush_rows(const T* s, int lds, T* g, int ldg, int ncols, int nb,
@@ -433,7 +553,7 @@ __device__ __forceinline__ void glimpse_geom(const float4* tabR, const float* th
 // barrier per slab.  The samplers' gathers run LA k-steps ahead of the
 // samples (HBM latency).  A sampler lane samples pixel 32ks + (lane&31) of its
 // wave's images sw*M/8 + 2u + (lane>>5), u < M/16.
-template <int MT, int NW, bool SEP>
+template <int MT, int NW, bool SEP, int LA = 3>
 __device__ __forceinline__ void read_recognition(const StepArgs& p, unsigned char* arena,
                                                  const float (*sth)[12], int b0, int nb,
                                                  floatx4 (&acc)[MT][64 / NW], int (&ct)[64 / NW],
@@ -466,7 +586,6 @@ __device__ __forceinline__ void read_recognition(const StepArgs& p, unsigned cha
     // reach of a DS instruction's offset field).
     const int tabo = mw * TABR * 16;                       // the lane's first table
     const int kbo = Ly::TAB + (mw * SK + kk) * 2;          // its first sample in slab 0
-    constexpr int LA = 3;
     float I[LA][NU][4];
     auto gather = [&](int ks, float (&I)[NU][4]) {
       const int k = 32 * ks + kk;
@@ -603,7 +722,7 @@ __device__ __forceinline__ void read_recognition(const StepArgs& p, unsigned cha
   }
 }
 
-template <int MT, int NW, int OCC>
+template <int MT, int NW, int OCC, int LA = 3>
 __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) {
 #pragma clang fp contract(off)
   using Ly = Lay<MT, NW>;
@@ -667,8 +786,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
     floatx4 acc[MT][TW];
     int ct[TW];
     floatx4 b1q[TW];
-    if (all_sep) read_recognition<MT, NW, true>(p, arena, sth, b0, nb, acc, ct, b1q);
-    else read_recognition<MT, NW, false>(p, arena, sth, b0, nb, acc, ct, b1q);
+    if (all_sep) read_recognition<MT, NW, true, LA>(p, arena, sth, b0, nb, acc, ct, b1q);
+    else read_recognition<MT, NW, false, 3>(p, arena, sth, b0, nb, acc, ct, b1q);
     STAMP(1);
     __bf16* sA1 = reinterpret_cast<__bf16*>(arena);
     const int li = lane & 15, g = lane >> 4;
@@ -687,18 +806,26 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   STAMP(2);
   __bf16* sA1 = reinterpret_cast<__bf16*>(arena);
   __bf16* sA2 = sA1;
-  if (p.phases & 16) flush_rows<NTHR>(sA1, S512, p.a1b + (size_t)b0 * 512, 512, 512, nb);
   // ---- 3. a2 = softplus(a1 W2 + b2)  [M x 256], in place ------------------
-  if (p.phases & 2) {
-    dense_tiles<MT, 512, 256, 16 / NW, 4, true>(sA1, S512, p.wt[1], p.bias[1], 0, 0, NW,
-                                     [&](int m, int n0, const floatx4& v, const floatx4& b) {
-                                       store_softplus4(sA2 + m * S256 + n0, v, b);
-                                     });
+  // (a1's saved copy is flushed inside the k loop, finished before the
+  // in-place epilogue)
+  {
+    RowFlush<__bf16, 512, NTHR> fl(sA1, S512, p.a1b + (size_t)b0 * 512, 512, nb,
+                                   (p.phases & 16) != 0, tid);
+    if (p.phases & 2) {
+      dense_tiles<MT, 512, 256, 16 / NW, 4, true>(sA1, S512, p.wt[1], p.bias[1], 0, 0, NW,
+                                       [&](int m, int n0, const floatx4& v, const floatx4& b) {
+                                         store_softplus4(sA2 + m * S256 + n0, v, b);
+                                       },
+                                       LdsBarrier{}, fl);
+    } else {
+      fl();
+    }
   }
   lds_barrier();
   STAMP(3);
-  if (p.phases & 16) flush_rows<NTHR>(sA2, S256, p.a2b + (size_t)b0 * 256, 256, 256, nb);
-  // ---- 4. mu | lv = a2 W + b  [M x 50] fp32 (waves 0-3 | 4-7) -------------
+  // ---- 4. mu | lv = a2 W + b  [M x 50] fp32 (waves 0-3 | 4-7; the others --
+  // flush a2's saved copy meanwhile)
   float* sMu = reinterpret_cast<float*>(arena + Ly::OFF_MU);
   float* sLv = reinterpret_cast<float*>(arena + Ly::OFF_LV);
   if (p.phases & 2) {
@@ -709,8 +836,17 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
           if (n0 + k < 50) dst[m * 50 + n0 + k] = v[k] + b[k];
       };
     };
-    dense_tiles<MT, 256, 50, 1, 4, false>(sA2, S256, p.wt[2], p.bias[2], 0, 0, 4, epi_f32(sMu));
-    dense_tiles<MT, 256, 50, 1, 4, false>(sA2, S256, p.wt[3], p.bias[3], 0, 4, 4, epi_f32(sLv));
+    if (wv < 8) {
+      dense_tiles<MT, 256, 50, 1, 4, false>(sA2, S256, p.wt[2], p.bias[2], 0, 0, 4, epi_f32(sMu));
+      dense_tiles<MT, 256, 50, 1, 4, false>(sA2, S256, p.wt[3], p.bias[3], 0, 4, 4, epi_f32(sLv));
+    }
+  }
+  if (p.phases & 16) {
+    if (NW == 16 && (p.phases & 2)) {
+      if (wv >= 8) flush_rows<NTHR / 2>(sA2, S256, p.a2b + (size_t)b0 * 256, 256, 256, nb, tid - NTHR / 2);
+    } else {
+      flush_rows<NTHR>(sA2, S256, p.a2b + (size_t)b0 * 256, 256, 256, nb);
+    }
   }
   lds_barrier();
   STAMP(4);
@@ -772,19 +908,26 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   }
   lds_barrier();
   STAMP(6);
-  if (p.phases & 16) flush_rows<NTHR>(sD1, S256, p.d1b + (size_t)b0 * 256, 256, 256, nb);
-  // ---- 7. d2 = softplus(d1 Wg2 + b)  [M x 512] at 0 (in place over d1) -----
+  // ---- 7. d2 = softplus(d1 Wg2 + b)  [M x 512] at 0 (in place over d1; d1's
+  // saved copy flushed inside the k loop) ---------------------------------------
   __bf16* sD2 = reinterpret_cast<__bf16*>(arena);
-  if (p.phases & 2) {
-    dense_tiles<MT, 256, 512, 32 / NW, NW / 4, true>(sD1, S256, p.wt[5], p.bias[5], 0, 0, NW,
-                                     [&](int m, int n0, const floatx4& v, const floatx4& b) {
-                                       store_softplus4(sD2 + m * S512 + n0, v, b);
-                                     });
+  {
+    RowFlush<__bf16, 256, NTHR> fl(sD1, S256, p.d1b + (size_t)b0 * 256, 256, nb,
+                                   (p.phases & 16) != 0, tid);
+    if (p.phases & 2) {
+      dense_tiles<MT, 256, 512, 32 / NW, NW / 4, true>(sD1, S256, p.wt[5], p.bias[5], 0, 0, NW,
+                                       [&](int m, int n0, const floatx4& v, const floatx4& b) {
+                                         store_softplus4(sD2 + m * S512 + n0, v, b);
+                                       },
+                                       LdsBarrier{}, fl);
+    } else {
+      fl();
+    }
   }
   lds_barrier();
   STAMP(7);
-  if (p.phases & 16) flush_rows<NTHR>(sD2, S512, p.d2b + (size_t)b0 * 512, 512, 512, nb);
   // ---- 8. r = sigmoid(d2 Wgo + b + std eps)  [M x 784] fp32 -> HBM ----------
+  // (d2's saved copy flushed inside the first pass's k loop)
   // The 4 x 4 accumulator quads are transposed across lanes (two DPP quad
   // exchanges) so that a lane owns four consecutive pixels of one row: one
   // Philox quad of eps_x (generated in-kernel exactly as mog_rng_fill would,
@@ -811,8 +954,15 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
         reinterpret_cast<float4*>(p.r)[q] = make_float4(o[0], o[1], o[2], o[3]);
       }
     };
-    dense_tiles<MT, 512, W2, 32 / NW, 8, false>(sD2, S512, p.wt[6], p.bias[6], 0, 0, NW, epi);
-    dense_tiles<MT, 512, W2, 16 / NW, 8, false>(sD2, S512, p.wt[6], p.bias[6], 32, 0, NW, epi);
+    RowFlush<__bf16, 512, NTHR> fl(sD2, S512, p.d2b + (size_t)b0 * 512, 512, nb,
+                                   (p.phases & 16) != 0, tid);
+    if constexpr (MT == 4) {
+      dense_out<MT, 32 / NW, 4>(sD2, S512, p, 0, 0, NW, b0, nb, tid, fl);
+    } else {  // (the 32-image forms: the hook would not fit their registers)
+      fl();
+      dense_out<MT, 32 / NW, 4>(sD2, S512, p, 0, 0, NW, b0, nb, tid);
+    }
+    dense_out<MT, 16 / NW, 4>(sD2, S512, p, 32, 0, NW, b0, nb, tid);
     dense_rowsplit<MT, 512, W2>(sD2, S512, p.wt[6], p.bias[6], 48, epi);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // r stores done before other waves read it
@@ -827,14 +977,13 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   // is stored and recorded.
   if (p.phases & 8) {
     // Wave-private: wave wv writes images wv, wv + NW, ... from its own LDS
-    // slot (r of one image + its write tables); the next image's r is
+    // slot (r of one image); the next image's r is
     // fetched into registers while the current one is computed, and the
     // waves meet no workgroup barrier, so their memory and VALU phases drift
     // apart and overlap.
     const bool vec = (C2 & 3) == 0;  // even C: 16-byte aligned image rows of parts
     unsigned char* slot = arena + wv * Ly::WSLOT;
     float* sRw = reinterpret_cast<float*>(slot);
-    float4* tabw = reinterpret_cast<float4*>(slot + W2 * 4);
     constexpr int NQ = (W2 / 4 + 63) / 64;
     float4 tmp[NQ];
     auto fetch = [&](int m) {
@@ -852,17 +1001,11 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
         const int i = lane + it * 64;
         if (i < W2 / 4) reinterpret_cast<float4*>(sRw)[i] = tmp[it];
       }
-      if (C <= CTAB_MAX)
-        for (int i = lane; i < 2 * C; i += 64)
-          tabw[i] = i < C ? axis4(axis_col(&sth[m][6], 28, 28, C, C, i), 4)
-                          : axis4(axis_row(&sth[m][6], 28, 28, C, C, i - C), 4 * 28);
       wave_lds_sync();
       if (m + NW < nb) fetch(m + NW);
       float* om = p.part + (size_t)(b0 + m) * C2;
       float4* om4 = reinterpret_cast<float4*>(om);
       const float* U = sRw;
-      const float4* tcol = tabw;
-      const float4* trow = tabw + C;
       const bool act = smask[m] != 0, tab = (ssep[m] & 2) != 0;
       const float zn = szv[m];
       if (!act) {  // inactive: the whole part is +0 -- nothing stored
@@ -872,49 +1015,51 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
         // with coinciding corner rows samples exactly +0 at every column:
         // the y weights are exact negatives on one source row, and within
         // a live row no sample is dead): store the even-aligned range
-        // [rlo, rhi) of such rows and record it.
-        const float4 el = trow[lane < C ? lane : 0];
+        // [rlo, rhi) of such rows and record it.  Lane i holds row entry i
+        // in registers; a pass reads rows r, r + 1 with readlane.
+        const float4 el = axis4(axis_row(&sth[m][6], 28, 28, C, C, lane < C ? lane : 0), 4 * 28);
         const unsigned long long lm =
             __builtin_amdgcn_ballot_w64(lane < C && __float_as_int(el.x) != __float_as_int(el.y));
         const int rlo = lm ? (__builtin_ctzll(lm) & ~1) : 0;
         const int rhi = lm ? min(C, (64 - __builtin_clzll(lm) + 1) & ~1) : 0;
         if (lane == 0) p.part_rows[b0 + m] = rlo | (rhi << 16);
-        // Pixel pairs of the range, flattened over the wave: a lane reads
-        // its row entry and two column entries, gathers 8 corners from the
-        // staged r, computes both samples with packed fp32 ops (the same
-        // products and summation order as sample4, per pixel) and stores
-        // 8 bytes.
-        // The pair index idx = rr * PR + pr is walked incrementally (no
-        // per-iteration division) and the store address is linear in it:
-        // row * C + 2 pr = rlo * C + 2 idx.
-        const int PR = C >> 1;  // pairs per row
-        const int np = (rhi - rlo) * PR;
-        const int dq = 64 / PR, dr = 64 - dq * PR;
-        int rr = lane / PR, pr = lane - (lane / PR) * PR;
+        // Lane -> pixel pair pr of row r + half (PR pairs per row, two rows
+        // per pass; C = 50 leaves 14 lanes idle): the column geometry stays
+        // in registers, and a corner pair (x0, x0 + 1) of a source row is
+        // one ds_read2 -- a live column has x1 = x0 + 1, a dead one x1 = x0
+        // (its second corner is the first).  Same products and summation
+        // order as sample4, per pixel.
+        const int PR = C >> 1, half = lane >= PR ? 1 : 0, pr = lane - half * PR;
+        const bool on = lane < 2 * PR;
+        const float4 e0 = axis4(axis_col(&sth[m][6], 28, 28, C, C, on ? 2 * pr : 0), 4);
+        const float4 e1 = axis4(axis_col(&sth[m][6], 28, 28, C, C, on ? 2 * pr + 1 : 0), 4);
+        const int a0 = __float_as_int(e0.x), a1 = __float_as_int(e1.x);
+        const bool dd0 = a0 == __float_as_int(e0.y), dd1 = a1 == __float_as_int(e1.y);
         typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 xz = {e0.z, e1.z}, xw = {e0.w, e1.w};
         const char* Ub = reinterpret_cast<const char*>(sRw);
         auto ld = [Ub](int a, int b) { return *reinterpret_cast<const float*>(Ub + a + b); };
-        f2* dst = reinterpret_cast<f2*>(om + rlo * C) + lane;
-#pragma unroll 2
-        for (int idx = lane; idx < np; idx += 64) {
-          const float4 ey = trow[rlo + rr];
-          const float4 e0 = tcol[2 * pr], e1 = tcol[2 * pr + 1];
-          const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
-          const int a0 = __float_as_int(e0.x), c0 = __float_as_int(e0.y);
-          const int a1 = __float_as_int(e1.x), c1 = __float_as_int(e1.y);
-          const f2 Ia = {ld(y0, a0), ld(y0, a1)}, Ib = {ld(y1, a0), ld(y1, a1)};
-          const f2 Ic = {ld(y0, c0), ld(y0, c1)}, Id = {ld(y1, c0), ld(y1, c1)};
-          const f2 xz = {e0.z, e1.z}, xw = {e0.w, e1.w};
-          const f2 wa = xz * ey.z, wb = xz * ey.w, wc = xw * ey.z, wd = xw * ey.w;
-          const f2 sv = ((wa * Ia + wb * Ib) + wc * Ic) + wd * Id;
-          st_stream(dst, zn * sv);
-          dst += 64;
-          pr += dr;
-          rr += dq;
-          if (pr >= PR) {
-            pr -= PR;
-            ++rr;
+        f2* dst = reinterpret_cast<f2*>(om + (rlo + half) * C) + pr;
+        const int eyx = __float_as_int(el.x), eyy = __float_as_int(el.y);
+        const int eyz = __float_as_int(el.z), eyw = __float_as_int(el.w);
+        for (int r = rlo; r < rhi; r += 2) {
+          // (readlane takes a uniform lane: both rows' entries, then select)
+          const int y0a = __builtin_amdgcn_readlane(eyx, r), y0b = __builtin_amdgcn_readlane(eyx, r + 1);
+          const int y1a = __builtin_amdgcn_readlane(eyy, r), y1b = __builtin_amdgcn_readlane(eyy, r + 1);
+          const int za = __builtin_amdgcn_readlane(eyz, r), zb = __builtin_amdgcn_readlane(eyz, r + 1);
+          const int wa_ = __builtin_amdgcn_readlane(eyw, r), wb_ = __builtin_amdgcn_readlane(eyw, r + 1);
+          const int y0 = half ? y0b : y0a, y1 = half ? y1b : y1a;
+          const float ez = __int_as_float(half ? zb : za), ew = __int_as_float(half ? wb_ : wa_);
+          if (on) {
+            const f2 Ia = {ld(y0, a0), ld(y0, a1)}, Ib = {ld(y1, a0), ld(y1, a1)};
+            const f2 In = {ld(y0, a0 + 4), ld(y0, a1 + 4)}, Jn = {ld(y1, a0 + 4), ld(y1, a1 + 4)};
+            const f2 Ic = {dd0 ? Ia.x : In.x, dd1 ? Ia.y : In.y};
+            const f2 Id = {dd0 ? Ib.x : Jn.x, dd1 ? Ib.y : Jn.y};
+            const f2 wa = xz * ez, wb = xz * ew, wc = xw * ez, wd = xw * ew;
+            const f2 sv = ((wa * Ia + wb * Ib) + wc * Ic) + wd * Id;
+            st_stream(dst, zn * sv);
           }
+          dst += C;  // two rows of C / 2 pairs
         }
       } else {  // general transform or odd C: per-pixel geometry, flat order
         if (lane == 0) p.part_rows[b0 + m] = C << 16;
@@ -945,625 +1090,6 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   }
 }
 
-// ===========================================================================
-// Pipelined persistent form.  The lockstep kernel above runs each 64-image
-// tile's phases in sequence on the whole CU, so a launch pays the SUM of its
-// phases' bottlenecks (gather latency, the L2 weight stream, the canvas-part
-// stores).  Here one 16-wave workgroup per CU loops over its tiles and the
-// waves are split by ROLE, each role a stage of a software pipeline over the
-// tiles, handing work on through LDS counters (no workgroup barrier after the
-// prologue):
-//   S (waves 12-15): STN read of tile j+1 -> bf16 glimpse rows to HBM (the
-//       saved activation `gb`, or a workspace in the forward-only form);
-//   D (wave 11):     LDS-DMA of tile j's glimpse, k-slab by k-slab, into a
-//       3-slot ring (buffer_load ... lds: no registers, 16-B chunks swizzled
-//       so the MFMA A-fragment reads are bank-conflict free);
-//   M (waves 0-7):   the seven dense layers of tile j on MFMA (the same k-
-//       ordered chains and epilogues as the lockstep kernel: bit-identical),
-//       r to HBM;
-//   W (waves 8-10):  STN write of tile j-1's canvas parts from r.
-// So the weight stream (M), the gathers (S) and the part stores (W) overlap
-// instead of alternating.  Counters are monotonic; a role waits for a count
-// with a bounded spin (a missed count reports through `err` and the wave
-// moves on: no wave can hang the GPU).
-constexpr int PT = 64;                       // images per tile
-constexpr int P_NM = 8, P_NW = 3, P_NS = 4;  // MFMA, STN-write, sampler waves (+1 DMA wave)
-constexpr int P_WW0 = P_NM, P_WD = P_NM + P_NW, P_WS0 = P_WD + 1;
-static_assert(P_WS0 + P_NS == 16, "16 waves");
-constexpr int P_KG = 5, P_NSLAB = KS1 / P_KG;  // recognition k-steps per ring slab, slabs per tile
-constexpr int P_SLAB = P_KG * PT * 64;         // ring slab bytes: [k-step][row][4 x 16 B]
-constexpr int P_RING = 3;
-// M's activation arena: a1 at 0, a2 in place, mu | lv behind a2, kl | z at 0
-// (Lay<4, 16> offsets), d1 behind a1's extent and d2 at 0, so g2 needs no
-// in-place barrier (two light passes).  The ring overlays the arena (dead
-// from the a1 epilogue to the next tile's L1).
-constexpr int P_D1 = Lay<4, 16>::A1;
-constexpr int P_ARENA = cmax(P_D1 + Lay<4, 16>::A2, P_RING * P_SLAB);
-constexpr int P_STAB = 8 * TABR * 16 + 8 * 8 * 4;  // S: read tables + theta of 8 images per wave
-constexpr int P_OFF_W = P_ARENA, P_OFF_S = P_OFF_W + P_NW * Lay<4, 16>::WSLOT;
-constexpr int P_LDS = P_OFF_S + P_NS * P_STAB;
-enum { F_SDONE, F_FILLED, F_CONSUMED, F_ARENA, F_RDONE, F_MBAR, F_N };
-
-// A-fragment chunk swizzle of a ring slab: 16-B chunk c of row r sits at
-// position c ^ pswz(r); over ds_read_b128's 16-lane groups rows r & 15 and the
-// chunk index g = lane >> 4 then hit 16 distinct 4-bank groups.
-__device__ __forceinline__ int pswz(int r) { return (4 - ((r >> 2) & 3)) & 3; }
-
-// a value the compiler cannot see through (keeps per-iteration recomputation
-// of lane-derived addresses inside the persistent tile loops)
-__device__ __forceinline__ int opq(int v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-
-__device__ __forceinline__ unsigned lds_load_acq(unsigned* f) {
-  return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// wait until *f >= v (wave-uniform); bounded
-__device__ __forceinline__ void wait_ge(unsigned* f, unsigned v, int* err, int code) {
-  if (lds_load_acq(f) >= v) return;
-  for (int n = 0;; ++n) {
-    __builtin_amdgcn_s_sleep(2);
-    if (lds_load_acq(f) >= v) return;
-    if (n == (1 << 21)) {  // ~0.1 s: a miscount, never a real wait
-      if (err && (threadIdx.x & 63) == 0) err[0] = code;
-      return;
-    }
-  }
-}
-// lane 0 adds 1 once this wave's earlier LDS and global operations completed
-__device__ __forceinline__ void signal_add(unsigned* f) {
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(f, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// barrier of the M role's 8 waves (LDS hand-offs between its layers)
-struct MBar {
-  unsigned* f;
-  unsigned* gen;  // per-wave generation (a register of the caller)
-  int* err;
-  __device__ __forceinline__ void operator()() const {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    *gen += P_NM;
-    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(f, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    wait_ge(f, *gen, err, 6);
-  }
-};
-
-#define PSTAMP(k) \
-  if (p.tstamp && (threadIdx.x & 63) == 0) p.tstamp[(size_t)blockIdx.x * 64 + (k)] = wall_clock64()
-
-__device__ __forceinline__ void set_prio(int v) {
-  if (v == 1) __builtin_amdgcn_s_setprio(1);
-  else if (v == 2) __builtin_amdgcn_s_setprio(2);
-  else if (v == 3) __builtin_amdgcn_s_setprio(3);
-}
-
-// ---- S role: the STN read of 8 images (m0 .. m0+7 of the tile) -> gb rows --
-// Lane (kk = lane & 31, h = lane >> 5) samples pixel 32 ks + kk of images
-// m0 + h + 2u, u < 4, gathers LA k-steps ahead (as the lockstep kernel's
-// samplers; LA k-steps of gathers in flight, the last LA-1 ahead).  Table addresses go through an opaque per-k-step base so the
-// compiler re-reads the tables instead of hoisting 25 k-steps of them.
-template <bool SEP, int LA>
-__device__ __forceinline__ void pipe_sample8(const StepArgs& p, unsigned char* lds, int tabo,
-                                             const float* th8, __bf16* gdst, int b0, int nb,
-                                             int m0, int tid) {
-#pragma clang fp contract(off)
-  constexpr int NU = 4;
-  const int lane = tid & 63, kk = lane & 31, h = lane >> 5;
-  const int C = p.C, C2 = C * C;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(p.x) + (size_t)(b0 % p.x_period) * C2, 0, nb * C2 * 4, 0x00020000);
-  auto opaque = [](int v) {
-    asm volatile("" : "+v"(v));
-    return v;
-  };
-  const int tb = tabo + h * TABR * 16;  // the lane's first table
-  float I[LA][NU][4];
-  auto gather = [&](int ks, float (&I)[NU][4]) {
-    const int k = 32 * ks + kk;
-    const int i = min(k / 28, 27), j = k - (k / 28) * 28;
-    const float4* tc = reinterpret_cast<const float4*>(lds + opaque(tb + j * 16));
-    const float4* tr = reinterpret_cast<const float4*>(lds + opaque(tb + (28 + i) * 16));
-    int xo = (m0 + h) * C2 * 4;
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      float4 ex, ey;
-      if constexpr (SEP) {
-        ex = tc[2 * u * TABR];
-        ey = tr[2 * u * TABR];
-      } else {
-        glimpse_geom<false>(nullptr, th8 + (h + 2 * u) * 8, 0, k, C, ex, ey);
-      }
-      const int xb = __float_as_int(ex.x) + xo;
-      const u32x2 r0 = __builtin_amdgcn_raw_buffer_load_b64(xr, xb + __float_as_int(ey.x), 0, 0);
-      const u32x2 r1 = __builtin_amdgcn_raw_buffer_load_b64(xr, xb + __float_as_int(ey.y), 0, 0);
-      I[u][0] = __uint_as_float(r0[0]);
-      I[u][1] = __uint_as_float(r0[1]);
-      I[u][2] = __uint_as_float(r1[0]);
-      I[u][3] = __uint_as_float(r1[1]);
-      xo += 2 * C2 * 4;
-    }
-  };
-  auto sample = [&](int ks, const float (&I)[NU][4]) {
-    const int k = 32 * ks + kk;
-    const int i = min(k / 28, 27), j = k - (k / 28) * 28;
-    asm volatile("" ::: "memory");  // re-read the tables instead of keeping them live
-    const float4* tc = reinterpret_cast<const float4*>(lds + opaque(tb + j * 16));
-    const float4* tr = reinterpret_cast<const float4*>(lds + opaque(tb + (28 + i) * 16));
-    __bf16* gd = gdst + (size_t)(m0 + h) * W2 + k;
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int m = m0 + h + 2 * u;
-      float4 ex, ey;
-      if constexpr (SEP) {
-        ex = tc[2 * u * TABR];
-        ey = tr[2 * u * TABR];
-      } else {
-        glimpse_geom<false>(nullptr, th8 + (h + 2 * u) * 8, 0, k, C, ex, ey);
-      }
-      const int fl = __float_as_int(ex.y);
-      const float Ia = (fl & 1) ? I[u][1] : I[u][0], Ib = (fl & 1) ? I[u][3] : I[u][2];
-      const float Ic = (fl & 2) ? I[u][1] : I[u][0], Id = (fl & 2) ? I[u][3] : I[u][2];
-      const int xlive = (fl ^ (fl >> 1)) & 1;
-      const int ylive = __float_as_int(ey.x) != __float_as_int(ey.y) ? 1 : 0;
-      const float v = sample4(ex, ey, Ia, Ib, Ic, Id);
-      if (k < W2 && m < nb) gd[(size_t)(2 * u) * W2] = (__bf16)((xlive | ylive) ? v : 0.0f);
-    }
-  };
-  if constexpr (LA == 1) {
-#pragma unroll 1
-    for (int ks = 0; ks < KS1; ++ks) {
-      gather(ks, I[0]);
-      sample(ks, I[0]);
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < LA; ++k) gather(k, I[k]);
-    static_for<0, KS1>([&](auto kc) {
-      constexpr int ks = decltype(kc)::value;
-      sample(ks, I[ks % LA]);
-      if constexpr (ks + LA < KS1) gather(ks + LA, I[ks % LA]);
-    });
-  }
-}
-
-// ---- D role: LDS-DMA of glimpse slab s of a tile into ring slot `slot` -----
-__device__ __forceinline__ void pipe_dma_slab(__amdgpu_buffer_rsrc_t gr, unsigned char* ring,
-                                              int slot, int s, int tid) {
-  const int lane = tid & 63;
-  const int row_l = lane >> 2, pos = lane & 3;
-  const int c = pos ^ pswz(row_l);
-#pragma unroll
-  for (int q = 0; q < P_KG * 4; ++q) {
-    const int ks = P_KG * s + q / 4, row = 16 * (q & 3) + row_l;
-    const int k = ks * 32 + c * 8;
-    const int off = k < W2 ? row * (W2 * 2) + k * 2 : 0x7ffffff0;  // k >= 784 reads 0
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(
-        gr, (__attribute__((address_space(3))) void*)(ring + slot * P_SLAB + (q / 4) * 4096 + (q & 3) * 1024),
-        16, off, 0, 0, 0);
-  }
-}
-
-__global__ __launch_bounds__(1024, 4) void stn_vae_pipe_kernel(StepArgs p, int ntiles, __bf16* gbuf,
-                                                               int* err) {
-#pragma clang fp contract(off)
-  using Ly = Lay<4, 16>;
-  constexpr int M = PT, MT = 4, NTHR = P_NM * 64;
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[P_LDS];
-  __shared__ unsigned flags[8];
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int C = p.C, C2 = C * C;
-  if (threadIdx.x < 8) flags[threadIdx.x] = 0;
-  __syncthreads();  // the only workgroup barrier
-  PSTAMP(48);
-  unsigned char* arena = lds;
-  auto tile_of = [&](int jl) { return (int)blockIdx.x + jl * (int)gridDim.x; };
-
-  if (wv >= P_WS0) {
-#ifndef PIPE_SKIP_S
-    // ------------------------------------------------------------ S role --
-    set_prio(p.prio & 15);
-    const int sw = wv - P_WS0;
-    float4* tab = reinterpret_cast<float4*>(lds + P_OFF_S + sw * P_STAB);
-    float* th8 = reinterpret_cast<float*>(lds + P_OFF_S + sw * P_STAB + 8 * TABR * 16);
-    for (int jl = 0; tile_of(jl) < ntiles; ++jl) {
-      const int b0 = tile_of(jl) * M, nb = min(M, p.B - b0);
-      const int tidv = opq(threadIdx.x), lane = tidv & 63;  // per tile: nothing lane-derived is hoisted
-      if (jl < 4) PSTAMP(jl * 2);
-      __bf16* gdst = gbuf + (size_t)b0 * W2;
-#pragma unroll 1
-      for (int pass = 0; pass < 2; ++pass) {
-        const int m0 = sw * 16 + pass * 8;
-        if (lane < 64) {  // theta of the 8 images (stride 8), 0 past the batch
-          const int lt = lane >> 3, k = lane & 7;
-          th8[lane] = (k < 6 && m0 + lt < nb) ? p.theta_f[(size_t)(b0 + m0 + lt) * 6 + k] : 0.0f;
-        }
-        wave_lds_sync();
-        const bool sep = __builtin_amdgcn_ballot_w64(lane < 8 && !stn_separable(th8 + lane * 8)) == 0;
-        for (int i = lane; i < 8 * TABR; i += 64) {
-          const int lt = i / TABR, n = i - lt * TABR;
-          const float* th = th8 + lt * 8;
-          tab[i] = n < 28 ? col_pair4(axis_col(th, C, C, 28, 28, n), C)
-                          : axis4(axis_row(th, C, C, 28, 28, n - 28), 4 * C);
-        }
-        wave_lds_sync();
-        const int tabo = P_OFF_S + sw * P_STAB;
-        if (!(p.phases & 1)) continue;  // profiling aid: no STN read
-        // (the general-transform fallback, never taken by AIR's axis-aligned
-        // theta, without gather lookahead: it would not fit the registers)
-        if (sep) pipe_sample8<true, 3>(p, lds, tabo, th8, gdst, b0, nb, m0, tidv);
-        else pipe_sample8<false, 1>(p, lds, tabo, th8, gdst, b0, nb, m0, tidv);
-        wave_lds_sync();  // the tables are rewritten by the next pass
-      }
-      signal_add(&flags[F_SDONE]);  // this wave's glimpse rows of the tile are in memory
-      if (jl < 4) PSTAMP(jl * 2 + 1);
-    }
-#endif
-    return;
-  }
-
-  if (wv == P_WD) {
-    // ------------------------------------------------------------ D role --
-    const int lane = threadIdx.x & 63;
-    unsigned n = 0;  // slabs issued so far (over all tiles)
-    for (int jl = 0; tile_of(jl) < ntiles; ++jl) {
-      const int b0 = tile_of(jl) * M, nb = min(M, p.B - b0);
-      const __amdgpu_buffer_rsrc_t gr =
-          __builtin_amdgcn_make_buffer_rsrc(gbuf + (size_t)b0 * W2, 0, nb * W2 * 2, 0x00020000);
-      wait_ge(&flags[F_SDONE], P_NS * (jl + 1), err, 1);  // the tile's glimpse is complete
-      wait_ge(&flags[F_ARENA], P_NM * jl, err, 2);        // tile jl-1 no longer reads the arena
-#pragma unroll
-      for (int s = 0; s < P_NSLAB; ++s, ++n) {
-        // slot n % 3 was slab n-3's: every M wave has consumed it
-        if (s >= P_RING) wait_ge(&flags[F_CONSUMED], P_NM * (n - P_RING + 1), err, 3);
-        pipe_dma_slab(gr, arena, n % P_RING, s, opq(threadIdx.x));
-        if (s > 0) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P_KG * 4) : "memory");  // slab n-1 landed
-          if (lane == 0) __hip_atomic_fetch_add(&flags[F_FILLED], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(&flags[F_FILLED], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (jl < 4) PSTAMP(40 + jl);
-    }
-    return;
-  }
-
-  if (wv >= P_WW0) {
-#ifndef PIPE_SKIP_W
-    // ------------------------------------------------------------ W role --
-    set_prio((p.prio >> 4) & 15);
-    const int ww = wv - P_WW0;
-    unsigned char* slot = lds + P_OFF_W + ww * Ly::WSLOT;
-    float* sRw = reinterpret_cast<float*>(slot);
-    float4* tabw = reinterpret_cast<float4*>(slot + W2 * 4);
-    const bool vec = (C2 & 3) == 0;
-    constexpr int NQ = (W2 / 4 + 63) / 64;
-    float4 tmp[NQ];
-    for (int jl = 0; tile_of(jl) < ntiles; ++jl) {
-      const int b0 = tile_of(jl) * M, nb = min(M, p.B - b0);
-      const int lane = opq(threadIdx.x) & 63;
-      wait_ge(&flags[F_RDONE], P_NM * (jl + 1), err, 4);  // r of the tile is in memory
-      if (jl < 4) PSTAMP(24 + jl * 2);
-      auto fetch = [&](int m) {
-        const float4* src = reinterpret_cast<const float4*>(p.r + (size_t)(b0 + m) * W2);
-#pragma unroll
-        for (int it = 0; it < NQ; ++it) {
-          const int i = lane + it * 64;
-          if (i < W2 / 4) tmp[it] = src[i];
-        }
-      };
-      if (ww < nb) fetch(ww);
-      for (int m = ww; m < nb && (p.phases & 8); m += P_NW) {
-        float th[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) th[k] = p.theta_b[(size_t)(b0 + m) * 6 + k];
-        const bool act = p.mask[b0 + m] != 0.0f;
-        const float zn = act ? p.zval[b0 + m] : 0.0f;
-        const bool tab = stn_separable(th) && C <= CTAB_MAX;
-#pragma unroll
-        for (int it = 0; it < NQ; ++it) {
-          const int i = lane + it * 64;
-          if (i < W2 / 4) reinterpret_cast<float4*>(sRw)[i] = tmp[it];
-        }
-        if (tab)
-          for (int i = lane; i < 2 * C; i += 64)
-            tabw[i] = i < C ? axis4(axis_col(th, 28, 28, C, C, i), 4)
-                            : axis4(axis_row(th, 28, 28, C, C, i - C), 4 * 28);
-        wave_lds_sync();
-        if (m + P_NW < nb) fetch(m + P_NW);
-        float* om = p.part + (size_t)(b0 + m) * C2;
-        const float4* tcol = tabw;
-        const float4* trow = tabw + C;
-        if (!act) {
-          if (lane == 0) p.part_rows[b0 + m] = 0;
-        } else if (tab && vec) {
-          const float4 el = trow[lane < C ? lane : 0];
-          const unsigned long long lmask =
-              __builtin_amdgcn_ballot_w64(lane < C && __float_as_int(el.x) != __float_as_int(el.y));
-          const int rlo = lmask ? (__builtin_ctzll(lmask) & ~1) : 0;
-          const int rhi = lmask ? min(C, (64 - __builtin_clzll(lmask) + 1) & ~1) : 0;
-          if (lane == 0) p.part_rows[b0 + m] = rlo | (rhi << 16);
-          const int PR = C >> 1;
-          const int np = (rhi - rlo) * PR;
-          const int dq = 64 / PR, dr = 64 - dq * PR;
-          int rr = lane / PR, pr = lane - (lane / PR) * PR;
-          typedef float f2 __attribute__((ext_vector_type(2)));
-          const char* Ub = reinterpret_cast<const char*>(sRw);
-          auto ld = [Ub](int a, int b) { return *reinterpret_cast<const float*>(Ub + a + b); };
-          f2* dst = reinterpret_cast<f2*>(om + rlo * C) + lane;
-#pragma unroll 2
-          for (int idx = lane; idx < np; idx += 64) {
-            const float4 ey = trow[rlo + rr];
-            const float4 e0 = tcol[2 * pr], e1 = tcol[2 * pr + 1];
-            const int y0 = __float_as_int(ey.x), y1 = __float_as_int(ey.y);
-            const int a0 = __float_as_int(e0.x), c0 = __float_as_int(e0.y);
-            const int a1 = __float_as_int(e1.x), c1 = __float_as_int(e1.y);
-            const f2 Ia = {ld(y0, a0), ld(y0, a1)}, Ib = {ld(y1, a0), ld(y1, a1)};
-            const f2 Ic = {ld(y0, c0), ld(y0, c1)}, Id = {ld(y1, c0), ld(y1, c1)};
-            const f2 xz = {e0.z, e1.z}, xw = {e0.w, e1.w};
-            const f2 wa = xz * ey.z, wb = xz * ey.w, wc = xw * ey.z, wd = xw * ey.w;
-            const f2 sv = ((wa * Ia + wb * Ib) + wc * Ic) + wd * Id;
-            st_stream(dst, zn * sv);
-            dst += 64;
-            pr += dr;
-            rr += dq;
-            if (pr >= PR) {
-              pr -= PR;
-              ++rr;
-            }
-          }
-        } else {  // general transform or odd C: per-pixel geometry, flat order
-          if (lane == 0) p.part_rows[b0 + m] = C << 16;
-          const float* U = sRw;
-          float4* om4 = reinterpret_cast<float4*>(om);
-          const int nq = vec ? C2 / 4 : C2;
-          const int per = vec ? 4 : 1;
-          for (int q = lane; q < nq; q += 64) {
-            float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            int pix = q * per;
-            int i = pix / C, j = pix - (pix / C) * C;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              if (e < per) {
-                const Tap t = stn_tap(th, 28, 28, mog_linspace(j, C), mog_linspace(i, C));
-                v[e] = t.dead ? 0.0f : zn * tap_value(t, U);
-                if (++j == C) { j = 0; ++i; }
-              }
-            }
-            if (vec) st_stream(reinterpret_cast<floatx4*>(om4 + q), floatx4{v[0], v[1], v[2], v[3]});
-            else st_stream(om + q, v[0]);
-          }
-        }
-        wave_lds_sync();  // the slot is rewritten for the next image
-      }
-      if (jl < 4) PSTAMP(25 + jl * 2);
-    }
-#endif
-    return;
-  }
-
-  // -------------------------------------------------------------- M role --
-  set_prio((p.prio >> 8) & 15);
-  const bool save = p.a1b != nullptr;
-  auto opaque = [](int v) {
-    asm volatile("" : "+v"(v));
-    return v;
-  };
-  unsigned gen = 0;
-  const MBar mbar{&flags[F_MBAR], &gen, err};
-  unsigned n = 0;  // ring slabs consumed so far
-  for (int jl = 0; tile_of(jl) < ntiles; ++jl) {
-    const int b0 = tile_of(jl) * M, nb = min(M, p.B - b0);
-    // per tile, so that nothing lane-derived is hoisted out of the tile loop
-    const int tid = opq(threadIdx.x), lane = tid & 63;
-    const int li = lane & 15, g = lane >> 4;
-    const LdsBarrier lb{};
-    const NoHook nh{};
-    // ---- 1+2. a1 = softplus(g W1 + b1): glimpse slabs from the ring ------
-    {
-      constexpr int TW = 4, DB = 2;
-      const int rot = (int)(blockIdx.x >> 3);
-      const __amdgpu_buffer_rsrc_t wr = weight_rsrc(p.wt[0]);
-      int ct[TW], wo[TW];
-#pragma unroll
-      for (int c = 0; c < TW; ++c) {
-        ct[c] = (wv + P_NM * c + rot) % 32;
-        wo[c] = frag_voff(ct[c], lane);
-      }
-      floatx4 acc[MT][TW];
-#pragma unroll
-      for (int rt = 0; rt < MT; ++rt)
-#pragma unroll
-        for (int c = 0; c < TW; ++c) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-      bf16x8 q[DB][TW];
-      auto loadB = [&](int ks, bf16x8* b) {
-#pragma unroll
-        for (int c = 0; c < TW; ++c) b[c] = load_frag<32>(wr, wo[c], ks);
-      };
-#pragma unroll
-      for (int d = 0; d < DB; ++d) loadB(d, q[d]);
-      const int aoff = li * 64 + ((g ^ pswz(li)) << 4);
-      if (jl < 4) PSTAMP(8 + jl * 4);
-#ifndef PIPE_SKIP_L1
-      static_for<0, P_NSLAB>([&](auto sc) {
-        constexpr int s = decltype(sc)::value;
-        wait_ge(&flags[F_FILLED], n + 1, err, 5);
-        const int sbo = (n % P_RING) * P_SLAB + aoff;
-        static_for<0, P_KG>([&](auto kc) {
-          constexpr int kk = decltype(kc)::value, ks = P_KG * s + kk;
-          const unsigned char* sb = arena + opaque(sbo + kk * 4096);
-#pragma unroll
-          for (int rt = 0; rt < MT; ++rt) {
-            const bf16x8 a = *reinterpret_cast<const bf16x8*>(sb + rt * 1024);
-#pragma unroll
-            for (int c = 0; c < TW; ++c)
-              acc[rt][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, q[ks % DB][c], acc[rt][c], 0, 0, 0);
-          }
-          if constexpr (ks + DB < KS1) loadB(ks + DB, q[ks % DB]);
-        });
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slab done
-        if (lane == 0) __hip_atomic_fetch_add(&flags[F_CONSUMED], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        ++n;
-      });
-#endif
-      floatx4 b1q[TW];
-#pragma unroll
-      for (int c = 0; c < TW; ++c) b1q[c] = load_bias4(p.bias[0], ct[c] * 16 + (li & ~3), 512);
-      if (jl < 4) PSTAMP(9 + jl * 4);
-      mbar();  // every wave is done with the ring, which a1 overwrites
-      __bf16* sA1 = reinterpret_cast<__bf16*>(arena);
-#pragma unroll
-      for (int c = 0; c < TW; ++c) {
-        const int n0 = ct[c] * 16 + (li & ~3);
-#pragma unroll
-        for (int rt = 0; rt < MT; ++rt)
-          store_softplus4(sA1 + (rt * 16 + g * 4 + (li & 3)) * S512 + n0,
-                          quad_transpose(acc[rt][c], tid), b1q[c]);
-      }
-    }
-    mbar();
-    __bf16* sA1 = reinterpret_cast<__bf16*>(arena);
-    __bf16* sA2 = sA1;
-    if (save) flush_rows<NTHR>(sA1, S512, p.a1b + (size_t)b0 * 512, 512, 512, nb, tid);
-    // ---- 3. a2 = softplus(a1 W2 + b2), in place ------------------------------
-    dense_tiles<MT, 512, 256, 2, 4, true>(sA1, S512, p.wt[1], p.bias[1], 0, 0, P_NM,
-                                          [&](int m, int n0, const floatx4& v, const floatx4& b) {
-                                            store_softplus4(sA2 + m * S256 + n0, v, b);
-                                          },
-                                          mbar, nh, tid);
-    mbar();
-    if (save) flush_rows<NTHR>(sA2, S256, p.a2b + (size_t)b0 * 256, 256, 256, nb, tid);
-    // ---- 4. mu | lv (waves 0-3 | 4-7) ---------------------------------------
-    float* sMu = reinterpret_cast<float*>(arena + Ly::OFF_MU);
-    float* sLv = reinterpret_cast<float*>(arena + Ly::OFF_LV);
-    {
-      auto epi_f32 = [&](float* dst) {
-        return [dst](int m, int n0, const floatx4& v, const floatx4& b) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (n0 + k < 50) dst[m * 50 + n0 + k] = v[k] + b[k];
-        };
-      };
-      dense_tiles<MT, 256, 50, 1, 4, false>(sA2, S256, p.wt[2], p.bias[2], 0, 0, 4, epi_f32(sMu),
-                                            lb, nh, tid);
-      dense_tiles<MT, 256, 50, 1, 4, false>(sA2, S256, p.wt[3], p.bias[3], 0, 4, 4, epi_f32(sLv),
-                                            lb, nh, tid);
-    }
-    mbar();
-    // ---- 5. z = mu + eps sqrt(exp(lv)); VAE KL -> runloss ---------------------
-    float* sKl = reinterpret_cast<float*>(arena + Ly::OFF_KL);
-    __bf16* sZ = reinterpret_cast<__bf16*>(arena + Ly::OFF_Z);
-    {
-      constexpr int NS = M * 64 / NTHR;
-      float ez[NS];
-#pragma unroll
-      for (int it = 0; it < NS; ++it) {
-        const int i = tid + it * NTHR, m = i >> 6, k = i & 63;
-        ez[it] = (k < 50 && m < nb) ? p.eps_z[(size_t)(b0 + m) * 50 + k] : 0.0f;
-      }
-#pragma unroll
-      for (int it = 0; it < NS; ++it) {
-        const int i = tid + it * NTHR, m = i >> 6, k = i & 63;
-        float zv = 0.0f;
-        if (k < 50 && m < nb) {
-          const size_t o = (size_t)(b0 + m) * 50 + k;
-          const float l = sLv[m * 50 + k];
-          const float mv = sMu[m * 50 + k];
-          const float var = mog_expf(l);
-          zv = mv + ez[it] * sqrtf(var);
-          if (p.z) st_stream(p.z + o, zv);
-          if (save) {
-            st_stream(p.mu + o, mv);
-            st_stream(p.lv + o, l);
-            p.zb[(size_t)(b0 + m) * 56 + k] = (__bf16)zv;
-          }
-          const float d = mv - p.v_pm;
-          sKl[m * 50 + k] = (((p.v_plv - l) - 1.0f) + var / p.v_pv) + (d * d) / p.v_pv;
-        }
-        sZ[m * SZ + k] = (__bf16)zv;
-      }
-    }
-    mbar();
-    if (tid < nb) {
-      const int m = tid;
-      float t[50];
-#pragma unroll
-      for (int k = 0; k < 50; ++k) t[k] = sKl[m * 50 + k];
-      float sum = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 50; ++k) sum = sum + t[k];
-      const float vkl = 0.5f * sum;
-      p.vkl[b0 + m] = vkl;
-      if (p.runloss && p.mask[b0 + m] != 0.0f) p.runloss[b0 + m] = p.runloss[b0 + m] + vkl;
-    }
-    // ---- 6. d1 = softplus(z Wg1 + b) (over mu | lv) ---------------------------
-    __bf16* sD1 = reinterpret_cast<__bf16*>(arena + P_D1);
-    dense_tiles<MT, 64, 256, 2, 2, false>(sZ, SZ, p.wt[4], p.bias[4], 0, 0, P_NM,
-                                          [&](int m, int n0, const floatx4& v, const floatx4& b) {
-                                            store_softplus4(sD1 + m * S256 + n0, v, b);
-                                          },
-                                          lb, nh, tid);
-    mbar();
-    if (save) flush_rows<NTHR>(sD1, S256, p.d1b + (size_t)b0 * 256, 256, 256, nb, tid);
-    // ---- 7. d2 = softplus(d1 Wg2 + b) at 0 (beside d1): two passes ------------
-    __bf16* sD2 = reinterpret_cast<__bf16*>(arena);
-    {
-      auto epi = [&](int m, int n0, const floatx4& v, const floatx4& b) {
-        store_softplus4(sD2 + m * S512 + n0, v, b);
-      };
-      dense_tiles<MT, 256, 512, 2, 4, false>(sD1, S256, p.wt[5], p.bias[5], 0, 0, P_NM, epi, lb, nh,
-                                             tid);
-      dense_tiles<MT, 256, 512, 2, 4, false>(sD1, S256, p.wt[5], p.bias[5], 16, 0, P_NM, epi, lb,
-                                             nh, tid);
-    }
-    mbar();
-    if (save) flush_rows<NTHR>(sD2, S512, p.d2b + (size_t)b0 * 512, 512, 512, nb, tid);
-    if (jl < 4) PSTAMP(10 + jl * 4);
-    // ---- 8. r = sigmoid(d2 Wgo + b + std eps) -> HBM ---------------------------
-    {
-      const float sd = p.lik_std;
-      auto epi = [&](int m, int n, const floatx4& v, const floatx4& b) {
-        if (m < nb) {
-          float ev[4];
-          const size_t qi = (size_t)(b0 + m) * (W2 / 4) + (n >> 2);
-          if (p.eps_gen) {
-            mog_philox_quad(p.eps_seed, p.eps_offset + qi, true, ev);
-          } else {
-            const float4 e4 = reinterpret_cast<const float4*>(p.eps_x)[qi];
-            ev[0] = e4.x; ev[1] = e4.y; ev[2] = e4.z; ev[3] = e4.w;
-          }
-          float o[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float y = __builtin_fmaf(ev[k], sd, v[k] + b[k]);
-            o[k] = mog_sigmoid_hw(y);
-          }
-          reinterpret_cast<float4*>(p.r)[qi] = make_float4(o[0], o[1], o[2], o[3]);
-        }
-      };
-      // 49 column tiles: the last split over the row tiles (waves 0-3), then
-      // three passes of two tiles per wave; after the last pass's k loop the
-      // arena is free for the next tile's ring
-#ifndef PIPE_SKIP_OUT
-      dense_rowsplit<MT, 512, W2>(sD2, S512, p.wt[6], p.bias[6], 48, epi, tid);
-      dense_tiles<MT, 512, W2, 2, 8, false>(sD2, S512, p.wt[6], p.bias[6], 0, 0, P_NM, epi, lb, nh,
-                                            tid);
-      dense_tiles<MT, 512, W2, 2, 8, false>(sD2, S512, p.wt[6], p.bias[6], 16, 0, P_NM, epi, lb,
-                                            nh, tid);
-      auto arena_free = [&]() {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add(&flags[F_ARENA], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      };
-      dense_tiles<MT, 512, W2, 2, 8, false>(sD2, S512, p.wt[6], p.bias[6], 32, 0, P_NM, epi, lb,
-                                            arena_free, tid);
-#endif
-    }
-    signal_add(&flags[F_RDONE]);  // this wave's r stores are in memory
-    if (jl < 4) PSTAMP(11 + jl * 4);
-  }
-}
-
 }  // namespace
 
 extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int Z, int G1,
@@ -1584,9 +1110,8 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   MOG_CHECK_ARG(W == 28 && R1 == 512 && R2 == 256 && Z == 50 && G1 == 256 && G2 == 512);
   MOG_CHECK_ARG(x && theta_f && theta_b && mask && zval && eps_z && (eps_x || eps_gen) && wt && bias);
   MOG_CHECK_ARG(canvas_part && part_rows && vkl && r);
-  // the saved activations: all given (train) or all NULL (forward only); in
-  // the forward-only form gb may still be given as the glimpse workspace of
-  // the pipelined kernel
+  // the saved activations: all given (train) or all NULL (forward only); gb
+  // (the saved glimpse) may be given in either form
   const bool save = a1b != nullptr;
   MOG_CHECK_ARG(!save || (gb && a2b && mu && lv && z && zb && d1b && d2b));
   MOG_CHECK_ARG(save || !(a2b || mu || lv || zb || d1b || d2b));
@@ -1608,87 +1133,9 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   const char* ph = getenv("MOG_VS_PHASES");
   p.phases = ph ? atoi(ph) : 31;
   if (!save) p.phases &= ~16;
-  p.prio = 0;
-  if (const char* e = getenv("MOG_VS_PRIO")) p.prio = (int)strtol(e, nullptr, 16);
   p.B = B; p.C = C; p.lik_std = lik_std; p.v_pm = v_pm; p.v_pv = v_pv; p.v_plv = v_plv;
   p.x_period = x_period > 0 ? x_period : B;
   hipStream_t s = mog_stream(stream);
-  // Pipelined persistent form (one workgroup per CU, roles over 64-image
-  // tiles) once every CU gets a tile; it stages the glimpse through gb.
-  // MOG_VS_PIPE=0 / 1 disables / forces it.
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = 256;
-  }
-  bool pipe = B >= PT * ncu;
-  if (const char* e = getenv("MOG_VS_PIPE")) pipe = atoi(e) != 0;
-  if (pipe && gb && (p.x_period == B || p.x_period % PT == 0) &&
-      (p.x_period == B || !runloss)) {
-    const int ntiles = (int)mog_cdiv(B, PT);
-    // MOG_VS_PIPE_GRID (tests): fewer workgroups, several tiles each
-    int grid = std::min(ntiles, ncu);
-    if (const char* e = getenv("MOG_VS_PIPE_GRID")) grid = std::min(ntiles, std::max(1, atoi(e)));
-    static int* ebuf = nullptr;
-    const bool chk = getenv("MOG_VS_CHECK") != nullptr;
-    if (chk && !ebuf && hipMalloc(&ebuf, sizeof(int)) != hipSuccess) return MOG_ERR_INVALID;
-    if (chk) (void)hipMemsetAsync(ebuf, 0, sizeof(int), s);
-    static long long* pbuf = nullptr;
-    static size_t pcap = 0;
-    p.tstamp = nullptr;
-    if (getenv("MOG_VS_TIMING")) {
-      if (pcap < (size_t)grid * 64) {
-        if (pbuf) (void)hipFree(pbuf);
-        pcap = (size_t)grid * 64;
-        if (hipMalloc(&pbuf, pcap * sizeof(long long)) != hipSuccess) return MOG_ERR_INVALID;
-      }
-      (void)hipMemsetAsync(pbuf, 0, pcap * sizeof(long long), s);
-      p.tstamp = pbuf;
-    }
-    stn_vae_pipe_kernel<<<grid, 1024, 0, s>>>(p, ntiles, reinterpret_cast<__bf16*>(gb),
-                                              chk ? ebuf : nullptr);
-    const int rc = (int)hipGetLastError();
-    if (rc) return rc;
-    if (chk) {
-      int e = 0;
-      (void)hipMemcpyAsync(&e, ebuf, sizeof(int), hipMemcpyDeviceToHost, s);
-      (void)hipStreamSynchronize(s);
-      if (e) {
-        fprintf(stderr, "stn_vae_pipe_kernel: role wait timed out (code %d)\n", e);
-        return MOG_ERR_INVALID;
-      }
-    }
-    if (p.tstamp) {
-      // per-tile role spans (us, mean over workgroups, 100 MHz clock) relative
-      // to the workgroup's start: S tile j [start, end], M tile j [L1 start,
-      // L1 end, output start, end], W tile j [start, end], D tile j end
-      std::vector<long long> h((size_t)grid * 64);
-      (void)hipStreamSynchronize(s);
-      (void)hipMemcpy(h.data(), pbuf, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
-      const int nt = std::min(4, (ntiles + grid - 1) / grid);
-      auto avg = [&](int k) {
-        double a = 0;
-        int c = 0;
-        for (int b = 0; b < grid; ++b)
-          if (h[(size_t)b * 64 + k]) { a += (double)(h[(size_t)b * 64 + k] - h[(size_t)b * 64 + 48]); ++c; }
-        return c ? a / c / 100.0 : -1.0;
-      };
-      long long t0 = h[48], t1 = 0;
-      for (int b = 0; b < grid; ++b) {
-        t0 = std::min(t0, h[(size_t)b * 64 + 48]);
-        for (int k = 0; k < 48; ++k) t1 = std::max(t1, h[(size_t)b * 64 + k]);
-      }
-      fprintf(stderr, "stn_vae_pipe B=%d grid=%d tiles/wg=%d span %.2f us\n", B, grid,
-              (ntiles + grid - 1) / grid, (t1 - t0) / 100.0);
-      for (int j = 0; j < nt; ++j)
-        fprintf(stderr, "  tile %d: S %.1f-%.1f | D end %.1f | M L1 %.1f-%.1f out %.1f-%.1f | W %.1f-%.1f\n",
-                j, avg(j * 2), avg(j * 2 + 1), avg(40 + j), avg(8 + j * 4), avg(9 + j * 4),
-                avg(10 + j * 4), avg(11 + j * 4), avg(24 + j * 2), avg(25 + j * 2));
-    }
-    return 0;
-  }
   // Tile height: 64 images per workgroup (one per CU) once the batch gives
   // every CU at least one such tile, else 32 so small batches still spread
   // over the chip (two 8-wave workgroups per CU).  MOG_VS_MT overrides: 4 =
@@ -1717,7 +1164,11 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
     }
     p.tstamp = tbuf;
   }
-  if (mt == 4) stn_vae_step_kernel<4, 16, 4><<<nblk, 1024, 0, s>>>(p);
+  // MOG_VS_LA (profiling): sampler gather lookahead of the 64-image form
+  static const int la = getenv("MOG_VS_LA") ? atoi(getenv("MOG_VS_LA")) : 3;
+  if (mt == 4 && la == 4) stn_vae_step_kernel<4, 16, 4, 4><<<nblk, 1024, 0, s>>>(p);
+  else if (mt == 4 && la == 5) stn_vae_step_kernel<4, 16, 4, 5><<<nblk, 1024, 0, s>>>(p);
+  else if (mt == 4) stn_vae_step_kernel<4, 16, 4><<<nblk, 1024, 0, s>>>(p);
   else if (mt == 2) stn_vae_step_kernel<2, 8, 4><<<nblk, 512, 0, s>>>(p);
   else stn_vae_step_kernel<2, 16, 4><<<nblk, 1024, 0, s>>>(p);
   if (p.tstamp) {

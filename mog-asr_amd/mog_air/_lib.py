@@ -11,7 +11,8 @@ import re
 from typing import List
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libmog_air.so")
+# MOG_AIR_LIB: another build of the library (A/B timing scripts only)
+LIB_PATH = os.environ.get("MOG_AIR_LIB") or os.path.join(_HERE, "_lib", "libmog_air.so")
 HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "mog_air.h"))
 
 P = ctypes.c_void_p

@@ -506,13 +506,11 @@ class AIRModel:
             # forward only (no backward follows): the backward's saved
             # activations are not written (vae_step.hip moves its own bytes)
             sv = r_ if save else (lambda a: None)  # noqa: E731
-            # (gb is passed in both forms: the pipelined kernel stages the
-            # glimpse through it)
             _ops.stn_vae_step_(TB, C, X, r_(ws.th_f), r_(ws.th_b), r_(ws.zmask), r_(ws.zval),
                                r_(ws.eps_z), r_(ws.eps_x), ops._i64(self.noise_seed),
                                ops._i64(off), gen, wt, bias, lik_std, float(self.vae_prior_mean),
                                float(self.vae_prior_variance), self.vae_prior_log_variance,
-                               r_(ws.cparts), r_(ws.prows), None, r_(ws.vkl), r_(ws.gb),
+                               r_(ws.cparts), r_(ws.prows), None, r_(ws.vkl), sv(ws.gb),
                                sv(ws.a1b), sv(ws.a2b), sv(ws.mu), sv(ws.lv), r_(ws.z), sv(ws.zb),
                                sv(ws.d1b), sv(ws.d2b), r_(ws.r), B)
             return

@@ -6,6 +6,8 @@ within 1e-5 relative, margin within 1e-6 relative — and its gradients
 against float64 torch autograd (oracle/asr_torch.py) under a well-conditioned
 canvas cotangent, for the learned z_pres prior and fix_steps, train and test
 models, fp32 and the bf16 glimpse-VAE configuration."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -122,6 +124,7 @@ def test_asr_gradients_vs_float64_autograd(kw, precision, tol, cos_min, global_t
             conditioned[name] = np.linalg.norm(a - b) < 0.1 * np.linalg.norm(a)
     worst, checked = 0.0, 0
     got_all, ref_all = [], []
+    report = []
     for name, p in Pt.items():
         ref = p.grad.numpy() if p.grad is not None else np.zeros(p.shape)
         got_all.append(np.asarray(grads[name], np.float64).ravel())
@@ -132,6 +135,7 @@ def test_asr_gradients_vs_float64_autograd(kw, precision, tol, cos_min, global_t
         err = np.linalg.norm(grads[name] - ref) / np.linalg.norm(ref)
         cos = float(np.dot(grads[name].ravel(), ref.ravel()) /
                     (np.linalg.norm(grads[name]) * np.linalg.norm(ref) + 1e-30))
+        report.append((name, float(err), cos, bool(conditioned[name])))
         if not conditioned[name]:
             continue
         worst = max(worst, err)
@@ -143,6 +147,11 @@ def test_asr_gradients_vs_float64_autograd(kw, precision, tol, cos_min, global_t
     assert gerr < global_tol and gcos > 0.99, (gerr, gcos)
     assert checked >= 25
     print(f"ASR {precision} worst relative gradient error {worst:.2e}, global {gerr:.2e}")
+    if os.environ.get("MOG_GRAD_REPORT"):
+        import json
+        with open(os.environ["MOG_GRAD_REPORT"] + f"_{precision}{cfg.fix_steps}.json", "w") as f:
+            json.dump({"per_tensor": report, "global_rel": float(gerr), "global_cos": gcos}, f,
+                      indent=1)
 
 
 def test_asr_train_steps_finite():
