@@ -294,6 +294,9 @@ class AIRModel(_AirBase):
     def _eps_x_in_kernel(self, B: int) -> bool:
         return self.fused_step  # the fp32 ASR VAE runs per step and reads eps_x
 
+    def _batched_vae(self, B: int) -> bool:
+        return False  # per step: the ASR loop feeds z of step t into step t+1's input
+
     def _forward(self, X, targets, ws, need_grad, outputs=True):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
         C, W, C2 = self.canvas_size, self.windows_size, self.C2
