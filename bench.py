@@ -256,10 +256,12 @@ def vae_chain_flops_per_image(W2=784, R1=512, R2=256, Z=50, G1=256, G2=512) -> f
 def fp32_step_roofline(batch: int, launches: int, dev):
     """SURVEY §8 D.3's fp32 step (STN read -> glimpse VAE -> STN write at
     reference precision) at `batch` images, priced against the fp32 MFMA roof
-    (batch x 2.21 MFLOP; >= 919 us at 65,536).  This build runs it unfused: the
-    STN read, seven bit-exact fp32 GEMMs with fused epilogues, the latent
-    sample and the STN write into canvas parts (AIRModel._vae_forward_all,
-    one step over `batch` rows); timed with HIP events on the launch stream."""
+    (batch x 2.21 MFLOP; >= 919 us at 65,536): the fused fp32 step kernel
+    (stn_vae_step_f32_kernel, bit-identical to the unfused sequence), one step
+    over `batch` rows (AIRModel._vae_forward_all); timed with HIP events on the
+    launch stream.  The unfused sequence (STN read, seven bit-exact fp32 GEMMs
+    with fused epilogues, latent sample, STN write into canvas parts) is timed
+    beside it as `unfused_us`."""
     from mog_air.air_model import AIRModel
     m = AIRModel(max_steps=1, max_digits=1, canvas_size=50, scale_prior_variance=0.05,
                  z_pres_prior_log_odds=-0.01, learning_rate=1e-4, gradient_clipping_norm=1.0,
@@ -271,27 +273,39 @@ def fp32_step_roofline(batch: int, launches: int, dev):
     m.infer(X, K)
     ws = m._ws
     assert m._batched_vae(batch)
-    for _ in range(2):
-        m._vae_forward_all(X, ws, 0.3)
-    torch.cuda.synchronize()
-    s = torch.cuda.current_stream()
-    evs = []
-    for _ in range(launches):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        m._vae_forward_all(X, ws, 0.3)
-        e1.record(s)
-        evs.append((e0, e1))
-    torch.cuda.synchronize()
-    avg = sum(a.elapsed_time(b) * 1e-3 for a, b in evs) / len(evs)
+    fused = m.fused_f32
+
+    def timed(n):
+        for _ in range(2):
+            m._vae_forward_all(X, ws, 0.3)
+        torch.cuda.synchronize()
+        s = torch.cuda.current_stream()
+        evs = []
+        for _ in range(n):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            m._vae_forward_all(X, ws, 0.3)
+            e1.record(s)
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) * 1e-3 for a, b in evs) / len(evs)
+
+    avg = timed(launches)
+    unfused = None
+    if fused:
+        m.fused_f32 = False
+        unfused = timed(max(2, launches // 2)) * 1e6
+        m.fused_f32 = True
     flop = batch * vae_chain_flops_per_image()
-    out = {"kernel": "fp32 STN read + VAE GEMM chain + STN write (unfused, bit-exact)",
+    kern = ("stn_vae_step_f32 (fused fp32 STN read + VAE chain + STN write, bit-exact)" if fused
+            else "fp32 STN read + VAE GEMM chain + STN write (unfused, bit-exact)")
+    out = {"kernel": kern,
            "batch": batch, "bound": "mfma", "achieved": flop / avg / 1e12,
            "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
            "frac": flop / avg / 1e12 / FP32_MFMA_PEAK_TFLOPS, "launches": launches,
            "avg_chain_us": avg * 1e6, "roof_us": flop / FP32_MFMA_PEAK_TFLOPS / 1e6,
-           "flop_per_image": vae_chain_flops_per_image()}
+           "flop_per_image": vae_chain_flops_per_image(), "unfused_us": unfused}
     del m, ws
     torch.cuda.empty_cache()
     return out

@@ -190,6 +190,36 @@ int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int Z, int G1,
                              void* a1b, void* a2b, float* mu, float* lv, float* z, void* zb,
                              void* d1b, void* d2b, float* r, int x_period, void* stream);
 
+/* fp32 MFMA B-fragment packs of n <= 8 weight matrices W[i] [K[i]][N[i]]
+ * (row-major fp32, TF [in, out]) into out[i] ((K+15)/16 * (N+15)/16 KiB):
+ * fragment (ks, ct) at ((ks * NCT + ct) * 64 + lane) * 4 floats holds
+ * W[16 ks + 4 kk + g][16 ct + li], kk < 4, lane = 16 g + li; zero outside W.
+ * The weight operand of mog_stn_vae_step_forward_f32. */
+int mog_pack_frag_f32(int n, const float* const* W, const int* K, const int* N,
+                      float* const* out, void* stream);
+
+/* The fp32 fused step: mog_stn_vae_step_forward at the reference precision,
+ * bit-identical to the unfused fp32 sequence (mog_stn_forward, the seven
+ * mog_gemm_f32 layers with their pre-activations, mog_vae_sample_forward,
+ * mog_gemm_f32_sigmoid_philox / EPI_SIGMOID_NOISE, mog_stn_write_parts).
+ * wt[7]: mog_pack_frag_f32 packs of the seven VAE weights (order as
+ * mog_stn_vae_step_forward's), bias[7] fp32.  Saved for the backward, fp32:
+ * g [B,784], a1pre/a1 [B,512], a2pre/a2 [B,256], mu/lv [B,50], d1pre/d1
+ * [B,256], d2pre/d2 [B,512] -- all given, or all NULL (forward only); z
+ * [B,50] and r [B,784] are always written.  Tiles of 32 images: x_period > 0
+ * requires x_period % 32 == 0 and runloss == NULL.  Reference VAE shape only.
+ * Replaces air_model.py:523-588 at fp32. */
+int mog_stn_vae_step_forward_f32(int B, int C, const float* x, const float* theta_f,
+                                 const float* theta_b, const float* mask, const float* zval,
+                                 const float* eps_z, const float* eps_x, int eps_gen,
+                                 unsigned long long eps_seed, unsigned long long eps_offset,
+                                 const float* const* wt, const float* const* bias, float lik_std,
+                                 float v_pm, float v_pv, float v_plv, float* canvas_part,
+                                 int* part_rows, float* runloss, float* vkl, float* g,
+                                 float* a1pre, float* a1, float* a2pre, float* a2, float* mu,
+                                 float* lv, float* z, float* d1pre, float* d1, float* d2pre,
+                                 float* d2, float* r, int x_period, void* stream);
+
 /* dmu/dlv fp32 [B,Z] and/or bf16 copies with row stride ld_b (any may be NULL,
  * but one complete pair must be given). */
 int mog_vae_sample_backward(int B, int Z, float v_pm, float v_pv, float grad_scale,

@@ -513,6 +513,78 @@ void stn_vae_step_(int64_t B, int64_t C, const Tensor& x, const Tensor& theta_f,
         o.name);
 }
 
+void pack_frag_f32_(at::TensorList W, at::IntArrayRef K, at::IntArrayRef N,
+                    const c10::List<optional<Tensor>>& out) {
+  Op o("pack_frag_f32_");
+  const int n = (int)W.size();
+  TORCH_CHECK(n >= 1 && n <= 8 && (int)K.size() == n && (int)N.size() == n && (int)out.size() == n,
+              o.name, ": 1..8 matrices with K, N and an output each");
+  vector<void*> w, d;
+  vector<int> k, nn;
+  for (int i = 0; i < n; ++i) {
+    TORCH_CHECK(K[i] > 0 && N[i] > 0, o.name, ": K, N > 0");
+    w.push_back(o.f(W[i], K[i] * N[i], "W"));
+    const optional<Tensor> oi = out.get(i);
+    TORCH_CHECK(oi.has_value(), o.name, ": out given");
+    d.push_back(o.f(oi, (K[i] + 15) / 16 * ((N[i] + 15) / 16) * 256, "out"));
+    k.push_back((int)K[i]);
+    nn.push_back((int)N[i]);
+  }
+  GUARD(o);
+  check(mog_pack_frag_f32(n, arr<float>(w), k.data(), nn.data(), marr<float>(d), o.stream()),
+        o.name);
+}
+
+void stn_vae_step_f32_(int64_t B, int64_t C, const Tensor& x, const Tensor& theta_f,
+                       const Tensor& theta_b, const Tensor& mask, const Tensor& zval,
+                       const Tensor& eps_z, const optional<Tensor>& eps_x, int64_t eps_seed,
+                       int64_t eps_offset, bool eps_gen, at::TensorList wt, at::TensorList bias,
+                       double lik_std, double v_pm, double v_pv, double v_plv,
+                       Tensor canvas_part, Tensor part_rows, const optional<Tensor>& runloss,
+                       Tensor vkl, const c10::List<optional<Tensor>>& saved, Tensor z, Tensor r,
+                       int64_t x_period) {
+  Op o("stn_vae_step_f32_");
+  TORCH_CHECK(wt.size() == 7 && bias.size() == 7, o.name, ": 7 VAE layers");
+  TORCH_CHECK(saved.size() == 11, o.name,
+              ": saved = [g, a1pre, a1, a2pre, a2, mu, lv, d1pre, d1, d2pre, d2]");
+  const int64_t C2 = C * C;
+  // fp32 B-fragment packs: (K + 15) / 16 x (N + 15) / 16 KiB
+  static const int64_t pack[7] = {49 * 32 * 256, 32 * 16 * 256, 16 * 4 * 256, 16 * 4 * 256,
+                                  4 * 16 * 256, 16 * 32 * 256, 32 * 49 * 256};
+  static const int64_t nb[7] = {512, 256, 50, 50, 256, 512, 784};
+  vector<void*> w, b;
+  for (int k = 0; k < 7; ++k) {
+    w.push_back(o.f(wt[k], pack[k], "wt"));
+    b.push_back(o.f(bias[k], nb[k], "bias"));
+  }
+  static const int64_t cols[11] = {784, 512, 512, 256, 256, 50, 50, 256, 256, 512, 512};
+  static const char* names[11] = {"g", "a1pre", "a1", "a2pre", "a2", "mu", "lv",
+                                  "d1pre", "d1", "d2pre", "d2"};
+  vector<void*> sv;
+  for (int k = 0; k < 11; ++k) sv.push_back(o.f(saved.get(k), B * cols[k], names[k]));
+  float* px = o.f(x, (x_period > 0 ? x_period : B) * C2, "x");
+  float* ptf = o.f(theta_f, 6 * B, "theta_f");
+  float* ptb = o.f(theta_b, 6 * B, "theta_b");
+  float* pm = o.f(mask, B, "mask");
+  float* pzv = o.f(zval, B, "zval");
+  float* pez = o.f(eps_z, 50 * B, "eps_z");
+  float* pex = o.f(eps_x, 784 * B, "eps_x");
+  float* pcp = o.f(canvas_part, B * C2, "canvas_part");
+  int* prw = o.i(part_rows, B, "part_rows");
+  float* prl = o.f(runloss, B, "runloss");
+  float* pk = o.f(vkl, B, "vkl");
+  float* pz = o.f(z, B * 50, "z");
+  float* pr = o.f(r, B * 784, "r");
+  auto S = [&](int k) { return reinterpret_cast<float*>(sv[k]); };
+  GUARD(o);
+  check(mog_stn_vae_step_forward_f32(B, C, px, ptf, ptb, pm, pzv, pez, pex, eps_gen,
+                                     (unsigned long long)eps_seed, (unsigned long long)eps_offset,
+                                     arr<float>(w), arr<float>(b), lik_std, v_pm, v_pv, v_plv, pcp,
+                                     prw, prl, pk, S(0), S(1), S(2), S(3), S(4), S(5), S(6), pz,
+                                     S(7), S(8), S(9), S(10), pr, x_period, o.stream()),
+        o.name);
+}
+
 // ------------------------------------------------- loss / optimizer / RNG ----
 void recon_loss_(const Tensor& x, const optional<Tensor>& canvas, const optional<Tensor>& parts,
                  int64_t nparts, int64_t part_stride, const optional<Tensor>& part_rows, int64_t C,
@@ -830,6 +902,13 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "Tensor(e!)? gb, Tensor(f!)? a1b, Tensor(g!)? a2b, Tensor(h!)? mu, Tensor(i!)? lv, "
       "Tensor(j!)? z, Tensor(k!)? zb, Tensor(l!)? d1b, Tensor(m!)? d2b, Tensor(n!) r, "
       "int x_period=0) -> ()");
+  m.def("pack_frag_f32_(Tensor[] W, int[] K, int[] N, Tensor(a!)?[] out) -> ()");
+  m.def(
+      "stn_vae_step_f32_(int B, int C, Tensor x, Tensor theta_f, Tensor theta_b, Tensor mask, "
+      "Tensor zval, Tensor eps_z, Tensor? eps_x, int eps_seed, int eps_offset, bool eps_gen, "
+      "Tensor[] wt, Tensor[] bias, float lik_std, float v_pm, float v_pv, float v_plv, "
+      "Tensor(a!) canvas_part, Tensor(b!) part_rows, Tensor(c!)? runloss, Tensor(d!) vkl, "
+      "Tensor(e!)?[] saved, Tensor(f!) z, Tensor(g!) r, int x_period=0) -> ()");
   m.def(
       "recon_loss_(Tensor x, Tensor(a!)? canvas, Tensor? parts, int nparts, int part_stride, "
       "Tensor? part_rows, int C, Tensor runloss, Tensor digits, Tensor? targets, int B, int C2, "
@@ -895,6 +974,8 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("stn_write_parts_", &stn_write_parts_);
   m.impl("sigmoid_backward_", &sigmoid_backward_);
   m.impl("stn_vae_step_", &stn_vae_step_);
+  m.impl("pack_frag_f32_", &pack_frag_f32_);
+  m.impl("stn_vae_step_f32_", &stn_vae_step_f32_);
   m.impl("recon_loss_", &recon_loss_);
   m.impl("batch_mean_", &batch_mean_);
   m.impl("clip_adam_", &clip_adam_);

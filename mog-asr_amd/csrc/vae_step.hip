@@ -722,6 +722,130 @@ __device__ __forceinline__ void read_recognition(const StepArgs& p, unsigned cha
   }
 }
 
+// ---- STN write (air_model.py:580-588): this step's canvas part -----------
+// part = active ? z * w : 0 (mog_recon_loss sums the parts in step order).
+// r is staged back one image per wave into the wave's LDS slot; the lanes
+// walk the image's pixel pairs and store 8 bytes each.  Only rows whose
+// clipped corner rows differ can be nonzero; the even-aligned range of them
+// is stored and recorded.  Shared by the bf16 and fp32 step kernels.
+template <int NW>
+__device__ __forceinline__ void stn_write_tile(const float* __restrict__ r, float* part,
+                                               int* part_rows, int C, unsigned char* arena,
+                                               int wslot, const float (*sth)[12],
+                                               const int* smask, const int* ssep,
+                                               const float* szv, int b0, int nb, int wv,
+                                               int lane) {
+#pragma clang fp contract(off)
+  const int C2 = C * C;
+  // Wave-private: wave wv writes images wv, wv + NW, ... from its own LDS
+  // slot (r of one image); the next image's r is
+  // fetched into registers while the current one is computed, and the
+  // waves meet no workgroup barrier, so their memory and VALU phases drift
+  // apart and overlap.
+  const bool vec = (C2 & 3) == 0;  // even C: 16-byte aligned image rows of parts
+  unsigned char* slot = arena + wv * wslot;
+  float* sRw = reinterpret_cast<float*>(slot);
+  constexpr int NQ = (W2 / 4 + 63) / 64;
+  // (native vectors, unconditional loads at clamped indices: with HIP's
+  // float4 and a predicated load the array went to scratch and every fetch
+  // waited for its loads on the spot)
+  floatx4 tmp[NQ];
+  auto fetch = [&](int m) {
+    const floatx4* src = reinterpret_cast<const floatx4*>(r + (size_t)(b0 + m) * W2);
+#pragma unroll
+    for (int it = 0; it < NQ; ++it) tmp[it] = src[min(lane + it * 64, W2 / 4 - 1)];
+  };
+  if (wv < nb) fetch(wv);
+  for (int m = wv; m < nb; m += NW) {
+#pragma unroll
+    for (int it = 0; it < NQ; ++it) {
+      const int i = lane + it * 64;
+      if (i < W2 / 4) reinterpret_cast<floatx4*>(sRw)[i] = tmp[it];
+    }
+    wave_lds_sync();
+    if (m + NW < nb) fetch(m + NW);
+    float* om = part + (size_t)(b0 + m) * C2;
+    float4* om4 = reinterpret_cast<float4*>(om);
+    const float* U = sRw;
+    const bool act = smask[m] != 0, tab = (ssep[m] & 2) != 0;
+    const float zn = szv[m];
+    if (!act) {  // inactive: the whole part is +0 -- nothing stored
+      if (lane == 0) part_rows[b0 + m] = 0;
+    } else if (tab && vec && C <= CTAB_MAX) {
+      // Only rows whose clipped corner rows differ can be nonzero (a row
+      // with coinciding corner rows samples exactly +0 at every column:
+      // the y weights are exact negatives on one source row, and within
+      // a live row no sample is dead): store the even-aligned range
+      // [rlo, rhi) of such rows and record it.  Lane i holds row entry i
+      // in registers; a pass reads rows r, r + 1 with readlane.
+      const float4 el = axis4(axis_row(&sth[m][6], 28, 28, C, C, lane < C ? lane : 0), 4 * 28);
+      const unsigned long long lm =
+          __builtin_amdgcn_ballot_w64(lane < C && __float_as_int(el.x) != __float_as_int(el.y));
+      const int rlo = lm ? (__builtin_ctzll(lm) & ~1) : 0;
+      const int rhi = lm ? min(C, (64 - __builtin_clzll(lm) + 1) & ~1) : 0;
+      if (lane == 0) part_rows[b0 + m] = rlo | (rhi << 16);
+      // Lane -> pixel pair pr of row r + half (PR pairs per row, two rows
+      // per pass; C = 50 leaves 14 lanes idle): the column geometry stays
+      // in registers, and a corner pair (x0, x0 + 1) of a source row is
+      // one ds_read2 -- a live column has x1 = x0 + 1, a dead one x1 = x0
+      // (its second corner is the first).  Same products and summation
+      // order as sample4, per pixel.
+      const int PR = C >> 1, half = lane >= PR ? 1 : 0, pr = lane - half * PR;
+      const bool on = lane < 2 * PR;
+      const float4 e0 = axis4(axis_col(&sth[m][6], 28, 28, C, C, on ? 2 * pr : 0), 4);
+      const float4 e1 = axis4(axis_col(&sth[m][6], 28, 28, C, C, on ? 2 * pr + 1 : 0), 4);
+      const int a0 = __float_as_int(e0.x), a1 = __float_as_int(e1.x);
+      const bool dd0 = a0 == __float_as_int(e0.y), dd1 = a1 == __float_as_int(e1.y);
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      const f2 xz = {e0.z, e1.z}, xw = {e0.w, e1.w};
+      const char* Ub = reinterpret_cast<const char*>(sRw);
+      auto ld = [Ub](int a, int b) { return *reinterpret_cast<const float*>(Ub + a + b); };
+      f2* dst = reinterpret_cast<f2*>(om + (rlo + half) * C) + pr;
+      const int eyx = __float_as_int(el.x), eyy = __float_as_int(el.y);
+      const int eyz = __float_as_int(el.z), eyw = __float_as_int(el.w);
+      for (int r = rlo; r < rhi; r += 2) {
+        // (readlane takes a uniform lane: both rows' entries, then select)
+        const int y0a = __builtin_amdgcn_readlane(eyx, r), y0b = __builtin_amdgcn_readlane(eyx, r + 1);
+        const int y1a = __builtin_amdgcn_readlane(eyy, r), y1b = __builtin_amdgcn_readlane(eyy, r + 1);
+        const int za = __builtin_amdgcn_readlane(eyz, r), zb = __builtin_amdgcn_readlane(eyz, r + 1);
+        const int wa_ = __builtin_amdgcn_readlane(eyw, r), wb_ = __builtin_amdgcn_readlane(eyw, r + 1);
+        const int y0 = half ? y0b : y0a, y1 = half ? y1b : y1a;
+        const float ez = __int_as_float(half ? zb : za), ew = __int_as_float(half ? wb_ : wa_);
+        if (on) {
+          const f2 Ia = {ld(y0, a0), ld(y0, a1)}, Ib = {ld(y1, a0), ld(y1, a1)};
+          const f2 In = {ld(y0, a0 + 4), ld(y0, a1 + 4)}, Jn = {ld(y1, a0 + 4), ld(y1, a1 + 4)};
+          const f2 Ic = {dd0 ? Ia.x : In.x, dd1 ? Ia.y : In.y};
+          const f2 Id = {dd0 ? Ib.x : Jn.x, dd1 ? Ib.y : Jn.y};
+          const f2 wa = xz * ez, wb = xz * ew, wc = xw * ez, wd = xw * ew;
+          const f2 sv = ((wa * Ia + wb * Ib) + wc * Ic) + wd * Id;
+          st_stream(dst, zn * sv);
+        }
+        dst += C;  // two rows of C / 2 pairs
+      }
+    } else {  // general transform or odd C: per-pixel geometry, flat order
+      if (lane == 0) part_rows[b0 + m] = C << 16;
+      const int nq = vec ? C2 / 4 : C2;
+      const int per = vec ? 4 : 1;
+      for (int q = lane; q < nq; q += 64) {
+        float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        int pix = q * per;
+        int i = pix / C, j = pix - (pix / C) * C;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (e < per) {
+            const Tap t = stn_tap(&sth[m][6], 28, 28, mog_linspace(j, C), mog_linspace(i, C));
+            v[e] = t.dead ? 0.0f : zn * tap_value(t, U);
+            if (++j == C) { j = 0; ++i; }
+          }
+        }
+        if (vec) st_stream(reinterpret_cast<floatx4*>(om4 + q), floatx4{v[0], v[1], v[2], v[3]});
+        else st_stream(om + q, v[0]);
+      }
+    }
+    wave_lds_sync();  // the slot is rewritten for the next image
+  }
+}
+
 template <int MT, int NW, int OCC, int LA = 3>
 __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) {
 #pragma clang fp contract(off)
@@ -740,7 +864,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   const int lane = tid & 63;
   const int b0 = blockIdx.x * M;
   const int nb = min(M, p.B - b0);
-  const int C = p.C, C2 = C * C;
+  const int C = p.C;
   STAMP(11);
 
   for (int i = tid; i < M * 12; i += NTHR) {
@@ -969,124 +1093,488 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   lds_barrier();
   STAMP(8);
   STAMP(9);
-  // ---- 9. STN write (air_model.py:580-588): this step's canvas part -------
-  // part = active ? z * w : 0 (mog_recon_loss sums the parts in step order).
-  // r is staged back one image per wave into the wave's LDS slot; the lanes
-  // walk the image's pixel pairs and store 8 bytes each.  Only rows whose
-  // clipped corner rows differ can be nonzero; the even-aligned range of them
-  // is stored and recorded.
-  if (p.phases & 8) {
-    // Wave-private: wave wv writes images wv, wv + NW, ... from its own LDS
-    // slot (r of one image); the next image's r is
-    // fetched into registers while the current one is computed, and the
-    // waves meet no workgroup barrier, so their memory and VALU phases drift
-    // apart and overlap.
-    const bool vec = (C2 & 3) == 0;  // even C: 16-byte aligned image rows of parts
-    unsigned char* slot = arena + wv * Ly::WSLOT;
-    float* sRw = reinterpret_cast<float*>(slot);
-    constexpr int NQ = (W2 / 4 + 63) / 64;
-    float4 tmp[NQ];
-    auto fetch = [&](int m) {
-      const float4* src = reinterpret_cast<const float4*>(p.r + (size_t)(b0 + m) * W2);
-#pragma unroll
-      for (int it = 0; it < NQ; ++it) {
-        const int i = lane + it * 64;
-        if (i < W2 / 4) tmp[it] = src[i];
-      }
-    };
-    if (wv < nb) fetch(wv);
-    for (int m = wv; m < nb; m += NW) {
-#pragma unroll
-      for (int it = 0; it < NQ; ++it) {
-        const int i = lane + it * 64;
-        if (i < W2 / 4) reinterpret_cast<float4*>(sRw)[i] = tmp[it];
-      }
-      wave_lds_sync();
-      if (m + NW < nb) fetch(m + NW);
-      float* om = p.part + (size_t)(b0 + m) * C2;
-      float4* om4 = reinterpret_cast<float4*>(om);
-      const float* U = sRw;
-      const bool act = smask[m] != 0, tab = (ssep[m] & 2) != 0;
-      const float zn = szv[m];
-      if (!act) {  // inactive: the whole part is +0 -- nothing stored
-        if (lane == 0) p.part_rows[b0 + m] = 0;
-      } else if (tab && vec && C <= CTAB_MAX) {
-        // Only rows whose clipped corner rows differ can be nonzero (a row
-        // with coinciding corner rows samples exactly +0 at every column:
-        // the y weights are exact negatives on one source row, and within
-        // a live row no sample is dead): store the even-aligned range
-        // [rlo, rhi) of such rows and record it.  Lane i holds row entry i
-        // in registers; a pass reads rows r, r + 1 with readlane.
-        const float4 el = axis4(axis_row(&sth[m][6], 28, 28, C, C, lane < C ? lane : 0), 4 * 28);
-        const unsigned long long lm =
-            __builtin_amdgcn_ballot_w64(lane < C && __float_as_int(el.x) != __float_as_int(el.y));
-        const int rlo = lm ? (__builtin_ctzll(lm) & ~1) : 0;
-        const int rhi = lm ? min(C, (64 - __builtin_clzll(lm) + 1) & ~1) : 0;
-        if (lane == 0) p.part_rows[b0 + m] = rlo | (rhi << 16);
-        // Lane -> pixel pair pr of row r + half (PR pairs per row, two rows
-        // per pass; C = 50 leaves 14 lanes idle): the column geometry stays
-        // in registers, and a corner pair (x0, x0 + 1) of a source row is
-        // one ds_read2 -- a live column has x1 = x0 + 1, a dead one x1 = x0
-        // (its second corner is the first).  Same products and summation
-        // order as sample4, per pixel.
-        const int PR = C >> 1, half = lane >= PR ? 1 : 0, pr = lane - half * PR;
-        const bool on = lane < 2 * PR;
-        const float4 e0 = axis4(axis_col(&sth[m][6], 28, 28, C, C, on ? 2 * pr : 0), 4);
-        const float4 e1 = axis4(axis_col(&sth[m][6], 28, 28, C, C, on ? 2 * pr + 1 : 0), 4);
-        const int a0 = __float_as_int(e0.x), a1 = __float_as_int(e1.x);
-        const bool dd0 = a0 == __float_as_int(e0.y), dd1 = a1 == __float_as_int(e1.y);
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        const f2 xz = {e0.z, e1.z}, xw = {e0.w, e1.w};
-        const char* Ub = reinterpret_cast<const char*>(sRw);
-        auto ld = [Ub](int a, int b) { return *reinterpret_cast<const float*>(Ub + a + b); };
-        f2* dst = reinterpret_cast<f2*>(om + (rlo + half) * C) + pr;
-        const int eyx = __float_as_int(el.x), eyy = __float_as_int(el.y);
-        const int eyz = __float_as_int(el.z), eyw = __float_as_int(el.w);
-        for (int r = rlo; r < rhi; r += 2) {
-          // (readlane takes a uniform lane: both rows' entries, then select)
-          const int y0a = __builtin_amdgcn_readlane(eyx, r), y0b = __builtin_amdgcn_readlane(eyx, r + 1);
-          const int y1a = __builtin_amdgcn_readlane(eyy, r), y1b = __builtin_amdgcn_readlane(eyy, r + 1);
-          const int za = __builtin_amdgcn_readlane(eyz, r), zb = __builtin_amdgcn_readlane(eyz, r + 1);
-          const int wa_ = __builtin_amdgcn_readlane(eyw, r), wb_ = __builtin_amdgcn_readlane(eyw, r + 1);
-          const int y0 = half ? y0b : y0a, y1 = half ? y1b : y1a;
-          const float ez = __int_as_float(half ? zb : za), ew = __int_as_float(half ? wb_ : wa_);
-          if (on) {
-            const f2 Ia = {ld(y0, a0), ld(y0, a1)}, Ib = {ld(y1, a0), ld(y1, a1)};
-            const f2 In = {ld(y0, a0 + 4), ld(y0, a1 + 4)}, Jn = {ld(y1, a0 + 4), ld(y1, a1 + 4)};
-            const f2 Ic = {dd0 ? Ia.x : In.x, dd1 ? Ia.y : In.y};
-            const f2 Id = {dd0 ? Ib.x : Jn.x, dd1 ? Ib.y : Jn.y};
-            const f2 wa = xz * ez, wb = xz * ew, wc = xw * ez, wd = xw * ew;
-            const f2 sv = ((wa * Ia + wb * Ib) + wc * Ic) + wd * Id;
-            st_stream(dst, zn * sv);
-          }
-          dst += C;  // two rows of C / 2 pairs
-        }
-      } else {  // general transform or odd C: per-pixel geometry, flat order
-        if (lane == 0) p.part_rows[b0 + m] = C << 16;
-        const int nq = vec ? C2 / 4 : C2;
-        const int per = vec ? 4 : 1;
-        for (int q = lane; q < nq; q += 64) {
-          float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-          int pix = q * per;
-          int i = pix / C, j = pix - (pix / C) * C;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (e < per) {
-              const Tap t = stn_tap(&sth[m][6], 28, 28, mog_linspace(j, C), mog_linspace(i, C));
-              v[e] = t.dead ? 0.0f : zn * tap_value(t, U);
-              if (++j == C) { j = 0; ++i; }
-            }
-          }
-          if (vec) st_stream(reinterpret_cast<floatx4*>(om4 + q), floatx4{v[0], v[1], v[2], v[3]});
-          else st_stream(om + q, v[0]);
-        }
-      }
-      wave_lds_sync();  // the slot is rewritten for the next image
-    }
-  }
+  // ---- 9. STN write (stn_write_tile) --------------------------------------
+  if (p.phases & 8)
+    stn_write_tile<NW>(p.r, p.part, p.part_rows, C, arena, Ly::WSLOT, sth, smask, ssep, szv, b0, nb,
+                       wv, lane);
   if (p.tstamp) {
     lds_barrier();
     STAMP(10);
+  }
+}
+
+
+// ===========================================================================
+// fp32 step kernel: the reference-precision form of the same fused step
+// (air_model.py:523-588, vae.py:5-48, transformer.py:18-175 at fp32),
+// bit-identical to the unfused fp32 sequence -- stn_forward, the seven
+// mog_gemm_f32 chains with their exact epilogues and pre-activations,
+// vae_sample_forward, mog_gemm_f32_sigmoid_philox, mog_stn_write_parts.
+// Dense layers on v_mfma_f32_16x16x4_f32 fed in natural k order (MFMA kk of
+// k-step ks takes k = 16 ks + 4 kk + g from lane group g), so every output is
+// the one k-ordered fma chain of gemm_f32.hip, then + bias, then the
+// epilogue.  A tile is 32 images x 16 waves (fp32 activations are twice the
+// bf16 bytes); the layers are MFMA-bound (141 MFLOP per 64 images), so the
+// phases need no overlap beyond the read / recognition split:
+//   * LDS activations are rows of k PERMUTED inside each 16-group (k = 16 s +
+//     4 j + g at 16 s + 4 g + j), so lane (row, g) reads its four k-slots of a
+//     k-step with one ds_read_b128;
+//   * weights are fp32 B-fragment packs (mog_pack_frag_f32): fragment (ks, ct)
+//     is 1 KiB, lane (li, g) holds W[16 ks + 4 kk + g][16 ct + li], kk < 4;
+//   * epilogues write pre- and post-activation rows to HBM (16-byte stores
+//     after the quad transpose) and the post-activation into the next layer's
+//     permuted LDS rows.
+constexpr int FM = 32;             // images per tile
+constexpr int FKS1 = 49;           // recognition k-steps (784 = 49 x 16: no padding)
+constexpr int FKG = 7;             // k-steps per glimpse slab
+constexpr int FSK = 16 * FKG + 4;  // slab row stride (floats)
+constexpr int FS512 = 512 + 4, FS256 = 256 + 4, FSZ = 64 + 4, FS50 = 52;
+static_assert(FKS1 % FKG == 0, "slabs");
+
+// LDS arena (bytes): tables + two glimpse slabs during the read; R1 = a1 ->
+// mu | lv | kl | z -> d2; R2 = a2 -> d1; write slots (r of one image per wave)
+struct LayF {
+  static constexpr int TAB = FM * TABR * 16;
+  static constexpr int KB = FM * FSK * 4;
+  static constexpr int R1 = FM * FS512 * 4;
+  static constexpr int OFF_R2 = R1, R2 = FM * FS256 * 4;
+  static constexpr int OFF_MU = 0, OFF_LV = FM * FS50 * 4, OFF_KL = 2 * FM * FS50 * 4,
+                       OFF_Z = 3 * FM * FS50 * 4;
+  static constexpr int WSLOT = W2 * 4;
+  static constexpr int ARENA0 = cmax(OFF_R2 + R2, cmax(TAB + 2 * KB, 16 * WSLOT));
+  static constexpr int OFF_EZ = ARENA0;
+  static constexpr int ARENA = ARENA0 + FM * 50 * 4;
+  static_assert(OFF_Z + FM * FSZ * 4 <= R1, "mu / lv / kl / z inside R1");
+};
+
+struct StepArgsF {
+  const float* x;
+  const float* theta_f;
+  const float* theta_b;
+  const float* mask;
+  const float* zval;
+  const float* eps_z;
+  const float* eps_x;
+  unsigned long long eps_seed, eps_offset;
+  int eps_gen;
+  const float* wt[7];  // fp32 B-fragment packs: r1, r2, mu, lv, g1, g2, go
+  const float* bias[7];
+  float* part;
+  int* part_rows;
+  float* runloss;
+  float* vkl;
+  float* g;                  // [B, 784]  saved for the backward (may be null: forward only)
+  float *a1pre, *a1;         // [B, 512]
+  float *a2pre, *a2;         // [B, 256]
+  float *mu, *lv, *z;        // [B, 50]   (z always written)
+  float *d1pre, *d1;         // [B, 256]
+  float *d2pre, *d2;         // [B, 512]
+  float* r;                  // [B, 784]  (always written)
+  int B, C;
+  int x_period;
+  float lik_std, v_pm, v_pv, v_plv;
+  int phases;                // (always all: the profiling masks are the bf16 kernel's)
+  long long* tstamp;
+};
+
+// position of k inside a permuted row
+__device__ __forceinline__ int kperm(int k) { return (k & ~15) | ((k & 3) << 2) | ((k >> 2) & 3); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frag_rsrc_f32(const float* W) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W), 0, 0x7ffffff0, 0x00020000);
+}
+template <int NCT>
+__device__ __forceinline__ floatx4 load_frag_f32(__amdgpu_buffer_rsrc_t r, int voff, int ks) {
+  return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, ks * NCT * 1024, 0));
+}
+
+// One fp32 dense layer over row tiles [0, MT) (rows from A + row0 * lda) and
+// the column tiles of waves wbase .. wbase + nw - 1: wave w owns column tiles
+// tile_base + (w + nw c + rot) % (nw TPW), c < TPW.  No barrier inside.
+// epi(m, n0, v, b): row m, columns n0 .. n0+3 (quad-transposed), biases b.
+template <int MT, int KS, int NCT, int TPW, int D, class Epi>
+__device__ __forceinline__ void dense_f32(const float* A, int lda, const float* W,
+                                          const float* __restrict__ bias, int N, int tile_base,
+                                          int wbase, int nw, Epi epi, int tid) {
+  const int rot = (int)(blockIdx.x >> 3);
+  const int lane = tid & 63, w = (tid >> 6) - wbase;
+  if (w < 0 || w >= nw) return;
+  const int li = lane & 15, g = lane >> 4;
+  int ct[TPW], wo[TPW];
+  const __amdgpu_buffer_rsrc_t wr = frag_rsrc_f32(W);
+  floatx4 bq[TPW];
+#pragma unroll
+  for (int c = 0; c < TPW; ++c) {
+    ct[c] = tile_base + (w + nw * c + rot) % (nw * TPW);
+    wo[c] = frag_voff(ct[c], lane);
+    bq[c] = load_bias4(bias, ct[c] * 16 + (li & ~3), N);
+  }
+  floatx4 acc[MT][TPW];
+#pragma unroll
+  for (int rt = 0; rt < MT; ++rt)
+#pragma unroll
+    for (int c = 0; c < TPW; ++c) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  floatx4 q[D][TPW];
+  auto loadB = [&](int ks, floatx4* b) {
+#pragma unroll
+    for (int c = 0; c < TPW; ++c) b[c] = load_frag_f32<NCT>(wr, wo[c], ks);
+  };
+#pragma unroll
+  for (int d = 0; d < D && d < KS; ++d) loadB(d, q[d]);
+  static_for<0, KS>([&](auto kc) {
+    constexpr int ks = decltype(kc)::value;
+    floatx4 a[MT];
+#pragma unroll
+    for (int rt = 0; rt < MT; ++rt)
+      a[rt] = *reinterpret_cast<const floatx4*>(&A[(rt * 16 + li) * lda + 16 * ks + 4 * g]);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int rt = 0; rt < MT; ++rt)
+#pragma unroll
+        for (int c = 0; c < TPW; ++c)
+          acc[rt][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][kk], q[ks % D][c][kk], acc[rt][c],
+                                                            0, 0, 0);
+    if constexpr (ks + D < KS) loadB(ks + D, q[ks % D]);
+  });
+#pragma unroll
+  for (int c = 0; c < TPW; ++c)
+#pragma unroll
+    for (int rt = 0; rt < MT; ++rt)
+      epi(rt * 16 + g * 4 + (li & 3), ct[c] * 16 + (li & ~3), quad_transpose(acc[rt][c], tid), bq[c]);
+}
+
+__global__ __launch_bounds__(1024, 1) void stn_vae_step_f32_kernel(StepArgsF p) {
+#pragma clang fp contract(off)
+  constexpr int M = FM, NW = 16, NTHR = 1024;
+  __shared__ __attribute__((aligned(16))) unsigned char arena[LayF::ARENA];
+  __shared__ float sth[M][12];
+  __shared__ float szv[M];
+  __shared__ int smask[M];
+  __shared__ int ssep[M];
+  const int tid = threadIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, li = lane & 15, g = lane >> 4;
+  const int b0 = blockIdx.x * M;
+  const int nb = min(M, p.B - b0);
+  const int C = p.C, C2 = C * C;
+  STAMP(11);
+  // ---- prologue: the bf16 kernel's (thetas, masks, read tables, eps_z) -----
+  for (int i = tid; i < M * 12; i += NTHR) {
+    const int m = i / 12, k = i % 12;
+    float v = 0.0f;
+    if (m < nb) v = k < 6 ? p.theta_f[(size_t)(b0 + m) * 6 + k] : p.theta_b[(size_t)(b0 + m) * 6 + k - 6];
+    sth[m][k] = v;
+  }
+  if (tid < M) {
+    const bool act = tid < nb && p.mask[b0 + tid] != 0.0f;
+    smask[tid] = act;
+    szv[tid] = act ? p.zval[b0 + tid] : 0.0f;
+  }
+  lds_barrier();
+  bool sep_f = true;
+  if (tid < M) {
+    sep_f = stn_separable(&sth[tid][0]);
+    ssep[tid] = (sep_f ? 1 : 0) | (stn_separable(&sth[tid][6]) && C <= CTAB_MAX ? 2 : 0);
+  }
+  {
+    float4* tabR = reinterpret_cast<float4*>(arena);
+    for (int i = tid; i < M * TABR; i += NTHR) {
+      const int m = i / TABR, n = i - (i / TABR) * TABR;
+      const float* th = sth[m];
+      tabR[i] = n < 28 ? col_pair4(axis_col(th, C, C, 28, 28, n), C)
+                       : axis4(axis_row(th, C, C, 28, 28, n - 28), 4 * C);
+    }
+  }
+  {
+    float* sEz = reinterpret_cast<float*>(arena + LayF::OFF_EZ);
+    for (int i = tid; i < nb * 50; i += NTHR) sEz[i] = p.eps_z[(size_t)b0 * 50 + i];
+  }
+  const bool all_sep = __syncthreads_and(sep_f) != 0;
+  STAMP(0);
+  const bool save = p.a1 != nullptr;
+
+  // ---- 1+2. STN read (transformer.py:18-175) -> a1 = softplus(g W1 + b1) --
+  // Waves 8-15 sample (lane: image (wv - 8) * 4 + (lane >> 4), pixel 16 ks +
+  // (lane & 15) of k-step ks) into two LDS slabs of FKG k-steps and store g;
+  // waves 0-7 run the MFMAs (four of the 32 column tiles each) on the other
+  // slab; one barrier per slab.
+  {
+    const float4* tabR = reinterpret_cast<const float4*>(arena);
+    floatx4 acc[2][4];
+    int ct[4];
+    if (wv >= 8) {
+      constexpr int LA = 4;
+      const int m = (wv - 8) * 4 + (lane >> 4), kk = lane & 15;
+      const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(p.x) + (size_t)(b0 % p.x_period) * C2, 0, nb * C2 * 4, 0x00020000);
+      const int xo = m * C2 * 4;
+      float I[LA][4];
+      auto geom = [&](int ks, float4& ex, float4& ey) {
+        const int k = 16 * ks + kk;
+        if (all_sep) {
+          const int i = k / 28, j = k - (k / 28) * 28;
+          ex = tabR[m * TABR + j];
+          ey = tabR[m * TABR + 28 + i];
+        } else {
+          glimpse_geom<false>(tabR, sth[m], m, k, C, ex, ey);
+        }
+      };
+      auto gather = [&](int ks, float (&v)[4]) {
+        float4 ex, ey;
+        geom(ks, ex, ey);
+        const int xb = __float_as_int(ex.x) + xo;
+        const u32x2 r0 = __builtin_amdgcn_raw_buffer_load_b64(xr, xb + __float_as_int(ey.x), 0, 0);
+        const u32x2 r1 = __builtin_amdgcn_raw_buffer_load_b64(xr, xb + __float_as_int(ey.y), 0, 0);
+        v[0] = __uint_as_float(r0[0]);
+        v[1] = __uint_as_float(r0[1]);
+        v[2] = __uint_as_float(r1[0]);
+        v[3] = __uint_as_float(r1[1]);
+      };
+      float* gdst = (save && m < nb) ? p.g + (size_t)(b0 + m) * W2 + kk : nullptr;
+      const int so = LayF::TAB + (m * FSK + ((kk & 3) << 2) + (kk >> 2)) * 4;
+      auto sample = [&](int ks, const float (&v)[4]) {
+        float4 ex, ey;
+        geom(ks, ex, ey);
+        const int fl = __float_as_int(ex.y);
+        const float Ia = (fl & 1) ? v[1] : v[0], Ib = (fl & 1) ? v[3] : v[2];
+        const float Ic = (fl & 2) ? v[1] : v[0], Id = (fl & 2) ? v[3] : v[2];
+        const int xlive = (fl ^ (fl >> 1)) & 1;
+        const int ylive = __float_as_int(ey.x) != __float_as_int(ey.y) ? 1 : 0;
+        const int live = (int)(m < nb) & (xlive | ylive);
+        const float s = sample4(ex, ey, Ia, Ib, Ic, Id);
+        const float val = live ? s : 0.0f;
+        const int slab = (ks / FKG) & 1;
+        *reinterpret_cast<float*>(arena + so + slab * LayF::KB + (ks % FKG) * 64) = val;
+        if (gdst) st_stream(gdst + 16 * ks, val);
+      };
+#pragma unroll
+      for (int k = 0; k < LA; ++k) gather(k, I[k]);
+      static_for<0, FKS1>([&](auto kc) {
+        constexpr int ks = decltype(kc)::value;
+        sample(ks, I[ks % LA]);
+        if constexpr (ks + LA < FKS1) gather(ks + LA, I[ks % LA]);
+        if constexpr (ks % FKG == FKG - 1) lds_barrier();  // slab filled
+      });
+      lds_barrier();  // the MFMA waves are done with the last slab
+    } else {
+      const int rot = (int)(blockIdx.x >> 3);
+      const __amdgpu_buffer_rsrc_t wr = frag_rsrc_f32(p.wt[0]);
+      int wo[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        ct[c] = (wv + 8 * c + rot) % 32;
+        wo[c] = frag_voff(ct[c], lane);
+      }
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+      constexpr int DB = 2;
+      floatx4 q[DB][4];
+      auto loadB = [&](int ks, floatx4* b) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) b[c] = load_frag_f32<32>(wr, wo[c], ks);
+      };
+#pragma unroll
+      for (int d = 0; d < DB; ++d) loadB(d, q[d]);
+      const int ao = LayF::TAB + (li * FSK + 4 * g) * 4;
+      lds_barrier();  // slab 0 filled
+      static_for<0, FKS1>([&](auto kc) {
+        constexpr int ks = decltype(kc)::value;
+        const unsigned char* sa = arena + ao + ((ks / FKG) & 1) * LayF::KB + (ks % FKG) * 64;
+        floatx4 a[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) a[rt] = *reinterpret_cast<const floatx4*>(sa + rt * 16 * FSK * 4);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              acc[rt][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][kk], q[ks % DB][c][kk],
+                                                                acc[rt][c], 0, 0, 0);
+        if constexpr (ks + DB < FKS1) loadB(ks + DB, q[ks % DB]);
+        if constexpr (ks % FKG == FKG - 1) lds_barrier();  // slab consumed / next filled
+      });
+    }
+    STAMP(1);
+    if (wv < 8) {  // a1 epilogue (the slabs are dead: every wave passed the last barrier)
+      float* sA1 = reinterpret_cast<float*>(arena);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int n0 = ct[c] * 16 + (li & ~3);
+        const floatx4 b = load_bias4(p.bias[0], n0, 512);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          const int mrow = rt * 16 + g * 4 + (li & 3);
+          const floatx4 v = quad_transpose(acc[rt][c], tid);
+          floatx4 pre, post;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pre[j] = v[j] + b[j];
+            post[j] = mog_softplusf(pre[j]);
+            sA1[mrow * FS512 + kperm(n0 + j)] = post[j];
+          }
+          if (save && mrow < nb) {
+            st_stream(reinterpret_cast<floatx4*>(p.a1pre + (size_t)(b0 + mrow) * 512 + n0), pre);
+            st_stream(reinterpret_cast<floatx4*>(p.a1 + (size_t)(b0 + mrow) * 512 + n0), post);
+          }
+        }
+      }
+    }
+  }
+  lds_barrier();
+  STAMP(2);
+  // softplus layer epilogue: pre / post rows to HBM, post into the next
+  // layer's permuted LDS rows
+  auto sp_epi = [&](float* dst, int ldd, float* gpre, float* gpost, int ldg) {
+    return [=](int m, int n0, const floatx4& v, const floatx4& b) {
+      floatx4 pre, post;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pre[j] = v[j] + b[j];
+        post[j] = mog_softplusf(pre[j]);
+        dst[m * ldd + kperm(n0 + j)] = post[j];
+      }
+      if (gpre != nullptr && m < nb) {
+        st_stream(reinterpret_cast<floatx4*>(gpre + (size_t)(b0 + m) * ldg + n0), pre);
+        st_stream(reinterpret_cast<floatx4*>(gpost + (size_t)(b0 + m) * ldg + n0), post);
+      }
+    };
+  };
+  float* sR1 = reinterpret_cast<float*>(arena);
+  float* sR2 = reinterpret_cast<float*>(arena + LayF::OFF_R2);
+  // ---- 3. a2 = softplus(a1 W2 + b2) [M x 256] -> R2 ------------------------
+  dense_f32<2, 32, 16, 1, 4>(sR1, FS512, p.wt[1], p.bias[1], 256, 0, 0, NW,
+                             sp_epi(sR2, FS256, save ? p.a2pre : nullptr, p.a2, 256), tid);
+  lds_barrier();
+  STAMP(3);
+  // ---- 4. mu | lv = a2 W + b [M x 50] (waves 0-3 | 4-7) -> R1 -------------
+  float* sMu = reinterpret_cast<float*>(arena + LayF::OFF_MU);
+  float* sLv = reinterpret_cast<float*>(arena + LayF::OFF_LV);
+  {
+    auto epi50 = [&](float* dst) {
+      return [dst](int m, int n0, const floatx4& v, const floatx4& b) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (n0 + j < 50) dst[m * FS50 + n0 + j] = v[j] + b[j];
+      };
+    };
+    dense_f32<2, 16, 4, 1, 4>(sR2, FS256, p.wt[2], p.bias[2], 50, 0, 0, 4, epi50(sMu), tid);
+    dense_f32<2, 16, 4, 1, 4>(sR2, FS256, p.wt[3], p.bias[3], 50, 0, 4, 4, epi50(sLv), tid);
+  }
+  lds_barrier();
+  STAMP(4);
+  // ---- 5. z = mu + eps sqrt(exp(lv)); VAE KL (vae.py:27-30) -> R1 ---------
+  float* sKl = reinterpret_cast<float*>(arena + LayF::OFF_KL);
+  float* sZ = reinterpret_cast<float*>(arena + LayF::OFF_Z);
+  {
+    const float* sEz = reinterpret_cast<const float*>(arena + LayF::OFF_EZ);
+#pragma unroll
+    for (int it = 0; it < M * 64 / NTHR; ++it) {
+      const int i = tid + it * NTHR, m = i >> 6, k = i & 63;
+      float zv = 0.0f;
+      if (k < 50 && m < nb) {
+        const size_t o = (size_t)(b0 + m) * 50 + k;
+        const float l = sLv[m * FS50 + k];
+        const float mv = sMu[m * FS50 + k];
+        const float var = mog_expf(l);
+        zv = mv + sEz[m * 50 + k] * sqrtf(var);
+        st_stream(p.z + o, zv);
+        if (save) {
+          st_stream(p.mu + o, mv);
+          st_stream(p.lv + o, l);
+        }
+        const float d = mv - p.v_pm;
+        sKl[m * 50 + k] = (((p.v_plv - l) - 1.0f) + var / p.v_pv) + (d * d) / p.v_pv;
+      }
+      sZ[m * FSZ + kperm(k)] = zv;
+    }
+  }
+  lds_barrier();
+  if (tid < nb) {  // sequential KL sum per image (k order, as vae_sample_fwd_kernel)
+    const int m = tid;
+    float sum = 0.0f;
+    for (int k = 0; k < 50; ++k) sum = sum + sKl[m * 50 + k];
+    const float vkl = 0.5f * sum;
+    p.vkl[b0 + m] = vkl;
+    if (p.runloss && smask[m]) p.runloss[b0 + m] = p.runloss[b0 + m] + vkl;
+  }
+  STAMP(5);
+  // ---- 6. d1 = softplus(z Wg1 + b) [M x 256] -> R2 (K = 50 padded to 64) --
+  dense_f32<2, 4, 16, 1, 4>(sZ, FSZ, p.wt[4], p.bias[4], 256, 0, 0, NW,
+                            sp_epi(sR2, FS256, save ? p.d1pre : nullptr, p.d1, 256), tid);
+  lds_barrier();
+  STAMP(6);
+  // ---- 7. d2 = softplus(d1 Wg2 + b) [M x 512] -> R1 -------------------------
+  dense_f32<2, 16, 32, 2, 4>(sR2, FS256, p.wt[5], p.bias[5], 512, 0, 0, NW,
+                             sp_epi(sR1, FS512, save ? p.d2pre : nullptr, p.d2, 512), tid);
+  lds_barrier();
+  STAMP(7);
+  // ---- 8. r = sigmoid((d2 Wgo + b) + std eps) [M x 784] -> HBM ------------
+  // (gemm_f32's EPI_SIGMOID_NOISE: eps_x from the Philox quad of (row, col / 4)
+  // or read; 49 column tiles: 48 over the 16 waves, the last split by rows)
+  {
+    const float sd = p.lik_std;
+    auto epi = [&](int m, int n0, const floatx4& v, const floatx4& b) {
+      if (m >= nb) return;
+      float e[4];
+      const size_t q = (size_t)(b0 + m) * (W2 / 4) + (n0 >> 2);
+      if (p.eps_gen) {
+        mog_philox_quad(p.eps_seed, p.eps_offset + q, true, e);
+      } else {
+        const float4 e4 = reinterpret_cast<const float4*>(p.eps_x)[q];
+        e[0] = e4.x; e[1] = e4.y; e[2] = e4.z; e[3] = e4.w;
+      }
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float w = v[j] + b[j];
+        o[j] = mog_sigmoidf(w + e[j] * sd);
+      }
+      reinterpret_cast<float4*>(p.r)[q] = make_float4(o[0], o[1], o[2], o[3]);
+    };
+    dense_f32<2, 32, 49, 3, 4>(sR1, FS512, p.wt[6], p.bias[6], W2, 0, 0, NW, epi, tid);
+    if (wv >= 14) {  // column tile 48: row tile wv - 14
+      const int rt = wv - 14;
+      dense_f32<1, 32, 49, 1, 4>(sR1 + rt * 16 * FS512, FS512, p.wt[6], p.bias[6], W2, 48, 14, 1,
+                                 [&](int m, int n0, const floatx4& v, const floatx4& b) {
+                                   epi(m + rt * 16, n0, v, b);
+                                 },
+                                 tid - rt * 64);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // r stores done before other waves read it
+  lds_barrier();
+  STAMP(8);
+  STAMP(9);
+  // ---- 9. STN write: the bf16 kernel's (stn_write_tile) ---------------------
+  stn_write_tile<NW>(p.r, p.part, p.part_rows, C, arena, LayF::WSLOT, sth, smask, ssep, szv, b0,
+                     nb, wv, lane);
+  if (p.tstamp) {
+    lds_barrier();
+    STAMP(10);
+  }
+}
+
+// W [K][N] row-major fp32 -> B-fragment pack ((ks * NCT + ct) * 64 + lane) * 4
+// + kk = W[16 ks + 4 kk + g][16 ct + li] (lane = 16 g + li), zero outside.
+struct PackF32 {
+  const float* W[8];
+  float* out[8];
+  int K[8], N[8];
+};
+__global__ __launch_bounds__(256) void pack_frag_f32_kernel(PackF32 a) {
+  const int L = blockIdx.y;
+  const int K = a.K[L], N = a.N[L], KS = (K + 15) / 16, NCT = (N + 15) / 16;
+  const long total = (long)KS * NCT * 256;
+  for (long o = (long)blockIdx.x * 256 + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
+    const int kk = (int)(o & 3), lane = (int)((o >> 2) & 63);
+    const long f = o >> 8;
+    const int ct = (int)(f % NCT), ks = (int)(f / NCT);
+    const int k = 16 * ks + 4 * kk + (lane >> 4), n = 16 * ct + (lane & 15);
+    a.out[L][o] = (k < K && n < N) ? a.W[L][(size_t)k * N + n] : 0.0f;
   }
 }
 
@@ -1188,6 +1676,98 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
     }
     fprintf(stderr, "stn_vae_step M=%d phases (us, mean over %u blocks; 100 MHz clock): prologue %.2f",
             M, nblk, pro / nblk / 100.0);
+    for (int k = 0; k < 10; ++k) fprintf(stderr, " %s %.2f", names[k], acc[k] / nblk / 100.0);
+    fprintf(stderr, " | block %.2f | span %.2f\n", acc[10] / nblk / 100.0, (t1 - t0) / 100.0);
+  }
+  MOG_LAUNCH_RET();
+}
+
+// fp32 B-fragment packs of n <= 8 weight matrices (W[i] [K[i]][N[i]] fp32 ->
+// out[i], (K + 15) / 16 * (N + 15) / 16 KiB), see stn_vae_step_f32_kernel
+extern "C" int mog_pack_frag_f32(int n, const float* const* W, const int* K, const int* N,
+                                 float* const* out, void* stream) {
+  MOG_CHECK_ARG(n >= 1 && n <= 8 && W && K && N && out);
+  PackF32 a = {};
+  long most = 0;
+  for (int i = 0; i < n; ++i) {
+    MOG_CHECK_ARG(W[i] && out[i] && K[i] > 0 && N[i] > 0);
+    a.W[i] = W[i]; a.out[i] = out[i]; a.K[i] = K[i]; a.N[i] = N[i];
+    most = std::max(most, (long)((K[i] + 15) / 16) * ((N[i] + 15) / 16) * 256);
+  }
+  const dim3 grid((unsigned)std::min<long>(1024, (most + 255) / 256), n);
+  pack_frag_f32_kernel<<<grid, 256, 0, mog_stream(stream)>>>(a);
+  MOG_LAUNCH_RET();
+}
+
+// The fp32 fused step (see stn_vae_step_f32_kernel): the arguments of
+// mog_stn_vae_step_forward with fp32 weight packs (mog_pack_frag_f32) and the
+// fp32 saved activations of the unfused sequence (g, a1pre, a1, a2pre, a2,
+// mu, lv, d1pre, d1, d2pre, d2: all given, or all NULL for a forward-only
+// step); z and r are always written.
+extern "C" int mog_stn_vae_step_forward_f32(
+    int B, int C, const float* x, const float* theta_f, const float* theta_b, const float* mask,
+    const float* zval, const float* eps_z, const float* eps_x, int eps_gen,
+    unsigned long long eps_seed, unsigned long long eps_offset, const float* const* wt,
+    const float* const* bias, float lik_std, float v_pm, float v_pv, float v_plv,
+    float* canvas_part, int* part_rows, float* runloss, float* vkl, float* g, float* a1pre,
+    float* a1, float* a2pre, float* a2, float* mu, float* lv, float* z, float* d1pre, float* d1,
+    float* d2pre, float* d2, float* r, int x_period, void* stream) {
+  MOG_CHECK_ARG(B >= 0 && C >= 2 && C * C <= 16384);
+  MOG_CHECK_ARG(x && theta_f && theta_b && mask && zval && eps_z && (eps_x || eps_gen) && wt && bias);
+  MOG_CHECK_ARG(canvas_part && part_rows && vkl && z && r);
+  const bool save = a1 != nullptr;
+  MOG_CHECK_ARG(!save || (g && a1pre && a2pre && a2 && mu && lv && d1pre && d1 && d2pre && d2));
+  MOG_CHECK_ARG(save || !(g || a1pre || a2pre || a2 || mu || lv || d1pre || d1 || d2pre || d2));
+  if (B == 0) return 0;
+  StepArgsF p;
+  p.x = x; p.theta_f = theta_f; p.theta_b = theta_b; p.mask = mask; p.zval = zval;
+  p.eps_z = eps_z; p.eps_x = eps_x;
+  p.eps_gen = eps_gen; p.eps_seed = eps_seed; p.eps_offset = eps_offset;
+  for (int i = 0; i < 7; ++i) {
+    MOG_CHECK_ARG(wt[i] && bias[i]);
+    p.wt[i] = wt[i];
+    p.bias[i] = bias[i];
+  }
+  p.part = canvas_part; p.part_rows = part_rows; p.runloss = runloss; p.vkl = vkl;
+  p.g = g; p.a1pre = a1pre; p.a1 = a1; p.a2pre = a2pre; p.a2 = a2; p.mu = mu; p.lv = lv; p.z = z;
+  p.d1pre = d1pre; p.d1 = d1; p.d2pre = d2pre; p.d2 = d2; p.r = r;
+  p.B = B; p.C = C; p.lik_std = lik_std; p.v_pm = v_pm; p.v_pv = v_pv; p.v_plv = v_plv;
+  p.x_period = x_period > 0 ? x_period : B;
+  p.phases = 31;
+  // a tile must not straddle two periods of x; several steps' rows in one
+  // launch rule out the running loss (mog_air_runloss replays it)
+  MOG_CHECK_ARG(p.x_period == B || (p.x_period % FM == 0 && !runloss));
+  hipStream_t s = mog_stream(stream);
+  const unsigned nblk = mog_cdiv(B, FM);
+  static long long* tbuf = nullptr;
+  static size_t tcap = 0;
+  p.tstamp = nullptr;
+  if (getenv("MOG_VS_TIMING")) {
+    if (tcap < (size_t)nblk * 16) {
+      if (tbuf) (void)hipFree(tbuf);
+      tcap = (size_t)nblk * 16;
+      if (hipMalloc(&tbuf, tcap * sizeof(long long)) != hipSuccess) return MOG_ERR_INVALID;
+    }
+    p.tstamp = tbuf;
+  }
+  stn_vae_step_f32_kernel<<<nblk, 1024, 0, s>>>(p);
+  if (p.tstamp) {
+    std::vector<long long> h((size_t)nblk * 16);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), tbuf, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
+    static const char* names[10] = {"read+L1", "L1epi", "L2", "mu_lv", "sample",
+                                    "g1", "g2", "go", "-", "write"};
+    double acc[11] = {0}, pro = 0;
+    long long t0 = h[0], t1 = h[10];
+    for (unsigned b = 0; b < nblk; ++b) {
+      for (int k = 0; k < 10; ++k) acc[k] += (double)(h[b * 16 + k + 1] - h[b * 16 + k]);
+      acc[10] += (double)(h[b * 16 + 10] - h[b * 16]);
+      pro += (double)(h[b * 16] - h[b * 16 + 11]);
+      t0 = std::min(t0, h[b * 16]);
+      t1 = std::max(t1, h[b * 16 + 10]);
+    }
+    fprintf(stderr, "stn_vae_step_f32 M=%d phases (us, mean over %u blocks; 100 MHz clock): prologue %.2f",
+            FM, nblk, pro / nblk / 100.0);
     for (int k = 0; k < 10; ++k) fprintf(stderr, " %s %.2f", names[k], acc[k] / nblk / 100.0);
     fprintf(stderr, " | block %.2f | span %.2f\n", acc[10] / nblk / 100.0, (t1 - t0) / 100.0);
   }

@@ -39,6 +39,9 @@ _SIGS = {
     "mog_vae_sample_forward": [I, I, F, F, F, P, P, P, P, P, I, P, P, P, P],
     "mog_stn_vae_step_forward": ([I] * 8 + [P] * 7 + [I, ULL, ULL] + [P] * 2 + [F] * 4 + [P] * 14
                                  + [I, P]),
+    "mog_pack_frag_f32": [I, P, P, P, P, P],
+    "mog_stn_vae_step_forward_f32": ([I, I] + [P] * 7 + [I, ULL, ULL] + [P] * 2 + [F] * 4
+                                     + [P] * 19 + [I, P]),
     "mog_air_runloss": [I, I, P, L, P, P, P, P, P],
     "mog_stn_write_parts": [P, I, I, I, P, I, I, P, P, P, P, P],
     "mog_vae_sample_backward": [I, I, F, F, F, P, P, P, P, P, P, P, P, P, I, P],

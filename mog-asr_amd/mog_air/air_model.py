@@ -210,6 +210,13 @@ class AIRModel:
         self.fused_step = bool(fused_step) and precision == "bf16" and (
             windows_size == 28 and tuple(vae_recognition_units) == (512, 256)
             and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512))
+        # fp32: the same fused step at the reference precision over the T*B
+        # rows of the batched VAE (stn_vae_step_f32_kernel; MOG_FUSED_F32=0
+        # runs the unfused sequence it is bit-identical to)
+        self.fused_f32 = bool(fused_step) and precision == "fp32" and (
+            windows_size == 28 and tuple(vae_recognition_units) == (512, 256)
+            and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512)
+            and os.environ.get("MOG_FUSED_F32", "1") != "0")
         # the glimpse VAE of all T steps after the loop, over T*B rows (AIR).
         # (Measured and not kept: step 0's VAE on a second stream under the
         # rest of the recurrent loop -- no gain at B = 8192, slower at 64.)
@@ -513,6 +520,21 @@ class AIRModel:
                                r_(ws.cparts), r_(ws.prows), None, r_(ws.vkl), sv(ws.gb),
                                sv(ws.a1b), sv(ws.a2b), sv(ws.mu), sv(ws.lv), r_(ws.z), sv(ws.zb),
                                sv(ws.d1b), sv(ws.d2b), r_(ws.r), B)
+            return
+        if self.precision == "fp32" and self.fused_f32:
+            self._pack_f32()
+            gen = getattr(ws, "eps_x_offset", None) is not None
+            off = ws.eps_x_offset + t0 * B * (W2 // 4) if gen else 0
+            bias = [self._P("vae/" + n + "/biases") for n in self._VAE]
+            saved = [r_(getattr(ws, n)) if save else None
+                     for n in ("g", "a1pre", "a1", "a2pre", "a2", "mu", "lv", "d1pre", "d1",
+                               "d2pre", "d2")]
+            _ops.stn_vae_step_f32_(TB, C, X, r_(ws.th_f), r_(ws.th_b), r_(ws.zmask), r_(ws.zval),
+                                   r_(ws.eps_z), r_(ws.eps_x), ops._i64(self.noise_seed),
+                                   ops._i64(off), gen, self._wf32, bias, lik_std,
+                                   float(self.vae_prior_mean), float(self.vae_prior_variance),
+                                   self.vae_prior_log_variance, r_(ws.cparts), r_(ws.prows), None,
+                                   r_(ws.vkl), saved, r_(ws.z), r_(ws.r), B)
             return
         v = lambda a: a[t0:t1].reshape(TB, -1)  # noqa: E731
         vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
@@ -820,6 +842,26 @@ class AIRModel:
             self._pack_args = (srcs, dsts, dims)
         _ops.cvt_bf16_batch_(*self._pack_args)
         self._pack_version = self.params.version
+
+    def _pack_f32(self):
+        """Refresh the fp32 MFMA B-fragment packs of the VAE weights (the fp32
+        fused step's weight operand) after a parameter update: one launch."""
+        if getattr(self, "_pack32_version", None) == self.params.version:
+            return
+        if not hasattr(self, "_pack32_args"):
+            ws_, ks, ns, outs = [], [], [], []
+            for n in self._VAE:
+                w = self._P("vae/" + n + "/weights")
+                K, N = w.shape
+                ws_.append(w)
+                ks.append(int(K))
+                ns.append(int(N))
+                outs.append(torch.empty(((K + 15) // 16) * ((N + 15) // 16) * 256,
+                                        device=self.device))
+            self._wf32 = outs
+            self._pack32_args = (ws_, ks, ns, outs)
+        _ops.pack_frag_f32_(*self._pack32_args)
+        self._pack32_version = self.params.version
 
     def _vae_forward_bf16(self, X, ws, t, lik_std):
         from .ops import BF_SIGMOID_NOISE, BF_SOFTPLUS, BF_STORE, gemm_bf16
