@@ -166,10 +166,11 @@ def make_asr_model(precision, dev, scope, canvas=50, world=1, rank=0, cfg=None):
 
 
 def timed_train(precision, B, steps, warmup, dev, world=1, rank=0, events=False, scope="bench",
-                model=None, canvas=50, data=None):
+                model=None, canvas=50, data=None, graph=False):
     """Time `steps` train steps of batch B per rank (after `warmup`); returns
     (seconds, model).  Barrier + synchronize on both sides; the caller takes
-    the max over ranks.  data: synthetic() keywords (counts, side)."""
+    the max over ranks.  data: synthetic() keywords (counts, side).  graph:
+    the captured train step (AIRModel.train_step_graphed; one device)."""
     if model is None:
         model = make_model(precision, dev, world, rank, scope, canvas=canvas)
     if world > 1:
@@ -178,8 +179,9 @@ def timed_train(precision, B, steps, warmup, dev, world=1, rank=0, events=False,
     x, k = synthetic(B, 1234 + rank, canvas, **(data or {}))
     X = torch.from_numpy(x).to(dev)
     K = torch.from_numpy(k).to(dev)
+    step = model.train_step_graphed if graph else model.train_step_async
     for _ in range(warmup):
-        model.train_step_async(X, K, global_batch=B * world)
+        step(X, K, global_batch=B * world)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -187,7 +189,7 @@ def timed_train(precision, B, steps, warmup, dev, world=1, rank=0, events=False,
     model.kernel_events = {} if events else None
     t0 = time.perf_counter()
     for _ in range(steps):
-        model.train_step_async(X, K, global_batch=B * world)
+        step(X, K, global_batch=B * world)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -531,12 +533,18 @@ def main():
                             "(2-4 objects of side 22-30), bf16 fused step kernel"}
             del m6
             torch.cuda.empty_cache()
-            el3, m3 = timed_train("fp32", 64, 50, 5, dev, scope="bench_b64")
+            el3, m3 = timed_train("fp32", 64, 50, 5, dev, scope="bench_b64", graph=True)
+            el3e, m3e = timed_train("fp32", 64, 50, 5, dev, scope="bench_b64e")
             out["config_1_batch64_fp32"] = {
                 "value": 64 * 50 / el3, "unit": "images/sec", "ms_per_step": el3 / 50 * 1e3,
                 "dtype": "fp32", "batch": 64, "steps": 50,
-                "workload": "configs[0] shape (the reference's batch of 64) on one MI355X"}
-            del m3
+                "eager_ms_per_step": el3e / 50 * 1e3,
+                "workload": "configs[0] shape (the reference's batch of 64) on one MI355X: "
+                            "the captured train step (forward + backward replayed from one "
+                            "hipGraph; noise fills, annealed prior and TF Adam launched around "
+                            "it, AIRModel.train_step_graphed); eager_ms_per_step: the same step "
+                            "launched kernel by kernel"}
+            del m3, m3e
             torch.cuda.empty_cache()
             if args.roofline_batch > 0:
                 out["fused_step_roofline"] = fused_step_roofline(args.roofline_batch,

@@ -111,7 +111,10 @@ int mog_lstm_cell_backward(const float* G, const float* bias, const float* c_pre
  * :677-705 (scale/shift KLs), loop predicate :428-432 via live[step+1].
  * hid/w2/b2: HOST arrays of 5 device pointers (scale-mean, scale-logvar,
  * shift-mean, shift-logvar, z_pres log-odds). rec: [17, B] saved records
- * (slot 16: the z_pres KL term this step added to runloss, for mog_air_runloss). */
+ * (slot 16: the z_pres KL term this step added to runloss, for mog_air_runloss).
+ * prior_lo_dev (may be NULL): device float read instead of prior_lo -- the
+ * annealed z_pres prior (air_model.py:164-184) of a graph-captured train step,
+ * whose kernel arguments are fixed at capture. */
 int mog_air_step_forward(int B, int HS, int HZ, int step, int train, int use_num_prior,
                          float thr, float temperature, float prior_lo, float prior_bias,
                          float s_pm, float s_pv, float s_plv, float h_pm, float h_pv, float h_plv,
@@ -121,7 +124,8 @@ int mog_air_step_forward(int B, int HS, int HZ, int step, int train, int use_num
                          int* digits, int* live, float* rec, float* theta_fwd,
                          float* theta_back, float* scale_out, float* shift_out,
                          float* zprob_out, float* zkl_out, float* skl_out, float* shkl_out,
-                         float* zmask, float* zval, float* zc, void* stream);
+                         float* zmask, float* zval, float* zc, const float* prior_lo_dev,
+                         void* stream);
 /* Backward of the above: writes dout [5][B, 2] and dhid [5][B, HS] (head
  * strides dout_hs / dhid_hs elements; dhid_hs == HS means the heads side by
  * side, [B][5][HS] with rows 5 HS apart).  The KL terms this step added to the
@@ -134,7 +138,7 @@ int mog_air_step_backward(int B, int HS, int train, int use_num_prior, float tem
                           const float* eps_shift, const float* dtheta_fwd,
                           const float* dtheta_back, const float* dot, const float* const* hid,
                           const float* const* w2, float* dout, long dout_hs, float* dhid,
-                          long dhid_hs, void* stream);
+                          long dhid_hs, const float* prior_lo_dev, void* stream);
 
 /* ---- VAE latent sample + KL (air/vae.py:27-30, air_model.py:718-736) ----
  * z_bf16 (may be NULL): bf16 copy of z with row stride ld_zb (GEMM operand).
@@ -279,8 +283,10 @@ int mog_add(const float* a, const float* b, float* out, long n, void* stream);
  * Per-tensor inf/nan -> 0, clip_by_norm(clip), TF ApplyAdam with lr_t given.
  * off/len: tensor table; block_tensor/block_start: block -> (tensor, first
  * element), chunks of mog_optim_chunk_elems() elements; all device arrays.
- * sumsq [n_tensors] must be zero on entry; sumsq == NULL skips the NaN/Inf
- * zeroing and the clip (gradient_clipping_norm=None, air_model.py:948). */
+ * sumsq: device scratch of nblocks floats (each chunk's sum of squares; a
+ * tensor's norm is summed from them in chunk order: deterministic, no
+ * atomics); sumsq == NULL skips the NaN/Inf zeroing and the clip
+ * (gradient_clipping_norm=None, air_model.py:948). */
 int mog_optim_chunk_elems(void);
 int mog_clip_adam(float* params, float* grads, float* m, float* v, const long* off,
                   const long* len, const int* block_tensor, const long* block_start,

@@ -80,7 +80,14 @@ struct StepCfg {
   float thr, temperature, prior_lo, prior_bias;
   float s_pm, s_pv, s_plv, h_pm, h_pv, h_plv;
   float grad_scale;  // dL/d(per-image loss) = 1/B_global
+  // when set, the z_pres prior log-odds is read from device memory instead of
+  // prior_lo (the annealed value of a captured step changes every replay)
+  const float* prior_lo_dev;
 };
+
+__device__ __forceinline__ float prior_log_odds(const StepCfg& c) {
+  return c.prior_lo_dev ? *c.prior_lo_dev : c.prior_lo;
+}
 
 // record slots [NREC][B] per step
 enum {
@@ -199,7 +206,7 @@ __global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp,
   const int live = io.live[cfg.step];
   float kl_end = 0.0f;
   if (cfg.use_num_prior) kl_end = concrete_kl(y, -100.0f, cfg.temperature, lo, cfg.temperature);
-  const float zkl = concrete_kl(y, cfg.prior_lo + cfg.prior_bias, cfg.temperature, lo,
+  const float zkl = concrete_kl(y, prior_log_odds(cfg) + cfg.prior_bias, cfg.temperature, lo,
                                 cfg.temperature);
   const float stop_old = io.stop[b];
   const bool act_old = stop_old < cfg.thr;
@@ -285,7 +292,7 @@ __global__ __launch_bounds__(256) void step_bwd_kernel(StepCfg cfg, StepBwdIO io
   float dz = act ? io.dot[b] : 0.0f;
   float dy = cfg.train ? dz * z * (1.0f - z) : 0.0f;
   const float aq = -y * T + lo;
-  const float ap = -y * T + (cfg.prior_lo + cfg.prior_bias);
+  const float ap = -y * T + (prior_log_odds(cfg) + cfg.prior_bias);
   const float sq = mog_sigmoidf(aq), sp = mog_sigmoidf(ap);
   const float wz = (live && act_old) ? gL : 0.0f;
   float dlo = 0.0f;
@@ -668,7 +675,7 @@ extern "C" int mog_air_step_forward(
     const float* eps_scale, const float* eps_shift, const float* u, float* stop, float* runloss,
     int* digits, int* live, float* rec, float* theta_fwd, float* theta_back, float* scale_out,
     float* shift_out, float* zprob_out, float* zkl_out, float* skl_out, float* shkl_out,
-    float* zmask, float* zval, float* zc, void* stream) {
+    float* zmask, float* zval, float* zc, const float* prior_lo_dev, void* stream) {
   MOG_CHECK_ARG(B >= 0 && hid && w2 && b2 && eps_scale && eps_shift && u && stop && runloss);
   MOG_CHECK_ARG(digits && live && rec && theta_fwd && theta_back && scale_out && shift_out);
   MOG_CHECK_ARG(zprob_out && zkl_out && skl_out && shkl_out && zmask && zval);
@@ -677,7 +684,7 @@ extern "C" int mog_air_step_forward(
   c.B = B; c.H = 0; c.HS = HS; c.HZ = HZ; c.train = train; c.use_num_prior = use_num_prior;
   c.step = step; c.thr = thr; c.temperature = temperature; c.prior_lo = prior_lo;
   c.prior_bias = prior_bias; c.s_pm = s_pm; c.s_pv = s_pv; c.s_plv = s_plv; c.h_pm = h_pm;
-  c.h_pv = h_pv; c.h_plv = h_plv; c.grad_scale = 0.0f;
+  c.h_pv = h_pv; c.h_plv = h_plv; c.grad_scale = 0.0f; c.prior_lo_dev = prior_lo_dev;
   HeadPtrs hp;
   for (int i = 0; i < 5; ++i) {
     MOG_CHECK_ARG(hid[i] && w2[i] && b2[i]);
@@ -699,7 +706,7 @@ extern "C" int mog_air_step_backward(int B, int HS, int train, int use_num_prior
                                      const float* dtheta_back, const float* dot,
                                      const float* const* hid, const float* const* w2,
                                      float* dout, long dout_hs, float* dhid, long dhid_hs,
-                                     void* stream) {
+                                     const float* prior_lo_dev, void* stream) {
   MOG_CHECK_ARG(B >= 0 && rec && eps_scale && eps_shift && dtheta_fwd && dtheta_back && dot);
   MOG_CHECK_ARG(hid && w2 && dout && dhid);
   if (B == 0) return 0;
@@ -707,7 +714,7 @@ extern "C" int mog_air_step_backward(int B, int HS, int train, int use_num_prior
   c.B = B; c.H = 0; c.HS = HS; c.HZ = HS; c.train = train; c.use_num_prior = use_num_prior;
   c.step = 0; c.thr = 0.0f; c.temperature = temperature; c.prior_lo = prior_lo;
   c.prior_bias = prior_bias; c.s_pm = s_pm; c.s_pv = s_pv; c.s_plv = 0.0f; c.h_pm = h_pm;
-  c.h_pv = h_pv; c.h_plv = 0.0f; c.grad_scale = grad_scale;
+  c.h_pv = h_pv; c.h_plv = 0.0f; c.grad_scale = grad_scale; c.prior_lo_dev = prior_lo_dev;
   StepBwdIO io{rec, eps_scale, eps_shift, dtheta_fwd, dtheta_back, dot, dloss, dout, dout_hs};
   hipStream_t s = mog_stream(stream);
   step_bwd_kernel<<<mog_cdiv(B, 256), 256, 0, s>>>(c, io);

@@ -6,7 +6,10 @@
 // then ApplyAdam (epsilon outside the bias correction, TF training_ops):
 //   m += (g - m) * (1 - b1);  v += (g*g - v) * (1 - b2)
 //   var -= (m * lr_t) / (sqrt(v) + eps),  lr_t = lr sqrt(1 - b2^t) / (1 - b1^t)
-// Two launches: (1) sanitize + per-tensor sum of squares, (2) clip + Adam.
+// Two launches: (1) sanitize + each block's sum of squares of its chunk,
+// (2) clip + Adam, every block forming its tensor's squared norm from the
+// tensor's chunk sums in chunk order -- no atomics, so the norm, the clip and
+// the update are the same bits on every run (and in a replayed graph).
 // The tensor table maps a block to (tensor, chunk) so one launch covers all
 // ~36 parameter tensors of the flat parameter buffer.
 #include "mog_common.h"
@@ -19,7 +22,7 @@ __global__ __launch_bounds__(256) void sanitize_sumsq_kernel(float* g, const lon
                                                             const long* len,
                                                             const int* block_tensor,
                                                             const long* block_start,
-                                                            float* sumsq) {
+                                                            float* part) {
   __shared__ float red[4];
   const int ti = block_tensor[blockIdx.x];
   const long base = off[ti], n = len[ti];
@@ -35,25 +38,35 @@ __global__ __launch_bounds__(256) void sanitize_sumsq_kernel(float* g, const lon
     s += v * v;
   }
   s = mog_block_sum256(s, red);
-  if (threadIdx.x == 0) atomicAdd(sumsq + ti, s);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
 __global__ __launch_bounds__(256) void clip_adam_kernel(float* p, const float* g, float* m,
                                                        float* v, const long* off, const long* len,
                                                        const int* block_tensor,
                                                        const long* block_start,
-                                                       const float* sumsq, float clip,
+                                                       const float* part, float clip,
                                                        float lr_t, float b1, float b2,
                                                        float eps) {
 #pragma clang fp contract(off)
+  __shared__ float red[4];
   const int ti = block_tensor[blockIdx.x];
   const long base = off[ti], n = len[ti];
   const long c0 = block_start[blockIdx.x];
   const long c1 = min(n, c0 + CHUNK);
-  // sumsq == nullptr: gradient_clipping_norm=None -- no sanitize, no clip
+  // part == nullptr: gradient_clipping_norm=None -- no sanitize, no clip
   // (air_model.py:948 skips both), plain ApplyAdam
-  const bool clipped = sumsq != nullptr;
-  const float l2 = clipped ? sumsq[ti] : 0.0f;
+  const bool clipped = part != nullptr;
+  float l2 = 0.0f;
+  if (clipped) {
+    // the tensor's chunk sums: blocks first .. first + nc - 1, summed in a
+    // fixed order (per thread strided, then the block tree)
+    const int first = blockIdx.x - (int)(c0 / CHUNK);
+    const int nc = (int)((n + CHUNK - 1) / CHUNK);
+    float s = 0.0f;
+    for (int j = threadIdx.x; j < nc; j += 256) s += part[first + j];
+    l2 = mog_block_sum256(s, red);
+  }
   const float norm = l2 > 0.0f ? sqrtf(l2) : l2;
   const float denom = fmaxf(norm, clip);
   for (long i = c0 + threadIdx.x; i < c1; i += 256) {
@@ -72,7 +85,7 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* p, const float* g
 
 extern "C" int mog_optim_chunk_elems(void) { return CHUNK; }
 
-// `sumsq` must be zeroed by the caller (it is an in/out accumulator); a null
+// `sumsq`: scratch of nblocks floats (per-chunk sums of squares); a null
 // `sumsq` skips the NaN/Inf zeroing and the clip (gradient_clipping_norm=None).
 extern "C" int mog_clip_adam(float* params, float* grads, float* m, float* v, const long* off,
                              const long* len, const int* block_tensor, const long* block_start,

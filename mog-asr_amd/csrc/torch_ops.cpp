@@ -319,7 +319,7 @@ void air_step_forward_(int64_t B, int64_t HS, int64_t HZ, int64_t step, bool tra
                        const Tensor& u, Tensor stop, Tensor runloss, Tensor digits, Tensor live,
                        Tensor rec, Tensor theta_fwd, Tensor theta_back, Tensor scale, Tensor shift,
                        Tensor zprob, Tensor zkl, Tensor skl, Tensor shkl, Tensor zmask, Tensor zval,
-                       Tensor zc) {
+                       Tensor zc, const optional<Tensor>& prior_lo_dev) {
   Op o("air_step_forward_");
   TORCH_CHECK(hid.size() == 5 && w2.size() == 5 && b2.size() == 5, o.name, ": 5 heads");
   float* pst = o.f(stop, B, "stop");
@@ -343,11 +343,12 @@ void air_step_forward_(int64_t B, int64_t HS, int64_t HZ, int64_t step, bool tra
   float* pzm = o.f(zmask, B, "zmask");
   float* pzv = o.f(zval, B, "zval");
   float* pzc = o.f(zc, B, "zc");
+  float* pplo = o.f(prior_lo_dev, 1, "prior_lo_dev");
   GUARD(o);
   check(mog_air_step_forward(B, HS, HZ, step, train, use_num_prior, thr, temperature, prior_lo,
                              prior_bias, s_pm, s_pv, s_plv, h_pm, h_pv, h_plv, arr<float>(h),
                              arr<float>(w), arr<float>(b), pes, peh, pu, pst, prl, pd, pl, pr, ptf,
-                             ptb, psc, psh, pzp, pzk, psk, phk, pzm, pzv, pzc, o.stream()),
+                             ptb, psc, psh, pzp, pzk, psk, phk, pzm, pzv, pzc, pplo, o.stream()),
         o.name);
 }
 
@@ -358,7 +359,7 @@ void air_step_backward_(int64_t B, int64_t HS, bool train, bool use_num_prior,
                         const Tensor& eps_shift, const Tensor& dtheta_fwd,
                         const Tensor& dtheta_back, const Tensor& dot, at::TensorList hid,
                         at::TensorList w2, Tensor dout, int64_t dout_hs, Tensor dhid,
-                        int64_t dhid_hs) {
+                        int64_t dhid_hs, const optional<Tensor>& prior_lo_dev) {
   Op o("air_step_backward_");
   TORCH_CHECK(hid.size() == 5 && w2.size() == 5, o.name, ": 5 heads");
   float* pdo = o.f(dout, 4 * dout_hs + 2 * B, "dout");
@@ -371,10 +372,11 @@ void air_step_backward_(int64_t B, int64_t HS, bool train, bool use_num_prior,
   float* ptf = o.f(dtheta_fwd, 6 * B, "dtheta_fwd");
   float* ptb = o.f(dtheta_back, 6 * B, "dtheta_back");
   float* pd = o.f(dot, B, "dot");
+  float* pplo = o.f(prior_lo_dev, 1, "prior_lo_dev");
   GUARD(o);
   check(mog_air_step_backward(B, HS, train, use_num_prior, temperature, prior_lo, prior_bias, s_pm,
                               s_pv, h_pm, h_pv, grad_scale, pl, pr, pes, peh, ptf, ptb, pd,
-                              arr<float>(h), arr<float>(w), pdo, dout_hs, pdh, dhid_hs,
+                              arr<float>(h), arr<float>(w), pdo, dout_hs, pdh, dhid_hs, pplo,
                               o.stream()),
         o.name);
 }
@@ -642,7 +644,7 @@ void clip_adam_(Tensor params, Tensor grads, Tensor m, Tensor v, const Tensor& o
   auto* plen = static_cast<const long*>(o.need(len, at::kLong, 0, "len"));
   const int* pbt = o.i(block_tensor, nblocks, "block_tensor");
   auto* pbs = static_cast<const long*>(o.need(block_start, at::kLong, nblocks, "block_start"));
-  float* ps = o.f(sumsq, off.numel(), "sumsq");
+  float* ps = o.f(sumsq, nblocks, "sumsq");  // per-chunk scratch
   GUARD(o);
   check(mog_clip_adam(pp, pg, pm, pv, poff, plen, pbt, pbs, nblocks, ps, clip, lr_t, beta1, beta2,
                       eps, o.stream()),
@@ -868,13 +870,13 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "Tensor(b!) runloss, Tensor(c!) digits, Tensor(d!) live, Tensor(e!) rec, "
       "Tensor(f!) theta_fwd, Tensor(g!) theta_back, Tensor(h!) scale, Tensor(i!) shift, "
       "Tensor(j!) zprob, Tensor(k!) zkl, Tensor(l!) skl, Tensor(m!) shkl, Tensor(n!) zmask, "
-      "Tensor(o!) zval, Tensor(p!) zc) -> ()");
+      "Tensor(o!) zval, Tensor(p!) zc, Tensor? prior_lo_dev=None) -> ()");
   m.def(
       "air_step_backward_(int B, int HS, bool train, bool use_num_prior, float temperature, "
       "float prior_lo, float prior_bias, float s_pm, float s_pv, float h_pm, float h_pv, "
       "float grad_scale, Tensor? dloss, Tensor rec, Tensor eps_scale, Tensor eps_shift, "
       "Tensor dtheta_fwd, Tensor dtheta_back, Tensor dot, Tensor[] hid, Tensor[] w2, "
-      "Tensor(a!) dout, int dout_hs, Tensor(b!) dhid, int dhid_hs) -> ()");
+      "Tensor(a!) dout, int dout_hs, Tensor(b!) dhid, int dhid_hs, Tensor? prior_lo_dev=None) -> ()");
   m.def(
       "generation_prior_(int G, int Z, float s_pm, float s_plv, float h_pm, float h_plv, "
       "float v_pm, float v_plv, Tensor eps_scale, Tensor eps_shift, Tensor eps_z, "

@@ -1082,6 +1082,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
                                    (p.phases & 16) != 0, tid);
     if constexpr (MT == 4) {
       dense_out<MT, 32 / NW, 4>(sD2, S512, p, 0, 0, NW, b0, nb, tid, fl);
+      STAMP(8);
     } else {  // (the 32-image forms: the hook would not fit their registers)
       fl();
       dense_out<MT, 32 / NW, 4>(sD2, S512, p, 0, 0, NW, b0, nb, tid);
@@ -1091,7 +1092,6 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // r stores done before other waves read it
   lds_barrier();
-  STAMP(8);
   STAMP(9);
   // ---- 9. STN write (stn_write_tile) --------------------------------------
   if (p.phases & 8)
@@ -1664,7 +1664,7 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
     (void)hipStreamSynchronize(s);
     (void)hipMemcpy(h.data(), tbuf, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
     static const char* names[10] = {"read+L1", "L1epi", "L2", "mu_lv", "sample",
-                                    "g1", "g2", "go", "-", "write"};
+                                    "g1", "g2", "go1", "go23", "write"};
     double acc[11] = {0}, pro = 0;
     long long t0 = h[0], t1 = h[10];
     for (unsigned b = 0; b < nblk; ++b) {

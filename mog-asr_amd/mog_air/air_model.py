@@ -386,7 +386,7 @@ class AIRModel:
         for k, normal in (("eps_scale", True), ("eps_shift", True), ("eps_z", True),
                           ("eps_x", True), ("u", False)):
             buf = getattr(ws, k)
-            if k == "eps_x" and self._eps_x_in_kernel(ws.B):
+            if k == "eps_x" and self._eps_x_in_kernel(ws.B) and not self._graph_noise:
                 # generated inside the fused step kernel / the fp32 output
                 # layer's epilogue from the same Philox counters (bit-identical
                 # to filling the buffer)
@@ -413,7 +413,7 @@ class AIRModel:
         ws.runloss.zero_()
         ws.digits.zero_()
         ws.live.zero_()
-        ws.live[0] = 1
+        ws.live[:1].fill_(1)  # (a fill kernel: capturable, unlike a host copy)
         prior_lo = self.hyper("z_pres_prior_log_odds")
         temperature = self.hyper("z_pres_temperature")
         thr = self.hyper("stopping_threshold")
@@ -446,7 +446,8 @@ class AIRModel:
                 float(self.shift_prior_variance), self.shift_prior_log_variance, hid_t, w2, b2,
                 ws.eps_scale[t], ws.eps_shift[t], ws.u[t], ws.stop, ws.runloss, ws.digits,
                 ws.live, rec, ws.th_f[t], ws.th_b[t], ws.scale[t], ws.shift[t], ws.zprob[t],
-                ws.zkl[t], ws.skl[t], ws.shkl[t], ws.zmask[t], ws.zval[t], ws.zc[t])
+                ws.zkl[t], ws.skl[t], ws.shkl[t], ws.zmask[t], ws.zval[t], ws.zc[t],
+                self._prior_dev)
             if self.live_hook is not None:
                 self.live_hook(ws.live, t)
             if batched:
@@ -492,6 +493,8 @@ class AIRModel:
         straddle two steps (B % 64)."""
         return self.batch_vae and B % 64 == 0
 
+    FUSED_F32_MIN_ROWS = 8192
+
     def _vae_forward_all(self, X, ws, lik_std, t0=0, t1=None, save=True):
         """The glimpse VAE (STN read -> VAE -> STN write into the canvas
         parts) of loop steps [t0, t1) as one set of launches over their rows.
@@ -521,7 +524,11 @@ class AIRModel:
                                sv(ws.a1b), sv(ws.a2b), sv(ws.mu), sv(ws.lv), r_(ws.z), sv(ws.zb),
                                sv(ws.d1b), sv(ws.d2b), r_(ws.r), B)
             return
-        if self.precision == "fp32" and self.fused_f32:
+        # the fused fp32 kernel runs one 32-row tile per workgroup with a long
+        # serial chain per tile (~200 us): below one tile per CU (T*B < 8192
+        # rows, e.g. the reference's batch of 64) the unfused launches, which
+        # spread every layer over the chip, finish first -- same bits either way
+        if self.precision == "fp32" and self.fused_f32 and TB >= self.FUSED_F32_MIN_ROWS:
             self._pack_f32()
             gen = getattr(ws, "eps_x_offset", None) is not None
             off = ws.eps_x_offset + t0 * B * (W2 // 4) if gen else 0
@@ -678,7 +685,8 @@ class AIRModel:
                 float(self.scale_prior_mean), float(self.scale_prior_variance),
                 float(self.shift_prior_mean), float(self.shift_prior_variance), float(gscale),
                 None, ws.rec[t], ws.eps_scale[t], ws.eps_shift[t], ws.dth_f_all[t], ws.dth_b_all[t],
-                ws.dot_all[t], hid_t, w2, ws.dout[0, t], T * B * 2, ws.dhid[t], HS)
+                ws.dot_all[t], hid_t, w2, ws.dout[0, t], T * B * 2, ws.dhid[t], HS,
+                self._prior_dev)
         # dh[t] = sum_z dhid_z W1_z^T for every step: one plain GEMM over
         # K = 5 HS ([dhid_0 .. dhid_4] rows against [W1_0 .. W1_4]), the same
         # k-ordered chain as the per-head sum
@@ -1119,6 +1127,80 @@ class AIRModel:
         self.params.apply_adam(self.hyper("learning_rate"), self.gradient_clipping_norm)
         self.params.global_step += 1
         self._X = X
+
+    # ---------------------------------------------------- graph capture ---
+    # A captured train step (hipGraph through torch.cuda.CUDAGraph): the whole
+    # forward + backward -- ~80 launches, every one of them with arguments that
+    # are the same from step to step -- replays as ONE graph launch.  What
+    # changes per step stays outside the graph or is read from device memory:
+    # the Philox noise fills (their counter offsets advance, eager launches
+    # before the replay; eps_x is filled too instead of being generated inside
+    # the VAE kernels), the annealed z_pres prior log-odds (a device scalar the
+    # step kernels read, filled before the replay) and TF Adam (lr_t from the
+    # fp32 beta powers, an eager launch after it).  The reference's batch of 64
+    # (training_air_original.py:22) is launch-bound without it.
+    _graph_noise = False  # eps_x filled into its buffer (graph mode)
+    _prior_dev = None     # device z_pres prior log-odds (graph mode)
+    _graph = None
+
+    def _graph_ok(self):
+        others = [k for k in self.annealing_schedules if k != "z_pres_prior_log_odds"]
+        if others:
+            raise NotImplementedError(f"graph mode: annealed {others} would be frozen at capture")
+        if self.grad_reducer is not None or self.live_hook is not None:
+            raise NotImplementedError("graph mode is the single-device train step")
+
+    def train_step_graphed(self, images, targets=None, global_batch: Optional[int] = None) -> None:
+        """train_step_async with the forward + backward replayed from a captured
+        graph; bit-identical to it.  The first call at a batch shape runs the
+        step eagerly and captures the graph (capture executes nothing); later
+        calls copy the inputs into the graph's static buffers and replay."""
+        if not self.train:
+            raise RuntimeError("train_step on a model built with train=False")
+        self._graph_ok()
+        X, tg = self._prep(images, targets)
+        key = (tuple(X.shape), None if tg is None else tuple(tg.shape), global_batch)
+        if self._graph is None or self._graph_key != key:
+            self._graph = None
+            self._graph_noise = True
+            if self._prior_dev is None:
+                self._prior_dev = torch.zeros(1, device=self.device)
+            self._prior_dev.fill_(self.hyper("z_pres_prior_log_odds"))
+            self.train_step_async(X, tg, global_batch=global_batch)  # this call's step
+            self._capture(X, tg, global_batch)
+            self._graph_key = key
+            return
+        gX, gT = self._graph_io
+        if X.data_ptr() != gX.data_ptr():
+            gX.copy_(X)
+        if tg is not None and tg.data_ptr() != gT.data_ptr():
+            gT.copy_(tg)
+        ws = self._ws
+        self._fill_noise(ws, None)
+        self._prior_dev.fill_(self.hyper("z_pres_prior_log_odds"))
+        self._graph.replay()
+        self.params.apply_adam(self.hyper("learning_rate"), self.gradient_clipping_norm)
+        self.params.global_step += 1
+        self._X = gX
+        self._loss_inputs = (gX, gT)
+        ws.materialized = False
+        self._outputs_ready = True
+
+    def _capture(self, X, tg, global_batch):
+        ws = self._ws
+        gX = X.clone()
+        gT = tg.clone() if tg is not None else None
+        self._graph_io = (gX, gT)
+        # the weight packs are refreshed by a launch inside the graph on every
+        # replay (the parameters change every step): force it to be recorded
+        self._pack_version = self._pack32_version = self._w1cat_version = None
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        self._global_batch = global_batch
+        with torch.cuda.graph(g):
+            self._forward(gX, gT, ws, need_grad=True, outputs=False)
+            self._backward(gX, ws)
+        self._graph = g
 
     def step(self, images, targets=None, noise=None, global_batch: Optional[int] = None):
         """``sess.run([training, loss, accuracy, mse_loss, global_step])``

@@ -160,7 +160,8 @@ class ParamStore:
         self.t_bt = torch.tensor(btens, dtype=torch.int32, device=dev)
         self.t_bs = torch.tensor(bstart, dtype=torch.int64, device=dev)
         self.n_blocks = len(btens)
-        self.sumsq = torch.zeros(len(self.specs), dtype=torch.float32, device=dev)
+        # per-chunk sums of squares (clip_adam scratch: one per block)
+        self.sumsq = torch.zeros(self.n_blocks, dtype=torch.float32, device=dev)
 
     def apply_adam(self, lr: float, clip, beta1=0.9, beta2=0.999, eps=1e-8) -> None:
         """TF AdamOptimizer.apply_gradients after the reference's per-tensor
@@ -171,8 +172,6 @@ class ParamStore:
                                         dtype=np.float32) / (np.float32(1) - self.beta1_power)
         # clip None (gradient_clipping_norm=None): the reference applies the
         # gradients as they are, without NaN/Inf zeroing (air_model.py:948)
-        if clip is not None:
-            self.sumsq.zero_()
         torch.ops.mog_air.clip_adam_(self.flat, self.grad, self.m, self.v, self.t_off, self.t_len,
                                      self.t_bt, self.t_bs, self.n_blocks,
                                      self.sumsq if clip is not None else None,

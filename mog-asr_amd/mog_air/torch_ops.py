@@ -533,7 +533,7 @@ def tf_adam_clip_(params: torch.Tensor, grads: torch.Tensor, m: torch.Tensor, v:
     ln = torch.full((1,), n, device=dev, dtype=torch.int64)
     bt = torch.zeros(nblk, device=dev, dtype=torch.int32)
     bs = torch.arange(nblk, device=dev, dtype=torch.int64) * chunk
-    sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
+    sumsq = torch.zeros(nblk, device=dev, dtype=torch.float32)  # per-chunk scratch
     f = np.float32
     b1p, b2p = f(1), f(1)
     for _ in range(int(step)):  # TF keeps the beta powers as fp32 variables

@@ -18,20 +18,24 @@ constexpr int NFRAG = 2240;  // 2.24 MB of 1-KiB fragments
 
 // each wave: fragments f = (w + nw * i + rot) % NFRAG, i < PER (PER fragments per wave)
 template <int D, int MT>
-__global__ void stream_regs(const __bf16* W, float* out, int per, int passes) {
+__global__ void stream_regs(const __bf16* W, float* out, int per, int passes, int lock = 0) {
   __shared__ __bf16 A[MT * 16 * 40];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int li = lane & 15, g = lane >> 4;
   for (int i = threadIdx.x; i < MT * 16 * 40; i += blockDim.x) A[i] = (__bf16)(0.001f * (i & 7));
   __syncthreads();
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(W), 0, NFRAG * 1024, 0x00020000);
-  const int rot = (blockIdx.x * 37) % NFRAG;
+  // lock: every CU streams the same fragment sequence at the same time (the
+  // fused step kernel's lockstep layers: fragment i*nw + w at step i)
+  const int rot = lock ? 0 : (blockIdx.x * 37) % NFRAG;
   floatx4 acc[MT];
   for (int m = 0; m < MT; ++m) acc[m] = floatx4{0, 0, 0, 0};
   bf16x8 a[MT];
   for (int m = 0; m < MT; ++m) a[m] = *reinterpret_cast<const bf16x8*>(&A[(m * 16 + li) * 40 + 8 * g]);
   for (int ps = 0; ps < passes; ++ps) {
-    auto off = [&](int i) { return (((w + nw * i + rot + ps * 97) % NFRAG) * 64 + lane) * 16; };
+    auto off = [&](int i) {
+      return (((w + nw * i + rot + (lock ? 0 : ps * 97)) % NFRAG) * 64 + lane) * 16;
+    };
     bf16x8 q[D];
 #pragma unroll
     for (int d = 0; d < D; ++d)
@@ -144,6 +148,16 @@ int main() {
   RUN_REGS(8, 1, 16);
   RUN_REGS(8, 4, 4);
   RUN_REGS(16, 4, 4);
+  {  // lockstep: every CU the same fragments in the same order
+    const int per = NFRAG / 16;
+    for (int D4 = 0; D4 < 2; ++D4) {
+      float ms = timeit([&] {
+        if (D4) stream_regs<4, 4><<<grid, 1024>>>(W, out, per, passes, 1);
+        else stream_regs<4, 1><<<grid, 1024>>>(W, out, per, passes, 1);
+      }, 10);
+      report(D4 ? "regs D=4 MT=4 LOCKSTEP" : "regs D=4 MT=1 LOCKSTEP", 16, (double)per * 16 * passes, ms);
+    }
+  }
 #define RUN_LDS(NL, SLOTS, SLOT, NW)                                                              \
   {                                                                                               \
     const int nslab = NFRAG / SLOT;                                                               \

@@ -44,6 +44,7 @@ def _model(cfg, P, scope, fused, num_prior=None):
                  z_pres_prior_log_odds=-0.01, learning_rate=1e-4, gradient_clipping_norm=1.0,
                  cnn=False, train=True, scope=scope, device=DEV, precision="fp32",
                  fused_step=fused, batch_vae=True, num_prior=num_prior)
+    m.FUSED_F32_MIN_ROWS = 0  # the fused kernel at these test batches too
     m.params.load_dict(P)
     return m
 

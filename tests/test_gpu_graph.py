@@ -1,0 +1,89 @@
+"""Captured train step (AIRModel.train_step_graphed: the forward + backward
+replayed from one hipGraph, the noise fills, the annealed z_pres prior and TF
+Adam outside it) against the eager train step, bit for bit: per-step loss /
+accuracy / mse, the object counts and every parameter after several Adam
+steps -- at the reference's own batch of 64 (training_air_original.py:22,
+304-310), fp32 and bf16, with the z_pres prior annealed as the entry point
+anneals it (training_air_original.py:193-201)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+ANNEAL = {"z_pres_prior_log_odds": {"init": 10000.0, "min": 1e-9, "factor": 0.1, "iters": 3000,
+                                    "staircase": False, "log": True}}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+
+
+def _model(scope, precision):
+    from mog_air.air_model import AIRModel
+    return AIRModel(max_steps=3, max_digits=3, canvas_size=50, scale_prior_variance=0.05,
+                    z_pres_prior_log_odds=-0.01, learning_rate=1e-3, gradient_clipping_norm=1.0,
+                    cnn=False, train=True, scope=scope, device=DEV, precision=precision,
+                    annealing_schedules=ANNEAL, seed=21, noise_seed=22)
+
+
+def _batches(n, B=64):
+    import bench
+    out = []
+    for i in range(n):
+        x, k = bench.synthetic(B, 300 + i)
+        out.append((torch.as_tensor(x).to(DEV), torch.as_tensor(k).to(DEV)))
+    return out
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_graph_replay_matches_eager_bitwise(precision):
+    data = _batches(4)
+    me, mg = _model("ge" + precision, precision), _model("gg" + precision, precision)
+    assert torch.equal(me.params.flat, mg.params.flat)
+    for i, (x, k) in enumerate(data):
+        me.train_step_async(x, k)
+        mg.train_step_graphed(x, k)
+        torch.cuda.synchronize()
+        assert mg._graph is not None  # captured after the first (eager) step
+        a, b = me._ws.means[:3].cpu().numpy(), mg._ws.means[:3].cpu().numpy()  # loss, acc, mse
+        np.testing.assert_array_equal(a, b, err_msg=f"step {i} means")
+        np.testing.assert_array_equal(me.rec_num_digits.cpu().numpy(),
+                                      mg.rec_num_digits.cpu().numpy())
+        assert me.global_step == mg.global_step == i + 1
+    assert torch.equal(me.params.flat.view(torch.int32), mg.params.flat.view(torch.int32))
+    assert torch.equal(me.params.m.view(torch.int32), mg.params.m.view(torch.int32))
+    # the device prior was refreshed for the last replay (global step 3)
+    from mog_air.air_model import annealed_value
+    want = np.float32(annealed_value(ANNEAL["z_pres_prior_log_odds"], 3))
+    assert np.float32(mg._prior_dev.item()) == want
+
+
+def test_graph_replays_new_inputs_and_recaptures_on_shape_change():
+    """The replay reads the static input buffers (new images every step), and
+    a new batch shape captures a new graph; outputs stay equal to eager."""
+    me, mg = _model("gs_e", "fp32"), _model("gs_g", "fp32")
+    for B, n in ((64, 3), (128, 2)):
+        for x, k in _batches(n, B):
+            me.train_step_async(x, k)
+            mg.train_step_graphed(x, k)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(me._ws.means[:3].cpu().numpy(),
+                                          mg._ws.means[:3].cpu().numpy())
+        assert mg._graph_key[0] == (B, 2500)
+    assert torch.equal(me.params.flat.view(torch.int32), mg.params.flat.view(torch.int32))
+
+
+def test_graph_outputs_accessible_after_replay():
+    """loss / reconstruction accessors after a replay (materialised on demand
+    from the graph's static inputs)."""
+    me, mg = _model("go_e", "fp32"), _model("go_g", "fp32")
+    for x, k in _batches(2):
+        me.train_step_async(x, k)
+        mg.train_step_graphed(x, k)
+    torch.cuda.synchronize()
+    assert me.loss == mg.loss
+    np.testing.assert_array_equal(me.reconstruction.cpu().numpy(), mg.reconstruction.cpu().numpy())
