@@ -1370,7 +1370,7 @@ __global__ __launch_bounds__(1024, 1) void stn_vae_step_f32_kernel(StepArgsF p) 
       for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-      constexpr int DB = 2;
+      constexpr int DB = 3;
       floatx4 q[DB][4];
       auto loadB = [&](int ks, floatx4* b) {
 #pragma unroll
@@ -1446,7 +1446,7 @@ __global__ __launch_bounds__(1024, 1) void stn_vae_step_f32_kernel(StepArgsF p) 
   float* sR1 = reinterpret_cast<float*>(arena);
   float* sR2 = reinterpret_cast<float*>(arena + LayF::OFF_R2);
   // ---- 3. a2 = softplus(a1 W2 + b2) [M x 256] -> R2 ------------------------
-  dense_f32<2, 32, 16, 1, 4>(sR1, FS512, p.wt[1], p.bias[1], 256, 0, 0, NW,
+  dense_f32<2, 32, 16, 1, 8>(sR1, FS512, p.wt[1], p.bias[1], 256, 0, 0, NW,
                              sp_epi(sR2, FS256, save ? p.a2pre : nullptr, p.a2, 256), tid);
   lds_barrier();
   STAMP(3);
@@ -1508,7 +1508,7 @@ __global__ __launch_bounds__(1024, 1) void stn_vae_step_f32_kernel(StepArgsF p) 
   lds_barrier();
   STAMP(6);
   // ---- 7. d2 = softplus(d1 Wg2 + b) [M x 512] -> R1 -------------------------
-  dense_f32<2, 16, 32, 2, 4>(sR2, FS256, p.wt[5], p.bias[5], 512, 0, 0, NW,
+  dense_f32<2, 16, 32, 2, 6>(sR2, FS256, p.wt[5], p.bias[5], 512, 0, 0, NW,
                              sp_epi(sR1, FS512, save ? p.d2pre : nullptr, p.d2, 512), tid);
   lds_barrier();
   STAMP(7);
@@ -1535,7 +1535,7 @@ __global__ __launch_bounds__(1024, 1) void stn_vae_step_f32_kernel(StepArgsF p) 
       }
       reinterpret_cast<float4*>(p.r)[q] = make_float4(o[0], o[1], o[2], o[3]);
     };
-    dense_f32<2, 32, 49, 3, 4>(sR1, FS512, p.wt[6], p.bias[6], W2, 0, 0, NW, epi, tid);
+    dense_f32<2, 32, 49, 3, 5>(sR1, FS512, p.wt[6], p.bias[6], W2, 0, 0, NW, epi, tid);
     if (wv >= 14) {  // column tile 48: row tile wv - 14
       const int rt = wv - 14;
       dense_f32<1, 32, 49, 1, 4>(sR1 + rt * 16 * FS512, FS512, p.wt[6], p.bias[6], W2, 48, 14, 1,

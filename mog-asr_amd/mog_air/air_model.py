@@ -670,9 +670,13 @@ class AIRModel:
             self._vae_backward_fp32_all(ws, gscale)
         # The VAE weight gradients need only the activations and the VAE input
         # gradients, final here: they run on a second stream (MFMA-bound
-        # split-K GEMMs) under the latency-bound STN read backward, the heads
-        # and the LSTM chain below; the main stream joins before the bucket
-        # all-reduce / the optimizer.
+        # split-K GEMMs) under the latency-bound STN read backward and the
+        # heads' backward; the main stream joins them before the glimpse-side
+        # all-reduce bucket and the LSTM chain (joining only before Adam, so
+        # they would also overlap the LSTM chain and the x-weight gradient,
+        # was measured slower: 3.74 -> 3.81 ms).
+        # (measured: forking them after the STN read backward instead, so that
+        # kernel runs alone, leaves the step unchanged -- 3.53 ms either way)
         vae_done = self._vae_weight_grads_async(ws)
         # STN read backward of all steps against the shared input canvas
         ops.stn_backward(X, ws.th_f, (W, W), ws.dg_all, want_dU=False, dtheta=ws.dth_f_all,

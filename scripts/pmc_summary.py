@@ -48,6 +48,8 @@ TAGS = {
     "stn_vae_step_b65536": ("stn_vae_step", 65536 // 64 * 1024),
     "stn_vae_step_b65536_c64": ("stn_vae_step", 65536 // 64 * 1024),
     "stn_vae_step_b65536_fwd": ("stn_vae_step", 65536 // 64 * 1024),
+    # bench.fp32_step_roofline: the fp32 fused step, 32-image tiles
+    "stn_vae_step_f32_b65536": ("stn_vae_step_f32_kernel", 65536 // 32 * 1024),
 }
 # bench.py runs the three B = 65,536 fused-step measurements in this order
 # (same symbol and grid): training form at C = 50, at C = 64, forward-only at C = 50

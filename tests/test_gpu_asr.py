@@ -95,10 +95,13 @@ def test_asr_forward_bit_exact_vs_oracle(kw):
                           # weights by 0.4 % (float64, no bf16 anywhere) moves
                           # inf_shift/dense_3/bias by 120 % (cosine 0.17).  Gate: every
                           # tensor whose float64 gradient moves < 10 % under that
-                          # perturbation within 50 %, cosine >= 0.9 (an indexing or
+                          # perturbation within 20 %, cosine >= 0.99 (an indexing or
                           # missing-term bug gives ~100 % / cosine ~0), and the whole
-                          # concatenated gradient within 10 %, cosine >= 0.99.
-                          (dict(), "bf16", 5e-1, 0.9, 1e-1)])
+                          # concatenated gradient within 8 %.  Measured on MI355X
+                          # (profiles/r03_asr_bf16_grad_report.json): worst checked
+                          # tensor 11.3 % / cosine 0.9948 (inf_shift/dense_1/kernel),
+                          # 42 of 49 tensors checked, global 4.95 % / cosine 0.9988.
+                          (dict(), "bf16", 2e-1, 0.99, 8e-2)])
 def test_asr_gradients_vs_float64_autograd(kw, precision, tol, cos_min, global_tol):
     cfg, P, nz, x, k = _setup(30, **kw)
     rng = np.random.default_rng(31)
@@ -145,7 +148,7 @@ def test_asr_gradients_vs_float64_autograd(kw, precision, tol, cos_min, global_t
     gerr = np.linalg.norm(g - r) / np.linalg.norm(r)
     gcos = float(np.dot(g, r) / (np.linalg.norm(g) * np.linalg.norm(r)))
     assert gerr < global_tol and gcos > 0.99, (gerr, gcos)
-    assert checked >= 25
+    assert checked >= 40  # (bf16: 42 of 49 conditioned tensors measured)
     print(f"ASR {precision} worst relative gradient error {worst:.2e}, global {gerr:.2e}")
     if os.environ.get("MOG_GRAD_REPORT"):
         import json

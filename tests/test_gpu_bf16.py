@@ -127,8 +127,9 @@ def test_bf16_forward_vs_fp32_oracle():
     rel = abs(m.loss - ro["loss_mean"]) / abs(ro["loss_mean"])
     print(f"bf16 ELBO relative deviation {rel:.2e}")
     # decomposed in test_bf16_elbo_deviation_decomposed (batch 256: 1.0e-3,
-    # all but 5e-5 of it in the out-of-window STN residue band)
-    assert rel < 5e-3
+    # all but 5e-5 of it in the out-of-window STN residue band); this batch
+    # measured 8.95e-4 on MI355X
+    assert rel < 2e-3
 
 
 def test_bf16_gradients_vs_float64_autograd():
