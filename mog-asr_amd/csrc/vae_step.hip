@@ -1624,11 +1624,25 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   p.B = B; p.C = C; p.lik_std = lik_std; p.v_pm = v_pm; p.v_pv = v_pv; p.v_plv = v_plv;
   p.x_period = x_period > 0 ? x_period : B;
   hipStream_t s = mog_stream(stream);
-  // Tile height: 64 images per workgroup (one per CU) once the batch gives
-  // every CU at least one such tile, else 32 so small batches still spread
-  // over the chip (two 8-wave workgroups per CU).  MOG_VS_MT overrides: 4 =
-  // 64 images x 16 waves, 2 = 32 images x 8 waves, 3 = 32 images x 16 waves.
-  int mt = B >= 256 * 64 ? 4 : 3;
+  // Tile height: the one with the shorter estimated launch, rounds of tiles
+  // over the CUs x the measured per-tile time (one 16-wave workgroup per CU:
+  // ~112 us per 64-image tile, ~73 us per 32-image tile on MI355X).  64-image
+  // tiles halve the weight stream per image, but a partial last round (the
+  // train step's T*B = 24,576 rows: 1.5 rounds of 64-image tiles, 3 of
+  // 32-image ones) can cost more than they save: 225 -> 220 us, bf16 train
+  // step 2.32 -> 2.28 ms.  MOG_VS_MT overrides: 4 = 64 images x 16 waves,
+  // 2 = 32 images x 8 waves, 3 = 32 images x 16 waves.
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      ncu = v;
+    else
+      ncu = 256;
+  }
+  const long r64 = ((long)B + 64L * ncu - 1) / (64L * ncu), r32 = ((long)B + 32L * ncu - 1) / (32L * ncu);
+  int mt = r64 * 112 <= r32 * 73 ? 4 : 3;
   if (const char* e = getenv("MOG_VS_MT")) {
     const int v = atoi(e);
     if (v == 2 || v == 3 || v == 4) mt = v;
