@@ -283,6 +283,7 @@ int mog_add(const float* a, const float* b, float* out, long n, void* stream);
  * Per-tensor inf/nan -> 0, clip_by_norm(clip), TF ApplyAdam with lr_t given.
  * off/len: tensor table; block_tensor/block_start: block -> (tensor, first
  * element), chunks of mog_optim_chunk_elems() elements; all device arrays.
+ * params / grads / m / v 16-byte aligned, every off[] a multiple of 4.
  * sumsq: device scratch of nblocks floats (each chunk's sum of squares; a
  * tensor's norm is summed from them in chunk order: deterministic, no
  * atomics); sumsq == NULL skips the NaN/Inf zeroing and the clip

@@ -101,10 +101,27 @@ struct HeadPtrs {
   const float* b2[5];   // [k]
 };
 
+// sum_k a[k] w[k ldw] as ONE fma chain in k order (the oracle's dense()).
+// The operands of 32 k-steps are loaded before their fmas: a rolled
+// load-then-fma loop paid one memory round trip per k (16 us per launch at
+// the reference's batch of 64, where the step kernel is one or two
+// workgroups); same fma sequence, same bits.
 __device__ __forceinline__ float chain_dot(const float* a, const float* w, int K, int ldw) {
 #pragma clang fp contract(off)
+  constexpr int KB = 32;
   float acc = 0.0f;
-  for (int k = 0; k < K; ++k) acc = fmaf(a[k], w[(size_t)k * ldw], acc);
+  int k = 0;
+  for (; k + KB <= K; k += KB) {
+    float av[KB], wv[KB];
+#pragma unroll
+    for (int i = 0; i < KB; ++i) {
+      av[i] = a[k + i];
+      wv[i] = w[(size_t)(k + i) * ldw];
+    }
+#pragma unroll
+    for (int i = 0; i < KB; ++i) acc = fmaf(av[i], wv[i], acc);
+  }
+  for (; k < K; ++k) acc = fmaf(a[k], w[(size_t)k * ldw], acc);
   return acc;
 }
 
@@ -177,13 +194,23 @@ __global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp,
   const float hv0 = __shfl(v, 4, 8), hv1 = __shfl(v, 5, 8);
   const float lo = __shfl(v, 6, 8);
   if (b >= B || j != 0) return;
+  // every per-image input loaded up front: the outputs below are stores
+  // through pointers the compiler must assume may alias them, so a load
+  // issued after a store waits for it -- at small batches (one or two
+  // workgroups) those serialized memory round trips were the kernel's time
+  const float e_s = io.eps_scale[b], e_h0 = io.eps_shift[2 * b], e_h1 = io.eps_shift[2 * b + 1];
+  const float uu = io.u[b];
+  const int live = io.live[cfg.step];
+  const float stop_old = io.stop[b];
+  const float rl0 = io.runloss[b];
+  const int dig = io.digits[b];
 
   // scale / shift sampling (air_model.py:471-477, :492-498; :186-192)
   const float svar = mog_expf(slv);
-  const float s = mog_sigmoidf(sm + io.eps_scale[b] * sqrtf(svar));
+  const float s = mog_sigmoidf(sm + e_s * sqrtf(svar));
   const float hvar0 = mog_expf(hv0), hvar1 = mog_expf(hv1);
-  const float tx = mog_tanhf(hm0 + io.eps_shift[2 * b] * sqrtf(hvar0));
-  const float ty = mog_tanhf(hm1 + io.eps_shift[2 * b + 1] * sqrtf(hvar1));
+  const float tx = mog_tanhf(hm0 + e_h0 * sqrtf(hvar0));
+  const float ty = mog_tanhf(hm1 + e_h1 * sqrtf(hvar1));
   float* tf = io.theta_fwd + (size_t)b * 6;
   tf[0] = s; tf[1] = 0.0f; tf[2] = tx; tf[3] = 0.0f; tf[4] = s; tf[5] = ty;
   const float is = 1.0f / s;
@@ -195,7 +222,6 @@ __global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp,
 
   // z_pres (air_model.py:590-620, concrete.py:20-27)
   const float eps = 1e-9f;
-  const float uu = io.u[b];
   const float noise = mog_logf(uu + eps) - mog_logf((1.0f - uu) + eps);
   const float y = (lo + noise) / cfg.temperature;
   float z = mog_sigmoidf(y);
@@ -203,14 +229,12 @@ __global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp,
   io.zprob_out[b] = mog_sigmoidf(lo);
 
   // z_pres KL with the OLD stopping sum (:622-653)
-  const int live = io.live[cfg.step];
   float kl_end = 0.0f;
   if (cfg.use_num_prior) kl_end = concrete_kl(y, -100.0f, cfg.temperature, lo, cfg.temperature);
   const float zkl = concrete_kl(y, prior_log_odds(cfg) + cfg.prior_bias, cfg.temperature, lo,
                                 cfg.temperature);
-  const float stop_old = io.stop[b];
   const bool act_old = stop_old < cfg.thr;
-  float rl = io.runloss[b];
+  float rl = rl0;
   // the z_pres term this step adds (recorded: mog_air_runloss replays the sum)
   const float zterm = live ? (act_old ? zkl : kl_end) : 0.0f;
   if (live) rl = rl + zterm;
@@ -221,7 +245,7 @@ __global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp,
   io.stop[b] = stop_new;
   const bool act = stop_new < cfg.thr;
   if (act) {
-    io.digits[b] += 1;
+    io.digits[b] = dig + 1;
     io.live[cfg.step + 1] = 1;
   }
 

@@ -47,10 +47,22 @@ struct AsrHid {
 
 constexpr int HS = 64;
 
+// one k-ordered fma chain; the operands of 32 k-steps loaded before their
+// fmas (one memory round trip per 32 k, not per k; same bits)
 __device__ __forceinline__ float chain64(const float* a, const float* w, int ldw) {
 #pragma clang fp contract(off)
   float acc = 0.0f;
-  for (int k = 0; k < HS; ++k) acc = fmaf(a[k], w[(size_t)k * ldw], acc);
+#pragma unroll
+  for (int k0 = 0; k0 < HS; k0 += 32) {
+    float av[32], wv[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      av[i] = a[k0 + i];
+      wv[i] = w[(size_t)(k0 + i) * ldw];
+    }
+#pragma unroll
+    for (int i = 0; i < 32; ++i) acc = fmaf(av[i], wv[i], acc);
+  }
   return acc;
 }
 

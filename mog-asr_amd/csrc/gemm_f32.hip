@@ -818,10 +818,14 @@ void launch_dma(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, Gem
   D.nx = mog_cdiv(D.N, BN);
   D.ny = mog_cdiv(D.M, BM);
   dim3 g(D.nx, D.ny, batch * D.splitk);
-  if (!ta && !tb) launch_dma_epi<BM, BN, BK, NS, false, false>(epi, g, s, P, D);
-  else if (!ta && tb) launch_dma_epi<BM, BN, BK, NS, false, true>(epi, g, s, P, D);
-  else if (ta && !tb) launch_dma_epi<BM, BN, BK, NS, true, false>(epi, g, s, P, D);
-  else launch_dma_epi<BM, BN, BK, NS, true, true>(epi, g, s, P, D);
+  if (!ta && !tb) {
+    launch_dma_epi<BM, BN, BK, NS, false, false>(epi, g, s, P, D);
+  } else if (!ta && tb) {
+    launch_dma_epi<BM, BN, BK, NS, false, true>(epi, g, s, P, D);
+  } else if constexpr (BM >= 64) {  // (a transposed A is a row-contiguous image: >= 64 rows)
+    if (!tb) launch_dma_epi<BM, BN, BK, NS, true, false>(epi, g, s, P, D);
+    else launch_dma_epi<BM, BN, BK, NS, true, true>(epi, g, s, P, D);
+  }
 }
 
 // Tile shape (measured on MI355X, scripts/bench_gemm_f32.py):
@@ -850,6 +854,18 @@ void launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, co
                    D.vecB && (ta ? D.M % 4 == 0 : D.K % 4 == 0) &&
                    (tb ? D.K % 4 == 0 : D.N % 4 == 0) && !(tb && P.colsum[0] != nullptr);
   if (dma) {
+    // Small M (the reference's batch of 64: M = 64 / 192 rows): the 64 x 64
+    // grid leaves most CUs idle and every workgroup walks the whole K (no
+    // split-K in a bit-exact forward chain), so 32 x 64 tiles (one 16-row
+    // MFMA tile per wave, 32-deep k-tiles) double the workgroups and halve
+    // each one's MFMA chain per k-step.  Same k order: same bits.
+    const long t64 = (long)mog_cdiv(D.M, 64) * mog_cdiv(D.N, 64) * batch * D.splitk;
+    bool small = !ta && t64 < 128;
+    if (force != nullptr) small = !ta && atoi(force) == 3264;
+    if (small) {
+      launch_dma<32, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
+      return;
+    }
     // stages (measured, scripts/bench_gemm_f32.py): 4 with fragment
     // double-buffering for the split-K weight gradients (transA), 3 for the
     // rest, where a fifth/sixth workgroup per CU beats the deeper pipeline

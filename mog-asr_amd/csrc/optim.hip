@@ -28,8 +28,25 @@ __global__ __launch_bounds__(256) void sanitize_sumsq_kernel(float* g, const lon
   const long base = off[ti], n = len[ti];
   const long c0 = block_start[blockIdx.x];
   const long c1 = min(n, c0 + CHUNK);
+  // 16-byte accesses (tensors start 256-B aligned, chunks at multiples of
+  // CHUNK elements); the ragged end of a tensor element by element
+  const long v1 = c0 + ((c1 - c0) & ~3L);
   float s = 0.0f;
-  for (long i = c0 + threadIdx.x; i < c1; i += 256) {
+  for (long i = c0 + 4 * threadIdx.x; i < v1; i += 1024) {
+    float4 v = *reinterpret_cast<const float4*>(g + base + i);
+    float e[4] = {v.x, v.y, v.z, v.w};
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (isinf(e[k]) || isnan(e[k])) {
+        e[k] = 0.0f;
+        bad = true;
+      }
+    if (bad) *reinterpret_cast<float4*>(g + base + i) = make_float4(e[0], e[1], e[2], e[3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s += e[k] * e[k];
+  }
+  for (long i = v1 + threadIdx.x; i < c1; i += 256) {
     float v = g[base + i];
     if (isinf(v) || isnan(v)) {
       v = 0.0f;
@@ -69,15 +86,34 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* p, const float* g
   }
   const float norm = l2 > 0.0f ? sqrtf(l2) : l2;
   const float denom = fmaxf(norm, clip);
-  for (long i = c0 + threadIdx.x; i < c1; i += 256) {
-    const long k = base + i;
-    const float gc = clipped ? (g[k] * clip) / denom : g[k];
-    float mm = m[k], vv = v[k];
+  auto upd = [&](float gk, float& mm, float& vv, float& pp) {
+    const float gc = clipped ? (gk * clip) / denom : gk;
     mm = mm + (gc - mm) * (1.0f - b1);
     vv = vv + (gc * gc - vv) * (1.0f - b2);
+    pp = pp - (mm * lr_t) / (sqrtf(vv) + eps);
+  };
+  const long v1 = c0 + ((c1 - c0) & ~3L);
+  for (long i = c0 + 4 * threadIdx.x; i < v1; i += 1024) {  // 16-byte accesses
+    const long k = base + i;
+    const float4 g4 = *reinterpret_cast<const float4*>(g + k);
+    float4 m4 = *reinterpret_cast<const float4*>(m + k);
+    float4 v4 = *reinterpret_cast<const float4*>(v + k);
+    float4 p4 = *reinterpret_cast<const float4*>(p + k);
+    upd(g4.x, m4.x, v4.x, p4.x);
+    upd(g4.y, m4.y, v4.y, p4.y);
+    upd(g4.z, m4.z, v4.z, p4.z);
+    upd(g4.w, m4.w, v4.w, p4.w);
+    *reinterpret_cast<float4*>(m + k) = m4;
+    *reinterpret_cast<float4*>(v + k) = v4;
+    *reinterpret_cast<float4*>(p + k) = p4;
+  }
+  for (long i = v1 + threadIdx.x; i < c1; i += 256) {
+    const long k = base + i;
+    float mm = m[k], vv = v[k], pp = p[k];
+    upd(g[k], mm, vv, pp);
     m[k] = mm;
     v[k] = vv;
-    p[k] = p[k] - (mm * lr_t) / (sqrtf(vv) + eps);
+    p[k] = pp;
   }
 }
 
@@ -93,6 +129,10 @@ extern "C" int mog_clip_adam(float* params, float* grads, float* m, float* v, co
                              float beta2, float eps, void* stream) {
   MOG_CHECK_ARG(params && grads && m && v && off && len && block_tensor && block_start);
   MOG_CHECK_ARG(nblocks >= 0);
+  // 16-byte vector accesses: the flat buffers 16-byte aligned (and every
+  // tensor offset a multiple of 4 elements: the parameter store aligns them to 64)
+  for (const void* q : {(const void*)params, (const void*)grads, (const void*)m, (const void*)v})
+    MOG_CHECK_ARG((reinterpret_cast<uintptr_t>(q) & 15) == 0);
   if (nblocks == 0) return 0;
   hipStream_t s = mog_stream(stream);
   if (sumsq != nullptr)

@@ -674,7 +674,7 @@ class AIRModel:
         # heads' backward; the main stream joins them before the glimpse-side
         # all-reduce bucket and the LSTM chain (joining only before Adam, so
         # they would also overlap the LSTM chain and the x-weight gradient,
-        # was measured slower: 3.74 -> 3.81 ms, DESIGN.md §4.4).
+        # was measured slower: 3.74 -> 3.81 ms, DESIGN.md §4.5).
         # (measured: forking them after the STN read backward instead, so that
         # kernel runs alone, leaves the step unchanged -- 3.53 ms either way)
         vae_done = self._vae_weight_grads_async(ws)
