@@ -532,9 +532,12 @@ struct DmaOperand {
   static constexpr int NWQ = NQ / 4;               // per wave
   static constexpr int CPR = BK / 4;               // KC: 16-B chunks per row
   static_assert(NQ % 4 == 0, "four waves share a tile's DMAs");
-  static_assert(KC || ROWS == 64 || ROWS == 128, "RC swizzle");
-  // RC: float offset XOR of k-row k
-  __device__ static __forceinline__ int rcs(int k) { return ROWS == 64 ? (k & 1) << 5 : 0; }
+  static_assert(KC || ROWS == 32 || ROWS == 64 || ROWS == 128, "RC swizzle");
+  // RC: float offset XOR of k-row k (32-float rows: the two k-rows a b32 lane
+  // group reads land in opposite 16-bank halves)
+  __device__ static __forceinline__ int rcs(int k) {
+    return ROWS == 64 ? (k & 1) << 5 : ROWS == 32 ? (k & 1) << 4 : 0;
+  }
   int voff[NWQ];  // this lane's source byte offset at k0 = 0
   int kof[NWQ];   // its k within the tile (KC: first of its 4; RC: its k-row)
   __device__ __forceinline__ void init(int w, int lane, int r0, int ld) {
@@ -860,8 +863,19 @@ void launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, co
     // MFMA tile per wave, 32-deep k-tiles) double the workgroups and halve
     // each one's MFMA chain per k-step.  Same k order: same bits.
     const long t64 = (long)mog_cdiv(D.M, 64) * mog_cdiv(D.N, 64) * batch * D.splitk;
+    const long t3264 = (long)mog_cdiv(D.M, 32) * mog_cdiv(D.N, 64) * batch * D.splitk;
     bool small = !ta && t64 < 128;
-    if (force != nullptr) small = !ta && atoi(force) == 3264;
+    // still under 128 workgroups at 32 x 64 (M = 64 x N = 1024 x-projection
+    // of the reference's batch): 32 x 32 tiles, one 16 x 16 MFMA tile per wave
+    bool tiny = small && t3264 < 128;
+    if (force != nullptr) {
+      small = !ta && (atoi(force) == 3264 || atoi(force) == 3232);
+      tiny = !ta && atoi(force) == 3232;
+    }
+    if (tiny) {
+      launch_dma<32, 32, 32, 2>(ta, tb, epi, s, P, D, batch);
+      return;
+    }
     if (small) {
       launch_dma<32, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
       return;

@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_golden.py tests/test_gpu_graph.py tests/test_gpu_torch_ops.py tests/test_gpu_batched_vae.py tests/test_gpu_asr.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/small2.log 2>&1 || { tail -30 gpurun_out/small2.log; exit 1; }
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_golden.py tests/test_gpu_graph.py tests/test_gpu_torch_ops.py tests/test_gpu_batched_vae.py tests/test_gpu_asr.py tests/test_gpu_dp.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/small2.log 2>&1 || { tail -30 gpurun_out/small2.log; exit 1; }
 tail -1 gpurun_out/small2.log
 timeout -k 10 200 python -u -c "
 import sys, torch; sys.path.insert(0, 'mog-asr_amd'); sys.path.insert(0, '.')

@@ -10,7 +10,14 @@ air64 / air64b (128 images, 64-row shards, fp32 / bf16: the batched T*B-row
 VAE, the VAE weight gradients on the side stream joined before the bucket
 all-reduce -- the configuration bench.py and the trainer run).
 
-usage: gpu_dp_worker.py <out_prefix> air|asr|air64|air64b"""
+Kind rccl1: ONE rank over RCCL (backend "nccl" on the HIP device; RCCL
+refuses two ranks on one GPU, so a one-GPU box can only run it at world 1),
+with the reducer and the global loop-flag hook installed by hand (attach
+installs nothing at world 1): the bucketed async all-reduces and the MAX
+all-reduce of the live flag go through RCCL on the device exactly as on an
+8-GPU node, and the gradient must equal the no-reducer run bit for bit.
+
+usage: gpu_dp_worker.py <out_prefix> air|asr|air64|air64b|rccl1"""
 import os
 import sys
 
@@ -27,7 +34,7 @@ from mog_air import parallel  # noqa: E402
 DEV = "cuda:0"
 
 
-BATCH = {"air": 13, "asr": 11, "air64": 128, "air64b": 128}
+BATCH = {"air": 13, "asr": 11, "air64": 128, "air64b": 128, "rccl1": 128}
 
 
 def air_case(batch=13):
@@ -102,6 +109,11 @@ def run(kind, lo, hi, world, scope, attach=True):
     if attach and world > 1:
         reducer = parallel.attach(m, global_steps=True)
         reducer.log = []
+    if attach and kind == "rccl1":  # world 1 over RCCL: the hooks by hand
+        reducer = parallel.GradReducer()
+        reducer.log = []
+        m.grad_reducer = reducer
+        m.live_hook = lambda live, t: dist.all_reduce(live[t + 1:t + 2], op=dist.ReduceOp.MAX)
     noise = {n: torch.as_tensor(np.ascontiguousarray(v[:, lo:hi])).to(DEV) for n, v in nz.items()}
     grads = m.compute_gradients(x[lo:hi], k[lo:hi], noise=noise,
                                 canvas_cotangent=torch.as_tensor(G[lo:hi]).to(DEV),
@@ -122,7 +134,11 @@ def run(kind, lo, hi, world, scope, attach=True):
 
 def main():
     prefix, kind = sys.argv[1], sys.argv[2]
-    dist.init_process_group("gloo")
+    if kind == "rccl1":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", device_id=torch.device(DEV))
+    else:
+        dist.init_process_group("gloo")
     try:
         rank, world = dist.get_rank(), dist.get_world_size()
         n = BATCH[kind]
