@@ -513,14 +513,18 @@ def main():
                                 "MAX_STEPS 6)"}
                 del m4
             # configs[2] at the reference's own batch of 64
-            el5, m5 = timed_train("fp32", 64, 30, 5, dev,
+            el5, m5 = timed_train("fp32", 64, 30, 5, dev, graph=True,
                                   model=make_asr_model("fp32", dev, "bench_asr_b64"))
+            el5e, m5e = timed_train("fp32", 64, 30, 5, dev,
+                                    model=make_asr_model("fp32", dev, "bench_asr_b64e"))
             out["configs_2_asr_fp32_b64"] = {
                 "value": 64 * 30 / el5, "unit": "images/sec", "ms_per_step": el5 / 30 * 1e3,
                 "dtype": "fp32", "batch": 64, "steps": 30, "max_steps": 6,
+                "eager_ms_per_step": el5e / 30 * 1e3,
                 "workload": "configs[2] (train_air_pr.py -dn 13 -gm 100 -gne 10) at the "
-                            "reference's batch of 64"}
-            del m5
+                            "reference's batch of 64, the captured train step "
+                            "(train_step_graphed); eager_ms_per_step: launched kernel by kernel"}
+            del m5, m5e
             # configs[3]: Multi-dSprites 2-4 objects on 64 x 64 canvases
             # (multi_dsprites.py:391-392, training_air_original.py -data sprites -dn 24),
             # bf16 fused step, max_steps 3 as the headline metric

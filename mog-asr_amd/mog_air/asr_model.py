@@ -21,6 +21,7 @@ steps at the end, as the reference's TensorArrays are (:917-923).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional, Sequence
 
 import numpy as np
@@ -158,6 +159,11 @@ class AIRModel(_AirBase):
         self.fused_step = bool(fused_step) and precision == "bf16" and (
             windows_size == 28 and tuple(vae_recognition_units) == (512, 256)
             and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512))
+        # fp32: the fused fp32 step kernel per loop step (AIRModel._vae_forward_all)
+        self.fused_f32 = bool(fused_step) and precision == "fp32" and (
+            windows_size == 28 and tuple(vae_recognition_units) == (512, 256)
+            and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512)
+            and os.environ.get("MOG_FUSED_F32", "1") != "0")
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         if self.device.type != "cuda":
             raise RuntimeError("AIRModel runs on a HIP device only (no CPU fallback)")
@@ -288,11 +294,20 @@ class AIRModel(_AirBase):
         super()._fill_noise(ws, None)
 
     # ---------------------------------------------------------- forward ---
+    def _f32_parts(self, B: int) -> bool:
+        """fp32 with B >= FUSED_F32_MIN_ROWS: each step's VAE is the fused fp32
+        step kernel over that step's rows (AIRModel._vae_forward_all), writing
+        the step's canvas part (summed in step order by the loss kernel: the
+        running canvas bit for bit).  Smaller batches keep the per-step
+        launches (the fused kernel would leave most CUs idle, and the extra
+        host work of the parts path shows at the reference's batch of 64)."""
+        return self.precision == "fp32" and self.fused_f32 and B >= self.FUSED_F32_MIN_ROWS
+
     def _parts_layout(self, B: int) -> bool:
-        return self.fused_step
+        return self.fused_step or self._f32_parts(B)
 
     def _eps_x_in_kernel(self, B: int) -> bool:
-        return self.fused_step  # the fp32 ASR VAE runs per step and reads eps_x
+        return self.fused_step or self._f32_parts(B)
 
     def _batched_vae(self, B: int) -> bool:
         return False  # per step: the ASR loop feeds z of step t into step t+1's input
@@ -309,7 +324,7 @@ class AIRModel(_AirBase):
         ws.runloss.zero_()
         ws.digits.zero_()
         ws.live.zero_()
-        ws.live[0] = 1
+        ws.live[:1].fill_(1)  # (a fill kernel: a host copy would stall the host)
         thr = self.hyper("stopping_threshold")
         temp = self.hyper("z_pres_temperature")
         lik_std = float(self.hyper("vae_likelihood_std"))
@@ -362,6 +377,9 @@ class AIRModel(_AirBase):
                 self.live_hook(ws.live, t)
             if self.fused_step:
                 self._step_fused(X, ws, t, lik_std)
+                continue
+            if self._f32_parts(B):
+                self._vae_forward_all(X, ws, lik_std, t, t + 1, save=need_grad)
                 continue
             if self.precision == "bf16":
                 self._vae_forward_bf16(X, ws, t, lik_std)

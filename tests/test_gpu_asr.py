@@ -57,12 +57,19 @@ def _setup(seed, **kw):
     return cfg, P, nz, x, k
 
 
-@pytest.mark.parametrize("kw", [dict(), dict(train=False), dict(fix_steps=2),
-                                dict(z_pres_temperature=1.0, stopping_threshold=0.99)])
-def test_asr_forward_bit_exact_vs_oracle(kw):
+@pytest.mark.parametrize("kw,fused", [(dict(), False), (dict(train=False), False),
+                                      (dict(fix_steps=2), False),
+                                      (dict(z_pres_temperature=1.0, stopping_threshold=0.99), False),
+                                      (dict(), True), (dict(fix_steps=2), True)])
+def test_asr_forward_bit_exact_vs_oracle(kw, fused):
+    """fused: each step's glimpse VAE through the fused fp32 step kernel
+    (forced at this small batch; the model uses it from 8192 rows per step),
+    the canvas from per-step parts -- the same bits."""
     cfg, P, nz, x, k = _setup(20, **kw)
     ref = so.forward(cfg, P, nz, x, k)
-    m = _model(cfg, P, "asrf%d" % hash(tuple(sorted(kw.items()))))
+    m = _model(cfg, P, "asrf%d%d" % (hash(tuple(sorted(kw.items()))), fused))
+    if fused:
+        m.FUSED_F32_MIN_ROWS = 0
     m.infer(x, k, noise={n: torch.as_tensor(v).to(DEV) for n, v in nz.items()})
     T = ref["T"]
     assert m.executed_steps == T
@@ -88,6 +95,9 @@ def test_asr_forward_bit_exact_vs_oracle(kw):
 @pytest.mark.parametrize("kw,precision,tol,cos_min,global_tol",
                          [(dict(), "fp32", 2e-3, 0.999, 2e-3),
                           (dict(fix_steps=2), "fp32", 2e-3, 0.999, 2e-3),
+                          # the fused fp32 step kernel's saved activations into the
+                          # same backward (forced at this batch)
+                          (dict(), "fp32-fused", 2e-3, 0.999, 2e-3),
                           # bf16: the bf16 VAE latents feed the next step's LSTM input
                           # and the shift / scale heads in ASR (unlike AIR), so the bf16
                           # forward trajectory itself drifts from the float64 one.  Some
@@ -106,7 +116,11 @@ def test_asr_gradients_vs_float64_autograd(kw, precision, tol, cos_min, global_t
     cfg, P, nz, x, k = _setup(30, **kw)
     rng = np.random.default_rng(31)
     Gc = (rng.standard_normal((cfg.batch, cfg.canvas_size ** 2)) * 0.01).astype(np.float32)
-    m = _model(cfg, P, "asrg%s%s" % (precision, cfg.fix_steps), precision)
+    fused = precision == "fp32-fused"
+    precision = "fp32" if fused else precision
+    m = _model(cfg, P, "asrg%s%s%d" % (precision, cfg.fix_steps, fused), precision)
+    if fused:
+        m.FUSED_F32_MIN_ROWS = 0
     grads = m.compute_gradients(x, k, noise={n: torch.as_tensor(v).to(DEV) for n, v in nz.items()},
                                 canvas_cotangent=torch.as_tensor(Gc).to(DEV))
     Pt = {n: torch.tensor(v, dtype=torch.float64, requires_grad=True) for n, v in P.items()}

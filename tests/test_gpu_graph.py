@@ -87,3 +87,19 @@ def test_graph_outputs_accessible_after_replay():
     torch.cuda.synchronize()
     assert me.loss == mg.loss
     np.testing.assert_array_equal(me.reconstruction.cpu().numpy(), mg.reconstruction.cpu().numpy())
+
+
+def test_asr_graph_replay_matches_eager_bitwise():
+    """The AIR-ASR train step (train_air_pr.py -dn 13 -gm 100 -gne 10 at the
+    reference's batch of 64) captured and replayed: same bits as eager."""
+    import bench
+    me = bench.make_asr_model("fp32", torch.device(DEV), "gasr_e")
+    mg = bench.make_asr_model("fp32", torch.device(DEV), "gasr_g")
+    for x, k in _batches(3):
+        me.train_step_async(x, k)
+        mg.train_step_graphed(x, k)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(me._ws.means[:3].cpu().numpy(),
+                                      mg._ws.means[:3].cpu().numpy())
+    assert mg._graph is not None
+    assert torch.equal(me.params.flat.view(torch.int32), mg.params.flat.view(torch.int32))
