@@ -216,9 +216,14 @@ __global__ __launch_bounds__(256) void asr_step_fwd_kernel(AsrCfg cfg, AsrW W, A
   const float gsm0 = sv[m][4], gsm1 = sv[m][5], gslv0 = sv[m][6], gslv1 = sv[m][7];
   const float lo = sv[m][8], plo = sv[m][9];
   const float cm = sv[m][12], clv = sv[m][13];
+  // every per-image input read before the first store (stores through
+  // possibly-aliasing pointers would otherwise order each later load behind
+  // them: one memory round trip per load on this one-lane chain)
+  const float e_s = io.eps_scale[b], uu = io.u[b], stop_old = io.stop[b];
+  const int live = io.live[cfg.step], dig = io.digits[b];
   const float tx = mog_tanhf(sl0), ty = mog_tanhf(sl1);
   const float cvar = mog_expf(clv);
-  const float cl = cm + io.eps_scale[b] * sqrtf(cvar);
+  const float cl = cm + e_s * sqrtf(cvar);
   const float s = mog_sigmoidf(cl);
   float* tf = io.theta_fwd + (size_t)b * 6;
   tf[0] = s; tf[1] = 0.0f; tf[2] = tx; tf[3] = 0.0f; tf[4] = s; tf[5] = ty;
@@ -232,14 +237,12 @@ __global__ __launch_bounds__(256) void asr_step_fwd_kernel(AsrCfg cfg, AsrW W, A
   io.shift[2 * b + 1] = ty;
   // z_pres (:604-620)
   const float eps = 1e-9f;
-  const float uu = io.u[b];
   const float noise = mog_logf(uu + eps) - mog_logf((1.0f - uu) + eps);
   const float y = (lo + noise) / cfg.temperature;
   float z = mog_sigmoidf(y);
   if (!cfg.train) z = rintf(z);
   const float zprob = mog_sigmoidf(lo);
   io.zprob[b] = zprob;
-  const int live = io.live[cfg.step];
   // entropy regulariser (:660-668), every executed step
   float prn = 0.0f;
   if (cfg.g_num > 1e-8f) {
@@ -247,14 +250,13 @@ __global__ __launch_bounds__(256) void asr_step_fwd_kernel(AsrCfg cfg, AsrW W, A
     prn = ent * cfg.g_num;
   }
   // z_pres KL with the OLD stopping sum (:688-703)
-  const float stop_old = io.stop[b];
   const bool act_old = stop_old < cfg.thr;
   const float zkl = concrete_kl(y, plo, cfg.temperature, lo, cfg.temperature);
   const float stop_new = stop_old + (1.0f - z);
   io.stop[b] = stop_new;
   const bool act = stop_new < cfg.thr;
   if (act) {
-    io.digits[b] += 1;
+    io.digits[b] = dig + 1;
     io.live[cfg.step + 1] = 1;
   }
   // scale / shift KLs with the NEW stopping sum (:728-765)
