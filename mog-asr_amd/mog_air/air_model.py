@@ -677,7 +677,7 @@ class AIRModel:
         # was measured slower: 3.74 -> 3.81 ms).
         # (measured: forking them after the STN read backward instead, so that
         # kernel runs alone, leaves the step unchanged -- 3.53 ms either way)
-        vae_done = self._vae_weight_grads_async(ws)
+        w1_done, vae_done = self._vae_weight_grads_async(ws)
         # STN read backward of all steps against the shared input canvas
         ops.stn_backward(X, ws.th_f, (W, W), ws.dg_all, want_dU=False, dtheta=ws.dth_f_all,
                          n=TB)
@@ -694,14 +694,29 @@ class AIRModel:
         # dh[t] = sum_z dhid_z W1_z^T for every step: one plain GEMM over
         # K = 5 HS ([dhid_0 .. dhid_4] rows against [W1_0 .. W1_4]), the same
         # k-ordered chain as the per-head sum
-        gemm([ws.dhid], [self._w1cat()], [ws.dh], TB, H, 5 * HS, 5 * HS, 5 * HS, H,
+        torch.cuda.current_stream().wait_event(w1_done)
+        gemm([ws.dhid], [self._w1cat_buf], [ws.dh], TB, H, 5 * HS, 5 * HS, 5 * HS, H,
              transB=True)
-        # the heads' and the VAE's weight gradients are final here: their
-        # all-reduce bucket runs while the LSTM chain below computes
-        self._weight_grads_heads(ws)
-        torch.cuda.current_stream().wait_event(vae_done)
-        split = self._bucket_split()
-        self._reduce_bucket(split, self.params.total)
+        heads_side = self.grad_reducer is None and self.HEADS_WGRAD_SIDE
+        if heads_side:
+            # one GPU, no bucket to hand over: the heads' weight gradients
+            # follow the VAE's on the side stream, under the latency-bound
+            # LSTM chain; the main stream joins them before Adam
+            main, side = torch.cuda.current_stream(), self._side_stream()
+            heads_ready = torch.cuda.Event()
+            heads_ready.record(main)
+            side.wait_event(heads_ready)
+            with torch.cuda.stream(side):
+                self._weight_grads_heads(ws)
+                vae_done = torch.cuda.Event()
+                vae_done.record(side)
+        else:
+            # the heads' and the VAE's weight gradients are final here: their
+            # all-reduce bucket runs while the LSTM chain below computes
+            self._weight_grads_heads(ws)
+            torch.cuda.current_stream().wait_event(vae_done)
+            split = self._bucket_split()
+            self._reduce_bucket(split, self.params.total)
         ws.dGsum.zero_()
         for t in reversed(range(T)):
             dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
@@ -712,6 +727,11 @@ class AIRModel:
                 gemm([ws.dG[t]], [Wh], [ws.dh[t - 1]], B, H, 4 * H, 4 * H, 4 * H, H,
                      transB=True, Cin=[ws.dh[t - 1]])
         self._weight_grads_lstm(X, ws)
+        if heads_side:
+            torch.cuda.current_stream().wait_event(vae_done)
+
+    # single GPU: heads' weight gradients on the side stream (see _backward)
+    HEADS_WGRAD_SIDE = os.environ.get("MOG_HEADS_SIDE", "1") == "1"
 
     def _vae_backward_fp32_all(self, ws, gscale):
         TB = ws.B * self.max_steps
@@ -1024,13 +1044,18 @@ class AIRModel:
         ready.record(main)
         side.wait_event(ready)
         with torch.cuda.stream(side):
+            # the heads' concatenated W1 (B operand of the dh GEMM) first: off
+            # the main stream, which waits for it only at that GEMM
+            self._w1cat()
+            w1_done = torch.cuda.Event()
+            w1_done.record(side)
             if self.precision == "bf16":
                 self._vae_weight_grads_bf16(ws)
             else:
                 self._vae_weight_grads_fp32(ws)
             done = torch.cuda.Event()
             done.record(side)
-        return done
+        return w1_done, done
 
     def _w1cat(self):
         """[W1_0 .. W1_4] side by side ([H, 5 HS]): the B operand of the heads'
