@@ -20,6 +20,7 @@ No host synchronisation happens inside a train step.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from typing import Dict, Optional
@@ -374,6 +375,7 @@ class AIRModel:
 
     def _fill_noise(self, ws: _Workspace, noise: Optional[Dict[str, torch.Tensor]]):
         ws.eps_x_offset = None  # injected noise: every consumer reads the buffers
+        ws.noise_side = False
         if noise is not None:
             for k in ("eps_scale", "eps_shift", "eps_z", "eps_x", "u"):
                 src = noise[k]
@@ -383,17 +385,31 @@ class AIRModel:
                                      f"expected {tuple(dst.shape)}")
                 dst.copy_(src)
             return
-        for k, normal in (("eps_scale", True), ("eps_shift", True), ("eps_z", True),
-                          ("eps_x", True), ("u", False)):
-            buf = getattr(ws, k)
-            if k == "eps_x" and self._eps_x_in_kernel(ws.B) and not self._graph_noise:
-                # generated inside the fused step kernel / the fp32 output
-                # layer's epilogue from the same Philox counters (bit-identical
-                # to filling the buffer)
-                ws.eps_x_offset = self._noise_ctr
-            else:
-                ops.rng_fill(buf, self.noise_seed, self._noise_ctr, normal)
-            self._noise_ctr += (buf.numel() + 3) // 4
+        side = None
+        if self.NOISE_ON_SIDE:
+            # on the side stream, under the x-projection (which needs none of
+            # it); _forward joins it after that GEMM
+            side = self._side_stream()
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream())
+            side.wait_event(ready)
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            for k, normal in (("eps_scale", True), ("eps_shift", True), ("eps_z", True),
+                              ("eps_x", True), ("u", False)):
+                buf = getattr(ws, k)
+                if k == "eps_x" and self._eps_x_in_kernel(ws.B) and not self._graph_noise:
+                    # generated inside the fused step kernel / the fp32 output
+                    # layer's epilogue from the same Philox counters
+                    # (bit-identical to filling the buffer)
+                    ws.eps_x_offset = self._noise_ctr
+                else:
+                    ops.rng_fill(buf, self.noise_seed, self._noise_ctr, normal)
+                self._noise_ctr += (buf.numel() + 3) // 4
+        ws.noise_side = side is not None
+
+    # AIR's _forward joins side-stream noise after the x-projection (the ASR
+    # subclass fills on the current stream)
+    NOISE_ON_SIDE = True
 
     # ----------------------------------------------------------- forward ---
     def _forward(self, X: torch.Tensor, targets: Optional[torch.Tensor], ws: _Workspace,
@@ -407,13 +423,20 @@ class AIRModel:
         K = self._P("rnn/basic_lstm_cell/kernel")
         bK = self._P("rnn/basic_lstm_cell/bias")
         Wx, Wh = K[:C2], K[C2:]
-        if ws.cparts is None:  # parts: the loss kernel sums them into the canvas
-            ws.canvas.zero_()
-        ws.stop.zero_()
-        ws.runloss.zero_()
-        ws.digits.zero_()
-        ws.live.zero_()
-        ws.live[:1].fill_(1)  # (a fill kernel: capturable, unlike a host copy)
+        side = self._side_stream() if getattr(ws, "noise_side", False) else None
+        ws.noise_side = False
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            # (after the noise on the side stream, when it went there)
+            if ws.cparts is None:  # parts: the loss kernel sums them into the canvas
+                ws.canvas.zero_()
+            ws.stop.zero_()
+            ws.runloss.zero_()
+            ws.digits.zero_()
+            ws.live.zero_()
+            ws.live[:1].fill_(1)  # (a fill kernel: capturable, unlike a host copy)
+            if side is not None:
+                pre_done = torch.cuda.Event()
+                pre_done.record(side)
         prior_lo = self.hyper("z_pres_prior_log_odds")
         temperature = self.hyper("z_pres_temperature")
         thr = self.hyper("stopping_threshold")
@@ -422,6 +445,8 @@ class AIRModel:
         # hoisted x-projection of the LSTM input (input is loop-invariant in AIR)
         with self._timed("lstm_x_projection"):
             gemm([X], [Wx], [ws.Gx], B, 4 * H, C2, C2, 4 * H, 4 * H)
+        if side is not None:
+            torch.cuda.current_stream().wait_event(pre_done)
         w1 = [self._P(h + "/hidden/weights") for h in self._HEADS]
         b1 = [self._P(h + "/hidden/biases") for h in self._HEADS]
         w2 = [self._P(h + "/output/weights") for h in self._HEADS]
@@ -671,10 +696,12 @@ class AIRModel:
         # The VAE weight gradients need only the activations and the VAE input
         # gradients, final here: they run on a second stream (MFMA-bound
         # split-K GEMMs) under the latency-bound STN read backward and the
-        # heads' backward; the main stream joins them before the glimpse-side
-        # all-reduce bucket and the LSTM chain (joining only before Adam, so
-        # they would also overlap the LSTM chain and the x-weight gradient,
-        # was measured slower: 3.74 -> 3.81 ms).
+        # heads' backward.  Data parallel: the main stream joins them before
+        # the glimpse-side all-reduce bucket and the LSTM chain.  One GPU: the
+        # heads' weight gradients follow them on the side stream and the join
+        # is before Adam, so both overlap the LSTM chain (3.49 -> 3.45 ms;
+        # the VAE's alone joined before Adam, heads on the main stream, was
+        # measured slower in round 2: 3.74 -> 3.81 ms).
         # (measured: forking them after the STN read backward instead, so that
         # kernel runs alone, leaves the step unchanged -- 3.53 ms either way)
         w1_done, vae_done = self._vae_weight_grads_async(ws)
@@ -1206,6 +1233,9 @@ class AIRModel:
             gT.copy_(tg)
         ws = self._ws
         self._fill_noise(ws, None)
+        if ws.noise_side:  # the graph's first launch reads it
+            torch.cuda.current_stream().wait_stream(self._side_stream())
+            ws.noise_side = False
         self._prior_dev.fill_(self.hyper("z_pres_prior_log_odds"))
         self._graph.replay()
         self.params.apply_adam(self.hyper("learning_rate"), self.gradient_clipping_norm)

@@ -121,6 +121,8 @@ class AIRModel(_AirBase):
     """See module docstring.  Extra keyword-only arguments as the AIR model
     (device, seed, noise_seed, grad_world, precision, fused_step)."""
 
+    NOISE_ON_SIDE = False  # _forward below uses the noise from its first launch
+
     _SCOPE_PREFIX = ROOT
 
     def __init__(self, input_images=None, target_num_digits=None, max_steps=3, max_digits=2,
