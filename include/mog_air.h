@@ -39,6 +39,18 @@ int mog_gemm_f32(int batch, const float* const* A, const float* const* B, float*
                  const float* const* aux, float* const* colsum, int M, int N, int K, int lda,
                  int ldb, int ldc, int ldaux, int transA, int transB, int epi, float aux_scale,
                  int splitk, void* stream);
+
+/* fp32 weight gradient on the bf16 matrix cores (mog-asr_amd/csrc/gemm_x3.hip):
+ * C[m][n] += sum_k A[k*lda+m] B[k*ldb+n] (atomic, split into `splitk` k-ranges),
+ * colsum[n] += sum_k B[k*ldb+n] when colsum != NULL.  Each fp32 operand is split
+ * exactly into three bf16 pieces; the six products down to 2^-16 relative are
+ * accumulated in fp32 (error of the order of one fp32 product rounding; not a
+ * k-ordered chain, so tolerance-gated like every split-K gradient).  The x-part
+ * of the LSTM kernel gradient (TF MatMul gradient of air_model.py:454-456).
+ * A, B 16-byte aligned; M, N, lda, ldb multiples of 4. */
+int mog_gemm_f32_x3_tn(const float* A, const float* B, float* C, float* colsum, int M, int N,
+                       int K, int lda, int ldb, int ldc, int splitk, void* stream);
+
 /* C = sigmoid((A B + bias) + scale * eps) for A [M][K] (lda), B [K][N] (ldb):
  * the VAE output layer (vae.py:44-46) with the likelihood noise eps generated
  * in the epilogue -- element (m, n) is lane n % 4 of Philox4x32-10 quad

@@ -1,0 +1,238 @@
+// fp32 weight gradient on the bf16 matrix cores: C[M][N] += sum_k A[k][m] B[k][n]
+// (both operands fp32, k-major: dW = X^T dY over the batch rows), split-K with fp32
+// atomics, optional column sums of B (the bias gradient).
+//
+// Every fp32 operand is split EXACTLY into three bf16 pieces by truncation,
+// x = x0 + x1 + x2 (x0 = the top 8 significand bits, x1 the next 8 of x - x0,
+// x2 = the rest, which has at most 8 significant bits), so
+//   a b = sum_{i+j<=2} a_i b_j  +  (a1 b2 + a2 b1 + a2 b2)
+// and the six kept products carry every term down to 2^-16 of a b; the dropped
+// three are below 2^-23 of it -- the size of the rounding of one fp32 product.
+// bf16 x bf16 products are exact in the MFMA's fp32 accumulator, so the result
+// differs from an fp32 fma chain by summation order only (a gradient, gated by
+// tolerance like every split-K/atomic gradient; the forward layers keep the
+// bit-exact fp32 kernels of gemm_f32.hip).  Six v_mfma_f32_16x16x32_bf16 per
+// 16x16x32 block against eight v_mfma_f32_16x16x4_f32: 96 vs 256 MFMA cycles.
+//
+// Tile 128 x 128 x 32, four waves of 64 x 64.  Each k-tile is loaded as fp32
+// float4 rows (k-major, coalesced), split in registers and stored as three
+// k-major bf16 LDS images per operand; fragments come out with the gfx950
+// transpose read ds_read_b64_tr_b16 (as the TN form of gemm_bf16.hip).  One
+// LDS stage, register prefetch of the next k-tile, two workgroups per CU.
+//
+// Measured (scripts/x3_time.py, M 2500 x N 1024 x K 8192 with the column sums):
+// 318 us at split-K 8 against 410 us for the fp32 MFMA split-K GEMM; inside the
+// fp32 train step no change (3.433 vs 3.434 ms: the x-part gradient shares the
+// chip with the side-stream weight gradients), so the model keeps the fp32
+// chain by default (AIRModel.X_GRAD_X3, MOG_X_GRAD_X3=1 selects this form).
+// MFMA is ~38 % busy here: the per-workgroup split (7 VALU per element, each
+// A tile split again by every workgroup of its row panel) is the next cost.
+#include <cstdlib>
+
+#include "mog_common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int LDR = BM + 8;                 // LDS row (k) pitch in bf16 (BM == BN)
+constexpr int PIECE = BK * LDR;             // one bf16 image
+constexpr int STAGE = 6 * PIECE;            // A0 A1 A2 B0 B1 B2
+constexpr int NL = (BM * BK / 4) / 256;     // float4 loads per thread per operand (4)
+
+// bijective XCD-grouping remap of the linear workgroup id (as gemm_bf16.hip)
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// the three truncated bf16 pieces of one float (as fp32 bit patterns whose low
+// halves are zero, except lo's, which the packing drops)
+__device__ __forceinline__ void split1(float f, unsigned& hi, unsigned& mid, unsigned& lo) {
+  hi = __float_as_uint(f) & 0xffff0000u;
+  const float r1 = f - __uint_as_float(hi);  // exact
+  mid = __float_as_uint(r1) & 0xffff0000u;
+  lo = __float_as_uint(r1 - __uint_as_float(mid));  // exact, <= 8 significant bits
+}
+
+__device__ __forceinline__ unsigned pack2(unsigned a, unsigned b) {
+  return (a >> 16) | (b & 0xffff0000u);
+}
+
+// the pieces of four floats, packed two bf16 per dword
+__device__ __forceinline__ void split4(const float4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
+  unsigned h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
+  split1(v.x, h0, m0, l0);
+  split1(v.y, h1, m1, l1);
+  split1(v.z, h2, m2, l2);
+  split1(v.w, h3, m3, l3);
+  p0.x = pack2(h0, h1);
+  p0.y = pack2(h2, h3);
+  p1.x = pack2(m0, m1);
+  p1.y = pack2(m2, m3);
+  p2.x = pack2(l0, l1);
+  p2.y = pack2(l2, l3);
+}
+
+struct X3Args {
+  const float* A;
+  const float* B;
+  float* C;
+  float* colsum;
+  int M, N, K, lda, ldb, ldc, kchunk, nx, ny;
+};
+
+__global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[STAGE];
+
+  const int nwg = gridDim.x;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int bx = wg % D.nx, by = (wg / D.nx) % D.ny, ks = wg / (D.nx * D.ny);
+  const int m0 = by * BM, n0 = bx * BN;
+  const int kbeg = ks * D.kchunk;
+  const int kend = min(D.K, kbeg + D.kchunk);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const int M = D.M, N = D.N;
+  // staging roles: float4 i of this thread covers k-row t/32 + 8 i, columns 4 (t % 32) ..
+  const int sk = t >> 5, sc = (t & 31) * 4;
+  const bool do_cs = D.colsum != nullptr && by == 0;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  float4 ra[NL], rb[NL];
+  const float4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  auto load_tiles = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int gk = k0 + sk + 8 * i;
+      const int gm = m0 + sc, gn = n0 + sc;
+      ra[i] = (gk < kend && gm < M)
+                  ? *reinterpret_cast<const float4*>(D.A + (size_t)gk * D.lda + gm) : zero4;
+      rb[i] = (gk < kend && gn < N)
+                  ? *reinterpret_cast<const float4*>(D.B + (size_t)gk * D.ldb + gn) : zero4;
+    }
+  };
+  auto store_tiles = [&](int stage) {
+    __bf16* S = lds + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int o = (sk + 8 * i) * LDR + sc;
+      u32x2 p0, p1, p2;
+      split4(ra[i], p0, p1, p2);
+      *reinterpret_cast<u32x2*>(S + 0 * PIECE + o) = p0;
+      *reinterpret_cast<u32x2*>(S + 1 * PIECE + o) = p1;
+      *reinterpret_cast<u32x2*>(S + 2 * PIECE + o) = p2;
+      split4(rb[i], p0, p1, p2);
+      *reinterpret_cast<u32x2*>(S + 3 * PIECE + o) = p0;
+      *reinterpret_cast<u32x2*>(S + 4 * PIECE + o) = p1;
+      *reinterpret_cast<u32x2*>(S + 5 * PIECE + o) = p2;
+      if (do_cs) {
+        cs[0] += rb[i].x;
+        cs[1] += rb[i].y;
+        cs[2] += rb[i].z;
+        cs[3] += rb[i].w;
+      }
+    }
+  };
+
+  const int g = lane >> 4, li = lane & 15;
+  const int tq = li >> 2, tp = li & 3;  // transpose-read roles (gemm_bf16.hip TN form)
+  auto frag = [&](const __bf16* P, int col) -> bf16x8 {
+    const __bf16* p0 = P + (8 * g + tq) * LDR + col + 4 * tp;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p0 + 4 * LDR));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto compute = [&](int stage) {
+    const __bf16* S = lds + stage * STAGE;
+    bf16x8 a[3][4], b[3][4];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[p][i] = frag(S + p * PIECE, wm + 16 * i);
+        b[p][i] = frag(S + (3 + p) * PIECE, wn + 16 * i);
+      }
+    // smallest terms first: (2,0) (1,1) (0,2), (1,0) (0,1), (0,0)
+    auto pass = [&](const bf16x8 (&x)[4], const bf16x8 (&y)[4]) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[mi], y[ni], acc[mi][ni], 0, 0, 0);
+    };
+    pass(a[2], b[0]);
+    pass(a[1], b[1]);
+    pass(a[0], b[2]);
+    pass(a[1], b[0]);
+    pass(a[0], b[1]);
+    pass(a[0], b[0]);
+  };
+
+  const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
+  {
+    // one LDS stage (52 KB: two workgroups per CU overlap each other's split
+    // and MFMA phases; two stages at one workgroup per CU measured 417 vs
+    // 318 us); the next k-tile's loads are in flight under the MFMAs
+    if (nk > 0) load_tiles(kbeg);
+    for (int it = 0; it < nk; ++it) {
+      store_tiles(0);
+      if (it + 1 < nk) load_tiles(kbeg + (it + 1) * BK);
+      __syncthreads();
+      compute(0);
+      __syncthreads();
+    }
+  }
+  if (do_cs) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (n0 + sc + c < N) atomicAdd(D.colsum + n0 + sc + c, cs[c]);
+  }
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + mi * 16 + (lane >> 4) * 4 + r;
+        const int col = n0 + wn + ni * 16 + (lane & 15);
+        if (row < M && col < N) atomicAdd(D.C + (size_t)row * D.ldc + col, acc[mi][ni][r]);
+      }
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int mog_gemm_f32_x3_tn(const float* A, const float* B, float* C, float* colsum,
+                                  int M, int N, int K, int lda, int ldb, int ldc, int splitk,
+                                  void* stream) {
+  MOG_CHECK_ARG(A && B && C && M >= 0 && N >= 0 && K >= 0 && splitk >= 1);
+  // float4 rows: 16-byte operands, widths and strides multiples of 4
+  MOG_CHECK_ARG(al16(A) && al16(B) && M % 4 == 0 && N % 4 == 0 && lda % 4 == 0 &&
+                ldb % 4 == 0 && lda >= M && ldb >= N && ldc >= N);
+  if (M == 0 || N == 0 || K == 0) return 0;
+  X3Args D;
+  D.A = A; D.B = B; D.C = C; D.colsum = colsum;
+  D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc;
+  int kchunk = (K + splitk - 1) / splitk;
+  kchunk = ((kchunk + BK - 1) / BK) * BK;
+  D.kchunk = kchunk;
+  const int nsplit = (K + kchunk - 1) / kchunk;
+  D.nx = mog_cdiv(N, BN);
+  D.ny = mog_cdiv(M, BM);
+  const long nwg = (long)D.nx * D.ny * nsplit;
+  gemm_x3_tn_kernel<<<dim3((unsigned)nwg), 256, 0, mog_stream(stream)>>>(D);
+  MOG_LAUNCH_RET();
+}

@@ -828,7 +828,22 @@ void asr_step_backward_(int64_t B, bool train, int64_t fix_steps, double tempera
 
 }  // namespace
 
+void gemm_f32_x3_tn_(const Tensor& A, const Tensor& B, Tensor C, const optional<Tensor>& colsum,
+                     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc,
+                     int64_t splitk) {
+  Op o("gemm_f32_x3_tn_");
+  float* c = o.f(C, mat(M, N, ldc), "C");
+  float* a = o.f(A, mat(K, M, lda), "A");
+  float* b = o.f(B, mat(K, N, ldb), "B");
+  float* cs = o.f(colsum, N, "colsum");
+  GUARD(o);
+  check(mog_gemm_f32_x3_tn(a, b, c, cs, M, N, K, lda, ldb, ldc, splitk, o.stream()), o.name);
+}
+
 TORCH_LIBRARY_FRAGMENT(mog_air, m) {
+  m.def(
+      "gemm_f32_x3_tn_(Tensor A, Tensor B, Tensor(a!) C, Tensor(b!)? colsum, int M, int N, "
+      "int K, int lda, int ldb, int ldc, int splitk) -> ()");
   m.def(
       "gemm_f32_(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, Tensor?[] Cin, "
       "Tensor(b!)?[] Cpre, Tensor?[] aux, Tensor(c!)?[] colsum, int M, int N, int K, int lda, "
@@ -960,6 +975,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("gemm_f32_", &gemm_f32_);
   m.impl("gemm_f32_kseg_", &gemm_f32_kseg_);
   m.impl("gemm_f32_sigmoid_philox_", &gemm_f32_sigmoid_philox_);
+  m.impl("gemm_f32_x3_tn_", &gemm_f32_x3_tn_);
   m.impl("gemm_bf16_", &gemm_bf16_);
   m.impl("cvt_bf16_batch_", &cvt_bf16_batch_);
   m.impl("stn_forward_", &stn_forward_);

@@ -25,6 +25,7 @@ ULL = ctypes.c_ulonglong
 _SIGS = {
     "mog_gemm_f32": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, I, P],
     "mog_gemm_f32_kseg": [I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "mog_gemm_f32_x3_tn": [P, P, P, P, I, I, I, I, I, I, I, P],
     "mog_gemm_f32_sigmoid_philox": [P, P, P, P, I, I, I, I, I, I, F, ULL, ULL, P],
     "mog_stn_forward": [P, I, I, I, P, I, I, P, P, P, I, P],
     "mog_stn_backward": [P, I, I, I, P, I, I, P, P, P, P, P, I, I, P],

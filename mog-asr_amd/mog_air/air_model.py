@@ -1109,6 +1109,13 @@ class AIRModel:
                      [self._G(h + "/output/weights") for _, h in sel], TB, HS, k, HS, 2,
                      [self._G(h + "/output/biases") for _, h in sel])
 
+    # fp32 configuration, opt-in (MOG_X_GRAD_X3=1): the x-part of the LSTM
+    # kernel gradient on the bf16 matrix cores with exact three-piece operand
+    # splits (gemm_x3.hip: 318 vs 410 us stand-alone, no change inside the
+    # step); default: the fp32 MFMA split-K GEMM
+    X_GRAD_X3 = os.environ.get("MOG_X_GRAD_X3", "0") == "1"
+    X3_SPLITK = int(os.environ.get("MOG_X3_SPLITK", "8"))
+
     # rows of the x-part of the LSTM kernel gradient per all-reduce bucket
     # (multiple of the 64-row GEMM tile; data parallel only)
     X_GRAD_CHUNK = 640
@@ -1136,6 +1143,11 @@ class AIRModel:
                     # bf16 configuration: X^T dGsum on bf16 operands (fp32
                     # accumulate); the forward x-projection stays fp32
                     self._x_grad_bf16(X, ws, gK, bias, m0, m1)
+                elif self.X_GRAD_X3:
+                    # fp32 operands split exactly into three bf16 pieces on the
+                    # bf16 matrix cores (gemm_x3.hip: fp32-level accuracy)
+                    ops.gemm_x3_tn(X[:, m0:], ws.dGsum, gK[m0:m1], m1 - m0, 4 * H, B, C2, 4 * H,
+                                   4 * H, splitk=self.X3_SPLITK, colsum=bias)
                 else:
                     self._dw(X[:, m0:], ws.dGsum, gK[m0:m1], B, m1 - m0, 4 * H, C2, 4 * H, bias)
                 if m1 < C2:

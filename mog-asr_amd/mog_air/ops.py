@@ -56,6 +56,14 @@ def gemm(A: Sequence[torch.Tensor], B: Sequence[torch.Tensor], C: Sequence[torch
                    bool(transA), bool(transB), epi, float(aux_scale), int(splitk))
 
 
+def gemm_x3_tn(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: int,
+               lda: int, ldb: int, ldc: int, splitk: int = 8, colsum=None) -> None:
+    """C[M,N] += A^T B over K rows on the bf16 matrix cores with exact
+    three-piece operand splits (fp32-level accuracy; mog_gemm_f32_x3_tn);
+    colsum += column sums of B."""
+    _ops.gemm_f32_x3_tn_(A, B, C, colsum, M, N, K, lda, ldb, ldc, int(splitk))
+
+
 def gemm_sigmoid_philox(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias, M: int, N: int,
                         K: int, lda: int, ldb: int, ldc: int, scale: float, seed: int,
                         offset: int) -> None:

@@ -1,0 +1,98 @@
+"""The fp32 weight-gradient GEMM on the bf16 matrix cores (csrc/gemm_x3.hip,
+mog_gemm_f32_x3_tn): C += A^T B with every operand split exactly into three
+bf16 pieces.  Bar: fp32-level accuracy -- the error against a float64 product,
+normalised by |A|^T |B|, within 1e-6 everywhere and no larger than 2x the
+error of the fp32 MFMA chain (mog_gemm_f32, the form it replaces for the
+LSTM x-part gradient, air_model.py:454-456) on the same operands; column sums
+of B within the same bound.  Ragged shapes, split-K counts, a column window of
+a wider operand (the data-parallel row chunks) and a wide exponent range (the
+exact split must hold for every binade)."""
+import numpy as np
+import pytest
+import torch
+
+from mog_air import ops
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _case(M, N, K, lda, ldb, spread, seed):
+    g = torch.Generator().manual_seed(seed)
+    A = torch.randn(K, lda, generator=g, dtype=torch.float64)
+    B = torch.randn(K, ldb, generator=g, dtype=torch.float64)
+    if spread:
+        A *= torch.exp2(torch.randint(-spread, spread + 1, A.shape, generator=g).double())
+        B *= torch.exp2(torch.randint(-spread, spread + 1, B.shape, generator=g).double())
+    return A.float(), B.float()
+
+
+def _err(got, ref, scale):
+    return float(((got.double() - ref).abs() / (scale + 1e-300)).max())
+
+
+@pytest.mark.parametrize("M,N,K,lda,ldb,m0,splitk,spread", [
+    (2500, 1024, 8192, 2500, 1024, 0, 8, 0),     # the x-part gradient of the bench step
+    (640, 1024, 4096, 2500, 1024, 1280, 4, 0),   # a data-parallel row chunk (column window)
+    (132, 36, 77, 136, 36, 0, 1, 0),             # ragged tiles, K not a multiple of 32
+    (260, 200, 999, 260, 200, 0, 3, 12),         # exponent spread 2^-12 .. 2^12
+    (128, 128, 32, 128, 128, 0, 16, 0),          # more splits than k-tiles
+    (4, 4, 1, 4, 4, 0, 1, 0),
+])
+def test_x3_accuracy(M, N, K, lda, ldb, m0, splitk, spread):
+    A, B = _case(M, N, K, lda, ldb, spread, seed=M + N + K)
+    Ad, Bd = A.to(DEV), B.to(DEV)
+    ref = A[:, m0:m0 + M].double().T @ B[:, :N].double()
+    scale = A[:, m0:m0 + M].double().abs().T @ B[:, :N].double().abs()
+    C0 = torch.randn(M, N, generator=torch.Generator().manual_seed(1)).float()
+    C = C0.to(DEV)
+    cs0 = torch.randn(N, generator=torch.Generator().manual_seed(2)).float()
+    cs = cs0.to(DEV)
+    ops.gemm_x3_tn(Ad[:, m0:], Bd, C, M, N, K, lda, ldb, N, splitk=splitk, colsum=cs)
+    torch.cuda.synchronize()
+    e_x3 = _err(C.cpu() - C0, ref, scale + C0.double().abs())
+    # the fp32 MFMA chain (split-K atomics) on the same operands
+    C32 = C0.to(DEV)
+    ops.gemm([Ad[:, m0:]], [Bd], [C32], M, N, K, lda, ldb, N, transA=True, epi=ops.EPI_ATOMIC,
+             splitk=max(1, min(K // 256, 4)))
+    torch.cuda.synchronize()
+    e_32 = _err(C32.cpu() - C0, ref, scale + C0.double().abs())
+    assert e_x3 <= 1e-6, (e_x3, e_32)
+    assert e_x3 <= 2 * e_32 + 1e-7, (e_x3, e_32)
+    cref = B[:, :N].double().sum(0)
+    cscale = B[:, :N].double().abs().sum(0)
+    assert _err(cs.cpu() - cs0, cref, cscale + cs0.double().abs()) <= 1e-6
+
+
+def test_x3_zero_extents_and_checks():
+    A = torch.zeros(8, 8, device=DEV)
+    C = torch.ones(8, 8, device=DEV)
+    ops.gemm_x3_tn(A, A, C, 8, 8, 0, 8, 8, 8)     # K = 0: no launch, C unchanged
+    torch.cuda.synchronize()
+    assert bool((C == 1).all())
+    with pytest.raises(RuntimeError):
+        ops.gemm_x3_tn(A, A, C, 6, 8, 8, 8, 8, 8)  # M not a multiple of 4
+    with pytest.raises(RuntimeError):
+        ops.gemm_x3_tn(A[:, 1:], A, C, 4, 8, 8, 8, 8, 8)  # A not 16-byte aligned
+
+
+def test_x3_fp32_step_gradients_match_chain():
+    """The whole fp32 train step's gradients with the x3 x-part gradient and
+    with the fp32 chain agree to fp32 level (every gradient; only the LSTM
+    kernel's x rows and bias take a different path)."""
+    from mog_air.air_model import AIRModel
+    rng = np.random.default_rng(5)
+    x = (rng.uniform(size=(256, 2500)) * (rng.uniform(size=(256, 2500)) < 0.3)).astype(np.float32)
+    grads = []
+    for x3 in (True, False):
+        m = AIRModel(max_steps=3, max_digits=3, canvas_size=50, scale_prior_variance=0.05,
+                     z_pres_prior_log_odds=-0.01, cnn=False, train=True, scope="x3",
+                     device=DEV, precision="fp32", seed=3, noise_seed=4)
+        m.X_GRAD_X3 = x3
+        grads.append({k: torch.as_tensor(np.asarray(v), dtype=torch.float64)
+                      for k, v in m.compute_gradients(x).items()})
+    for k in grads[0]:
+        a, b = grads[0][k], grads[1][k]
+        scale = b.abs().max().item() + 1e-30
+        assert (a - b).abs().max().item() <= 1e-5 * scale, k
