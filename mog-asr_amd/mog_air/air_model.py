@@ -386,7 +386,7 @@ class AIRModel:
                 dst.copy_(src)
             return
         side = None
-        if self.NOISE_ON_SIDE:
+        if self.NOISE_ON_SIDE and ws.B >= self.SIDE_MIN_BATCH:
             # on the side stream, under the x-projection (which needs none of
             # it); _forward joins it after that GEMM
             side = self._side_stream()
@@ -721,10 +721,12 @@ class AIRModel:
         # dh[t] = sum_z dhid_z W1_z^T for every step: one plain GEMM over
         # K = 5 HS ([dhid_0 .. dhid_4] rows against [W1_0 .. W1_4]), the same
         # k-ordered chain as the per-head sum
-        torch.cuda.current_stream().wait_event(w1_done)
-        gemm([ws.dhid], [self._w1cat_buf], [ws.dh], TB, H, 5 * HS, 5 * HS, 5 * HS, H,
+        if w1_done is not None:
+            torch.cuda.current_stream().wait_event(w1_done)
+        gemm([ws.dhid], [self._w1cat()], [ws.dh], TB, H, 5 * HS, 5 * HS, 5 * HS, H,
              transB=True)
-        heads_side = self.grad_reducer is None and self.HEADS_WGRAD_SIDE
+        heads_side = (self.grad_reducer is None and self.HEADS_WGRAD_SIDE
+                      and B >= self.SIDE_MIN_BATCH)
         if heads_side:
             # one GPU, no bucket to hand over: the heads' weight gradients
             # follow the VAE's on the side stream, under the latency-bound
@@ -759,6 +761,11 @@ class AIRModel:
 
     # single GPU: heads' weight gradients on the side stream (see _backward)
     HEADS_WGRAD_SIDE = os.environ.get("MOG_HEADS_SIDE", "1") == "1"
+    # the round-3 side-stream moves (noise + resets under the x-projection,
+    # heads' weight gradients under the LSTM chain) from this batch: below it
+    # the launches are too short to hide the cross-stream waits (batch 64:
+    # eager 0.90 -> 1.00 ms, captured 0.60 -> 0.65 ms with them)
+    SIDE_MIN_BATCH = 1024
 
     def _vae_backward_fp32_all(self, ws, gscale):
         TB = ws.B * self.max_steps
@@ -1070,12 +1077,14 @@ class AIRModel:
         ready = torch.cuda.Event()
         ready.record(main)
         side.wait_event(ready)
+        w1_done = None
         with torch.cuda.stream(side):
-            # the heads' concatenated W1 (B operand of the dh GEMM) first: off
-            # the main stream, which waits for it only at that GEMM
-            self._w1cat()
-            w1_done = torch.cuda.Event()
-            w1_done.record(side)
+            if ws.B >= self.SIDE_MIN_BATCH:
+                # the heads' concatenated W1 (B operand of the dh GEMM) first:
+                # off the main stream, which waits for it only at that GEMM
+                self._w1cat()
+                w1_done = torch.cuda.Event()
+                w1_done.record(side)
             if self.precision == "bf16":
                 self._vae_weight_grads_bf16(ws)
             else:
