@@ -59,8 +59,14 @@ def kernel_work(name, B, precision, C2=2500, H=256, T=3):
     if name == "lstm_x_projection":          # Gx = X Wx, [B,C2] x [C2,4H], fp32 MFMA
         return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", FP32_MFMA_PEAK_TFLOPS
     if name == "lstm_x_projection_grad":     # dWx = X^T dGsum (bf16 MFMA in the bf16 config)
-        peak = BF16_MFMA_PEAK_TFLOPS if precision == "bf16" else FP32_MFMA_PEAK_TFLOPS
-        return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", peak
+        if precision == "bf16":
+            return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", BF16_MFMA_PEAK_TFLOPS
+        from mog_air.air_model import AIRModel
+        if AIRModel.X_GRAD_X3:
+            # fp32 operands split into three bf16 pieces: six bf16 MFMA products
+            # per fp32 product, priced at the bf16 peak
+            return "mfma", 6 * 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", BF16_MFMA_PEAK_TFLOPS
+        return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", FP32_MFMA_PEAK_TFLOPS
     if name == "stn_vae_step":
         return "hbm", B * fused_bytes_per_image_step(C2) / 1e9, "GB/s", HBM_PEAK_GBS
     if name == "stn_vae_step_all":           # all T steps' rows in one launch

@@ -37,6 +37,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 128, BN = 128, BK = 32;
 constexpr int LDR = BM + 8;                 // LDS row (k) pitch in bf16 (BM == BN)
@@ -81,11 +82,20 @@ __device__ __forceinline__ void split4(const float4 v, u32x2& p0, u32x2& p1, u32
 struct X3Args {
   const float* A;
   const float* B;
+  const __bf16* A3;  // PRE: the pieces split beforehand (mog_split3_bf16), piece p
+  const __bf16* B3;  // at A3 + p * sa (B3 + p * sb)
+  long sa, sb;
   float* C;
   float* colsum;
   int M, N, K, lda, ldb, ldc, kchunk, nx, ny;
 };
 
+constexpr int NP = (BM * BK / 8) / 256;  // 16-byte bf16 chunks per thread per piece (2)
+
+__device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+
+template <bool PRE>
 __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[STAGE];
 
@@ -102,6 +112,10 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
   const int sk = t >> 5, sc = (t & 31) * 4;
   const bool do_cs = D.colsum != nullptr && by == 0;
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  // PRE staging roles: 16-byte chunk i covers k-row t/16 + 16 i, columns 8 (t % 16) ..
+  const int pk = t >> 4, pc = (t & 15) * 8;
+  float cs8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  u32x4 pa[3][NP], pb[3][NP];
 
   floatx4 acc[4][4];
 #pragma unroll
@@ -112,6 +126,24 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
   float4 ra[NL], rb[NL];
   const float4 zero4 = {0.f, 0.f, 0.f, 0.f};
   auto load_tiles = [&](int k0) {
+    if constexpr (PRE) {
+      const u32x4 z4 = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int gk = k0 + pk + 16 * i;
+        const int gm = m0 + pc, gn = n0 + pc;
+        // gm < M <= lda, both multiples of 8: the chunk stays inside the row
+        // (columns >= M are pad zeros or a neighbour window's, never stored)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          pa[p][i] = (gk < kend && gm < M)
+              ? *reinterpret_cast<const u32x4*>(D.A3 + p * D.sa + (size_t)gk * D.lda + gm) : z4;
+          pb[p][i] = (gk < kend && gn < N)
+              ? *reinterpret_cast<const u32x4*>(D.B3 + p * D.sb + (size_t)gk * D.ldb + gn) : z4;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int gk = k0 + sk + 8 * i;
@@ -124,6 +156,25 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
   };
   auto store_tiles = [&](int stage) {
     __bf16* S = lds + stage * STAGE;
+    if constexpr (PRE) {
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int o = (pk + 16 * i) * LDR + pc;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          *reinterpret_cast<u32x4*>(S + p * PIECE + o) = pa[p][i];
+          *reinterpret_cast<u32x4*>(S + (3 + p) * PIECE + o) = pb[p][i];
+        }
+        if (do_cs) {  // x = x0 + x1 + x2 exactly
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            cs8[2 * j] += (bf_lo(pb[0][i][j]) + bf_lo(pb[1][i][j])) + bf_lo(pb[2][i][j]);
+            cs8[2 * j + 1] += (bf_hi(pb[0][i][j]) + bf_hi(pb[1][i][j])) + bf_hi(pb[2][i][j]);
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int o = (sk + 8 * i) * LDR + sc;
@@ -195,9 +246,25 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
     }
   }
   if (do_cs) {
+    // the per-thread column partials summed in a fixed order through LDS (free
+    // after the loop's last barrier): one atomic per column and workgroup, so
+    // the bias gradient is deterministic whenever split-K is 1
+    float* red = reinterpret_cast<float*>(lds);  // [16 row groups][BN]
+    constexpr int RG = PRE ? 16 : 8;
+    if (PRE) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-      if (n0 + sc + c < N) atomicAdd(D.colsum + n0 + sc + c, cs[c]);
+      for (int c = 0; c < 8; ++c) red[pk * BN + pc + c] = cs8[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) red[sk * BN + sc + c] = cs[c];
+    }
+    __syncthreads();
+    if (t < BN && n0 + t < N) {
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < RG; ++r) v += red[r * BN + t];
+      atomicAdd(D.colsum + n0 + t, v);
+    }
   }
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
@@ -213,7 +280,69 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+void launch_x3(bool pre, X3Args D, int splitk, hipStream_t s) {
+  int kchunk = (D.K + splitk - 1) / splitk;
+  kchunk = ((kchunk + BK - 1) / BK) * BK;
+  D.kchunk = kchunk;
+  const int nsplit = (D.K + kchunk - 1) / kchunk;
+  D.nx = mog_cdiv(D.N, BN);
+  D.ny = mog_cdiv(D.M, BM);
+  const long nwg = (long)D.nx * D.ny * nsplit;
+  if (pre) gemm_x3_tn_kernel<true><<<dim3((unsigned)nwg), 256, 0, s>>>(D);
+  else gemm_x3_tn_kernel<false><<<dim3((unsigned)nwg), 256, 0, s>>>(D);
+}
+
+// the three exact truncated bf16 pieces of an fp32 [rows][cols] matrix: piece p
+// at dst + p * pstride, element (r, c) at r * ld_dst + c; columns cols..ld_dst-1
+// are written as zeros
+__global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ src, int rows,
+                                                     int cols, int ld_src, __bf16* dst, int ld_dst,
+                                                     long pstride) {
+  const int q4 = ld_dst / 4;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)rows * q4) return;
+  const int r = (int)(i / q4), c = (int)(i % q4) * 4;
+  const float4 v = c < cols ? *reinterpret_cast<const float4*>(src + (size_t)r * ld_src + c)
+                            : float4{0.f, 0.f, 0.f, 0.f};
+  u32x2 p0, p1, p2;
+  split4(v, p0, p1, p2);
+  __bf16* d = dst + (size_t)r * ld_dst + c;
+  *reinterpret_cast<u32x2*>(d) = p0;
+  *reinterpret_cast<u32x2*>(d + pstride) = p1;
+  *reinterpret_cast<u32x2*>(d + 2 * pstride) = p2;
+}
+
 }  // namespace
+
+extern "C" int mog_split3_bf16(const float* src, int rows, int cols, int ld_src, void* dst,
+                               int ld_dst, long piece_stride, void* stream) {
+  MOG_CHECK_ARG(src && dst && rows >= 0 && cols >= 0 && cols % 4 == 0 && ld_src % 4 == 0 &&
+                ld_dst % 4 == 0 && ld_dst >= cols && ld_src >= cols && piece_stride % 4 == 0 &&
+                piece_stride >= (long)rows * ld_dst && al16(src) && al16(dst));
+  const long n = (long)rows * (ld_dst / 4);
+  if (n == 0) return 0;
+  split3_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, mog_stream(stream)>>>(
+      src, rows, cols, ld_src, reinterpret_cast<__bf16*>(dst), ld_dst, piece_stride);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb, float* C,
+                               float* colsum, int M, int N, int K, int lda, int ldb, int ldc,
+                               int splitk, void* stream) {
+  MOG_CHECK_ARG(A3 && B3 && C && M >= 0 && N >= 0 && K >= 0 && splitk >= 1);
+  // 16-byte chunks of 8 bf16: strides and piece strides multiples of 8 (a chunk
+  // that starts below M ends inside the row; its columns >= M are not stored)
+  MOG_CHECK_ARG(al16(A3) && al16(B3) && lda % 8 == 0 && ldb % 8 == 0 && sa % 8 == 0 &&
+                sb % 8 == 0 && lda >= M && ldb >= N && ldc >= N);
+  if (M == 0 || N == 0 || K == 0) return 0;
+  X3Args D{};
+  D.A3 = reinterpret_cast<const __bf16*>(A3);
+  D.B3 = reinterpret_cast<const __bf16*>(B3);
+  D.sa = sa; D.sb = sb; D.C = C; D.colsum = colsum;
+  D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc;
+  launch_x3(true, D, splitk, mog_stream(stream));
+  MOG_LAUNCH_RET();
+}
 
 extern "C" int mog_gemm_f32_x3_tn(const float* A, const float* B, float* C, float* colsum,
                                   int M, int N, int K, int lda, int ldb, int ldc, int splitk,
@@ -223,16 +352,9 @@ extern "C" int mog_gemm_f32_x3_tn(const float* A, const float* B, float* C, floa
   MOG_CHECK_ARG(al16(A) && al16(B) && M % 4 == 0 && N % 4 == 0 && lda % 4 == 0 &&
                 ldb % 4 == 0 && lda >= M && ldb >= N && ldc >= N);
   if (M == 0 || N == 0 || K == 0) return 0;
-  X3Args D;
+  X3Args D{};
   D.A = A; D.B = B; D.C = C; D.colsum = colsum;
   D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc;
-  int kchunk = (K + splitk - 1) / splitk;
-  kchunk = ((kchunk + BK - 1) / BK) * BK;
-  D.kchunk = kchunk;
-  const int nsplit = (K + kchunk - 1) / kchunk;
-  D.nx = mog_cdiv(N, BN);
-  D.ny = mog_cdiv(M, BM);
-  const long nwg = (long)D.nx * D.ny * nsplit;
-  gemm_x3_tn_kernel<<<dim3((unsigned)nwg), 256, 0, mog_stream(stream)>>>(D);
+  launch_x3(false, D, splitk, mog_stream(stream));
   MOG_LAUNCH_RET();
 }

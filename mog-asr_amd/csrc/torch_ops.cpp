@@ -840,7 +840,34 @@ void gemm_f32_x3_tn_(const Tensor& A, const Tensor& B, Tensor C, const optional<
   check(mog_gemm_f32_x3_tn(a, b, c, cs, M, N, K, lda, ldb, ldc, splitk, o.stream()), o.name);
 }
 
+void split3_bf16_(const Tensor& src, Tensor dst, int64_t rows, int64_t cols, int64_t ld_src,
+                  int64_t ld_dst, int64_t piece_stride) {
+  Op o("split3_bf16_");
+  const float* a = o.f(src, mat(rows, cols, ld_src), "src");
+  void* d = o.need(dst, BF16, 2 * piece_stride + mat(rows, ld_dst, ld_dst), "dst");
+  GUARD(o);
+  check(mog_split3_bf16(a, rows, cols, ld_src, d, ld_dst, piece_stride, o.stream()), o.name);
+}
+
+void gemm_x3p_tn_(const Tensor& A3, int64_t sa, const Tensor& B3, int64_t sb, Tensor C,
+                  const optional<Tensor>& colsum, int64_t M, int64_t N, int64_t K, int64_t lda,
+                  int64_t ldb, int64_t ldc, int64_t splitk) {
+  Op o("gemm_x3p_tn_");
+  float* c = o.f(C, mat(M, N, ldc), "C");
+  const void* a = o.need(A3, BF16, 2 * sa + mat(K, M, lda), "A3");
+  const void* b = o.need(B3, BF16, 2 * sb + mat(K, N, ldb), "B3");
+  float* cs = o.f(colsum, N, "colsum");
+  GUARD(o);
+  check(mog_gemm_x3p_tn(a, sa, b, sb, c, cs, M, N, K, lda, ldb, ldc, splitk, o.stream()), o.name);
+}
+
 TORCH_LIBRARY_FRAGMENT(mog_air, m) {
+  m.def(
+      "split3_bf16_(Tensor src, Tensor(a!) dst, int rows, int cols, int ld_src, int ld_dst, "
+      "int piece_stride) -> ()");
+  m.def(
+      "gemm_x3p_tn_(Tensor A3, int sa, Tensor B3, int sb, Tensor(a!) C, Tensor(b!)? colsum, "
+      "int M, int N, int K, int lda, int ldb, int ldc, int splitk) -> ()");
   m.def(
       "gemm_f32_x3_tn_(Tensor A, Tensor B, Tensor(a!) C, Tensor(b!)? colsum, int M, int N, "
       "int K, int lda, int ldb, int ldc, int splitk) -> ()");
@@ -976,6 +1003,8 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("gemm_f32_kseg_", &gemm_f32_kseg_);
   m.impl("gemm_f32_sigmoid_philox_", &gemm_f32_sigmoid_philox_);
   m.impl("gemm_f32_x3_tn_", &gemm_f32_x3_tn_);
+  m.impl("split3_bf16_", &split3_bf16_);
+  m.impl("gemm_x3p_tn_", &gemm_x3p_tn_);
   m.impl("gemm_bf16_", &gemm_bf16_);
   m.impl("cvt_bf16_batch_", &cvt_bf16_batch_);
   m.impl("stn_forward_", &stn_forward_);

@@ -434,6 +434,12 @@ class AIRModel:
             ws.digits.zero_()
             ws.live.zero_()
             ws.live[:1].fill_(1)  # (a fill kernel: capturable, unlike a host copy)
+            if need_grad and self.precision == "fp32" and self.X_GRAD_X3 == 2:
+                # the x-part gradient's A operand, split once per step
+                C2p = self._pad8(C2)
+                if getattr(ws, "X3", None) is None:
+                    ws.X3 = torch.empty((3, B, C2p), device=self.device, dtype=torch.bfloat16)
+                ops.split3_bf16(X, ws.X3, B, C2, C2, C2p, B * C2p)
             if side is not None:
                 pre_done = torch.cuda.Event()
                 pre_done.record(side)
@@ -1118,11 +1124,13 @@ class AIRModel:
                      [self._G(h + "/output/weights") for _, h in sel], TB, HS, k, HS, 2,
                      [self._G(h + "/output/biases") for _, h in sel])
 
-    # fp32 configuration, opt-in (MOG_X_GRAD_X3=1): the x-part of the LSTM
-    # kernel gradient on the bf16 matrix cores with exact three-piece operand
-    # splits (gemm_x3.hip: 318 vs 410 us stand-alone, no change inside the
-    # step); default: the fp32 MFMA split-K GEMM
-    X_GRAD_X3 = os.environ.get("MOG_X_GRAD_X3", "0") == "1"
+    # fp32 configuration: the x-part of the LSTM kernel gradient on the bf16
+    # matrix cores with exact three-piece operand splits (gemm_x3.hip,
+    # DESIGN.md §4.4).  2 (default): the operands split once per step, X on
+    # the side stream under the x-projection, dG before the GEMM (gemm_x3p_tn:
+    # 244 vs 428 us stand-alone, step 3.44 -> 3.37 ms); 1: split inside the
+    # GEMM (318 us, no change in the step); 0: the fp32 MFMA split-K GEMM.
+    X_GRAD_X3 = int(os.environ.get("MOG_X_GRAD_X3", "2"))
     X3_SPLITK = int(os.environ.get("MOG_X3_SPLITK", "8"))
 
     # rows of the x-part of the LSTM kernel gradient per all-reduce bucket
@@ -1152,11 +1160,21 @@ class AIRModel:
                     # bf16 configuration: X^T dGsum on bf16 operands (fp32
                     # accumulate); the forward x-projection stays fp32
                     self._x_grad_bf16(X, ws, gK, bias, m0, m1)
+                elif self.X_GRAD_X3 == 2:
+                    if m0 == 0:
+                        if getattr(ws, "dG3", None) is None:
+                            ws.dG3 = torch.empty((3, B, 4 * H), device=self.device,
+                                                 dtype=torch.bfloat16)
+                        ops.split3_bf16(ws.dGsum, ws.dG3, B, 4 * H, 4 * H, 4 * H, B * 4 * H)
+                    C2p = self._pad8(C2)
+                    ops.gemm_x3p_tn(ws.X3.view(-1)[m0:], B * C2p, ws.dG3, B * 4 * H, gK[m0:m1],
+                                    m1 - m0, 4 * H, B, C2p, 4 * H, 4 * H, splitk=max(1, min(B // 256, self.X3_SPLITK)),
+                                    colsum=bias)
                 elif self.X_GRAD_X3:
                     # fp32 operands split exactly into three bf16 pieces on the
                     # bf16 matrix cores (gemm_x3.hip: fp32-level accuracy)
                     ops.gemm_x3_tn(X[:, m0:], ws.dGsum, gK[m0:m1], m1 - m0, 4 * H, B, C2, 4 * H,
-                                   4 * H, splitk=self.X3_SPLITK, colsum=bias)
+                                   4 * H, splitk=max(1, min(B // 256, self.X3_SPLITK)), colsum=bias)
                 else:
                     self._dw(X[:, m0:], ws.dGsum, gK[m0:m1], B, m1 - m0, 4 * H, C2, 4 * H, bias)
                 if m1 < C2:

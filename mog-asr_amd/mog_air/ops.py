@@ -64,6 +64,20 @@ def gemm_x3_tn(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int
     _ops.gemm_f32_x3_tn_(A, B, C, colsum, M, N, K, lda, ldb, ldc, int(splitk))
 
 
+def split3_bf16(src: torch.Tensor, dst: torch.Tensor, rows: int, cols: int, ld_src: int,
+                ld_dst: int, piece_stride: int) -> None:
+    """The three exact truncated bf16 pieces of an fp32 matrix
+    (mog_split3_bf16)."""
+    _ops.split3_bf16_(src, dst, rows, cols, ld_src, ld_dst, int(piece_stride))
+
+
+def gemm_x3p_tn(A3: torch.Tensor, sa: int, B3: torch.Tensor, sb: int, C: torch.Tensor, M: int,
+                N: int, K: int, lda: int, ldb: int, ldc: int, splitk: int = 8,
+                colsum=None) -> None:
+    """gemm_x3_tn from operands split beforehand by split3_bf16 (mog_gemm_x3p_tn)."""
+    _ops.gemm_x3p_tn_(A3, int(sa), B3, int(sb), C, colsum, M, N, K, lda, ldb, ldc, int(splitk))
+
+
 def gemm_sigmoid_philox(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias, M: int, N: int,
                         K: int, lda: int, ldb: int, ldc: int, scale: float, seed: int,
                         offset: int) -> None:

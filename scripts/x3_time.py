@@ -34,6 +34,16 @@ for sk in (4, 8, 16):
     us = t(lambda: ops.gemm_x3_tn(X, G, C, M, N, K, M, N, N, splitk=sk, colsum=cs))
     print(f"x3 stages={os.environ.get('MOG_X3_STAGES', '1')} splitk={sk}: {us:.1f} us "
           f"({fl / us / 1e6:.0f} TF/s fp32-equivalent)")
+X3 = torch.empty(3, K, 2504, device=dev, dtype=torch.bfloat16)
+G3 = torch.empty(3, K, N, device=dev, dtype=torch.bfloat16)
+us = t(lambda: ops.split3_bf16(X, X3, K, M, M, 2504, K * 2504))
+print(f"split X: {us:.1f} us")
+us = t(lambda: ops.split3_bf16(G, G3, K, N, N, N, K * N))
+print(f"split dG: {us:.1f} us")
+for sk in (4, 8, 16):
+    us = t(lambda: ops.gemm_x3p_tn(X3, K * 2504, G3, K * N, C, M, N, K, 2504, N, N, splitk=sk,
+                                   colsum=cs))
+    print(f"x3 pre-split splitk={sk}: {us:.1f} us ({fl / us / 1e6:.0f} TF/s fp32-equivalent)")
 us = t(lambda: ops.gemm([X], [G], [C], M, N, K, M, N, N, transA=True, epi=ops.EPI_ATOMIC,
                         splitk=4, colsum=[cs]))
 print(f"fp32 chain splitk=4: {us:.1f} us ({fl / us / 1e6:.0f} TF/s)")

@@ -52,6 +52,26 @@ def test_x3_accuracy(M, N, K, lda, ldb, m0, splitk, spread):
     ops.gemm_x3_tn(Ad[:, m0:], Bd, C, M, N, K, lda, ldb, N, splitk=splitk, colsum=cs)
     torch.cuda.synchronize()
     e_x3 = _err(C.cpu() - C0, ref, scale + C0.double().abs())
+    # the pre-split form: pieces in HBM (row pitch padded to 8), same product
+    p8 = lambda n: (n + 7) // 8 * 8  # noqa: E731
+    A3 = torch.empty(3, K, p8(lda), device=DEV, dtype=torch.bfloat16)
+    B3 = torch.empty(3, K, p8(ldb), device=DEV, dtype=torch.bfloat16)
+    ops.split3_bf16(Ad, A3, K, lda, lda, p8(lda), K * p8(lda))
+    ops.split3_bf16(Bd, B3, K, ldb, ldb, p8(ldb), K * p8(ldb))
+    # the split is exact: the pieces sum back to the operand
+    assert torch.equal(((A3[0].float() + A3[1].float()) + A3[2].float())[:, :lda].cpu(), A)
+    assert bool((A3[:, :, lda:] == 0).all())
+    Cp = C0.to(DEV)
+    csp = cs0.to(DEV)
+    if m0 % 8 == 0:
+        ops.gemm_x3p_tn(A3.view(-1)[m0:], K * p8(lda), B3, K * p8(ldb), Cp, M, N, K, p8(lda),
+                        p8(ldb), N, splitk=splitk, colsum=csp)
+        torch.cuda.synchronize()
+        e_p = _err(Cp.cpu() - C0, ref, scale + C0.double().abs())
+        assert e_p <= 1e-6, e_p
+        cref_p = B[:, :N].double().sum(0)
+        assert _err(csp.cpu() - cs0, cref_p, B[:, :N].double().abs().sum(0) + cs0.double().abs()) \
+            <= 1e-6
     # the fp32 MFMA chain (split-K atomics) on the same operands
     C32 = C0.to(DEV)
     ops.gemm([Ad[:, m0:]], [Bd], [C32], M, N, K, lda, ldb, N, transA=True, epi=ops.EPI_ATOMIC,
@@ -78,21 +98,22 @@ def test_x3_zero_extents_and_checks():
 
 
 def test_x3_fp32_step_gradients_match_chain():
-    """The whole fp32 train step's gradients with the x3 x-part gradient and
-    with the fp32 chain agree to fp32 level (every gradient; only the LSTM
+    """The whole fp32 train step's gradients with the x3 x-part gradient (in-
+    kernel split and pre-split) and with the fp32 chain agree to fp32 level (every gradient; only the LSTM
     kernel's x rows and bias take a different path)."""
     from mog_air.air_model import AIRModel
     rng = np.random.default_rng(5)
     x = (rng.uniform(size=(256, 2500)) * (rng.uniform(size=(256, 2500)) < 0.3)).astype(np.float32)
     grads = []
-    for x3 in (True, False):
+    for x3 in (1, 2, 0):
         m = AIRModel(max_steps=3, max_digits=3, canvas_size=50, scale_prior_variance=0.05,
                      z_pres_prior_log_odds=-0.01, cnn=False, train=True, scope="x3",
                      device=DEV, precision="fp32", seed=3, noise_seed=4)
         m.X_GRAD_X3 = x3
         grads.append({k: torch.as_tensor(np.asarray(v), dtype=torch.float64)
                       for k, v in m.compute_gradients(x).items()})
-    for k in grads[0]:
-        a, b = grads[0][k], grads[1][k]
-        scale = b.abs().max().item() + 1e-30
-        assert (a - b).abs().max().item() <= 1e-5 * scale, k
+    for g in grads[:2]:
+        for k in g:
+            a, b = g[k], grads[2][k]
+            scale = b.abs().max().item() + 1e-30
+            assert (a - b).abs().max().item() <= 1e-5 * scale, k
