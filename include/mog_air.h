@@ -55,11 +55,14 @@ int mog_gemm_f32_x3_tn(const float* A, const float* B, float* C, float* colsum, 
  * three exact bf16 pieces of an fp32 [rows][cols] matrix (piece p at dst + p *
  * piece_stride elements, row pitch ld_dst, columns cols..ld_dst-1 zero);
  * mog_gemm_x3p_tn reads piece p of A at A3 + p * sa and of B at B3 + p * sb
- * (bf16 elements; lda, ldb, sa, sb multiples of 8, 16-byte aligned). */
+ * (bf16 elements; lda, ldb, sa, sb multiples of 8, 16-byte aligned).
+ * npieces = 1: A3 / B3 are plain bf16 operands and the one product is taken
+ * (the bf16 configuration's weight gradient of the LSTM kernel's x rows). */
 int mog_split3_bf16(const float* src, int rows, int cols, int ld_src, void* dst, int ld_dst,
                     long piece_stride, void* stream);
 int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb, float* C, float* colsum,
-                    int M, int N, int K, int lda, int ldb, int ldc, int splitk, void* stream);
+                    int M, int N, int K, int lda, int ldb, int ldc, int splitk, int npieces,
+                    void* stream);
 
 /* C = sigmoid((A B + bias) + scale * eps) for A [M][K] (lda), B [K][N] (ldb):
  * the VAE output layer (vae.py:44-46) with the likelihood noise eps generated

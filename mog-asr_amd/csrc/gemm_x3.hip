@@ -95,7 +95,8 @@ constexpr int NP = (BM * BK / 8) / 256;  // 16-byte bf16 chunks per thread per p
 __device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
 
-template <bool PRE>
+// NPC: pieces per operand (3; 1 = plain bf16 operands, one product)
+template <bool PRE, int NPC = 3>
 __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[STAGE];
 
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
         // gm < M <= lda, both multiples of 8: the chunk stays inside the row
         // (columns >= M are pad zeros or a neighbour window's, never stored)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
+        for (int p = 0; p < NPC; ++p) {
           pa[p][i] = (gk < kend && gm < M)
               ? *reinterpret_cast<const u32x4*>(D.A3 + p * D.sa + (size_t)gk * D.lda + gm) : z4;
           pb[p][i] = (gk < kend && gn < N)
@@ -161,11 +162,17 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
       for (int i = 0; i < NP; ++i) {
         const int o = (pk + 16 * i) * LDR + pc;
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
+        for (int p = 0; p < NPC; ++p) {
           *reinterpret_cast<u32x4*>(S + p * PIECE + o) = pa[p][i];
           *reinterpret_cast<u32x4*>(S + (3 + p) * PIECE + o) = pb[p][i];
         }
-        if (do_cs) {  // x = x0 + x1 + x2 exactly
+        if (do_cs && NPC == 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            cs8[2 * j] += bf_lo(pb[0][i][j]);
+            cs8[2 * j + 1] += bf_hi(pb[0][i][j]);
+          }
+        } else if (do_cs) {  // x = x0 + x1 + x2 exactly
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             cs8[2 * j] += (bf_lo(pb[0][i][j]) + bf_lo(pb[1][i][j])) + bf_lo(pb[2][i][j]);
@@ -206,9 +213,9 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
   };
   auto compute = [&](int stage) {
     const __bf16* S = lds + stage * STAGE;
-    bf16x8 a[3][4], b[3][4];
+    bf16x8 a[NPC][4], b[NPC][4];
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < NPC; ++p)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         a[p][i] = frag(S + p * PIECE, wm + 16 * i);
@@ -223,11 +230,13 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
           acc[mi][ni] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[mi], y[ni], acc[mi][ni], 0, 0, 0);
     };
-    pass(a[2], b[0]);
-    pass(a[1], b[1]);
-    pass(a[0], b[2]);
-    pass(a[1], b[0]);
-    pass(a[0], b[1]);
+    if constexpr (NPC == 3) {
+      pass(a[2], b[0]);
+      pass(a[1], b[1]);
+      pass(a[0], b[2]);
+      pass(a[1], b[0]);
+      pass(a[0], b[1]);
+    }
     pass(a[0], b[0]);
   };
 
@@ -280,7 +289,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-void launch_x3(bool pre, X3Args D, int splitk, hipStream_t s) {
+void launch_x3(bool pre, X3Args D, int splitk, hipStream_t s, int npieces = 3) {
   int kchunk = (D.K + splitk - 1) / splitk;
   kchunk = ((kchunk + BK - 1) / BK) * BK;
   D.kchunk = kchunk;
@@ -288,7 +297,8 @@ void launch_x3(bool pre, X3Args D, int splitk, hipStream_t s) {
   D.nx = mog_cdiv(D.N, BN);
   D.ny = mog_cdiv(D.M, BM);
   const long nwg = (long)D.nx * D.ny * nsplit;
-  if (pre) gemm_x3_tn_kernel<true><<<dim3((unsigned)nwg), 256, 0, s>>>(D);
+  if (pre && npieces == 1) gemm_x3_tn_kernel<true, 1><<<dim3((unsigned)nwg), 256, 0, s>>>(D);
+  else if (pre) gemm_x3_tn_kernel<true><<<dim3((unsigned)nwg), 256, 0, s>>>(D);
   else gemm_x3_tn_kernel<false><<<dim3((unsigned)nwg), 256, 0, s>>>(D);
 }
 
@@ -328,8 +338,9 @@ extern "C" int mog_split3_bf16(const float* src, int rows, int cols, int ld_src,
 
 extern "C" int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb, float* C,
                                float* colsum, int M, int N, int K, int lda, int ldb, int ldc,
-                               int splitk, void* stream) {
+                               int splitk, int npieces, void* stream) {
   MOG_CHECK_ARG(A3 && B3 && C && M >= 0 && N >= 0 && K >= 0 && splitk >= 1);
+  MOG_CHECK_ARG(npieces == 3 || npieces == 1);
   // 16-byte chunks of 8 bf16: strides and piece strides multiples of 8 (a chunk
   // that starts below M ends inside the row; its columns >= M are not stored)
   MOG_CHECK_ARG(al16(A3) && al16(B3) && lda % 8 == 0 && ldb % 8 == 0 && sa % 8 == 0 &&
@@ -340,7 +351,7 @@ extern "C" int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb,
   D.B3 = reinterpret_cast<const __bf16*>(B3);
   D.sa = sa; D.sb = sb; D.C = C; D.colsum = colsum;
   D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc;
-  launch_x3(true, D, splitk, mog_stream(stream));
+  launch_x3(true, D, splitk, mog_stream(stream), npieces);
   MOG_LAUNCH_RET();
 }
 

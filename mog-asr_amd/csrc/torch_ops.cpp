@@ -851,14 +851,17 @@ void split3_bf16_(const Tensor& src, Tensor dst, int64_t rows, int64_t cols, int
 
 void gemm_x3p_tn_(const Tensor& A3, int64_t sa, const Tensor& B3, int64_t sb, Tensor C,
                   const optional<Tensor>& colsum, int64_t M, int64_t N, int64_t K, int64_t lda,
-                  int64_t ldb, int64_t ldc, int64_t splitk) {
+                  int64_t ldb, int64_t ldc, int64_t splitk, int64_t npieces) {
   Op o("gemm_x3p_tn_");
   float* c = o.f(C, mat(M, N, ldc), "C");
-  const void* a = o.need(A3, BF16, 2 * sa + mat(K, M, lda), "A3");
-  const void* b = o.need(B3, BF16, 2 * sb + mat(K, N, ldb), "B3");
+  const int64_t np1 = npieces - 1;
+  const void* a = o.need(A3, BF16, np1 * sa + mat(K, M, lda), "A3");
+  const void* b = o.need(B3, BF16, np1 * sb + mat(K, N, ldb), "B3");
   float* cs = o.f(colsum, N, "colsum");
   GUARD(o);
-  check(mog_gemm_x3p_tn(a, sa, b, sb, c, cs, M, N, K, lda, ldb, ldc, splitk, o.stream()), o.name);
+  check(mog_gemm_x3p_tn(a, sa, b, sb, c, cs, M, N, K, lda, ldb, ldc, splitk, npieces,
+                        o.stream()),
+        o.name);
 }
 
 TORCH_LIBRARY_FRAGMENT(mog_air, m) {
@@ -867,7 +870,7 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "int piece_stride) -> ()");
   m.def(
       "gemm_x3p_tn_(Tensor A3, int sa, Tensor B3, int sb, Tensor(a!) C, Tensor(b!)? colsum, "
-      "int M, int N, int K, int lda, int ldb, int ldc, int splitk) -> ()");
+      "int M, int N, int K, int lda, int ldb, int ldc, int splitk, int npieces=3) -> ()");
   m.def(
       "gemm_f32_x3_tn_(Tensor A, Tensor B, Tensor(a!) C, Tensor(b!)? colsum, int M, int N, "
       "int K, int lda, int ldb, int ldc, int splitk) -> ()");

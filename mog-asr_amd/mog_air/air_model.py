@@ -1191,8 +1191,20 @@ class AIRModel:
                 ws.dGsumb = torch.empty((B, 4 * H), **bf)
             _ops.cvt_bf16_batch_([X, ws.dGsum], [ws.Xb, ws.dGsumb],
                                  [B, C2, C2, B, C2p, C2p, 0, B, 4 * H, 4 * H, B, 4 * H, 4 * H, 0])
-        self._dw_bf16(ws.Xb[:, m0:], ws.dGsumb, gK[m0:m1], B, m1 - m0, 4 * H, C2p, 4 * H,
-                      bias_out)
+        if self.X_GRAD_BF16_X1:
+            # the x3p kernel with one piece (plain bf16 operands, one MFMA
+            # product per k-block): 128 x 128 tiles, two workgroups per CU
+            ops.gemm_x3p_tn(ws.Xb.view(-1)[m0:], 0, ws.dGsumb, 0, gK[m0:m1], m1 - m0, 4 * H, B,
+                            C2p, 4 * H, 4 * H, splitk=max(1, min(B // 256, self.X3_SPLITK)),
+                            colsum=bias_out, npieces=1)
+        else:
+            self._dw_bf16(ws.Xb[:, m0:], ws.dGsumb, gK[m0:m1], B, m1 - m0, 4 * H, C2p, 4 * H,
+                          bias_out)
+
+    # bf16 configuration, opt-in (MOG_X_GRAD_BF16_X1=1): the x-rows gradient on
+    # gemm_x3p_tn's one-piece form instead of gemm_bf16.hip's TN GEMM (bf16
+    # step 2.19 ms either way, two A/B pairs: not on the critical path there)
+    X_GRAD_BF16_X1 = os.environ.get("MOG_X_GRAD_BF16_X1", "0") == "1"
 
     # ------------------------------------------------------------- API ----
     def _prep(self, images, targets):

@@ -73,9 +73,11 @@ def split3_bf16(src: torch.Tensor, dst: torch.Tensor, rows: int, cols: int, ld_s
 
 def gemm_x3p_tn(A3: torch.Tensor, sa: int, B3: torch.Tensor, sb: int, C: torch.Tensor, M: int,
                 N: int, K: int, lda: int, ldb: int, ldc: int, splitk: int = 8,
-                colsum=None) -> None:
-    """gemm_x3_tn from operands split beforehand by split3_bf16 (mog_gemm_x3p_tn)."""
-    _ops.gemm_x3p_tn_(A3, int(sa), B3, int(sb), C, colsum, M, N, K, lda, ldb, ldc, int(splitk))
+                colsum=None, npieces: int = 3) -> None:
+    """gemm_x3_tn from operands split beforehand by split3_bf16
+    (mog_gemm_x3p_tn); npieces=1: plain bf16 operands, one product."""
+    _ops.gemm_x3p_tn_(A3, int(sa), B3, int(sb), C, colsum, M, N, K, lda, ldb, ldc, int(splitk),
+                      int(npieces))
 
 
 def gemm_sigmoid_philox(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias, M: int, N: int,

@@ -117,3 +117,24 @@ def test_x3_fp32_step_gradients_match_chain():
             a, b = g[k], grads[2][k]
             scale = b.abs().max().item() + 1e-30
             assert (a - b).abs().max().item() <= 1e-5 * scale, k
+
+
+@pytest.mark.parametrize("M,N,K,m0,splitk", [(2500, 1024, 4096, 0, 8), (580, 1024, 777, 1920, 1),
+                                             (132, 40, 300, 0, 2)])
+def test_x1_plain_bf16_operands(M, N, K, m0, splitk):
+    """npieces = 1 (the bf16 configuration's x-rows gradient): plain bf16
+    operands, one product; exact bf16 products accumulated in fp32, so within
+    1e-6 of |A|^T |B| of the float64 product of the same bf16 values, and the
+    column sums of the bf16 B likewise."""
+    lda = (m0 + M + 7) // 8 * 8
+    g = torch.Generator().manual_seed(K)
+    A = torch.randn(K, lda, generator=g).bfloat16()
+    B = torch.randn(K, N, generator=g).bfloat16()
+    C = torch.zeros(M, N, device=DEV)
+    cs = torch.zeros(N, device=DEV)
+    ops.gemm_x3p_tn(A.to(DEV).view(-1)[m0:], 0, B.to(DEV), 0, C, M, N, K, lda, N, N,
+                    splitk=splitk, colsum=cs, npieces=1)
+    torch.cuda.synchronize()
+    Ad, Bd = A[:, m0:m0 + M].double(), B.double()
+    assert _err(C.cpu(), Ad.T @ Bd, Ad.abs().T @ Bd.abs()) <= 1e-6
+    assert _err(cs.cpu(), Bd.sum(0), Bd.abs().sum(0)) <= 1e-6
