@@ -761,12 +761,14 @@ class AIRModel:
             if t > 0:
                 gemm([ws.dG[t]], [Wh], [ws.dh[t - 1]], B, H, 4 * H, 4 * H, 4 * H, H,
                      transB=True, Cin=[ws.dh[t - 1]])
-        self._weight_grads_lstm(X, ws)
-        if heads_side:
-            torch.cuda.current_stream().wait_event(vae_done)
+        self._weight_grads_lstm(X, ws, side=heads_side)
+        if heads_side:  # (everything on the side stream: VAE, heads, dW_rec)
+            torch.cuda.current_stream().wait_stream(self._side_stream())
 
     # single GPU: heads' weight gradients on the side stream (see _backward)
     HEADS_WGRAD_SIDE = os.environ.get("MOG_HEADS_SIDE", "1") == "1"
+    # ... and the LSTM kernel's recurrent-rows gradient beside the x-rows one
+    REC_WGRAD_SIDE = os.environ.get("MOG_REC_SIDE", "1") == "1"
     # the round-3 side-stream moves (noise + resets under the x-projection,
     # heads' weight gradients under the LSTM chain) from this batch: below it
     # the launches are too short to hide the cross-stream waits (batch 64:
@@ -1137,7 +1139,7 @@ class AIRModel:
     # (multiple of the 64-row GEMM tile; data parallel only)
     X_GRAD_CHUNK = 640
 
-    def _weight_grads_lstm(self, X, ws):
+    def _weight_grads_lstm(self, X, ws, side=False):
         """LSTM kernel / bias gradients.  Data parallel: the x-part X^T dGsum
         (2500 x 1024, 10 MB) is produced in row chunks, each handed to the
         all-reduce as soon as it is final, so the collective of chunk i runs
@@ -1145,7 +1147,16 @@ class AIRModel:
         B, T, H, C2 = ws.B, self.max_steps, self.rnn_units, self.C2
         gK = self._G("rnn/basic_lstm_cell/kernel")
         gbK = self._G("rnn/basic_lstm_cell/bias")
-        if T > 1:
+        if T > 1 and side and self.REC_WGRAD_SIDE:
+            # one GPU: the recurrent rows' gradient on the side stream, beside
+            # the x-rows gradient below (both need only the finished chain)
+            main, st = torch.cuda.current_stream(), self._side_stream()
+            ev = torch.cuda.Event()
+            ev.record(main)
+            st.wait_event(ev)
+            with torch.cuda.stream(st):
+                self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
+        elif T > 1:
             self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
         chunk = self.X_GRAD_CHUNK if self.grad_reducer is not None else C2
         base = self.params.offsets[self._SCOPE_PREFIX + "rnn/basic_lstm_cell/kernel"]
