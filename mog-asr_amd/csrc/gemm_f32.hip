@@ -809,9 +809,11 @@ void launch_dma_epi(int epi, dim3 g, hipStream_t s, const GemmPtrs& P, const Gem
 #undef MOG_GEMM_LAUNCH
 }
 
+// Returns MOG_ERR_INVALID (nothing launched) for a transposed A with BM < 64:
+// a transposed A is a row-contiguous LDS image, which needs >= 64 rows.
 template <int BM, int BN, int BK, int NS>
-void launch_dma(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, GemmDims D,
-                int batch) {
+int launch_dma(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, GemmDims D,
+               int batch) {
   int kchunk = (D.K + D.splitk - 1) / D.splitk;
   kchunk = ((kchunk + BK - 1) / BK) * BK;
   if (kchunk == 0) kchunk = BK;
@@ -828,7 +830,10 @@ void launch_dma(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, Gem
   } else if constexpr (BM >= 64) {  // (a transposed A is a row-contiguous image: >= 64 rows)
     if (!tb) launch_dma_epi<BM, BN, BK, NS, true, false>(epi, g, s, P, D);
     else launch_dma_epi<BM, BN, BK, NS, true, true>(epi, g, s, P, D);
+  } else {
+    return MOG_ERR_INVALID;
   }
+  return 0;
 }
 
 // Tile shape (measured on MI355X, scripts/bench_gemm_f32.py):
@@ -842,8 +847,8 @@ void launch_dma(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, Gem
 // shapes), 128x64 / 64x128 tiles, a 3-stage register pipeline with fragment
 // prefetch (1 wave per SIMD at 128x128).  MOG_GEMM_TILE ("64" / "128")
 // forces a tile, MOG_GEMM_DMA=0 the register-staged kernel.
-void launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, const GemmDims& D,
-                 int batch) {
+int launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, const GemmDims& D,
+                int batch) {
   static const char* force = getenv("MOG_GEMM_TILE");
   const long big = (long)mog_cdiv(D.M, 128) * mog_cdiv(D.N, 128) * batch * D.splitk;
   bool b128 = !ta && D.K >= 2048 && D.M >= 128 && D.N >= 128 && big >= 512;
@@ -873,12 +878,10 @@ void launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, co
       tiny = !ta && atoi(force) == 3232;
     }
     if (tiny) {
-      launch_dma<32, 32, 32, 2>(ta, tb, epi, s, P, D, batch);
-      return;
+      return launch_dma<32, 32, 32, 2>(ta, tb, epi, s, P, D, batch);
     }
     if (small) {
-      launch_dma<32, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
-      return;
+      return launch_dma<32, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
     }
     // stages (measured, scripts/bench_gemm_f32.py): 4 with fragment
     // double-buffering for the split-K weight gradients (transA), 3 for the
@@ -902,26 +905,25 @@ void launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, co
       // MOG_GEMM_NS=3|4: deeper 32-deep pipelines (48 / 64 KB per workgroup)
       static const char* ns_env = getenv("MOG_GEMM_NS");
       const int ns = ns_env != nullptr ? atoi(ns_env) : 2;
-      if (t12864) launch_dma<128, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
-      else if (ns == 4) launch_dma<64, 64, 32, 4>(ta, tb, epi, s, P, D, batch);
-      else if (ns == 3) launch_dma<64, 64, 32, 3>(ta, tb, epi, s, P, D, batch);
-      else launch_dma<64, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
-      return;
+      if (t12864) return launch_dma<128, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
+      else if (ns == 4) return launch_dma<64, 64, 32, 4>(ta, tb, epi, s, P, D, batch);
+      else if (ns == 3) return launch_dma<64, 64, 32, 3>(ta, tb, epi, s, P, D, batch);
+      else return launch_dma<64, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
     }
     if (t12864) {
-      if (ta) launch_dma<128, 64, 16, 4>(ta, tb, epi, s, P, D, batch);
-      else launch_dma<128, 64, 16, 3>(ta, tb, epi, s, P, D, batch);
+      if (ta) return launch_dma<128, 64, 16, 4>(ta, tb, epi, s, P, D, batch);
+      else return launch_dma<128, 64, 16, 3>(ta, tb, epi, s, P, D, batch);
     } else if (b128) {
-      if (ta) launch_dma<128, 128, 16, 4>(ta, tb, epi, s, P, D, batch);
-      else launch_dma<128, 128, 16, 3>(ta, tb, epi, s, P, D, batch);
+      if (ta) return launch_dma<128, 128, 16, 4>(ta, tb, epi, s, P, D, batch);
+      else return launch_dma<128, 128, 16, 3>(ta, tb, epi, s, P, D, batch);
     } else {
-      if (ta) launch_dma<64, 64, 16, 4>(ta, tb, epi, s, P, D, batch);
-      else launch_dma<64, 64, 16, 3>(ta, tb, epi, s, P, D, batch);
+      if (ta) return launch_dma<64, 64, 16, 4>(ta, tb, epi, s, P, D, batch);
+      else return launch_dma<64, 64, 16, 3>(ta, tb, epi, s, P, D, batch);
     }
-    return;
   }
   if (b128) launch_tile<128, 128, 16, 1>(ta, tb, epi, s, P, D, batch);
   else launch_tile<64, 64, 16, 1>(ta, tb, epi, s, P, D, batch);
+  return 0;
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -980,7 +982,7 @@ extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const
   D.kseg = 0;
   D.eps_gen = 0;
   D.eps_seed = D.eps_off = 0;
-  launch_auto(transA, transB, epi, mog_stream(stream), P, D, batch);
+  MOG_TRY(launch_auto(transA, transB, epi, mog_stream(stream), P, D, batch));
   MOG_LAUNCH_RET();
 }
 
@@ -1009,7 +1011,7 @@ extern "C" int mog_gemm_f32_sigmoid_philox(const float* A, const float* B, float
   D.eps_gen = 1;
   D.eps_seed = seed;
   D.eps_off = offset;
-  launch_auto(false, false, EPI_SIGMOID_NOISE, mog_stream(stream), P, D, 1);
+  MOG_TRY(launch_auto(false, false, EPI_SIGMOID_NOISE, mog_stream(stream), P, D, 1));
   MOG_LAUNCH_RET();
 }
 
@@ -1049,6 +1051,6 @@ extern "C" int mog_gemm_f32_kseg(int nseg, const float* const* A, const float* c
   D.kseg = kseg;
   D.eps_gen = 0;
   D.eps_seed = D.eps_off = 0;
-  launch_auto(transA, transB, epi, mog_stream(stream), P, D, 1);
+  MOG_TRY(launch_auto(transA, transB, epi, mog_stream(stream), P, D, 1));
   MOG_LAUNCH_RET();
 }

@@ -19,6 +19,13 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 #define MOG_LAUNCH_RET() return (int)hipGetLastError()
 
+// propagate a nonzero status of a launch helper
+#define MOG_TRY(expr)            \
+  do {                           \
+    const int mog_rc_ = (expr);  \
+    if (mog_rc_ != 0) return mog_rc_; \
+  } while (0)
+
 static inline hipStream_t mog_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 static inline unsigned mog_cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }

@@ -855,8 +855,11 @@ void gemm_x3p_tn_(const Tensor& A3, int64_t sa, const Tensor& B3, int64_t sb, Te
   Op o("gemm_x3p_tn_");
   float* c = o.f(C, mat(M, N, ldc), "C");
   const int64_t np1 = npieces - 1;
-  const void* a = o.need(A3, BF16, np1 * sa + mat(K, M, lda), "A3");
-  const void* b = o.need(B3, BF16, np1 * sb + mat(K, N, ldb), "B3");
+  // the kernel reads 16-byte chunks (8 bf16) of every k-row: the last row of
+  // the last piece is read up to round8(M) / round8(N) elements
+  auto ext = [](int64_t K, int64_t n, int64_t ld) { return K > 0 ? (K - 1) * ld + (n + 7) / 8 * 8 : 0; };
+  const void* a = o.need(A3, BF16, np1 * sa + ext(K, M, lda), "A3");
+  const void* b = o.need(B3, BF16, np1 * sb + ext(K, N, ldb), "B3");
   float* cs = o.f(colsum, N, "colsum");
   GUARD(o);
   check(mog_gemm_x3p_tn(a, sa, b, sb, c, cs, M, N, K, lda, ldb, ldc, splitk, npieces,

@@ -478,7 +478,7 @@ class AIRModel:
                 ws.eps_scale[t], ws.eps_shift[t], ws.u[t], ws.stop, ws.runloss, ws.digits,
                 ws.live, rec, ws.th_f[t], ws.th_b[t], ws.scale[t], ws.shift[t], ws.zprob[t],
                 ws.zkl[t], ws.skl[t], ws.shkl[t], ws.zmask[t], ws.zval[t], ws.zc[t],
-                self._prior_dev)
+                self._prior_arg())
             if self.live_hook is not None:
                 self.live_hook(ws.live, t)
             if batched:
@@ -723,7 +723,7 @@ class AIRModel:
                 float(self.shift_prior_mean), float(self.shift_prior_variance), float(gscale),
                 None, ws.rec[t], ws.eps_scale[t], ws.eps_shift[t], ws.dth_f_all[t], ws.dth_b_all[t],
                 ws.dot_all[t], hid_t, w2, ws.dout[0, t], T * B * 2, ws.dhid[t], HS,
-                self._prior_dev)
+                self._prior_arg())
         # dh[t] = sum_z dhid_z W1_z^T for every step: one plain GEMM over
         # K = 5 HS ([dhid_0 .. dhid_4] rows against [W1_0 .. W1_4]), the same
         # k-ordered chain as the per-head sum
@@ -1258,8 +1258,17 @@ class AIRModel:
     # fp32 beta powers, an eager launch after it).  The reference's batch of 64
     # (training_air_original.py:22) is launch-bound without it.
     _graph_noise = False  # eps_x filled into its buffer (graph mode)
-    _prior_dev = None     # device z_pres prior log-odds (graph mode)
+    _graph_mode = False   # inside train_step_graphed (eager first step, capture, replay)
+    _prior_dev = None     # device z_pres prior log-odds (graph mode only)
     _graph = None
+    _graph_ws = None      # the workspace the graph was captured on (its pointers)
+
+    def _prior_arg(self):
+        """The device prior log-odds the step kernels read instead of the host
+        scalar: only in graph mode, where train_step_graphed refreshes it
+        before every replay.  Eager steps pass the host value (None here), so a
+        stale device value from an earlier graphed step is never read."""
+        return self._prior_dev if self._graph_mode else None
 
     def _graph_ok(self):
         others = [k for k in self.annealing_schedules if k != "z_pres_prior_log_odds"]
@@ -1276,11 +1285,17 @@ class AIRModel:
         if not self.train:
             raise RuntimeError("train_step on a model built with train=False")
         self._graph_ok()
+        self._graph_mode = self._graph_noise = True
+        try:
+            self._train_step_graphed(images, targets, global_batch)
+        finally:
+            self._graph_mode = self._graph_noise = False
+
+    def _train_step_graphed(self, images, targets, global_batch):
         X, tg = self._prep(images, targets)
         key = (tuple(X.shape), None if tg is None else tuple(tg.shape), global_batch)
         if self._graph is None or self._graph_key != key:
-            self._graph = None
-            self._graph_noise = True
+            self._graph = self._graph_ws = None
             if self._prior_dev is None:
                 self._prior_dev = torch.zeros(1, device=self.device)
             self._prior_dev.fill_(self.hyper("z_pres_prior_log_odds"))
@@ -1293,7 +1308,10 @@ class AIRModel:
             gX.copy_(X)
         if tg is not None and tg.data_ptr() != gT.data_ptr():
             gT.copy_(tg)
-        ws = self._ws
+        # The graph holds raw pointers into the workspace it was captured on:
+        # replay on that one (kept alive by _graph_ws), even when an infer /
+        # step / compute_gradients at another batch has replaced self._ws since
+        ws = self._ws = self._graph_ws
         self._fill_noise(ws, None)
         if ws.noise_side:  # the graph's first launch reads it
             torch.cuda.current_stream().wait_stream(self._side_stream())
@@ -1322,6 +1340,7 @@ class AIRModel:
             self._forward(gX, gT, ws, need_grad=True, outputs=False)
             self._backward(gX, ws)
         self._graph = g
+        self._graph_ws = ws
 
     def step(self, images, targets=None, noise=None, global_batch: Optional[int] = None):
         """``sess.run([training, loss, accuracy, mse_loss, global_step])``

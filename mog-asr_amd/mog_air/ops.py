@@ -151,15 +151,6 @@ def gemm_bf16(A, B, C, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, tn=
                     float(aux_scale), int(splitk))
 
 
-def cvt_bf16(src: torch.Tensor, dst: torch.Tensor, transpose: bool) -> None:
-    """Pack an fp32 [R, C] matrix into a zero-padded bf16 matrix dst
-    ([C', R'] when transposed)."""
-    R, Cc = src.shape
-    rows, cols = dst.shape
-    _lib.call("mog_cvt_bf16", dp(src), R, Cc, Cc, dp(dst), rows, cols, cols, int(transpose),
-              stream_ptr())
-
-
 def stn_backward(U: torch.Tensor, theta: torch.Tensor, out_hw, G: torch.Tensor,
                  gscale: Optional[torch.Tensor] = None, want_dU=True, want_dtheta=True,
                  want_dot=False, dU=None, dtheta=None, dot=None, n: Optional[int] = None,
@@ -207,10 +198,6 @@ def stn_backward(U: torch.Tensor, theta: torch.Tensor, out_hw, G: torch.Tensor,
                        dtheta if want_dtheta else None, dot if want_dot else None,
                        NU if NU < N else 0, NG if NG < N else 0)
     return dU, dtheta, dot
-
-
-def colsum_add(X: torch.Tensor, R: int, N: int, ld: int, out: torch.Tensor) -> None:
-    _lib.call("mog_colsum_add", dp(X), R, N, ld, dp(out), stream_ptr())
 
 
 def _i64(v: int) -> int:

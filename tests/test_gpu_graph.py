@@ -103,3 +103,109 @@ def test_asr_graph_replay_matches_eager_bitwise():
                                       mg._ws.means[:3].cpu().numpy())
     assert mg._graph is not None
     assert torch.equal(me.params.flat.view(torch.int32), mg.params.flat.view(torch.int32))
+
+
+def test_graph_replay_after_other_batch_uses_captured_workspace():
+    """graphed(64) -> infer(100) -> graphed(64): the replay runs on the
+    workspace it was captured on (the infer at another batch replaced
+    self._ws), and still equals eager."""
+    data = _batches(3)
+    x100, k100 = _batches(1, 100)[0]
+    me, mg = _model("gw_e", "fp32"), _model("gw_g", "fp32")
+    for i, (x, k) in enumerate(data):
+        me.train_step_async(x, k)
+        mg.train_step_graphed(x, k)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(me._ws.means[:3].cpu().numpy(),
+                                      mg._ws.means[:3].cpu().numpy(), err_msg=f"step {i}")
+        np.testing.assert_array_equal(me.rec_num_digits.cpu().numpy(),
+                                      mg.rec_num_digits.cpu().numpy())
+        if i == 0:
+            me.infer(x100, k100)
+            mg.infer(x100, k100)
+            torch.cuda.synchronize()
+            assert mg._ws.B == 100 and mg._graph_ws.B == 64
+            assert me.loss == mg.loss
+    assert mg._ws is mg._graph_ws
+    assert torch.equal(me.params.flat.view(torch.int32), mg.params.flat.view(torch.int32))
+
+
+def test_eager_step_after_graph_reads_the_current_prior():
+    """After graphed steps, an eager step uses the host's annealed z_pres
+    prior of ITS global step (not the device copy the last replay read)."""
+    data = _batches(4)
+    me, mg = _model("gp_e", "fp32"), _model("gp_g", "fp32")
+    for i, (x, k) in enumerate(data):
+        me.train_step_async(x, k)
+        if i < 2:
+            mg.train_step_graphed(x, k)
+        else:
+            mg.train_step_async(x, k)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(me._ws.means[:3].cpu().numpy(),
+                                      mg._ws.means[:3].cpu().numpy(), err_msg=f"step {i}")
+    assert torch.equal(me.params.flat.view(torch.int32), mg.params.flat.view(torch.int32))
+
+
+def _copy_state(dst, src):
+    for n in ("flat", "m", "v"):
+        getattr(dst.params, n).copy_(getattr(src.params, n))
+    for n in ("beta1_power", "beta2_power", "adam_t", "global_step"):
+        setattr(dst.params, n, getattr(src.params, n))
+    dst.params.version += 1
+    dst._noise_ctr = src._noise_ctr
+
+
+def _grad_close(ga, gb, rel=1e-4):
+    """Per tensor: max |a - b| <= rel * max |a| (split-K atomics reorder the
+    weight-gradient sums from B = 1024 on)."""
+    bad = []
+    for name in ga:
+        a, b = ga[name], gb[name]
+        scale = float(np.abs(a).max())
+        err = float(np.abs(a - b).max())
+        if err > rel * max(scale, 1e-30):
+            bad.append((name, err, scale))
+    assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_side_streams_match_serial_at_b1024(precision):
+    """From B = 1024 (SIDE_MIN_BATCH) the step forks noise fills, loop-state
+    resets, the X split, the heads' and the recurrent-rows weight gradients
+    onto a side stream: forward bitwise and gradients (split-K tolerance)
+    equal to the same step with every fork off."""
+    (x, k), = _batches(1, 1024)
+    ms, mp = _model("sd_s" + precision, precision), _model("sd_p" + precision, precision)
+    ms.HEADS_WGRAD_SIDE = ms.REC_WGRAD_SIDE = ms.NOISE_ON_SIDE = False
+    assert mp.HEADS_WGRAD_SIDE and mp.REC_WGRAD_SIDE and mp.NOISE_ON_SIDE
+    gs = ms.compute_gradients(x, k)
+    gp = mp.compute_gradients(x, k)
+    np.testing.assert_array_equal(ms._ws.means[:3].cpu().numpy(), mp._ws.means[:3].cpu().numpy())
+    np.testing.assert_array_equal(ms.rec_num_digits.cpu().numpy(), mp.rec_num_digits.cpu().numpy())
+    _grad_close(gs, gp)
+    # and a full train step (clip + Adam) on each: parameters within Adam's
+    # sensitivity to the reordered sums (lr 1e-3)
+    ms.train_step_async(x, k)
+    mp.train_step_async(x, k)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(ms._ws.means[:3].cpu().numpy(), mp._ws.means[:3].cpu().numpy())
+    d = (ms.params.flat - mp.params.flat).abs()
+    assert float(d.max()) <= 2.5e-3 and float((d > 1e-6).float().mean()) < 1e-3
+
+
+def test_graph_replay_with_side_stream_forks_at_b1024():
+    """The side-stream forks captured into the graph (B = 1024): a replay's
+    forward equals the eager step from the same state bit for bit, its
+    gradient within the split-K tolerance."""
+    data = _batches(2, 1024)
+    me, mg = _model("gb_e", "fp32"), _model("gb_g", "fp32")
+    mg.train_step_graphed(*data[0])  # eager step + capture
+    torch.cuda.synchronize()
+    _copy_state(me, mg)
+    me.train_step_async(*data[1])
+    mg.train_step_graphed(*data[1])  # replay
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(me._ws.means[:3].cpu().numpy(), mg._ws.means[:3].cpu().numpy())
+    np.testing.assert_array_equal(me.rec_num_digits.cpu().numpy(), mg.rec_num_digits.cpu().numpy())
+    _grad_close(me.params.grad_dict(), mg.params.grad_dict())
