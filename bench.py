@@ -71,6 +71,8 @@ def kernel_work(name, B, precision, C2=2500, H=256, T=3):
         return "hbm", B * fused_bytes_per_image_step(C2) / 1e9, "GB/s", HBM_PEAK_GBS
     if name == "stn_vae_step_all":           # all T steps' rows in one launch
         return "hbm", T * B * fused_bytes_per_image_step(C2) / 1e9, "GB/s", HBM_PEAK_GBS
+    if name == "stn_vae_step_f32_all":       # the fp32 fused step over T*B rows: MFMA-bound
+        return "mfma", T * B * vae_chain_flops_per_image() / 1e12, "TFLOP/s", FP32_MFMA_PEAK_TFLOPS
     return None
 
 
@@ -83,26 +85,33 @@ def pmc_traffic(tag):
 
 
 def roofline(events, B, precision):
-    """Dominant tagged kernel (largest total time in the timed region)."""
-    best = None
+    """The dominant launch of the timed step: among the tagged launches (each
+    tag is one kernel launch per occurrence: the x-projection, its weight
+    gradient, the fused STN + VAE step), the one with the largest total time.
+    Every tagged launch's own roofline is listed under ``launches_priced``."""
+    rows = []
     for name, evs in events.items():
-        durs = [a.elapsed_time(b) * 1e-3 for a, b in evs]  # seconds
-        tot = sum(durs)
-        if kernel_work(name, B, precision) is None:
+        work = kernel_work(name, B, precision)
+        if work is None:
             continue
-        if best is None or tot > best[1]:
-            best = (name, tot, durs)
-    if best is None:
+        durs = [a.elapsed_time(b) * 1e-3 for a, b in evs]  # seconds
+        bound, amount, unit, peak = work
+        avg = sum(durs) / len(durs)
+        achieved = amount / avg
+        rows.append({"kernel": name, "bound": bound, "achieved": achieved, "peak": peak,
+                     "unit": unit, "frac": achieved / peak,
+                     "traffic": pmc_traffic(f"{name}_{precision}_b{B}"),
+                     "launches": len(durs), "avg_launch_us": avg * 1e6,
+                     "total_us": sum(durs) * 1e6,
+                     "algorithmic_per_launch": amount * 1e12 if bound == "mfma" else amount * 1e9,
+                     "algorithmic_unit": "flop" if bound == "mfma" else "bytes"})
+    if not rows:
         return None
-    name, tot, durs = best
-    bound, amount, unit, peak = kernel_work(name, B, precision)
-    avg = tot / len(durs)
-    achieved = amount / avg
-    return {"kernel": name, "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
-            "frac": achieved / peak, "traffic": pmc_traffic(f"{name}_{precision}_b{B}"),
-            "launches": len(durs), "avg_launch_us": avg * 1e6,
-            "algorithmic_per_launch": amount * 1e12 if bound == "mfma" else amount * 1e9,
-            "algorithmic_unit": "flop" if bound == "mfma" else "bytes"}
+    rows.sort(key=lambda r: -r["total_us"])
+    out = dict(rows[0])
+    out["launches_priced"] = [{k: r[k] for k in ("kernel", "frac", "avg_launch_us", "unit",
+                                                 "achieved")} for r in rows]
+    return out
 
 
 def synthetic(batch, seed, canvas=50, counts=None, side=None):

@@ -547,13 +547,8 @@ class AIRModel:
             # forward only (no backward follows): the backward's saved
             # activations are not written (vae_step.hip moves its own bytes)
             sv = r_ if save else (lambda a: None)  # noqa: E731
-            _ops.stn_vae_step_(TB, C, X, r_(ws.th_f), r_(ws.th_b), r_(ws.zmask), r_(ws.zval),
-                               r_(ws.eps_z), r_(ws.eps_x), ops._i64(self.noise_seed),
-                               ops._i64(off), gen, wt, bias, lik_std, float(self.vae_prior_mean),
-                               float(self.vae_prior_variance), self.vae_prior_log_variance,
-                               r_(ws.cparts), r_(ws.prows), None, r_(ws.vkl), sv(ws.gb),
-                               sv(ws.a1b), sv(ws.a2b), sv(ws.mu), sv(ws.lv), r_(ws.z), sv(ws.zb),
-                               sv(ws.d1b), sv(ws.d2b), r_(ws.r), B)
+            with self._timed("stn_vae_step_all"):
+                self._stn_vae_step_bf16(TB, C, X, r_, sv, gen, off, wt, bias, lik_std, ws, B)
             return
         # the fused fp32 kernel runs one 32-row tile per workgroup with a long
         # serial chain per tile (~200 us): below one tile per CU (T*B < 8192
@@ -567,12 +562,14 @@ class AIRModel:
             saved = [r_(getattr(ws, n)) if save else None
                      for n in ("g", "a1pre", "a1", "a2pre", "a2", "mu", "lv", "d1pre", "d1",
                                "d2pre", "d2")]
-            _ops.stn_vae_step_f32_(TB, C, X, r_(ws.th_f), r_(ws.th_b), r_(ws.zmask), r_(ws.zval),
-                                   r_(ws.eps_z), r_(ws.eps_x), ops._i64(self.noise_seed),
-                                   ops._i64(off), gen, self._wf32, bias, lik_std,
-                                   float(self.vae_prior_mean), float(self.vae_prior_variance),
-                                   self.vae_prior_log_variance, r_(ws.cparts), r_(ws.prows), None,
-                                   r_(ws.vkl), saved, r_(ws.z), r_(ws.r), B)
+            with self._timed("stn_vae_step_f32_all"):
+                _ops.stn_vae_step_f32_(TB, C, X, r_(ws.th_f), r_(ws.th_b), r_(ws.zmask),
+                                       r_(ws.zval), r_(ws.eps_z), r_(ws.eps_x),
+                                       ops._i64(self.noise_seed), ops._i64(off), gen, self._wf32,
+                                       bias, lik_std, float(self.vae_prior_mean),
+                                       float(self.vae_prior_variance), self.vae_prior_log_variance,
+                                       r_(ws.cparts), r_(ws.prows), None, r_(ws.vkl), saved,
+                                       r_(ws.z), r_(ws.r), B)
             return
         v = lambda a: a[t0:t1].reshape(TB, -1)  # noqa: E731
         vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
@@ -627,6 +624,16 @@ class AIRModel:
         # the loss kernel adds the parts in step order (:665-675)
         _ops.stn_write_parts_(v(ws.r), TB, W, W, r_(ws.th_b), C, C, r_(ws.zval), r_(ws.zmask),
                               r_(ws.cparts), r_(ws.prows))
+
+    def _stn_vae_step_bf16(self, TB, C, X, r_, sv, gen, off, wt, bias, lik_std, ws, B):
+        """The bf16 fused step over the TB rows of loop steps r_ (x row = row % B)."""
+        _ops.stn_vae_step_(TB, C, X, r_(ws.th_f), r_(ws.th_b), r_(ws.zmask), r_(ws.zval),
+                           r_(ws.eps_z), r_(ws.eps_x), ops._i64(self.noise_seed), ops._i64(off),
+                           gen, wt, bias, lik_std, float(self.vae_prior_mean),
+                           float(self.vae_prior_variance), self.vae_prior_log_variance,
+                           r_(ws.cparts), r_(ws.prows), None, r_(ws.vkl), sv(ws.gb), sv(ws.a1b),
+                           sv(ws.a2b), sv(ws.mu), sv(ws.lv), r_(ws.z), sv(ws.zb), sv(ws.d1b),
+                           sv(ws.d2b), r_(ws.r), B)
 
     def _vae_sample_fwd_all(self, ws, zb, ldzb, t0=0, t1=None):
         t1 = self.max_steps if t1 is None else t1
