@@ -33,7 +33,11 @@
 namespace {
 
 constexpr int PM = 64, PMT = 4;   // images per tile, 16-row MFMA tiles
-constexpr int MW = 4, SW = 4;     // waves per role: one of each per SIMD
+#ifndef MOG_PIPE_WAVES
+#define MOG_PIPE_WAVES 4
+#endif
+// waves per role: 4 + 4 (one of each per SIMD, 256 registers) or 8 + 8 (128)
+constexpr int MW = MOG_PIPE_WAVES, SW = MOG_PIPE_WAVES;
 constexpr int MTHR = MW * 64;     // M-role threads (tid 0..255)
 constexpr int NTHR_P = (MW + SW) * 64;
 constexpr int KGP = 5;            // recognition k-steps per DMA slab
@@ -262,6 +266,7 @@ __device__ __forceinline__ void m_tile(const StepArgs& p_, unsigned char* lds, u
                       b1q[c]);
   }
   mbar();
+  stamp(p, li_tile, 8);
   // ---- a2 = softplus(a1 W2 + b2) [64 x 256], in place; a1's saved copy
   // flushed inside the k loop
   __bf16* sA2 = sA1;
@@ -274,7 +279,8 @@ __device__ __forceinline__ void m_tile(const StepArgs& p_, unsigned char* lds, u
                                            mbar, fl, tid);
   }
   mbar();
-  // ---- mu | lv = a2 W + b [64 x 50] fp32 (waves 0-3 | 4-7), then a2's copy
+  stamp(p, li_tile, 9);
+  // ---- mu | lv = a2 W + b [64 x 50] fp32 (first | second half of the waves), then a2's copy
   float* sMu = reinterpret_cast<float*>(lds + L::OFF_MU);
   float* sLv = reinterpret_cast<float*>(lds + L::OFF_LV);
   {
@@ -294,6 +300,7 @@ __device__ __forceinline__ void m_tile(const StepArgs& p_, unsigned char* lds, u
     if (save) flush_rows<MTHR>(sA2, S256, p.a2b + (size_t)b0 * 256, 256, 256, nb, tid);
   }
   mbar();
+  stamp(p, li_tile, 10);
   // ---- z = mu + eps sqrt(exp(lv)); VAE KL (vae.py:27-30) -------------------
   float* sKl = reinterpret_cast<float*>(lds + L::OFF_KL);
   __bf16* sZ = reinterpret_cast<__bf16*>(lds + L::OFF_Z);
@@ -341,6 +348,7 @@ __device__ __forceinline__ void m_tile(const StepArgs& p_, unsigned char* lds, u
     p.vkl[b0 + m] = vkl;
     if (p.runloss && p.mask[b0 + m] != 0.0f) p.runloss[b0 + m] = p.runloss[b0 + m] + vkl;
   }
+  stamp(p, li_tile, 11);
   // ---- d1 = softplus(z Wg1 + b) [64 x 256] (over mu | lv) -------------------
   __bf16* sD1 = reinterpret_cast<__bf16*>(lds + L::OFF_D1);
   dense_tiles<PMT, 64, 256, 16 / MW, 2, false>(sZ, SZ, p.wt[4], p.bias[4], 0, 0, MW,
@@ -349,6 +357,7 @@ __device__ __forceinline__ void m_tile(const StepArgs& p_, unsigned char* lds, u
                                          },
                                          mbar, NoHook{}, tid);
   mbar();
+  stamp(p, li_tile, 12);
   // ---- d2 = softplus(d1 Wg2 + b) [64 x 512] at 0 (in place over d1) --------
   __bf16* sD2 = reinterpret_cast<__bf16*>(lds);
   {
@@ -535,7 +544,7 @@ __device__ __forceinline__ void s_sample(const StepArgs& p, unsigned char* lds, 
 // The persistent pipelined kernel: one 16-wave workgroup per CU, tiles
 // blockIdx.x, blockIdx.x + gridDim.x, ... (at most 8 per workgroup).
 template <int LA>
-__global__ __launch_bounds__(NTHR_P, 2) void stn_vae_step_pipe_kernel(StepArgs p) {
+__global__ __launch_bounds__(NTHR_P, 8 / MW) void stn_vae_step_pipe_kernel(StepArgs p) {
 #pragma clang fp contract(off)
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LayP::TOTAL];
   const int tid = threadIdx.x;

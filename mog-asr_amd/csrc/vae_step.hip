@@ -887,8 +887,9 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
         std::vector<long long> h((size_t)grid * 128);
         (void)hipStreamSynchronize(s);
         (void)hipMemcpy(h.data(), pbuf, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
-        // per tile: M wait->L1 end, L1 end->g2 end, output; S sample, write
-        double a[5] = {0};
+        // per tile: M wait->L1 end, L1 end->g2 end, output; S sample, write;
+        // inside L1 end->g2 end: L1 epilogue, L2, mu/lv, sample, g1, g2
+        double a[5] = {0}, f[6] = {0};
         long cnt = 0, scnt = 0;
         long long t0 = -1, t1 = 0;
         for (int b = 0; b < grid; ++b)
@@ -899,6 +900,8 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
             a[0] += (double)(r[1] - r[0]); a[1] += (double)(r[2] - r[1]); a[2] += (double)(r[3] - r[2]);
             if (r[4] && r[5]) a[3] += (double)(r[5] - r[4]);
             if (r[6] && r[7]) { a[4] += (double)(r[7] - r[6]); ++scnt; }
+            const long long ms[7] = {r[1], r[8], r[9], r[10], r[11], r[12], r[2]};
+            for (int q = 0; q < 6; ++q) if (ms[q] && ms[q + 1]) f[q] += (double)(ms[q + 1] - ms[q]);
             t0 = t0 < 0 ? r[0] : std::min(t0, r[0]);
             t1 = std::max(t1, std::max(r[3], r[7]));
           }
@@ -907,6 +910,10 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
                   "L2..g2 %.2f out %.2f | S sample %.2f write %.2f | span %.2f\n", grid, cnt,
                   a[0] / cnt / 100.0, a[1] / cnt / 100.0, a[2] / cnt / 100.0, a[3] / cnt / 100.0,
                   scnt ? a[4] / scnt / 100.0 : 0.0, (t1 - t0) / 100.0);
+        if (cnt)
+          fprintf(stderr, "  M detail: L1epi %.2f L2 %.2f mulv %.2f sample %.2f g1 %.2f g2 %.2f\n",
+                  f[0] / cnt / 100.0, f[1] / cnt / 100.0, f[2] / cnt / 100.0, f[3] / cnt / 100.0,
+                  f[4] / cnt / 100.0, f[5] / cnt / 100.0);
       }
       return 0;
     }

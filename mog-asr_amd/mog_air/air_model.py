@@ -1057,18 +1057,33 @@ class AIRModel:
         gemm(X, dY, out, M, N, K, lda, ldb, N, transA=True, epi=EPI_ATOMIC,
              splitk=splitk, colsum=bias_out)
 
+    # fp32 configuration: the VAE weight gradients whose operands are 16-byte
+    # rows (M, N multiples of 4: the 784/512/256-wide layers, 98 % of the
+    # flops) on the bf16 matrix cores with exact three-piece splits inside the
+    # GEMM (gemm_x3.hip: fp32-level accuracy, as the LSTM x-rows gradient,
+    # DESIGN.md §4.4); MOG_VAE_WGRAD_X3=0 keeps them on the fp32 split-K GEMM
+    VAE_WGRAD_X3 = os.environ.get("MOG_VAE_WGRAD_X3", "1") == "1"
+
+    def _dw_x3(self, X, dY, out, K, M, N, lda, ldb, bias_out):
+        """out[M,N] += X^T dY over K rows (gemm_x3_tn), bias_out += colsum(dY)."""
+        if not (self.VAE_WGRAD_X3 and M % 4 == 0 and N % 4 == 0):
+            return self._dw(X, dY, out, K, M, N, lda, ldb, bias_out)
+        tiles = ((M + 127) // 128) * ((N + 127) // 128)
+        splitk = max(1, min(K // 256, (512 + tiles - 1) // tiles))
+        ops.gemm_x3_tn(X, dY, out, M, N, K, lda, ldb, N, splitk=splitk, colsum=bias_out)
+
     def _vae_weight_grads_fp32(self, ws):
         TB = ws.B * self.max_steps
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
         gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
-        self._dw(ws.g, ws.da1, g("recognition_1"), TB, W2, R1, W2, R1, gb("recognition_1"))
-        self._dw(ws.a1, ws.da2, g("recognition_2"), TB, R1, R2, R1, R2, gb("recognition_2"))
+        self._dw_x3(ws.g, ws.da1, g("recognition_1"), TB, W2, R1, W2, R1, gb("recognition_1"))
+        self._dw_x3(ws.a1, ws.da2, g("recognition_2"), TB, R1, R2, R1, R2, gb("recognition_2"))
         self._dw([ws.a2] * 2, [ws.dmu, ws.dlv], [g("rec_mean"), g("rec_log_variance")], TB, R2,
                  Z, R2, Z, [gb("rec_mean"), gb("rec_log_variance")])
         self._dw(ws.z, ws.dd1, g("generative_1"), TB, Z, G1, Z, G1, gb("generative_1"))
-        self._dw(ws.d1, ws.dd2, g("generative_2"), TB, G1, G2, G1, G2, gb("generative_2"))
-        self._dw(ws.d2, ws.dm, g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
+        self._dw_x3(ws.d1, ws.dd2, g("generative_2"), TB, G1, G2, G1, G2, gb("generative_2"))
+        self._dw_x3(ws.d2, ws.dm, g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
 
     def _weight_grads_glimpse(self, ws):
         """Weight gradients of the VAE and the five heads (every loop step at

@@ -314,6 +314,12 @@ class AIRModel(_AirBase):
     def _batched_vae(self, B: int) -> bool:
         return False  # per step: the ASR loop feeds z of step t into step t+1's input
 
+    def _x3_asr(self, B: int) -> bool:
+        """fp32: the inference LSTM's x-rows weight gradient X^T dGsum on the
+        three-piece bf16-core form (MOG_X_GRAD_X3=2, the default, as for AIR)
+        from the batch where the side stream pays (SIDE_MIN_BATCH)."""
+        return self.precision == "fp32" and self.X_GRAD_X3 == 2 and B >= self.SIDE_MIN_BATCH
+
     def _forward(self, X, targets, ws, need_grad, outputs=True):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
         C, W, C2 = self.canvas_size, self.windows_size, self.C2
@@ -332,6 +338,22 @@ class AIRModel(_AirBase):
         lik_std = float(self.hyper("vae_likelihood_std"))
         fix = -1 if self.fix_steps is None else int(self.fix_steps)
         w20 = self._w20()
+        x3 = need_grad and self._x3_asr(B)
+        if x3:
+            # the x-rows gradient's A operand split into three bf16 pieces on
+            # the side stream, under the x-projection (AIRModel._forward does
+            # the same); joined in _weight_grads
+            main, side = torch.cuda.current_stream(), self._side_stream()
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                C2p = self._pad8(C2)
+                if getattr(ws, "X3", None) is None:
+                    ws.X3 = torch.empty((3, B, C2p), device=self.device, dtype=torch.bfloat16)
+                ops.split3_bf16(X, ws.X3, B, C2, C2, C2p, B * C2p)
+                ws.x3_ready = torch.cuda.Event()
+                ws.x3_ready.record(side)
         # loop-invariant x-projection of the inference LSTM (chain over x first)
         with self._timed("lstm_x_projection"):
             gemm([X], [Ki[:C2]], [ws.Gx], B, 4 * H, C2, C2, 4 * H, 4 * H)
@@ -500,6 +522,19 @@ class AIRModel(_AirBase):
         with self._timed("lstm_x_projection_grad"):
             if self.precision == "bf16":
                 self._x_grad_bf16(X, ws, gKi, G("infer_rnn_running/bias"), 0, C2)
+            elif getattr(ws, "x3_ready", None) is not None:
+                # X^T dGsum on the bf16 matrix cores from exact three-piece
+                # splits of both operands (gemm_x3.hip): the
+                # AIR x-rows gradient's form
+                torch.cuda.current_stream().wait_event(ws.x3_ready)
+                ws.x3_ready = None
+                if getattr(ws, "dG3", None) is None:
+                    ws.dG3 = torch.empty((3, B, 4 * H), device=self.device, dtype=torch.bfloat16)
+                ops.split3_bf16(ws.dGsum, ws.dG3, B, 4 * H, 4 * H, 4 * H, B * 4 * H)
+                C2p = self._pad8(C2)
+                ops.gemm_x3p_tn(ws.X3.view(-1), B * C2p, ws.dG3, B * 4 * H, gKi[:C2], C2, 4 * H,
+                                B, C2p, 4 * H, 4 * H, splitk=max(1, min(B // 256, self.X3_SPLITK)),
+                                colsum=G("infer_rnn_running/bias"))
             else:
                 self._dw(X, ws.dGsum, gKi[:C2], B, C2, 4 * H, C2, 4 * H,
                          G("infer_rnn_running/bias"))

@@ -99,8 +99,8 @@ def test_x3_zero_extents_and_checks():
 
 def test_x3_fp32_step_gradients_match_chain():
     """The whole fp32 train step's gradients with the x3 x-part gradient (in-
-    kernel split and pre-split) and with the fp32 chain agree to fp32 level (every gradient; only the LSTM
-    kernel's x rows and bias take a different path)."""
+    kernel split and pre-split) and the x3 VAE weight gradients, and with the
+    fp32 chain, agree to fp32 level (every gradient)."""
     from mog_air.air_model import AIRModel
     rng = np.random.default_rng(5)
     x = (rng.uniform(size=(256, 2500)) * (rng.uniform(size=(256, 2500)) < 0.3)).astype(np.float32)
@@ -110,6 +110,7 @@ def test_x3_fp32_step_gradients_match_chain():
                      z_pres_prior_log_odds=-0.01, cnn=False, train=True, scope="x3",
                      device=DEV, precision="fp32", seed=3, noise_seed=4)
         m.X_GRAD_X3 = x3
+        m.VAE_WGRAD_X3 = x3 != 0  # (the VAE weight gradients' x3 form rides along)
         grads.append({k: torch.as_tensor(np.asarray(v), dtype=torch.float64)
                       for k, v in m.compute_gradients(x).items()})
     for g in grads[:2]:
@@ -138,3 +139,25 @@ def test_x1_plain_bf16_operands(M, N, K, m0, splitk):
     Ad, Bd = A[:, m0:m0 + M].double(), B.double()
     assert _err(C.cpu(), Ad.T @ Bd, Ad.abs().T @ Bd.abs()) <= 1e-6
     assert _err(cs.cpu(), Bd.sum(0), Bd.abs().sum(0)) <= 1e-6
+
+
+def test_x3_asr_step_gradients_match_chain():
+    """AIR-ASR (configs[2]) from B = 1024: the inference LSTM's x-rows
+    gradient on the three-piece bf16 form (X split on the side stream under the
+    x-projection) against the fp32 chain: every gradient to fp32 level."""
+    import bench
+    rng = np.random.default_rng(6)
+    B = 1024
+    x = (rng.uniform(size=(B, 2500)) * (rng.uniform(size=(B, 2500)) < 0.3)).astype(np.float32)
+    X = torch.as_tensor(x).to(DEV)
+    grads = []
+    for x3 in (2, 0):
+        m = bench.make_asr_model("fp32", torch.device(DEV), "x3asr%d" % x3)
+        m.X_GRAD_X3 = x3
+        assert m._x3_asr(B) == (x3 == 2)
+        grads.append({k: torch.as_tensor(np.asarray(v), dtype=torch.float64)
+                      for k, v in m.compute_gradients(X).items()})
+    for k in grads[0]:
+        a, b = grads[0][k], grads[1][k]
+        scale = b.abs().max().item() + 1e-30
+        assert (a - b).abs().max().item() <= 1e-5 * scale, k
