@@ -64,6 +64,16 @@ int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb, float* C, 
                     int M, int N, int K, int lda, int ldb, int ldc, int splitk, int npieces,
                     void* stream);
 
+/* dX = epi(dY W^T) at fp32-level accuracy on the bf16 matrix cores (the VAE
+ * input gradients; replaces the MatMul gradients of vae.py:18-46's dense
+ * layers w.r.t. their inputs): C[M][N] = sum_k A[m][k] B[n][k], A fp32 [M][lda]
+ * split into three bf16 pieces inside the kernel, B = W [N][K] given as the
+ * three pieces of mog_split3_bf16 (piece p at B3 + p * sb, row pitch ldb).
+ * epi 0: store; 1: C = v * sigmoid(aux[m][n]) (dX through softplus).
+ * K, N, lda, ldc, ldaux multiples of 4; ldb, sb multiples of 8; deterministic. */
+int mog_gemm_x3_nt(const float* A, const void* B3, long sb, float* C, const float* aux, int M,
+                   int N, int K, int lda, int ldb, int ldc, int ldaux, int epi, void* stream);
+
 /* C = sigmoid((A B + bias) + scale * eps) for A [M][K] (lda), B [K][N] (ldb):
  * the VAE output layer (vae.py:44-46) with the likelihood noise eps generated
  * in the epilogue -- element (m, n) is lane n % 4 of Philox4x32-10 quad

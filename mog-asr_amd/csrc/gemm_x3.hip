@@ -322,6 +322,173 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ s
   *reinterpret_cast<u32x2*>(d + 2 * pstride) = p2;
 }
 
+
+// ---- NT form: C[M][N] = epi(sum_k A[m][k] B[n][k]) ------------------------
+// The input gradients of the VAE (dX = dY W^T: A = dY [M][lda] fp32,
+// k-contiguous rows; B = W [N][K] given as its three bf16 pieces, split once
+// per optimizer step, k-contiguous rows of ldb) at fp32-level accuracy on the
+// bf16 matrix cores: A is split in registers as it is staged, both operands
+// live in LDS as k-contiguous rows, so every MFMA fragment (row li, k 8g ..
+// 8g+7) is one ds_read_b128; six products per 16x16x32 block, smallest first.
+// Epilogue: the accumulator quads transposed across lanes (a lane owns four
+// consecutive columns), then store or softplus backward (C = v * sigmoid(aux),
+// gemm_f32.hip's EPI_SOFTPLUS_BWD), 16-byte stores.  No split-K: the sums
+// over K (<= 784) stay inside one workgroup, so the result is deterministic.
+constexpr int NT_LDK = BK + 8;                 // LDS row pitch (bf16): 80 B, conflict-free b128
+constexpr int NT_PIECE = BM * NT_LDK;
+constexpr int NT_STAGE = 6 * NT_PIECE;         // A0 A1 A2 B0 B1 B2 (61,440 B)
+constexpr int NT_NLA = (BM * BK / 4) / 256;    // float4 loads of A per thread (4)
+constexpr int NT_NLB = (BN * BK / 8) / 256;    // 16-byte chunks of a B piece per thread (2)
+
+struct X3NtArgs {
+  const float* A;
+  const __bf16* B3;
+  long sb;
+  float* C;
+  const float* aux;
+  int M, N, K, lda, ldb, ldc, ldaux, nx, ny, epi;
+};
+
+__device__ __forceinline__ float xt_dpp1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float xt_dpp2(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+// 4 x 4 transpose inside lane quads: row g*4 + r of column li in, row
+// g*4 + (li & 3) at columns (li & ~3) + r out
+__device__ __forceinline__ floatx4 xt_quad_transpose(const floatx4& a, int lane) {
+  const int e = lane & 3;
+  float r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3];
+  {
+    const bool hi = (e & 2) != 0;
+    const float t0 = xt_dpp2(hi ? r0 : r2), t1 = xt_dpp2(hi ? r1 : r3);
+    if (hi) { r0 = t0; r1 = t1; } else { r2 = t0; r3 = t1; }
+  }
+  {
+    const bool od = (e & 1) != 0;
+    const float t0 = xt_dpp1(od ? r0 : r1), t1 = xt_dpp1(od ? r2 : r3);
+    if (od) { r0 = t0; r2 = t1; } else { r1 = t0; r3 = t1; }
+  }
+  return floatx4{r0, r1, r2, r3};
+}
+
+template <int EPI>  // 0 store, 1 softplus backward
+__global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[NT_STAGE];
+  const int nwg = gridDim.x;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int bx = wg % D.nx, by = wg / D.nx;
+  const int m0 = by * BM, n0 = bx * BN;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const int M = D.M, N = D.N, K = D.K;
+  // staging roles: A float4 i covers row t/8 + 32 i, k 4 (t % 8) ..; B chunk i
+  // of a piece covers row t/4 + 64 i, k 8 (t % 4) ..
+  const int ar = t >> 3, ak = (t & 7) * 4;
+  const int br = t >> 2, bk = (t & 3) * 8;
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float4 ra[NT_NLA];
+  u32x4 rb[3][NT_NLB];
+  const float4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const u32x4 z4 = {0u, 0u, 0u, 0u};
+  auto load_tiles = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NT_NLA; ++i) {
+      const int gm = m0 + ar + 32 * i, gk = k0 + ak;
+      // K % 4 == 0: a float4 is wholly inside or outside the k range
+      ra[i] = (gm < M && gk < K) ? *reinterpret_cast<const float4*>(D.A + (size_t)gm * D.lda + gk)
+                                 : zero4;
+    }
+#pragma unroll
+    for (int i = 0; i < NT_NLB; ++i) {
+      const int gn = n0 + br + 64 * i, gk = k0 + bk;
+      // ldb % 8 == 0 and the pieces are zero past K: a chunk starting below
+      // K stays inside the row
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        rb[p][i] = (gn < N && gk < K)
+                       ? *reinterpret_cast<const u32x4*>(D.B3 + p * D.sb + (size_t)gn * D.ldb + gk)
+                       : z4;
+    }
+  };
+  auto store_tiles = [&]() {
+#pragma unroll
+    for (int i = 0; i < NT_NLA; ++i) {
+      const int o = (ar + 32 * i) * NT_LDK + ak;
+      u32x2 p0, p1, p2;
+      split4(ra[i], p0, p1, p2);
+      *reinterpret_cast<u32x2*>(lds + 0 * NT_PIECE + o) = p0;
+      *reinterpret_cast<u32x2*>(lds + 1 * NT_PIECE + o) = p1;
+      *reinterpret_cast<u32x2*>(lds + 2 * NT_PIECE + o) = p2;
+    }
+#pragma unroll
+    for (int i = 0; i < NT_NLB; ++i) {
+      const int o = (br + 64 * i) * NT_LDK + bk;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(lds + (3 + p) * NT_PIECE + o) = rb[p][i];
+    }
+  };
+  const int g = lane >> 4, li = lane & 15;
+  auto frag = [&](int piece, int row) -> bf16x8 {
+    return *reinterpret_cast<const bf16x8*>(lds + piece * NT_PIECE + (row + li) * NT_LDK + 8 * g);
+  };
+  auto compute = [&]() {
+    bf16x8 a[3][4], b[3][4];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[p][i] = frag(p, wm + 16 * i);
+        b[p][i] = frag(3 + p, wn + 16 * i);
+      }
+    auto pass = [&](const bf16x8 (&x)[4], const bf16x8 (&y)[4]) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[mi], y[ni], acc[mi][ni], 0, 0, 0);
+    };
+    pass(a[2], b[0]);
+    pass(a[1], b[1]);
+    pass(a[0], b[2]);
+    pass(a[1], b[0]);
+    pass(a[0], b[1]);
+    pass(a[0], b[0]);
+  };
+  const int nk = (K + BK - 1) / BK;
+  load_tiles(0);
+  for (int it = 0; it < nk; ++it) {
+    store_tiles();
+    if (it + 1 < nk) load_tiles((it + 1) * BK);
+    __syncthreads();
+    compute();
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const floatx4 v = xt_quad_transpose(acc[mi][ni], lane);
+      const int row = m0 + wm + mi * 16 + g * 4 + (li & 3);
+      const int col = n0 + wn + ni * 16 + (li & ~3);
+      if (row >= M || col >= N) continue;
+      float o[4] = {v[0], v[1], v[2], v[3]};
+      if (EPI == 1) {
+        const float4 x = *reinterpret_cast<const float4*>(D.aux + (size_t)row * D.ldaux + col);
+        o[0] = v[0] * mog_sigmoidf(x.x);
+        o[1] = v[1] * mog_sigmoidf(x.y);
+        o[2] = v[2] * mog_sigmoidf(x.z);
+        o[3] = v[3] * mog_sigmoidf(x.w);
+      }
+      *reinterpret_cast<float4*>(D.C + (size_t)row * D.ldc + col) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+
 }  // namespace
 
 extern "C" int mog_split3_bf16(const float* src, int rows, int cols, int ld_src, void* dst,
@@ -367,5 +534,27 @@ extern "C" int mog_gemm_f32_x3_tn(const float* A, const float* B, float* C, floa
   D.A = A; D.B = B; D.C = C; D.colsum = colsum;
   D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc;
   launch_x3(false, D, splitk, mog_stream(stream));
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_gemm_x3_nt(const float* A, const void* B3, long sb, float* C, const float* aux,
+                              int M, int N, int K, int lda, int ldb, int ldc, int ldaux, int epi,
+                              void* stream) {
+  MOG_CHECK_ARG(A && B3 && C && M >= 0 && N >= 0 && K >= 0 && (epi == 0 || epi == 1));
+  MOG_CHECK_ARG(epi == 0 || (aux && ldaux % 4 == 0 && ldaux >= N && al16(aux)));
+  // 16-byte accesses: float4 rows of A and C (K, N, lda, ldc multiples of 4),
+  // 8-bf16 chunks of the B pieces (ldb, sb multiples of 8)
+  MOG_CHECK_ARG(al16(A) && al16(B3) && al16(C) && K % 4 == 0 && N % 4 == 0 && lda % 4 == 0 &&
+                ldc % 4 == 0 && ldb % 8 == 0 && sb % 8 == 0 && lda >= K && ldb >= K && ldc >= N);
+  if (M == 0 || N == 0) return 0;
+  X3NtArgs D{};
+  D.A = A; D.B3 = reinterpret_cast<const __bf16*>(B3); D.sb = sb; D.C = C; D.aux = aux;
+  D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc; D.ldaux = ldaux;
+  D.nx = mog_cdiv(N, BN);
+  D.ny = mog_cdiv(M, BM);
+  D.epi = epi;
+  const unsigned nwg = (unsigned)D.nx * D.ny;
+  if (epi == 1) gemm_x3_nt_kernel<1><<<nwg, 256, 0, mog_stream(stream)>>>(D);
+  else gemm_x3_nt_kernel<0><<<nwg, 256, 0, mog_stream(stream)>>>(D);
   MOG_LAUNCH_RET();
 }

@@ -867,7 +867,22 @@ void gemm_x3p_tn_(const Tensor& A3, int64_t sa, const Tensor& B3, int64_t sb, Te
         o.name);
 }
 
+void gemm_x3_nt_(const Tensor& A, const Tensor& B3, int64_t sb, Tensor C,
+                 const optional<Tensor>& aux, int64_t M, int64_t N, int64_t K, int64_t lda,
+                 int64_t ldb, int64_t ldc, int64_t ldaux, int64_t epi) {
+  Op o("gemm_x3_nt_");
+  float* c = o.f(C, mat(M, N, ldc), "C");
+  const float* a = o.f(A, mat(M, K, lda), "A");
+  const void* b = o.need(B3, BF16, 2 * sb + mat(N, ldb, ldb), "B3");
+  const float* x = o.f(aux, mat(M, N, ldaux), "aux");
+  GUARD(o);
+  check(mog_gemm_x3_nt(a, b, sb, c, x, M, N, K, lda, ldb, ldc, ldaux, epi, o.stream()), o.name);
+}
+
 TORCH_LIBRARY_FRAGMENT(mog_air, m) {
+  m.def(
+      "gemm_x3_nt_(Tensor A, Tensor B3, int sb, Tensor(a!) C, Tensor? aux, int M, int N, int K, "
+      "int lda, int ldb, int ldc, int ldaux, int epi) -> ()");
   m.def(
       "split3_bf16_(Tensor src, Tensor(a!) dst, int rows, int cols, int ld_src, int ld_dst, "
       "int piece_stride) -> ()");
@@ -1010,6 +1025,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("gemm_f32_sigmoid_philox_", &gemm_f32_sigmoid_philox_);
   m.impl("gemm_f32_x3_tn_", &gemm_f32_x3_tn_);
   m.impl("split3_bf16_", &split3_bf16_);
+  m.impl("gemm_x3_nt_", &gemm_x3_nt_);
   m.impl("gemm_x3p_tn_", &gemm_x3p_tn_);
   m.impl("gemm_bf16_", &gemm_bf16_);
   m.impl("cvt_bf16_batch_", &cvt_bf16_batch_);

@@ -782,15 +782,49 @@ class AIRModel:
     # eager 0.90 -> 1.00 ms, captured 0.60 -> 0.65 ms with them)
     SIDE_MIN_BATCH = 1024
 
+    # fp32 configuration: the VAE input gradients dX = dY W^T of the 256- to
+    # 784-wide layers on the bf16 matrix cores with exact three-piece splits
+    # (gemm_x3.hip NT form: dY split in the kernel, W split once per optimizer
+    # step) -- the chain is on the step's critical path; fp32-level accuracy
+    # like the weight gradients.  MOG_VAE_DX_X3=0: the fp32 MFMA GEMMs.
+    VAE_DX_X3 = os.environ.get("MOG_VAE_DX_X3", "1") == "1"
+    _X3_DX = ("gen_mean", "generative_2", "recognition_2", "recognition_1")
+
+    def _w3(self):
+        """The three bf16 pieces of the VAE weights the x3 input gradients read
+        (W [in][out] -> [3][in][out]), refreshed when the parameters change."""
+        if getattr(self, "_w3_version", None) != self.params.version:
+            if getattr(self, "_w3_buf", None) is None:
+                self._w3_buf = {}
+                for n in self._X3_DX:
+                    I, O = self._P("vae/" + n + "/weights").shape
+                    self._w3_buf[n] = torch.empty((3, I, O), device=self.device,
+                                                  dtype=torch.bfloat16)
+            for n in self._X3_DX:
+                w = self._P("vae/" + n + "/weights")
+                I, O = w.shape
+                ops.split3_bf16(w, self._w3_buf[n], I, O, O, O, I * O)
+            self._w3_version = self.params.version
+        return self._w3_buf
+
+    def _dx(self, dY, name, out, M, N, K, aux=None):
+        """out[M,N] = dY W^T (W = vae/name/weights [N][K]) [* sigmoid(aux)]."""
+        if self.VAE_DX_X3 and K % 8 == 0 and N % 4 == 0:
+            w3 = self._w3()[name]
+            ops.gemm_x3_nt(dY, w3, N * K, out, M, N, K, K, K, N, aux=aux,
+                           ldaux=N if aux is not None else 0)
+            return
+        gemm([dY], [self._P("vae/" + name + "/weights")], [out], M, N, K, K, K, N, transB=True,
+             epi=EPI_SOFTPLUS_BWD if aux is not None else EPI_STORE,
+             aux=[aux] if aux is not None else None, ldaux=N if aux is not None else 0)
+
     def _vae_backward_fp32_all(self, ws, gscale):
         TB = ws.B * self.max_steps
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
         # dm = SigmoidGrad(r, dr) was written by the STN write backward
-        gemm([ws.dm], [vw["gen_mean"]], [ws.dd2], TB, G2, W2, W2, W2, G2,
-             transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d2pre], ldaux=G2)
-        gemm([ws.dd2], [vw["generative_2"]], [ws.dd1], TB, G1, G2, G2, G2, G1,
-             transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d1pre], ldaux=G1)
+        self._dx(ws.dm, "gen_mean", ws.dd2, TB, G2, W2, aux=ws.d2pre)
+        self._dx(ws.dd2, "generative_2", ws.dd1, TB, G1, G2, aux=ws.d1pre)
         gemm([ws.dd1], [vw["generative_1"]], [ws.dz_all], TB, Z, G1, G1, G1, Z, transB=True)
         _ops.vae_sample_backward_(TB, Z, float(self.vae_prior_mean),
                                   float(self.vae_prior_variance), float(gscale), ws.mu, ws.lv,
@@ -798,9 +832,8 @@ class AIRModel:
         gemm([ws.dmu], [vw["rec_mean"]], [ws.tmp_a2_all], TB, R2, Z, Z, Z, R2, transB=True)
         gemm([ws.dlv], [vw["rec_log_variance"]], [ws.da2], TB, R2, Z, Z, Z, R2,
              transB=True, epi=EPI_SOFTPLUS_BWD, Cin=[ws.tmp_a2_all], aux=[ws.a2pre], ldaux=R2)
-        gemm([ws.da2], [vw["recognition_2"]], [ws.da1], TB, R1, R2, R2, R2, R1,
-             transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.a1pre], ldaux=R1)
-        gemm([ws.da1], [vw["recognition_1"]], [ws.dg_all], TB, W2, R1, R1, R1, W2, transB=True)
+        self._dx(ws.da2, "recognition_2", ws.da1, TB, R1, R2, aux=ws.a1pre)
+        self._dx(ws.da1, "recognition_1", ws.dg_all, TB, W2, R1)
 
     def _vae_backward_bf16_all(self, ws, gscale):
         from .ops import BF_SOFTPLUS_BWD, BF_STORE, gemm_bf16
@@ -1355,6 +1388,7 @@ class AIRModel:
         # the weight packs are refreshed by a launch inside the graph on every
         # replay (the parameters change every step): force it to be recorded
         self._pack_version = self._pack32_version = self._w1cat_version = None
+        self._w3_version = None
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         self._global_batch = global_batch

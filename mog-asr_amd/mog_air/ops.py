@@ -80,6 +80,15 @@ def gemm_x3p_tn(A3: torch.Tensor, sa: int, B3: torch.Tensor, sb: int, C: torch.T
                       int(npieces))
 
 
+def gemm_x3_nt(A: torch.Tensor, B3: torch.Tensor, sb: int, C: torch.Tensor, M: int, N: int,
+               K: int, lda: int, ldb: int, ldc: int, aux=None, ldaux: int = 0) -> None:
+    """C[M,N] = A B^T at fp32-level accuracy (A split into three bf16 pieces
+    in the kernel, B given as split3_bf16's pieces of W [N][K]); with aux:
+    C = (A B^T) * sigmoid(aux) (the softplus backward) -- mog_gemm_x3_nt."""
+    _ops.gemm_x3_nt_(A, B3, int(sb), C, aux, M, N, K, lda, ldb, ldc, int(ldaux),
+                     1 if aux is not None else 0)
+
+
 def gemm_sigmoid_philox(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias, M: int, N: int,
                         K: int, lda: int, ldb: int, ldc: int, scale: float, seed: int,
                         offset: int) -> None:

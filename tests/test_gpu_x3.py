@@ -110,7 +110,7 @@ def test_x3_fp32_step_gradients_match_chain():
                      z_pres_prior_log_odds=-0.01, cnn=False, train=True, scope="x3",
                      device=DEV, precision="fp32", seed=3, noise_seed=4)
         m.X_GRAD_X3 = x3
-        m.VAE_WGRAD_X3 = x3 != 0  # (the VAE weight gradients' x3 form rides along)
+        m.VAE_WGRAD_X3 = m.VAE_DX_X3 = x3 != 0  # (the VAE gradients' x3 forms ride along)
         grads.append({k: torch.as_tensor(np.asarray(v), dtype=torch.float64)
                       for k, v in m.compute_gradients(x).items()})
     for g in grads[:2]:
@@ -161,3 +161,30 @@ def test_x3_asr_step_gradients_match_chain():
         a, b = grads[0][k], grads[1][k]
         scale = b.abs().max().item() + 1e-30
         assert (a - b).abs().max().item() <= 1e-5 * scale, k
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(777, 512, 784, 1), (300, 784, 512, 0), (129, 256, 512, 1),
+                                       (64, 512, 256, 1), (5, 4, 8, 0)])
+def test_x3_nt_accuracy(M, N, K, epi):
+    """mog_gemm_x3_nt (the VAE input gradients dY W^T, optional softplus
+    backward) against float64: error <= 1e-6 of |A||B|^T (the fp32 chain's
+    level; test_x3_accuracy's gate) with ragged M / N tiles."""
+    from mog_air import ops
+    rng = np.random.default_rng(M + N + K)
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    W = (rng.standard_normal((N, K)) * np.exp2(rng.integers(-6, 6, (N, 1)))).astype(np.float32)
+    aux = rng.standard_normal((M, N)).astype(np.float32)
+    At, Wt = torch.as_tensor(A).to(DEV), torch.as_tensor(W).to(DEV)
+    W3 = torch.empty((3, N, K), device=DEV, dtype=torch.bfloat16)
+    ops.split3_bf16(Wt, W3, N, K, K, K, N * K)
+    C = torch.full((M, N), float("nan"), device=DEV)
+    ops.gemm_x3_nt(At, W3, N * K, C, M, N, K, K, K, N,
+                   aux=torch.as_tensor(aux).to(DEV) if epi else None, ldaux=N if epi else 0)
+    ref = A.astype(np.float64) @ W.astype(np.float64).T
+    bound = np.abs(A).astype(np.float64) @ np.abs(W).astype(np.float64).T
+    if epi:
+        sig = 1.0 / (1.0 + np.exp(-aux.astype(np.float64)))
+        ref, bound = ref * sig, bound * sig
+    err = np.abs(C.cpu().numpy().astype(np.float64) - ref)
+    assert np.isfinite(C.cpu().numpy()).all()
+    assert (err <= 1e-6 * bound + 1e-30).all(), float((err / (bound + 1e-30)).max())
