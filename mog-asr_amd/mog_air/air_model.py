@@ -87,7 +87,12 @@ def marginal_objective(num_prior, max_steps) -> np.ndarray:
 
 
 class _Workspace:
-    """All per-batch device buffers of one train step (HBM-resident, reused)."""
+    """All per-batch device buffers of one train step (HBM-resident, reused).
+    Buffers in ZERO_PADDED carry zero pad columns written once at allocation
+    (the bf16 latents' 50 -> 56 columns: the K padding of the GEMMs that read
+    them); every other element is written by the step before it is read."""
+
+    ZERO_PADDED = ("zb", "dmub", "dlvb", "Xb")
 
     def __init__(self, m: "AIRModel", B: int):
         dev = m.device
@@ -809,7 +814,7 @@ class AIRModel:
 
     def _dx(self, dY, name, out, M, N, K, aux=None):
         """out[M,N] = dY W^T (W = vae/name/weights [N][K]) [* sigmoid(aux)]."""
-        if self.VAE_DX_X3 and K % 8 == 0 and N % 4 == 0:
+        if self.VAE_DX_X3 and K % 8 == 0 and N % 4 == 0 and M >= self.X3_MIN_ROWS:
             w3 = self._w3()[name]
             ops.gemm_x3_nt(dY, w3, N * K, out, M, N, K, K, K, N, aux=aux,
                            ldaux=N if aux is not None else 0)
@@ -904,10 +909,8 @@ class AIRModel:
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
         _ops.sigmoid_backward_(ws.r[t], ws.dr, ws.dm[t], B * W2)
-        gemm([ws.dm[t]], [vw["gen_mean"]], [ws.dd2[t]], B, G2, W2, W2, W2, G2,
-             transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d2pre[t]], ldaux=G2)
-        gemm([ws.dd2[t]], [vw["generative_2"]], [ws.dd1[t]], B, G1, G2, G2, G2, G1,
-             transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.d1pre[t]], ldaux=G1)
+        self._dx(ws.dm[t], "gen_mean", ws.dd2[t], B, G2, W2, aux=ws.d2pre[t])
+        self._dx(ws.dd2[t], "generative_2", ws.dd1[t], B, G1, G2, aux=ws.d1pre[t])
         gemm([ws.dd1[t]], [vw["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z, transB=True)
         self._dz_hook(ws, t)
         _ops.vae_sample_backward_(B, Z, float(self.vae_prior_mean),
@@ -917,9 +920,8 @@ class AIRModel:
         gemm([ws.dmu[t]], [vw["rec_mean"]], [ws.tmp_a2], B, R2, Z, Z, Z, R2, transB=True)
         gemm([ws.dlv[t]], [vw["rec_log_variance"]], [ws.da2[t]], B, R2, Z, Z, Z, R2,
              transB=True, epi=EPI_SOFTPLUS_BWD, Cin=[ws.tmp_a2], aux=[ws.a2pre[t]], ldaux=R2)
-        gemm([ws.da2[t]], [vw["recognition_2"]], [ws.da1[t]], B, R1, R2, R2, R2, R1,
-             transB=True, epi=EPI_SOFTPLUS_BWD, aux=[ws.a1pre[t]], ldaux=R1)
-        gemm([ws.da1[t]], [vw["recognition_1"]], [ws.dg], B, W2, R1, R1, R1, W2, transB=True)
+        self._dx(ws.da2[t], "recognition_2", ws.da1[t], B, R1, R2, aux=ws.a1pre[t])
+        self._dx(ws.da1[t], "recognition_1", ws.dg, B, W2, R1)
 
     # bf16 configuration: VAE GEMM operands bf16 (fp32 accumulate), activations
     # stored bf16 (post-activation only: softplus' = 1 - exp(-softplus)), the
@@ -1097,9 +1099,14 @@ class AIRModel:
     # DESIGN.md §4.4); MOG_VAE_WGRAD_X3=0 keeps them on the fp32 split-K GEMM
     VAE_WGRAD_X3 = os.environ.get("MOG_VAE_WGRAD_X3", "1") == "1"
 
+    # the x3 forms from this many rows: below it (the reference's batch of 64:
+    # 192 rows) their 128 x 128 tiles leave most CUs idle, and the fp32 GEMMs'
+    # small-M tiles finish first
+    X3_MIN_ROWS = 2048
+
     def _dw_x3(self, X, dY, out, K, M, N, lda, ldb, bias_out):
         """out[M,N] += X^T dY over K rows (gemm_x3_tn), bias_out += colsum(dY)."""
-        if not (self.VAE_WGRAD_X3 and M % 4 == 0 and N % 4 == 0):
+        if not (self.VAE_WGRAD_X3 and M % 4 == 0 and N % 4 == 0 and K >= self.X3_MIN_ROWS):
             return self._dw(X, dY, out, K, M, N, lda, ldb, bias_out)
         tiles = ((M + 127) // 128) * ((N + 127) // 128)
         splitk = max(1, min(K // 256, (512 + tiles - 1) // tiles))
@@ -1126,6 +1133,15 @@ class AIRModel:
         else:
             self._vae_weight_grads_fp32(ws)
         self._weight_grads_heads(ws)
+
+    MAIN_PRIORITY = os.environ.get("MOG_MAIN_PRIO", "0") == "1"
+
+    def _hp_stream(self):
+        if getattr(self, "_hp", None) is None:
+            lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") \
+                else (0, -1)
+            self._hp = torch.cuda.Stream(device=self.device, priority=min(lo, hi))
+        return self._hp
 
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
@@ -1291,13 +1307,25 @@ class AIRModel:
         X, tg = self._prep(images, targets)
         ws = self._workspace(X.shape[0])
         ws.alloc_backward(self)
-        self._fill_noise(ws, noise)
-        self._global_batch = global_batch
-        self._forward(X, tg, ws, need_grad=True, outputs=False)
-        self._backward(X, ws)
-        if self.grad_reducer is not None:
-            self.grad_reducer.wait()
-        self.params.apply_adam(self.hyper("learning_rate"), self.gradient_clipping_norm)
+        hp = None
+        if self.MAIN_PRIORITY and not self._graph_mode and ws.B >= self.SIDE_MIN_BATCH:
+            # the step's critical chain on a high-priority stream: the side
+            # stream's throughput GEMMs (weight gradients) then take the CUs
+            # the latency-bound chain (STN read backward, heads, LSTM chain,
+            # recurrent dh GEMMs) leaves free, instead of starving it
+            cur = torch.cuda.current_stream()
+            hp = self._hp_stream()
+            hp.wait_stream(cur)
+        with torch.cuda.stream(hp) if hp is not None else contextlib.nullcontext():
+            self._fill_noise(ws, noise)
+            self._global_batch = global_batch
+            self._forward(X, tg, ws, need_grad=True, outputs=False)
+            self._backward(X, ws)
+            if self.grad_reducer is not None:
+                self.grad_reducer.wait()
+            self.params.apply_adam(self.hyper("learning_rate"), self.gradient_clipping_norm)
+        if hp is not None:
+            cur.wait_stream(hp)
         self.params.global_step += 1
         self._X = X
 

@@ -103,7 +103,9 @@ def test_x3_fp32_step_gradients_match_chain():
     fp32 chain, agree to fp32 level (every gradient)."""
     from mog_air.air_model import AIRModel
     rng = np.random.default_rng(5)
-    x = (rng.uniform(size=(256, 2500)) * (rng.uniform(size=(256, 2500)) < 0.3)).astype(np.float32)
+    # 1024 images: 3072 rows, past AIRModel.X3_MIN_ROWS, so the VAE's x3
+    # weight and input gradients run too
+    x = (rng.uniform(size=(1024, 2500)) * (rng.uniform(size=(1024, 2500)) < 0.3)).astype(np.float32)
     grads = []
     for x3 in (1, 2, 0):
         m = AIRModel(max_steps=3, max_digits=3, canvas_size=50, scale_prior_variance=0.05,
@@ -111,6 +113,7 @@ def test_x3_fp32_step_gradients_match_chain():
                      device=DEV, precision="fp32", seed=3, noise_seed=4)
         m.X_GRAD_X3 = x3
         m.VAE_WGRAD_X3 = m.VAE_DX_X3 = x3 != 0  # (the VAE gradients' x3 forms ride along)
+        assert 3 * 1024 >= m.X3_MIN_ROWS
         grads.append({k: torch.as_tensor(np.asarray(v), dtype=torch.float64)
                       for k, v in m.compute_gradients(x).items()})
     for g in grads[:2]:
