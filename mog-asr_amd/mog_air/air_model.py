@@ -814,7 +814,7 @@ class AIRModel:
 
     def _dx(self, dY, name, out, M, N, K, aux=None):
         """out[M,N] = dY W^T (W = vae/name/weights [N][K]) [* sigmoid(aux)]."""
-        if self.VAE_DX_X3 and K % 8 == 0 and N % 4 == 0 and M >= self.X3_MIN_ROWS:
+        if self.VAE_DX_X3 and K % 8 == 0 and N % 4 == 0 and M >= self.X3_DX_MIN_ROWS:
             w3 = self._w3()[name]
             ops.gemm_x3_nt(dY, w3, N * K, out, M, N, K, K, K, N, aux=aux,
                            ldaux=N if aux is not None else 0)
@@ -1103,6 +1103,11 @@ class AIRModel:
     # 192 rows) their 128 x 128 tiles leave most CUs idle, and the fp32 GEMMs'
     # small-M tiles finish first
     X3_MIN_ROWS = 2048
+    # the NT input-gradient form from this many rows (the AIR step's T*B =
+    # 24,576): at the ASR step's per-step 8,192 rows its 128 x 128 tiles give
+    # one workgroup per CU and the fp32 GEMM is faster (ASR fp32 step 9.6 ->
+    # 10.1 ms with it)
+    X3_DX_MIN_ROWS = 16384
 
     def _dw_x3(self, X, dY, out, K, M, N, lda, ldb, bias_out):
         """out[M,N] += X^T dY over K rows (gemm_x3_tn), bias_out += colsum(dY)."""

@@ -171,15 +171,18 @@ def _copy_state(dst, src):
     dst._noise_ctr = src._noise_ctr
 
 
-def _grad_close(ga, gb, rel=1e-4):
+def _grad_close(ga, gb, rel=1e-4, rel_small=1e-3):
     """Per tensor: max |a - b| <= rel * max |a| (split-K atomics reorder the
-    weight-gradient sums from B = 1024 on)."""
+    weight-gradient sums from B = 1024 on); tensors of at most 64 elements
+    (biases of 1-2 wide output layers: one sum of thousands of cancelling
+    terms each) to rel_small."""
     bad = []
     for name in ga:
         a, b = ga[name], gb[name]
         scale = float(np.abs(a).max())
         err = float(np.abs(a - b).max())
-        if err > rel * max(scale, 1e-30):
+        tol = rel_small if a.size <= 64 else rel
+        if err > tol * max(scale, 1e-30):
             bad.append((name, err, scale))
     assert not bad, bad[:5]
 
