@@ -43,6 +43,11 @@ enum {
 };
 
 constexpr int MAXB = 8;
+}  // namespace
+int mog_internal_gemm_tn_small(int batch, const float* const* A, const float* const* B,
+                               float* const* C, float* const* colsum, int M, int N, int K,
+                               int lda, int ldb, int ldc, hipStream_t stream);
+namespace {
 struct GemmPtrs {
   const float* A[MAXB];
   const float* B[MAXB];
@@ -982,6 +987,14 @@ extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const
   D.kseg = 0;
   D.eps_gen = 0;
   D.eps_seed = D.eps_off = 0;
+  // the 1- / 2-wide weight gradients (N <= 16, M <= 256): the LDS-free kernel
+  // of gemm_tn_small.hip, which picks its own K chunks (MOG_TN_SMALL=0: the
+  // tiled kernels below)
+  static const char* tn_env = getenv("MOG_TN_SMALL");
+  static const bool tn_small = tn_env == nullptr || atoi(tn_env) != 0;
+  if (tn_small && transA && !transB && epi == EPI_ATOMIC && M <= 256 && N <= 16 && K > 0)
+    return mog_internal_gemm_tn_small(batch, P.A, P.B, P.C, colsum ? P.colsum : nullptr, M, N,
+                                      K, lda, ldb, ldc, mog_stream(stream));
   MOG_TRY(launch_auto(transA, transB, epi, mog_stream(stream), P, D, batch));
   MOG_LAUNCH_RET();
 }

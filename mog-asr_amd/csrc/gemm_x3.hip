@@ -20,14 +20,22 @@
 // transpose read ds_read_b64_tr_b16 (as the TN form of gemm_bf16.hip).  One
 // LDS stage, register prefetch of the next k-tile, two workgroups per CU.
 //
-// Measured (scripts/x3_time.py, M 2500 x N 1024 x K 8192 with the column sums):
-// 318 us at split-K 8 against 410 us for the fp32 MFMA split-K GEMM; inside the
-// fp32 train step no change (3.433 vs 3.434 ms: the x-part gradient shares the
-// chip with the side-stream weight gradients), so the model keeps the fp32
-// chain by default (AIRModel.X_GRAD_X3, MOG_X_GRAD_X3=1 selects this form).
-// MFMA is ~38 % busy here: the per-workgroup split (7 VALU per element, each
-// A tile split again by every workgroup of its row panel) is the next cost.
+// Three forms (measured on MI355X, scripts/x3_lib_bench.py, us; fp32-level
+// accuracy gated in tests/test_gpu_x3.py):
+//   * gemm_x3_tn_kernel<false>: the split inside the GEMM (7 VALU per
+//     element, every workgroup of a row panel re-splits its A tile) -- the
+//     fp32 VAE weight gradients (AIRModel._dw_x3): 239 us at 784 x 512 x 24,576
+//     rows against 166 us pre-split;
+//   * gemm_x3_tn_kernel<true>: operands split once by mog_split3_bf16 -- the
+//     LSTM x-rows gradient X^T dG (AIR and ASR, the default MOG_X_GRAD_X3=2):
+//     251 us at 2500 x 1024 x 8192 (343 us split in-kernel);
+//   * gemm_x3_nt_kernel (below): dX = dY W^T, dY split in-kernel, W split once
+//     per optimizer step -- the fp32 VAE input-gradient chain: 161 / 184 us at
+//     24,576 x 512 x 784 / 24,576 x 784 x 512 (hipBLASLt fp32 176 / 222 us).
+// MFMA is under half busy in every form (0.26-0.41 of the bf16 peak): the
+// one-stage, register-staged pipeline is the next cost.
 #include <cstdlib>
+#include <type_traits>
 
 #include "mog_common.h"
 
@@ -373,7 +381,10 @@ __device__ __forceinline__ floatx4 xt_quad_transpose(const floatx4& a, int lane)
   return floatx4{r0, r1, r2, r3};
 }
 
-template <int EPI>  // 0 store, 1 softplus backward
+// EPI: 0 store, 1 softplus backward.  PD: k-tiles of prefetch in registers
+// (1: the next k-tile's loads in flight under the MFMAs; 2: two register sets,
+// each k-tile's loads issued two MFMA phases before its split and store)
+template <int EPI, int PD>
 __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[NT_STAGE];
   const int nwg = gridDim.x;
@@ -392,36 +403,49 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
-  float4 ra[NT_NLA];
-  u32x4 rb[3][NT_NLB];
+  float4 ra[PD][NT_NLA];
+  u32x4 rb[PD][3][NT_NLB];
   const float4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const u32x4 z4 = {0u, 0u, 0u, 0u};
-  auto load_tiles = [&](int k0) {
+  // Buffer loads: the workgroup's A rows and the B pieces behind two
+  // descriptors, one 32-bit offset register per thread and operand (the row /
+  // piece / k-tile steps are uniform: scalar offsets).  A rows >= M fall
+  // outside A's record range and load 0; k >= K (the last k-tile, K % 32 != 0)
+  // is zeroed after the load on both operands (with lda == K those addresses
+  // hold the next row).  B rows >= N load the next piece's rows or 0 past the
+  // last piece: they only reach output columns >= N, which are not stored.
+  const __amdgpu_buffer_rsrc_t arsc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(D.A) + (size_t)m0 * D.lda, 0, min(M - m0, BM) * D.lda * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t brsc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__bf16*>(D.B3), 0, (int)((2 * D.sb + (long)N * D.ldb) * 2), 0x00020000);
+  const int avo = (ar * D.lda + ak) * 4;
+  const int bvo = ((n0 + br) * D.ldb + bk) * 2;
+  auto load_tiles = [&](int k0, auto sc) {
+    constexpr int s = decltype(sc)::value;
+    const bool ka = k0 + ak < K, kb = k0 + bk < K;
 #pragma unroll
     for (int i = 0; i < NT_NLA; ++i) {
-      const int gm = m0 + ar + 32 * i, gk = k0 + ak;
-      // K % 4 == 0: a float4 is wholly inside or outside the k range
-      ra[i] = (gm < M && gk < K) ? *reinterpret_cast<const float4*>(D.A + (size_t)gm * D.lda + gk)
-                                 : zero4;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(arsc, avo, (32 * i * D.lda + k0) * 4, 0);
+      ra[s][i] = ka ? float4{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                             __uint_as_float(v[3])}
+                    : zero4;
     }
 #pragma unroll
-    for (int i = 0; i < NT_NLB; ++i) {
-      const int gn = n0 + br + 64 * i, gk = k0 + bk;
-      // ldb % 8 == 0 and the pieces are zero past K: a chunk starting below
-      // K stays inside the row
+    for (int i = 0; i < NT_NLB; ++i)
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
-        rb[p][i] = (gn < N && gk < K)
-                       ? *reinterpret_cast<const u32x4*>(D.B3 + p * D.sb + (size_t)gn * D.ldb + gk)
-                       : z4;
-    }
+      for (int p = 0; p < 3; ++p) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+            brsc, bvo, (int)((p * D.sb + (long)64 * i * D.ldb + k0) * 2), 0);
+        rb[s][p][i] = kb ? v : z4;
+      }
   };
-  auto store_tiles = [&]() {
+  auto store_tiles = [&](auto sc) {
+    constexpr int s = decltype(sc)::value;
 #pragma unroll
     for (int i = 0; i < NT_NLA; ++i) {
       const int o = (ar + 32 * i) * NT_LDK + ak;
       u32x2 p0, p1, p2;
-      split4(ra[i], p0, p1, p2);
+      split4(ra[s][i], p0, p1, p2);
       *reinterpret_cast<u32x2*>(lds + 0 * NT_PIECE + o) = p0;
       *reinterpret_cast<u32x2*>(lds + 1 * NT_PIECE + o) = p1;
       *reinterpret_cast<u32x2*>(lds + 2 * NT_PIECE + o) = p2;
@@ -430,22 +454,22 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
     for (int i = 0; i < NT_NLB; ++i) {
       const int o = (br + 64 * i) * NT_LDK + bk;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(lds + (3 + p) * NT_PIECE + o) = rb[p][i];
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(lds + (3 + p) * NT_PIECE + o) = rb[s][p][i];
     }
   };
   const int g = lane >> 4, li = lane & 15;
   auto frag = [&](int piece, int row) -> bf16x8 {
     return *reinterpret_cast<const bf16x8*>(lds + piece * NT_PIECE + (row + li) * NT_LDK + 8 * g);
   };
+  // the B pieces held for the whole k-tile, the A pieces one at a time
+  // (smallest first: a2 b0; a1 b1, a1 b0; a0 b2, a0 b1, a0 b0): 64 fragment
+  // registers live instead of 96
   auto compute = [&]() {
-    bf16x8 a[3][4], b[3][4];
+    bf16x8 b[3][4];
 #pragma unroll
     for (int p = 0; p < 3; ++p)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[p][i] = frag(p, wm + 16 * i);
-        b[p][i] = frag(3 + p, wn + 16 * i);
-      }
+      for (int i = 0; i < 4; ++i) b[p][i] = frag(3 + p, wn + 16 * i);
     auto pass = [&](const bf16x8 (&x)[4], const bf16x8 (&y)[4]) {
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
@@ -453,21 +477,41 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
         for (int ni = 0; ni < 4; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[mi], y[ni], acc[mi][ni], 0, 0, 0);
     };
-    pass(a[2], b[0]);
-    pass(a[1], b[1]);
-    pass(a[0], b[2]);
-    pass(a[1], b[0]);
-    pass(a[0], b[1]);
-    pass(a[0], b[0]);
+#pragma unroll
+    for (int pa = 2; pa >= 0; --pa) {
+      bf16x8 a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = frag(pa, wm + 16 * i);
+#pragma unroll
+      for (int pb = 2 - pa; pb >= 0; --pb) pass(a, b[pb]);
+    }
   };
   const int nk = (K + BK - 1) / BK;
-  load_tiles(0);
-  for (int it = 0; it < nk; ++it) {
-    store_tiles();
-    if (it + 1 < nk) load_tiles((it + 1) * BK);
-    __syncthreads();
-    compute();
-    __syncthreads();
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, PD - 1>;
+  if constexpr (PD == 1) {
+    load_tiles(0, S0{});
+    for (int it = 0; it < nk; ++it) {
+      store_tiles(S0{});
+      if (it + 1 < nk) load_tiles((it + 1) * BK, S0{});
+      __syncthreads();
+      compute();
+      __syncthreads();
+    }
+  } else {
+    load_tiles(0, S0{});
+    if (nk > 1) load_tiles(BK, S1{});
+    auto body = [&](int it, auto sc) {
+      store_tiles(sc);
+      if (it + 2 < nk) load_tiles((it + 2) * BK, sc);
+      __syncthreads();
+      compute();
+      __syncthreads();
+    };
+    for (int it = 0; it < nk; it += 2) {
+      body(it, S0{});
+      if (it + 1 < nk) body(it + 1, S1{});
+    }
   }
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
@@ -546,6 +590,8 @@ extern "C" int mog_gemm_x3_nt(const float* A, const void* B3, long sb, float* C,
   // 8-bf16 chunks of the B pieces (ldb, sb multiples of 8)
   MOG_CHECK_ARG(al16(A) && al16(B3) && al16(C) && K % 4 == 0 && N % 4 == 0 && lda % 4 == 0 &&
                 ldc % 4 == 0 && ldb % 8 == 0 && sb % 8 == 0 && lda >= K && ldb >= K && ldc >= N);
+  // 32-bit buffer offsets: the pieces and one 128-row panel of A
+  MOG_CHECK_ARG((2 * sb + (long)N * ldb) * 2 < (1L << 31) && (long)BM * lda * 4 < (1L << 31));
   if (M == 0 || N == 0) return 0;
   X3NtArgs D{};
   D.A = A; D.B3 = reinterpret_cast<const __bf16*>(B3); D.sb = sb; D.C = C; D.aux = aux;
@@ -554,7 +600,14 @@ extern "C" int mog_gemm_x3_nt(const float* A, const void* B3, long sb, float* C,
   D.ny = mog_cdiv(M, BM);
   D.epi = epi;
   const unsigned nwg = (unsigned)D.nx * D.ny;
-  if (epi == 1) gemm_x3_nt_kernel<1><<<nwg, 256, 0, mog_stream(stream)>>>(D);
-  else gemm_x3_nt_kernel<0><<<nwg, 256, 0, mog_stream(stream)>>>(D);
+  static const int pd = getenv("MOG_X3NT_PD") ? atoi(getenv("MOG_X3NT_PD")) : 1;
+  hipStream_t s = mog_stream(stream);
+  if (pd == 2) {
+    if (epi == 1) gemm_x3_nt_kernel<1, 2><<<nwg, 256, 0, s>>>(D);
+    else gemm_x3_nt_kernel<0, 2><<<nwg, 256, 0, s>>>(D);
+  } else {
+    if (epi == 1) gemm_x3_nt_kernel<1, 1><<<nwg, 256, 0, s>>>(D);
+    else gemm_x3_nt_kernel<0, 1><<<nwg, 256, 0, s>>>(D);
+  }
   MOG_LAUNCH_RET();
 }

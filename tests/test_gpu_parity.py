@@ -92,6 +92,42 @@ def test_gemm_splitk_atomic():
                                atol=2e-3)
 
 
+@pytest.mark.parametrize("M,N,K,lda,ldb,nb", [(256, 50, 24576, 256, 50, 2), (50, 256, 3001, 52, 260, 1),
+                                              (64, 1, 24576, 64, 2, 3), (64, 2, 777, 64, 2, 2),
+                                              (64, 2, 192, 64, 2, 2), (256, 64, 8192, 256, 320, 5),
+                                              (17, 13, 200, 20, 16, 1)])
+def test_gemm_tn_small_weight_gradients(M, N, K, lda, ldb, nb):
+    """The split-K weight gradients of the narrow layers (transA + atomic; N
+    <= 16 is routed to gemm_tn_small.hip): batched, with strides and column
+    sums, against float64; gemm_tn_small's single K chunk (K < 256) is
+    deterministic."""
+    from mog_air import ops
+    rng = np.random.default_rng(40 + M + N)
+    A = [rng.standard_normal((K, lda)).astype(np.float32) for _ in range(nb)]
+    Bm = [rng.standard_normal((K, ldb)).astype(np.float32) for _ in range(nb)]
+    Ad, Bd = [_cuda(a) for a in A], [_cuda(b) for b in Bm]
+
+    def run():
+        out = [torch.full((M, N), 0.5, device=DEV) for _ in range(nb)]
+        cs = [torch.full((N,), -1.0, device=DEV) for _ in range(nb)]
+        ops.gemm(Ad, Bd, out, M, N, K, lda, ldb, N, transA=True, epi=ops.EPI_ATOMIC,
+                 splitk=8, colsum=cs)
+        return [o.cpu().numpy() for o in out], [c.cpu().numpy() for c in cs]
+
+    out, cs = run()
+    for i in range(nb):
+        ref = A[i][:, :M].astype(np.float64).T @ Bm[i][:, :N] + 0.5
+        mag = np.abs(A[i][:, :M]).astype(np.float64).T @ np.abs(Bm[i][:, :N])
+        assert (np.abs(out[i] - ref) <= 1e-6 * mag + 1e-6).all()
+        csr = Bm[i][:, :N].astype(np.float64).sum(0) - 1.0
+        assert (np.abs(cs[i] - csr) <= 1e-6 * np.abs(Bm[i][:, :N]).sum(0) + 1e-6).all()
+    if K < 256 and N <= 16:
+        out2, cs2 = run()
+        for i in range(nb):
+            np.testing.assert_array_equal(out[i], out2[i])
+            np.testing.assert_array_equal(cs[i], cs2[i])
+
+
 def test_stn_forward_bit_exact():
     from mog_air import ops
     rng = np.random.default_rng(5)

@@ -104,23 +104,32 @@ def test_x3_fp32_step_gradients_match_chain():
     from mog_air.air_model import AIRModel
     rng = np.random.default_rng(5)
     # 1024 images: 3072 rows, past AIRModel.X3_MIN_ROWS, so the VAE's x3
-    # weight and input gradients run too
+    # weight gradients run too; the input gradients' NT form is let in from
+    # 2048 rows here (the model gates it at X3_DX_MIN_ROWS)
     x = (rng.uniform(size=(1024, 2500)) * (rng.uniform(size=(1024, 2500)) < 0.3)).astype(np.float32)
     grads = []
-    for x3 in (1, 2, 0):
+    for x3 in (1, 2, 0, 0):
         m = AIRModel(max_steps=3, max_digits=3, canvas_size=50, scale_prior_variance=0.05,
                      z_pres_prior_log_odds=-0.01, cnn=False, train=True, scope="x3",
                      device=DEV, precision="fp32", seed=3, noise_seed=4)
         m.X_GRAD_X3 = x3
         m.VAE_WGRAD_X3 = m.VAE_DX_X3 = x3 != 0  # (the VAE gradients' x3 forms ride along)
+        m.X3_DX_MIN_ROWS = 2048
         assert 3 * 1024 >= m.X3_MIN_ROWS
         grads.append({k: torch.as_tensor(np.asarray(v), dtype=torch.float64)
                       for k, v in m.compute_gradients(x).items()})
-    for g in grads[:2]:
+    # fp32-level agreement per tensor, in the 2-norm (the forms differ by
+    # summation order -- split-K atomics, three-piece products -- and the
+    # differences travel the whole backward chain, where gradients that are
+    # sums with heavy cancellation, e.g. the heads' bias column sums, move by
+    # ~1e-5 of their largest entry even between two runs of the fp32 chain),
+    # plus a loose elementwise bound
+    for g in (grads[0], grads[1], grads[3]):  # (the last: the chain against itself)
         for k in g:
             a, b = g[k], grads[2][k]
-            scale = b.abs().max().item() + 1e-30
-            assert (a - b).abs().max().item() <= 1e-5 * scale, k
+            nb = b.norm().item() + 1e-30
+            assert (a - b).norm().item() <= 2e-5 * nb, k
+            assert (a - b).abs().max().item() <= 1e-4 * (b.abs().max().item() + 1e-30), k
 
 
 @pytest.mark.parametrize("M,N,K,m0,splitk", [(2500, 1024, 4096, 0, 8), (580, 1024, 777, 1920, 1),
