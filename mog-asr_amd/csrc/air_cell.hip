@@ -51,16 +51,26 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
   if (idx >= (long)B * H) return;
   const int b = idx / H, u = idx - (long)b * H;
   const float* g = G + (size_t)b * 4 * H;
+  // every load up front and unconditional, the optional operands read
+  // through a valid stand-in pointer and selected away (a load under `p ? ..`
+  // compiles to a branch with a vmcnt(0) wait inside; the dGsum loads would
+  // otherwise wait behind the dG stores, which the compiler must assume alias)
+  const float* bp = bias ? bias : G;
+  const float* cp = c_prev ? c_prev : c_cur;
+  const float* dp = dc ? dc : dh;
+  float* sp = dGsum ? dGsum + (size_t)b * 4 * H : dG + (size_t)b * 4 * H;
   float gi = g[u], gj = g[H + u], gf = g[2 * H + u], go = g[3 * H + u];
+  const float bi = bp[u], bj = bp[H + u], bf = bp[2 * H + u], bo = bp[3 * H + u];
+  const float cpv = cp[idx], ctv = c_cur[idx], dhv = dh[idx], dcv = dp[idx];
+  const float s0 = sp[u], s1 = sp[H + u], s2 = sp[2 * H + u], s3 = sp[3 * H + u];
   if (bias) {
-    gi = gi + bias[u]; gj = gj + bias[H + u]; gf = gf + bias[2 * H + u]; go = go + bias[3 * H + u];
+    gi = gi + bi; gj = gj + bj; gf = gf + bf; go = go + bo;
   }
   const float si = mog_sigmoidf(gi), tj = mog_tanhf(gj), sf = mog_sigmoidf(gf + 1.0f);
   const float so = mog_sigmoidf(go);
-  const float c0 = c_prev ? c_prev[idx] : 0.0f;
-  const float tc = mog_tanhf(c_cur[idx]);
-  const float dhv = dh[idx];
-  const float dct = (dc ? dc[idx] : 0.0f) + dhv * so * (1.0f - tc * tc);
+  const float c0 = c_prev ? cpv : 0.0f;
+  const float tc = mog_tanhf(ctv);
+  const float dct = (dc ? dcv : 0.0f) + dhv * so * (1.0f - tc * tc);
   const float dgo = dhv * tc * so * (1.0f - so);
   const float dgf = dct * c0 * sf * (1.0f - sf);
   const float dgi = dct * tj * si * (1.0f - si);
@@ -68,8 +78,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
   float* d = dG + (size_t)b * 4 * H;
   d[u] = dgi; d[H + u] = dgj; d[2 * H + u] = dgf; d[3 * H + u] = dgo;
   if (dGsum) {
-    float* s = dGsum + (size_t)b * 4 * H;
-    s[u] += dgi; s[H + u] += dgj; s[2 * H + u] += dgf; s[3 * H + u] += dgo;
+    sp[u] = s0 + dgi; sp[H + u] = s1 + dgj; sp[2 * H + u] = s2 + dgf; sp[3 * H + u] = s3 + dgo;
   }
   if (dc_prev) dc_prev[idx] = dct * sf;
 }
@@ -399,12 +408,12 @@ __global__ __launch_bounds__(256) void heads_hidden_bwd4_kernel(HeadPtrs hp, con
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int l = l0 + e;
-    float a = 0.0f;
-    if (hv[e] > 0.0f) {
-      a = d0 * w[l * k];
-      if (k == 2) a += d1 * w[l * k + 1];
-    }
-    v[e] = a;
+    // weights loaded unconditionally (a load under the relu test compiles to
+    // a branch with a vmcnt(0) wait inside); same arithmetic where h > 0
+    const float w0 = w[l * k], w1 = w[l * k + (k == 2 ? 1 : 0)];
+    float a = d0 * w0;
+    if (k == 2) a += d1 * w1;
+    v[e] = hv[e] > 0.0f ? a : 0.0f;
   }
   const long rs = dhid_hs == HS ? 5L * HS : HS;
   *reinterpret_cast<float4*>(dhid + zh * dhid_hs + (size_t)b * rs + l0) =

@@ -605,8 +605,11 @@ __global__ __launch_bounds__(256) void asr_step_bwd_kernel(AsrCfg cfg, AsrW W, A
   // scale hidden layers: dpre6/7 and their contribution to the shift latent
   const size_t rq = (size_t)bc * HS + q;
   const float dcm = sv[m][4], dclv = sv[m][5];
-  const float d6 = hp.h[6][rq] > 0.0f ? dcm * W.w[W_IC1][q] : 0.0f;
-  const float d7 = hp.h[7][rq] > 0.0f ? dclv * W.w[W_IC3][q] : 0.0f;
+  // operands loaded unconditionally (a load under the relu test compiles to
+  // a branch with a vmcnt(0) wait inside); same arithmetic where h > 0
+  const float w6 = W.w[W_IC1][q], w7 = W.w[W_IC3][q];
+  const float d6 = hp.h[6][rq] > 0.0f ? dcm * w6 : 0.0f;
+  const float d7 = hp.h[7][rq] > 0.0f ? dclv * w7 : 0.0f;
   if (ok) {
     io.dpre[6][rq] = d6;
     io.dpre[7][rq] = d7;
@@ -648,12 +651,23 @@ __global__ __launch_bounds__(256) void asr_step_bwd_kernel(AsrCfg cfg, AsrW W, A
   __syncthreads();
   if (!ok) return;
   const float* v = sv[m];
-  io.dpre[0][rq] = hp.h[0][rq] > 0.0f ? v[0] * W.w[W_IS1][2 * q] + v[1] * W.w[W_IS1][2 * q + 1] : 0.0f;
-  io.dpre[1][rq] = hp.h[1][rq] > 0.0f ? v[2] * W.w[W_IS3][2 * q] + v[3] * W.w[W_IS3][2 * q + 1] : 0.0f;
-  io.dpre[2][rq] = hp.h[2][rq] > 0.0f ? v[8] * W.w[W_ZL1][q] : 0.0f;
-  io.dpre[3][rq] = hp.h[3][rq] > 0.0f ? v[9] * W.w[W_GS1][2 * q] + v[10] * W.w[W_GS1][2 * q + 1] : 0.0f;
-  io.dpre[4][rq] = hp.h[4][rq] > 0.0f ? v[11] * W.w[W_GS3][2 * q] + v[12] * W.w[W_GS3][2 * q + 1] : 0.0f;
-  if (io.dpre[5]) io.dpre[5][rq] = (hp.h[5] && hp.h[5][rq] > 0.0f) ? v[13] * W.w[W_ZP1][q] : 0.0f;
+  // every operand loaded before the first store (unconditionally, see above)
+  float hv[6], wa[6], wb[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) hv[k] = hp.h[k][rq];
+  hv[5] = hp.h[5] ? hp.h[5][rq] : 0.0f;
+  wa[0] = W.w[W_IS1][2 * q]; wb[0] = W.w[W_IS1][2 * q + 1];
+  wa[1] = W.w[W_IS3][2 * q]; wb[1] = W.w[W_IS3][2 * q + 1];
+  wa[2] = W.w[W_ZL1][q];
+  wa[3] = W.w[W_GS1][2 * q]; wb[3] = W.w[W_GS1][2 * q + 1];
+  wa[4] = W.w[W_GS3][2 * q]; wb[4] = W.w[W_GS3][2 * q + 1];
+  wa[5] = W.w[W_ZP1][q];
+  io.dpre[0][rq] = hv[0] > 0.0f ? v[0] * wa[0] + v[1] * wb[0] : 0.0f;
+  io.dpre[1][rq] = hv[1] > 0.0f ? v[2] * wa[1] + v[3] * wb[1] : 0.0f;
+  io.dpre[2][rq] = hv[2] > 0.0f ? v[8] * wa[2] : 0.0f;
+  io.dpre[3][rq] = hv[3] > 0.0f ? v[9] * wa[3] + v[10] * wb[3] : 0.0f;
+  io.dpre[4][rq] = hv[4] > 0.0f ? v[11] * wa[4] + v[12] * wb[4] : 0.0f;
+  if (io.dpre[5]) io.dpre[5][rq] = (hp.h[5] && hv[5] > 0.0f) ? v[13] * wa[5] : 0.0f;
 }
 
 }  // namespace

@@ -99,11 +99,14 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
     for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        // clamped, unconditional loads (a per-element `if` around a load
+        // compiles to a branch with a vmcnt(0) wait inside: one memory
+        // latency per element); the out-of-range elements are never stored
         float v = 0.0f;
         if (Cin != nullptr && ks == 0) {
-          const int row = m0 + wm + mi * 16 + (lane >> 4) * 4 + r;
-          const int col = n0 + wn + ni * 16 + (lane & 15);
-          if (row < M && col < N) v = Cin[(size_t)row * D.ldc + col];
+          const int row = min(m0 + wm + mi * 16 + (lane >> 4) * 4 + r, M - 1);
+          const int col = min(n0 + wn + ni * 16 + (lane & 15), N - 1);
+          v = Cin[(size_t)row * D.ldc + col];
         }
         acc[mi][ni][r] = v;
       }
@@ -246,6 +249,26 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
   void* Cv = P.C[z];
   const float* bias = P.bias[z];
   const void* aux = P.aux[z];
+  // bias and aux operands of the lane loaded up front from clamped indices,
+  // unconditionally (see the Cin loads above)
+  float bq[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni)
+    bq[ni] = bias != nullptr ? bias[min(n0 + wn + ni * 16 + (lane & 15), N - 1)] : 0.0f;
+  float xq[MI][NI][4];
+  if constexpr (EPI == B_SOFTPLUS_BWD || EPI == B_SIGMOID_NOISE) {
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const size_t ao = (size_t)min(m0 + wm + mi * 16 + (lane >> 4) * 4 + r, M - 1) * D.ldaux +
+                            min(n0 + wn + ni * 16 + (lane & 15), N - 1);
+          xq[mi][ni][r] = EPI == B_SOFTPLUS_BWD ? bf2f(reinterpret_cast<const __bf16*>(aux)[ao])
+                                                : reinterpret_cast<const float*>(aux)[ao];
+        }
+  }
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -264,16 +287,15 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(BPtrs P, BDims D) {
         // bf16 configuration: hardware transcendentals (v_exp/v_log, ~1 ulp);
         // the bit-exact spec functions are reserved for the fp32 parity path
         if (EPI == B_SOFTPLUS_BWD) {
-          const float post = bf2f(reinterpret_cast<const __bf16*>(aux)[(size_t)row * D.ldaux + col]);
+          const float post = xq[mi][ni][r];
           // sigmoid(pre) = 1 - exp(-softplus(pre)); series for small post
           const float sg = post < 1e-3f ? post * (1.0f - 0.5f * post) : 1.0f - __expf(-post);
           v = v * sg;
         } else {
-          if (bias != nullptr) v = v + bias[col];
+          if (bias != nullptr) v = v + bq[ni];
           if (EPI == B_SOFTPLUS) v = mog_softplus_hw(v);
           if (EPI == B_SIGMOID_NOISE) {
-            const float y = __builtin_fmaf(
-                reinterpret_cast<const float*>(aux)[(size_t)row * D.ldaux + col], D.aux_scale, v);
+            const float y = __builtin_fmaf(xq[mi][ni][r], D.aux_scale, v);
             v = mog_sigmoid_hw(y);
           }
         }

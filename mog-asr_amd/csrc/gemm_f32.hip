@@ -43,11 +43,6 @@ enum {
 };
 
 constexpr int MAXB = 8;
-}  // namespace
-int mog_internal_gemm_tn_small(int batch, const float* const* A, const float* const* B,
-                               float* const* C, float* const* colsum, int M, int N, int K,
-                               int lda, int ldb, int ldc, hipStream_t stream);
-namespace {
 struct GemmPtrs {
   const float* A[MAXB];
   const float* B[MAXB];
@@ -221,6 +216,27 @@ __device__ __forceinline__ void store_tile(const floatx4 (&acc)[MI][NI], const G
   const float* bias = P.bias[z];
   const float* aux = P.aux[z];
   float* Cpre = P.Cpre[z];
+  constexpr bool HAS_AUX = EPI == EPI_SOFTPLUS_BWD || EPI == EPI_RELU_BWD || EPI == EPI_SIGMOID_NOISE;
+  // every bias / aux operand of the lane loaded up front from clamped indices
+  // (a load under the per-element bounds test below compiles to a branch with
+  // a vmcnt(0) wait inside: one memory latency per element)
+  float bq[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni)
+    bq[ni] = bias != nullptr ? bias[min(c0 + acc_col<MI, NI, RA, RB>(ni, lane & 15), N - 1)] : 0.0f;
+  float xq[MI][NI][4];
+  if (HAS_AUX && !(EPI == EPI_SIGMOID_NOISE && D.eps_gen)) {
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = min(r0 + acc_row<MI, NI, RA, RB>(mi, (lane >> 4) * 4 + r), M - 1);
+          const int col = min(c0 + acc_col<MI, NI, RA, RB>(ni, lane & 15), N - 1);
+          xq[mi][ni][r] = aux[(size_t)row * D.ldaux + col];
+        }
+  }
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -237,14 +253,14 @@ __device__ __forceinline__ void store_tile(const floatx4 (&acc)[MI][NI], const G
           continue;
         }
         if (EPI == EPI_SOFTPLUS_BWD) {
-          C[o] = v * mog_sigmoidf(aux[(size_t)row * D.ldaux + col]);
+          C[o] = v * mog_sigmoidf(xq[mi][ni][r]);
           continue;
         }
         if (EPI == EPI_RELU_BWD) {
-          C[o] = aux[(size_t)row * D.ldaux + col] > 0.0f ? v : 0.0f;
+          C[o] = xq[mi][ni][r] > 0.0f ? v : 0.0f;
           continue;
         }
-        if (bias != nullptr) v = v + bias[col];
+        if (bias != nullptr) v = v + bq[ni];
         if (EPI == EPI_STORE) {
           C[o] = v;
         } else {
@@ -258,7 +274,7 @@ __device__ __forceinline__ void store_tile(const floatx4 (&acc)[MI][NI], const G
               noise_quad(D, row, col & ~3, q);
               nz = q[col & 3];
             } else {
-              nz = aux[(size_t)row * D.ldaux + col];
+              nz = xq[mi][ni][r];
             }
             C[o] = mog_sigmoidf(v + nz * D.aux_scale);
           }
@@ -301,13 +317,42 @@ __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[BM / 32][BN
     const float* bias = P.bias[z];
     const float* aux = P.aux[z];
     float* Cpre = P.Cpre[z];
-    constexpr int C4 = BN / 4;
+    constexpr int C4 = BN / 4, RSTEP = 256 / C4, ITER = BM / RSTEP;
+    static_assert(256 % C4 == 0 && BM % RSTEP == 0, "epilogue row mapping");
     constexpr bool HAS_PRE = EPI == EPI_RELU || EPI == EPI_SOFTPLUS || EPI == EPI_SIGMOID_NOISE;
     constexpr bool HAS_AUX = EPI == EPI_SOFTPLUS_BWD || EPI == EPI_RELU_BWD ||
                              EPI == EPI_SIGMOID_NOISE;
-    for (int q = t; q < BM * C4; q += 256) {
-      const int row = q / C4, c4 = q - row * C4;
-      const int grow = m0 + row, gcol = n0 + 4 * c4;
+    // the thread's column quad is the same in every row it visits: its bias
+    // quad is loaded once, and every aux quad up front, from clamped
+    // (in-bounds) indices, unconditionally -- a load under the bounds test
+    // compiles to a branch with a vmcnt(0) wait inside
+    const int c4 = t % C4, r00 = t / C4, gcol = n0 + 4 * c4;
+    float bq[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bias != nullptr) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bq[e] = bias[min(gcol + e, N - 1)];
+    }
+    float xq[ITER][4];
+    const bool aux_ld = HAS_AUX && !(EPI == EPI_SIGMOID_NOISE && D.eps_gen);
+    if (aux_ld) {
+      // gcol < N <= ldaux, both multiples of 4 where a quad is read whole
+      const int ac = gcol < N ? gcol : 0;
+#pragma unroll
+      for (int i = 0; i < ITER; ++i) {
+        const float* ar = aux + (size_t)min(m0 + r00 + RSTEP * i, M - 1) * D.ldaux;
+        if (D.ldaux % 4 == 0) {
+          const float4 x4 = *reinterpret_cast<const float4*>(ar + ac);
+          xq[i][0] = x4.x; xq[i][1] = x4.y; xq[i][2] = x4.z; xq[i][3] = x4.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) xq[i][e] = ar[min(ac + e, N - 1)];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int row = r00 + RSTEP * i;
+      const int grow = m0 + row;
       if (grow >= M || gcol >= N) continue;
       const bool full = gcol + 4 <= N;
       const float4 a4 = *reinterpret_cast<const float4*>(&sC[row * LDC + 4 * c4]);
@@ -316,13 +361,8 @@ __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[BM / 32][BN
       if (EPI == EPI_SIGMOID_NOISE && D.eps_gen) {
         noise_quad(D, grow, gcol, x);  // N % 4 == 0: the quad lies inside the row
       } else if constexpr (HAS_AUX) {
-        const float* ar = aux + (size_t)grow * D.ldaux + gcol;
-        if (full) {
-          const float4 x4 = *reinterpret_cast<const float4*>(ar);
-          x[0] = x4.x; x[1] = x4.y; x[2] = x4.z; x[3] = x4.w;
-        } else {
-          for (int e = 0; e < 4; ++e) x[e] = gcol + e < N ? ar[e] : 0.0f;
-        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = xq[i][e];
       }
       float o[4], pre[4];
 #pragma unroll
@@ -334,7 +374,7 @@ __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[BM / 32][BN
         } else if (EPI == EPI_RELU_BWD) {
           o[e] = x[e] > 0.0f ? w : 0.0f;
         } else {
-          if (bias != nullptr) w = w + bias[min(gcol + e, N - 1)];
+          if (bias != nullptr) w = w + bq[e];
           pre[e] = w;
           if (EPI == EPI_STORE) o[e] = w;
           if (EPI == EPI_RELU) o[e] = w > 0.0f ? w : 0.0f;
@@ -391,11 +431,14 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
     for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        // clamped, unconditional loads (a per-element `if` around a load
+        // compiles to a branch with a vmcnt(0) wait inside: one memory
+        // latency per element); the out-of-range elements are never stored
         float v = 0.0f;
         if (Cin != nullptr && ks == 0) {
-          const int row = m0 + wm + mi * 16 + (lane >> 4) * 4 + r;
-          const int col = n0 + wn + ni * 16 + (lane & 15);
-          if (row < M && col < N) v = Cin[(size_t)row * D.ldc + col];
+          const int row = min(m0 + wm + mi * 16 + (lane >> 4) * 4 + r, M - 1);
+          const int col = min(n0 + wn + ni * 16 + (lane & 15), N - 1);
+          v = Cin[(size_t)row * D.ldc + col];
         }
         acc[mi][ni][r] = v;
       }
@@ -623,11 +666,11 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_dma_kernel(GemmPtrs P, GemmDi
     for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = 0.0f;
+        float v = 0.0f;  // (clamped, unconditional: see gemm_f32_kernel)
         if (Cin != nullptr && ks == 0) {
-          const int row = m0 + wm + acc_row<MI, NI, RA, RB>(mi, (lane >> 4) * 4 + r);
-          const int col = n0 + wn + acc_col<MI, NI, RA, RB>(ni, lane & 15);
-          if (row < M && col < N) v = Cin[(size_t)row * D.ldc + col];
+          const int row = min(m0 + wm + acc_row<MI, NI, RA, RB>(mi, (lane >> 4) * 4 + r), M - 1);
+          const int col = min(n0 + wn + acc_col<MI, NI, RA, RB>(ni, lane & 15), N - 1);
+          v = Cin[(size_t)row * D.ldc + col];
         }
         acc[mi][ni][r] = v;
       }
@@ -987,14 +1030,6 @@ extern "C" int mog_gemm_f32(int batch, const float* const* A, const float* const
   D.kseg = 0;
   D.eps_gen = 0;
   D.eps_seed = D.eps_off = 0;
-  // the 1- / 2-wide weight gradients (N <= 16, M <= 256): the LDS-free kernel
-  // of gemm_tn_small.hip, which picks its own K chunks (MOG_TN_SMALL=0: the
-  // tiled kernels below)
-  static const char* tn_env = getenv("MOG_TN_SMALL");
-  static const bool tn_small = tn_env == nullptr || atoi(tn_env) != 0;
-  if (tn_small && transA && !transB && epi == EPI_ATOMIC && M <= 256 && N <= 16 && K > 0)
-    return mog_internal_gemm_tn_small(batch, P.A, P.B, P.C, colsum ? P.colsum : nullptr, M, N,
-                                      K, lda, ldb, ldc, mog_stream(stream));
   MOG_TRY(launch_auto(transA, transB, epi, mog_stream(stream), P, D, batch));
   MOG_LAUNCH_RET();
 }

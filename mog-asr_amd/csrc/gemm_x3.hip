@@ -409,35 +409,37 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
   const u32x4 z4 = {0u, 0u, 0u, 0u};
   // Buffer loads: the workgroup's A rows and the B pieces behind two
   // descriptors, one 32-bit offset register per thread and operand (the row /
-  // piece / k-tile steps are uniform: scalar offsets).  A rows >= M fall
-  // outside A's record range and load 0; k >= K (the last k-tile, K % 32 != 0)
-  // is zeroed after the load on both operands (with lda == K those addresses
-  // hold the next row).  B rows >= N load the next piece's rows or 0 past the
-  // last piece: they only reach output columns >= N, which are not stored.
+  // piece / k-tile steps are uniform: scalar offsets).  Every load is issued
+  // unconditionally -- a predicated load (`cond ? load : 0`) becomes a branch
+  // around it with a vmcnt(0) wait inside, one full memory latency per load --
+  // and what must read as zero is pushed out of the descriptor's range
+  // instead: A rows >= M fall outside A's record range; k >= K (the last
+  // k-tile, K % 32 != 0; with lda == K those addresses hold the next row) gets
+  // an offset past every range, on both operands.  B rows >= N load the next
+  // piece's rows or 0 past the last piece: they only reach output columns >= N,
+  // which are not stored.
   const __amdgpu_buffer_rsrc_t arsc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(D.A) + (size_t)m0 * D.lda, 0, min(M - m0, BM) * D.lda * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t brsc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<__bf16*>(D.B3), 0, (int)((2 * D.sb + (long)N * D.ldb) * 2), 0x00020000);
   const int avo = (ar * D.lda + ak) * 4;
   const int bvo = ((n0 + br) * D.ldb + bk) * 2;
+  constexpr int OOB = (int)0x80000000u;  // + any scalar offset here: past every range
   auto load_tiles = [&](int k0, auto sc) {
     constexpr int s = decltype(sc)::value;
-    const bool ka = k0 + ak < K, kb = k0 + bk < K;
+    const int av = k0 + ak < K ? avo : OOB, bv = k0 + bk < K ? bvo : OOB;
 #pragma unroll
     for (int i = 0; i < NT_NLA; ++i) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(arsc, avo, (32 * i * D.lda + k0) * 4, 0);
-      ra[s][i] = ka ? float4{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
-                             __uint_as_float(v[3])}
-                    : zero4;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(arsc, av, (32 * i * D.lda + k0) * 4, 0);
+      ra[s][i] = float4{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                        __uint_as_float(v[3])};
     }
 #pragma unroll
     for (int i = 0; i < NT_NLB; ++i)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
-            brsc, bvo, (int)((p * D.sb + (long)64 * i * D.ldb + k0) * 2), 0);
-        rb[s][p][i] = kb ? v : z4;
-      }
+      for (int p = 0; p < 3; ++p)
+        rb[s][p][i] = __builtin_amdgcn_raw_buffer_load_b128(
+            brsc, bv, (int)((p * D.sb + (long)64 * i * D.ldb + k0) * 2), 0);
   };
   auto store_tiles = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
@@ -513,6 +515,22 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
       if (it + 1 < nk) body(it + 1, S1{});
     }
   }
+  // softplus backward: every aux quad of the lane loaded up front,
+  // unconditionally (rows >= M fall outside the descriptor; columns >= N are
+  // loaded but not stored), so the sixteen loads share one latency
+  u32x4 xq[4][4];
+  if constexpr (EPI == 1) {
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(D.aux) + (size_t)m0 * D.ldaux, 0, min(M - m0, BM) * D.ldaux * 4,
+        0x00020000);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        xq[mi][ni] = __builtin_amdgcn_raw_buffer_load_b128(
+            xr, ((wm + mi * 16 + g * 4 + (li & 3)) * D.ldaux + n0 + wn + ni * 16 + (li & ~3)) * 4,
+            0, 0);
+  }
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -520,16 +538,13 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
       const floatx4 v = xt_quad_transpose(acc[mi][ni], lane);
       const int row = m0 + wm + mi * 16 + g * 4 + (li & 3);
       const int col = n0 + wn + ni * 16 + (li & ~3);
-      if (row >= M || col >= N) continue;
       float o[4] = {v[0], v[1], v[2], v[3]};
       if (EPI == 1) {
-        const float4 x = *reinterpret_cast<const float4*>(D.aux + (size_t)row * D.ldaux + col);
-        o[0] = v[0] * mog_sigmoidf(x.x);
-        o[1] = v[1] * mog_sigmoidf(x.y);
-        o[2] = v[2] * mog_sigmoidf(x.z);
-        o[3] = v[3] * mog_sigmoidf(x.w);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = v[q] * mog_sigmoidf(__uint_as_float(xq[mi][ni][q]));
       }
-      *reinterpret_cast<float4*>(D.C + (size_t)row * D.ldc + col) = make_float4(o[0], o[1], o[2], o[3]);
+      if (row < M && col < N)
+        *reinterpret_cast<float4*>(D.C + (size_t)row * D.ldc + col) = make_float4(o[0], o[1], o[2], o[3]);
     }
 }
 
@@ -591,7 +606,8 @@ extern "C" int mog_gemm_x3_nt(const float* A, const void* B3, long sb, float* C,
   MOG_CHECK_ARG(al16(A) && al16(B3) && al16(C) && K % 4 == 0 && N % 4 == 0 && lda % 4 == 0 &&
                 ldc % 4 == 0 && ldb % 8 == 0 && sb % 8 == 0 && lda >= K && ldb >= K && ldc >= N);
   // 32-bit buffer offsets: the pieces and one 128-row panel of A
-  MOG_CHECK_ARG((2 * sb + (long)N * ldb) * 2 < (1L << 31) && (long)BM * lda * 4 < (1L << 31));
+  MOG_CHECK_ARG((2 * sb + (long)N * ldb) * 2 < (1L << 31) && (long)BM * lda * 4 < (1L << 31) &&
+                (long)BM * ldaux * 4 < (1L << 31));
   if (M == 0 || N == 0) return 0;
   X3NtArgs D{};
   D.A = A; D.B3 = reinterpret_cast<const __bf16*>(B3); D.sb = sb; D.C = C; D.aux = aux;

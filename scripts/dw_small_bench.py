@@ -1,8 +1,7 @@
 """Stand-alone timing of the fp32 step's small weight-gradient GEMMs (the
 side-stream launches AIRModel._dw makes at T*B = 24,576 rows: the VAE's
 256 x 50 / 50 x 256 layers, the heads' hidden and output layers, the LSTM
-recurrent rows), HIP events, against the skinny-TN kernel when it is built.
-Not product code."""
+recurrent rows), HIP events, over the split-K targets.  Not product code."""
 import os
 import sys
 

@@ -11,3 +11,4 @@ grep NT gpurun_out/x3nt_new.log
 timeout -k 10 120 python3 scripts/dw_small_bench.py > gpurun_out/dw_small.log 2>&1 || { tail -5 gpurun_out/dw_small.log; exit 1; }
 grep -v amdgpu.ids gpurun_out/dw_small.log
 timeout -k 10 300 python -u -m pytest tests/test_gpu_x3.py tests/test_gpu_parity.py -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/x3nt_tests.log 2>&1; tail -2 gpurun_out/x3nt_tests.log
+bash scripts/pmc_x3nt.sh

