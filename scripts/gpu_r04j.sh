@@ -8,3 +8,4 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_x3.py tests/test_gpu_parity
 tail -2 gpurun_out/r04j_tests.log; grep -E "^(FAILED|ERROR)" gpurun_out/r04j_tests.log | head
 [ $rc -le 1 ] || exit $rc
 bash scripts/pmc_x3.sh
+bash scripts/gpu_r04k.sh
