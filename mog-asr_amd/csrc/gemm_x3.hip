@@ -132,23 +132,41 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  float4 ra[NL], rb[NL];
-  const float4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  // Operand loads through buffer descriptors, unconditional: rows past the
+  // K chunk get an offset past every range (they load 0; a predicated load
+  // compiled to a branch per load, and the generic-pointer form to FLAT loads,
+  // which also count in lgkmcnt -- so the barrier's lgkmcnt(0) waited for the
+  // next k-tile's prefetch every iteration).  Columns >= M / N load a
+  // neighbour's data (or 0 past the buffer): they reach only rows / columns of
+  // C that are not stored, and column sums that are not stored.  Kept as raw
+  // dwords until the split (a conversion at the load makes the compiler copy
+  // the registers there, which waits for the load).
+  u32x4 ra[NL], rb[NL];
+  constexpr int OOB = (int)0x80000000u;
+  // record ranges = the operands' validated extents (the last piece's last
+  // k-row ends at column round8(M) / M): nothing past them is read
+  const __amdgpu_buffer_rsrc_t arsc = __builtin_amdgcn_make_buffer_rsrc(
+      PRE ? (void*)D.A3 : (void*)D.A, 0,
+      PRE ? (int)((2 * D.sa + (long)(D.K - 1) * D.lda + ((M + 7) & ~7)) * 2)
+          : (int)(((long)(D.K - 1) * D.lda + M) * 4),
+      0x00020000);
+  const __amdgpu_buffer_rsrc_t brsc = __builtin_amdgcn_make_buffer_rsrc(
+      PRE ? (void*)D.B3 : (void*)D.B, 0,
+      PRE ? (int)((2 * D.sb + (long)(D.K - 1) * D.ldb + ((N + 7) & ~7)) * 2)
+          : (int)(((long)(D.K - 1) * D.ldb + N) * 4),
+      0x00020000);
   auto load_tiles = [&](int k0) {
     if constexpr (PRE) {
-      const u32x4 z4 = {0u, 0u, 0u, 0u};
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         const int gk = k0 + pk + 16 * i;
-        const int gm = m0 + pc, gn = n0 + pc;
-        // gm < M <= lda, both multiples of 8: the chunk stays inside the row
-        // (columns >= M are pad zeros or a neighbour window's, never stored)
+        // gm < lda, multiples of 8: a chunk starting in the row stays in it
+        const int ao = gk < kend ? (gk * D.lda + m0 + pc) * 2 : OOB;
+        const int bo = gk < kend ? (gk * D.ldb + n0 + pc) * 2 : OOB;
 #pragma unroll
         for (int p = 0; p < NPC; ++p) {
-          pa[p][i] = (gk < kend && gm < M)
-              ? *reinterpret_cast<const u32x4*>(D.A3 + p * D.sa + (size_t)gk * D.lda + gm) : z4;
-          pb[p][i] = (gk < kend && gn < N)
-              ? *reinterpret_cast<const u32x4*>(D.B3 + p * D.sb + (size_t)gk * D.ldb + gn) : z4;
+          pa[p][i] = __builtin_amdgcn_raw_buffer_load_b128(arsc, ao, (int)(p * D.sa * 2), 0);
+          pb[p][i] = __builtin_amdgcn_raw_buffer_load_b128(brsc, bo, (int)(p * D.sb * 2), 0);
         }
       }
       return;
@@ -156,12 +174,15 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int gk = k0 + sk + 8 * i;
-      const int gm = m0 + sc, gn = n0 + sc;
-      ra[i] = (gk < kend && gm < M)
-                  ? *reinterpret_cast<const float4*>(D.A + (size_t)gk * D.lda + gm) : zero4;
-      rb[i] = (gk < kend && gn < N)
-                  ? *reinterpret_cast<const float4*>(D.B + (size_t)gk * D.ldb + gn) : zero4;
+      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          arsc, gk < kend ? (gk * D.lda + m0 + sc) * 4 : OOB, 0, 0);
+      rb[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          brsc, gk < kend ? (gk * D.ldb + n0 + sc) * 4 : OOB, 0, 0);
     }
+  };
+  auto f4 = [](const u32x4& v) {
+    return float4{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                  __uint_as_float(v[3])};
   };
   auto store_tiles = [&](int stage) {
     __bf16* S = lds + stage * STAGE;
@@ -194,19 +215,20 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
     for (int i = 0; i < NL; ++i) {
       const int o = (sk + 8 * i) * LDR + sc;
       u32x2 p0, p1, p2;
-      split4(ra[i], p0, p1, p2);
+      split4(f4(ra[i]), p0, p1, p2);
       *reinterpret_cast<u32x2*>(S + 0 * PIECE + o) = p0;
       *reinterpret_cast<u32x2*>(S + 1 * PIECE + o) = p1;
       *reinterpret_cast<u32x2*>(S + 2 * PIECE + o) = p2;
-      split4(rb[i], p0, p1, p2);
+      const float4 bf = f4(rb[i]);
+      split4(bf, p0, p1, p2);
       *reinterpret_cast<u32x2*>(S + 3 * PIECE + o) = p0;
       *reinterpret_cast<u32x2*>(S + 4 * PIECE + o) = p1;
       *reinterpret_cast<u32x2*>(S + 5 * PIECE + o) = p2;
       if (do_cs) {
-        cs[0] += rb[i].x;
-        cs[1] += rb[i].y;
-        cs[2] += rb[i].z;
-        cs[3] += rb[i].w;
+        cs[0] += bf.x;
+        cs[1] += bf.y;
+        cs[2] += bf.z;
+        cs[3] += bf.w;
       }
     }
   };
@@ -403,7 +425,10 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
-  float4 ra[PD][NT_NLA];
+  // loaded as raw dwords and reinterpreted only at the split: a conversion at
+  // the load makes the compiler copy the registers right after it, which
+  // waits for the load there and serialises the prefetch
+  u32x4 ra[PD][NT_NLA];
   u32x4 rb[PD][3][NT_NLB];
   const float4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const u32x4 z4 = {0u, 0u, 0u, 0u};
@@ -429,11 +454,8 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
     constexpr int s = decltype(sc)::value;
     const int av = k0 + ak < K ? avo : OOB, bv = k0 + bk < K ? bvo : OOB;
 #pragma unroll
-    for (int i = 0; i < NT_NLA; ++i) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(arsc, av, (32 * i * D.lda + k0) * 4, 0);
-      ra[s][i] = float4{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
-                        __uint_as_float(v[3])};
-    }
+    for (int i = 0; i < NT_NLA; ++i)
+      ra[s][i] = __builtin_amdgcn_raw_buffer_load_b128(arsc, av, (32 * i * D.lda + k0) * 4, 0);
 #pragma unroll
     for (int i = 0; i < NT_NLB; ++i)
 #pragma unroll
@@ -447,7 +469,9 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
     for (int i = 0; i < NT_NLA; ++i) {
       const int o = (ar + 32 * i) * NT_LDK + ak;
       u32x2 p0, p1, p2;
-      split4(ra[s][i], p0, p1, p2);
+      split4(float4{__uint_as_float(ra[s][i][0]), __uint_as_float(ra[s][i][1]),
+                    __uint_as_float(ra[s][i][2]), __uint_as_float(ra[s][i][3])},
+             p0, p1, p2);
       *reinterpret_cast<u32x2*>(lds + 0 * NT_PIECE + o) = p0;
       *reinterpret_cast<u32x2*>(lds + 1 * NT_PIECE + o) = p1;
       *reinterpret_cast<u32x2*>(lds + 2 * NT_PIECE + o) = p2;
@@ -571,6 +595,8 @@ extern "C" int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb,
   // that starts below M ends inside the row; its columns >= M are not stored)
   MOG_CHECK_ARG(al16(A3) && al16(B3) && lda % 8 == 0 && ldb % 8 == 0 && sa % 8 == 0 &&
                 sb % 8 == 0 && lda >= M && ldb >= N && ldc >= N);
+  // 32-bit buffer offsets over the pieces
+  MOG_CHECK_ARG((2 * sa + (long)K * lda) * 2 < (1L << 31) && (2 * sb + (long)K * ldb) * 2 < (1L << 31));
   if (M == 0 || N == 0 || K == 0) return 0;
   X3Args D{};
   D.A3 = reinterpret_cast<const __bf16*>(A3);
@@ -588,6 +614,7 @@ extern "C" int mog_gemm_f32_x3_tn(const float* A, const float* B, float* C, floa
   // float4 rows: 16-byte operands, widths and strides multiples of 4
   MOG_CHECK_ARG(al16(A) && al16(B) && M % 4 == 0 && N % 4 == 0 && lda % 4 == 0 &&
                 ldb % 4 == 0 && lda >= M && ldb >= N && ldc >= N);
+  MOG_CHECK_ARG((long)K * lda * 4 < (1L << 31) && (long)K * ldb * 4 < (1L << 31));
   if (M == 0 || N == 0 || K == 0) return 0;
   X3Args D{};
   D.A = A; D.B = B; D.C = C; D.colsum = colsum;
