@@ -403,10 +403,11 @@ __device__ __forceinline__ floatx4 xt_quad_transpose(const floatx4& a, int lane)
   return floatx4{r0, r1, r2, r3};
 }
 
-// EPI: 0 store, 1 softplus backward.  PD: k-tiles of prefetch in registers
-// (1: the next k-tile's loads in flight under the MFMAs; 2: two register sets,
-// each k-tile's loads issued two MFMA phases before its split and store)
-template <int EPI, int PD>
+// EPI: 0 store, 1 softplus backward.  The next k-tile's loads are in flight
+// under the MFMAs (one register set: a second, loads two MFMA phases ahead,
+// measured no faster; neither was a double-buffered 8-wave form with the
+// split woven between the MFMA passes, 158 -> 162 us)
+template <int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[NT_STAGE];
   const int nwg = gridDim.x;
@@ -428,8 +429,8 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
   // loaded as raw dwords and reinterpreted only at the split: a conversion at
   // the load makes the compiler copy the registers right after it, which
   // waits for the load there and serialises the prefetch
-  u32x4 ra[PD][NT_NLA];
-  u32x4 rb[PD][3][NT_NLB];
+  u32x4 ra[NT_NLA];
+  u32x4 rb[3][NT_NLB];
   const float4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const u32x4 z4 = {0u, 0u, 0u, 0u};
   // Buffer loads: the workgroup's A rows and the B pieces behind two
@@ -450,27 +451,25 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
   const int avo = (ar * D.lda + ak) * 4;
   const int bvo = ((n0 + br) * D.ldb + bk) * 2;
   constexpr int OOB = (int)0x80000000u;  // + any scalar offset here: past every range
-  auto load_tiles = [&](int k0, auto sc) {
-    constexpr int s = decltype(sc)::value;
+  auto load_tiles = [&](int k0) {
     const int av = k0 + ak < K ? avo : OOB, bv = k0 + bk < K ? bvo : OOB;
 #pragma unroll
     for (int i = 0; i < NT_NLA; ++i)
-      ra[s][i] = __builtin_amdgcn_raw_buffer_load_b128(arsc, av, (32 * i * D.lda + k0) * 4, 0);
+      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(arsc, av, (32 * i * D.lda + k0) * 4, 0);
 #pragma unroll
     for (int i = 0; i < NT_NLB; ++i)
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        rb[s][p][i] = __builtin_amdgcn_raw_buffer_load_b128(
+        rb[p][i] = __builtin_amdgcn_raw_buffer_load_b128(
             brsc, bv, (int)((p * D.sb + (long)64 * i * D.ldb + k0) * 2), 0);
   };
-  auto store_tiles = [&](auto sc) {
-    constexpr int s = decltype(sc)::value;
+  auto store_tiles = [&]() {
 #pragma unroll
     for (int i = 0; i < NT_NLA; ++i) {
       const int o = (ar + 32 * i) * NT_LDK + ak;
       u32x2 p0, p1, p2;
-      split4(float4{__uint_as_float(ra[s][i][0]), __uint_as_float(ra[s][i][1]),
-                    __uint_as_float(ra[s][i][2]), __uint_as_float(ra[s][i][3])},
+      split4(float4{__uint_as_float(ra[i][0]), __uint_as_float(ra[i][1]),
+                    __uint_as_float(ra[i][2]), __uint_as_float(ra[i][3])},
              p0, p1, p2);
       *reinterpret_cast<u32x2*>(lds + 0 * NT_PIECE + o) = p0;
       *reinterpret_cast<u32x2*>(lds + 1 * NT_PIECE + o) = p1;
@@ -480,7 +479,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
     for (int i = 0; i < NT_NLB; ++i) {
       const int o = (br + 64 * i) * NT_LDK + bk;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(lds + (3 + p) * NT_PIECE + o) = rb[s][p][i];
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(lds + (3 + p) * NT_PIECE + o) = rb[p][i];
     }
   };
   const int g = lane >> 4, li = lane & 15;
@@ -513,31 +512,13 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
     }
   };
   const int nk = (K + BK - 1) / BK;
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, PD - 1>;
-  if constexpr (PD == 1) {
-    load_tiles(0, S0{});
-    for (int it = 0; it < nk; ++it) {
-      store_tiles(S0{});
-      if (it + 1 < nk) load_tiles((it + 1) * BK, S0{});
-      __syncthreads();
-      compute();
-      __syncthreads();
-    }
-  } else {
-    load_tiles(0, S0{});
-    if (nk > 1) load_tiles(BK, S1{});
-    auto body = [&](int it, auto sc) {
-      store_tiles(sc);
-      if (it + 2 < nk) load_tiles((it + 2) * BK, sc);
-      __syncthreads();
-      compute();
-      __syncthreads();
-    };
-    for (int it = 0; it < nk; it += 2) {
-      body(it, S0{});
-      if (it + 1 < nk) body(it + 1, S1{});
-    }
+  load_tiles(0);
+  for (int it = 0; it < nk; ++it) {
+    store_tiles();
+    if (it + 1 < nk) load_tiles((it + 1) * BK);
+    __syncthreads();
+    compute();
+    __syncthreads();
   }
   // softplus backward: every aux quad of the lane loaded up front,
   // unconditionally (rows >= M fall outside the descriptor; columns >= N are
@@ -643,14 +624,8 @@ extern "C" int mog_gemm_x3_nt(const float* A, const void* B3, long sb, float* C,
   D.ny = mog_cdiv(M, BM);
   D.epi = epi;
   const unsigned nwg = (unsigned)D.nx * D.ny;
-  static const int pd = getenv("MOG_X3NT_PD") ? atoi(getenv("MOG_X3NT_PD")) : 1;
   hipStream_t s = mog_stream(stream);
-  if (pd == 2) {
-    if (epi == 1) gemm_x3_nt_kernel<1, 2><<<nwg, 256, 0, s>>>(D);
-    else gemm_x3_nt_kernel<0, 2><<<nwg, 256, 0, s>>>(D);
-  } else {
-    if (epi == 1) gemm_x3_nt_kernel<1, 1><<<nwg, 256, 0, s>>>(D);
-    else gemm_x3_nt_kernel<0, 1><<<nwg, 256, 0, s>>>(D);
-  }
+  if (epi == 1) gemm_x3_nt_kernel<1><<<nwg, 256, 0, s>>>(D);
+  else gemm_x3_nt_kernel<0><<<nwg, 256, 0, s>>>(D);
   MOG_LAUNCH_RET();
 }

@@ -827,8 +827,11 @@ class AIRModel:
         TB = ws.B * self.max_steps
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
+        ws.early_wgrads = set()
         # dm = SigmoidGrad(r, dr) was written by the STN write backward
+        self._early_wgrad(ws, "gen_mean")
         self._dx(ws.dm, "gen_mean", ws.dd2, TB, G2, W2, aux=ws.d2pre)
+        self._early_wgrad(ws, "generative_2")
         self._dx(ws.dd2, "generative_2", ws.dd1, TB, G1, G2, aux=ws.d1pre)
         gemm([ws.dd1], [vw["generative_1"]], [ws.dz_all], TB, Z, G1, G1, G1, Z, transB=True)
         _ops.vae_sample_backward_(TB, Z, float(self.vae_prior_mean),
@@ -1117,18 +1120,55 @@ class AIRModel:
         splitk = max(1, min(K // 256, (512 + tiles - 1) // tiles))
         ops.gemm_x3_tn(X, dY, out, M, N, K, lda, ldb, N, splitk=splitk, colsum=bias_out)
 
-    def _vae_weight_grads_fp32(self, ws):
+    def _vae_wgrad_fp32(self, ws, name):
+        """One VAE layer's weight / bias gradient over all T*B rows (fp32)."""
         TB = ws.B * self.max_steps
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
         gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
-        self._dw_x3(ws.g, ws.da1, g("recognition_1"), TB, W2, R1, W2, R1, gb("recognition_1"))
-        self._dw_x3(ws.a1, ws.da2, g("recognition_2"), TB, R1, R2, R1, R2, gb("recognition_2"))
-        self._dw([ws.a2] * 2, [ws.dmu, ws.dlv], [g("rec_mean"), g("rec_log_variance")], TB, R2,
-                 Z, R2, Z, [gb("rec_mean"), gb("rec_log_variance")])
-        self._dw(ws.z, ws.dd1, g("generative_1"), TB, Z, G1, Z, G1, gb("generative_1"))
-        self._dw_x3(ws.d1, ws.dd2, g("generative_2"), TB, G1, G2, G1, G2, gb("generative_2"))
-        self._dw_x3(ws.d2, ws.dm, g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
+        if name == "recognition_1":
+            self._dw_x3(ws.g, ws.da1, g(name), TB, W2, R1, W2, R1, gb(name))
+        elif name == "recognition_2":
+            self._dw_x3(ws.a1, ws.da2, g(name), TB, R1, R2, R1, R2, gb(name))
+        elif name == "rec_mean":  # (with rec_log_variance: one batched launch)
+            self._dw([ws.a2] * 2, [ws.dmu, ws.dlv], [g("rec_mean"), g("rec_log_variance")], TB,
+                     R2, Z, R2, Z, [gb("rec_mean"), gb("rec_log_variance")])
+        elif name == "generative_1":
+            self._dw(ws.z, ws.dd1, g(name), TB, Z, G1, Z, G1, gb(name))
+        elif name == "generative_2":
+            self._dw_x3(ws.d1, ws.dd2, g(name), TB, G1, G2, G1, G2, gb(name))
+        elif name == "gen_mean":
+            self._dw_x3(ws.d2, ws.dm, g(name), TB, G2, W2, G2, W2, gb(name))
+
+    def _vae_weight_grads_fp32(self, ws):
+        early = getattr(ws, "early_wgrads", None) or ()
+        for name in ("recognition_1", "recognition_2", "rec_mean", "generative_1",
+                     "generative_2", "gen_mean"):
+            if name not in early:
+                self._vae_wgrad_fp32(ws, name)
+        ws.early_wgrads = None
+
+    # fp32, one GPU, from SIDE_MIN_BATCH: the decoder's two large weight
+    # gradients start on the side stream as soon as their dY exists (dm after
+    # the STN write backward, dd2 after the first input gradient), under the
+    # MFMA-bound VAE input-gradient chain, instead of under the latency-bound
+    # LSTM chain, where their workgroups held every CU while the chain's small
+    # launches waited.  Measured neutral (fp32 step 3.102 / 3.093 ms with it,
+    # 3.080 / 3.093 without: the contention moves to the input-gradient chain),
+    # so opt-in (MOG_WGRAD_EARLY=1)
+    WGRAD_EARLY = os.environ.get("MOG_WGRAD_EARLY", "0") == "1"
+
+    def _early_wgrad(self, ws, name):
+        if not (self.WGRAD_EARLY and self.precision == "fp32" and self.grad_reducer is None
+                and ws.B >= self.SIDE_MIN_BATCH):
+            return
+        main, side = torch.cuda.current_stream(), self._side_stream()
+        ready = torch.cuda.Event()
+        ready.record(main)
+        side.wait_event(ready)
+        with torch.cuda.stream(side):
+            self._vae_wgrad_fp32(ws, name)
+        ws.early_wgrads.add(name)
 
     def _weight_grads_glimpse(self, ws):
         """Weight gradients of the VAE and the five heads (every loop step at
