@@ -54,16 +54,45 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   const int C = p.C;
   STAMP(11);
 
-  for (int i = tid; i < M * 12; i += NTHR) {
-    const int m = i / 12, k = i % 12;
-    float v = 0.0f;
-    if (m < nb) v = k < 6 ? p.theta_f[(size_t)(b0 + m) * 6 + k] : p.theta_b[(size_t)(b0 + m) * 6 + k - 6];
-    sth[m][k] = v;
+  // Prologue: every global load issued up front from clamped indices and
+  // selected afterwards -- thetas, mask, z value, eps_z -- so the tile pays
+  // one memory latency here, not a chain of them (a load under `if (m < nb)`
+  // compiles to a branch with a vmcnt(0) wait inside; the z value waited for
+  // the mask)
+  constexpr int TH_IT = (M * 12 + NTHR - 1) / NTHR;
+  constexpr int EZ_IT = (M * 50 / 4 + NTHR - 1) / NTHR;
+  float thv[TH_IT];
+#pragma unroll
+  for (int j = 0; j < TH_IT; ++j) {
+    const int i = tid + j * NTHR, m = min(i / 12, nb - 1), k = i % 12;
+    thv[j] = k < 6 ? p.theta_f[(size_t)(b0 + m) * 6 + k] : p.theta_b[(size_t)(b0 + m) * 6 + k - 6];
+  }
+  const int tc = min(tid, nb - 1);
+  const float mk = p.mask[b0 + tc], zv = p.zval[b0 + tc];
+  const bool ez_al = ((reinterpret_cast<size_t>(p.eps_z) & 15) == 0);
+  const int nez4 = ez_al ? nb * 50 / 4 : 0;
+  float4 ezv[EZ_IT];
+  if (ez_al) {  // (uniform)
+    const float4* src = reinterpret_cast<const float4*>(p.eps_z + (size_t)b0 * 50);
+#pragma unroll
+    for (int j = 0; j < EZ_IT; ++j) ezv[j] = src[min(tid + j * NTHR, nez4 - 1)];
+  }
+#pragma unroll
+  for (int j = 0; j < TH_IT; ++j) {
+    const int i = tid + j * NTHR;
+    if (i < M * 12) sth[i / 12][i % 12] = i / 12 < nb ? thv[j] : 0.0f;
   }
   if (tid < M) {
-    const bool act = tid < nb && p.mask[b0 + tid] != 0.0f;
+    const bool act = tid < nb && mk != 0.0f;
     smask[tid] = act;
-    szv[tid] = act ? p.zval[b0 + tid] : 0.0f;
+    szv[tid] = act ? zv : 0.0f;
+  }
+  {  // eps_z of the tile -> LDS (contiguous [nb][50] rows), used in the sample phase
+    float* sEz = reinterpret_cast<float*>(arena + Ly::OFF_EZ);
+#pragma unroll
+    for (int j = 0; j < EZ_IT; ++j)
+      if (tid + j * NTHR < nez4) reinterpret_cast<float4*>(sEz)[tid + j * NTHR] = ezv[j];
+    for (int i = nez4 * 4 + tid; i < nb * 50; i += NTHR) sEz[i] = p.eps_z[(size_t)b0 * 50 + i];
   }
   lds_barrier();
   bool sep_f = true;
@@ -79,15 +108,6 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
       tabR[i] = n < 28 ? col_pair4(axis_col(th, C, C, 28, 28, n), C)
                        : axis4(axis_row(th, C, C, 28, 28, n - 28), 4 * C);
     }
-  }
-  {  // eps_z of the tile -> LDS (contiguous [nb][50] rows, 16-byte loads), used in the sample phase
-    float* sEz = reinterpret_cast<float*>(arena + Ly::OFF_EZ);
-    const float4* src = reinterpret_cast<const float4*>(p.eps_z + (size_t)b0 * 50);
-    const bool al = ((reinterpret_cast<size_t>(p.eps_z) & 15) == 0);
-    if (al)
-      for (int i = tid; i < nb * 50 / 4; i += NTHR) reinterpret_cast<float4*>(sEz)[i] = src[i];
-    for (int i = (al ? nb * 50 / 4 * 4 : 0) + tid; i < nb * 50; i += NTHR)
-      sEz[i] = p.eps_z[(size_t)b0 * 50 + i];
   }
   const bool all_sep = __syncthreads_and(sep_f) != 0;  // (no global stores issued yet)
   STAMP(0);
@@ -447,16 +467,34 @@ __global__ __launch_bounds__(1024, 1) void stn_vae_step_f32_kernel(StepArgsF p) 
   const int C = p.C, C2 = C * C;
   STAMP(11);
   // ---- prologue: the bf16 kernel's (thetas, masks, read tables, eps_z) -----
-  for (int i = tid; i < M * 12; i += NTHR) {
-    const int m = i / 12, k = i % 12;
-    float v = 0.0f;
-    if (m < nb) v = k < 6 ? p.theta_f[(size_t)(b0 + m) * 6 + k] : p.theta_b[(size_t)(b0 + m) * 6 + k - 6];
-    sth[m][k] = v;
+  // every global load issued up front from clamped indices (one latency)
+  constexpr int TH_IT = (M * 12 + NTHR - 1) / NTHR;
+  constexpr int EZ_IT = (M * 50 + NTHR - 1) / NTHR;
+  float thv[TH_IT], ezv[EZ_IT];
+#pragma unroll
+  for (int j = 0; j < TH_IT; ++j) {
+    const int i = tid + j * NTHR, m = min(i / 12, nb - 1), k = i % 12;
+    thv[j] = k < 6 ? p.theta_f[(size_t)(b0 + m) * 6 + k] : p.theta_b[(size_t)(b0 + m) * 6 + k - 6];
+  }
+  const int tc = min(tid, nb - 1);
+  const float mk = p.mask[b0 + tc], zv = p.zval[b0 + tc];
+#pragma unroll
+  for (int j = 0; j < EZ_IT; ++j) ezv[j] = p.eps_z[(size_t)b0 * 50 + min(tid + j * NTHR, nb * 50 - 1)];
+#pragma unroll
+  for (int j = 0; j < TH_IT; ++j) {
+    const int i = tid + j * NTHR;
+    if (i < M * 12) sth[i / 12][i % 12] = i / 12 < nb ? thv[j] : 0.0f;
   }
   if (tid < M) {
-    const bool act = tid < nb && p.mask[b0 + tid] != 0.0f;
+    const bool act = tid < nb && mk != 0.0f;
     smask[tid] = act;
-    szv[tid] = act ? p.zval[b0 + tid] : 0.0f;
+    szv[tid] = act ? zv : 0.0f;
+  }
+  {
+    float* sEz = reinterpret_cast<float*>(arena + LayF::OFF_EZ);
+#pragma unroll
+    for (int j = 0; j < EZ_IT; ++j)
+      if (tid + j * NTHR < nb * 50) sEz[tid + j * NTHR] = ezv[j];
   }
   lds_barrier();
   bool sep_f = true;
@@ -472,10 +510,6 @@ __global__ __launch_bounds__(1024, 1) void stn_vae_step_f32_kernel(StepArgsF p) 
       tabR[i] = n < 28 ? col_pair4(axis_col(th, C, C, 28, 28, n), C)
                        : axis4(axis_row(th, C, C, 28, 28, n - 28), 4 * C);
     }
-  }
-  {
-    float* sEz = reinterpret_cast<float*>(arena + LayF::OFF_EZ);
-    for (int i = tid; i < nb * 50; i += NTHR) sEz[i] = p.eps_z[(size_t)b0 * 50 + i];
   }
   const bool all_sep = __syncthreads_and(sep_f) != 0;
   STAMP(0);
