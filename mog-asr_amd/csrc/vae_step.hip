@@ -218,6 +218,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
   lds_barrier();
   if (tid < nb) {  // sequential KL sum per image (k order, as vae_sample_fwd_kernel)
     const int m = tid;
+    // (the running loss read before the sum: its latency under the adds)
+    const float rl = p.runloss ? p.runloss[b0 + m] : 0.0f;
     float t[50];
 #pragma unroll
     for (int k = 0; k < 50; ++k) t[k] = sKl[m * 50 + k];
@@ -226,7 +228,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void stn_vae_step_kernel(StepArgs p) 
     for (int k = 0; k < 50; ++k) sum = sum + t[k];
     const float vkl = 0.5f * sum;
     p.vkl[b0 + m] = vkl;
-    if (p.runloss && smask[m]) p.runloss[b0 + m] = p.runloss[b0 + m] + vkl;
+    if (p.runloss && smask[m]) p.runloss[b0 + m] = rl + vkl;
   }
   STAMP(5);
   // ---- 6. d1 = softplus(z Wg1 + b)  [M x 256] (over mu | lv) ---------------
@@ -716,11 +718,12 @@ __global__ __launch_bounds__(1024, 1) void stn_vae_step_f32_kernel(StepArgsF p) 
   lds_barrier();
   if (tid < nb) {  // sequential KL sum per image (k order, as vae_sample_fwd_kernel)
     const int m = tid;
+    const float rl = p.runloss ? p.runloss[b0 + m] : 0.0f;  // (latency under the sum)
     float sum = 0.0f;
     for (int k = 0; k < 50; ++k) sum = sum + sKl[m * 50 + k];
     const float vkl = 0.5f * sum;
     p.vkl[b0 + m] = vkl;
-    if (p.runloss && smask[m]) p.runloss[b0 + m] = p.runloss[b0 + m] + vkl;
+    if (p.runloss && smask[m]) p.runloss[b0 + m] = rl + vkl;
   }
   STAMP(5);
   // ---- 6. d1 = softplus(z Wg1 + b) [M x 256] -> R2 (K = 50 padded to 64) --

@@ -185,15 +185,16 @@ __device__ __forceinline__ void st_stream(T* p, T v) {
   __builtin_nontemporal_store(v, p);
 }
 
-// bias[n0 .. n0+3] (0 past N)
+// bias[n0 .. n0+3] (0 past N): four loads from clamped indices, selected
+// afterwards (a branch between a vector and a scalar form compiled to a load
+// under exec masking with a vmcnt(0) wait inside it)
 __device__ __forceinline__ floatx4 load_bias4(const float* __restrict__ bias, int n0, int N) {
-  if (n0 + 4 <= N) {
-    const float4 b = *reinterpret_cast<const float4*>(bias + n0);
-    return floatx4{b.x, b.y, b.z, b.w};
-  }
   floatx4 b;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) b[k] = n0 + k < N ? bias[n0 + k] : 0.0f;
+  for (int k = 0; k < 4; ++k) {
+    const float v = bias[min(n0 + k, N - 1)];
+    b[k] = n0 + k < N ? v : 0.0f;
+  }
   return b;
 }
 
