@@ -193,6 +193,19 @@ __global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp,
   const int head = j == 0 ? 0 : j == 1 ? 1 : j <= 3 ? 2 : j <= 5 ? 3 : 4;
   const int col = (j == 3 || j == 5) ? 1 : 0;
   const int kw = (head == 2 || head == 3) ? 2 : 1;
+  // every per-image input loaded up front, before the head dot chains (from
+  // a clamped image index, by every lane): the outputs below are stores
+  // through pointers the compiler must assume may alias them, so a load
+  // issued after a store waits for it, and loads behind the dot chains and the
+  // early return would add a memory round trip after them -- at small batches
+  // (one or two workgroups) those round trips are the kernel's time
+  const int bc = min(b, B - 1);
+  const float e_s = io.eps_scale[bc], e_h0 = io.eps_shift[2 * bc], e_h1 = io.eps_shift[2 * bc + 1];
+  const float uu = io.u[bc];
+  const int live = io.live[cfg.step];
+  const float stop_old = io.stop[bc];
+  const float rl0 = io.runloss[bc];
+  const int dig = io.digits[bc];
   float v = 0.0f;
   if (b < B && j < 7) {
     const int K = head == 4 ? HZ : HS;
@@ -203,16 +216,6 @@ __global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp,
   const float hv0 = __shfl(v, 4, 8), hv1 = __shfl(v, 5, 8);
   const float lo = __shfl(v, 6, 8);
   if (b >= B || j != 0) return;
-  // every per-image input loaded up front: the outputs below are stores
-  // through pointers the compiler must assume may alias them, so a load
-  // issued after a store waits for it -- at small batches (one or two
-  // workgroups) those serialized memory round trips were the kernel's time
-  const float e_s = io.eps_scale[b], e_h0 = io.eps_shift[2 * b], e_h1 = io.eps_shift[2 * b + 1];
-  const float uu = io.u[b];
-  const int live = io.live[cfg.step];
-  const float stop_old = io.stop[b];
-  const float rl0 = io.runloss[b];
-  const int dig = io.digits[b];
 
   // scale / shift sampling (air_model.py:471-477, :492-498; :186-192)
   const float svar = mog_expf(slv);
