@@ -1,7 +1,7 @@
 """Stand-alone timing of the NT x3 GEMM (dX = dY W^T, the fp32 VAE input
-gradients) at the train step's shapes, HIP events; the form is chosen by the
-environment (MOG_X3NT_PD), so run once per form.  Prints the max error against
-float64 relative to sum |a||b| as well."""
+gradients) at the train step's shapes, HIP events; MOG_AIR_LIB points at
+another build for A/B.  Prints the max error against float64 relative to
+sum |a||b| as well."""
 import os
 import sys
 
@@ -45,7 +45,7 @@ def nt(M, N, K, epi):
         ref, mag = ref * s, mag * s
     err = ((C[r].double() - ref).abs() / mag).max().item()
     fl = 2.0 * M * N * K * 6
-    print(f"NT pd={os.environ.get('MOG_X3NT_PD', '1')} M={M} N={N} K={K} epi={epi}: {us:.1f} us "
+    print(f"NT M={M} N={N} K={K} epi={epi}: {us:.1f} us "
           f"({fl / us / 1e6:.0f} TF bf16 = {fl / us / 1e6 / 2500:.2f} of peak), err {err:.1e}",
           flush=True)
 
