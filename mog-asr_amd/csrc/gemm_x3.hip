@@ -444,8 +444,12 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
   // an offset past every range, on both operands.  B rows >= N load the next
   // piece's rows or 0 past the last piece: they only reach output columns >= N,
   // which are not stored.
+  // record ranges: the panel's rows, ending at column K (or N) of the
+  // operand's last row -- its validated extent
+  const int arows = min(M - m0, BM);
   const __amdgpu_buffer_rsrc_t arsc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(D.A) + (size_t)m0 * D.lda, 0, min(M - m0, BM) * D.lda * 4, 0x00020000);
+      const_cast<float*>(D.A) + (size_t)m0 * D.lda, 0,
+      (M - m0 > BM ? BM * D.lda : (arows - 1) * D.lda + K) * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t brsc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<__bf16*>(D.B3), 0, (int)((2 * D.sb + (long)N * D.ldb) * 2), 0x00020000);
   const int avo = (ar * D.lda + ak) * 4;
@@ -526,8 +530,8 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
   u32x4 xq[4][4];
   if constexpr (EPI == 1) {
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(D.aux) + (size_t)m0 * D.ldaux, 0, min(M - m0, BM) * D.ldaux * 4,
-        0x00020000);
+        const_cast<float*>(D.aux) + (size_t)m0 * D.ldaux, 0,
+        (M - m0 > BM ? BM * D.ldaux : (arows - 1) * D.ldaux + N) * 4, 0x00020000);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll

@@ -722,10 +722,13 @@ class AIRModel:
         # measured slower in round 2: 3.74 -> 3.81 ms).
         # (measured: forking them after the STN read backward instead, so that
         # kernel runs alone, leaves the step unchanged -- 3.53 ms either way)
-        w1_done, vae_done = self._vae_weight_grads_async(ws)
+        if not self.FORK_AFTER_READ:
+            w1_done, vae_done = self._vae_weight_grads_async(ws)
         # STN read backward of all steps against the shared input canvas
         ops.stn_backward(X, ws.th_f, (W, W), ws.dg_all, want_dU=False, dtheta=ws.dth_f_all,
                          n=TB)
+        if self.FORK_AFTER_READ:
+            w1_done, vae_done = self._vae_weight_grads_async(ws)
         for t in range(T):
             hid_t = [ws.hid[z, t] for z in range(5)]
             _ops.air_step_backward_(
@@ -776,6 +779,11 @@ class AIRModel:
         self._weight_grads_lstm(X, ws, side=heads_side)
         if heads_side:  # (everything on the side stream: VAE, heads, dW_rec)
             torch.cuda.current_stream().wait_stream(self._side_stream())
+
+    # the side stream's weight gradients forked after the STN read backward
+    # (which then runs alone) instead of before it (MOG_FORK_AFTER_READ=1;
+    # measured neutral in round 4: 3.097 / 3.094 vs 3.098 / 3.097 ms)
+    FORK_AFTER_READ = os.environ.get("MOG_FORK_AFTER_READ", "0") == "1"
 
     # single GPU: heads' weight gradients on the side stream (see _backward)
     HEADS_WGRAD_SIDE = os.environ.get("MOG_HEADS_SIDE", "1") == "1"
