@@ -1,5 +1,7 @@
 #!/bin/bash
-# STN backward at 4 waves / SIMD (11 VGPRs spilled) vs 3 (no spill): stand-alone and in the fp32 step
+# STN backward at 4 waves / SIMD (11 VGPRs spilled) vs 3 (no spill): stand-alone and in the fp32 step.
+# The A/B library is built beforehand, in mog-asr_amd/: stn.hip with __launch_bounds__(256, 3) on
+# stn_bwd_kernel compiled to an object and linked with the other build/*.o into build_ab/libmog_air.so
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
