@@ -1115,10 +1115,11 @@ class AIRModel:
     # small-M tiles finish first
     X3_MIN_ROWS = 2048
     # the NT input-gradient form from this many rows (the AIR step's T*B =
-    # 24,576): at the ASR step's per-step 8,192 rows its 128 x 128 tiles give
-    # one workgroup per CU and the fp32 GEMM is faster (ASR fp32 step 9.6 ->
-    # 10.1 ms with it)
-    X3_DX_MIN_ROWS = 16384
+    # 24,576 and the ASR step's per-step 8,192): below it its 128 x 128 tiles
+    # leave CUs idle and the fp32 GEMM finishes first.  (Round 4, after the
+    # NT load fixes: ASR fp32 step 9.46 -> 9.43 ms with 8,192 in; before
+    # them the NT form lost there, 9.6 -> 10.1 ms.)
+    X3_DX_MIN_ROWS = int(os.environ.get("MOG_X3_DX_MIN_ROWS", "8192"))
 
     def _dw_x3(self, X, dY, out, K, M, N, lda, ldb, bias_out):
         """out[M,N] += X^T dY over K rows (gemm_x3_tn), bias_out += colsum(dY)."""
