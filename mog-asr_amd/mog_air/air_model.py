@@ -752,7 +752,9 @@ class AIRModel:
             # one GPU, no bucket to hand over: the heads' weight gradients
             # follow the VAE's on the side stream, under the latency-bound
             # LSTM chain; the main stream joins them before Adam
-            main, side = torch.cuda.current_stream(), self._side_stream()
+            # (on a third stream, beside the VAE's: HEADS_STREAM3)
+            main = torch.cuda.current_stream()
+            side = self._stream3() if self.HEADS_STREAM3 else self._side_stream()
             heads_ready = torch.cuda.Event()
             heads_ready.record(main)
             side.wait_event(heads_ready)
@@ -779,6 +781,8 @@ class AIRModel:
         self._weight_grads_lstm(X, ws, side=heads_side)
         if heads_side:  # (everything on the side stream: VAE, heads, dW_rec)
             torch.cuda.current_stream().wait_stream(self._side_stream())
+            if self.HEADS_STREAM3 or self.REC_STREAM3:
+                torch.cuda.current_stream().wait_stream(self._stream3())
 
     # the side stream's weight gradients forked after the STN read backward
     # (which then runs alone) instead of before it (MOG_FORK_AFTER_READ=1;
@@ -1197,6 +1201,19 @@ class AIRModel:
             self._hp = torch.cuda.Stream(device=self.device, priority=min(lo, hi))
         return self._hp
 
+    # one GPU, from SIDE_MIN_BATCH: the heads' weight gradients on a third
+    # stream, beside the VAE's instead of queued after them (fp32 step 3.10 /
+    # 3.10 -> 3.05 / 3.07 ms; MOG_HEADS_STREAM3=0: after them on the side stream)
+    HEADS_STREAM3 = os.environ.get("MOG_HEADS_STREAM3", "1") == "1"
+    # ... and the recurrent rows' gradient after them there (3.06 / 3.08 ->
+    # 3.04 / 3.04 ms; MOG_REC_STREAM3=0: on the side stream)
+    REC_STREAM3 = os.environ.get("MOG_REC_STREAM3", "1") == "1"
+
+    def _stream3(self):
+        if getattr(self, "_s3", None) is None:
+            self._s3 = torch.cuda.Stream(device=self.device)
+        return self._s3
+
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(device=self.device)
@@ -1275,7 +1292,8 @@ class AIRModel:
         if T > 1 and side and self.REC_WGRAD_SIDE:
             # one GPU: the recurrent rows' gradient on the side stream, beside
             # the x-rows gradient below (both need only the finished chain)
-            main, st = torch.cuda.current_stream(), self._side_stream()
+            main = torch.cuda.current_stream()
+            st = self._stream3() if self.REC_STREAM3 else self._side_stream()
             ev = torch.cuda.Event()
             ev.record(main)
             st.wait_event(ev)
