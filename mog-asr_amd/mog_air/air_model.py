@@ -86,6 +86,24 @@ def marginal_objective(num_prior, max_steps) -> np.ndarray:
     return obj.astype(np.float32)
 
 
+_STREAMS: Dict[torch.device, tuple] = {}
+
+
+def _shared_streams(device):
+    """The side stream and the third stream of AIRModel, created once per
+    process and device.  HIP places a stream on one of its GPU_MAX_HW_QUEUES
+    (4) hardware queues when the stream is created; with a pair created per
+    model, every other model of a process had both on ONE queue, which
+    serialised the third stream behind the side stream (fp32 step 3.09 ->
+    3.43 ms, bf16 2.09 -> 2.29 ms; scripts/gpu_slot_trace.sh: queues 2 / 3 for
+    the first model, 4 / 4 for the second).  The first pair of a process sits
+    on two queues of its own, and every model now uses it."""
+    key = torch.device(device)
+    if key not in _STREAMS:
+        _STREAMS[key] = (torch.cuda.Stream(device=key), torch.cuda.Stream(device=key))
+    return _STREAMS[key]
+
+
 class _Workspace:
     """All per-batch device buffers of one train step (HBM-resident, reused).
     Buffers in ZERO_PADDED carry zero pad columns written once at allocation
@@ -415,6 +433,11 @@ class AIRModel:
     # AIR's _forward joins side-stream noise after the x-projection (the ASR
     # subclass fills on the current stream)
     NOISE_ON_SIDE = True
+    # the x3 input gradients' weight pieces split in that side-stream prologue
+    # instead of on the backward's path (fp32 step 3.05 -> 3.02 ms).  Moving
+    # the gradient zeroing there too was measured and dropped: the step-
+    # gradient x3 test then failed 2 runs in 6 at ~2e-5 (in 6 runs without it: none)
+    EARLY_PREP = os.environ.get("MOG_EARLY_PREP", "1") == "1"
 
     # ----------------------------------------------------------- forward ---
     def _forward(self, X: torch.Tensor, targets: Optional[torch.Tensor], ws: _Workspace,
@@ -445,6 +468,9 @@ class AIRModel:
                 if getattr(ws, "X3", None) is None:
                     ws.X3 = torch.empty((3, B, C2p), device=self.device, dtype=torch.bfloat16)
                 ops.split3_bf16(X, ws.X3, B, C2, C2, C2p, B * C2p)
+            if (need_grad and self.EARLY_PREP and self.precision == "fp32" and self.VAE_DX_X3
+                    and B * self.max_steps >= self.X3_DX_MIN_ROWS):
+                self._w3()  # the x3 input gradients' weight pieces, off the backward's path
             if side is not None:
                 pre_done = torch.cuda.Event()
                 pre_done.record(side)
@@ -1209,14 +1235,20 @@ class AIRModel:
     # 3.04 / 3.04 ms; MOG_REC_STREAM3=0: on the side stream)
     REC_STREAM3 = os.environ.get("MOG_REC_STREAM3", "1") == "1"
 
+    # the side and third streams created once per process and device, shared
+    # by every model (see _shared_streams; MOG_SHARED_STREAMS=0: per model)
+    SHARED_STREAMS = os.environ.get("MOG_SHARED_STREAMS", "1") == "1"
+
     def _stream3(self):
         if getattr(self, "_s3", None) is None:
-            self._s3 = torch.cuda.Stream(device=self.device)
+            self._s3 = _shared_streams(self.device)[1] if self.SHARED_STREAMS else \
+                torch.cuda.Stream(device=self.device)
         return self._s3
 
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            self._side = _shared_streams(self.device)[0] if self.SHARED_STREAMS else \
+                torch.cuda.Stream(device=self.device)
         return self._side
 
     def _vae_weight_grads_async(self, ws):

@@ -6,6 +6,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "mog-asr_amd")]
+import torch  # noqa: E402
+
 import bench  # noqa: E402
 from mog_air.air_model import AIRModel  # noqa: E402
 
@@ -24,4 +26,6 @@ for rep in range(2):
             el, m = bench.timed_train(prec, 8192, 10, 3, dev, scope="ab", canvas=canvas, data=data)
             res.append(f"{prec} C{canvas} {el / 10 * 1e3:.3f}")
             del m
+            if os.environ.get("MOG_AB_EMPTY") == "1":
+                torch.cuda.empty_cache()
         print(rep, s or "defaults", "; ".join(res), flush=True)

@@ -9,3 +9,4 @@ timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trg
 grep "ms/step" gpurun_out/trg64.log
 f=$(ls gpurun_out/trg64/*kernel_trace.csv gpurun_out/trg64/*/*kernel_trace.csv 2>/dev/null | head -1)
 python3 scripts/prof_step.py "$f" > gpurun_out/step64g.txt && cat gpurun_out/step64g.txt
+python3 scripts/step_timeline.py "$f" > gpurun_out/step64g_timeline.txt
