@@ -1159,25 +1159,32 @@ class AIRModel:
         splitk = max(1, min(K // 256, (512 + tiles - 1) // tiles))
         ops.gemm_x3_tn(X, dY, out, M, N, K, lda, ldb, N, splitk=splitk, colsum=bias_out)
 
-    def _vae_wgrad_fp32(self, ws, name):
-        """One VAE layer's weight / bias gradient over all T*B rows (fp32)."""
+    def _vae_wgrad_fp32(self, ws, name, t=None):
+        """One VAE layer's weight / bias gradient over all T*B rows (fp32), or
+        over loop step t's B rows (accumulated: the per-step form of AIR-ASR)."""
         TB = ws.B * self.max_steps
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
         gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
+        if t is None:
+            v = lambda x: x  # noqa: E731
+        else:
+            TB = ws.B
+            v = lambda x: x[t]  # noqa: E731
         if name == "recognition_1":
-            self._dw_x3(ws.g, ws.da1, g(name), TB, W2, R1, W2, R1, gb(name))
+            self._dw_x3(v(ws.g), v(ws.da1), g(name), TB, W2, R1, W2, R1, gb(name))
         elif name == "recognition_2":
-            self._dw_x3(ws.a1, ws.da2, g(name), TB, R1, R2, R1, R2, gb(name))
+            self._dw_x3(v(ws.a1), v(ws.da2), g(name), TB, R1, R2, R1, R2, gb(name))
         elif name == "rec_mean":  # (with rec_log_variance: one batched launch)
-            self._dw([ws.a2] * 2, [ws.dmu, ws.dlv], [g("rec_mean"), g("rec_log_variance")], TB,
-                     R2, Z, R2, Z, [gb("rec_mean"), gb("rec_log_variance")])
+            self._dw([v(ws.a2)] * 2, [v(ws.dmu), v(ws.dlv)], [g("rec_mean"),
+                     g("rec_log_variance")], TB, R2, Z, R2, Z,
+                     [gb("rec_mean"), gb("rec_log_variance")])
         elif name == "generative_1":
-            self._dw(ws.z, ws.dd1, g(name), TB, Z, G1, Z, G1, gb(name))
+            self._dw(v(ws.z), v(ws.dd1), g(name), TB, Z, G1, Z, G1, gb(name))
         elif name == "generative_2":
-            self._dw_x3(ws.d1, ws.dd2, g(name), TB, G1, G2, G1, G2, gb(name))
+            self._dw_x3(v(ws.d1), v(ws.dd2), g(name), TB, G1, G2, G1, G2, gb(name))
         elif name == "gen_mean":
-            self._dw_x3(ws.d2, ws.dm, g(name), TB, G2, W2, G2, W2, gb(name))
+            self._dw_x3(v(ws.d2), v(ws.dm), g(name), TB, G2, W2, G2, W2, gb(name))
 
     def _vae_weight_grads_fp32(self, ws):
         early = getattr(ws, "early_wgrads", None) or ()

@@ -464,6 +464,11 @@ class AIRModel(_AirBase):
                                                      "z_pres/log_odds/dense", "inf_scale/dense",
                                                      "inf_scale/dense_2")]
         gen_w = [self._N(n + "/kernel") for n in ("gen_shift/dense", "gen_shift/dense_2")]
+        steps_side = (self.VAE_WGRAD_PER_STEP and self.precision == "fp32"
+                      and self.grad_reducer is None and B >= self.SIDE_MIN_BATCH)
+        side = self._side_stream() if steps_side else None
+        ws.vae_wgrads_done = steps_side
+        ws.u_wgrads_done = steps_side and self.U_WGRAD_PER_STEP
         for t in reversed(range(T)):
             ops.stn_backward(ws.r[t], ws.th_b[t], (C, C), ws.dcanvas, gscale=ws.zc[t],
                              dU=ws.dr, dtheta=ws.dth_b, dot=ws.dot, want_dot=True)
@@ -471,6 +476,15 @@ class AIRModel(_AirBase):
                 self._vae_backward_bf16(ws, t, gscale)
             else:
                 self._vae_backward_fp32(ws, t, gscale)
+                if steps_side:
+                    # step t's VAE weight gradients are final: accumulate them
+                    # on the side stream under the rest of the loop
+                    ready = torch.cuda.Event()
+                    ready.record(torch.cuda.current_stream())
+                    side.wait_event(ready)
+                    with torch.cuda.stream(side):
+                        for name in self._VAE_WGRAD_LAYERS:
+                            self._vae_wgrad_fp32(ws, name, t)
             ops.stn_backward(X, ws.th_f[t], (W, W), ws.dg, want_dU=False, dtheta=ws.dth_f)
             hid = [ws.hid8[k, t] for k in range(8)]
             dpre = [ws.dpre[k, t] for k in range(8)]
@@ -497,6 +511,13 @@ class AIRModel(_AirBase):
             dcg_in = ws.dcg[(t + 1) % 2] if t < T - 1 else None
             _ops.lstm_cell_backward_(ws.Gg[t], None, ws.cg[t - 1] if t > 0 else None, ws.cg[t],
                                      ws.dhg[t], dcg_in, ws.dGg[t], ws.dcg[t % 2], ws.dGgsum, B, H)
+            if steps_side and self.U_WGRAD_PER_STEP:
+                # step t's recurrent-rows gradients likewise (dG_t, dGg_t final)
+                ready = torch.cuda.Event()
+                ready.record(torch.cuda.current_stream())
+                side.wait_event(ready)
+                with torch.cuda.stream(side):
+                    self._u_rows_wgrad(ws, t)
             if t > 0:
                 # N = LU: the 3 pad columns of dU / dUg are scratch (unpack skips them)
                 gemm([ws.dG[t]], [Ki[C2:]], [ws.dU], B, LU, 4 * H, 4 * H, 4 * H, LU,
@@ -505,7 +526,32 @@ class AIRModel(_AirBase):
                 _ops.asr_unpack_(B, Z, H, LU, ws.dU, ws.dUg, ws.dz_carry, ws.dss_carry,
                                  ws.dh[t - 1], ws.dhg[t - 1])
         self._weight_grads(X, ws)
+        if steps_side:
+            torch.cuda.current_stream().wait_stream(side)
         self._reduce_bucket(0, self.params.total)
+
+    def _u_rows_wgrad(self, ws, t):
+        """The LSTMCells' recurrent-rows kernel gradients U^T dG (all T*B rows,
+        or loop step t's B rows, accumulated)."""
+        B, T, H = ws.B, self.max_steps, self.rnn_units
+        K = B if t is not None else B * T
+        v = (lambda x: x[t]) if t is not None else (lambda x: x)  # noqa: E731
+        gKi = self._Kpad("infer_rnn_running/kernel", "grad")
+        gKg = self._Kpad("gen_rnn_running/kernel", "grad")
+        self._dw(v(ws.U), v(ws.dG), gKi[self.C2:], K, LU, 4 * H, LU, 4 * H)
+        self._dw(v(ws.Ug), v(ws.dGg), gKg, K, LU, 4 * H, LU, 4 * H,
+                 self._Ng("gen_rnn_running/bias"))
+
+    # (with VAE_WGRAD_PER_STEP) the recurrent-rows gradients per step too
+    U_WGRAD_PER_STEP = os.environ.get("MOG_ASR_UGRAD_STEPS", "1") == "1"
+
+    # fp32, one GPU, from SIDE_MIN_BATCH: the VAE weight gradients of loop step
+    # t accumulate on the side stream as soon as that step's VAE backward is
+    # done, under the latency-bound rest of the reversed loop, instead of over
+    # all T*B rows after it (MOG_ASR_WGRAD_STEPS=0: after the loop)
+    VAE_WGRAD_PER_STEP = os.environ.get("MOG_ASR_WGRAD_STEPS", "1") == "1"
+    _VAE_WGRAD_LAYERS = ("recognition_1", "recognition_2", "rec_mean", "generative_1",
+                         "generative_2", "gen_mean")
 
     def _weight_grads(self, X, ws):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
@@ -513,8 +559,9 @@ class AIRModel(_AirBase):
         fix = -1 if self.fix_steps is None else int(self.fix_steps)
         if self.precision == "bf16":
             self._vae_weight_grads_bf16(ws)
-        else:
+        elif not getattr(ws, "vae_wgrads_done", False):
             self._vae_weight_grads_fp32(ws)
+        ws.vae_wgrads_done = False
         G = self._Ng
         gKi = self._Kpad("infer_rnn_running/kernel", "grad")
         gKg = self._Kpad("gen_rnn_running/kernel", "grad")
@@ -541,8 +588,9 @@ class AIRModel(_AirBase):
         # M = LU (16-byte aligned LDS-DMA operands): rows Z+3+H.. of the
         # product land in the kernels' own pad rows (ParamStore pad), never in
         # a neighbouring variable's gradient
-        self._dw(ws.U, ws.dG, gKi[C2:], TB, LU, 4 * H, LU, 4 * H)
-        self._dw(ws.Ug, ws.dGg, gKg, TB, LU, 4 * H, LU, 4 * H, G("gen_rnn_running/bias"))
+        if not getattr(ws, "u_wgrads_done", False):
+            self._u_rows_wgrad(ws, None)
+        ws.u_wgrads_done = False
         # hidden layers reading h_t, hg_t, hg_{t-1}
         hs = ("inf_shift/dense", "inf_shift/dense_2", "z_pres/log_odds/dense", "inf_scale/dense",
               "inf_scale/dense_2")
