@@ -1103,23 +1103,27 @@ class AIRModel:
         gemm_bf16([X], [dY], [out], M, N, K, lda, ldb, N, tn=True, epi=BF_ATOMIC,
                   splitk=splitk, colsum=[bias_out])
 
-    def _vae_weight_grads_bf16(self, ws):
-        TB = ws.B * self.max_steps
+    def _vae_weight_grads_bf16(self, ws, t=None):
+        """The VAE weight gradients over all T*B rows (bf16 operands), or over
+        loop step t's B rows (accumulated: the per-step form of AIR-ASR)."""
+        TB = ws.B * self.max_steps if t is None else ws.B
+        v = (lambda x: x) if t is None else (lambda x: x[t])  # noqa: E731
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         Zp = self._pad8(Z)
         g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
         gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
-        self._dw_bf16(ws.gb, ws.da1b, g("recognition_1"), TB, W2, R1, W2, R1,
+        self._dw_bf16(v(ws.gb), v(ws.da1b), g("recognition_1"), TB, W2, R1, W2, R1,
                       gb("recognition_1"))
-        self._dw_bf16(ws.a1b, ws.da2b, g("recognition_2"), TB, R1, R2, R1, R2,
+        self._dw_bf16(v(ws.a1b), v(ws.da2b), g("recognition_2"), TB, R1, R2, R1, R2,
                       gb("recognition_2"))
-        self._dw_bf16(ws.a2b, ws.dmub, g("rec_mean"), TB, R2, Z, R2, Zp, gb("rec_mean"))
-        self._dw_bf16(ws.a2b, ws.dlvb, g("rec_log_variance"), TB, R2, Z, R2, Zp,
+        self._dw_bf16(v(ws.a2b), v(ws.dmub), g("rec_mean"), TB, R2, Z, R2, Zp, gb("rec_mean"))
+        self._dw_bf16(v(ws.a2b), v(ws.dlvb), g("rec_log_variance"), TB, R2, Z, R2, Zp,
                       gb("rec_log_variance"))
-        self._dw_bf16(ws.zb, ws.dd1b, g("generative_1"), TB, Z, G1, Zp, G1, gb("generative_1"))
-        self._dw_bf16(ws.d1b, ws.dd2b, g("generative_2"), TB, G1, G2, G1, G2,
+        self._dw_bf16(v(ws.zb), v(ws.dd1b), g("generative_1"), TB, Z, G1, Zp, G1,
+                      gb("generative_1"))
+        self._dw_bf16(v(ws.d1b), v(ws.dd2b), g("generative_2"), TB, G1, G2, G1, G2,
                       gb("generative_2"))
-        self._dw_bf16(ws.d2b, ws.dmb, g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
+        self._dw_bf16(v(ws.d2b), v(ws.dmb), g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
 
     def _dw(self, X, dY, out, K, M, N, lda, ldb, bias_out=None):
         """out[M,N] += X^T dY over K rows (split-K, atomics); bias_out += colsum(dY).

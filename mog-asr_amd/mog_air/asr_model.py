@@ -464,8 +464,8 @@ class AIRModel(_AirBase):
                                                      "z_pres/log_odds/dense", "inf_scale/dense",
                                                      "inf_scale/dense_2")]
         gen_w = [self._N(n + "/kernel") for n in ("gen_shift/dense", "gen_shift/dense_2")]
-        steps_side = (self.VAE_WGRAD_PER_STEP and self.precision == "fp32"
-                      and self.grad_reducer is None and B >= self.SIDE_MIN_BATCH)
+        steps_side = (self.VAE_WGRAD_PER_STEP and self.grad_reducer is None
+                      and B >= self.SIDE_MIN_BATCH)
         side = self._side_stream() if steps_side else None
         ws.vae_wgrads_done = steps_side
         ws.u_wgrads_done = steps_side and self.U_WGRAD_PER_STEP
@@ -476,13 +476,16 @@ class AIRModel(_AirBase):
                 self._vae_backward_bf16(ws, t, gscale)
             else:
                 self._vae_backward_fp32(ws, t, gscale)
-                if steps_side:
-                    # step t's VAE weight gradients are final: accumulate them
-                    # on the side stream under the rest of the loop
-                    ready = torch.cuda.Event()
-                    ready.record(torch.cuda.current_stream())
-                    side.wait_event(ready)
-                    with torch.cuda.stream(side):
+            if steps_side:
+                # step t's VAE weight gradients are final: accumulate them on
+                # the side stream under the rest of the loop
+                ready = torch.cuda.Event()
+                ready.record(torch.cuda.current_stream())
+                side.wait_event(ready)
+                with torch.cuda.stream(side):
+                    if self.precision == "bf16":
+                        self._vae_weight_grads_bf16(ws, t)
+                    else:
                         for name in self._VAE_WGRAD_LAYERS:
                             self._vae_wgrad_fp32(ws, name, t)
             ops.stn_backward(X, ws.th_f[t], (W, W), ws.dg, want_dU=False, dtheta=ws.dth_f)
@@ -542,10 +545,12 @@ class AIRModel(_AirBase):
         self._dw(v(ws.Ug), v(ws.dGg), gKg, K, LU, 4 * H, LU, 4 * H,
                  self._Ng("gen_rnn_running/bias"))
 
-    # (with VAE_WGRAD_PER_STEP) the recurrent-rows gradients per step too
+    # (with VAE_WGRAD_PER_STEP) the recurrent-rows gradients per step too (9.20 ->
+    # 8.96 ms; the heads' gradients per step as well measured neutral, 9.01 vs
+    # 9.26 ms for neither on a slower box, and stay after the loop)
     U_WGRAD_PER_STEP = os.environ.get("MOG_ASR_UGRAD_STEPS", "1") == "1"
 
-    # fp32, one GPU, from SIDE_MIN_BATCH: the VAE weight gradients of loop step
+    # one GPU, from SIDE_MIN_BATCH: the VAE weight gradients of loop step
     # t accumulate on the side stream as soon as that step's VAE backward is
     # done, under the latency-bound rest of the reversed loop, instead of over
     # all T*B rows after it (MOG_ASR_WGRAD_STEPS=0: after the loop)
@@ -557,9 +562,11 @@ class AIRModel(_AirBase):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
         C2, TB, KU = self.C2, ws.B * self.max_steps, Z + 3 + H
         fix = -1 if self.fix_steps is None else int(self.fix_steps)
-        if self.precision == "bf16":
+        if getattr(ws, "vae_wgrads_done", False):
+            pass  # (per loop step, on the side stream)
+        elif self.precision == "bf16":
             self._vae_weight_grads_bf16(ws)
-        elif not getattr(ws, "vae_wgrads_done", False):
+        else:
             self._vae_weight_grads_fp32(ws)
         ws.vae_wgrads_done = False
         G = self._Ng
@@ -591,44 +598,54 @@ class AIRModel(_AirBase):
         if not getattr(ws, "u_wgrads_done", False):
             self._u_rows_wgrad(ws, None)
         ws.u_wgrads_done = False
+        self._heads_wgrad(ws, None)
+
+    def _heads_wgrad(self, ws, t):
+        """The heads' weight gradients (all T*B rows, or loop step t's B rows,
+        accumulated)."""
+        B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
+        K = B if t is not None else B * T
+        v = (lambda x: x[t]) if t is not None else (lambda x: x)  # noqa: E731
+        G = self._Ng
+        fix = -1 if self.fix_steps is None else int(self.fix_steps)
         # hidden layers reading h_t, hg_t, hg_{t-1}
         hs = ("inf_shift/dense", "inf_shift/dense_2", "z_pres/log_odds/dense", "inf_scale/dense",
               "inf_scale/dense_2")
-        self._dw([ws.h] * 5, [ws.dpre[k] for k in (0, 1, 2, 6, 7)],
-                 [G(n + "/kernel")[:H] for n in hs], TB, H, 64, H, 64,
+        self._dw([v(ws.h)] * 5, [v(ws.dpre[k]) for k in (0, 1, 2, 6, 7)],
+                 [G(n + "/kernel")[:H] for n in hs], K, H, 64, H, 64,
                  [G(n + "/bias") for n in hs])
-        self._dw([ws.hg] * 2, [ws.dpre[3], ws.dpre[4]],
-                 [G("gen_shift/dense/kernel"), G("gen_shift/dense_2/kernel")], TB, H, 64, H, 64,
+        self._dw([v(ws.hg)] * 2, [v(ws.dpre[3]), v(ws.dpre[4])],
+                 [G("gen_shift/dense/kernel"), G("gen_shift/dense_2/kernel")], K, H, 64, H, 64,
                  [G("gen_shift/dense/bias"), G("gen_shift/dense_2/bias")])
         if fix < 0:
-            self._dw(ws.Ug[:, :, Z + 3:], ws.dpre[5], G("z_pres/prior/dense/kernel"), TB, H, 64,
+            self._dw(v(ws.Ug)[..., Z + 3:], v(ws.dpre[5]), G("z_pres/prior/dense/kernel"), K, H, 64,
                      LU, 64, G("z_pres/prior/dense/bias"))
         # the shift-latent rows of the scale hidden layers
-        self._dw([ws.ss] * 2, [ws.dpre[6], ws.dpre[7]],
-                 [G("inf_scale/dense/kernel")[H:], G("inf_scale/dense_2/kernel")[H:]], TB, 2, 64,
+        self._dw([v(ws.ss)] * 2, [v(ws.dpre[6]), v(ws.dpre[7])],
+                 [G("inf_scale/dense/kernel")[H:], G("inf_scale/dense_2/kernel")[H:]], K, 2, 64,
                  3, 64)
         # output layers from douts [T, B, 12]
-        d = ws.douts
+        d = v(ws.douts)
         outs = (("inf_shift/dense_1", 0, 0, 2), ("inf_shift/dense_3", 1, 2, 2),
                 ("z_pres/log_odds/dense_1", 2, 4, 1), ("gen_shift/dense_1", 3, 5, 2),
                 ("gen_shift/dense_3", 4, 7, 2))
         # grouped by shape, one batched launch per group (each is a tiny
         # [64 x 1..2] product over K = T*B rows: launch-bound one by one)
-        one = [(ws.hid8[hk], d[..., col:], G(n + "/kernel"), G(n + "/bias"))
+        one = [(v(ws.hid8[hk]), d[..., col:], G(n + "/kernel"), G(n + "/bias"))
                for n, hk, col, k in outs if k == 1]
-        two = [(ws.hid8[hk], d[..., col:], G(n + "/kernel"), G(n + "/bias"))
+        two = [(v(ws.hid8[hk]), d[..., col:], G(n + "/kernel"), G(n + "/bias"))
                for n, hk, col, k in outs if k == 2]
         if fix < 0:
-            one.append((ws.hid8[5], d[..., 9:], G("z_pres/prior/dense_1/kernel"),
+            one.append((v(ws.hid8[5]), d[..., 9:], G("z_pres/prior/dense_1/kernel"),
                         G("z_pres/prior/dense_1/bias")))
         scl = (("inf_scale/dense_1", 6, 10), ("inf_scale/dense_3", 7, 11))
-        one += [(ws.hid8[hk], d[..., col:], G(n + "/kernel")[:64], G(n + "/bias"))
+        one += [(v(ws.hid8[hk]), d[..., col:], G(n + "/kernel")[:64], G(n + "/bias"))
                 for n, hk, col in scl]
         for grp, k in ((two, 2), (one, 1)):
-            self._dw([g[0] for g in grp], [g[1] for g in grp], [g[2] for g in grp], TB, 64, k,
+            self._dw([g[0] for g in grp], [g[1] for g in grp], [g[2] for g in grp], K, 64, k,
                      64, D_N, [g[3] for g in grp])
-        self._dw([ws.ss] * 2, [d[..., col:] for _, _, col in scl],
-                 [G(n + "/kernel")[64:] for n, _, _ in scl], TB, 2, 1, 3, D_N)
+        self._dw([v(ws.ss)] * 2, [d[..., col:] for _, _, col in scl],
+                 [G(n + "/kernel")[64:] for n, _, _ in scl], K, 2, 1, 3, D_N)
 
     # ------------------------------------------------------- outputs -----
     @property
