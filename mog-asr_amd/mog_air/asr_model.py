@@ -562,6 +562,16 @@ class AIRModel(_AirBase):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
         C2, TB, KU = self.C2, ws.B * self.max_steps, Z + 3 + H
         fix = -1 if self.fix_steps is None else int(self.fix_steps)
+        heads_s3 = getattr(ws, "vae_wgrads_done", False) and self.HEADS_S3
+        if heads_s3:
+            # the heads' weight gradients on the third stream, beside the
+            # x-rows gradient (main) and step 0's on the side stream
+            s3 = self._stream3()
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream())
+            s3.wait_event(ready)
+            with torch.cuda.stream(s3):
+                self._heads_wgrad(ws, None)
         if getattr(ws, "vae_wgrads_done", False):
             pass  # (per loop step, on the side stream)
         elif self.precision == "bf16":
@@ -598,7 +608,13 @@ class AIRModel(_AirBase):
         if not getattr(ws, "u_wgrads_done", False):
             self._u_rows_wgrad(ws, None)
         ws.u_wgrads_done = False
-        self._heads_wgrad(ws, None)
+        if heads_s3:
+            torch.cuda.current_stream().wait_stream(self._stream3())
+        else:
+            self._heads_wgrad(ws, None)
+
+    # (with the per-step gradients) the heads' gradients on the third stream
+    HEADS_S3 = os.environ.get("MOG_ASR_HEADS_S3", "1") == "1"
 
     def _heads_wgrad(self, ws, t):
         """The heads' weight gradients (all T*B rows, or loop step t's B rows,
