@@ -383,8 +383,9 @@ class AIRModel(_AirBase):
             _ops.lstm_cell_forward_(ws.Gg[t], None, ws.cg[t - 1] if prev else None, ws.cg[t],
                                     ws.hg[t], B, H)
             hid = [ws.hid8[k, t] for k in range(8)]
-            gemm([ws.h[t]] * 3, relu_w, hid[0:3], B, 64, H, H, 64, 64, epi=EPI_RELU, bias=relu_b)
-            gemm([ws.hg[t]] * 2, gen_w, hid[3:5], B, 64, H, H, 64, 64, epi=EPI_RELU, bias=gen_b)
+            # (the inference and generative ReLU heads in one batched launch)
+            gemm([ws.h[t]] * 3 + [ws.hg[t]] * 2, list(relu_w) + list(gen_w), hid[0:5], B, 64, H,
+                 H, 64, 64, epi=EPI_RELU, bias=list(relu_b) + list(gen_b))
             if fix < 0:  # learned prior from the previous generative output (:596-602)
                 gemm([ws.Ug[t][:, Z + 3:]], [self._N("z_pres/prior/dense/kernel")], [hid[5]], B,
                      64, H, LU, 64, 64, epi=EPI_RELU, bias=[self._N("z_pres/prior/dense/bias")])
@@ -523,9 +524,9 @@ class AIRModel(_AirBase):
                     self._u_rows_wgrad(ws, t)
             if t > 0:
                 # N = LU: the 3 pad columns of dU / dUg are scratch (unpack skips them)
-                gemm([ws.dG[t]], [Ki[C2:]], [ws.dU], B, LU, 4 * H, 4 * H, 4 * H, LU,
-                     transB=True)
-                gemm([ws.dGg[t]], [Kg], [ws.dUg], B, LU, 4 * H, 4 * H, 4 * H, LU, transB=True)
+                # (both LSTMCells in one batched launch: same shapes and chains)
+                gemm([ws.dG[t], ws.dGg[t]], [Ki[C2:], Kg], [ws.dU, ws.dUg], B, LU, 4 * H,
+                     4 * H, 4 * H, LU, transB=True)
                 _ops.asr_unpack_(B, Z, H, LU, ws.dU, ws.dUg, ws.dz_carry, ws.dss_carry,
                                  ws.dh[t - 1], ws.dhg[t - 1])
         self._weight_grads(X, ws)
