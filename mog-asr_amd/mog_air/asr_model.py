@@ -375,11 +375,12 @@ class AIRModel(_AirBase):
             # 0 * w (exactly +-0: the sum is unchanged bit for bit) and the
             # operands are 16-byte rows (LDS-DMA GEMM); the 3 weight rows past
             # the U-part are the kernels' own zero pad rows (ParamStore pad)
-            gemm([ws.U[t]], [Ki[C2:]], [ws.G[t]], B, 4 * H, LU, LU, 4 * H, 4 * H, bias=[bi],
-                 Cin=[ws.Gx])
+            # (both LSTMCells' gate GEMMs in one batched launch; the inference
+            # cell continues the hoisted x-projection's chain through Cin)
+            gemm([ws.U[t], ws.Ug[t]], [Ki[C2:], Kg], [ws.G[t], ws.Gg[t]], B, 4 * H, LU, LU,
+                 4 * H, 4 * H, bias=[bi, bg], Cin=[ws.Gx, None])
             _ops.lstm_cell_forward_(ws.G[t], None, ws.c[t - 1] if prev else None, ws.c[t],
                                     ws.h[t], B, H)
-            gemm([ws.Ug[t]], [Kg], [ws.Gg[t]], B, 4 * H, LU, LU, 4 * H, 4 * H, bias=[bg])
             _ops.lstm_cell_forward_(ws.Gg[t], None, ws.cg[t - 1] if prev else None, ws.cg[t],
                                     ws.hg[t], B, H)
             hid = [ws.hid8[k, t] for k in range(8)]
