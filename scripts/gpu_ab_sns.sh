@@ -1,5 +1,6 @@
 #!/bin/bash
 # captured batch-64 step with the small-M GEMM pipeline depth MOG_GEMM_SNS = 2 / 3 / 4
+# (MOG_GEMM_SNS was a temporary switch, measured and removed: the small-M tiles stay two-stage)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export PYTHONUNBUFFERED=1
