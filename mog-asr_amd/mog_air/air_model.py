@@ -1267,6 +1267,8 @@ class AIRModel:
         everything issued so far on the current stream); returns the event
         that marks their completion."""
         main, side = torch.cuda.current_stream(), self._side_stream()
+        if ws.B < self.SIDE_MIN_BATCH and os.environ.get("MOG_VAE_SIDE_SMALL", "1") == "0":
+            side = main  # (diagnosis of the bf16 batch-64 flake: no second stream)
         ready = torch.cuda.Event()
         ready.record(main)
         side.wait_event(ready)
