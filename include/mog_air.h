@@ -70,7 +70,7 @@ int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb, float* C, 
  * split into three bf16 pieces inside the kernel, B = W [N][K] given as the
  * three pieces of mog_split3_bf16 (piece p at B3 + p * sb, row pitch ldb).
  * epi 0: store; 1: C = v * sigmoid(aux[m][n]) (dX through softplus).
- * K, N, lda, ldc, ldaux multiples of 4; ldb, sb multiples of 8; deterministic. */
+ * K, ldb, sb multiples of 8; N, lda, ldc, ldaux multiples of 4; deterministic. */
 int mog_gemm_x3_nt(const float* A, const void* B3, long sb, float* C, const float* aux, int M,
                    int N, int K, int lda, int ldb, int ldc, int ldaux, int epi, void* stream);
 
@@ -399,6 +399,14 @@ int mog_asr_step_backward(int B, int train, int fix_steps, float temperature,
 /* ---- noise (tf.random_normal / random_uniform sites, perf mode) --------- */
 int mog_rng_fill(float* out, long n, unsigned long long seed, unsigned long long offset,
                  int normal, void* stream);
+
+/* ---- test instrument (no reference counterpart) -------------------------
+ * One wave occupying `stream` for `ticks` of the 100 MHz wall clock (<= 1 s):
+ * the stream-ordering tests hold one stream of a forked step back with it. */
+int mog_spin(long long ticks, void* stream);
+/* Fills the LDS of every CU with the 32-bit pattern `bits` (a NaN, say), so a
+ * kernel launched next that reads LDS it did not write shows it. */
+int mog_lds_poison(unsigned bits, void* stream);
 
 #ifdef __cplusplus
 }

@@ -335,12 +335,13 @@ __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[BM / 32][BN
     float xq[ITER][4];
     const bool aux_ld = HAS_AUX && !(EPI == EPI_SIGMOID_NOISE && D.eps_gen);
     if (aux_ld) {
-      // gcol < N <= ldaux, both multiples of 4 where a quad is read whole
+      // a quad is read whole only where N and ldaux are multiples of 4 (a
+      // uniform test): the quad then never passes column N - 1 of the row
       const int ac = gcol < N ? gcol : 0;
 #pragma unroll
       for (int i = 0; i < ITER; ++i) {
         const float* ar = aux + (size_t)min(m0 + r00 + RSTEP * i, M - 1) * D.ldaux;
-        if (D.ldaux % 4 == 0) {
+        if (D.ldaux % 4 == 0 && N % 4 == 0) {
           const float4 x4 = *reinterpret_cast<const float4*>(ar + ac);
           xq[i][0] = x4.x; xq[i][1] = x4.y; xq[i][2] = x4.z; xq[i][3] = x4.w;
         } else {

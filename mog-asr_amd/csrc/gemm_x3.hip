@@ -143,18 +143,24 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
   // the registers there, which waits for the load).
   u32x4 ra[NL], rb[NL];
   constexpr int OOB = (int)0x80000000u;
-  // record ranges = the operands' validated extents (the last piece's last
-  // k-row ends at column round8(M) / M): nothing past them is read
-  const __amdgpu_buffer_rsrc_t arsc = __builtin_amdgcn_make_buffer_rsrc(
-      PRE ? (void*)D.A3 : (void*)D.A, 0,
-      PRE ? (int)((2 * D.sa + (long)(D.K - 1) * D.lda + ((M + 7) & ~7)) * 2)
-          : (int)(((long)(D.K - 1) * D.lda + M) * 4),
-      0x00020000);
-  const __amdgpu_buffer_rsrc_t brsc = __builtin_amdgcn_make_buffer_rsrc(
-      PRE ? (void*)D.B3 : (void*)D.B, 0,
-      PRE ? (int)((2 * D.sb + (long)(D.K - 1) * D.ldb + ((N + 7) & ~7)) * 2)
-          : (int)(((long)(D.K - 1) * D.ldb + N) * 4),
-      0x00020000);
+  // record ranges = the operands' validated extents (each piece's last k-row
+  // ends at column round8(M) / round8(N)): nothing past them is read.  PRE:
+  // one descriptor per piece, so the range check (which covers the per-lane
+  // offset only, not the scalar one) holds every piece to its own extent.
+  __amdgpu_buffer_rsrc_t arsc[PRE ? NPC : 1], brsc[PRE ? NPC : 1];
+#pragma unroll
+  for (int p = 0; p < (PRE ? NPC : 1); ++p) {
+    arsc[p] = __builtin_amdgcn_make_buffer_rsrc(
+        PRE ? (void*)(D.A3 + p * D.sa) : (void*)D.A, 0,
+        PRE ? (int)(((long)(D.K - 1) * D.lda + ((M + 7) & ~7)) * 2)
+            : (int)(((long)(D.K - 1) * D.lda + M) * 4),
+        0x00020000);
+    brsc[p] = __builtin_amdgcn_make_buffer_rsrc(
+        PRE ? (void*)(D.B3 + p * D.sb) : (void*)D.B, 0,
+        PRE ? (int)(((long)(D.K - 1) * D.ldb + ((N + 7) & ~7)) * 2)
+            : (int)(((long)(D.K - 1) * D.ldb + N) * 4),
+        0x00020000);
+  }
   auto load_tiles = [&](int k0) {
     if constexpr (PRE) {
 #pragma unroll
@@ -165,8 +171,8 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
         const int bo = gk < kend ? (gk * D.ldb + n0 + pc) * 2 : OOB;
 #pragma unroll
         for (int p = 0; p < NPC; ++p) {
-          pa[p][i] = __builtin_amdgcn_raw_buffer_load_b128(arsc, ao, (int)(p * D.sa * 2), 0);
-          pb[p][i] = __builtin_amdgcn_raw_buffer_load_b128(brsc, bo, (int)(p * D.sb * 2), 0);
+          pa[p][i] = __builtin_amdgcn_raw_buffer_load_b128(arsc[p], ao, 0, 0);
+          pb[p][i] = __builtin_amdgcn_raw_buffer_load_b128(brsc[p], bo, 0, 0);
         }
       }
       return;
@@ -175,9 +181,9 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
     for (int i = 0; i < NL; ++i) {
       const int gk = k0 + sk + 8 * i;
       ra[i] = __builtin_amdgcn_raw_buffer_load_b128(
-          arsc, gk < kend ? (gk * D.lda + m0 + sc) * 4 : OOB, 0, 0);
+          arsc[0], gk < kend ? (gk * D.lda + m0 + sc) * 4 : OOB, 0, 0);
       rb[i] = __builtin_amdgcn_raw_buffer_load_b128(
-          brsc, gk < kend ? (gk * D.ldb + n0 + sc) * 4 : OOB, 0, 0);
+          brsc[0], gk < kend ? (gk * D.ldb + n0 + sc) * 4 : OOB, 0, 0);
     }
   };
   auto f4 = [](const u32x4& v) {
@@ -433,39 +439,44 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
   u32x4 rb[3][NT_NLB];
   const float4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const u32x4 z4 = {0u, 0u, 0u, 0u};
-  // Buffer loads: the workgroup's A rows and the B pieces behind two
-  // descriptors, one 32-bit offset register per thread and operand (the row /
-  // piece / k-tile steps are uniform: scalar offsets).  Every load is issued
-  // unconditionally -- a predicated load (`cond ? load : 0`) becomes a branch
-  // around it with a vmcnt(0) wait inside, one full memory latency per load --
-  // and what must read as zero is pushed out of the descriptor's range
-  // instead: A rows >= M fall outside A's record range; k >= K (the last
-  // k-tile, K % 32 != 0; with lda == K those addresses hold the next row) gets
-  // an offset past every range, on both operands.  B rows >= N load the next
-  // piece's rows or 0 past the last piece: they only reach output columns >= N,
-  // which are not stored.
-  // record ranges: the panel's rows, ending at column K (or N) of the
-  // operand's last row -- its validated extent
+  // Buffer loads: the workgroup's A rows behind one descriptor and each B
+  // piece behind its own, the row offsets in the per-thread (range-checked)
+  // offset, only the uniform k-tile step in the scalar offset, which the
+  // range check does not cover (it stays inside a row: k0 + 8 <= K <= ld).
+  // Every load is issued unconditionally -- a predicated load (`cond ? load
+  // : 0`) becomes a branch around it with a vmcnt(0) wait inside, one full
+  // memory latency per load -- and what must read as zero is pushed out of
+  // the descriptor's range instead: A rows >= M and B rows >= N fall outside
+  // their operand's record range; k >= K (the last k-tile, K % 32 != 0; with
+  // lda == K those addresses hold the next row) gets an offset past every
+  // range, on both operands.
+  // record ranges: the rows, ending at column K of the operand's last row --
+  // its validated extent
   const int arows = min(M - m0, BM);
   const __amdgpu_buffer_rsrc_t arsc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(D.A) + (size_t)m0 * D.lda, 0,
       (M - m0 > BM ? BM * D.lda : (arows - 1) * D.lda + K) * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t brsc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<__bf16*>(D.B3), 0, (int)((2 * D.sb + (long)N * D.ldb) * 2), 0x00020000);
-  const int avo = (ar * D.lda + ak) * 4;
-  const int bvo = ((n0 + br) * D.ldb + bk) * 2;
-  constexpr int OOB = (int)0x80000000u;  // + any scalar offset here: past every range
+  __amdgpu_buffer_rsrc_t brsc[3];
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+    brsc[p] = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(D.B3) + (size_t)p * D.sb, 0,
+                                                ((N - 1) * D.ldb + K) * 2, 0x00020000);
+  int avo[NT_NLA], bvo[NT_NLB];
+#pragma unroll
+  for (int i = 0; i < NT_NLA; ++i) avo[i] = ((ar + 32 * i) * D.lda + ak) * 4;
+#pragma unroll
+  for (int i = 0; i < NT_NLB; ++i) bvo[i] = ((n0 + br + 64 * i) * D.ldb + bk) * 2;
+  constexpr int OOB = (int)0x80000000u;  // past every range
   auto load_tiles = [&](int k0) {
-    const int av = k0 + ak < K ? avo : OOB, bv = k0 + bk < K ? bvo : OOB;
+    const bool ak_in = k0 + ak < K, bk_in = k0 + bk < K;
 #pragma unroll
     for (int i = 0; i < NT_NLA; ++i)
-      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(arsc, av, (32 * i * D.lda + k0) * 4, 0);
+      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(arsc, ak_in ? avo[i] : OOB, k0 * 4, 0);
 #pragma unroll
     for (int i = 0; i < NT_NLB; ++i)
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        rb[p][i] = __builtin_amdgcn_raw_buffer_load_b128(
-            brsc, bv, (int)((p * D.sb + (long)64 * i * D.ldb + k0) * 2), 0);
+        rb[p][i] = __builtin_amdgcn_raw_buffer_load_b128(brsc[p], bk_in ? bvo[i] : OOB, k0 * 2, 0);
   };
   auto store_tiles = [&]() {
 #pragma unroll
@@ -614,11 +625,12 @@ extern "C" int mog_gemm_x3_nt(const float* A, const void* B3, long sb, float* C,
   MOG_CHECK_ARG(A && B3 && C && M >= 0 && N >= 0 && K >= 0 && (epi == 0 || epi == 1));
   MOG_CHECK_ARG(epi == 0 || (aux && ldaux % 4 == 0 && ldaux >= N && al16(aux)));
   // 16-byte accesses: float4 rows of A and C (K, N, lda, ldc multiples of 4),
-  // 8-bf16 chunks of the B pieces (ldb, sb multiples of 8)
-  MOG_CHECK_ARG(al16(A) && al16(B3) && al16(C) && K % 4 == 0 && N % 4 == 0 && lda % 4 == 0 &&
+  // 8-bf16 chunks of the B pieces (K, ldb, sb multiples of 8: a chunk never
+  // straddles the end of a row, so no pad element of W is read)
+  MOG_CHECK_ARG(al16(A) && al16(B3) && al16(C) && K % 8 == 0 && N % 4 == 0 && lda % 4 == 0 &&
                 ldc % 4 == 0 && ldb % 8 == 0 && sb % 8 == 0 && lda >= K && ldb >= K && ldc >= N);
   // 32-bit buffer offsets: the pieces and one 128-row panel of A
-  MOG_CHECK_ARG((2 * sb + (long)N * ldb) * 2 < (1L << 31) && (long)BM * lda * 4 < (1L << 31) &&
+  MOG_CHECK_ARG((long)N * ldb * 2 < (1L << 31) && (long)BM * lda * 4 < (1L << 31) &&
                 (long)BM * ldaux * 4 < (1L << 31));
   if (M == 0 || N == 0) return 0;
   X3NtArgs D{};

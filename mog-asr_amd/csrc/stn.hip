@@ -163,6 +163,14 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#ifdef MOG_STN_DEBUG
+// diagnosis build only: every pixel's operands of the read backward
+__device__ float* mog_stn_dbg = nullptr;
+extern "C" int mog_stn_debug_set(float* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(mog_stn_dbg), &p, sizeof(p));
+}
+#endif
+
 // The per-pixel loop of stn_bwd_kernel, specialised so the hot body has no
 // branches: SEP (axis-aligned: geometry from the tables), DU (0 none,
 // 1 separable g tile, 2 LDS atomics).
@@ -271,6 +279,16 @@ __device__ __forceinline__ void bwd_pixels(const float* th, int Hin, int Win, in
         }
         const float dx = g * (ay * (Ic - Ia) + by * (Id - Ib)) * wm2;
         const float dy = g * (ax * (Ib - Ia) + bx * (Id - Ic)) * hm2;
+#ifdef MOG_STN_DEBUG
+        if (mog_stn_dbg != nullptr && valid && SEP && DU == 0) {
+          const int nn = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+          float* d = mog_stn_dbg + (((size_t)nn * Hout + i) * Wout + j) * 16;
+          d[0] = gout; d[1] = Ia; d[2] = Ib; d[3] = Ic; d[4] = Id; d[5] = ax; d[6] = bx;
+          d[7] = ay; d[8] = by; d[9] = __int_as_float(x0); d[10] = __int_as_float(x1);
+          d[11] = __int_as_float(y0); d[12] = __int_as_float(y1); d[13] = dx; d[14] = dy;
+          d[15] = g;
+        }
+#endif
         // the column coordinate xt is constant per lane: sum_rows dx, scaled once
         sdx += dx; a[1] += dx * yt;
         sdy += dy; a[4] += dy * yt;

@@ -669,6 +669,21 @@ void rng_fill_(Tensor out, int64_t seed, int64_t offset, bool normal) {
         o.name);
 }
 
+// stream-ordering test instrument (csrc/spin.hip): `anchor` names the device
+void spin_(const Tensor& anchor, int64_t ticks) {
+  Op o("spin_");
+  o.need(anchor, anchor.scalar_type(), 0, "anchor");
+  GUARD(o);
+  check(mog_spin(ticks, o.stream()), o.name);
+}
+
+void lds_poison_(const Tensor& anchor, int64_t bits) {
+  Op o("lds_poison_");
+  o.need(anchor, anchor.scalar_type(), 0, "anchor");
+  GUARD(o);
+  check(mog_lds_poison((unsigned)bits, o.stream()), o.name);
+}
+
 // ---------------------------------------------- AIR-ASR cells and losses ----
 // (air/air_number_bbox_location.py; records [T][28][B], asr_cell.hip)
 constexpr int64_t ASR_NQ = 28, ASR_DN = 12;
@@ -987,6 +1002,8 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "float clip, float lr_t, float beta1, float beta2, float eps) -> ()");
   m.def("add_(Tensor a, Tensor b, Tensor(a!) out, int n) -> ()");
   m.def("rng_fill_(Tensor(a!) out, int seed, int offset, bool normal) -> ()");
+  m.def("spin_(Tensor anchor, int ticks) -> ()");
+  m.def("lds_poison_(Tensor anchor, int bits) -> ()");
   // AIR-ASR (air_number_bbox_location.py:384-1084)
   m.def(
       "asr_pack_(int B, int Z, int H, int ld, Tensor? z, Tensor? ss, Tensor? h, "
@@ -1050,6 +1067,8 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("clip_adam_", &clip_adam_);
   m.impl("add_", &add_);
   m.impl("rng_fill_", &rng_fill_);
+  m.impl("spin_", &spin_);
+  m.impl("lds_poison_", &lds_poison_);
   m.impl("asr_pack_", &asr_pack_);
   m.impl("asr_unpack_", &asr_unpack_);
   m.impl("asr_step_forward_", &asr_step_forward_);

@@ -20,6 +20,7 @@ I = ctypes.c_int
 F = ctypes.c_float
 L = ctypes.c_long
 ULL = ctypes.c_ulonglong
+LL = ctypes.c_longlong
 
 # argtypes per entry point (mirrors include/mog_air.h)
 _SIGS = {
@@ -60,6 +61,8 @@ _SIGS = {
     "mog_optim_chunk_elems": [],
     "mog_clip_adam": [P, P, P, P, P, P, P, P, I, P, F, F, F, F, F, P],
     "mog_rng_fill": [P, L, ULL, ULL, I, P],
+    "mog_spin": [LL, P],
+    "mog_lds_poison": [ctypes.c_uint, P],
     "mog_generation_prior": [I, I, F, F, F, F, F, F, P, P, P, P, P, P, P, P],
     "mog_asr_pack": [I, I, I, I, P, P, P, P, P],
     "mog_asr_unpack": [I, I, I, I, P, P, P, P, P, P, P],

@@ -412,10 +412,7 @@ class AIRModel:
         if self.NOISE_ON_SIDE and ws.B >= self.SIDE_MIN_BATCH:
             # on the side stream, under the x-projection (which needs none of
             # it); _forward joins it after that GEMM
-            side = self._side_stream()
-            ready = torch.cuda.Event()
-            ready.record(torch.cuda.current_stream())
-            side.wait_event(ready)
+            side = self._fork(self._side_stream())
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             for k, normal in (("eps_scale", True), ("eps_shift", True), ("eps_z", True),
                               ("eps_x", True), ("u", False)):
@@ -747,14 +744,13 @@ class AIRModel:
         # the VAE's alone joined before Adam, heads on the main stream, was
         # measured slower in round 2: 3.74 -> 3.81 ms).
         # (measured: forking them after the STN read backward instead, so that
-        # kernel runs alone, leaves the step unchanged -- 3.53 ms either way)
-        if not self.FORK_AFTER_READ:
-            w1_done, vae_done = self._vae_weight_grads_async(ws)
+        # kernel runs alone, is neutral -- 3.097 / 3.094 vs 3.098 / 3.097 ms).
+        # Below SIDE_MIN_BATCH everything stays on the main stream (see
+        # _vae_weight_grads_async).
+        w1_done, vae_done = self._vae_weight_grads_async(ws)
         # STN read backward of all steps against the shared input canvas
         ops.stn_backward(X, ws.th_f, (W, W), ws.dg_all, want_dU=False, dtheta=ws.dth_f_all,
                          n=TB)
-        if self.FORK_AFTER_READ:
-            w1_done, vae_done = self._vae_weight_grads_async(ws)
         for t in range(T):
             hid_t = [ws.hid[z, t] for z in range(5)]
             _ops.air_step_backward_(
@@ -779,20 +775,15 @@ class AIRModel:
             # follow the VAE's on the side stream, under the latency-bound
             # LSTM chain; the main stream joins them before Adam
             # (on a third stream, beside the VAE's: HEADS_STREAM3)
-            main = torch.cuda.current_stream()
             side = self._stream3() if self.HEADS_STREAM3 else self._side_stream()
-            heads_ready = torch.cuda.Event()
-            heads_ready.record(main)
-            side.wait_event(heads_ready)
-            with torch.cuda.stream(side):
+            with torch.cuda.stream(self._fork(side)):
                 self._weight_grads_heads(ws)
-                vae_done = torch.cuda.Event()
-                vae_done.record(side)
         else:
             # the heads' and the VAE's weight gradients are final here: their
             # all-reduce bucket runs while the LSTM chain below computes
             self._weight_grads_heads(ws)
-            torch.cuda.current_stream().wait_event(vae_done)
+            if vae_done is not None:
+                torch.cuda.current_stream().wait_event(vae_done)
             split = self._bucket_split()
             self._reduce_bucket(split, self.params.total)
         ws.dGsum.zero_()
@@ -809,11 +800,6 @@ class AIRModel:
             torch.cuda.current_stream().wait_stream(self._side_stream())
             if self.HEADS_STREAM3 or self.REC_STREAM3:
                 torch.cuda.current_stream().wait_stream(self._stream3())
-
-    # the side stream's weight gradients forked after the STN read backward
-    # (which then runs alone) instead of before it (MOG_FORK_AFTER_READ=1;
-    # measured neutral in round 4: 3.097 / 3.094 vs 3.098 / 3.097 ms)
-    FORK_AFTER_READ = os.environ.get("MOG_FORK_AFTER_READ", "0") == "1"
 
     # single GPU: heads' weight gradients on the side stream (see _backward)
     HEADS_WGRAD_SIDE = os.environ.get("MOG_HEADS_SIDE", "1") == "1"
@@ -865,11 +851,8 @@ class AIRModel:
         TB = ws.B * self.max_steps
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
-        ws.early_wgrads = set()
         # dm = SigmoidGrad(r, dr) was written by the STN write backward
-        self._early_wgrad(ws, "gen_mean")
         self._dx(ws.dm, "gen_mean", ws.dd2, TB, G2, W2, aux=ws.d2pre)
-        self._early_wgrad(ws, "generative_2")
         self._dx(ws.dd2, "generative_2", ws.dd1, TB, G1, G2, aux=ws.d1pre)
         gemm([ws.dd1], [vw["generative_1"]], [ws.dz_all], TB, Z, G1, G1, G1, Z, transB=True)
         _ops.vae_sample_backward_(TB, Z, float(self.vae_prior_mean),
@@ -1093,13 +1076,21 @@ class AIRModel:
         gemm_bf16([ws.da1b[t]], [wn["recognition_1"]], [ws.dg], B, W2, R1, R1, R1, W2,
                   epi=BF_STORE)
 
+    # every weight gradient in one k pass (split-K 1, one atomic add per
+    # element onto the zeroed gradient): a bitwise-reproducible step, for the
+    # stream-ordering tests (tests/test_gpu_streams.py)
+    ONE_PASS_WGRADS = False
+
+    def _sk(self, splitk):
+        return 1 if self.ONE_PASS_WGRADS else splitk
+
     def _dw_bf16(self, X, dY, out, K, M, N, lda, ldb, bias_out):
         from .ops import BF_ATOMIC, gemm_bf16
         big = M >= 128 and N >= 128
         tiles = ((M + 127) // 128) * ((N + 127) // 128) if big else \
             ((M + 63) // 64) * ((N + 63) // 64)
         target = int(os.environ.get("MOG_DW_TARGET", "256"))
-        splitk = max(1, min(K // 512, (target + tiles - 1) // tiles))
+        splitk = self._sk(max(1, min(K // 512, (target + tiles - 1) // tiles)))
         gemm_bf16([X], [dY], [out], M, N, K, lda, ldb, N, tn=True, epi=BF_ATOMIC,
                   splitk=splitk, colsum=[bias_out])
 
@@ -1133,7 +1124,7 @@ class AIRModel:
             bias_out = None if bias_out is None else [bias_out]
         tiles = ((M + 63) // 64) * ((N + 63) // 64) * len(out)
         target = int(os.environ.get("MOG_DW32_TARGET", "2048"))
-        splitk = max(1, min(K // 256, (target + tiles - 1) // tiles))
+        splitk = self._sk(max(1, min(K // 256, (target + tiles - 1) // tiles)))
         gemm(X, dY, out, M, N, K, lda, ldb, N, transA=True, epi=EPI_ATOMIC,
              splitk=splitk, colsum=bias_out)
 
@@ -1160,7 +1151,7 @@ class AIRModel:
         if not (self.VAE_WGRAD_X3 and M % 4 == 0 and N % 4 == 0 and K >= self.X3_MIN_ROWS):
             return self._dw(X, dY, out, K, M, N, lda, ldb, bias_out)
         tiles = ((M + 127) // 128) * ((N + 127) // 128)
-        splitk = max(1, min(K // 256, (512 + tiles - 1) // tiles))
+        splitk = self._sk(max(1, min(K // 256, (512 + tiles - 1) // tiles)))
         ops.gemm_x3_tn(X, dY, out, M, N, K, lda, ldb, N, splitk=splitk, colsum=bias_out)
 
     def _vae_wgrad_fp32(self, ws, name, t=None):
@@ -1191,34 +1182,9 @@ class AIRModel:
             self._dw_x3(v(ws.d2), v(ws.dm), g(name), TB, G2, W2, G2, W2, gb(name))
 
     def _vae_weight_grads_fp32(self, ws):
-        early = getattr(ws, "early_wgrads", None) or ()
         for name in ("recognition_1", "recognition_2", "rec_mean", "generative_1",
                      "generative_2", "gen_mean"):
-            if name not in early:
-                self._vae_wgrad_fp32(ws, name)
-        ws.early_wgrads = None
-
-    # fp32, one GPU, from SIDE_MIN_BATCH: the decoder's two large weight
-    # gradients start on the side stream as soon as their dY exists (dm after
-    # the STN write backward, dd2 after the first input gradient), under the
-    # MFMA-bound VAE input-gradient chain, instead of under the latency-bound
-    # LSTM chain, where their workgroups held every CU while the chain's small
-    # launches waited.  Measured neutral (fp32 step 3.102 / 3.093 ms with it,
-    # 3.080 / 3.093 without: the contention moves to the input-gradient chain),
-    # so opt-in (MOG_WGRAD_EARLY=1)
-    WGRAD_EARLY = os.environ.get("MOG_WGRAD_EARLY", "0") == "1"
-
-    def _early_wgrad(self, ws, name):
-        if not (self.WGRAD_EARLY and self.precision == "fp32" and self.grad_reducer is None
-                and ws.B >= self.SIDE_MIN_BATCH):
-            return
-        main, side = torch.cuda.current_stream(), self._side_stream()
-        ready = torch.cuda.Event()
-        ready.record(main)
-        side.wait_event(ready)
-        with torch.cuda.stream(side):
             self._vae_wgrad_fp32(ws, name)
-        ws.early_wgrads.add(name)
 
     def _weight_grads_glimpse(self, ws):
         """Weight gradients of the VAE and the five heads (every loop step at
@@ -1229,15 +1195,6 @@ class AIRModel:
             self._vae_weight_grads_fp32(ws)
         self._weight_grads_heads(ws)
 
-    MAIN_PRIORITY = os.environ.get("MOG_MAIN_PRIO", "0") == "1"
-
-    def _hp_stream(self):
-        if getattr(self, "_hp", None) is None:
-            lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") \
-                else (0, -1)
-            self._hp = torch.cuda.Stream(device=self.device, priority=min(lo, hi))
-        return self._hp
-
     # one GPU, from SIDE_MIN_BATCH: the heads' weight gradients on a third
     # stream, beside the VAE's instead of queued after them (fp32 step 3.10 /
     # 3.10 -> 3.05 / 3.07 ms; MOG_HEADS_STREAM3=0: after them on the side stream)
@@ -1246,40 +1203,51 @@ class AIRModel:
     # 3.04 / 3.04 ms; MOG_REC_STREAM3=0: on the side stream)
     REC_STREAM3 = os.environ.get("MOG_REC_STREAM3", "1") == "1"
 
-    # the side and third streams created once per process and device, shared
-    # by every model (see _shared_streams; MOG_SHARED_STREAMS=0: per model)
-    SHARED_STREAMS = os.environ.get("MOG_SHARED_STREAMS", "1") == "1"
-
+    # the side and third streams are created once per process and device and
+    # shared by every model (see _shared_streams)
     def _stream3(self):
-        if getattr(self, "_s3", None) is None:
-            self._s3 = _shared_streams(self.device)[1] if self.SHARED_STREAMS else \
-                torch.cuda.Stream(device=self.device)
-        return self._s3
+        return _shared_streams(self.device)[1]
 
     def _side_stream(self):
-        if getattr(self, "_side", None) is None:
-            self._side = _shared_streams(self.device)[0] if self.SHARED_STREAMS else \
-                torch.cuda.Stream(device=self.device)
-        return self._side
+        return _shared_streams(self.device)[0]
+
+    # stream-ordering test instrument (tests/test_gpu_streams.py): ticks of the
+    # 100 MHz wall clock that a spin kernel holds back the head of every forked
+    # segment (SPIN_FORK) or the main stream at the start of a step (SPIN_MAIN)
+    SPIN_FORK = 0
+    SPIN_MAIN = 0
+
+    def _fork(self, stream):
+        """Order `stream` after everything issued so far on the current
+        stream; returns it."""
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream())
+        stream.wait_event(ready)
+        if self.SPIN_FORK:
+            with torch.cuda.stream(stream):
+                ops.spin(self.SPIN_FORK)
+        return stream
 
     def _vae_weight_grads_async(self, ws):
         """The VAE weight gradients on the side stream (ordered after
-        everything issued so far on the current stream); returns the event
-        that marks their completion."""
-        main, side = torch.cuda.current_stream(), self._side_stream()
-        if ws.B < self.SIDE_MIN_BATCH and os.environ.get("MOG_VAE_SIDE_SMALL", "1") == "0":
-            side = main  # (diagnosis of the bf16 batch-64 flake: no second stream)
-        ready = torch.cuda.Event()
-        ready.record(main)
-        side.wait_event(ready)
-        w1_done = None
+        everything issued so far on the current stream); returns the events
+        that mark the heads' W1 refresh and their completion.  Below
+        SIDE_MIN_BATCH they run in line on the current stream (events None):
+        at the reference's batch of 64 the launches are a few microseconds
+        each, too short to hide a cross-stream wait."""
+        if ws.B < self.SIDE_MIN_BATCH:
+            if self.precision == "bf16":
+                self._vae_weight_grads_bf16(ws)
+            else:
+                self._vae_weight_grads_fp32(ws)
+            return None, None
+        side = self._fork(self._side_stream())
         with torch.cuda.stream(side):
-            if ws.B >= self.SIDE_MIN_BATCH:
-                # the heads' concatenated W1 (B operand of the dh GEMM) first:
-                # off the main stream, which waits for it only at that GEMM
-                self._w1cat()
-                w1_done = torch.cuda.Event()
-                w1_done.record(side)
+            # the heads' concatenated W1 (B operand of the dh GEMM) first:
+            # off the main stream, which waits for it only at that GEMM
+            self._w1cat()
+            w1_done = torch.cuda.Event()
+            w1_done.record(side)
             if self.precision == "bf16":
                 self._vae_weight_grads_bf16(ws)
             else:
@@ -1337,12 +1305,8 @@ class AIRModel:
         if T > 1 and side and self.REC_WGRAD_SIDE:
             # one GPU: the recurrent rows' gradient on the side stream, beside
             # the x-rows gradient below (both need only the finished chain)
-            main = torch.cuda.current_stream()
             st = self._stream3() if self.REC_STREAM3 else self._side_stream()
-            ev = torch.cuda.Event()
-            ev.record(main)
-            st.wait_event(ev)
-            with torch.cuda.stream(st):
+            with torch.cuda.stream(self._fork(st)):
                 self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
         elif T > 1:
             self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
@@ -1367,13 +1331,13 @@ class AIRModel:
                         ops.split3_bf16(ws.dGsum, ws.dG3, B, 4 * H, 4 * H, 4 * H, B * 4 * H)
                     C2p = self._pad8(C2)
                     ops.gemm_x3p_tn(ws.X3.view(-1)[m0:], B * C2p, ws.dG3, B * 4 * H, gK[m0:m1],
-                                    m1 - m0, 4 * H, B, C2p, 4 * H, 4 * H, splitk=max(1, min(B // 256, self.X3_SPLITK)),
+                                    m1 - m0, 4 * H, B, C2p, 4 * H, 4 * H, splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
                                     colsum=bias)
                 elif self.X_GRAD_X3:
                     # fp32 operands split exactly into three bf16 pieces on the
                     # bf16 matrix cores (gemm_x3.hip: fp32-level accuracy)
                     ops.gemm_x3_tn(X[:, m0:], ws.dGsum, gK[m0:m1], m1 - m0, 4 * H, B, C2, 4 * H,
-                                   4 * H, splitk=max(1, min(B // 256, self.X3_SPLITK)), colsum=bias)
+                                   4 * H, splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))), colsum=bias)
                 else:
                     self._dw(X[:, m0:], ws.dGsum, gK[m0:m1], B, m1 - m0, 4 * H, C2, 4 * H, bias)
                 if m1 < C2:
@@ -1394,7 +1358,7 @@ class AIRModel:
             # the x3p kernel with one piece (plain bf16 operands, one MFMA
             # product per k-block): 128 x 128 tiles, two workgroups per CU
             ops.gemm_x3p_tn(ws.Xb.view(-1)[m0:], 0, ws.dGsumb, 0, gK[m0:m1], m1 - m0, 4 * H, B,
-                            C2p, 4 * H, 4 * H, splitk=max(1, min(B // 256, self.X3_SPLITK)),
+                            C2p, 4 * H, 4 * H, splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
                             colsum=bias_out, npieces=1)
         else:
             self._dw_bf16(ws.Xb[:, m0:], ws.dGsumb, gK[m0:m1], B, m1 - m0, 4 * H, C2p, 4 * H,
@@ -1424,25 +1388,15 @@ class AIRModel:
         X, tg = self._prep(images, targets)
         ws = self._workspace(X.shape[0])
         ws.alloc_backward(self)
-        hp = None
-        if self.MAIN_PRIORITY and not self._graph_mode and ws.B >= self.SIDE_MIN_BATCH:
-            # the step's critical chain on a high-priority stream: the side
-            # stream's throughput GEMMs (weight gradients) then take the CUs
-            # the latency-bound chain (STN read backward, heads, LSTM chain,
-            # recurrent dh GEMMs) leaves free, instead of starving it
-            cur = torch.cuda.current_stream()
-            hp = self._hp_stream()
-            hp.wait_stream(cur)
-        with torch.cuda.stream(hp) if hp is not None else contextlib.nullcontext():
-            self._fill_noise(ws, noise)
-            self._global_batch = global_batch
-            self._forward(X, tg, ws, need_grad=True, outputs=False)
-            self._backward(X, ws)
-            if self.grad_reducer is not None:
-                self.grad_reducer.wait()
-            self.params.apply_adam(self.hyper("learning_rate"), self.gradient_clipping_norm)
-        if hp is not None:
-            cur.wait_stream(hp)
+        if self.SPIN_MAIN:
+            ops.spin(self.SPIN_MAIN)
+        self._fill_noise(ws, noise)
+        self._global_batch = global_batch
+        self._forward(X, tg, ws, need_grad=True, outputs=False)
+        self._backward(X, ws)
+        if self.grad_reducer is not None:
+            self.grad_reducer.wait()
+        self.params.apply_adam(self.hyper("learning_rate"), self.gradient_clipping_norm)
         self.params.global_step += 1
         self._X = X
 
@@ -1559,6 +1513,8 @@ class AIRModel:
         X, tg = self._prep(images, targets)
         ws = self._workspace(X.shape[0])
         ws.alloc_backward(self)
+        if self.SPIN_MAIN:
+            ops.spin(self.SPIN_MAIN)
         self._fill_noise(ws, noise)
         self._global_batch = global_batch
         self._forward(X, tg, ws, need_grad=True)

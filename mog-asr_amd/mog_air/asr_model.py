@@ -343,10 +343,7 @@ class AIRModel(_AirBase):
             # the x-rows gradient's A operand split into three bf16 pieces on
             # the side stream, under the x-projection (AIRModel._forward does
             # the same); joined in _weight_grads
-            main, side = torch.cuda.current_stream(), self._side_stream()
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
+            side = self._fork(self._side_stream())
             with torch.cuda.stream(side):
                 C2p = self._pad8(C2)
                 if getattr(ws, "X3", None) is None:
@@ -481,10 +478,7 @@ class AIRModel(_AirBase):
             if steps_side:
                 # step t's VAE weight gradients are final: accumulate them on
                 # the side stream under the rest of the loop
-                ready = torch.cuda.Event()
-                ready.record(torch.cuda.current_stream())
-                side.wait_event(ready)
-                with torch.cuda.stream(side):
+                with torch.cuda.stream(self._fork(side)):
                     if self.precision == "bf16":
                         self._vae_weight_grads_bf16(ws, t)
                     else:
@@ -518,10 +512,7 @@ class AIRModel(_AirBase):
                                      ws.dhg[t], dcg_in, ws.dGg[t], ws.dcg[t % 2], ws.dGgsum, B, H)
             if steps_side and self.U_WGRAD_PER_STEP:
                 # step t's recurrent-rows gradients likewise (dG_t, dGg_t final)
-                ready = torch.cuda.Event()
-                ready.record(torch.cuda.current_stream())
-                side.wait_event(ready)
-                with torch.cuda.stream(side):
+                with torch.cuda.stream(self._fork(side)):
                     self._u_rows_wgrad(ws, t)
             if t > 0:
                 # N = LU: the 3 pad columns of dU / dUg are scratch (unpack skips them)
@@ -568,11 +559,7 @@ class AIRModel(_AirBase):
         if heads_s3:
             # the heads' weight gradients on the third stream, beside the
             # x-rows gradient (main) and step 0's on the side stream
-            s3 = self._stream3()
-            ready = torch.cuda.Event()
-            ready.record(torch.cuda.current_stream())
-            s3.wait_event(ready)
-            with torch.cuda.stream(s3):
+            with torch.cuda.stream(self._fork(self._stream3())):
                 self._heads_wgrad(ws, None)
         if getattr(ws, "vae_wgrads_done", False):
             pass  # (per loop step, on the side stream)
@@ -599,7 +586,7 @@ class AIRModel(_AirBase):
                 ops.split3_bf16(ws.dGsum, ws.dG3, B, 4 * H, 4 * H, 4 * H, B * 4 * H)
                 C2p = self._pad8(C2)
                 ops.gemm_x3p_tn(ws.X3.view(-1), B * C2p, ws.dG3, B * 4 * H, gKi[:C2], C2, 4 * H,
-                                B, C2p, 4 * H, 4 * H, splitk=max(1, min(B // 256, self.X3_SPLITK)),
+                                B, C2p, 4 * H, 4 * H, splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
                                 colsum=G("infer_rnn_running/bias"))
             else:
                 self._dw(X, ws.dGsum, gKi[:C2], B, C2, 4 * H, C2, 4 * H,

@@ -218,3 +218,25 @@ def _i64(v: int) -> int:
 def rng_fill(out: torch.Tensor, seed: int, offset: int, normal: bool) -> None:
     _chk(out, "out")
     _ops.rng_fill_(out, _i64(seed), _i64(offset), bool(normal))
+
+
+def spin(ticks: int, device=None) -> None:
+    """Hold the current stream for `ticks` of the 100 MHz wall clock (test
+    instrument, mog_spin)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    global _SPIN_ANCHOR
+    if ticks == 0 and _SPIN_ANCHOR is not None:
+        return
+    if _SPIN_ANCHOR is None or _SPIN_ANCHOR.device != torch.device(dev):
+        _SPIN_ANCHOR = torch.empty(1, device=dev)
+    _ops.spin_(_SPIN_ANCHOR, int(ticks))
+
+
+def lds_poison(bits: int = 0x7FC00000) -> None:
+    """Fill every CU's LDS with a 32-bit pattern on the current stream (test
+    instrument, mog_lds_poison; default a quiet NaN)."""
+    spin(0)
+    _ops.lds_poison_(_SPIN_ANCHOR, int(bits))
+
+
+_SPIN_ANCHOR = None

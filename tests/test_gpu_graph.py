@@ -219,6 +219,27 @@ def test_side_streams_match_serial_at_b1024(precision):
     assert float(d.max()) <= 2.5e-3 and float(d.mean()) < 2e-5, (float(d.max()), float(d.mean()))
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_asr_side_streams_match_serial_at_b1024(precision):
+    """AIR-ASR from B = 1024: the per-loop-step VAE and recurrent-rows weight
+    gradients on the side stream and the heads' on the third stream give the
+    gradients of the after-loop serial form (summation order aside: per-step
+    accumulation against one pass over every step's rows), and the forward
+    bit for bit."""
+    import bench
+    (x, k), = _batches(1, 1024)
+    ms = bench.make_asr_model(precision, torch.device(DEV), "asd_s" + precision)
+    mp = bench.make_asr_model(precision, torch.device(DEV), "asd_p" + precision)
+    ms.VAE_WGRAD_PER_STEP = ms.U_WGRAD_PER_STEP = ms.HEADS_S3 = False
+    assert mp.VAE_WGRAD_PER_STEP and mp.U_WGRAD_PER_STEP and mp.HEADS_S3
+    for m in (ms, mp):
+        m.ONE_PASS_WGRADS = True
+    gs = ms.compute_gradients(x, k)
+    gp = mp.compute_gradients(x, k)
+    np.testing.assert_array_equal(ms._ws.means[:3].cpu().numpy(), mp._ws.means[:3].cpu().numpy())
+    _grad_close(gs, gp, rel=1e-4, rel_small=1e-3)
+
+
 def test_graph_replay_with_side_stream_forks_at_b1024():
     """The side-stream forks captured into the graph (B = 1024): a replay's
     forward equals the eager step from the same state bit for bit, its
