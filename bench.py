@@ -17,7 +17,11 @@ elsewhere), ``config_1_batch64_fp32`` (the reference's own batch of 64),
 MFMA roof), ``fused_step_roofline`` / ``fused_step_roofline_c64`` (the north-star fused
 STN-read -> VAE -> STN-write kernel at B = 65,536, C = 50 and 64, training form),
 ``fused_step_roofline_fwd`` (its forward-only form, C = 50),
-``roofline`` (dominant kernel of the headline step) and ``cpu_baseline``.
+``configs_4_asr_bbox_{fp32,bf16}`` (configs[4] on one GPU), ``roofline`` (the
+dominant kernel group of the headline step: every tagged launch priced, the
+largest total time wins) and ``cpu_baseline``.  HBM-bound lines also carry
+``frac_of_measured_copy``: achieved bytes over a measured float4 copy
+(``copy_bandwidth``).
 
 ``python bench.py --gpus N`` without a torch.distributed launcher starts the
 N ranks itself (fresh child processes, before anything touches the GPU).
@@ -53,26 +57,37 @@ def fused_bytes_per_image_step(C2: int, x_bytes: int = 4) -> int:
     return C2 * x_bytes + 2 * C2 * 4 + 24
 
 
+# what each tagged kernel group is (the roofline's "kernel" names the group)
+KERNEL_NAMES = {
+    "lstm_x_projection": "gemm_f32 (LDS-DMA, bit-exact fp32 chain): Gx = X Wx",
+    "lstm_x_projection_grad": "gemm_x3p_tn: dWx = X^T dGsum (bf16 cores; fp32: 3-piece split)",
+    "stn_vae_step": "stn_vae_step_kernel (fused bf16 STN read + VAE + STN write)",
+    "stn_vae_step_all": "stn_vae_step_kernel (fused bf16, all T steps' rows)",
+    "stn_vae_step_f32_all": "stn_vae_step_f32_kernel (fused fp32 STN read + VAE + STN write)",
+    "vae_wgrad_x3": "gemm_x3_tn_kernel<false,3>: VAE weight gradients, fp32 operands split "
+                    "in-kernel (bf16 cores)",
+    "vae_dgrad_x3": "gemm_x3_nt_kernel: VAE input gradients dY W^T (bf16 cores, 3-piece)",
+    "vae_dgrad_f32": "gemm_f32 transB: VAE input gradients (fp32 chain)",
+    "wgrad_f32": "gemm_f32 transA split-K: heads / LSTM-recurrent / small VAE weight gradients",
+    "wgrad_bf16": "gemm_bf16 TN: bf16 VAE weight gradients",
+    "stn_write_bwd": "stn_bwd_kernel: STN write backward (through the output sigmoid)",
+    "stn_read_bwd": "stn_bwd_kernel: STN read backward (dtheta only)",
+}
+PEAKS = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS}
+
+
 def kernel_work(name, B, precision, C2=2500, H=256, T=3):
-    """Algorithmic work per launch of a tagged kernel: (bound, amount, unit,
-    peak).  Per-unit figures in DESIGN.md §4.1."""
+    """Algorithmic work of one launch of a tag the model records without its
+    own work figure: (bound, amount in flops or bytes, peak key).  Per-unit
+    figures in DESIGN.md §4.1."""
     if name == "lstm_x_projection":          # Gx = X Wx, [B,C2] x [C2,4H], fp32 MFMA
-        return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", FP32_MFMA_PEAK_TFLOPS
-    if name == "lstm_x_projection_grad":     # dWx = X^T dGsum (bf16 MFMA in the bf16 config)
-        if precision == "bf16":
-            return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", BF16_MFMA_PEAK_TFLOPS
-        from mog_air.air_model import AIRModel
-        if AIRModel.X_GRAD_X3:
-            # fp32 operands split into three bf16 pieces: six bf16 MFMA products
-            # per fp32 product, priced at the bf16 peak (DESIGN.md §4.4)
-            return "mfma", 6 * 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", BF16_MFMA_PEAK_TFLOPS
-        return "mfma", 2.0 * B * C2 * 4 * H / 1e12, "TFLOP/s", FP32_MFMA_PEAK_TFLOPS
+        return "mfma", 2.0 * B * C2 * 4 * H, "fp32"
     if name == "stn_vae_step":
-        return "hbm", B * fused_bytes_per_image_step(C2) / 1e9, "GB/s", HBM_PEAK_GBS
+        return "hbm", B * fused_bytes_per_image_step(C2), None
     if name == "stn_vae_step_all":           # all T steps' rows in one launch
-        return "hbm", T * B * fused_bytes_per_image_step(C2) / 1e9, "GB/s", HBM_PEAK_GBS
+        return "hbm", T * B * fused_bytes_per_image_step(C2), None
     if name == "stn_vae_step_f32_all":       # the fp32 fused step over T*B rows: MFMA-bound
-        return "mfma", T * B * vae_chain_flops_per_image() / 1e12, "TFLOP/s", FP32_MFMA_PEAK_TFLOPS
+        return "mfma", T * B * vae_chain_flops_per_image(), "fp32"
     return None
 
 
@@ -85,32 +100,49 @@ def pmc_traffic(tag):
 
 
 def roofline(events, B, precision):
-    """The dominant launch of the timed step: among the tagged launches (each
-    tag is one kernel launch per occurrence: the x-projection, its weight
-    gradient, the fused STN + VAE step), the one with the largest total time.
-    Every tagged launch's own roofline is listed under ``launches_priced``."""
+    """The dominant kernel group of the timed step: every tagged launch
+    (AIRModel._timed: one kernel launch each, on the stream it runs on, with
+    its algorithmic flops or bytes), grouped by tag; the group with the
+    largest total time is the line's roofline.  achieved = the group's
+    algorithmic work / its summed launch durations; peak: the fp32 or bf16
+    dense MFMA peak, or 8 TB/s of HBM.  Launches on the side streams share the
+    chip with the main stream's (their durations include that).  Every group
+    is listed under ``launches_priced``."""
     rows = []
     for name, evs in events.items():
-        work = kernel_work(name, B, precision)
-        if work is None:
+        durs, amount, bound, peak_key = [], 0.0, None, None
+        for e0, e1, work in evs:
+            if work is None:
+                work = kernel_work(name, B, precision)
+            if work is None:
+                continue
+            bound, a, peak_key = work
+            durs.append(e0.elapsed_time(e1) * 1e-3)  # seconds
+            amount += a
+        if not durs:
             continue
-        durs = [a.elapsed_time(b) * 1e-3 for a, b in evs]  # seconds
-        bound, amount, unit, peak = work
-        avg = sum(durs) / len(durs)
-        achieved = amount / avg
-        rows.append({"kernel": name, "bound": bound, "achieved": achieved, "peak": peak,
-                     "unit": unit, "frac": achieved / peak,
+        total = sum(durs)
+        extra = {}
+        if bound == "mfma":
+            achieved, unit, peak = amount / total / 1e12, "TFLOP/s", PEAKS[peak_key]
+        else:
+            achieved, unit, peak = amount / total / 1e9, "GB/s", HBM_PEAK_GBS
+            extra["frac_of_measured_copy"] = achieved / copy_bandwidth(torch.device(
+                "cuda", torch.cuda.current_device()))
+        rows.append({"kernel": name, "what": KERNEL_NAMES.get(name, name), "bound": bound,
+                     "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak,
+                     **extra,
                      "traffic": pmc_traffic(f"{name}_{precision}_b{B}"),
-                     "launches": len(durs), "avg_launch_us": avg * 1e6,
-                     "total_us": sum(durs) * 1e6,
-                     "algorithmic_per_launch": amount * 1e12 if bound == "mfma" else amount * 1e9,
+                     "launches": len(durs), "avg_launch_us": total / len(durs) * 1e6,
+                     "total_us": total * 1e6,
+                     "algorithmic_per_launch": amount / len(durs),
                      "algorithmic_unit": "flop" if bound == "mfma" else "bytes"})
     if not rows:
         return None
     rows.sort(key=lambda r: -r["total_us"])
     out = dict(rows[0])
-    out["launches_priced"] = [{k: r[k] for k in ("kernel", "frac", "avg_launch_us", "unit",
-                                                 "achieved")} for r in rows]
+    out["launches_priced"] = [{k: r[k] for k in ("kernel", "frac", "avg_launch_us", "total_us",
+                                                 "launches", "unit", "achieved")} for r in rows]
     return out
 
 
@@ -201,7 +233,6 @@ def timed_train(precision, B, steps, warmup, dev, world=1, rank=0, events=False,
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    model.kernel_events = {} if events else None
     t0 = time.perf_counter()
     for _ in range(steps):
         step(X, K, global_batch=B * world)
@@ -209,7 +240,47 @@ def timed_train(precision, B, steps, warmup, dev, world=1, rank=0, events=False,
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    return time.perf_counter() - t0, model
+    el = time.perf_counter() - t0
+    if events:
+        # the roofline's per-launch HIP events over `steps` more steps of the
+        # same model and batch (an event pair around each tagged launch costs
+        # a few microseconds: the value's steps above run without them)
+        model.kernel_events = {}
+        for _ in range(steps):
+            step(X, K, global_batch=B * world)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+    return el, model
+
+
+_COPY_GBS = None
+
+
+def copy_bandwidth(dev, gib: float = 1.0, launches: int = 20) -> float:
+    """Measured device copy bandwidth (GB/s of bytes read + written): a
+    float4 grid-stride copy (mog_copy_f4) of `gib` GiB, HIP events on the
+    launch stream -- the yardstick SURVEY.md §8 D.3 asks for beside the
+    8 TB/s spec.  Measured once per process."""
+    global _COPY_GBS
+    if _COPY_GBS is None:
+        from mog_air import ops
+        n = int(gib * (1 << 30)) // 4
+        src = torch.ones(n, device=dev)
+        dst = torch.empty(n, device=dev)
+        for _ in range(3):
+            ops._ops.copy_f4_(src, dst)
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(launches):
+            ops._ops.copy_f4_(src, dst)
+        e1.record(s)
+        torch.cuda.synchronize()
+        _COPY_GBS = 2.0 * n * 4 * launches / (e0.elapsed_time(e1) * 1e-3) / 1e9
+        del src, dst
+        torch.cuda.empty_cache()
+    return _COPY_GBS
 
 
 def fused_step_roofline(batch: int, launches: int, dev, canvas: int = 50, save: bool = True):
@@ -247,10 +318,16 @@ def fused_step_roofline(batch: int, launches: int, dev, canvas: int = 50, save: 
     achieved = batch * per / 1e9 / avg
     tag = "stn_vae_step_b%d" % batch + ("" if canvas == 50 else "_c%d" % canvas) + \
         ("" if save else "_fwd")
+    copy = copy_bandwidth(dev)
+    traffic = pmc_traffic(tag)
     out = {"kernel": "stn_vae_step", "mode": "train" if save else "forward-only",
            "batch": batch, "canvas": canvas, "bound": "hbm",
            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(tag), "launches": launches,
+           "frac": achieved / HBM_PEAK_GBS, "measured_copy_GBs": copy,
+           "frac_of_measured_copy": achieved / copy,
+           "traffic": traffic,
+           "actual_traffic_GBs": traffic / avg / 1e9 if traffic else None,
+           "launches": launches,
            "avg_launch_us": avg * 1e6, "algorithmic_bytes_per_launch": batch * per,
            "algorithmic_bytes_per_image_step": per}
     if save:
@@ -527,6 +604,19 @@ def main():
                                 "-gne 10: number regularisers, learned z_pres prior, "
                                 "MAX_STEPS 6)"}
                 del m4
+            # configs[4] (train_air_pr.py -dn 3 -ds bbox20k -gb 1 -gs 10 -ga 20) on one
+            # GPU; the driver's multi-GPU runs of it use --workload asr_bbox
+            for prec in ("fp32", "bf16"):
+                el7, m7 = timed_train(prec, B, 10, 3, dev, data=ASR_BBOX_DATA,
+                                      model=make_asr_model(prec, dev, "bench_asrbb_" + prec,
+                                                           cfg=ASR_BBOX))
+                out["configs_4_asr_bbox_" + prec] = {
+                    "value": B * 10 / el7, "unit": "images/sec", "ms_per_step": el7 / 10 * 1e3,
+                    "dtype": prec, "batch": B, "steps": 10, "max_steps": 6, "fix_steps": 3,
+                    "workload": "configs[4]: AIR-ASR bbox train step (train_air_pr.py -dn 3 -ds "
+                                "bbox20k -gb 1 -gs 10 -ga 20: 3 objects of side 11-15, fix_steps "
+                                "3, bbox / size / area regularisers), one MI355X"}
+                del m7
             # configs[2] at the reference's own batch of 64
             el5, m5 = timed_train("fp32", 64, 30, 5, dev, graph=True,
                                   model=make_asr_model("fp32", dev, "bench_asr_b64"))

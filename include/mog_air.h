@@ -400,8 +400,11 @@ int mog_asr_step_backward(int B, int train, int fix_steps, float temperature,
 int mog_rng_fill(float* out, long n, unsigned long long seed, unsigned long long offset,
                  int normal, void* stream);
 
-/* ---- test instrument (no reference counterpart) -------------------------
- * One wave occupying `stream` for `ticks` of the 100 MHz wall clock (<= 1 s):
+/* ---- measurement / test instruments (no reference counterpart) ----------
+ * dst[i] = src[i] for n4 float4s (16-byte aligned): the copy bandwidth the
+ * bench quotes beside the HBM spec. */
+int mog_copy_f4(const float* src, float* dst, long n4, void* stream);
+/* One wave occupying `stream` for `ticks` of the 100 MHz wall clock (<= 1 s):
  * the stream-ordering tests hold one stream of a forked step back with it. */
 int mog_spin(long long ticks, void* stream);
 /* Fills the LDS of every CU with the 32-bit pattern `bits` (a NaN, say), so a

@@ -677,6 +677,15 @@ void spin_(const Tensor& anchor, int64_t ticks) {
   check(mog_spin(ticks, o.stream()), o.name);
 }
 
+void copy_f4_(const Tensor& src, Tensor dst) {
+  Op o("copy_f4_");
+  TORCH_CHECK(src.numel() == dst.numel() && src.numel() % 4 == 0, "copy_f4_: sizes");
+  const float* ps = o.f(src, src.numel(), "src");
+  float* pd = o.f(dst, dst.numel(), "dst");
+  GUARD(o);
+  check(mog_copy_f4(ps, pd, src.numel() / 4, o.stream()), o.name);
+}
+
 void lds_poison_(const Tensor& anchor, int64_t bits) {
   Op o("lds_poison_");
   o.need(anchor, anchor.scalar_type(), 0, "anchor");
@@ -1004,6 +1013,7 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
   m.def("rng_fill_(Tensor(a!) out, int seed, int offset, bool normal) -> ()");
   m.def("spin_(Tensor anchor, int ticks) -> ()");
   m.def("lds_poison_(Tensor anchor, int bits) -> ()");
+  m.def("copy_f4_(Tensor src, Tensor(a!) dst) -> ()");
   // AIR-ASR (air_number_bbox_location.py:384-1084)
   m.def(
       "asr_pack_(int B, int Z, int H, int ld, Tensor? z, Tensor? ss, Tensor? h, "
@@ -1069,6 +1079,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("rng_fill_", &rng_fill_);
   m.impl("spin_", &spin_);
   m.impl("lds_poison_", &lds_poison_);
+  m.impl("copy_f4_", &copy_f4_);
   m.impl("asr_pack_", &asr_pack_);
   m.impl("asr_unpack_", &asr_unpack_);
   m.impl("asr_step_forward_", &asr_step_forward_);

@@ -62,6 +62,7 @@ _SIGS = {
     "mog_clip_adam": [P, P, P, P, P, P, P, P, I, P, F, F, F, F, F, P],
     "mog_rng_fill": [P, L, ULL, ULL, I, P],
     "mog_spin": [LL, P],
+    "mog_copy_f4": [P, P, L, P],
     "mog_lds_poison": [ctypes.c_uint, P],
     "mog_generation_prior": [I, I, F, F, F, F, F, F, P, P, P, P, P, P, P, P],
     "mog_asr_pack": [I, I, I, I, P, P, P, P, P],

@@ -308,8 +308,10 @@ class AIRModel:
 
     # ----------------------------------------------------------- helpers ---
     # Optional per-kernel HIP-event timing (bench.py roofline): when
-    # ``kernel_events`` is a dict, every tagged launch records a (start, end)
-    # event pair on the stream it is launched on.
+    # ``kernel_events`` is a dict, every tagged launch records a (start, end,
+    # work) triple on the stream it is launched on; work = (bound, amount,
+    # peak) -- algorithmic flops ("mfma", peak "fp32" / "bf16") or bytes
+    # ("hbm") of that one launch, or None (bench.kernel_work prices the tag).
     kernel_events = None
 
     class _NoTimer:
@@ -320,8 +322,8 @@ class AIRModel:
             return False
 
     class _Timer:
-        def __init__(self, sink, name):
-            self.sink, self.name = sink, name
+        def __init__(self, sink, name, work):
+            self.sink, self.name, self.work = sink, name, work
 
         def __enter__(self):
             self.e0 = torch.cuda.Event(enable_timing=True)
@@ -331,13 +333,13 @@ class AIRModel:
 
         def __exit__(self, *a):
             self.e1.record(torch.cuda.current_stream())
-            self.sink.setdefault(self.name, []).append((self.e0, self.e1))
+            self.sink.setdefault(self.name, []).append((self.e0, self.e1, self.work))
             return False
 
-    def _timed(self, name):
+    def _timed(self, name, work=None):
         if self.kernel_events is None:
             return AIRModel._NoTimer()
-        return AIRModel._Timer(self.kernel_events, name)
+        return AIRModel._Timer(self.kernel_events, name, work)
 
     @property
     def global_step(self) -> int:
@@ -465,6 +467,8 @@ class AIRModel:
                 if getattr(ws, "X3", None) is None:
                     ws.X3 = torch.empty((3, B, C2p), device=self.device, dtype=torch.bfloat16)
                 ops.split3_bf16(X, ws.X3, B, C2, C2, C2p, B * C2p)
+            if need_grad and self.precision == "bf16":
+                self._x_bf16(X, ws)  # (likewise: the bf16 x-part gradient's A operand)
             if (need_grad and self.EARLY_PREP and self.precision == "fp32" and self.VAE_DX_X3
                     and B * self.max_steps >= self.X3_DX_MIN_ROWS):
                 self._w3()  # the x3 input gradients' weight pieces, off the backward's path
@@ -721,15 +725,16 @@ class AIRModel:
         prior_lo = self.hyper("z_pres_prior_log_odds")
         temperature = self.hyper("z_pres_temperature")
         # STN write backward of all steps against the shared canvas gradient
-        if self.precision == "bf16":
-            # dr leaves through the output sigmoid as bf16 straight from the kernel
-            ops.stn_backward(ws.r.view(TB, -1), ws.th_b, (C, C), ws.dcanvas, gscale=ws.zc,
-                             dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True, n=TB,
-                             dm_bf16=ws.dmb.view(TB, -1))
-        else:  # fp32 dm through the output sigmoid, likewise
-            ops.stn_backward(ws.r.view(TB, -1), ws.th_b, (C, C), ws.dcanvas, gscale=ws.zc,
-                             dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True, n=TB,
-                             dm=ws.dm.view(TB, -1))
+        with self._timed("stn_write_bwd", self._stn_bwd_work(TB, write=True)):
+            if self.precision == "bf16":
+                # dr leaves through the output sigmoid as bf16 straight from the kernel
+                ops.stn_backward(ws.r.view(TB, -1), ws.th_b, (C, C), ws.dcanvas, gscale=ws.zc,
+                                 dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True, n=TB,
+                                 dm_bf16=ws.dmb.view(TB, -1))
+            else:  # fp32 dm through the output sigmoid, likewise
+                ops.stn_backward(ws.r.view(TB, -1), ws.th_b, (C, C), ws.dcanvas, gscale=ws.zc,
+                                 dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True, n=TB,
+                                 dm=ws.dm.view(TB, -1))
         if self.precision == "bf16":
             self._vae_backward_bf16_all(ws, gscale)
         else:
@@ -749,8 +754,9 @@ class AIRModel:
         # _vae_weight_grads_async).
         w1_done, vae_done = self._vae_weight_grads_async(ws)
         # STN read backward of all steps against the shared input canvas
-        ops.stn_backward(X, ws.th_f, (W, W), ws.dg_all, want_dU=False, dtheta=ws.dth_f_all,
-                         n=TB)
+        with self._timed("stn_read_bwd", self._stn_bwd_work(TB, write=False)):
+            ops.stn_backward(X, ws.th_f, (W, W), ws.dg_all, want_dU=False, dtheta=ws.dth_f_all,
+                             n=TB)
         for t in range(T):
             hid_t = [ws.hid[z, t] for z in range(5)]
             _ops.air_step_backward_(
@@ -836,16 +842,31 @@ class AIRModel:
             self._w3_version = self.params.version
         return self._w3_buf
 
+    def _stn_bwd_work(self, rows, write):
+        """Algorithmic HBM bytes of one STN backward launch over `rows` image-
+        steps: write -- r and dm (C2... of the glimpse), the
+        canvas cotangent shared by the T steps of an image, theta / dtheta /
+        dot; read -- the input canvas shared likewise, the glimpse cotangent,
+        theta / dtheta."""
+        W2, C2, T = self.W2, self.C2, self.max_steps
+        if write:
+            dm = 2 if self.precision == "bf16" else 4
+            return ("hbm", rows * (W2 * 4 + W2 * dm + C2 * 4 / T + 52), None)
+        return ("hbm", rows * (C2 * 4 / T + W2 * 4 + 48), None)
+
     def _dx(self, dY, name, out, M, N, K, aux=None):
         """out[M,N] = dY W^T (W = vae/name/weights [N][K]) [* sigmoid(aux)]."""
         if self.VAE_DX_X3 and K % 8 == 0 and N % 4 == 0 and M >= self.X3_DX_MIN_ROWS:
             w3 = self._w3()[name]
-            ops.gemm_x3_nt(dY, w3, N * K, out, M, N, K, K, K, N, aux=aux,
-                           ldaux=N if aux is not None else 0)
+            # six bf16 MFMA products per fp32 product (gemm_x3.hip)
+            with self._timed("vae_dgrad_x3", ("mfma", 12.0 * M * N * K, "bf16")):
+                ops.gemm_x3_nt(dY, w3, N * K, out, M, N, K, K, K, N, aux=aux,
+                               ldaux=N if aux is not None else 0)
             return
-        gemm([dY], [self._P("vae/" + name + "/weights")], [out], M, N, K, K, K, N, transB=True,
-             epi=EPI_SOFTPLUS_BWD if aux is not None else EPI_STORE,
-             aux=[aux] if aux is not None else None, ldaux=N if aux is not None else 0)
+        with self._timed("vae_dgrad_f32", ("mfma", 2.0 * M * N * K, "fp32")):
+            gemm([dY], [self._P("vae/" + name + "/weights")], [out], M, N, K, K, K, N, transB=True,
+                 epi=EPI_SOFTPLUS_BWD if aux is not None else EPI_STORE,
+                 aux=[aux] if aux is not None else None, ldaux=N if aux is not None else 0)
 
     def _vae_backward_fp32_all(self, ws, gscale):
         TB = ws.B * self.max_steps
@@ -1091,8 +1112,9 @@ class AIRModel:
             ((M + 63) // 64) * ((N + 63) // 64)
         target = int(os.environ.get("MOG_DW_TARGET", "256"))
         splitk = self._sk(max(1, min(K // 512, (target + tiles - 1) // tiles)))
-        gemm_bf16([X], [dY], [out], M, N, K, lda, ldb, N, tn=True, epi=BF_ATOMIC,
-                  splitk=splitk, colsum=[bias_out])
+        with self._timed("wgrad_bf16", ("mfma", 2.0 * K * M * N, "bf16")):
+            gemm_bf16([X], [dY], [out], M, N, K, lda, ldb, N, tn=True, epi=BF_ATOMIC,
+                      splitk=splitk, colsum=[bias_out])
 
     def _vae_weight_grads_bf16(self, ws, t=None):
         """The VAE weight gradients over all T*B rows (bf16 operands), or over
@@ -1125,8 +1147,9 @@ class AIRModel:
         tiles = ((M + 63) // 64) * ((N + 63) // 64) * len(out)
         target = int(os.environ.get("MOG_DW32_TARGET", "2048"))
         splitk = self._sk(max(1, min(K // 256, (target + tiles - 1) // tiles)))
-        gemm(X, dY, out, M, N, K, lda, ldb, N, transA=True, epi=EPI_ATOMIC,
-             splitk=splitk, colsum=bias_out)
+        with self._timed("wgrad_f32", ("mfma", 2.0 * K * M * N * len(out), "fp32")):
+            gemm(X, dY, out, M, N, K, lda, ldb, N, transA=True, epi=EPI_ATOMIC,
+                 splitk=splitk, colsum=bias_out)
 
     # fp32 configuration: the VAE weight gradients whose operands are 16-byte
     # rows (M, N multiples of 4: the 784/512/256-wide layers, 98 % of the
@@ -1152,7 +1175,9 @@ class AIRModel:
             return self._dw(X, dY, out, K, M, N, lda, ldb, bias_out)
         tiles = ((M + 127) // 128) * ((N + 127) // 128)
         splitk = self._sk(max(1, min(K // 256, (512 + tiles - 1) // tiles)))
-        ops.gemm_x3_tn(X, dY, out, M, N, K, lda, ldb, N, splitk=splitk, colsum=bias_out)
+        # six bf16 MFMA products per fp32 product (gemm_x3.hip)
+        with self._timed("vae_wgrad_x3", ("mfma", 12.0 * K * M * N, "bf16")):
+            ops.gemm_x3_tn(X, dY, out, M, N, K, lda, ldb, N, splitk=splitk, colsum=bias_out)
 
     def _vae_wgrad_fp32(self, ws, name, t=None):
         """One VAE layer's weight / bias gradient over all T*B rows (fp32), or
@@ -1314,60 +1339,79 @@ class AIRModel:
         base = self.params.offsets[self._SCOPE_PREFIX + "rnn/basic_lstm_cell/kernel"]
         # bias gradient = colsum(sum_t dG_t) = colsum(dGsum), fused into chunk 0
         m_last = 0
-        with self._timed("lstm_x_projection_grad"):
-            for m0 in range(0, C2, chunk):
-                m_last = m0
-                m1 = min(C2, m0 + chunk)
-                bias = gbK if m0 == 0 else None
-                if self.precision == "bf16":
-                    # bf16 configuration: X^T dGsum on bf16 operands (fp32
-                    # accumulate); the forward x-projection stays fp32
-                    self._x_grad_bf16(X, ws, gK, bias, m0, m1)
-                elif self.X_GRAD_X3 == 2:
-                    if m0 == 0:
-                        if getattr(ws, "dG3", None) is None:
-                            ws.dG3 = torch.empty((3, B, 4 * H), device=self.device,
-                                                 dtype=torch.bfloat16)
-                        ops.split3_bf16(ws.dGsum, ws.dG3, B, 4 * H, 4 * H, 4 * H, B * 4 * H)
-                    C2p = self._pad8(C2)
+        # (the x-rows gradient GEMM of every chunk is tagged; its operand
+        # conversions / splits are not: they are other launches)
+        x3p = self.precision != "bf16" and self.X_GRAD_X3 == 2
+        for m0 in range(0, C2, chunk):
+            m_last = m0
+            m1 = min(C2, m0 + chunk)
+            bias = gbK if m0 == 0 else None
+            if self.precision == "bf16":
+                # bf16 configuration: X^T dGsum on bf16 operands (fp32
+                # accumulate); the forward x-projection stays fp32
+                self._x_grad_bf16(X, ws, gK, bias, m0, m1)
+            elif x3p:
+                if m0 == 0:
+                    if getattr(ws, "dG3", None) is None:
+                        ws.dG3 = torch.empty((3, B, 4 * H), device=self.device,
+                                             dtype=torch.bfloat16)
+                    ops.split3_bf16(ws.dGsum, ws.dG3, B, 4 * H, 4 * H, 4 * H, B * 4 * H)
+                C2p = self._pad8(C2)
+                with self._timed("lstm_x_projection_grad",
+                                 ("mfma", 12.0 * B * (m1 - m0) * 4 * H, "bf16")):
                     ops.gemm_x3p_tn(ws.X3.view(-1)[m0:], B * C2p, ws.dG3, B * 4 * H, gK[m0:m1],
-                                    m1 - m0, 4 * H, B, C2p, 4 * H, 4 * H, splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
+                                    m1 - m0, 4 * H, B, C2p, 4 * H, 4 * H,
+                                    splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
                                     colsum=bias)
-                elif self.X_GRAD_X3:
-                    # fp32 operands split exactly into three bf16 pieces on the
-                    # bf16 matrix cores (gemm_x3.hip: fp32-level accuracy)
+            elif self.X_GRAD_X3:
+                # fp32 operands split exactly into three bf16 pieces on the
+                # bf16 matrix cores (gemm_x3.hip: fp32-level accuracy)
+                with self._timed("lstm_x_projection_grad",
+                                 ("mfma", 12.0 * B * (m1 - m0) * 4 * H, "bf16")):
                     ops.gemm_x3_tn(X[:, m0:], ws.dGsum, gK[m0:m1], m1 - m0, 4 * H, B, C2, 4 * H,
-                                   4 * H, splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))), colsum=bias)
-                else:
-                    self._dw(X[:, m0:], ws.dGsum, gK[m0:m1], B, m1 - m0, 4 * H, C2, 4 * H, bias)
-                if m1 < C2:
-                    self._reduce_bucket(base + m0 * 4 * H, base + m1 * 4 * H)
+                                   4 * H, splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
+                                   colsum=bias)
+            else:
+                self._dw(X[:, m0:], ws.dGsum, gK[m0:m1], B, m1 - m0, 4 * H, C2, 4 * H, bias)
+            if m1 < C2:
+                self._reduce_bucket(base + m0 * 4 * H, base + m1 * 4 * H)
         self._reduce_bucket(base + m_last * 4 * H, self._bucket_split())
 
+    def _x_bf16(self, X, ws):
+        """X in bf16 [B][C2p] (zero pad columns): the A operand of the bf16
+        configuration's x-rows gradient, converted once per step -- in the
+        forward's side-stream prologue from SIDE_MIN_BATCH (X is the step's
+        input, final before the x-projection)."""
+        B, C2 = ws.B, self.C2
+        C2p = self._pad8(C2)
+        if getattr(ws, "Xb", None) is None:
+            ws.Xb = torch.zeros((B, C2p), device=self.device, dtype=torch.bfloat16)
+        _ops.cvt_bf16_batch_([X], [ws.Xb], [B, C2, C2, B, C2p, C2p, 0])
+        ws.xb_fresh = True
+
     def _x_grad_bf16(self, X, ws, gK, bias_out, m0, m1):
+        """The bf16 configuration's x-rows gradient X^T dGsum on gemm_x3p_tn's
+        one-piece form (plain bf16 operands, 128 x 128 tiles): X was
+        converted in the forward (_x_bf16), dGsum is converted here."""
         B, H, C2 = ws.B, self.rnn_units, self.C2
         C2p = self._pad8(C2)
         if m0 == 0:
-            if getattr(ws, "Xb", None) is None:
-                bf = dict(device=self.device, dtype=torch.bfloat16)
-                ws.Xb = torch.zeros((B, C2p), **bf)
-                ws.dGsumb = torch.empty((B, 4 * H), **bf)
-            _ops.cvt_bf16_batch_([X, ws.dGsum], [ws.Xb, ws.dGsumb],
-                                 [B, C2, C2, B, C2p, C2p, 0, B, 4 * H, 4 * H, B, 4 * H, 4 * H, 0])
-        if self.X_GRAD_BF16_X1:
-            # the x3p kernel with one piece (plain bf16 operands, one MFMA
-            # product per k-block): 128 x 128 tiles, two workgroups per CU
+            if not getattr(ws, "xb_fresh", False):  # (no conversion in this step's forward)
+                self._x_bf16(X, ws)
+            ws.xb_fresh = False
+            if getattr(ws, "xb_ready", None) is not None:  # (converted on the side stream)
+                torch.cuda.current_stream().wait_event(ws.xb_ready)
+                ws.xb_ready = None
+            if getattr(ws, "dGsumb", None) is None:
+                ws.dGsumb = torch.empty((B, 4 * H), device=self.device, dtype=torch.bfloat16)
+            _ops.cvt_bf16_batch_([ws.dGsum], [ws.dGsumb], [B, 4 * H, 4 * H, B, 4 * H, 4 * H, 0])
+        # split-K 3 at B = 8192 (scripts/x1_sweep.py, us for 1/2/3/4/6/8/16:
+        # 137/84/76/81/79/90/134: one product per k-block leaves the split-K
+        # atomics a larger share than in the three-piece form)
+        with self._timed("lstm_x_projection_grad", ("mfma", 2.0 * B * (m1 - m0) * 4 * H, "bf16")):
             ops.gemm_x3p_tn(ws.Xb.view(-1)[m0:], 0, ws.dGsumb, 0, gK[m0:m1], m1 - m0, 4 * H, B,
-                            C2p, 4 * H, 4 * H, splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
+                            C2p, 4 * H, 4 * H, splitk=self._sk(max(1, min(B // 2048, 3))),
                             colsum=bias_out, npieces=1)
-        else:
-            self._dw_bf16(ws.Xb[:, m0:], ws.dGsumb, gK[m0:m1], B, m1 - m0, 4 * H, C2p, 4 * H,
-                          bias_out)
-
-    # bf16 configuration, opt-in (MOG_X_GRAD_BF16_X1=1): the x-rows gradient on
-    # gemm_x3p_tn's one-piece form instead of gemm_bf16.hip's TN GEMM (bf16
-    # step 2.19 ms either way, two A/B pairs: not on the critical path there)
-    X_GRAD_BF16_X1 = os.environ.get("MOG_X_GRAD_BF16_X1", "0") == "1"
 
     # ------------------------------------------------------------- API ----
     def _prep(self, images, targets):

@@ -351,6 +351,12 @@ class AIRModel(_AirBase):
                 ops.split3_bf16(X, ws.X3, B, C2, C2, C2p, B * C2p)
                 ws.x3_ready = torch.cuda.Event()
                 ws.x3_ready.record(side)
+        elif need_grad and self.precision == "bf16" and B >= self.SIDE_MIN_BATCH:
+            # bf16: X converted once for the x-rows gradient, likewise
+            with torch.cuda.stream(self._fork(self._side_stream())):
+                self._x_bf16(X, ws)
+                ws.xb_ready = torch.cuda.Event()
+                ws.xb_ready.record(torch.cuda.current_stream())
         # loop-invariant x-projection of the inference LSTM (chain over x first)
         with self._timed("lstm_x_projection"):
             gemm([X], [Ki[:C2]], [ws.Gx], B, 4 * H, C2, C2, 4 * H, 4 * H)
@@ -572,25 +578,26 @@ class AIRModel(_AirBase):
         gKi = self._Kpad("infer_rnn_running/kernel", "grad")
         gKg = self._Kpad("gen_rnn_running/kernel", "grad")
         # LSTMCells: x rows from sum_t dG (the x input is loop-invariant)
-        with self._timed("lstm_x_projection_grad"):
-            if self.precision == "bf16":
-                self._x_grad_bf16(X, ws, gKi, G("infer_rnn_running/bias"), 0, C2)
-            elif getattr(ws, "x3_ready", None) is not None:
-                # X^T dGsum on the bf16 matrix cores from exact three-piece
-                # splits of both operands (gemm_x3.hip): the
-                # AIR x-rows gradient's form
-                torch.cuda.current_stream().wait_event(ws.x3_ready)
-                ws.x3_ready = None
-                if getattr(ws, "dG3", None) is None:
-                    ws.dG3 = torch.empty((3, B, 4 * H), device=self.device, dtype=torch.bfloat16)
-                ops.split3_bf16(ws.dGsum, ws.dG3, B, 4 * H, 4 * H, 4 * H, B * 4 * H)
-                C2p = self._pad8(C2)
+        if self.precision == "bf16":
+            self._x_grad_bf16(X, ws, gKi, G("infer_rnn_running/bias"), 0, C2)
+        elif getattr(ws, "x3_ready", None) is not None:
+            # X^T dGsum on the bf16 matrix cores from exact three-piece
+            # splits of both operands (gemm_x3.hip): the
+            # AIR x-rows gradient's form
+            torch.cuda.current_stream().wait_event(ws.x3_ready)
+            ws.x3_ready = None
+            if getattr(ws, "dG3", None) is None:
+                ws.dG3 = torch.empty((3, B, 4 * H), device=self.device, dtype=torch.bfloat16)
+            ops.split3_bf16(ws.dGsum, ws.dG3, B, 4 * H, 4 * H, 4 * H, B * 4 * H)
+            C2p = self._pad8(C2)
+            with self._timed("lstm_x_projection_grad", ("mfma", 12.0 * B * C2 * 4 * H, "bf16")):
                 ops.gemm_x3p_tn(ws.X3.view(-1), B * C2p, ws.dG3, B * 4 * H, gKi[:C2], C2, 4 * H,
-                                B, C2p, 4 * H, 4 * H, splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
+                                B, C2p, 4 * H, 4 * H,
+                                splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
                                 colsum=G("infer_rnn_running/bias"))
-            else:
-                self._dw(X, ws.dGsum, gKi[:C2], B, C2, 4 * H, C2, 4 * H,
-                         G("infer_rnn_running/bias"))
+        else:
+            self._dw(X, ws.dGsum, gKi[:C2], B, C2, 4 * H, C2, 4 * H,
+                     G("infer_rnn_running/bias"))
         # M = LU (16-byte aligned LDS-DMA operands): rows Z+3+H.. of the
         # product land in the kernels' own pad rows (ParamStore pad), never in
         # a neighbouring variable's gradient
