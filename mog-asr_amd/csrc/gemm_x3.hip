@@ -437,8 +437,6 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
   // waits for the load there and serialises the prefetch
   u32x4 ra[NT_NLA];
   u32x4 rb[3][NT_NLB];
-  const float4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  const u32x4 z4 = {0u, 0u, 0u, 0u};
   // Buffer loads: the workgroup's A rows behind one descriptor and each B
   // piece behind its own, the row offsets in the per-thread (range-checked)
   // offset, only the uniform k-tile step in the scalar offset, which the

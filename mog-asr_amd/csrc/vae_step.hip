@@ -804,7 +804,6 @@ __global__ __launch_bounds__(256) void pack_frag_f32_kernel(PackF32 a) {
 
 }  // namespace
 
-int mog_internal_stn_vae_pipe(const StepArgs& p, int grid, int la, hipStream_t s);
 
 extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int Z, int G1,
                                         int G2, const float* x, const float* theta_f,
@@ -894,67 +893,6 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   }
   // MOG_VS_LA (profiling): sampler gather lookahead of the 64-image form
   static const int la = getenv("MOG_VS_LA") ? atoi(getenv("MOG_VS_LA")) : 3;
-  // The pipelined form (vae_pipe.hip: role-split persistent workgroups, two
-  // tiles in flight per CU) from three 64-image tiles per CU on; it needs the
-  // saved glimpse buffer as its staging area.  MOG_VS_PIPE=0 / 1 forces.
-  {
-    const long ntiles = ((long)B + 63) / 64;
-    bool pipe = false && save && gb != nullptr && ntiles >= 3L * ncu &&
-                (reinterpret_cast<size_t>(eps_z) & 15) == 0 &&
-                (p.x_period == B || p.x_period % 64 == 0);
-    if (const char* e = getenv("MOG_VS_PIPE")) pipe = atoi(e) != 0 && gb != nullptr &&
-        (reinterpret_cast<size_t>(eps_z) & 15) == 0 && (p.x_period == B || p.x_period % 64 == 0);
-    if (pipe) {
-      const int grid = (int)std::max<long>(std::min<long>(ncu, ntiles), (ntiles + 7) / 8);
-      static const int pla = getenv("MOG_VS_PIPE_LA") ? atoi(getenv("MOG_VS_PIPE_LA")) : 3;
-      static long long* pbuf = nullptr;
-      static size_t pcap = 0;
-      p.tstamp = nullptr;
-      if (getenv("MOG_VS_TIMING")) {
-        if (pcap < (size_t)grid * 128) {
-          if (pbuf) (void)hipFree(pbuf);
-          pcap = (size_t)grid * 128;
-          if (hipMalloc(&pbuf, pcap * sizeof(long long)) != hipSuccess) return MOG_ERR_INVALID;
-        }
-        (void)hipMemsetAsync(pbuf, 0, pcap * sizeof(long long), s);
-        p.tstamp = pbuf;
-      }
-      MOG_TRY(mog_internal_stn_vae_pipe(p, grid, pla, s));
-      if (p.tstamp) {
-        std::vector<long long> h((size_t)grid * 128);
-        (void)hipStreamSynchronize(s);
-        (void)hipMemcpy(h.data(), pbuf, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
-        // per tile: M wait->L1 end, L1 end->g2 end, output; S sample, write;
-        // inside L1 end->g2 end: L1 epilogue, L2, mu/lv, sample, g1, g2
-        double a[5] = {0}, f[6] = {0};
-        long cnt = 0, scnt = 0;
-        long long t0 = -1, t1 = 0;
-        for (int b = 0; b < grid; ++b)
-          for (int i = 0; i < 8; ++i) {
-            const long long* r = &h[((size_t)b * 8 + i) * 16];
-            if (r[0] == 0) continue;
-            ++cnt;
-            a[0] += (double)(r[1] - r[0]); a[1] += (double)(r[2] - r[1]); a[2] += (double)(r[3] - r[2]);
-            if (r[4] && r[5]) a[3] += (double)(r[5] - r[4]);
-            if (r[6] && r[7]) { a[4] += (double)(r[7] - r[6]); ++scnt; }
-            const long long ms[7] = {r[1], r[8], r[9], r[10], r[11], r[12], r[2]};
-            for (int q = 0; q < 6; ++q) if (ms[q] && ms[q + 1]) f[q] += (double)(ms[q + 1] - ms[q]);
-            t0 = t0 < 0 ? r[0] : std::min(t0, r[0]);
-            t1 = std::max(t1, std::max(r[3], r[7]));
-          }
-        if (cnt)
-          fprintf(stderr, "stn_vae_step pipe grid=%d tiles=%ld (us, mean per tile; 100 MHz): M L1 %.2f "
-                  "L2..g2 %.2f out %.2f | S sample %.2f write %.2f | span %.2f\n", grid, cnt,
-                  a[0] / cnt / 100.0, a[1] / cnt / 100.0, a[2] / cnt / 100.0, a[3] / cnt / 100.0,
-                  scnt ? a[4] / scnt / 100.0 : 0.0, (t1 - t0) / 100.0);
-        if (cnt)
-          fprintf(stderr, "  M detail: L1epi %.2f L2 %.2f mulv %.2f sample %.2f g1 %.2f g2 %.2f\n",
-                  f[0] / cnt / 100.0, f[1] / cnt / 100.0, f[2] / cnt / 100.0, f[3] / cnt / 100.0,
-                  f[4] / cnt / 100.0, f[5] / cnt / 100.0);
-      }
-      return 0;
-    }
-  }
   if (mt == 4 && la == 4) stn_vae_step_kernel<4, 16, 4, 4><<<nblk, 1024, 0, s>>>(p);
   else if (mt == 4 && la == 5) stn_vae_step_kernel<4, 16, 4, 5><<<nblk, 1024, 0, s>>>(p);
   else if (mt == 4) stn_vae_step_kernel<4, 16, 4><<<nblk, 1024, 0, s>>>(p);

@@ -1,6 +1,5 @@
 // Tile-level building blocks of the fused STN-read -> glimpse-VAE ->
-// STN-write step kernels (vae_step.hip: the lockstep form; vae_pipe.hip: the
-// role-split pipelined form): MFMA dense layers over LDS-resident activation
+// STN-write step kernels (vae_step.hip): MFMA dense layers over LDS-resident activation
 // tiles with weights streamed from L2 in B-fragment order, the STN read
 // sampler and the STN write of a tile's canvas parts.  Everything is in an
 // anonymous namespace: each translation unit gets its own copies.
