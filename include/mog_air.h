@@ -29,7 +29,8 @@ extern "C" {
  * Batched over `batch` (<= 8) problems given as HOST arrays of device
  * pointers.  A(m,k) = transA ? A[k*lda+m] : A[m*lda+k]; B likewise.
  * epi: 0 store(+bias) 1 relu 2 softplus(TF) 3 sigmoid(acc+bias+aux*aux_scale)
- *      4 acc*sigmoid(aux) 5 atomic-add 6 relu-backward (aux = activation).
+ *      4 acc*(1-exp(-aux)) [= acc*sigmoid(x), aux = softplus(x), the layer's
+ *      output] 5 atomic-add 6 relu-backward (aux = activation).
  * With splitk == 1 every output is one k-ordered fp32 fma chain (bit-exact
  * with the oracle).  splitk > 1 requires epi 5.  colsum (epi 5 only, may be
  * NULL): colsum[z][n] += sum_k B_z(k, n) — the bias gradient of a weight-
@@ -69,7 +70,8 @@ int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb, float* C, 
  * layers w.r.t. their inputs): C[M][N] = sum_k A[m][k] B[n][k], A fp32 [M][lda]
  * split into three bf16 pieces inside the kernel, B = W [N][K] given as the
  * three pieces of mog_split3_bf16 (piece p at B3 + p * sb, row pitch ldb).
- * epi 0: store; 1: C = v * sigmoid(aux[m][n]) (dX through softplus).
+ * epi 0: store; 1: C = v * (1 - exp(-aux[m][n])) (dX through softplus; aux =
+ * the softplus output, sigmoid(x) = 1 - exp(-softplus(x))).
  * K, ldb, sb multiples of 8; N, lda, ldc, ldaux multiples of 4; deterministic. */
 int mog_gemm_x3_nt(const float* A, const void* B3, long sb, float* C, const float* aux, int M,
                    int N, int K, int lda, int ldb, int ldc, int ldaux, int epi, void* stream);
@@ -243,8 +245,10 @@ int mog_pack_frag_f32(int n, const float* const* W, const int* K, const int* N,
  * mog_gemm_f32_sigmoid_philox / EPI_SIGMOID_NOISE, mog_stn_write_parts).
  * wt[7]: mog_pack_frag_f32 packs of the seven VAE weights (order as
  * mog_stn_vae_step_forward's), bias[7] fp32.  Saved for the backward, fp32:
- * g [B,784], a1pre/a1 [B,512], a2pre/a2 [B,256], mu/lv [B,50], d1pre/d1
- * [B,256], d2pre/d2 [B,512] -- all given, or all NULL (forward only); z
+ * g [B,784], a1 [B,512], a2 [B,256], mu/lv [B,50], d1 [B,256], d2 [B,512]
+ * -- all given, or all NULL (forward only); the pre-activations a1pre, a2pre,
+ * d1pre, d2pre are optional (NULL: not stored; the softplus backward needs
+ * only the outputs, epi 4 of mog_gemm_f32 / 1 of mog_gemm_x3_nt); z
  * [B,50] and r [B,784] are always written.  Tiles of 32 images: x_period > 0
  * requires x_period % 32 == 0 and runloss == NULL.  Reference VAE shape only.
  * Replaces air_model.py:523-588 at fp32. */
@@ -399,6 +403,18 @@ int mog_asr_step_backward(int B, int train, int fix_steps, float temperature,
 /* ---- noise (tf.random_normal / random_uniform sites, perf mode) --------- */
 int mog_rng_fill(float* out, long n, unsigned long long seed, unsigned long long offset,
                  int normal, void* stream);
+/* Up to 8 buffers in one launch (host arrays): buffer j is bit-identical to
+ * mog_rng_fill(out[j], n[j], seed, offset[j], normal[j]).  The step's five
+ * noise draws (air_model.py:191, vae.py:29,44, concrete.py:23). */
+int mog_rng_fill_batch(int nbuf, float* const* out, const long* n, unsigned long long seed,
+                       const unsigned long long* offset, const int* normal, void* stream);
+
+/* ---- step resets ----------------------------------------------------------
+ * Up to 8 buffers of n[j] 32-bit words set to value[j] in one launch (host
+ * arrays): the loop state at the start of a step (tf.while_loop's initial
+ * values, air_model.py:815-826) and the zeroed gradient accumulators. */
+int mog_fill32_batch(int nbuf, void* const* dst, const long* n, const unsigned* value,
+                     void* stream);
 
 /* ---- measurement / test instruments (no reference counterpart) ----------
  * dst[i] = src[i] for n4 float4s (16-byte aligned): the copy bandwidth the

@@ -15,6 +15,8 @@
 //   vae_sample_fwd/bwd   z = mu + eps sqrt(exp(lv)) (vae.py:27-30) + VAE KL
 //                        (air_model.py:718-736)
 //   recon_loss           clip, BCE, MSE, per-image loss, dL/dcanvas (:866-900)
+#include <algorithm>
+
 #include "mog_common.h"
 
 namespace {
@@ -649,6 +651,29 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* X, int R, int 
   atomicAdd(out + col, s);
 }
 
+// Up to 8 buffers filled with a 32-bit pattern in one launch (the step's
+// loop-state resets: stopping sum, running loss, counts, live flags; the
+// gradient buffer): grid row j covers buffer j.
+constexpr int FILL_MAX = 8;
+struct FillBatch {
+  unsigned* dst[FILL_MAX];
+  long n[FILL_MAX];
+  unsigned v[FILL_MAX];
+};
+__global__ __launch_bounds__(256) void fill32_batch_kernel(FillBatch f) {
+  const int j = blockIdx.y;
+  const long n = f.n[j], stride = (long)gridDim.x * 256 * 4;
+  const unsigned v = f.v[j];
+  unsigned* d = f.dst[j];
+  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 4 <= n && (reinterpret_cast<size_t>(d + i) & 15) == 0) {
+      *reinterpret_cast<uint4*>(d + i) = make_uint4(v, v, v, v);
+    } else {
+      for (long k = i; k < n && k < i + 4; ++k) d[k] = v;
+    }
+  }
+}
+
 // out[i] = a[i] + b[i]
 __global__ __launch_bounds__(256) void add_kernel(const float* a, const float* b, float* out,
                                                   long n) {
@@ -856,6 +881,27 @@ extern "C" int mog_colsum_add(const float* X, int R, int N, int ld, float* out, 
   const int rpb = 256;
   dim3 g(mog_cdiv(N, 256), mog_cdiv(R, rpb));
   colsum_kernel<<<g, 256, 0, mog_stream(stream)>>>(X, R, N, ld, rpb, out);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_fill32_batch(int nbuf, void* const* dst, const long* n, const unsigned* value,
+                                void* stream) {
+  MOG_CHECK_ARG(nbuf >= 0 && nbuf <= FILL_MAX && (nbuf == 0 || (dst && n && value)));
+  FillBatch f;
+  long mx = 0;
+  for (int j = 0; j < FILL_MAX; ++j) {
+    const bool on = j < nbuf;
+    f.dst[j] = on ? reinterpret_cast<unsigned*>(dst[j]) : nullptr;
+    f.n[j] = on ? n[j] : 0;
+    f.v[j] = on ? value[j] : 0u;
+    if (on) {
+      MOG_CHECK_ARG(dst[j] != nullptr && n[j] >= 0 && (reinterpret_cast<size_t>(dst[j]) & 3) == 0);
+      mx = n[j] > mx ? n[j] : mx;
+    }
+  }
+  if (nbuf == 0 || mx == 0) return 0;
+  const long blocks = std::min<long>((long)mog_cdiv((mx + 3) / 4, 256), 2048);
+  fill32_batch_kernel<<<dim3((unsigned)blocks, nbuf), 256, 0, mog_stream(stream)>>>(f);
   MOG_LAUNCH_RET();
 }
 

@@ -37,7 +37,8 @@ enum {
   EPI_RELU = 1,           // C = relu(acc + bias), Cpre = acc + bias
   EPI_SOFTPLUS = 2,       // C = softplus_tf(acc + bias), Cpre = acc + bias
   EPI_SIGMOID_NOISE = 3,  // C = sigmoid((acc + bias) + aux*scale), Cpre = acc + bias
-  EPI_SOFTPLUS_BWD = 4,   // C = acc * sigmoid(aux)        (dX through softplus)
+  EPI_SOFTPLUS_BWD = 4,   // C = acc * (1 - exp(-aux))     (dX through softplus; aux = its
+                          //  output: sigmoid(x) = 1 - exp(-softplus(x)))
   EPI_ATOMIC = 5,         // C += acc  (atomic; split-K / batch reduction)
   EPI_RELU_BWD = 6,       // C = aux > 0 ? acc : 0          (dX through relu)
 };
@@ -253,7 +254,7 @@ __device__ __forceinline__ void store_tile(const floatx4 (&acc)[MI][NI], const G
           continue;
         }
         if (EPI == EPI_SOFTPLUS_BWD) {
-          C[o] = v * mog_sigmoidf(xq[mi][ni][r]);
+          C[o] = v * -mog_expm1f(-xq[mi][ni][r]);
           continue;
         }
         if (EPI == EPI_RELU_BWD) {
@@ -371,7 +372,7 @@ __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[BM / 32][BN
         float w = v[e];
         pre[e] = w;
         if (EPI == EPI_SOFTPLUS_BWD) {
-          o[e] = w * mog_sigmoidf(x[e]);
+          o[e] = w * -mog_expm1f(-x[e]);
         } else if (EPI == EPI_RELU_BWD) {
           o[e] = x[e] > 0.0f ? w : 0.0f;
         } else {

@@ -409,7 +409,8 @@ __device__ __forceinline__ floatx4 xt_quad_transpose(const floatx4& a, int lane)
   return floatx4{r0, r1, r2, r3};
 }
 
-// EPI: 0 store, 1 softplus backward.  The next k-tile's loads are in flight
+// EPI: 0 store, 1 softplus backward (aux = the softplus output p:
+// sigmoid(x) = 1 - exp(-p) = -expm1(-p)).  The next k-tile's loads are in flight
 // under the MFMAs (one register set: a second, loads two MFMA phases ahead,
 // measured no faster; neither was a double-buffered 8-wave form with the
 // split woven between the MFMA passes, 158 -> 162 us)
@@ -559,7 +560,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_kernel(X3NtArgs D) {
       float o[4] = {v[0], v[1], v[2], v[3]};
       if (EPI == 1) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = v[q] * mog_sigmoidf(__uint_as_float(xq[mi][ni][q]));
+        for (int q = 0; q < 4; ++q) o[q] = v[q] * -mog_expm1f(-__uint_as_float(xq[mi][ni][q]));
       }
       if (row < M && col < N)
         *reinterpret_cast<float4*>(D.C + (size_t)row * D.ldc + col) = make_float4(o[0], o[1], o[2], o[3]);

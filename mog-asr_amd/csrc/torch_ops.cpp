@@ -669,6 +669,43 @@ void rng_fill_(Tensor out, int64_t seed, int64_t offset, bool normal) {
         o.name);
 }
 
+// several noise buffers / 32-bit fills in one launch
+void rng_fill_batch_(at::TensorList out, int64_t seed, at::IntArrayRef offset,
+                     at::IntArrayRef normal) {
+  Op o("rng_fill_batch_");
+  TORCH_CHECK(out.size() == offset.size() && out.size() == normal.size(), o.name, ": lengths");
+  vector<float*> p;
+  vector<long> n;
+  vector<unsigned long long> off;
+  vector<int> nm;
+  for (size_t j = 0; j < out.size(); ++j) {
+    p.push_back(o.f(out[j], out[j].numel(), "out"));
+    n.push_back(out[j].numel());
+    off.push_back((unsigned long long)offset[j]);
+    nm.push_back(normal[j] != 0);
+  }
+  GUARD(o);
+  check(mog_rng_fill_batch((int)p.size(), p.data(), n.data(), (unsigned long long)seed, off.data(),
+                           nm.data(), o.stream()),
+        o.name);
+}
+
+void fill32_batch_(at::TensorList dst, at::IntArrayRef value) {
+  Op o("fill32_batch_");
+  TORCH_CHECK(dst.size() == value.size(), o.name, ": lengths");
+  vector<void*> p;
+  vector<long> n;
+  vector<unsigned> v;
+  for (size_t j = 0; j < dst.size(); ++j) {
+    TORCH_CHECK(dst[j].element_size() == 4 && dst[j].is_contiguous(), o.name, ": 32-bit contiguous");
+    p.push_back(o.need(dst[j], dst[j].scalar_type(), dst[j].numel(), "dst"));
+    n.push_back(dst[j].numel());
+    v.push_back((unsigned)value[j]);
+  }
+  GUARD(o);
+  check(mog_fill32_batch((int)p.size(), p.data(), n.data(), v.data(), o.stream()), o.name);
+}
+
 // stream-ordering test instrument (csrc/spin.hip): `anchor` names the device
 void spin_(const Tensor& anchor, int64_t ticks) {
   Op o("spin_");
@@ -1012,6 +1049,8 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
   m.def("add_(Tensor a, Tensor b, Tensor(a!) out, int n) -> ()");
   m.def("rng_fill_(Tensor(a!) out, int seed, int offset, bool normal) -> ()");
   m.def("spin_(Tensor anchor, int ticks) -> ()");
+  m.def("rng_fill_batch_(Tensor(a!)[] out, int seed, int[] offset, int[] normal) -> ()");
+  m.def("fill32_batch_(Tensor(a!)[] dst, int[] value) -> ()");
   m.def("lds_poison_(Tensor anchor, int bits) -> ()");
   m.def("copy_f4_(Tensor src, Tensor(a!) dst) -> ()");
   // AIR-ASR (air_number_bbox_location.py:384-1084)
@@ -1078,6 +1117,8 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("add_", &add_);
   m.impl("rng_fill_", &rng_fill_);
   m.impl("spin_", &spin_);
+  m.impl("rng_fill_batch_", &rng_fill_batch_);
+  m.impl("fill32_batch_", &fill32_batch_);
   m.impl("lds_poison_", &lds_poison_);
   m.impl("copy_f4_", &copy_f4_);
   m.impl("asr_pack_", &asr_pack_);

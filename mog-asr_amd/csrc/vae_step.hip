@@ -640,7 +640,8 @@ __global__ __launch_bounds__(1024, 1) void stn_vae_step_f32_kernel(StepArgsF p) 
             sA1[mrow * FS512 + kperm(n0 + j)] = post[j];
           }
           if (save && mrow < nb) {
-            st_stream(reinterpret_cast<floatx4*>(p.a1pre + (size_t)(b0 + mrow) * 512 + n0), pre);
+            if (p.a1pre)
+              st_stream(reinterpret_cast<floatx4*>(p.a1pre + (size_t)(b0 + mrow) * 512 + n0), pre);
             st_stream(reinterpret_cast<floatx4*>(p.a1 + (size_t)(b0 + mrow) * 512 + n0), post);
           }
         }
@@ -660,8 +661,9 @@ __global__ __launch_bounds__(1024, 1) void stn_vae_step_f32_kernel(StepArgsF p) 
         post[j] = mog_softplusf(pre[j]);
         dst[m * ldd + kperm(n0 + j)] = post[j];
       }
-      if (gpre != nullptr && m < nb) {
-        st_stream(reinterpret_cast<floatx4*>(gpre + (size_t)(b0 + m) * ldg + n0), pre);
+      if (gpost != nullptr && m < nb) {
+        if (gpre != nullptr)
+          st_stream(reinterpret_cast<floatx4*>(gpre + (size_t)(b0 + m) * ldg + n0), pre);
         st_stream(reinterpret_cast<floatx4*>(gpost + (size_t)(b0 + m) * ldg + n0), post);
       }
     };
@@ -670,7 +672,7 @@ __global__ __launch_bounds__(1024, 1) void stn_vae_step_f32_kernel(StepArgsF p) 
   float* sR2 = reinterpret_cast<float*>(arena + LayF::OFF_R2);
   // ---- 3. a2 = softplus(a1 W2 + b2) [M x 256] -> R2 ------------------------
   dense_f32<2, 32, 16, 1, 8>(sR1, FS512, p.wt[1], p.bias[1], 256, 0, 0, NW,
-                             sp_epi(sR2, FS256, save ? p.a2pre : nullptr, p.a2, 256), tid);
+                             sp_epi(sR2, FS256, save ? p.a2pre : nullptr, save ? p.a2 : nullptr, 256), tid);
   lds_barrier();
   STAMP(3);
   // ---- 4. mu | lv = a2 W + b [M x 50] (waves 0-3 | 4-7) -> R1 -------------
@@ -728,12 +730,12 @@ __global__ __launch_bounds__(1024, 1) void stn_vae_step_f32_kernel(StepArgsF p) 
   STAMP(5);
   // ---- 6. d1 = softplus(z Wg1 + b) [M x 256] -> R2 (K = 50 padded to 64) --
   dense_f32<2, 4, 16, 1, 4>(sZ, FSZ, p.wt[4], p.bias[4], 256, 0, 0, NW,
-                            sp_epi(sR2, FS256, save ? p.d1pre : nullptr, p.d1, 256), tid);
+                            sp_epi(sR2, FS256, save ? p.d1pre : nullptr, save ? p.d1 : nullptr, 256), tid);
   lds_barrier();
   STAMP(6);
   // ---- 7. d2 = softplus(d1 Wg2 + b) [M x 512] -> R1 -------------------------
   dense_f32<2, 16, 32, 2, 6>(sR2, FS256, p.wt[5], p.bias[5], 512, 0, 0, NW,
-                             sp_epi(sR1, FS512, save ? p.d2pre : nullptr, p.d2, 512), tid);
+                             sp_epi(sR1, FS512, save ? p.d2pre : nullptr, save ? p.d2 : nullptr, 512), tid);
   lds_barrier();
   STAMP(7);
   // ---- 8. r = sigmoid((d2 Wgo + b) + std eps) [M x 784] -> HBM ------------
@@ -955,7 +957,8 @@ extern "C" int mog_stn_vae_step_forward_f32(
   MOG_CHECK_ARG(x && theta_f && theta_b && mask && zval && eps_z && (eps_x || eps_gen) && wt && bias);
   MOG_CHECK_ARG(canvas_part && part_rows && vkl && z && r);
   const bool save = a1 != nullptr;
-  MOG_CHECK_ARG(!save || (g && a1pre && a2pre && a2 && mu && lv && d1pre && d1 && d2pre && d2));
+  // (the pre-activations are optional: the backward reads the outputs)
+  MOG_CHECK_ARG(!save || (g && a1 && a2 && mu && lv && d1 && d2));
   MOG_CHECK_ARG(save || !(g || a1pre || a2pre || a2 || mu || lv || d1pre || d1 || d2pre || d2));
   if (B == 0) return 0;
   StepArgsF p;

@@ -61,6 +61,8 @@ _SIGS = {
     "mog_optim_chunk_elems": [],
     "mog_clip_adam": [P, P, P, P, P, P, P, P, I, P, F, F, F, F, F, P],
     "mog_rng_fill": [P, L, ULL, ULL, I, P],
+    "mog_rng_fill_batch": [I, P, P, ULL, P, P, P],
+    "mog_fill32_batch": [I, P, P, P, P],
     "mog_spin": [LL, P],
     "mog_copy_f4": [P, P, L, P],
     "mog_lds_poison": [ctypes.c_uint, P],

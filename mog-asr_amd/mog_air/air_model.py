@@ -144,10 +144,10 @@ class _Workspace:
             self.d1b, self.d2b = eb(T, B, G1), eb(T, B, G2)
         else:
             self.g = e(T, B, W2)
-            self.a1pre, self.a1 = e(T, B, R1), e(T, B, R1)
-            self.a2pre, self.a2 = e(T, B, R2), e(T, B, R2)
-            self.d1pre, self.d1 = e(T, B, G1), e(T, B, G1)
-            self.d2pre, self.d2 = e(T, B, G2), e(T, B, G2)
+            # (post-activations only: the softplus backward reads sigmoid(x)
+            # as 1 - exp(-softplus(x)), mog_gemm_f32 epi 4)
+            self.a1, self.a2 = e(T, B, R1), e(T, B, R2)
+            self.d1, self.d2 = e(T, B, G1), e(T, B, G2)
         self.canvas = e(B, C2)
         # fused bf16 step: per-step canvas contributions, summed by the loss kernel
         parts = m._parts_layout(B)
@@ -416,6 +416,9 @@ class AIRModel:
             # it); _forward joins it after that GEMM
             side = self._fork(self._side_stream())
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            # the step's noise buffers in one launch, each with its own Philox
+            # counter range (bit-identical to one mog_rng_fill per buffer)
+            outs, offs, nrm = [], [], []
             for k, normal in (("eps_scale", True), ("eps_shift", True), ("eps_z", True),
                               ("eps_x", True), ("u", False)):
                 buf = getattr(ws, k)
@@ -425,9 +428,24 @@ class AIRModel:
                     # (bit-identical to filling the buffer)
                     ws.eps_x_offset = self._noise_ctr
                 else:
-                    ops.rng_fill(buf, self.noise_seed, self._noise_ctr, normal)
+                    outs.append(buf)
+                    offs.append(ops._i64(self._noise_ctr))
+                    nrm.append(1 if normal else 0)
                 self._noise_ctr += (buf.numel() + 3) // 4
+            _ops.rng_fill_batch_(outs, ops._i64(self.noise_seed), offs, nrm)
         ws.noise_side = side is not None
+
+    def _reset_loop_state(self, ws):
+        """tf.while_loop's initial state (air_model.py:815-826): stopping sum,
+        running loss, counts 0, live flags 1 for step 0 and 0 after (and the
+        running canvas when the step does not use parts) -- one launch (a
+        fill kernel: capturable, unlike a host copy)."""
+        bufs = [ws.stop, ws.runloss, ws.digits, ws.live[:1], ws.live[1:]]
+        vals = [0, 0, 0, 1, 0]
+        if ws.cparts is None:
+            bufs.append(ws.canvas)
+            vals.append(0)
+        _ops.fill32_batch_(bufs, vals)
 
     # AIR's _forward joins side-stream noise after the x-projection (the ASR
     # subclass fills on the current stream)
@@ -454,14 +472,8 @@ class AIRModel:
         ws.noise_side = False
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             # (after the noise on the side stream, when it went there)
-            if ws.cparts is None:  # parts: the loss kernel sums them into the canvas
-                ws.canvas.zero_()
-            ws.stop.zero_()
-            ws.runloss.zero_()
-            ws.digits.zero_()
-            ws.live.zero_()
-            ws.live[:1].fill_(1)  # (a fill kernel: capturable, unlike a host copy)
-            if need_grad and self.precision == "fp32" and self.X_GRAD_X3 == 2:
+            self._reset_loop_state(ws)
+            if need_grad and self._x3p_xgrad(B):
                 # the x-part gradient's A operand, split once per step
                 C2p = self._pad8(C2)
                 if getattr(ws, "X3", None) is None:
@@ -591,9 +603,9 @@ class AIRModel:
             gen = getattr(ws, "eps_x_offset", None) is not None
             off = ws.eps_x_offset + t0 * B * (W2 // 4) if gen else 0
             bias = [self._P("vae/" + n + "/biases") for n in self._VAE]
-            saved = [r_(getattr(ws, n)) if save else None
-                     for n in ("g", "a1pre", "a1", "a2pre", "a2", "mu", "lv", "d1pre", "d1",
-                               "d2pre", "d2")]
+            # (the pre-activations are not stored: None in their slots)
+            saved = [r_(getattr(ws, n)) if save and n is not None else None
+                     for n in ("g", None, "a1", None, "a2", "mu", "lv", None, "d1", None, "d2")]
             with self._timed("stn_vae_step_f32_all"):
                 _ops.stn_vae_step_f32_(TB, C, X, r_(ws.th_f), r_(ws.th_b), r_(ws.zmask),
                                        r_(ws.zval), r_(ws.eps_z), r_(ws.eps_x),
@@ -632,17 +644,17 @@ class AIRModel:
             for t in range(t0, t1):
                 ops.stn_forward(X, ws.th_f[t], (W, W), out=ws.g[t])
             gemm([v(ws.g)], [vw["recognition_1"]], [v(ws.a1)], TB, R1, W2, W2, R1, R1,
-                 epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]], Cpre=[v(ws.a1pre)])
+                 epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]])
             gemm([v(ws.a1)], [vw["recognition_2"]], [v(ws.a2)], TB, R2, R1, R1, R2, R2,
-                 epi=EPI_SOFTPLUS, bias=[vb["recognition_2"]], Cpre=[v(ws.a2pre)])
+                 epi=EPI_SOFTPLUS, bias=[vb["recognition_2"]])
             gemm([v(ws.a2), v(ws.a2)], [vw["rec_mean"], vw["rec_log_variance"]],
                  [v(ws.mu), v(ws.lv)], TB, Z, R2, R2, Z, Z,
                  bias=[vb["rec_mean"], vb["rec_log_variance"]])
             self._vae_sample_fwd_all(ws, None, 0, t0, t1)
             gemm([v(ws.z)], [vw["generative_1"]], [v(ws.d1)], TB, G1, Z, Z, G1, G1,
-                 epi=EPI_SOFTPLUS, bias=[vb["generative_1"]], Cpre=[v(ws.d1pre)])
+                 epi=EPI_SOFTPLUS, bias=[vb["generative_1"]])
             gemm([v(ws.d1)], [vw["generative_2"]], [v(ws.d2)], TB, G2, G1, G1, G2, G2,
-                 epi=EPI_SOFTPLUS, bias=[vb["generative_2"]], Cpre=[v(ws.d2pre)])
+                 epi=EPI_SOFTPLUS, bias=[vb["generative_2"]])
             if ws.eps_x_offset is not None:
                 # eps_x of steps t0.. in the epilogue: [T, B, W2] fill order
                 ops.gemm_sigmoid_philox(v(ws.d2), vw["gen_mean"], v(ws.r), vb["gen_mean"], TB, W2,
@@ -715,7 +727,8 @@ class AIRModel:
         HS = self.scale_hidden_units
         TB = T * B
         st = self.params
-        st.grad.zero_()
+        # the gradient buffer and the LSTM chain's dG sum, zeroed in one launch
+        _ops.fill32_batch_([st.grad, ws.dGsum], [0, 0])
         K = self._P("rnn/basic_lstm_cell/kernel")
         bK = self._P("rnn/basic_lstm_cell/bias")
         Wh = K[C2:]
@@ -792,7 +805,6 @@ class AIRModel:
                 torch.cuda.current_stream().wait_event(vae_done)
             split = self._bucket_split()
             self._reduce_bucket(split, self.params.total)
-        ws.dGsum.zero_()
         for t in reversed(range(T)):
             dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
             _ops.lstm_cell_backward_(ws.Gx if t == 0 else ws.G[t], bK if t == 0 else None,
@@ -873,16 +885,18 @@ class AIRModel:
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
         # dm = SigmoidGrad(r, dr) was written by the STN write backward
-        self._dx(ws.dm, "gen_mean", ws.dd2, TB, G2, W2, aux=ws.d2pre)
-        self._dx(ws.dd2, "generative_2", ws.dd1, TB, G1, G2, aux=ws.d1pre)
+        # (aux = the softplus outputs: epi 4 / NT epi 1 take sigmoid(x) as
+        # 1 - exp(-softplus(x)))
+        self._dx(ws.dm, "gen_mean", ws.dd2, TB, G2, W2, aux=ws.d2)
+        self._dx(ws.dd2, "generative_2", ws.dd1, TB, G1, G2, aux=ws.d1)
         gemm([ws.dd1], [vw["generative_1"]], [ws.dz_all], TB, Z, G1, G1, G1, Z, transB=True)
         _ops.vae_sample_backward_(TB, Z, float(self.vae_prior_mean),
                                   float(self.vae_prior_variance), float(gscale), ws.mu, ws.lv,
                                   ws.eps_z, ws.dz_all, ws.zmask, ws.dmu, ws.dlv, None, None, 0)
         gemm([ws.dmu], [vw["rec_mean"]], [ws.tmp_a2_all], TB, R2, Z, Z, Z, R2, transB=True)
         gemm([ws.dlv], [vw["rec_log_variance"]], [ws.da2], TB, R2, Z, Z, Z, R2,
-             transB=True, epi=EPI_SOFTPLUS_BWD, Cin=[ws.tmp_a2_all], aux=[ws.a2pre], ldaux=R2)
-        self._dx(ws.da2, "recognition_2", ws.da1, TB, R1, R2, aux=ws.a1pre)
+             transB=True, epi=EPI_SOFTPLUS_BWD, Cin=[ws.tmp_a2_all], aux=[ws.a2], ldaux=R2)
+        self._dx(ws.da2, "recognition_2", ws.da1, TB, R1, R2, aux=ws.a1)
         self._dx(ws.da1, "recognition_1", ws.dg_all, TB, W2, R1)
 
     def _vae_backward_bf16_all(self, ws, gscale):
@@ -923,17 +937,17 @@ class AIRModel:
         vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
         ops.stn_forward(X, ws.th_f[t], (W, W), out=ws.g[t])
         gemm([ws.g[t]], [vw["recognition_1"]], [ws.a1[t]], B, R1, W2, W2, R1, R1,
-             epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]], Cpre=[ws.a1pre[t]])
+             epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]])
         gemm([ws.a1[t]], [vw["recognition_2"]], [ws.a2[t]], B, R2, R1, R1, R2, R2,
-             epi=EPI_SOFTPLUS, bias=[vb["recognition_2"]], Cpre=[ws.a2pre[t]])
+             epi=EPI_SOFTPLUS, bias=[vb["recognition_2"]])
         gemm([ws.a2[t], ws.a2[t]], [vw["rec_mean"], vw["rec_log_variance"]],
              [ws.mu[t], ws.lv[t]], B, Z, R2, R2, Z, Z,
              bias=[vb["rec_mean"], vb["rec_log_variance"]])
         self._vae_sample_fwd(ws, t, None, 0)
         gemm([ws.z[t]], [vw["generative_1"]], [ws.d1[t]], B, G1, Z, Z, G1, G1,
-             epi=EPI_SOFTPLUS, bias=[vb["generative_1"]], Cpre=[ws.d1pre[t]])
+             epi=EPI_SOFTPLUS, bias=[vb["generative_1"]])
         gemm([ws.d1[t]], [vw["generative_2"]], [ws.d2[t]], B, G2, G1, G1, G2, G2,
-             epi=EPI_SOFTPLUS, bias=[vb["generative_2"]], Cpre=[ws.d2pre[t]])
+             epi=EPI_SOFTPLUS, bias=[vb["generative_2"]])
         gemm([ws.d2[t]], [vw["gen_mean"]], [ws.r[t]], B, W2, G2, G2, W2, W2,
              epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]],
              aux=[ws.eps_x[t]], ldaux=W2, aux_scale=lik_std)
@@ -954,8 +968,8 @@ class AIRModel:
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
         _ops.sigmoid_backward_(ws.r[t], ws.dr, ws.dm[t], B * W2)
-        self._dx(ws.dm[t], "gen_mean", ws.dd2[t], B, G2, W2, aux=ws.d2pre[t])
-        self._dx(ws.dd2[t], "generative_2", ws.dd1[t], B, G1, G2, aux=ws.d1pre[t])
+        self._dx(ws.dm[t], "gen_mean", ws.dd2[t], B, G2, W2, aux=ws.d2[t])
+        self._dx(ws.dd2[t], "generative_2", ws.dd1[t], B, G1, G2, aux=ws.d1[t])
         gemm([ws.dd1[t]], [vw["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z, transB=True)
         self._dz_hook(ws, t)
         _ops.vae_sample_backward_(B, Z, float(self.vae_prior_mean),
@@ -964,8 +978,8 @@ class AIRModel:
                                   None, None, 0)
         gemm([ws.dmu[t]], [vw["rec_mean"]], [ws.tmp_a2], B, R2, Z, Z, Z, R2, transB=True)
         gemm([ws.dlv[t]], [vw["rec_log_variance"]], [ws.da2[t]], B, R2, Z, Z, Z, R2,
-             transB=True, epi=EPI_SOFTPLUS_BWD, Cin=[ws.tmp_a2], aux=[ws.a2pre[t]], ldaux=R2)
-        self._dx(ws.da2[t], "recognition_2", ws.da1[t], B, R1, R2, aux=ws.a1pre[t])
+             transB=True, epi=EPI_SOFTPLUS_BWD, Cin=[ws.tmp_a2], aux=[ws.a2[t]], ldaux=R2)
+        self._dx(ws.da2[t], "recognition_2", ws.da1[t], B, R1, R2, aux=ws.a1[t])
         self._dx(ws.da1[t], "recognition_1", ws.dg, B, W2, R1)
 
     # bf16 configuration: VAE GEMM operands bf16 (fp32 accumulate), activations
@@ -1313,6 +1327,13 @@ class AIRModel:
     # 244 vs 428 us stand-alone, step 3.44 -> 3.37 ms); 1: split inside the
     # GEMM (318 us, no change in the step); 0: the fp32 MFMA split-K GEMM.
     X_GRAD_X3 = int(os.environ.get("MOG_X_GRAD_X3", "2"))
+    # the pre-split form from this batch: below it (the reference's batch of
+    # 64) the two split launches cost more than the fp32 chain's K = B pass
+    # (batch 64: x3p 12.3 + splits 9.6 us)
+    X3P_MIN_B = 256
+
+    def _x3p_xgrad(self, B):
+        return self.precision == "fp32" and self.X_GRAD_X3 == 2 and B >= self.X3P_MIN_B
     X3_SPLITK = int(os.environ.get("MOG_X3_SPLITK", "8"))
 
     # rows of the x-part of the LSTM kernel gradient per all-reduce bucket
@@ -1341,7 +1362,7 @@ class AIRModel:
         m_last = 0
         # (the x-rows gradient GEMM of every chunk is tagged; its operand
         # conversions / splits are not: they are other launches)
-        x3p = self.precision != "bf16" and self.X_GRAD_X3 == 2
+        x3p = self._x3p_xgrad(B)
         for m0 in range(0, C2, chunk):
             m_last = m0
             m1 = min(C2, m0 + chunk)
@@ -1363,7 +1384,7 @@ class AIRModel:
                                     m1 - m0, 4 * H, B, C2p, 4 * H, 4 * H,
                                     splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
                                     colsum=bias)
-            elif self.X_GRAD_X3:
+            elif self.X_GRAD_X3 == 1:
                 # fp32 operands split exactly into three bf16 pieces on the
                 # bf16 matrix cores (gemm_x3.hip: fp32-level accuracy)
                 with self._timed("lstm_x_projection_grad",

@@ -326,13 +326,7 @@ class AIRModel(_AirBase):
         Ki = self._Kpad("infer_rnn_running/kernel")
         Kg = self._Kpad("gen_rnn_running/kernel")
         bi, bg = self._N("infer_rnn_running/bias"), self._N("gen_rnn_running/bias")
-        if ws.cparts is None:
-            ws.canvas.zero_()
-        ws.stop.zero_()
-        ws.runloss.zero_()
-        ws.digits.zero_()
-        ws.live.zero_()
-        ws.live[:1].fill_(1)  # (a fill kernel: a host copy would stall the host)
+        self._reset_loop_state(ws)
         thr = self.hyper("stopping_threshold")
         temp = self.hyper("z_pres_temperature")
         lik_std = float(self.hyper("vae_likelihood_std"))
@@ -452,17 +446,14 @@ class AIRModel(_AirBase):
     def _backward(self, X, ws):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
         C, W, C2 = self.canvas_size, self.windows_size, self.C2
-        self.params.grad.zero_()
+        # the gradient buffer and the LSTM chains' accumulators in one launch
+        _ops.fill32_batch_([self.params.grad, ws.dh, ws.dhg, ws.dGsum, ws.dGgsum], [0] * 5)
         Ki = self._Kpad("infer_rnn_running/kernel")
         Kg = self._Kpad("gen_rnn_running/kernel")
         KU = Z + 3 + H
         gscale = self._gscale(B)
         fix = -1 if self.fix_steps is None else int(self.fix_steps)
         w20 = self._w20()
-        ws.dh.zero_()
-        ws.dhg.zero_()
-        ws.dGsum.zero_()
-        ws.dGgsum.zero_()
         _ops.asr_terms_backward_(B, T, self.canvas_size, self._cons, self._gammas(), float(gscale),
                                  float(gscale), ws.arec, ws.live, ws.zsum, ws.dreg)
         head_w = [self._N(n + "/kernel")[:H] for n in ("inf_shift/dense", "inf_shift/dense_2",

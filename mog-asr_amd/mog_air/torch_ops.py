@@ -239,10 +239,11 @@ def _gv_bwd(ctx, grads):
     dr = zeros(B, 784) if dr is None else dr.contiguous()
     dm, dd2, dd1, dzt = e(B, 784), e(B, 512), e(B, 256), e(B, 50)
     _ops.sigmoid_backward_(r, dr, dm, B * 784)
+    # (epi 4 reads the softplus OUTPUT: sigmoid(x) = 1 - exp(-softplus(x)))
     gemm([dm], [W[6]], [dd2], B, 512, 784, 784, 784, 512, transB=True, epi=EPI_SOFTPLUS_BWD,
-         aux=[d2p], ldaux=512)
+         aux=[d2], ldaux=512)
     gemm([dd2], [W[5]], [dd1], B, 256, 512, 512, 512, 256, transB=True, epi=EPI_SOFTPLUS_BWD,
-         aux=[d1p], ldaux=256)
+         aux=[d1], ldaux=256)
     gemm([dd1], [W[4]], [dzt], B, 50, 256, 256, 256, 50, transB=True)
     if dz is not None:
         _ops.add_(dzt, dz.contiguous(), dzt, B * 50)
@@ -257,9 +258,9 @@ def _gv_bwd(ctx, grads):
     tmp, da2, da1, dg = e(B, 256), e(B, 256), e(B, 512), e(B, 784)
     gemm([dmut], [W[2]], [tmp], B, 256, 50, 50, 50, 256, transB=True)
     gemm([dlvt], [W[3]], [da2], B, 256, 50, 50, 50, 256, transB=True, epi=EPI_SOFTPLUS_BWD,
-         Cin=[tmp], aux=[a2p], ldaux=256)
+         Cin=[tmp], aux=[a2], ldaux=256)
     gemm([da2], [W[1]], [da1], B, 512, 256, 256, 256, 512, transB=True, epi=EPI_SOFTPLUS_BWD,
-         aux=[a1p], ldaux=512)
+         aux=[a1], ldaux=512)
     gemm([da1], [W[0]], [dg], B, 784, 512, 512, 512, 784, transB=True)
     # weight / bias gradients: dW = X^T dY (fp32 atomics), db = colsum(dY)
     xs = (g, a1, a2, a2, z, d1, d2)
