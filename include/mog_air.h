@@ -42,15 +42,20 @@ int mog_gemm_f32(int batch, const float* const* A, const float* const* B, float*
                  int splitk, void* stream);
 
 /* fp32 weight gradient on the bf16 matrix cores (mog-asr_amd/csrc/gemm_x3.hip):
- * C[m][n] += sum_k A[k*lda+m] B[k*ldb+n] (atomic, split into `splitk` k-ranges),
- * colsum[n] += sum_k B[k*ldb+n] when colsum != NULL.  Each fp32 operand is split
+ * C[m][n] += sum_k A[k*lda+m] B[k*ldb+n] over `splitk` k-ranges, colsum[n] +=
+ * sum_k B[k*ldb+n] when colsum != NULL.  Split-K partials: with `work` (>=
+ * splitk * M * N floats) each range's product is stored there and a second
+ * launch adds the ranges into C in a fixed order (deterministic; plain stores
+ * instead of float atomics, which run at about 1.3 TB/s); work == NULL: float
+ * atomics into C.  One k-range: C += product by a plain read-add-write.  Each fp32 operand is split
  * exactly into three bf16 pieces; the six products down to 2^-16 relative are
  * accumulated in fp32 (error of the order of one fp32 product rounding; not a
  * k-ordered chain, so tolerance-gated like every split-K gradient).  The x-part
  * of the LSTM kernel gradient (TF MatMul gradient of air_model.py:454-456).
  * A, B 16-byte aligned; M, N, lda, ldb multiples of 4. */
 int mog_gemm_f32_x3_tn(const float* A, const float* B, float* C, float* colsum, int M, int N,
-                       int K, int lda, int ldb, int ldc, int splitk, void* stream);
+                       int K, int lda, int ldb, int ldc, int splitk, float* work, long work_elems,
+                       void* stream);
 
 /* The same product from operands split beforehand: mog_split3_bf16 writes the
  * three exact bf16 pieces of an fp32 [rows][cols] matrix (piece p at dst + p *
@@ -63,7 +68,7 @@ int mog_split3_bf16(const float* src, int rows, int cols, int ld_src, void* dst,
                     long piece_stride, void* stream);
 int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb, float* C, float* colsum,
                     int M, int N, int K, int lda, int ldb, int ldc, int splitk, int npieces,
-                    void* stream);
+                    float* work, long work_elems, void* stream);
 
 /* dX = epi(dY W^T) at fp32-level accuracy on the bf16 matrix cores (the VAE
  * input gradients; replaces the MatMul gradients of vae.py:18-46's dense

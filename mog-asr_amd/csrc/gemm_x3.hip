@@ -1,6 +1,10 @@
 // fp32 weight gradient on the bf16 matrix cores: C[M][N] += sum_k A[k][m] B[k][n]
-// (both operands fp32, k-major: dW = X^T dY over the batch rows), split-K with fp32
-// atomics, optional column sums of B (the bias gradient).
+// (both operands fp32, k-major: dW = X^T dY over the batch rows), split-K, optional
+// column sums of B (the bias gradient).  Split-K partials go to a workspace and
+// a second launch adds them into C in split order (deterministic; the float
+// atomics it replaces measured equal at 3 splits and 71.6 vs 87.7 us at 8 on
+// the bf16 x-rows gradient, scripts/x1_sweep.py); one split adds C += acc with
+// plain loads and stores.
 //
 // Every fp32 operand is split EXACTLY into three bf16 pieces by truncation,
 // x = x0 + x1 + x2 (x0 = the top 8 significand bits, x1 the next 8 of x - x0,
@@ -32,8 +36,14 @@
 //   * gemm_x3_nt_kernel (below): dX = dY W^T, dY split in-kernel, W split once
 //     per optimizer step -- the fp32 VAE input-gradient chain: 161 / 184 us at
 //     24,576 x 512 x 784 / 24,576 x 784 x 512 (hipBLASLt fp32 176 / 222 us).
-// MFMA is under half busy in every form (0.26-0.41 of the bf16 peak): the
-// one-stage, register-staged pipeline is the next cost.
+// MFMA is under half busy in every form (0.26-0.45 of the bf16 peak).  The
+// kernel moves ~9 TB/s of operand tiles from L2 / Infinity Cache into LDS in
+// both the one- and three-piece forms (663 MB / 72 us, 1.99 GB / 224 us at
+// 2500 x 1024 x 8192: 128 x 128 tiles re-read A 8x and B 20x), so its time
+// follows the bytes its tiles re-read, not the MFMA count.  An LDS-DMA
+// multi-stage form of the pre-split kernel (buffer_load ... lds, 2-4 stages,
+// 128 x 128 and 256 x 128 tiles, bank-swizzled transposed reads) measured no
+// faster: 70-95 us one-piece, 237-340 us three-piece (round 5, git history).
 #include <cstdlib>
 #include <type_traits>
 
@@ -95,8 +105,34 @@ struct X3Args {
   long sa, sb;
   float* C;
   float* colsum;
-  int M, N, K, lda, ldb, ldc, kchunk, nx, ny;
+  float* work;  // split-K partials [nsplit][M][N] (summed into C by splitk_reduce_kernel), or null
+  int M, N, K, lda, ldb, ldc, kchunk, nx, ny, nsplit;
 };
+
+// the accumulator tile of one wave (4 x 4 blocks of 16 x 16, lane (g, li) holds
+// rows 4 g .. 4 g + 3 of column li of each) into C: one split -> C += acc (a
+// plain read-add-write: no other workgroup touches these elements); split-K
+// with a workspace -> stored as this split's partial; else float atomics
+__device__ __forceinline__ void x3_epilogue(const X3Args& D, const floatx4 (&acc)[4][4], int r0,
+                                            int c0, int ks, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  const int mode = D.nsplit == 1 ? 0 : D.work != nullptr ? 1 : 2;
+  float* W = D.work + (size_t)ks * D.M * D.N;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + mi * 16 + g * 4 + r;
+        const int col = c0 + ni * 16 + li;
+        if (row < D.M && col < D.N) {
+          if (mode == 0) D.C[(size_t)row * D.ldc + col] += acc[mi][ni][r];
+          else if (mode == 1) W[(size_t)row * D.N + col] = acc[mi][ni][r];
+          else atomicAdd(D.C + (size_t)row * D.ldc + col, acc[mi][ni][r]);
+        }
+      }
+}
 
 constexpr int NP = (BM * BK / 8) / 256;  // 16-byte bf16 chunks per thread per piece (2)
 
@@ -311,31 +347,27 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
       atomicAdd(D.colsum + n0 + t, v);
     }
   }
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm + mi * 16 + (lane >> 4) * 4 + r;
-        const int col = n0 + wn + ni * 16 + (lane & 15);
-        if (row < M && col < N) atomicAdd(D.C + (size_t)row * D.ldc + col, acc[mi][ni][r]);
-      }
+  x3_epilogue(D, acc, m0 + wm, n0 + wn, ks, lane);
 }
 
+
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+void splitk_reduce(const X3Args& D, hipStream_t s);
 
 void launch_x3(bool pre, X3Args D, int splitk, hipStream_t s, int npieces = 3) {
   int kchunk = (D.K + splitk - 1) / splitk;
   kchunk = ((kchunk + BK - 1) / BK) * BK;
   D.kchunk = kchunk;
   const int nsplit = (D.K + kchunk - 1) / kchunk;
+  D.nsplit = nsplit;
   D.nx = mog_cdiv(D.N, BN);
   D.ny = mog_cdiv(D.M, BM);
   const long nwg = (long)D.nx * D.ny * nsplit;
   if (pre && npieces == 1) gemm_x3_tn_kernel<true, 1><<<dim3((unsigned)nwg), 256, 0, s>>>(D);
   else if (pre) gemm_x3_tn_kernel<true><<<dim3((unsigned)nwg), 256, 0, s>>>(D);
   else gemm_x3_tn_kernel<false><<<dim3((unsigned)nwg), 256, 0, s>>>(D);
+  if (nsplit > 1 && D.work != nullptr) splitk_reduce(D, s);
 }
 
 // the three exact truncated bf16 pieces of an fp32 [rows][cols] matrix: piece p
@@ -358,6 +390,40 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ s
   *reinterpret_cast<u32x2*>(d + 2 * pstride) = p2;
 }
 
+// C[m][n] += sum over s = 0 .. nsplit-1 of work[s][m][n], in that order (the
+// split-K partials of the TN forms: deterministic, plain loads and stores)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ W, int nsplit,
+                                                            float* C, int M, int N, int ldc,
+                                                            bool vec) {
+  const long MN = (long)M * N;
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= MN) return;
+  if (vec) {
+    float4 v = *reinterpret_cast<const float4*>(W + i);
+    for (int s = 1; s < nsplit; ++s) {
+      const floatx4 u = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(W + s * MN + i));
+      v.x += u[0]; v.y += u[1]; v.z += u[2]; v.w += u[3];
+    }
+    const int m = (int)(i / N), n = (int)(i % N);
+    float4* c = reinterpret_cast<float4*>(C + (size_t)m * ldc + n);
+    float4 o = *c;
+    o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
+    *c = o;
+    return;
+  }
+  for (long e = i; e < min(i + 4, MN); ++e) {
+    float v = W[e];
+    for (int s = 1; s < nsplit; ++s) v += W[s * MN + e];
+    C[(size_t)(e / N) * ldc + e % N] += v;
+  }
+}
+
+void splitk_reduce(const X3Args& D, hipStream_t s) {
+  const long n4 = ((long)D.M * D.N + 3) / 4;
+  const bool vec = D.N % 4 == 0 && D.ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(D.C) & 15) == 0;
+  splitk_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), 256, 0, s>>>(D.work, D.nsplit, D.C, D.M,
+                                                                         D.N, D.ldc, vec);
+}
 
 // ---- NT form: C[M][N] = epi(sum_k A[m][k] B[n][k]) ------------------------
 // The input gradients of the VAE (dX = dY W^T: A = dY [M][lda] fp32,
@@ -583,8 +649,10 @@ extern "C" int mog_split3_bf16(const float* src, int rows, int cols, int ld_src,
 
 extern "C" int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb, float* C,
                                float* colsum, int M, int N, int K, int lda, int ldb, int ldc,
-                               int splitk, int npieces, void* stream) {
+                               int splitk, int npieces, float* work, long work_elems,
+                               void* stream) {
   MOG_CHECK_ARG(A3 && B3 && C && M >= 0 && N >= 0 && K >= 0 && splitk >= 1);
+  MOG_CHECK_ARG(work == nullptr || work_elems >= (long)splitk * M * N);
   MOG_CHECK_ARG(npieces == 3 || npieces == 1);
   // 16-byte chunks of 8 bf16: strides and piece strides multiples of 8 (a chunk
   // that starts below M ends inside the row; its columns >= M are not stored)
@@ -596,7 +664,7 @@ extern "C" int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb,
   X3Args D{};
   D.A3 = reinterpret_cast<const __bf16*>(A3);
   D.B3 = reinterpret_cast<const __bf16*>(B3);
-  D.sa = sa; D.sb = sb; D.C = C; D.colsum = colsum;
+  D.sa = sa; D.sb = sb; D.C = C; D.colsum = colsum; D.work = work;
   D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc;
   launch_x3(true, D, splitk, mog_stream(stream), npieces);
   MOG_LAUNCH_RET();
@@ -604,15 +672,16 @@ extern "C" int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb,
 
 extern "C" int mog_gemm_f32_x3_tn(const float* A, const float* B, float* C, float* colsum,
                                   int M, int N, int K, int lda, int ldb, int ldc, int splitk,
-                                  void* stream) {
+                                  float* work, long work_elems, void* stream) {
   MOG_CHECK_ARG(A && B && C && M >= 0 && N >= 0 && K >= 0 && splitk >= 1);
+  MOG_CHECK_ARG(work == nullptr || work_elems >= (long)splitk * M * N);
   // float4 rows: 16-byte operands, widths and strides multiples of 4
   MOG_CHECK_ARG(al16(A) && al16(B) && M % 4 == 0 && N % 4 == 0 && lda % 4 == 0 &&
                 ldb % 4 == 0 && lda >= M && ldb >= N && ldc >= N);
   MOG_CHECK_ARG((long)K * lda * 4 < (1L << 31) && (long)K * ldb * 4 < (1L << 31));
   if (M == 0 || N == 0 || K == 0) return 0;
   X3Args D{};
-  D.A = A; D.B = B; D.C = C; D.colsum = colsum;
+  D.A = A; D.B = B; D.C = C; D.colsum = colsum; D.work = work;
   D.M = M; D.N = N; D.K = K; D.lda = lda; D.ldb = ldb; D.ldc = ldc;
   launch_x3(false, D, splitk, mog_stream(stream));
   MOG_LAUNCH_RET();

@@ -889,16 +889,28 @@ void asr_step_backward_(int64_t B, bool train, int64_t fix_steps, double tempera
 
 }  // namespace
 
+// split-K partials of the TN forms: reduce = 1 -> a transient [splitk][M][N]
+// fp32 workspace from the caching allocator (on the op's stream) summed into C
+// in a fixed order after the GEMM (deterministic); 0 -> float atomics into C
+Tensor splitk_work(const Op& o, int64_t splitk, int64_t M, int64_t N, int64_t reduce) {
+  if (!reduce || splitk <= 1 || M <= 0 || N <= 0) return Tensor();
+  return at::empty({splitk * M * N}, at::TensorOptions().dtype(F32).device(*o.dev));
+}
+
 void gemm_f32_x3_tn_(const Tensor& A, const Tensor& B, Tensor C, const optional<Tensor>& colsum,
                      int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc,
-                     int64_t splitk) {
+                     int64_t splitk, int64_t reduce) {
   Op o("gemm_f32_x3_tn_");
   float* c = o.f(C, mat(M, N, ldc), "C");
   float* a = o.f(A, mat(K, M, lda), "A");
   float* b = o.f(B, mat(K, N, ldb), "B");
   float* cs = o.f(colsum, N, "colsum");
   GUARD(o);
-  check(mog_gemm_f32_x3_tn(a, b, c, cs, M, N, K, lda, ldb, ldc, splitk, o.stream()), o.name);
+  Tensor w = splitk_work(o, splitk, M, N, reduce);
+  check(mog_gemm_f32_x3_tn(a, b, c, cs, M, N, K, lda, ldb, ldc, splitk,
+                           w.defined() ? w.data_ptr<float>() : nullptr,
+                           w.defined() ? w.numel() : 0, o.stream()),
+        o.name);
 }
 
 void split3_bf16_(const Tensor& src, Tensor dst, int64_t rows, int64_t cols, int64_t ld_src,
@@ -912,7 +924,7 @@ void split3_bf16_(const Tensor& src, Tensor dst, int64_t rows, int64_t cols, int
 
 void gemm_x3p_tn_(const Tensor& A3, int64_t sa, const Tensor& B3, int64_t sb, Tensor C,
                   const optional<Tensor>& colsum, int64_t M, int64_t N, int64_t K, int64_t lda,
-                  int64_t ldb, int64_t ldc, int64_t splitk, int64_t npieces) {
+                  int64_t ldb, int64_t ldc, int64_t splitk, int64_t npieces, int64_t reduce) {
   Op o("gemm_x3p_tn_");
   float* c = o.f(C, mat(M, N, ldc), "C");
   const int64_t np1 = npieces - 1;
@@ -923,7 +935,9 @@ void gemm_x3p_tn_(const Tensor& A3, int64_t sa, const Tensor& B3, int64_t sb, Te
   const void* b = o.need(B3, BF16, np1 * sb + ext(K, N, ldb), "B3");
   float* cs = o.f(colsum, N, "colsum");
   GUARD(o);
+  Tensor w = splitk_work(o, splitk, M, N, reduce);
   check(mog_gemm_x3p_tn(a, sa, b, sb, c, cs, M, N, K, lda, ldb, ldc, splitk, npieces,
+                        w.defined() ? w.data_ptr<float>() : nullptr, w.defined() ? w.numel() : 0,
                         o.stream()),
         o.name);
 }
@@ -949,10 +963,10 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "int piece_stride) -> ()");
   m.def(
       "gemm_x3p_tn_(Tensor A3, int sa, Tensor B3, int sb, Tensor(a!) C, Tensor(b!)? colsum, "
-      "int M, int N, int K, int lda, int ldb, int ldc, int splitk, int npieces=3) -> ()");
+      "int M, int N, int K, int lda, int ldb, int ldc, int splitk, int npieces=3, int reduce=1) -> ()");
   m.def(
       "gemm_f32_x3_tn_(Tensor A, Tensor B, Tensor(a!) C, Tensor(b!)? colsum, int M, int N, "
-      "int K, int lda, int ldb, int ldc, int splitk) -> ()");
+      "int K, int lda, int ldb, int ldc, int splitk, int reduce=1) -> ()");
   m.def(
       "gemm_f32_(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, Tensor?[] Cin, "
       "Tensor(b!)?[] Cpre, Tensor?[] aux, Tensor(c!)?[] colsum, int M, int N, int K, int lda, "

@@ -805,15 +805,20 @@ class AIRModel:
                 torch.cuda.current_stream().wait_event(vae_done)
             split = self._bucket_split()
             self._reduce_bucket(split, self.params.total)
+        rec_early = T > 1 and heads_side and self.REC_WGRAD_SIDE
         for t in reversed(range(T)):
             dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
             _ops.lstm_cell_backward_(ws.Gx if t == 0 else ws.G[t], bK if t == 0 else None,
                                      ws.c[t - 1] if t > 0 else None, ws.c[t], ws.dh[t], dc_in,
                                      ws.dG[t], ws.dc[t % 2], ws.dGsum, B, H)
+            if t == 1 and rec_early:
+                # dG[1:] is final: the recurrent rows' gradient runs beside the
+                # chain's last step instead of beside the x-rows gradient
+                self._weight_grads_rec_side(ws)
             if t > 0:
                 gemm([ws.dG[t]], [Wh], [ws.dh[t - 1]], B, H, 4 * H, 4 * H, 4 * H, H,
                      transB=True, Cin=[ws.dh[t - 1]])
-        self._weight_grads_lstm(X, ws, side=heads_side)
+        self._weight_grads_lstm(X, ws, side=heads_side, rec_done=rec_early)
         if heads_side:  # (everything on the side stream: VAE, heads, dW_rec)
             torch.cuda.current_stream().wait_stream(self._side_stream())
             if self.HEADS_STREAM3 or self.REC_STREAM3:
@@ -1189,9 +1194,12 @@ class AIRModel:
             return self._dw(X, dY, out, K, M, N, lda, ldb, bias_out)
         tiles = ((M + 127) // 128) * ((N + 127) // 128)
         splitk = self._sk(max(1, min(K // 256, (512 + tiles - 1) // tiles)))
-        # six bf16 MFMA products per fp32 product (gemm_x3.hip)
+        # six bf16 MFMA products per fp32 product (gemm_x3.hip); float atomics
+        # for the 19-64 split-K partials of these <= 0.4 M-element outputs
+        # (through the workspace: 160 -> 229 us per launch in the step)
         with self._timed("vae_wgrad_x3", ("mfma", 12.0 * K * M * N, "bf16")):
-            ops.gemm_x3_tn(X, dY, out, M, N, K, lda, ldb, N, splitk=splitk, colsum=bias_out)
+            ops.gemm_x3_tn(X, dY, out, M, N, K, lda, ldb, N, splitk=splitk, colsum=bias_out,
+                           reduce=False)
 
     def _vae_wgrad_fp32(self, ws, name, t=None):
         """One VAE layer's weight / bias gradient over all T*B rows (fp32), or
@@ -1340,20 +1348,30 @@ class AIRModel:
     # (multiple of the 64-row GEMM tile; data parallel only)
     X_GRAD_CHUNK = 640
 
-    def _weight_grads_lstm(self, X, ws, side=False):
+    def _weight_grads_rec_side(self, ws):
+        """One GPU: the LSTM kernel's recurrent-rows gradient sum_t h[t-1]^T
+        dG[t] on a side stream, forked as soon as dG[1:] is final (before the
+        chain's step 0), so it overlaps that step instead of the x-rows
+        gradient."""
+        B, T, H, C2 = ws.B, self.max_steps, self.rnn_units, self.C2
+        gK = self._G("rnn/basic_lstm_cell/kernel")
+        st = self._stream3() if self.REC_STREAM3 else self._side_stream()
+        with torch.cuda.stream(self._fork(st)):
+            self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
+
+    def _weight_grads_lstm(self, X, ws, side=False, rec_done=False):
         """LSTM kernel / bias gradients.  Data parallel: the x-part X^T dGsum
         (2500 x 1024, 10 MB) is produced in row chunks, each handed to the
         all-reduce as soon as it is final, so the collective of chunk i runs
-        under the GEMM of chunk i+1; the recurrent rows and the bias go last."""
+        under the GEMM of chunk i+1; the recurrent rows and the bias go last.
+        rec_done: the recurrent rows were forked already (_weight_grads_rec_side)."""
         B, T, H, C2 = ws.B, self.max_steps, self.rnn_units, self.C2
         gK = self._G("rnn/basic_lstm_cell/kernel")
         gbK = self._G("rnn/basic_lstm_cell/bias")
-        if T > 1 and side and self.REC_WGRAD_SIDE:
-            # one GPU: the recurrent rows' gradient on the side stream, beside
-            # the x-rows gradient below (both need only the finished chain)
-            st = self._stream3() if self.REC_STREAM3 else self._side_stream()
-            with torch.cuda.stream(self._fork(st)):
-                self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
+        if rec_done:
+            pass
+        elif T > 1 and side and self.REC_WGRAD_SIDE:
+            self._weight_grads_rec_side(ws)
         elif T > 1:
             self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
         chunk = self.X_GRAD_CHUNK if self.grad_reducer is not None else C2
@@ -1383,7 +1401,7 @@ class AIRModel:
                     ops.gemm_x3p_tn(ws.X3.view(-1)[m0:], B * C2p, ws.dG3, B * 4 * H, gK[m0:m1],
                                     m1 - m0, 4 * H, B, C2p, 4 * H, 4 * H,
                                     splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
-                                    colsum=bias)
+                                    colsum=bias, reduce=False)
             elif self.X_GRAD_X3 == 1:
                 # fp32 operands split exactly into three bf16 pieces on the
                 # bf16 matrix cores (gemm_x3.hip: fp32-level accuracy)
@@ -1426,12 +1444,12 @@ class AIRModel:
             if getattr(ws, "dGsumb", None) is None:
                 ws.dGsumb = torch.empty((B, 4 * H), device=self.device, dtype=torch.bfloat16)
             _ops.cvt_bf16_batch_([ws.dGsum], [ws.dGsumb], [B, 4 * H, 4 * H, B, 4 * H, 4 * H, 0])
-        # split-K 3 at B = 8192 (scripts/x1_sweep.py, us for 1/2/3/4/6/8/16:
-        # 137/84/76/81/79/90/134: one product per k-block leaves the split-K
-        # atomics a larger share than in the three-piece form)
+        # split-K 8 at B = 8192, partials summed through the workspace
+        # (scripts/x1_sweep.py, us for 1/2/3/4/6/8 splits: 138/84/77/73/73/72;
+        # with float atomics 77/76/81/88 from 3 splits)
         with self._timed("lstm_x_projection_grad", ("mfma", 2.0 * B * (m1 - m0) * 4 * H, "bf16")):
             ops.gemm_x3p_tn(ws.Xb.view(-1)[m0:], 0, ws.dGsumb, 0, gK[m0:m1], m1 - m0, 4 * H, B,
-                            C2p, 4 * H, 4 * H, splitk=self._sk(max(1, min(B // 2048, 3))),
+                            C2p, 4 * H, 4 * H, splitk=self._sk(max(1, min(B // 1024, 8))),
                             colsum=bias_out, npieces=1)
 
     # ------------------------------------------------------------- API ----

@@ -57,11 +57,13 @@ def gemm(A: Sequence[torch.Tensor], B: Sequence[torch.Tensor], C: Sequence[torch
 
 
 def gemm_x3_tn(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: int,
-               lda: int, ldb: int, ldc: int, splitk: int = 8, colsum=None) -> None:
+               lda: int, ldb: int, ldc: int, splitk: int = 8, colsum=None,
+               reduce: bool = True) -> None:
     """C[M,N] += A^T B over K rows on the bf16 matrix cores with exact
     three-piece operand splits (fp32-level accuracy; mog_gemm_f32_x3_tn);
-    colsum += column sums of B."""
-    _ops.gemm_f32_x3_tn_(A, B, C, colsum, M, N, K, lda, ldb, ldc, int(splitk))
+    colsum += column sums of B.  reduce: split-K partials summed through a
+    workspace in a fixed order (deterministic); False: float atomics."""
+    _ops.gemm_f32_x3_tn_(A, B, C, colsum, M, N, K, lda, ldb, ldc, int(splitk), int(reduce))
 
 
 def split3_bf16(src: torch.Tensor, dst: torch.Tensor, rows: int, cols: int, ld_src: int,
@@ -73,11 +75,11 @@ def split3_bf16(src: torch.Tensor, dst: torch.Tensor, rows: int, cols: int, ld_s
 
 def gemm_x3p_tn(A3: torch.Tensor, sa: int, B3: torch.Tensor, sb: int, C: torch.Tensor, M: int,
                 N: int, K: int, lda: int, ldb: int, ldc: int, splitk: int = 8,
-                colsum=None, npieces: int = 3) -> None:
+                colsum=None, npieces: int = 3, reduce: bool = True) -> None:
     """gemm_x3_tn from operands split beforehand by split3_bf16
     (mog_gemm_x3p_tn); npieces=1: plain bf16 operands, one product."""
     _ops.gemm_x3p_tn_(A3, int(sa), B3, int(sb), C, colsum, M, N, K, lda, ldb, ldc, int(splitk),
-                      int(npieces))
+                      int(npieces), int(reduce))
 
 
 def gemm_x3_nt(A: torch.Tensor, B3: torch.Tensor, sb: int, C: torch.Tensor, M: int, N: int,

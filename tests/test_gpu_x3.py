@@ -214,3 +214,28 @@ def test_x3_nt_accuracy(M, N, K, epi):
     err = np.abs(C.cpu().numpy().astype(np.float64) - ref)
     assert np.isfinite(C.cpu().numpy()).all()
     assert (err <= 1e-6 * bound + 1e-30).all(), float((err / (bound + 1e-30)).max())
+
+
+@pytest.mark.parametrize("npieces", [1, 3])
+def test_x3p_splitk_reduce_deterministic(npieces):
+    """Split-K through the workspace (reduce=True, the default): the partials
+    are added in split order, so two launches give the same bits, and they
+    agree with the float-atomic form (reduce=False) to fp32 level."""
+    M, N, K = 300, 260, 3000
+    g = torch.Generator().manual_seed(7)
+    A = torch.randn(K, 304, generator=g).to(DEV)
+    B = torch.randn(K, N, generator=g).to(DEV)
+    A3 = torch.empty(3, K, 304, device=DEV, dtype=torch.bfloat16)
+    B3 = torch.empty(3, K, 264, device=DEV, dtype=torch.bfloat16)
+    ops.split3_bf16(A, A3, K, 304, 304, 304, K * 304)
+    ops.split3_bf16(B, B3, K, N, N, 264, K * 264)
+    outs = []
+    for red in (True, True, False):
+        C = torch.ones(M, N, device=DEV)
+        cs = torch.ones(N, device=DEV)
+        ops.gemm_x3p_tn(A3.view(-1), K * 304, B3, K * 264, C, M, N, K, 304, 264, N, splitk=7,
+                        colsum=cs, npieces=npieces, reduce=red)
+        torch.cuda.synchronize()
+        outs.append(C.cpu())
+    assert torch.equal(outs[0], outs[1])
+    assert float((outs[0] - outs[2]).abs().max()) <= 1e-5 * float(outs[2].abs().max())
