@@ -68,7 +68,9 @@ KERNEL_NAMES = {
                     "in-kernel (bf16 cores)",
     "vae_dgrad_x3": "gemm_x3_nt_kernel: VAE input gradients dY W^T (bf16 cores, 3-piece)",
     "vae_dgrad_f32": "gemm_f32 transB: VAE input gradients (fp32 chain)",
-    "wgrad_f32": "gemm_f32 transA split-K: heads / LSTM-recurrent / small VAE weight gradients",
+    "wgrad_f32": "gemm_f32 transA split-K: heads / small VAE weight gradients",
+    "rec_wgrad_x3": "gemm_x3_tn_kernel<false,3>: LSTM recurrent-rows weight gradient (bf16 cores, "
+                    "3-piece)",
     "wgrad_bf16": "gemm_bf16 TN: bf16 VAE weight gradients",
     "stn_write_bwd": "stn_bwd_kernel: STN write backward (through the output sigmoid)",
     "stn_read_bwd": "stn_bwd_kernel: STN read backward (dtheta only)",

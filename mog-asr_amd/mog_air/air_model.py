@@ -1353,11 +1353,28 @@ class AIRModel:
         dG[t] on a side stream, forked as soon as dG[1:] is final (before the
         chain's step 0), so it overlaps that step instead of the x-rows
         gradient."""
-        B, T, H, C2 = ws.B, self.max_steps, self.rnn_units, self.C2
-        gK = self._G("rnn/basic_lstm_cell/kernel")
         st = self._stream3() if self.REC_STREAM3 else self._side_stream()
         with torch.cuda.stream(self._fork(st)):
-            self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
+            self._dw_rec(ws)
+
+    def _dw_rec(self, ws):
+        """The LSTM kernel's recurrent rows: gK[C2:] += sum_t h[t-1]^T dG[t]
+        over (T-1) B rows.  fp32 from X3_MIN_ROWS: on the bf16 matrix cores
+        with exact three-piece splits (gemm_x3_tn, as the VAE weight
+        gradients; 256 x 1024 x 16,384 at B = 8192), else the fp32 split-K GEMM."""
+        B, T, H, C2 = ws.B, self.max_steps, self.rnn_units, self.C2
+        gK = self._G("rnn/basic_lstm_cell/kernel")
+        K = (T - 1) * B
+        if self.precision == "fp32" and self.REC_WGRAD_X3 and K >= self.X3_MIN_ROWS:
+            tiles = ((H + 127) // 128) * ((4 * H + 127) // 128)
+            splitk = self._sk(max(1, min(K // 256, (512 + tiles - 1) // tiles)))
+            with self._timed("rec_wgrad_x3", ("mfma", 12.0 * K * H * 4 * H, "bf16")):
+                ops.gemm_x3_tn(ws.h, ws.dG[1:], gK[C2:], H, 4 * H, K, H, 4 * H, 4 * H,
+                               splitk=splitk, reduce=False)
+        else:
+            self._dw(ws.h, ws.dG[1:], gK[C2:], K, H, 4 * H, H, 4 * H)
+
+    REC_WGRAD_X3 = os.environ.get("MOG_REC_WGRAD_X3", "1") == "1"
 
     def _weight_grads_lstm(self, X, ws, side=False, rec_done=False):
         """LSTM kernel / bias gradients.  Data parallel: the x-part X^T dGsum
@@ -1373,7 +1390,7 @@ class AIRModel:
         elif T > 1 and side and self.REC_WGRAD_SIDE:
             self._weight_grads_rec_side(ws)
         elif T > 1:
-            self._dw(ws.h, ws.dG[1:], gK[C2:], (T - 1) * B, H, 4 * H, H, 4 * H)
+            self._dw_rec(ws)
         chunk = self.X_GRAD_CHUNK if self.grad_reducer is not None else C2
         base = self.params.offsets[self._SCOPE_PREFIX + "rnn/basic_lstm_cell/kernel"]
         # bias gradient = colsum(sum_t dG_t) = colsum(dGsum), fused into chunk 0

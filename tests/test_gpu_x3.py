@@ -113,7 +113,8 @@ def test_x3_fp32_step_gradients_match_chain():
                      z_pres_prior_log_odds=-0.01, cnn=False, train=True, scope="x3",
                      device=DEV, precision="fp32", seed=3, noise_seed=4)
         m.X_GRAD_X3 = x3
-        m.VAE_WGRAD_X3 = m.VAE_DX_X3 = x3 != 0  # (the VAE gradients' x3 forms ride along)
+        # (the VAE gradients' and the recurrent rows' x3 forms ride along)
+        m.VAE_WGRAD_X3 = m.VAE_DX_X3 = m.REC_WGRAD_X3 = x3 != 0
         m.X3_DX_MIN_ROWS = 2048
         # one k pass per weight gradient: no split-K atomics, so each form is
         # reproducible and the forms differ by their products' summation only
