@@ -70,6 +70,18 @@ int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb, float* C, 
                     int M, int N, int K, int lda, int ldb, int ldc, int splitk, int npieces,
                     float* work, long work_elems, void* stream);
 
+/* Grouped fp32 weight gradients (mog-asr_amd/csrc/gemm_group.hip): for every
+ * problem p of `table` (HOST memory, 10 int64 per problem: A, B, C, colsum
+ * device pointers -- colsum may be 0 -- then M, N, K, lda, ldb, ldc),
+ * C_p[m][n] += sum_k A_p[k*lda+m] B_p[k*ldb+n] and colsum_p[n] += sum_k
+ * B_p[k*ldb+n], as one launch per 24 problems (the problems travel in the
+ * kernel argument: graph-capturable with no table upload).  One writer per
+ * output element (deterministic): no two problems may share an output.  The
+ * weight gradients of the small-batch train step (TF MatMul gradients of
+ * vae.py:18-46, the heads of air_model.py:458-520 and the LSTM kernel of
+ * :454-456, K = the batch rows). */
+int mog_gemm_f32_wgrad_group(const long long* table, int nprob, void* stream);
+
 /* dX = epi(dY W^T) at fp32-level accuracy on the bf16 matrix cores (the VAE
  * input gradients; replaces the MatMul gradients of vae.py:18-46's dense
  * layers w.r.t. their inputs): C[M][N] = sum_k A[m][k] B[n][k], A fp32 [M][lda]

@@ -942,6 +942,18 @@ void gemm_x3p_tn_(const Tensor& A3, int64_t sa, const Tensor& B3, int64_t sb, Te
         o.name);
 }
 
+// the problem table holds device pointers the caller validated
+// (mog_air.ops.WgradGroup checks every operand's extent before building it)
+void gemm_f32_wgrad_group_(at::IntArrayRef table, const Tensor& anchor) {
+  Op o("gemm_f32_wgrad_group_");
+  TORCH_CHECK(table.size() % 10 == 0, o.name, ": table of 10 int64 per problem");
+  o.need(anchor, F32, 0, "anchor");  // fixes the device (and stream) of the launch
+  GUARD(o);
+  check(mog_gemm_f32_wgrad_group(reinterpret_cast<const long long*>(table.data()),
+                                 (int)(table.size() / 10), o.stream()),
+        o.name);
+}
+
 void gemm_x3_nt_(const Tensor& A, const Tensor& B3, int64_t sb, Tensor C,
                  const optional<Tensor>& aux, int64_t M, int64_t N, int64_t K, int64_t lda,
                  int64_t ldb, int64_t ldc, int64_t ldaux, int64_t epi) {
@@ -958,6 +970,7 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
   m.def(
       "gemm_x3_nt_(Tensor A, Tensor B3, int sb, Tensor(a!) C, Tensor? aux, int M, int N, int K, "
       "int lda, int ldb, int ldc, int ldaux, int epi) -> ()");
+  m.def("gemm_f32_wgrad_group_(int[] table, Tensor anchor) -> ()");
   m.def(
       "split3_bf16_(Tensor src, Tensor(a!) dst, int rows, int cols, int ld_src, int ld_dst, "
       "int piece_stride) -> ()");
@@ -1107,6 +1120,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("split3_bf16_", &split3_bf16_);
   m.impl("gemm_x3_nt_", &gemm_x3_nt_);
   m.impl("gemm_x3p_tn_", &gemm_x3p_tn_);
+  m.impl("gemm_f32_wgrad_group_", &gemm_f32_wgrad_group_);
   m.impl("gemm_bf16_", &gemm_bf16_);
   m.impl("cvt_bf16_batch_", &cvt_bf16_batch_);
   m.impl("stn_forward_", &stn_forward_);

@@ -29,6 +29,7 @@ _SIGS = {
     "mog_gemm_f32_x3_tn": [P, P, P, P, I, I, I, I, I, I, I, P, L, P],
     "mog_split3_bf16": [P, I, I, I, P, I, L, P],
     "mog_gemm_x3p_tn": [P, L, P, L, P, P, I, I, I, I, I, I, I, I, P, L, P],
+    "mog_gemm_f32_wgrad_group": [P, I, P],
     "mog_gemm_x3_nt": [P, P, L, P, P, I, I, I, I, I, I, I, I, P],
     "mog_gemm_f32_sigmoid_philox": [P, P, P, P, I, I, I, I, I, I, F, ULL, ULL, P],
     "mog_stn_forward": [P, I, I, I, P, I, I, P, P, P, I, P],

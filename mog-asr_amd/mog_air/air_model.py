@@ -729,6 +729,37 @@ class AIRModel:
         st = self.params
         # the gradient buffer and the LSTM chain's dG sum, zeroed in one launch
         _ops.fill32_batch_([st.grad, ws.dGsum], [0, 0])
+        # small batch, one GPU: the fp32-chain weight gradients are collected
+        # and run as one grouped launch at the end (_wgrad_group_end)
+        self._wgroup = (self._wgroup_obj if (self.WGRAD_GROUP and B < self.SIDE_MIN_BATCH
+                                             and self.grad_reducer is None) else None)
+        try:
+            self._backward_body(X, ws)
+        finally:
+            wg, self._wgroup = self._wgroup, None
+        if wg is not None and wg.probs:
+            flops = sum(2.0 * p[4] * p[5] * p[6] for p in wg.probs)
+            with self._timed("wgrad_group", ("mfma", flops, "fp32")):
+                wg.launch()
+
+    # the grouped weight-gradient launch below SIDE_MIN_BATCH (batch 64: 11
+    # launches of a few k-steps each -> one)
+    WGRAD_GROUP = os.environ.get("MOG_WGRAD_GROUP", "1") == "1"
+    _wgroup = None
+
+    @property
+    def _wgroup_obj(self):
+        g = self.__dict__.get("_wgroup_obj_")
+        if g is None:
+            g = self.__dict__["_wgroup_obj_"] = ops.WgradGroup()
+        return g
+
+    def _backward_body(self, X: torch.Tensor, ws: _Workspace) -> None:
+        B, T, H = ws.B, self.max_steps, self.rnn_units
+        C, W, C2 = self.canvas_size, self.windows_size, self.C2
+        HS = self.scale_hidden_units
+        TB = T * B
+        st = self.params
         K = self._P("rnn/basic_lstm_cell/kernel")
         bK = self._P("rnn/basic_lstm_cell/bias")
         Wh = K[C2:]
@@ -1163,6 +1194,10 @@ class AIRModel:
         if not isinstance(out, (list, tuple)):
             X, dY, out = [X], [dY], [out]
             bias_out = None if bias_out is None else [bias_out]
+        if self._wgroup is not None:  # collected: one grouped launch ends the backward
+            for x, dy, o, b in zip(X, dY, out, bias_out or [None] * len(out)):
+                self._wgroup.add(x, dy, o, M, N, K, lda, ldb, N, b)
+            return
         tiles = ((M + 63) // 64) * ((N + 63) // 64) * len(out)
         target = int(os.environ.get("MOG_DW32_TARGET", "2048"))
         splitk = self._sk(max(1, min(K // 256, (target + tiles - 1) // tiles)))

@@ -91,6 +91,45 @@ def gemm_x3_nt(A: torch.Tensor, B3: torch.Tensor, sb: int, C: torch.Tensor, M: i
                      1 if aux is not None else 0)
 
 
+class WgradGroup:
+    """Weight gradients collected over a backward pass and run as ONE grouped
+    launch (mog_gemm_f32_wgrad_group): each problem is out[M,N] += X^T dY
+    over K rows (+ bias_out += column sums of dY); the problems travel in the
+    kernel argument (graph-capturable).  No two problems may share an output."""
+
+    def __init__(self):
+        self.probs = []
+
+    @staticmethod
+    def _check(t, extent, what):
+        if t.dtype != torch.float32 or not t.is_cuda:
+            raise RuntimeError(f"WgradGroup: {what} must be a float32 device tensor")
+        avail = t.untyped_storage().nbytes() // 4 - t.storage_offset()
+        if extent > avail:
+            raise RuntimeError(f"WgradGroup: {what} holds {avail} elements, needs {extent}")
+
+    def add(self, X, dY, out, M, N, K, lda, ldb, ldc, bias_out=None):
+        if min(M, N) <= 0:
+            return
+        span = lambda r, c, ld: 0 if r <= 0 else (r - 1) * ld + c  # noqa: E731
+        self._check(X, span(K, M, lda), "X")
+        self._check(dY, span(K, N, ldb), "dY")
+        self._check(out, span(M, N, ldc), "out")
+        if bias_out is not None:
+            self._check(bias_out, N, "bias_out")
+        self.probs.append((X, dY, out, bias_out, M, N, K, lda, ldb, ldc))
+
+    def launch(self):
+        if not self.probs:
+            return
+        table = []
+        for X, dY, out, b, M, N, K, lda, ldb, ldc in self.probs:
+            table += [X.data_ptr(), dY.data_ptr(), out.data_ptr(),
+                      0 if b is None else b.data_ptr(), M, N, K, lda, ldb, ldc]
+        _ops.gemm_f32_wgrad_group_(table, self.probs[0][2])
+        self.probs = []
+
+
 def gemm_sigmoid_philox(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias, M: int, N: int,
                         K: int, lda: int, ldb: int, ldc: int, scale: float, seed: int,
                         offset: int) -> None:
