@@ -444,6 +444,20 @@ class AIRModel(_AirBase):
             _ops.add_(ws.dz, ws.dz_carry, ws.dz, ws.B * self.vae_latent_dimensions)
 
     def _backward(self, X, ws):
+        # small batch, one GPU: the fp32-chain weight gradients as grouped
+        # launches at the end (as AIRModel._backward)
+        self._wgroup = (self._wgroup_obj if (self.WGRAD_GROUP and ws.B < self.SIDE_MIN_BATCH
+                                             and self.grad_reducer is None) else None)
+        try:
+            self._backward_body(X, ws)
+        finally:
+            wg, self._wgroup = self._wgroup, None
+        if wg is not None and wg.probs:
+            flops = sum(2.0 * p[4] * p[5] * p[6] for p in wg.probs)
+            with self._timed("wgrad_group", ("mfma", flops, "fp32")):
+                wg.launch()
+
+    def _backward_body(self, X, ws):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions
         C, W, C2 = self.canvas_size, self.windows_size, self.C2
         # the gradient buffer and the LSTM chains' accumulators in one launch

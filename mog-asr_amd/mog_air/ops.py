@@ -95,7 +95,8 @@ class WgradGroup:
     """Weight gradients collected over a backward pass and run as ONE grouped
     launch (mog_gemm_f32_wgrad_group): each problem is out[M,N] += X^T dY
     over K rows (+ bias_out += column sums of dY); the problems travel in the
-    kernel argument (graph-capturable).  No two problems may share an output."""
+    kernel argument (graph-capturable).  Problems that share output elements
+    go to successive launches (one writer per element within a launch)."""
 
     def __init__(self):
         self.probs = []
@@ -120,13 +121,27 @@ class WgradGroup:
         self.probs.append((X, dY, out, bias_out, M, N, K, lda, ldb, ldc))
 
     def launch(self):
-        if not self.probs:
-            return
-        table = []
+        """In collection order; a problem whose output or bias range overlaps
+        one already in the current launch starts the next launch (same
+        stream, so the two accumulate in order)."""
+        table, ranges = [], []
+
+        def flush():
+            if table:
+                _ops.gemm_f32_wgrad_group_(list(table), self.probs[0][2])
+            table.clear()
+            ranges.clear()
+
         for X, dY, out, b, M, N, K, lda, ldb, ldc in self.probs:
+            mine = [(out.data_ptr(), out.data_ptr() + 4 * ((M - 1) * ldc + N))]
+            if b is not None:
+                mine.append((b.data_ptr(), b.data_ptr() + 4 * N))
+            if any(lo < h and l2 < hi for lo, hi in mine for l2, h in ranges):
+                flush()
+            ranges.extend(mine)
             table += [X.data_ptr(), dY.data_ptr(), out.data_ptr(),
                       0 if b is None else b.data_ptr(), M, N, K, lda, ldb, ldc]
-        _ops.gemm_f32_wgrad_group_(table, self.probs[0][2])
+        flush()
         self.probs = []
 
 

@@ -89,3 +89,45 @@ def test_batch64_step_grouped_matches_per_gradient_launches():
         a, b = grads[0][k], grads[1][k]
         tol = 2e-5 if b.numel() > 64 else 2e-4
         assert (a - b).norm().item() <= tol * (b.norm().item() + 1e-30), k
+
+
+def test_wgrad_group_shared_outputs_accumulate_in_order():
+    """Two problems adding into the same output (and bias): they go to
+    successive launches, so both products land."""
+    g = torch.Generator().manual_seed(5)
+    A1, A2 = (torch.randn(100, 70, generator=g).to(DEV) for _ in range(2))
+    B1, B2 = (torch.randn(100, 40, generator=g).to(DEV) for _ in range(2))
+    C = torch.zeros(70, 40, device=DEV)
+    b = torch.zeros(40, device=DEV)
+    grp = ops.WgradGroup()
+    grp.add(A1, B1, C, 70, 40, 100, 70, 40, 40, b)
+    grp.add(A2, B2, C[10:], 60, 40, 100, 70, 40, 40, b)  # rows 10.. of the same output
+    grp.launch()
+    torch.cuda.synchronize()
+    ref = A1.cpu().double().T @ B1.cpu().double()
+    ref[10:] += A2.cpu().double()[:, :60].T @ B2.cpu().double()
+    scale = A1.cpu().double().abs().T @ B1.cpu().double().abs()
+    scale[10:] += A2.cpu().double()[:, :60].abs().T @ B2.cpu().double().abs()
+    assert _err(C.cpu(), ref, scale) <= 1e-6
+    bref = B1.cpu().double().sum(0) + B2.cpu().double().sum(0)
+    assert _err(b.cpu(), bref, B1.cpu().double().abs().sum(0) + B2.cpu().double().abs().sum(0)) <= 1e-6
+
+
+def test_asr_batch64_step_grouped_matches_per_gradient_launches():
+    """AIR-ASR (configs[2]) at the reference's batch of 64: grouped against
+    one launch per gradient, every gradient to fp32 level."""
+    import bench
+    rng = np.random.default_rng(10)
+    x = (rng.uniform(size=(64, 2500)) * (rng.uniform(size=(64, 2500)) < 0.3)).astype(np.float32)
+    X = torch.as_tensor(x).to(DEV)
+    grads = []
+    for grouped in (True, False):
+        m = bench.make_asr_model("fp32", torch.device(DEV), "wgasr%d" % grouped)
+        m.WGRAD_GROUP = grouped
+        m.ONE_PASS_WGRADS = True
+        grads.append({k: torch.as_tensor(np.asarray(v), dtype=torch.float64)
+                      for k, v in m.compute_gradients(X).items()})
+    for k in grads[0]:
+        a, b = grads[0][k], grads[1][k]
+        tol = 2e-5 if b.numel() > 64 else 2e-4
+        assert (a - b).norm().item() <= tol * (b.norm().item() + 1e-30), k
