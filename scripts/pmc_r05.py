@@ -19,10 +19,14 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
-# bench tag -> (workload, symbol predicate, which dispatches: "all" | "even" | "odd" | "last5")
+# bench tag -> (workload, symbol predicate, which dispatches: "all" | "even" | "odd" | "last5"
+# | "5not4" / "5is4": all but / only every fifth, from the fifth)
 TAGS = {
     "stn_vae_step_f32_all_fp32_b8192": ("step_fp32_8192", lambda k: "stn_vae_step_f32_kernel" in k, "all"),
-    "vae_wgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_x3_tn_kernel<false, 3>" in k, "all"),
+    # gemm_x3_tn_kernel<false,3> runs the four VAE weight gradients, then (launched
+    # later in the step) the LSTM recurrent rows: five per step in that order
+    "vae_wgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_x3_tn_kernel<false, 3>" in k, "5not4"),
+    "rec_wgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_x3_tn_kernel<false, 3>" in k, "5is4"),
     "vae_dgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_x3_nt_kernel" in k, "all"),
     "lstm_x_projection_grad_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_x3_tn_kernel<true, 3>" in k, "all"),
     "lstm_x_projection_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_f32_dma_kernel<128, 128, 16, 3, false, false, 0>" in k, "all"),
@@ -79,6 +83,10 @@ def pick(v, which):
         return v[1::2]
     if which == "last5":
         return v[-5:]
+    if which == "5not4":
+        return [x for i, x in enumerate(v) if i % 5 != 4]
+    if which == "5is4":
+        return v[4::5]
     return v
 
 
