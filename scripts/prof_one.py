@@ -6,6 +6,7 @@ be mixed with others' (kernel trace, --pmc FETCH_SIZE / WRITE_SIZE):
   step_fp32 [B]       the headline fp32 train step (bench defaults), 3 steps after 2
   step_bf16 [B]       configs[1]'s bf16 train step, 3 steps after 2
   fused_f32 [B]       the fp32 fused step over B rows (bench.fp32_step_roofline)
+  asr_fp32 / asr_bf16 [B]  configs[2]'s AIR-ASR train step, 3 steps after 2
 
 usage: python scripts/prof_one.py <workload> [B] [C]"""
 import os
@@ -30,6 +31,12 @@ def main():
         B = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
         prec = w.split("_")[1]
         el, m = bench.timed_train(prec, B, 3, 2, dev, scope="prof_" + prec)
+        print(f"{w} B={B}: {el / 3 * 1e3:.3f} ms per step")
+    elif w in ("asr_fp32", "asr_bf16"):
+        B = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
+        prec = w.split("_")[1]
+        m = bench.make_asr_model(prec, dev, "prof_asr_" + prec)
+        el, m = bench.timed_train(prec, B, 3, 2, dev, model=m)
         print(f"{w} B={B}: {el / 3 * 1e3:.3f} ms per step")
     elif w == "fused_f32":
         B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536

@@ -175,7 +175,7 @@ def test_x3_asr_step_gradients_match_chain():
     for x3 in (2, 0):
         m = bench.make_asr_model("fp32", torch.device(DEV), "x3asr%d" % x3)
         m.X_GRAD_X3 = x3
-        m.VAE_DX_X3 = x3 != 0
+        m.VAE_DX_X3 = m.REC_WGRAD_X3 = x3 != 0
         m.X3_DX_MIN_ROWS = 1024
         assert m._x3_asr(B) == (x3 == 2)
         grads.append({k: torch.as_tensor(np.asarray(v), dtype=torch.float64)
