@@ -1394,13 +1394,14 @@ class AIRModel:
 
     def _dw_rec(self, ws):
         """The LSTM kernel's recurrent rows: gK[C2:] += sum_t h[t-1]^T dG[t]
-        over (T-1) B rows.  fp32 from X3_MIN_ROWS: on the bf16 matrix cores
-        with exact three-piece splits (gemm_x3_tn, as the VAE weight
-        gradients; 256 x 1024 x 16,384 at B = 8192), else the fp32 split-K GEMM."""
+        over (T-1) B rows.  From X3_MIN_ROWS (either precision: fp32-level, and
+        faster than the fp32 chain): on the bf16 matrix cores with exact
+        three-piece splits (gemm_x3_tn, as the fp32 VAE weight gradients;
+        256 x 1024 x 16,384 at B = 8192), else the fp32 split-K GEMM."""
         B, T, H, C2 = ws.B, self.max_steps, self.rnn_units, self.C2
         gK = self._G("rnn/basic_lstm_cell/kernel")
         K = (T - 1) * B
-        if self.precision == "fp32" and self.REC_WGRAD_X3 and K >= self.X3_MIN_ROWS:
+        if self.REC_WGRAD_X3 and K >= self.X3_MIN_ROWS:
             tiles = ((H + 127) // 128) * ((4 * H + 127) // 128)
             splitk = self._sk(max(1, min(K // 256, (512 + tiles - 1) // tiles)))
             with self._timed("rec_wgrad_x3", ("mfma", 12.0 * K * H * 4 * H, "bf16")):

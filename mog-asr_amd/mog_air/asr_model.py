@@ -545,7 +545,7 @@ class AIRModel(_AirBase):
         v = (lambda x: x[t]) if t is not None else (lambda x: x)  # noqa: E731
         gKi = self._Kpad("infer_rnn_running/kernel", "grad")
         gKg = self._Kpad("gen_rnn_running/kernel", "grad")
-        if self.precision == "fp32" and self.REC_WGRAD_X3 and K >= self.X3_MIN_ROWS:
+        if self.REC_WGRAD_X3 and K >= self.X3_MIN_ROWS:
             # on the bf16 matrix cores with exact three-piece splits (as AIR's
             # recurrent rows, AIRModel._dw_rec): 312 x 1024 x K per cell
             tiles = ((LU + 127) // 128) * ((4 * H + 127) // 128)
