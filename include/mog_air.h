@@ -70,6 +70,12 @@ int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb, float* C, 
                     int M, int N, int K, int lda, int ldb, int ldc, int splitk, int npieces,
                     float* work, long work_elems, void* stream);
 
+/* Build provenance: copies the library's source hash (16 hex digits: sha256
+ * of csrc/*.hip, csrc/*.h, include/*.h in sorted order) and a NUL into out
+ * (cap >= 17).  The Python host refuses a library whose hash differs from
+ * the sources beside it (mog_air/_lib.py). */
+int mog_build_id(char* out, int cap);
+
 /* Grouped fp32 weight gradients (mog-asr_amd/csrc/gemm_group.hip): for every
  * problem p of `table` (HOST memory, 10 int64 per problem: A, B, C, colsum
  * device pointers -- colsum may be 0 -- then M, N, K, lda, ldb, ldc),

@@ -30,6 +30,7 @@ _SIGS = {
     "mog_split3_bf16": [P, I, I, I, P, I, L, P],
     "mog_gemm_x3p_tn": [P, L, P, L, P, P, I, I, I, I, I, I, I, I, P, L, P],
     "mog_gemm_f32_wgrad_group": [P, I, P],
+    "mog_build_id": [P, I],
     "mog_gemm_x3_nt": [P, P, L, P, P, I, I, I, I, I, I, I, I, P],
     "mog_gemm_f32_sigmoid_philox": [P, P, P, P, I, I, I, I, I, I, F, ULL, ULL, P],
     "mog_stn_forward": [P, I, I, I, P, I, I, P, P, P, I, P],
@@ -106,8 +107,39 @@ def load():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = I
+    built, src = library_build_id(lib), source_build_id()
+    if src is not None and built != src:
+        raise MogError(f"{LIB_PATH} was built from other sources (library {built}, sources "
+                       f"{src}); rebuild it with `make -C mog-asr_amd`")
     _lib = lib
     return lib
+
+
+def library_build_id(lib=None) -> str:
+    """The source hash compiled into libmog_air.so (mog_build_id)."""
+    buf = ctypes.create_string_buffer(32)
+    if (lib or load()).mog_build_id(buf, 32) != 0:
+        raise MogError("mog_build_id failed")
+    return buf.value.decode()
+
+
+def source_build_id():
+    """The Makefile's hash of the sources beside the library (None when they
+    are not there)."""
+    import glob
+    import hashlib
+    pkg = os.path.dirname(_HERE)
+    csrc, inc = os.path.join(pkg, "csrc"), os.path.join(os.path.dirname(pkg), "include")
+    files = (sorted(glob.glob(os.path.join(csrc, "*.hip"))) +
+             sorted(glob.glob(os.path.join(csrc, "*.h"))) +
+             sorted(glob.glob(os.path.join(inc, "*.h"))))
+    if not files:
+        return None
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def call(name: str, *args) -> None:

@@ -26,6 +26,15 @@ def test_library_exports_every_header_symbol():
     assert set(syms) == set(_lib._SIGS)
 
 
+def test_library_built_from_these_sources():
+    """Build provenance: the source hash compiled into libmog_air.so
+    (mog_build_id) equals the hash of the sources beside it, which
+    _lib.load() checks before any launch (a stale library refuses to load)."""
+    from mog_air import _lib
+    built = _lib.library_build_id()
+    assert len(built) == 16 and built == _lib.source_build_id()
+
+
 def test_all_headers_symbols_exported():
     from mog_air import _lib
     lib = ctypes.CDLL(_lib.LIB_PATH)
