@@ -58,7 +58,11 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 128, BN = 128, BK = 32;
-constexpr int LDR = BM + 8;                 // LDS row (k) pitch in bf16 (BM == BN)
+constexpr int LDR = BM;                     // LDS row (k) pitch in bf16 (BM == BN), unpadded:
+// the 8-byte units (4 bf16) of k-row r sit at unit u ^ tsw(r), so the 16 rows x
+// 32 B that one ds_read_b64_tr_b16 touches (rows 8g + tq [+ 4], four units per
+// row) cover the 64 banks once (a padded pitch of 136 left them 2-way
+// conflicted: SQ_LDS_BANK_CONFLICT a third of the LDS cycles)
 constexpr int PIECE = BK * LDR;             // one bf16 image
 constexpr int STAGE = 6 * PIECE;            // A0 A1 A2 B0 B1 B2
 constexpr int NL = (BM * BK / 4) / 256;     // float4 loads per thread per operand (4)
@@ -68,6 +72,10 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
+
+__device__ __forceinline__ int tsw(int r) { return ((r & 3) << 2) | (((r >> 3) & 1) << 4); }
+// bf16 offset of (k-row r, column c), c a multiple of 4, in a TN operand image
+__device__ __forceinline__ int tpos(int r, int c) { return r * LDR + (((c >> 2) ^ tsw(r)) << 2); }
 
 // the three truncated bf16 pieces of one float (as fp32 bit patterns whose low
 // halves are zero, except lo's, which the packing drops)
@@ -231,7 +239,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
     if constexpr (PRE) {
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
-        const int o = (pk + 16 * i) * LDR + pc;
+        const int o = tpos(pk + 16 * i, pc);
 #pragma unroll
         for (int p = 0; p < NPC; ++p) {
           *reinterpret_cast<u32x4*>(S + p * PIECE + o) = pa[p][i];
@@ -255,7 +263,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
     }
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-      const int o = (sk + 8 * i) * LDR + sc;
+      const int o = tpos(sk + 8 * i, sc);
       u32x2 p0, p1, p2;
       split4(f4(ra[i]), p0, p1, p2);
       *reinterpret_cast<u32x2*>(S + 0 * PIECE + o) = p0;
@@ -278,7 +286,8 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
   const int g = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;  // transpose-read roles (gemm_bf16.hip TN form)
   auto frag = [&](const __bf16* P, int col) -> bf16x8 {
-    const __bf16* p0 = P + (8 * g + tq) * LDR + col + 4 * tp;
+    // (tsw(r + 4) == tsw(r) for r = 8g + tq: the hi rows keep the lo rows' units)
+    const __bf16* p0 = P + tpos(8 * g + tq, col + 4 * tp);
     const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
     const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p0 + 4 * LDR));
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);

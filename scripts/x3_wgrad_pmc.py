@@ -1,0 +1,31 @@
+"""One x3 VAE weight-gradient shape (gemm_x3_tn_kernel<false,3>, the fp32 step's
+784 x 512 x 24,576 with its split-K 19) launched 10 times, for rocprofv3 --pmc
+passes (scripts/gpu_x3_pmc.sh); prints the event-timed launch."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mog-asr_amd")]
+import torch  # noqa: E402
+
+from mog_air import ops  # noqa: E402
+
+M, N, K = int(os.environ.get("M", 784)), int(os.environ.get("N", 512)), 24576
+dev = "cuda:0"
+g = torch.Generator(device=dev).manual_seed(0)
+A = torch.rand(K, M, device=dev, generator=g)
+B = torch.randn(K, N, device=dev, generator=g) * 1e-3
+C = torch.zeros(M, N, device=dev)
+cs = torch.zeros(N, device=dev)
+tiles = ((M + 127) // 128) * ((N + 127) // 128)
+sk = max(1, min(K // 256, (512 + tiles - 1) // tiles))
+for _ in range(3):
+    ops.gemm_x3_tn(A, B, C, M, N, K, M, N, N, splitk=sk, colsum=cs, reduce=False)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(10):
+    ops.gemm_x3_tn(A, B, C, M, N, K, M, N, N, splitk=sk, colsum=cs, reduce=False)
+e1.record()
+torch.cuda.synchronize()
+print(f"x3 tn {M}x{N}x{K} splitk {sk}: {e0.elapsed_time(e1) / 10 * 1e3:.1f} us", flush=True)
