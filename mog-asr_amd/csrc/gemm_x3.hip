@@ -294,15 +294,6 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
   };
   auto compute = [&](int stage) {
     const __bf16* S = lds + stage * STAGE;
-    bf16x8 a[NPC][4], b[NPC][4];
-#pragma unroll
-    for (int p = 0; p < NPC; ++p)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[p][i] = frag(S + p * PIECE, wm + 16 * i);
-        b[p][i] = frag(S + (3 + p) * PIECE, wn + 16 * i);
-      }
-    // smallest terms first: (2,0) (1,1) (0,2), (1,0) (0,1), (0,0)
     auto pass = [&](const bf16x8 (&x)[4], const bf16x8 (&y)[4]) {
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
@@ -311,14 +302,22 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
           acc[mi][ni] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[mi], y[ni], acc[mi][ni], 0, 0, 0);
     };
-    if constexpr (NPC == 3) {
-      pass(a[2], b[0]);
-      pass(a[1], b[1]);
-      pass(a[0], b[2]);
-      pass(a[1], b[0]);
-      pass(a[0], b[1]);
+    // the B pieces held for the k-tile, the A pieces one at a time (smallest
+    // terms first: a2 b0; a1 b1, a1 b0; a0 b2, a0 b1, a0 b0): 64 fragment
+    // registers live instead of 96
+    bf16x8 b[NPC][4];
+#pragma unroll
+    for (int p = 0; p < NPC; ++p)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b[p][i] = frag(S + (3 + p) * PIECE, wn + 16 * i);
+#pragma unroll
+    for (int pa = NPC - 1; pa >= 0; --pa) {
+      bf16x8 a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = frag(S + pa * PIECE, wm + 16 * i);
+#pragma unroll
+      for (int pb = NPC - 1 - pa; pb >= 0; --pb) pass(a, b[pb]);
     }
-    pass(a[0], b[0]);
   };
 
   const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
