@@ -444,9 +444,11 @@ void splitk_reduce(const X3Args& D, hipStream_t s) {
 // consecutive columns), then store or softplus backward (C = v * sigmoid(aux),
 // gemm_f32.hip's EPI_SOFTPLUS_BWD), 16-byte stores.  No split-K: the sums
 // over K (<= 784) stay inside one workgroup, so the result is deterministic.
-constexpr int NT_LDK = BK + 8;                 // LDS row pitch (bf16): 80 B, conflict-free b128
+constexpr int NT_LDK = BK + 16;  // LDS row pitch (bf16): 96 B -- the fragment reads (ds_read_b128,
+                                 // lane groups of MI355X_MICROARCH §LDS) hit distinct banks; 80 B
+                                 // left them 2-way conflicted (half the LDS cycles, SQ_LDS_BANK_CONFLICT)
 constexpr int NT_PIECE = BM * NT_LDK;
-constexpr int NT_STAGE = 6 * NT_PIECE;         // A0 A1 A2 B0 B1 B2 (61,440 B)
+constexpr int NT_STAGE = 6 * NT_PIECE;         // A0 A1 A2 B0 B1 B2 (73,728 B)
 constexpr int NT_NLA = (BM * BK / 4) / 256;    // float4 loads of A per thread (4)
 constexpr int NT_NLB = (BN * BK / 8) / 256;    // 16-byte chunks of a B piece per thread (2)
 

@@ -20,7 +20,7 @@ import csv, glob, collections
 acc = collections.defaultdict(list)
 for f in glob.glob("gpurun_out/x3pmc/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "gemm_x3_tn_kernel" in r["Kernel_Name"]:
+        if "gemm_x3_" in r["Kernel_Name"]:
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in sorted(acc.items()):
     print(f"{k:28s} {sum(v) / len(v):.4g}  (n={len(v)})")
