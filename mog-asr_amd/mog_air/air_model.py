@@ -1003,7 +1003,8 @@ class AIRModel:
         B = ws.B
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
-        _ops.sigmoid_backward_(ws.r[t], ws.dr, ws.dm[t], B * W2)
+        if not getattr(ws, "dm_ready", False):  # (AIR-ASR: dm came from the batched write backward)
+            _ops.sigmoid_backward_(ws.r[t], ws.dr, ws.dm[t], B * W2)
         self._dx(ws.dm[t], "gen_mean", ws.dd2[t], B, G2, W2, aux=ws.d2[t])
         self._dx(ws.dd2[t], "generative_2", ws.dd1[t], B, G1, G2, aux=ws.d1[t])
         gemm([ws.dd1[t]], [vw["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z, transB=True)
@@ -1126,7 +1127,8 @@ class AIRModel:
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         Zp = self._pad8(Z)
         wn = self._wn
-        _ops.sigmoid_backward_(ws.r[t], ws.dr, ws.dmb[t], B * W2)
+        if not getattr(ws, "dm_ready", False):  # (AIR-ASR: dm came from the batched write backward)
+            _ops.sigmoid_backward_(ws.r[t], ws.dr, ws.dmb[t], B * W2)
         gemm_bf16([ws.dmb[t]], [wn["gen_mean"]], [ws.dd2b[t]], B, G2, W2, W2, W2, G2,
                   epi=BF_SOFTPLUS_BWD, aux=[ws.d2b[t]], ldaux=G2)
         gemm_bf16([ws.dd2b[t]], [wn["generative_2"]], [ws.dd1b[t]], B, G1, G2, G2, G2, G1,

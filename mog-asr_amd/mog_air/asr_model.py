@@ -452,6 +452,7 @@ class AIRModel(_AirBase):
             self._backward_body(X, ws)
         finally:
             wg, self._wgroup = self._wgroup, None
+            ws.dm_ready = False
         if wg is not None and wg.probs:
             flops = sum(2.0 * p[4] * p[5] * p[6] for p in wg.probs)
             with self._timed("wgrad_group", ("mfma", flops, "fp32")):
@@ -479,9 +480,22 @@ class AIRModel(_AirBase):
         side = self._side_stream() if steps_side else None
         ws.vae_wgrads_done = steps_side
         ws.u_wgrads_done = steps_side and self.U_WGRAD_PER_STEP
+        # every step's STN write backward in ONE launch over T*B rows, before
+        # the loop (it reads only the forward's records and the canvas
+        # gradient, shared by the steps; AIRModel._backward does the same),
+        # the glimpse gradient taken through the output sigmoid (dm, bit-identical
+        # to dU + mog_sigmoid_backward): six launches of B rows -> one
+        TB = T * B
+        if self.precision == "bf16":
+            ops.stn_backward(ws.r.view(TB, -1), ws.th_b, (C, C), ws.dcanvas, gscale=ws.zc,
+                             dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True, n=TB,
+                             dm_bf16=ws.dmb.view(TB, -1))
+        else:
+            ops.stn_backward(ws.r.view(TB, -1), ws.th_b, (C, C), ws.dcanvas, gscale=ws.zc,
+                             dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True, n=TB,
+                             dm=ws.dm.view(TB, -1))
+        ws.dm_ready = True
         for t in reversed(range(T)):
-            ops.stn_backward(ws.r[t], ws.th_b[t], (C, C), ws.dcanvas, gscale=ws.zc[t],
-                             dU=ws.dr, dtheta=ws.dth_b, dot=ws.dot, want_dot=True)
             if self.precision == "bf16":
                 self._vae_backward_bf16(ws, t, gscale)
             else:
@@ -503,7 +517,7 @@ class AIRModel(_AirBase):
                                     float(self.scale_prior_variance), float(gscale), w20,
                                     [x if (k != 5 or fix < 0) else None for k, x in enumerate(hid)],
                                     ws.arec[t], ws.eps_shift[t], ws.eps_scale[t], ws.dth_f,
-                                    ws.dth_b, ws.dot, ws.dreg[t],
+                                    ws.dth_b_all[t], ws.dot_all[t], ws.dreg[t],
                                     ws.dss_carry if t < T - 1 else None, ws.douts[t],
                                     [x if (k != 5 or fix < 0) else None
                                      for k, x in enumerate(dpre)])
@@ -532,6 +546,7 @@ class AIRModel(_AirBase):
                      4 * H, 4 * H, LU, transB=True)
                 _ops.asr_unpack_(B, Z, H, LU, ws.dU, ws.dUg, ws.dz_carry, ws.dss_carry,
                                  ws.dh[t - 1], ws.dhg[t - 1])
+        ws.dm_ready = False
         self._weight_grads(X, ws)
         if steps_side:
             torch.cuda.current_stream().wait_stream(side)
