@@ -994,24 +994,56 @@ class AIRModel:
                                  ws.mu[t], ws.lv[t], ws.eps_z[t], ws.z[t], zb, ldzb,
                                  ws.zmask[t], ws.runloss, ws.vkl[t])
 
-    def _dz_hook(self, ws, t):
-        """Extra gradient reaching the latent z of step t before the sample
-        backward (none in AIR; the ASR model adds the next step's LSTM-input
-        gradient here)."""
+    def _dz_hook(self, ws, t, dz):
+        """Extra gradient reaching the latent z of step t (in dz) before the
+        sample backward (none in AIR; the ASR model adds the next step's
+        LSTM-input gradient here)."""
+
+    def _vae_decoder_backward_all(self, ws):
+        """The decoder half of every loop step's VAE backward over all T*B
+        rows (dm -> dd2 -> dd1 -> dz_all; dm already through the output
+        sigmoid), for a loop that needs only the encoder half per step: the
+        AIR-ASR reversed loop, whose dz_t takes the next step's carry (the
+        same chains as the per-step launches, so the same values)."""
+        T, B = self.max_steps, ws.B
+        TB = T * B
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        if getattr(ws, "dz_all", None) is None:
+            ws.dz_all = torch.empty((T, B, Z), device=self.device)
+        v = lambda x: x.view(TB, -1)  # noqa: E731
+        if self.precision == "bf16":
+            from .ops import BF_SOFTPLUS_BWD, BF_STORE, gemm_bf16
+            wn = self._wn
+            gemm_bf16([v(ws.dmb)], [wn["gen_mean"]], [v(ws.dd2b)], TB, G2, W2, W2, W2, G2,
+                      epi=BF_SOFTPLUS_BWD, aux=[v(ws.d2b)], ldaux=G2)
+            gemm_bf16([v(ws.dd2b)], [wn["generative_2"]], [v(ws.dd1b)], TB, G1, G2, G2, G2, G1,
+                      epi=BF_SOFTPLUS_BWD, aux=[v(ws.d1b)], ldaux=G1)
+            gemm_bf16([v(ws.dd1b)], [wn["generative_1"]], [v(ws.dz_all)], TB, Z, G1, G1, G1, Z,
+                      epi=BF_STORE)
+        else:
+            self._dx(v(ws.dm), "gen_mean", v(ws.dd2), TB, G2, W2, aux=v(ws.d2))
+            self._dx(v(ws.dd2), "generative_2", v(ws.dd1), TB, G1, G2, aux=v(ws.d1))
+            gemm([v(ws.dd1)], [self._P("vae/generative_1/weights")], [v(ws.dz_all)], TB, Z, G1, G1,
+                 G1, Z, transB=True)
+        ws.dec_ready = True
 
     def _vae_backward_fp32(self, ws, t, gscale):
         B = ws.B
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
-        if not getattr(ws, "dm_ready", False):  # (AIR-ASR: dm came from the batched write backward)
-            _ops.sigmoid_backward_(ws.r[t], ws.dr, ws.dm[t], B * W2)
-        self._dx(ws.dm[t], "gen_mean", ws.dd2[t], B, G2, W2, aux=ws.d2[t])
-        self._dx(ws.dd2[t], "generative_2", ws.dd1[t], B, G1, G2, aux=ws.d1[t])
-        gemm([ws.dd1[t]], [vw["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z, transB=True)
-        self._dz_hook(ws, t)
+        if getattr(ws, "dec_ready", False):  # (the decoder half ran over T*B rows)
+            dz = ws.dz_all[t]
+        else:
+            dz = ws.dz
+            if not getattr(ws, "dm_ready", False):
+                _ops.sigmoid_backward_(ws.r[t], ws.dr, ws.dm[t], B * W2)
+            self._dx(ws.dm[t], "gen_mean", ws.dd2[t], B, G2, W2, aux=ws.d2[t])
+            self._dx(ws.dd2[t], "generative_2", ws.dd1[t], B, G1, G2, aux=ws.d1[t])
+            gemm([ws.dd1[t]], [vw["generative_1"]], [dz], B, Z, G1, G1, G1, Z, transB=True)
+        self._dz_hook(ws, t, dz)
         _ops.vae_sample_backward_(B, Z, float(self.vae_prior_mean),
                                   float(self.vae_prior_variance), float(gscale), ws.mu[t],
-                                  ws.lv[t], ws.eps_z[t], ws.dz, ws.zmask[t], ws.dmu[t], ws.dlv[t],
+                                  ws.lv[t], ws.eps_z[t], dz, ws.zmask[t], ws.dmu[t], ws.dlv[t],
                                   None, None, 0)
         gemm([ws.dmu[t]], [vw["rec_mean"]], [ws.tmp_a2], B, R2, Z, Z, Z, R2, transB=True)
         gemm([ws.dlv[t]], [vw["rec_log_variance"]], [ws.da2[t]], B, R2, Z, Z, Z, R2,
@@ -1127,18 +1159,22 @@ class AIRModel:
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         Zp = self._pad8(Z)
         wn = self._wn
-        if not getattr(ws, "dm_ready", False):  # (AIR-ASR: dm came from the batched write backward)
-            _ops.sigmoid_backward_(ws.r[t], ws.dr, ws.dmb[t], B * W2)
-        gemm_bf16([ws.dmb[t]], [wn["gen_mean"]], [ws.dd2b[t]], B, G2, W2, W2, W2, G2,
-                  epi=BF_SOFTPLUS_BWD, aux=[ws.d2b[t]], ldaux=G2)
-        gemm_bf16([ws.dd2b[t]], [wn["generative_2"]], [ws.dd1b[t]], B, G1, G2, G2, G2, G1,
-                  epi=BF_SOFTPLUS_BWD, aux=[ws.d1b[t]], ldaux=G1)
-        gemm_bf16([ws.dd1b[t]], [wn["generative_1"]], [ws.dz], B, Z, G1, G1, G1, Z,
-                  epi=BF_STORE)
-        self._dz_hook(ws, t)
+        if getattr(ws, "dec_ready", False):  # (the decoder half ran over T*B rows)
+            dz = ws.dz_all[t]
+        else:
+            dz = ws.dz
+            if not getattr(ws, "dm_ready", False):
+                _ops.sigmoid_backward_(ws.r[t], ws.dr, ws.dmb[t], B * W2)
+            gemm_bf16([ws.dmb[t]], [wn["gen_mean"]], [ws.dd2b[t]], B, G2, W2, W2, W2, G2,
+                      epi=BF_SOFTPLUS_BWD, aux=[ws.d2b[t]], ldaux=G2)
+            gemm_bf16([ws.dd2b[t]], [wn["generative_2"]], [ws.dd1b[t]], B, G1, G2, G2, G2, G1,
+                      epi=BF_SOFTPLUS_BWD, aux=[ws.d1b[t]], ldaux=G1)
+            gemm_bf16([ws.dd1b[t]], [wn["generative_1"]], [dz], B, Z, G1, G1, G1, Z,
+                      epi=BF_STORE)
+        self._dz_hook(ws, t, dz)
         _ops.vae_sample_backward_(B, Z, float(self.vae_prior_mean),
                                   float(self.vae_prior_variance), float(gscale), ws.mu[t],
-                                  ws.lv[t], ws.eps_z[t], ws.dz, ws.zmask[t], None, None,
+                                  ws.lv[t], ws.eps_z[t], dz, ws.zmask[t], None, None,
                                   ws.dmub[t], ws.dlvb[t], Zp)
         gemm_bf16([ws.dmub[t]], [wn["rec_mean"]], [ws.tmp_a2], B, R2, Zp, Zp, Zp, R2,
                   epi=BF_STORE)

@@ -439,9 +439,9 @@ class AIRModel(_AirBase):
         self._outputs_ready = True
 
     # --------------------------------------------------------- backward ---
-    def _dz_hook(self, ws, t):
+    def _dz_hook(self, ws, t, dz):
         if t < self.max_steps - 1:
-            _ops.add_(ws.dz, ws.dz_carry, ws.dz, ws.B * self.vae_latent_dimensions)
+            _ops.add_(dz, ws.dz_carry, dz, ws.B * self.vae_latent_dimensions)
 
     def _backward(self, X, ws):
         # small batch, one GPU: the fp32-chain weight gradients as grouped
@@ -452,7 +452,7 @@ class AIRModel(_AirBase):
             self._backward_body(X, ws)
         finally:
             wg, self._wgroup = self._wgroup, None
-            ws.dm_ready = False
+            ws.dm_ready = ws.dec_ready = False
         if wg is not None and wg.probs:
             flops = sum(2.0 * p[4] * p[5] * p[6] for p in wg.probs)
             with self._timed("wgrad_group", ("mfma", flops, "fp32")):
@@ -495,6 +495,9 @@ class AIRModel(_AirBase):
                              dtheta=ws.dth_b_all, dot=ws.dot_all, want_dot=True, n=TB,
                              dm=ws.dm.view(TB, -1))
         ws.dm_ready = True
+        # and the decoder half of every step's VAE backward (dz_t before the
+        # loop's carry), likewise over T*B rows
+        self._vae_decoder_backward_all(ws)
         for t in reversed(range(T)):
             if self.precision == "bf16":
                 self._vae_backward_bf16(ws, t, gscale)
@@ -546,7 +549,7 @@ class AIRModel(_AirBase):
                      4 * H, 4 * H, LU, transB=True)
                 _ops.asr_unpack_(B, Z, H, LU, ws.dU, ws.dUg, ws.dz_carry, ws.dss_carry,
                                  ws.dh[t - 1], ws.dhg[t - 1])
-        ws.dm_ready = False
+        ws.dm_ready = ws.dec_ready = False
         self._weight_grads(X, ws)
         if steps_side:
             torch.cuda.current_stream().wait_stream(side)
