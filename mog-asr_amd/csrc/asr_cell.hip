@@ -151,6 +151,16 @@ __global__ __launch_bounds__(256) void asr_step_fwd_kernel(AsrCfg cfg, AsrW W, A
   const int B = cfg.B;
   const bool ok = b < B;
   const int bc = ok ? b : 0;
+  // the later phases' global operands loaded up front, unconditionally (one
+  // memory latency for all of them instead of one per phase behind the
+  // barriers; clamped image index, as the chains below)
+  const size_t r6 = (size_t)bc * HS + q;
+  const float es0 = io.eps_shift[(size_t)bc * 2], es1 = io.eps_shift[(size_t)bc * 2 + 1];
+  const float h6 = hp.h[6][r6], h7 = hp.h[7][r6];
+  const float w6a = W.w[W_IC0][256 * HS + q], w6b = W.w[W_IC0][257 * HS + q], b6 = W.w[B_IC0][q];
+  const float w7a = W.w[W_IC2][256 * HS + q], w7b = W.w[W_IC2][257 * HS + q], b7 = W.w[B_IC2][q];
+  const float e_s = io.eps_scale[bc], uu = io.u[bc], stop_old = io.stop[bc];
+  const int live = io.live[cfg.step], dig = io.digits[bc];
   // phase 1: ten output-layer chains over the 64 hidden units
   if (q < 10) {
     float v = 0.0f;
@@ -176,22 +186,21 @@ __global__ __launch_bounds__(256) void asr_step_fwd_kernel(AsrCfg cfg, AsrW W, A
   if (q == 0) {
     for (int d = 0; d < 2; ++d) {
       const float svar = mog_expf(sv[m][2 + d]);
-      sv[m][10 + d] = sv[m][d] + io.eps_shift[(size_t)bc * 2 + d] * sqrtf(svar);
+      sv[m][10 + d] = sv[m][d] + (d == 0 ? es0 : es1) * sqrtf(svar);
     }
   }
   __syncthreads();
   // phase 3: inf_scale hidden layers on concat([h, shift_latent]) (:429-447):
   // the GEMM left the chain over h; add the two latent terms, bias, relu
   const float sl0 = sv[m][10], sl1 = sv[m][11];
-  const size_t r6 = (size_t)bc * HS + q;
   {
-    float a6 = hp.h[6][r6], a7 = hp.h[7][r6];
-    a6 = fmaf(sl0, W.w[W_IC0][256 * HS + q], a6);
-    a6 = fmaf(sl1, W.w[W_IC0][257 * HS + q], a6);
-    a6 = a6 + W.w[B_IC0][q];
-    a7 = fmaf(sl0, W.w[W_IC2][256 * HS + q], a7);
-    a7 = fmaf(sl1, W.w[W_IC2][257 * HS + q], a7);
-    a7 = a7 + W.w[B_IC2][q];
+    float a6 = h6, a7 = h7;
+    a6 = fmaf(sl0, w6a, a6);
+    a6 = fmaf(sl1, w6b, a6);
+    a6 = a6 + b6;
+    a7 = fmaf(sl0, w7a, a7);
+    a7 = fmaf(sl1, w7b, a7);
+    a7 = a7 + b7;
     sh6[m][q] = a6 > 0.0f ? a6 : 0.0f;
     sh7[m][q] = a7 > 0.0f ? a7 : 0.0f;
   }
@@ -216,11 +225,9 @@ __global__ __launch_bounds__(256) void asr_step_fwd_kernel(AsrCfg cfg, AsrW W, A
   const float gsm0 = sv[m][4], gsm1 = sv[m][5], gslv0 = sv[m][6], gslv1 = sv[m][7];
   const float lo = sv[m][8], plo = sv[m][9];
   const float cm = sv[m][12], clv = sv[m][13];
-  // every per-image input read before the first store (stores through
-  // possibly-aliasing pointers would otherwise order each later load behind
-  // them: one memory round trip per load on this one-lane chain)
-  const float e_s = io.eps_scale[b], uu = io.u[b], stop_old = io.stop[b];
-  const int live = io.live[cfg.step], dig = io.digits[b];
+  // (every per-image input was read at the top, before the first store:
+  // stores through possibly-aliasing pointers would otherwise order each
+  // later load behind them -- one memory round trip per load on this chain)
   const float tx = mog_tanhf(sl0), ty = mog_tanhf(sl1);
   const float cvar = mog_expf(clv);
   const float cl = cm + e_s * sqrtf(cvar);
