@@ -380,12 +380,15 @@ int mog_generation_prior(int G, int Z, float s_pm, float s_plv, float h_pm, floa
  * bias, relu).  gammas[8] = num, margin, element, bbox, size, area, area_min,
  * area_max.  T <= 8 steps, <= 8 allowed counts. */
 /* U rows [z (Z) | ss (3) | h (H) | 0] of the two LSTMCell inputs (:403-412,
- * :457-463); null sources read as zeros. */
+ * :457-463); null sources read as zeros.  out2 != NULL: the second cell's rows
+ * [z | ss | h2 | 0] into out2 in the same launch. */
 int mog_asr_pack(int B, int Z, int H, int ld, const float* z, const float* ss, const float* h,
-                 float* out, void* stream);
-/* dz = dU[:, :Z] + dUg[:, :Z]; dss likewise; dh += dU[:, Z+3:]; dhg += dUg[:, Z+3:] */
+                 float* out, const float* h2, float* out2, void* stream);
+/* dz = dU[:, :Z] + dUg[:, :Z] (acc_dz: dz += that sum, the carry added into
+ * an existing latent gradient); dss likewise (stored); dh += dU[:, Z+3:];
+ * dhg += dUg[:, Z+3:] */
 int mog_asr_unpack(int B, int Z, int H, int ld, const float* dU, const float* dUg, float* dz,
-                   float* dss, float* dh, float* dhg, void* stream);
+                   float* dss, float* dh, float* dhg, int acc_dz, void* stream);
 /* heads, latents, theta, concrete z_pres, KLs, entropy, stop / counts /
  * live flag of one step (:414-772) */
 int mog_asr_step_forward(int B, int step, int train, int fix_steps, float thr, float temperature,

@@ -85,11 +85,20 @@ __device__ __forceinline__ float concrete_kl(float y, float plo, float pT, float
 
 // U rows [z_prev (Z) | ss_prev (3) | h_prev (H) | 0 pad] (the LSTMCell input
 // concat order, :403-412 / :457-463); null sources are zeros (step 0)
+// (out2 != null: a second output from h2 in the same launch -- the two cells'
+// rows share z and ss)
 __global__ __launch_bounds__(256) void asr_pack_kernel(int B, int Z, int H, int ld,
                                                        const float* z, const float* ss,
-                                                       const float* h, float* out) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long)B * ld) return;
+                                                       const float* h, float* out,
+                                                       const float* h2, float* out2) {
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long n = (long)B * ld;
+  if (i >= (out2 ? 2 * n : n)) return;
+  if (i >= n) {
+    i -= n;
+    h = h2;
+    out = out2;
+  }
   const int b = i / ld, k = i - (long)b * ld;
   float v = 0.0f;
   if (k < Z) v = z ? z[(size_t)b * Z + k] : 0.0f;
@@ -103,14 +112,17 @@ __global__ __launch_bounds__(256) void asr_pack_kernel(int B, int Z, int H, int 
 __global__ __launch_bounds__(256) void asr_unpack_kernel(int B, int Z, int H, int ld,
                                                          const float* dU, const float* dUg,
                                                          float* dz, float* dss, float* dh,
-                                                         float* dhg) {
+                                                         float* dhg, int acc_dz) {
 #pragma clang fp contract(off)
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)B * (Z + 3 + H)) return;
   const int n = Z + 3 + H;
   const int b = i / n, k = i - (long)b * n;
   const float a = dU[(size_t)b * ld + k], g = dUg[(size_t)b * ld + k];
-  if (k < Z) dz[(size_t)b * Z + k] = a + g;
+  if (k < Z) {
+    const size_t o = (size_t)b * Z + k;
+    dz[o] = acc_dz ? dz[o] + (a + g) : a + g;  // (the same sum as add_(dz, carry))
+  }
   else if (k < Z + 3) dss[(size_t)b * 3 + k - Z] = a + g;
   else {
     const size_t o = (size_t)b * H + k - Z - 3;
@@ -680,21 +692,24 @@ __global__ __launch_bounds__(256) void asr_step_bwd_kernel(AsrCfg cfg, AsrW W, A
 }  // namespace
 
 extern "C" int mog_asr_pack(int B, int Z, int H, int ld, const float* z, const float* ss,
-                            const float* h, float* out, void* stream) {
+                            const float* h, float* out, const float* h2, float* out2,
+                            void* stream) {
   MOG_CHECK_ARG(B >= 0 && Z > 0 && H > 0 && ld >= Z + 3 + H && out);
   if (B == 0) return 0;
-  asr_pack_kernel<<<mog_cdiv((long)B * ld, 256), 256, 0, mog_stream(stream)>>>(B, Z, H, ld, z, ss,
-                                                                             h, out);
+  const long n = (long)B * ld * (out2 ? 2 : 1);
+  asr_pack_kernel<<<mog_cdiv(n, 256), 256, 0, mog_stream(stream)>>>(B, Z, H, ld, z, ss, h, out, h2,
+                                                                   out2);
   MOG_LAUNCH_RET();
 }
 
 extern "C" int mog_asr_unpack(int B, int Z, int H, int ld, const float* dU, const float* dUg,
-                              float* dz, float* dss, float* dh, float* dhg, void* stream) {
+                              float* dz, float* dss, float* dh, float* dhg, int acc_dz,
+                              void* stream) {
   MOG_CHECK_ARG(B >= 0 && Z > 0 && H > 0 && ld >= Z + 3 + H && dU && dUg && dz && dss && dh &&
                 dhg);
   if (B == 0) return 0;
   asr_unpack_kernel<<<mog_cdiv((long)B * (Z + 3 + H), 256), 256, 0, mog_stream(stream)>>>(
-      B, Z, H, ld, dU, dUg, dz, dss, dh, dhg);
+      B, Z, H, ld, dU, dUg, dz, dss, dh, dhg, acc_dz);
   MOG_LAUNCH_RET();
 }
 

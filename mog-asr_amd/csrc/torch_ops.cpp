@@ -735,18 +735,21 @@ void lds_poison_(const Tensor& anchor, int64_t bits) {
 constexpr int64_t ASR_NQ = 28, ASR_DN = 12;
 
 void asr_pack_(int64_t B, int64_t Z, int64_t H, int64_t ld, const optional<Tensor>& z,
-               const optional<Tensor>& ss, const optional<Tensor>& h, Tensor out) {
+               const optional<Tensor>& ss, const optional<Tensor>& h, Tensor out,
+               const optional<Tensor>& h2, const optional<Tensor>& out2) {
   Op o("asr_pack_");
   float* po = o.f(out, B * ld, "out");
   float* pz = o.f(z, B * Z, "z");
   float* ps = o.f(ss, B * 3, "ss");
   float* ph = o.f(h, B * H, "h");
+  float* ph2 = o.f(h2, B * H, "h2");
+  float* po2 = o.f(out2, B * ld, "out2");
   GUARD(o);
-  check(mog_asr_pack(B, Z, H, ld, pz, ps, ph, po, o.stream()), o.name);
+  check(mog_asr_pack(B, Z, H, ld, pz, ps, ph, po, ph2, po2, o.stream()), o.name);
 }
 
 void asr_unpack_(int64_t B, int64_t Z, int64_t H, int64_t ld, const Tensor& dU, const Tensor& dUg,
-                 Tensor dz, Tensor dss, Tensor dh, Tensor dhg) {
+                 Tensor dz, Tensor dss, Tensor dh, Tensor dhg, int64_t acc_dz) {
   Op o("asr_unpack_");
   float* pdz = o.f(dz, B * Z, "dz");
   float* pds = o.f(dss, B * 3, "dss");
@@ -755,7 +758,8 @@ void asr_unpack_(int64_t B, int64_t Z, int64_t H, int64_t ld, const Tensor& dU, 
   float* pu = o.f(dU, B * ld, "dU");
   float* pug = o.f(dUg, B * ld, "dUg");
   GUARD(o);
-  check(mog_asr_unpack(B, Z, H, ld, pu, pug, pdz, pds, pdh, pdg, o.stream()), o.name);
+  check(mog_asr_unpack(B, Z, H, ld, pu, pug, pdz, pds, pdh, pdg, (int)acc_dz, o.stream()),
+        o.name);
 }
 
 void asr_step_forward_(int64_t B, int64_t step, bool train, int64_t fix_steps, double thr,
@@ -1083,10 +1087,10 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
   // AIR-ASR (air_number_bbox_location.py:384-1084)
   m.def(
       "asr_pack_(int B, int Z, int H, int ld, Tensor? z, Tensor? ss, Tensor? h, "
-      "Tensor(a!) out) -> ()");
+      "Tensor(a!) out, Tensor? h2=None, Tensor(b!)? out2=None) -> ()");
   m.def(
       "asr_unpack_(int B, int Z, int H, int ld, Tensor dU, Tensor dUg, Tensor(a!) dz, "
-      "Tensor(b!) dss, Tensor(c!) dh, Tensor(d!) dhg) -> ()");
+      "Tensor(b!) dss, Tensor(c!) dh, Tensor(d!) dhg, int acc_dz=0) -> ()");
   m.def(
       "asr_step_forward_(int B, int step, bool train, int fix_steps, float thr, "
       "float temperature, float s_pm, float s_pv, float s_plv, float gamma_num, Tensor[] w, "

@@ -69,8 +69,8 @@ _SIGS = {
     "mog_copy_f4": [P, P, L, P],
     "mog_lds_poison": [ctypes.c_uint, P],
     "mog_generation_prior": [I, I, F, F, F, F, F, F, P, P, P, P, P, P, P, P],
-    "mog_asr_pack": [I, I, I, I, P, P, P, P, P],
-    "mog_asr_unpack": [I, I, I, I, P, P, P, P, P, P, P],
+    "mog_asr_pack": [I, I, I, I, P, P, P, P, P, P, P],
+    "mog_asr_unpack": [I, I, I, I, P, P, P, P, P, P, I, P],
     "mog_asr_step_forward": [I, I, I, I, F, F, F, F, F, F, P, P, P, P, P, P, P, P, P, P, P, P,
                              P, P, P, P, P, P, P],
     "mog_asr_terms": [I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],

@@ -363,11 +363,10 @@ class AIRModel(_AirBase):
         sc_w = [self._N("inf_scale/dense/kernel")[:H], self._N("inf_scale/dense_2/kernel")[:H]]
         for t in range(T):
             prev = t > 0
+            # both cells' input rows in one launch
             _ops.asr_pack_(B, Z, H, LU, ws.z[t - 1] if prev else None,
-                           ws.ss[t - 1] if prev else None, ws.h[t - 1] if prev else None, ws.U[t])
-            _ops.asr_pack_(B, Z, H, LU, ws.z[t - 1] if prev else None,
-                           ws.ss[t - 1] if prev else None, ws.hg[t - 1] if prev else None,
-                           ws.Ug[t])
+                           ws.ss[t - 1] if prev else None, ws.h[t - 1] if prev else None, ws.U[t],
+                           ws.hg[t - 1] if prev else None, ws.Ug[t])
             # K = LU: the packed rows end in zeros, so the chain's last terms are
             # 0 * w (exactly +-0: the sum is unchanged bit for bit) and the
             # operands are 16-byte rows (LDS-DMA GEMM); the 3 weight rows past
@@ -440,7 +439,8 @@ class AIRModel(_AirBase):
 
     # --------------------------------------------------------- backward ---
     def _dz_hook(self, ws, t, dz):
-        if t < self.max_steps - 1:
+        # (with the batched decoder half, asr_unpack_ added the carry already)
+        if t < self.max_steps - 1 and not getattr(ws, "dec_ready", False):
             _ops.add_(dz, ws.dz_carry, dz, ws.B * self.vae_latent_dimensions)
 
     def _backward(self, X, ws):
@@ -547,8 +547,10 @@ class AIRModel(_AirBase):
                 # (both LSTMCells in one batched launch: same shapes and chains)
                 gemm([ws.dG[t], ws.dGg[t]], [Ki[C2:], Kg], [ws.dU, ws.dUg], B, LU, 4 * H,
                      4 * H, 4 * H, LU, transB=True)
-                _ops.asr_unpack_(B, Z, H, LU, ws.dU, ws.dUg, ws.dz_carry, ws.dss_carry,
-                                 ws.dh[t - 1], ws.dhg[t - 1])
+                # the latent carry added straight into step t-1's dz (its decoder
+                # half is there already: no separate add launch)
+                _ops.asr_unpack_(B, Z, H, LU, ws.dU, ws.dUg, ws.dz_all[t - 1], ws.dss_carry,
+                                 ws.dh[t - 1], ws.dhg[t - 1], 1)
         ws.dm_ready = ws.dec_ready = False
         self._weight_grads(X, ws)
         if steps_side:
