@@ -115,6 +115,16 @@ int mog_gemm_f32_sigmoid_philox(const float* A, const float* B, float* C, const 
 int mog_gemm_f32_kseg(int nseg, const float* const* A, const float* const* B, float* C,
                       const float* bias, const float* Cin, int M, int N, int kseg, int lda,
                       int ldb, int ldc, int transA, int transB, int epi, void* stream);
+/* nprob <= 4 independent k-segment chains of one shape (M x N, kseg, lda /
+ * ldb / ldc, NT when transB) in ONE launch: C[z] = Cin[z] (or 0) + sum of
+ * problem z's nseg[z] segments A_s op(B_s), the problems' segments back to
+ * back in the HOST arrays A / B (at most 8 in all); C / Cin / nseg HOST
+ * arrays of nprob.  Same chains and bits as nprob mog_gemm_f32_kseg calls.
+ * Replaces one AIR-ASR loop step's three head-gradient GEMMs (dh_t, dhg_t,
+ * dhg_{t-1} through the z_pres prior; air_model_pr.py's heads). */
+int mog_gemm_f32_kseg_group(int nprob, const int* nseg, const float* const* A,
+                            const float* const* B, float* const* C, const float* const* Cin, int M,
+                            int N, int kseg, int lda, int ldb, int ldc, int transB, void* stream);
 
 /* ---- spatial transformer -------------------------------------------------
  * air/transformer.py:18-175 transformer(U, theta, out_size) for N images:
@@ -164,6 +174,15 @@ int mog_lstm_cell_forward(const float* G, const float* bias, const float* c_prev
 int mog_lstm_cell_backward(const float* G, const float* bias, const float* c_prev,
                            const float* c_cur, const float* dh, const float* dc, float* dG,
                            float* dc_prev, float* dGsum, int B, int H, void* stream);
+/* Two independent cells of one batch in one launch (AIR-ASR's inference and
+ * generative LSTMCells, asr_model.py's loop): `cells` is a HOST array of
+ * 2 x 5 device pointers {G, bias, c_prev, c_out, h_out} (forward) or
+ * 2 x 9 {G, bias, c_prev, c_cur, dh, dc, dG, dc_prev, dGsum} (backward),
+ * each cell's NULLs as in the single-cell calls; results bit-identical to two
+ * single-cell calls.  Replaces the two rnn_cell calls per step of
+ * air/air_model_pr.py's ASR loop. */
+int mog_lstm_cell_forward_pair(const float* const* cells, int B, int H, void* stream);
+int mog_lstm_cell_backward_pair(const float* const* cells, int B, int H, void* stream);
 
 /* ---- per-step scalars ----------------------------------------------------
  * air_model.py:458-520 (head outputs, scale/shift sampling, theta),

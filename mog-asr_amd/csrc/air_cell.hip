@@ -24,65 +24,98 @@ namespace {
 // ------------------------------------------------------------------ LSTM ---
 // G: [B, 4H] pre-activation (i, j, f, o); bias added here when `bias` != null
 // (step 0, where the h-projection of the zero state is skipped).
-__global__ __launch_bounds__(256) void lstm_fwd_kernel(const float* __restrict__ G,
-                                                       const float* __restrict__ bias,
-                                                       const float* __restrict__ c_prev,
-                                                       float* c_out, float* h_out, int B, int H) {
+struct LstmFwd {
+  const float* G;
+  const float* bias;
+  const float* c_prev;
+  float* c_out;
+  float* h_out;
+};
+
+__device__ __forceinline__ void lstm_fwd_body(const LstmFwd& a, int B, int H, long idx) {
 #pragma clang fp contract(off)
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (long)B * H) return;
   const int b = idx / H, u = idx - (long)b * H;
-  const float* g = G + (size_t)b * 4 * H;
+  const float* g = a.G + (size_t)b * 4 * H;
   float gi = g[u], gj = g[H + u], gf = g[2 * H + u], go = g[3 * H + u];
-  if (bias) {
+  if (a.bias) {
+    const float* bias = a.bias;
     gi = gi + bias[u]; gj = gj + bias[H + u]; gf = gf + bias[2 * H + u]; go = go + bias[3 * H + u];
   }
-  const float c0 = c_prev ? c_prev[idx] : 0.0f;
+  const float c0 = a.c_prev ? a.c_prev[idx] : 0.0f;
   const float nc = c0 * mog_sigmoidf(gf + 1.0f) + mog_sigmoidf(gi) * mog_tanhf(gj);
-  c_out[idx] = nc;
-  h_out[idx] = mog_tanhf(nc) * mog_sigmoidf(go);
+  a.c_out[idx] = nc;
+  a.h_out[idx] = mog_tanhf(nc) * mog_sigmoidf(go);
 }
 
-// dh, dc (incoming, may alias dc_prev_out? no) -> dG [B,4H], dc_prev [B,H];
-// dGsum += dG (sum over steps for the hoisted x-projection gradient).
-__global__ __launch_bounds__(256) void lstm_bwd_kernel(
-    const float* __restrict__ G, const float* __restrict__ bias, const float* __restrict__ c_prev,
-    const float* __restrict__ c_cur, const float* __restrict__ dh, const float* __restrict__ dc,
-    float* dG, float* dc_prev, float* dGsum, int B, int H) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(256) void lstm_fwd_kernel(const LstmFwd a, int B, int H) {
+  lstm_fwd_body(a, B, H, (long)blockIdx.x * 256 + threadIdx.x);
+}
+
+// two independent cells of one batch (AIR-ASR's inference and generative
+// LSTMCells), blockIdx.y picking the cell: one launch per step instead of two
+__global__ __launch_bounds__(256) void lstm_fwd_pair_kernel(const LstmFwd a0, const LstmFwd a1,
+                                                            int B, int H) {
+  lstm_fwd_body(blockIdx.y ? a1 : a0, B, H, (long)blockIdx.x * 256 + threadIdx.x);
+}
+
+// dh, dc (incoming) -> dG [B,4H], dc_prev [B,H]; dGsum += dG (sum over steps
+// for the hoisted x-projection gradient).
+struct LstmBwd {
+  const float* G;
+  const float* bias;
+  const float* c_prev;
+  const float* c_cur;
+  const float* dh;
+  const float* dc;
+  float* dG;
+  float* dc_prev;
+  float* dGsum;
+};
+
+__device__ __forceinline__ void lstm_bwd_body(const LstmBwd& a, int B, int H, long idx) {
   if (idx >= (long)B * H) return;
   const int b = idx / H, u = idx - (long)b * H;
-  const float* g = G + (size_t)b * 4 * H;
+  const float* g = a.G + (size_t)b * 4 * H;
   // every load up front and unconditional, the optional operands read
   // through a valid stand-in pointer and selected away (a load under `p ? ..`
   // compiles to a branch with a vmcnt(0) wait inside; the dGsum loads would
   // otherwise wait behind the dG stores, which the compiler must assume alias)
-  const float* bp = bias ? bias : G;
-  const float* cp = c_prev ? c_prev : c_cur;
-  const float* dp = dc ? dc : dh;
-  float* sp = dGsum ? dGsum + (size_t)b * 4 * H : dG + (size_t)b * 4 * H;
+  const float* bp = a.bias ? a.bias : a.G;
+  const float* cp = a.c_prev ? a.c_prev : a.c_cur;
+  const float* dp = a.dc ? a.dc : a.dh;
+  float* sp = a.dGsum ? a.dGsum + (size_t)b * 4 * H : a.dG + (size_t)b * 4 * H;
   float gi = g[u], gj = g[H + u], gf = g[2 * H + u], go = g[3 * H + u];
   const float bi = bp[u], bj = bp[H + u], bf = bp[2 * H + u], bo = bp[3 * H + u];
-  const float cpv = cp[idx], ctv = c_cur[idx], dhv = dh[idx], dcv = dp[idx];
+  const float cpv = cp[idx], ctv = a.c_cur[idx], dhv = a.dh[idx], dcv = dp[idx];
   const float s0 = sp[u], s1 = sp[H + u], s2 = sp[2 * H + u], s3 = sp[3 * H + u];
-  if (bias) {
+  if (a.bias) {
     gi = gi + bi; gj = gj + bj; gf = gf + bf; go = go + bo;
   }
   const float si = mog_sigmoidf(gi), tj = mog_tanhf(gj), sf = mog_sigmoidf(gf + 1.0f);
   const float so = mog_sigmoidf(go);
-  const float c0 = c_prev ? cpv : 0.0f;
+  const float c0 = a.c_prev ? cpv : 0.0f;
   const float tc = mog_tanhf(ctv);
-  const float dct = (dc ? dcv : 0.0f) + dhv * so * (1.0f - tc * tc);
+  const float dct = (a.dc ? dcv : 0.0f) + dhv * so * (1.0f - tc * tc);
   const float dgo = dhv * tc * so * (1.0f - so);
   const float dgf = dct * c0 * sf * (1.0f - sf);
   const float dgi = dct * tj * si * (1.0f - si);
   const float dgj = dct * si * (1.0f - tj * tj);
-  float* d = dG + (size_t)b * 4 * H;
+  float* d = a.dG + (size_t)b * 4 * H;
   d[u] = dgi; d[H + u] = dgj; d[2 * H + u] = dgf; d[3 * H + u] = dgo;
-  if (dGsum) {
+  if (a.dGsum) {
     sp[u] = s0 + dgi; sp[H + u] = s1 + dgj; sp[2 * H + u] = s2 + dgf; sp[3 * H + u] = s3 + dgo;
   }
-  if (dc_prev) dc_prev[idx] = dct * sf;
+  if (a.dc_prev) a.dc_prev[idx] = dct * sf;
+}
+
+__global__ __launch_bounds__(256) void lstm_bwd_kernel(const LstmBwd a, int B, int H) {
+  lstm_bwd_body(a, B, H, (long)blockIdx.x * 256 + threadIdx.x);
+}
+
+__global__ __launch_bounds__(256) void lstm_bwd_pair_kernel(const LstmBwd a0, const LstmBwd a1,
+                                                            int B, int H) {
+  lstm_bwd_body(blockIdx.y ? a1 : a0, B, H, (long)blockIdx.x * 256 + threadIdx.x);
 }
 
 // -------------------------------------------------------- step scalars ---
@@ -713,8 +746,8 @@ extern "C" int mog_lstm_cell_forward(const float* G, const float* bias, const fl
                                      float* c_out, float* h_out, int B, int H, void* stream) {
   MOG_CHECK_ARG(G && c_out && h_out && B >= 0 && H > 0);
   if (B == 0) return 0;
-  lstm_fwd_kernel<<<mog_cdiv((long)B * H, 256), 256, 0, mog_stream(stream)>>>(G, bias, c_prev,
-                                                                              c_out, h_out, B, H);
+  lstm_fwd_kernel<<<mog_cdiv((long)B * H, 256), 256, 0, mog_stream(stream)>>>(
+      LstmFwd{G, bias, c_prev, c_out, h_out}, B, H);
   MOG_LAUNCH_RET();
 }
 
@@ -725,7 +758,35 @@ extern "C" int mog_lstm_cell_backward(const float* G, const float* bias, const f
   MOG_CHECK_ARG(G && c_cur && dh && dG && B >= 0 && H > 0);
   if (B == 0) return 0;
   lstm_bwd_kernel<<<mog_cdiv((long)B * H, 256), 256, 0, mog_stream(stream)>>>(
-      G, bias, c_prev, c_cur, dh, dc, dG, dc_prev, dGsum, B, H);
+      LstmBwd{G, bias, c_prev, c_cur, dh, dc, dG, dc_prev, dGsum}, B, H);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_lstm_cell_forward_pair(const float* const* cells, int B, int H, void* stream) {
+  MOG_CHECK_ARG(cells && B >= 0 && H > 0);
+  const float* const* a = cells;
+  const float* const* b = cells + 5;
+  MOG_CHECK_ARG(a[0] && a[3] && a[4] && b[0] && b[3] && b[4]);
+  if (B == 0) return 0;
+  lstm_fwd_pair_kernel<<<dim3(mog_cdiv((long)B * H, 256), 2), 256, 0, mog_stream(stream)>>>(
+      LstmFwd{a[0], a[1], a[2], const_cast<float*>(a[3]), const_cast<float*>(a[4])},
+      LstmFwd{b[0], b[1], b[2], const_cast<float*>(b[3]), const_cast<float*>(b[4])}, B, H);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_lstm_cell_backward_pair(const float* const* cells, int B, int H,
+                                           void* stream) {
+  MOG_CHECK_ARG(cells && B >= 0 && H > 0);
+  LstmBwd c[2];
+  for (int k = 0; k < 2; ++k) {
+    const float* const* a = cells + 9 * k;
+    MOG_CHECK_ARG(a[0] && a[3] && a[4] && a[6]);
+    c[k] = LstmBwd{a[0], a[1], a[2], a[3], a[4], a[5], const_cast<float*>(a[6]),
+                   const_cast<float*>(a[7]), const_cast<float*>(a[8])};
+  }
+  if (B == 0) return 0;
+  lstm_bwd_pair_kernel<<<dim3(mog_cdiv((long)B * H, 256), 2), 256, 0, mog_stream(stream)>>>(
+      c[0], c[1], B, H);
   MOG_LAUNCH_RET();
 }
 

@@ -57,6 +57,9 @@ struct GemmPtrs {
 struct GemmDims {
   int M, N, K, lda, ldb, ldc, ldaux, splitk, kchunk, vecA, vecB, nx, ny;
   int kseg;  // > 0: K is nseg segments of kseg, segment s read from A[s] / B[s]
+  // (kseg) problem z of the batch owns segments segoff[z] .. segoff[z+1]-1
+  // (its K = that count * kseg; D.K is the largest problem's)
+  int segoff[5];
   int vecC;  // C / Cpre / aux 16-byte aligned with ldc, ldaux % 4 == 0 (row-staged epilogue)
   float aux_scale;
   // EPI_SIGMOID_NOISE with in-kernel noise (eps_gen): the noise of element
@@ -417,7 +420,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
   const int z = bz / D.splitk, ks = bz - z * D.splitk;
   const int m0 = by * BM, n0 = bx * BN;
   const int kbeg = ks * D.kchunk;
-  const int kend = min(D.K, kbeg + D.kchunk);
+  const int sb = KSEG ? D.segoff[z] : 0;  // (kseg) problem z's first segment
+  const int kend = min(KSEG ? (D.segoff[z + 1] - sb) * D.kseg : D.K, kbeg + D.kchunk);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
   const int M = D.M, N = D.N;
@@ -450,8 +454,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
   const int ka = KSEG ? D.kseg : D.K;
   const long extA = TA ? (long)(ka - 1) * D.lda + M : (long)(M - 1) * D.lda + ka;
   const long extB = TB ? (long)(N - 1) * D.ldb + ka : (long)(ka - 1) * D.ldb + N;
-  __amdgpu_buffer_rsrc_t ra = frsrc(P.A[KSEG ? 0 : z], extA);
-  __amdgpu_buffer_rsrc_t rb = frsrc(P.B[KSEG ? 0 : z], extB);
+  __amdgpu_buffer_rsrc_t ra = frsrc(P.A[KSEG ? sb : z], extA);
+  __amdgpu_buffer_rsrc_t rb = frsrc(P.B[KSEG ? sb : z], extB);
   int seg = 0;
 
   // PF register sets of staged tiles: tile j+1 is loaded PF iterations
@@ -464,8 +468,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmPtrs P, GemmDims D) {
       const int sg = k0 / D.kseg;
       if (sg != seg) {
         seg = sg;
-        ra = frsrc(P.A[sg], extA);
-        rb = frsrc(P.B[sg], extB);
+        ra = frsrc(P.A[sb + sg], extA);
+        rb = frsrc(P.B[sb + sg], extB);
       }
       kl = k0 - sg * D.kseg;
       kl_end = kend - sg * D.kseg;
@@ -1099,8 +1103,56 @@ extern "C" int mog_gemm_f32_kseg(int nseg, const float* const* A, const float* c
   D.splitk = 1;
   D.kchunk = 0;
   D.kseg = kseg;
+  D.segoff[0] = 0;
+  D.segoff[1] = nseg;
   D.eps_gen = 0;
   D.eps_seed = D.eps_off = 0;
   MOG_TRY(launch_auto(transA, transB, epi, mog_stream(stream), P, D, 1));
+  MOG_LAUNCH_RET();
+}
+
+// nprob independent k-segment chains of one shape in ONE launch: problem z
+// is C_z = Cin_z + sum_s A_s B_s^T over its nseg[z] segments (A / B hold the
+// problems' segments back to back): e.g. one AIR-ASR loop step's dh (five
+// heads), dhg (two generative heads) and dhg_{t-1} (the z_pres prior).
+extern "C" int mog_gemm_f32_kseg_group(int nprob, const int* nseg, const float* const* A,
+                                       const float* const* B, float* const* C,
+                                       const float* const* Cin, int M, int N, int kseg, int lda,
+                                       int ldb, int ldc, int transB, void* stream) {
+  MOG_CHECK_ARG(nprob >= 1 && nprob <= 4 && nseg && A && B && C && kseg > 0 && kseg % 16 == 0);
+  MOG_CHECK_ARG(M >= 0 && N >= 0);
+  if (M == 0 || N == 0) return 0;
+  GemmPtrs P = {};
+  GemmDims D;
+  bool va = true, vb = true;
+  int tot = 0, most = 0;
+  for (int z = 0; z < nprob; ++z) {
+    MOG_CHECK_ARG(nseg[z] >= 1 && C[z]);
+    D.segoff[z] = tot;
+    tot += nseg[z];
+    most = nseg[z] > most ? nseg[z] : most;
+    P.C[z] = C[z];
+    P.Cin[z] = Cin ? Cin[z] : nullptr;
+  }
+  MOG_CHECK_ARG(tot <= MAXB);
+  D.segoff[nprob] = tot;
+  for (int i = 0; i < tot; ++i) {
+    MOG_CHECK_ARG(A[i] && B[i]);
+    P.A[i] = A[i];
+    P.B[i] = B[i];
+    va = va && aligned16(A[i]);
+    vb = vb && aligned16(B[i]);
+  }
+  D.M = M; D.N = N; D.K = most * kseg; D.lda = lda; D.ldb = ldb; D.ldc = ldc; D.ldaux = 0;
+  D.aux_scale = 0.0f;
+  D.vecA = va && (lda % 4 == 0);
+  D.vecB = vb && (ldb % 4 == 0);
+  D.vecC = 0;
+  D.splitk = 1;
+  D.kchunk = 0;
+  D.kseg = kseg;
+  D.eps_gen = 0;
+  D.eps_seed = D.eps_off = 0;
+  MOG_TRY(launch_auto(false, transB != 0, EPI_STORE, mog_stream(stream), P, D, nprob));
   MOG_LAUNCH_RET();
 }

@@ -165,6 +165,32 @@ void gemm_f32_kseg_(at::TensorList A, at::TensorList B, Tensor C, const optional
         o.name);
 }
 
+void gemm_f32_kseg_group_(at::TensorList A, at::TensorList B, at::TensorList C,
+                          const c10::List<optional<Tensor>>& Cin, at::IntArrayRef nseg, int64_t M,
+                          int64_t N, int64_t kseg, int64_t lda, int64_t ldb, int64_t ldc,
+                          bool transB) {
+  Op o("gemm_f32_kseg_group_");
+  auto c = o.list(C, F32, mat(M, N, ldc), "C");
+  auto a = o.list(A, F32, mat(M, kseg, lda), "A");
+  auto b = o.list(B, F32, transB ? mat(N, kseg, ldb) : mat(kseg, N, ldb), "B");
+  auto ci = o.list(Cin, F32, mat(M, N, ldc), "Cin");
+  TORCH_CHECK(nseg.size() == c.size() && ci.size() == c.size(), o.name,
+              ": nseg / Cin / C of one length");
+  int64_t tot = 0;
+  std::vector<int> ns;
+  for (auto n : nseg) {
+    ns.push_back((int)n);
+    tot += n;
+  }
+  TORCH_CHECK(a.size() == (size_t)tot && b.size() == (size_t)tot, o.name,
+              ": sum(nseg) A and B segments");
+  GUARD(o);
+  check(mog_gemm_f32_kseg_group((int)c.size(), ns.data(), arr<float>(a), arr<float>(b),
+                                marr<float>(c), arr<float>(ci), M, N,
+                                kseg, lda, ldb, ldc, transB, o.stream()),
+        o.name);
+}
+
 void gemm_bf16_(at::TensorList A, at::TensorList B, at::TensorList C,
                 const c10::List<optional<Tensor>>& bias, const c10::List<optional<Tensor>>& Cin,
                 const c10::List<optional<Tensor>>& aux, const c10::List<optional<Tensor>>& colsum,
@@ -308,6 +334,40 @@ void lstm_cell_backward_(const Tensor& G, const optional<Tensor>& bias,
   GUARD(o);
   check(mog_lstm_cell_backward(pg, pb, pcp, pcc, pdh, pdc, pdg, pdcp, pgs, B, H, o.stream()),
         o.name);
+}
+
+// the two cells of one batch in one launch (no bias: both cells' gate GEMMs
+// add theirs)
+void lstm_cell_forward2_(const Tensor& G0, const optional<Tensor>& c_prev0, Tensor c_out0,
+                         Tensor h_out0, const Tensor& G1, const optional<Tensor>& c_prev1,
+                         Tensor c_out1, Tensor h_out1, int64_t B, int64_t H) {
+  Op o("lstm_cell_forward2_");
+  const float* p[10] = {o.f(G0, B * 4 * H, "G0"), nullptr, o.f(c_prev0, B * H, "c_prev0"),
+                        o.f(c_out0, B * H, "c_out0"), o.f(h_out0, B * H, "h_out0"),
+                        o.f(G1, B * 4 * H, "G1"), nullptr, o.f(c_prev1, B * H, "c_prev1"),
+                        o.f(c_out1, B * H, "c_out1"), o.f(h_out1, B * H, "h_out1")};
+  GUARD(o);
+  check(mog_lstm_cell_forward_pair(p, B, H, o.stream()), o.name);
+}
+
+void lstm_cell_backward2_(const Tensor& G0, const optional<Tensor>& c_prev0, const Tensor& c_cur0,
+                          const Tensor& dh0, const optional<Tensor>& dc0, Tensor dG0,
+                          Tensor dc_prev0, const optional<Tensor>& dGsum0, const Tensor& G1,
+                          const optional<Tensor>& c_prev1, const Tensor& c_cur1,
+                          const Tensor& dh1, const optional<Tensor>& dc1, Tensor dG1,
+                          Tensor dc_prev1, const optional<Tensor>& dGsum1, int64_t B, int64_t H) {
+  Op o("lstm_cell_backward2_");
+  const float* p[18] = {o.f(G0, B * 4 * H, "G0"),        nullptr,
+                        o.f(c_prev0, B * H, "c_prev0"),  o.f(c_cur0, B * H, "c_cur0"),
+                        o.f(dh0, B * H, "dh0"),          o.f(dc0, B * H, "dc0"),
+                        o.f(dG0, B * 4 * H, "dG0"),      o.f(dc_prev0, B * H, "dc_prev0"),
+                        o.f(dGsum0, B * 4 * H, "dGsum0"), o.f(G1, B * 4 * H, "G1"),
+                        nullptr,                         o.f(c_prev1, B * H, "c_prev1"),
+                        o.f(c_cur1, B * H, "c_cur1"),    o.f(dh1, B * H, "dh1"),
+                        o.f(dc1, B * H, "dc1"),          o.f(dG1, B * 4 * H, "dG1"),
+                        o.f(dc_prev1, B * H, "dc_prev1"), o.f(dGsum1, B * 4 * H, "dGsum1")};
+  GUARD(o);
+  check(mog_lstm_cell_backward_pair(p, B, H, o.stream()), o.name);
 }
 
 // ------------------------------------------------ heads / concrete / masks ----
@@ -996,6 +1056,9 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "gemm_f32_kseg_(Tensor[] A, Tensor[] B, Tensor(a!) C, Tensor? bias, Tensor? Cin, int M, "
       "int N, int kseg, int lda, int ldb, int ldc, bool transA, bool transB, int epi) -> ()");
   m.def(
+      "gemm_f32_kseg_group_(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] Cin, int[] nseg, "
+      "int M, int N, int kseg, int lda, int ldb, int ldc, bool transB) -> ()");
+  m.def(
       "gemm_bf16_(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, Tensor?[] Cin, "
       "Tensor?[] aux, Tensor(b!)?[] colsum, int M, int N, int K, int lda, int ldb, int ldc, "
       "int ldaux, bool tn, int epi, float aux_scale, int splitk) -> ()");
@@ -1017,6 +1080,14 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
   m.def(
       "lstm_cell_backward_(Tensor G, Tensor? bias, Tensor? c_prev, Tensor c_cur, Tensor dh, "
       "Tensor? dc, Tensor(a!) dG, Tensor(b!) dc_prev, Tensor(c!)? dGsum, int B, int H) -> ()");
+  m.def(
+      "lstm_cell_forward2_(Tensor G0, Tensor? c_prev0, Tensor(a!) c_out0, Tensor(b!) h_out0, "
+      "Tensor G1, Tensor? c_prev1, Tensor(c!) c_out1, Tensor(d!) h_out1, int B, int H) -> ()");
+  m.def(
+      "lstm_cell_backward2_(Tensor G0, Tensor? c_prev0, Tensor c_cur0, Tensor dh0, Tensor? dc0, "
+      "Tensor(a!) dG0, Tensor(b!) dc_prev0, Tensor(c!)? dGsum0, Tensor G1, Tensor? c_prev1, "
+      "Tensor c_cur1, Tensor dh1, Tensor? dc1, Tensor(d!) dG1, Tensor(e!) dc_prev1, "
+      "Tensor(f!)? dGsum1, int B, int H) -> ()");
   m.def(
       "air_step_forward_(int B, int HS, int HZ, int step, bool train, bool use_num_prior, "
       "float thr, float temperature, float prior_lo, float prior_bias, float s_pm, float s_pv, "
@@ -1132,6 +1203,9 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("stn_backward_sigmoid_", &stn_backward_sigmoid_);
   m.impl("lstm_cell_forward_", &lstm_cell_forward_);
   m.impl("lstm_cell_backward_", &lstm_cell_backward_);
+  m.impl("gemm_f32_kseg_group_", &gemm_f32_kseg_group_);
+  m.impl("lstm_cell_forward2_", &lstm_cell_forward2_);
+  m.impl("lstm_cell_backward2_", &lstm_cell_backward2_);
   m.impl("air_step_forward_", &air_step_forward_);
   m.impl("air_step_backward_", &air_step_backward_);
   m.impl("generation_prior_", &generation_prior_);

@@ -375,10 +375,10 @@ class AIRModel(_AirBase):
             # cell continues the hoisted x-projection's chain through Cin)
             gemm([ws.U[t], ws.Ug[t]], [Ki[C2:], Kg], [ws.G[t], ws.Gg[t]], B, 4 * H, LU, LU,
                  4 * H, 4 * H, bias=[bi, bg], Cin=[ws.Gx, None])
-            _ops.lstm_cell_forward_(ws.G[t], None, ws.c[t - 1] if prev else None, ws.c[t],
-                                    ws.h[t], B, H)
-            _ops.lstm_cell_forward_(ws.Gg[t], None, ws.cg[t - 1] if prev else None, ws.cg[t],
-                                    ws.hg[t], B, H)
+            # (both cells' gates in one launch)
+            _ops.lstm_cell_forward2_(ws.G[t], ws.c[t - 1] if prev else None, ws.c[t], ws.h[t],
+                                     ws.Gg[t], ws.cg[t - 1] if prev else None, ws.cg[t],
+                                     ws.hg[t], B, H)
             hid = [ws.hid8[k, t] for k in range(8)]
             # (the inference and generative ReLU heads in one batched launch)
             gemm([ws.h[t]] * 3 + [ws.hg[t]] * 2, list(relu_w) + list(gen_w), hid[0:5], B, 64, H,
@@ -524,20 +524,22 @@ class AIRModel(_AirBase):
                                     ws.dss_carry if t < T - 1 else None, ws.douts[t],
                                     [x if (k != 5 or fix < 0) else None
                                      for k, x in enumerate(dpre)])
-            # dh[t] += the five heads reading h_t; dhg[t] += the generative shift heads
-            ops.gemm_kseg([dpre[k] for k in (0, 1, 2, 6, 7)], head_w, ws.dh[t], B, H, 64, 64, 64,
-                          H, transB=True, Cin=ws.dh[t])
-            ops.gemm_kseg([dpre[3], dpre[4]], gen_w, ws.dhg[t], B, H, 64, 64, 64, H, transB=True,
-                          Cin=ws.dhg[t])
-            if fix < 0 and t > 0:  # the prior at step t reads hg_{t-1}
-                gemm([dpre[5]], [self._N("z_pres/prior/dense/kernel")], [ws.dhg[t - 1]], B, H,
-                     64, 64, 64, H, transB=True, Cin=[ws.dhg[t - 1]])
+            # dh[t] += the five heads reading h_t; dhg[t] += the generative shift
+            # heads; dhg[t-1] += the prior at step t (it reads hg_{t-1}): three
+            # chains of one shape in one launch
+            probs = [([dpre[k] for k in (0, 1, 2, 6, 7)], head_w, ws.dh[t], ws.dh[t]),
+                     ([dpre[3], dpre[4]], gen_w, ws.dhg[t], ws.dhg[t])]
+            if fix < 0 and t > 0:
+                probs.append(([dpre[5]], [self._N("z_pres/prior/dense/kernel")], ws.dhg[t - 1],
+                              ws.dhg[t - 1]))
+            ops.gemm_kseg_group(probs, B, H, 64, 64, 64, H, transB=True)
             dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
-            _ops.lstm_cell_backward_(ws.G[t], None, ws.c[t - 1] if t > 0 else None, ws.c[t],
-                                     ws.dh[t], dc_in, ws.dG[t], ws.dc[t % 2], ws.dGsum, B, H)
             dcg_in = ws.dcg[(t + 1) % 2] if t < T - 1 else None
-            _ops.lstm_cell_backward_(ws.Gg[t], None, ws.cg[t - 1] if t > 0 else None, ws.cg[t],
-                                     ws.dhg[t], dcg_in, ws.dGg[t], ws.dcg[t % 2], ws.dGgsum, B, H)
+            # (both cells in one launch)
+            _ops.lstm_cell_backward2_(ws.G[t], ws.c[t - 1] if t > 0 else None, ws.c[t], ws.dh[t],
+                                      dc_in, ws.dG[t], ws.dc[t % 2], ws.dGsum, ws.Gg[t],
+                                      ws.cg[t - 1] if t > 0 else None, ws.cg[t], ws.dhg[t],
+                                      dcg_in, ws.dGg[t], ws.dcg[t % 2], ws.dGgsum, B, H)
             if steps_side and self.U_WGRAD_PER_STEP:
                 # step t's recurrent-rows gradients likewise (dG_t, dGg_t final)
                 with torch.cuda.stream(self._fork(side)):

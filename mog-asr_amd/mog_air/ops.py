@@ -163,6 +163,18 @@ def gemm_kseg(A: Sequence[torch.Tensor], B: Sequence[torch.Tensor], C: torch.Ten
                         bool(transB), epi)
 
 
+def gemm_kseg_group(probs, M: int, N: int, kseg: int, lda: int, ldb: int, ldc: int,
+                    transB=False) -> None:
+    """Independent k-segment chains of one shape in ONE launch
+    (mog_gemm_f32_kseg_group): ``probs`` = [(A_list, B_list, C, Cin), ...],
+    C_z = Cin_z + sum_s A_s op(B_s) -- the same bits as one gemm_kseg each."""
+    A = [a for p in probs for a in p[0]]
+    B = [b for p in probs for b in p[1]]
+    _ops.gemm_f32_kseg_group_(A, B, [p[2] for p in probs], [p[3] for p in probs],
+                              [len(p[0]) for p in probs], M, N, kseg, lda, ldb, ldc,
+                              bool(transB))
+
+
 def dense(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor,
           epi=EPI_STORE, pre: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = act(x @ w + b), one k-ordered fp32 chain per output."""

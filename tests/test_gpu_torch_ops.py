@@ -310,8 +310,8 @@ def test_asr_model_dispatches_through_torch_ops():
             want = {"mog_air.asr_pack_", "mog_air.asr_step_forward_", "mog_air.asr_terms_",
                     "mog_air.asr_finalize_", "mog_air.asr_terms_backward_",
                     "mog_air.asr_step_backward_", "mog_air.asr_unpack_", "mog_air.add_",
-                    "mog_air.gemm_f32_", "mog_air.lstm_cell_forward_", "mog_air.recon_loss_",
-                    "mog_air.lstm_cell_backward_", "mog_air.clip_adam_"}
+                    "mog_air.gemm_f32_", "mog_air.lstm_cell_forward2_", "mog_air.recon_loss_",
+                    "mog_air.lstm_cell_backward2_", "mog_air.clip_adam_"}
             assert want <= rec.names, sorted(want - rec.names)
     finally:
         _lib.call = real
@@ -363,6 +363,82 @@ def test_opcheck_launch_level_ops():
             (G, None, torch.randn(B, 256, device=DEV), torch.empty(B, 256, device=DEV),
              torch.empty(B, 256, device=DEV), B, 256),
             test_utils=("test_schema",))
+
+
+def test_lstm_cell_pair_ops_match_single_cells_bitwise():
+    """lstm_cell_forward2_ / lstm_cell_backward2_ (both AIR-ASR cells in one
+    launch) write exactly what two single-cell launches write, the optional
+    operands (c_prev, dc, dGsum) absent in one cell and present in the other;
+    the schemas' mutation annotations hold (opcheck)."""
+    from torch.library import opcheck
+    ops = torch.ops.mog_air
+    g = torch.Generator(device="cpu").manual_seed(11)
+    B, H = 77, 256
+
+    def rn(*s):
+        return torch.randn(*s, generator=g).to(DEV)
+
+    G0, G1, cp1 = rn(B, 4 * H), rn(B, 4 * H), rn(B, H)
+    single = [torch.empty(B, H, device=DEV) for _ in range(4)]
+    ops.lstm_cell_forward_(G0, None, None, single[0], single[1], B, H)
+    ops.lstm_cell_forward_(G1, None, cp1, single[2], single[3], B, H)
+    pair = [torch.empty(B, H, device=DEV) for _ in range(4)]
+    ops.lstm_cell_forward2_(G0, None, pair[0], pair[1], G1, cp1, pair[2], pair[3], B, H)
+    for a, b in zip(single, pair):
+        assert torch.equal(a, b)
+    cc0, cc1, dh0, dh1, dc1 = rn(B, H), rn(B, H), rn(B, H), rn(B, H), rn(B, H)
+    s0, s1 = rn(B, 4 * H), rn(B, 4 * H)
+    outs_s = [torch.empty(B, 4 * H, device=DEV), torch.empty(B, H, device=DEV),
+              torch.empty(B, 4 * H, device=DEV), torch.empty(B, H, device=DEV)]
+    gs_s = s1.clone()
+    ops.lstm_cell_backward_(G0, None, None, cc0, dh0, None, outs_s[0], outs_s[1], None, B, H)
+    ops.lstm_cell_backward_(G1, None, cp1, cc1, dh1, dc1, outs_s[2], outs_s[3], gs_s, B, H)
+    outs_p = [torch.empty_like(x) for x in outs_s]
+    gs_p = s1.clone()
+    ops.lstm_cell_backward2_(G0, None, cc0, dh0, None, outs_p[0], outs_p[1], None,
+                             G1, cp1, cc1, dh1, dc1, outs_p[2], outs_p[3], gs_p, B, H)
+    torch.cuda.synchronize()
+    for a, b in zip(outs_s + [gs_s], outs_p + [gs_p]):
+        assert torch.equal(a, b)
+    assert not torch.equal(gs_p, s1)
+    opcheck(ops.lstm_cell_forward2_.default,
+            (G0, None, pair[0], pair[1], G1, cp1, pair[2], pair[3], B, H),
+            test_utils=("test_schema",))
+    opcheck(ops.lstm_cell_backward2_.default,
+            (G0, cp1, cc0, dh0, dc1, outs_p[0], outs_p[1], s0.clone(),
+             G1, cp1, cc1, dh1, dc1, outs_p[2], outs_p[3], s1.clone(), B, H),
+            test_utils=("test_schema",))
+
+
+def test_gemm_kseg_group_matches_single_chains_bitwise():
+    """gemm_f32_kseg_group_ (AIR-ASR's three head-gradient chains of one loop
+    step in one launch, segment counts 5 / 2 / 1) writes exactly what one
+    gemm_f32_kseg_ per problem writes, Cin and a missing Cin included, and the
+    chains match a float64 restatement to fp32 accuracy."""
+    from mog_air import ops as mops
+    g = torch.Generator(device="cpu").manual_seed(5)
+    M, N, KS = 70, 256, 64
+
+    def rn(*s):
+        return torch.randn(*s, generator=g).to(DEV)
+
+    segs = [([rn(M, KS) for _ in range(n)], [rn(N + 8, KS)[:N] for _ in range(n)]) for n in (5, 2, 1)]
+    cin = [rn(M, N), None, rn(M, N)]
+    want = []
+    for (A, Bs), c in zip(segs, cin):
+        out = torch.empty(M, N, device=DEV)
+        mops.gemm_kseg(A, Bs, out, M, N, KS, KS, KS, N, transB=True, Cin=c)
+        want.append(out)
+    got = [torch.empty(M, N, device=DEV) for _ in segs]
+    mops.gemm_kseg_group([(A, Bs, o, c) for (A, Bs), o, c in zip(segs, got, cin)], M, N, KS, KS,
+                         KS, N, transB=True)
+    torch.cuda.synchronize()
+    for (A, Bs), c, w, o in zip(segs, cin, want, got):
+        assert torch.equal(w, o)
+        ref = sum(a.double() @ b.double().T for a, b in zip(A, Bs))
+        if c is not None:
+            ref = ref + c.double()
+        assert (o.double() - ref).abs().max() <= 1e-5 * ref.abs().max()
 
 
 # ------------------------------------------------ heads + concrete step op ----

@@ -54,7 +54,8 @@ def test_torch_ops_extension_registers_every_launch_op():
     _lib.load_torch_ops()
     names = ("gemm_f32_", "gemm_f32_kseg_", "gemm_bf16_", "cvt_bf16_batch_", "stn_forward_",
              "stn_backward_", "stn_backward_sigmoid_", "lstm_cell_forward_",
-             "lstm_cell_backward_", "air_step_forward_", "air_step_backward_",
+             "lstm_cell_backward_", "lstm_cell_forward2_", "lstm_cell_backward2_", "gemm_f32_kseg_group_",
+             "air_step_forward_", "air_step_backward_",
              "vae_sample_forward_", "vae_sample_backward_", "sigmoid_backward_", "stn_vae_step_",
              "recon_loss_", "batch_mean_", "clip_adam_", "add_", "rng_fill_",
              "generation_prior_", "asr_pack_", "asr_unpack_", "asr_step_forward_", "asr_terms_",
@@ -69,6 +70,8 @@ def test_torch_ops_extension_registers_every_launch_op():
                "stn_backward_": {"dU", "dtheta", "dot"},
                "stn_backward_sigmoid_": {"dm", "dtheta", "dot"},
                "lstm_cell_backward_": {"dG", "dc_prev", "dGsum"},
+               "lstm_cell_forward2_": {"c_out0", "h_out0", "c_out1", "h_out1"},
+               "lstm_cell_backward2_": {"dG0", "dc_prev0", "dGsum0", "dG1", "dc_prev1", "dGsum1"},
                "vae_sample_forward_": {"z", "z_bf16", "runloss", "vkl"},
                "vae_sample_backward_": {"dmu", "dlv", "dmu_bf16", "dlv_bf16"},
                "recon_loss_": {"canvas", "recon", "bce", "mse", "loss", "acc", "dcanvas"},
