@@ -97,7 +97,8 @@ class _AsrWorkspace(_Workspace):
         self.area, self.outl, self.size, self.over = e(B), e(B), e(B), e(B)
         self.zsum = e(T)
         self.margin = e(1)
-        self.cg_prev_zero = torch.zeros((B, H), device=dev, dtype=torch.float32)
+        # hg_{-1}: the zero state the learned prior reads at step 0
+        self.hg_zero = torch.zeros((B, H), device=dev, dtype=torch.float32)
 
     def alloc_backward(self, m):
         if self._bwd:
@@ -380,12 +381,16 @@ class AIRModel(_AirBase):
                                      ws.Gg[t], ws.cg[t - 1] if prev else None, ws.cg[t],
                                      ws.hg[t], B, H)
             hid = [ws.hid8[k, t] for k in range(8)]
-            # (the inference and generative ReLU heads in one batched launch)
-            gemm([ws.h[t]] * 3 + [ws.hg[t]] * 2, list(relu_w) + list(gen_w), hid[0:5], B, 64, H,
-                 H, 64, 64, epi=EPI_RELU, bias=list(relu_b) + list(gen_b))
-            if fix < 0:  # learned prior from the previous generative output (:596-602)
-                gemm([ws.Ug[t][:, Z + 3:]], [self._N("z_pres/prior/dense/kernel")], [hid[5]], B,
-                     64, H, LU, 64, 64, epi=EPI_RELU, bias=[self._N("z_pres/prior/dense/bias")])
+            # (the inference and generative ReLU heads in one batched launch, with
+            # the learned prior from the previous generative output (:596-602):
+            # hg_{t-1}, the rows asr_pack_ copied into Ug[t])
+            ra, rw = [ws.h[t]] * 3 + [ws.hg[t]] * 2, list(relu_w) + list(gen_w)
+            rb = list(relu_b) + list(gen_b)
+            if fix < 0:
+                ra.append(ws.hg[t - 1] if prev else ws.hg_zero)
+                rw.append(self._N("z_pres/prior/dense/kernel"))
+                rb.append(self._N("z_pres/prior/dense/bias"))
+            gemm(ra, rw, hid[0:len(ra)], B, 64, H, H, 64, 64, epi=EPI_RELU, bias=rb)
             gemm([ws.h[t]] * 2, sc_w, hid[6:8], B, 64, H, H, 64, 64, epi=EPI_STORE)
             hid_l = [x if (k != 5 or fix < 0) else None for k, x in enumerate(hid)]
             _ops.asr_step_forward_(B, t, self.train, fix, thr, temp, float(self.scale_prior_mean),
