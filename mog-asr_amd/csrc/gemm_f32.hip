@@ -975,6 +975,22 @@ int launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, con
       else return launch_dma<64, 64, 16, 3>(ta, tb, epi, s, P, D, batch);
     }
   }
+  // k-segment NT chains of a small batch (AIR / AIR-ASR's per-step head
+  // gradients at the reference's batch of 64: a 64 x 64 grid of a dozen
+  // workgroups, each a serial K = 64..320 chain): 32 x 32 tiles 32 deep --
+  // four times the workgroups, half the barriers per k.  Same k order: same
+  // bits.  MOG_KSEG_SMALL=0 keeps 64 x 64 x 16.
+  static const char* ks_env = getenv("MOG_KSEG_SMALL");
+  if (D.kseg > 0 && !ta && tb && D.kseg % 32 == 0 && (ks_env == nullptr || atoi(ks_env) != 0) &&
+      (long)mog_cdiv(D.M, 64) * mog_cdiv(D.N, 64) * batch < 128) {
+    GemmDims E = D;
+    E.kchunk = ((E.K + 31) / 32) * 32;
+    E.splitk = 1;
+    E.nx = mog_cdiv(E.N, 32);
+    E.ny = mog_cdiv(E.M, 32);
+    launch_epi<32, 32, 32, 1, false, true, true>(epi, dim3(E.nx, E.ny, batch), s, P, E);
+    return 0;
+  }
   if (b128) launch_tile<128, 128, 16, 1>(ta, tb, epi, s, P, D, batch);
   else launch_tile<64, 64, 16, 1>(ta, tb, epi, s, P, D, batch);
   return 0;
