@@ -816,8 +816,16 @@ class AIRModel:
         # k-ordered chain as the per-head sum
         if w1_done is not None:
             torch.cuda.current_stream().wait_event(w1_done)
-        gemm([ws.dhid], [self._w1cat()], [ws.dh], TB, H, 5 * HS, 5 * HS, 5 * HS, H,
-             transB=True)
+        if B < self.SIDE_MIN_BATCH and HS % 16 == 0:
+            # small batch: the same chain as five k-segments read from the
+            # heads' own W1 (no concatenation launch per step)
+            dhid = ws.dhid.view(TB, 5 * HS)
+            ops.gemm_kseg([dhid[:, z * HS:] for z in range(5)],
+                          [self._P(h + "/hidden/weights") for h in self._HEADS], ws.dh, TB, H,
+                          HS, 5 * HS, HS, H, transB=True)
+        else:
+            gemm([ws.dhid], [self._w1cat()], [ws.dh], TB, H, 5 * HS, 5 * HS, 5 * HS, H,
+                 transB=True)
         heads_side = (self.grad_reducer is None and self.HEADS_WGRAD_SIDE
                       and B >= self.SIDE_MIN_BATCH)
         if heads_side:
@@ -1588,6 +1596,7 @@ class AIRModel:
     _graph_noise = False  # eps_x filled into its buffer (graph mode)
     _graph_mode = False   # inside train_step_graphed (eager first step, capture, replay)
     _prior_dev = None     # device z_pres prior log-odds (graph mode only)
+    _prior_dev_val = None  # the value last written there
     _graph = None
     _graph_ws = None      # the workspace the graph was captured on (its pointers)
 
@@ -1626,7 +1635,8 @@ class AIRModel:
             self._graph = self._graph_ws = None
             if self._prior_dev is None:
                 self._prior_dev = torch.zeros(1, device=self.device)
-            self._prior_dev.fill_(self.hyper("z_pres_prior_log_odds"))
+            self._prior_dev_val = float(self.hyper("z_pres_prior_log_odds"))
+            self._prior_dev.fill_(self._prior_dev_val)
             self.train_step_async(X, tg, global_batch=global_batch)  # this call's step
             self._capture(X, tg, global_batch)
             self._graph_key = key
@@ -1644,7 +1654,10 @@ class AIRModel:
         if ws.noise_side:  # the graph's first launch reads it
             torch.cuda.current_stream().wait_stream(self._side_stream())
             ws.noise_side = False
-        self._prior_dev.fill_(self.hyper("z_pres_prior_log_odds"))
+        lo = float(self.hyper("z_pres_prior_log_odds"))
+        if lo != self._prior_dev_val:  # (a fill launch only when the value moves)
+            self._prior_dev.fill_(lo)
+            self._prior_dev_val = lo
         self._graph.replay()
         self.params.apply_adam(self.hyper("learning_rate"), self.gradient_clipping_norm)
         self.params.global_step += 1
