@@ -975,6 +975,11 @@ class AIRModel:
         return self.W2, R1, R2, self.vae_latent_dimensions, G1, G2
 
     def _vae_forward_fp32(self, X, ws, t, lik_std):
+        self._vae_encoder_fp32(X, ws, t)
+        self._vae_decoder_fp32(ws, lik_std, t, t + 1)
+
+    def _vae_encoder_fp32(self, X, ws, t):
+        """STN read -> recognition layers -> z sample of loop step t."""
         B, W = ws.B, self.windows_size
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
@@ -988,13 +993,22 @@ class AIRModel:
              [ws.mu[t], ws.lv[t]], B, Z, R2, R2, Z, Z,
              bias=[vb["rec_mean"], vb["rec_log_variance"]])
         self._vae_sample_fwd(ws, t, None, 0)
-        gemm([ws.z[t]], [vw["generative_1"]], [ws.d1[t]], B, G1, Z, Z, G1, G1,
+
+    def _vae_decoder_fp32(self, ws, lik_std, t0, t1):
+        """Generative layers of loop steps [t0, t1) over their rows at once
+        (rows are independent: the same chains as step by step)."""
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        n = (t1 - t0) * ws.B
+        v = lambda a: a[t0:t1].reshape(n, -1)  # noqa: E731
+        vw = {k: self._P("vae/" + k + "/weights") for k in self._VAE[4:]}
+        vb = {k: self._P("vae/" + k + "/biases") for k in self._VAE[4:]}
+        gemm([v(ws.z)], [vw["generative_1"]], [v(ws.d1)], n, G1, Z, Z, G1, G1,
              epi=EPI_SOFTPLUS, bias=[vb["generative_1"]])
-        gemm([ws.d1[t]], [vw["generative_2"]], [ws.d2[t]], B, G2, G1, G1, G2, G2,
+        gemm([v(ws.d1)], [vw["generative_2"]], [v(ws.d2)], n, G2, G1, G1, G2, G2,
              epi=EPI_SOFTPLUS, bias=[vb["generative_2"]])
-        gemm([ws.d2[t]], [vw["gen_mean"]], [ws.r[t]], B, W2, G2, G2, W2, W2,
+        gemm([v(ws.d2)], [vw["gen_mean"]], [v(ws.r)], n, W2, G2, G2, W2, W2,
              epi=EPI_SIGMOID_NOISE, bias=[vb["gen_mean"]],
-             aux=[ws.eps_x[t]], ldaux=W2, aux_scale=lik_std)
+             aux=[v(ws.eps_x)], ldaux=W2, aux_scale=lik_std)
 
     def _vae_sample_fwd(self, ws, t, zb, ldzb):
         _ops.vae_sample_forward_(ws.B, self.vae_latent_dimensions, float(self.vae_prior_mean),

@@ -410,11 +410,28 @@ class AIRModel(_AirBase):
                 continue
             if self.precision == "bf16":
                 self._vae_forward_bf16(X, ws, t, lik_std)
+            elif self.DEFER_DECODER:
+                # only z feeds the recurrence: the generative half waits
+                self._vae_encoder_fp32(X, ws, t)
+                continue
             else:
                 self._vae_forward_fp32(X, ws, t, lik_std)
             ops.stn_forward(ws.r[t], ws.th_b[t], (C, C), out=ws.canvas, z=ws.zval[t],
                             mask=ws.zmask[t], accumulate=True)
+        if (self.precision == "fp32" and self.DEFER_DECODER and not self.fused_step
+                and not self._f32_parts(B)):
+            # the decoder of every step over T*B rows in one set of launches,
+            # then the canvas accumulated in step order (the same bits)
+            self._vae_decoder_fp32(ws, lik_std, 0, T)
+            for t in range(T):
+                ops.stn_forward(ws.r[t], ws.th_b[t], (C, C), out=ws.canvas, z=ws.zval[t],
+                                mask=ws.zmask[t], accumulate=True)
         self._forward_loss(X, targets, ws, need_grad, outputs)
+
+    # fp32 below FUSED_F32_MIN_ROWS: the generative half of each step's VAE
+    # (which feeds only the canvas, never the loop) after the loop, over T*B
+    # rows (MOG_ASR_DEFER_DECODER=0: inside the loop, step by step)
+    DEFER_DECODER = os.environ.get("MOG_ASR_DEFER_DECODER", "1") == "1"
 
     def _forward_loss(self, X, targets, ws, need_grad, outputs=True):
         """elbo (:917-935, recon :937-962) + pr_loss + element + margin
