@@ -218,6 +218,22 @@ int mog_air_step_backward(int B, int HS, int train, int use_num_prior, float tem
                           const float* dtheta_back, const float* dot, const float* const* hid,
                           const float* const* w2, float* dout, long dout_hs, float* dhid,
                           long dhid_hs, const float* prior_lo_dev, void* stream);
+/* The same over `steps` loop steps in one launch (AIR's reversed loop: every
+ * input of a step's head backward is final before the loop -- the STN
+ * backwards run over all T*B rows first): rows b = t * B + i, the records of
+ * step t at rec + t * 17 * B ([T][17][B], as the forward writes them), dloss
+ * per image i, every other operand over the steps * B rows back to back.
+ * prior_bias is one value for all steps (no per-step marginal).  Bits of
+ * `steps` single-step calls. */
+int mog_air_step_backward_steps(int steps, int B, int HS, int train, int use_num_prior,
+                                float temperature, float prior_lo, float prior_bias, float s_pm,
+                                float s_pv, float h_pm, float h_pv, float grad_scale,
+                                const float* dloss, const float* rec, const float* eps_scale,
+                                const float* eps_shift, const float* dtheta_fwd,
+                                const float* dtheta_back, const float* dot,
+                                const float* const* hid, const float* const* w2, float* dout,
+                                long dout_hs, float* dhid, long dhid_hs, const float* prior_lo_dev,
+                                void* stream);
 
 /* ---- VAE latent sample + KL (air/vae.py:27-30, air_model.py:718-736) ----
  * z_bf16 (may be NULL): bf16 copy of z with row stride ld_zb (GEMM operand).

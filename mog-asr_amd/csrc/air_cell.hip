@@ -333,21 +333,24 @@ struct StepBwdIO {
   const float* dloss;       // [B] per-image cotangent of the running loss (or null: grad_scale)
   float* dout;              // [5][B, 2] grads wrt head outputs, head stride dout_hs
   long dout_hs;
+  int steps;                // loop steps in one launch: rows b = t * B + i, records of
+                            // step t at rec + t * R_NREC * B, the rest [steps * B] rows
 };
 
 __global__ __launch_bounds__(256) void step_bwd_kernel(StepCfg cfg, StepBwdIO io) {
   const int b = blockIdx.x * 256 + threadIdx.x;
   const int B = cfg.B;
-  if (b >= B) return;
-  const float* r = io.rec;
-  const float sm = r[R_SM * B + b], slv = r[R_SLV * B + b];
-  const float hm0 = r[R_HM0 * B + b], hm1 = r[R_HM1 * B + b];
-  const float hv0 = r[R_HLV0 * B + b], hv1 = r[R_HLV1 * B + b];
-  const float lo = r[R_LO * B + b], s = r[R_S * B + b], tx = r[R_TX * B + b];
-  const float ty = r[R_TY * B + b], y = r[R_Y * B + b], z = r[R_Z * B + b];
-  const bool act_old = r[R_ACT_OLD * B + b] != 0.0f, act = r[R_ACT * B + b] != 0.0f;
-  const bool live = r[R_LIVE * B + b] != 0.0f;
-  const float gL = io.dloss ? io.dloss[b] : cfg.grad_scale;
+  if (b >= B * io.steps) return;
+  const int st = b / B, bi = b - st * B;  // loop step, image
+  const float* r = io.rec + (size_t)st * R_NREC * B;  // step st's records
+  const float sm = r[R_SM * B + bi], slv = r[R_SLV * B + bi];
+  const float hm0 = r[R_HM0 * B + bi], hm1 = r[R_HM1 * B + bi];
+  const float hv0 = r[R_HLV0 * B + bi], hv1 = r[R_HLV1 * B + bi];
+  const float lo = r[R_LO * B + bi], s = r[R_S * B + bi], tx = r[R_TX * B + bi];
+  const float ty = r[R_TY * B + bi], y = r[R_Y * B + bi], z = r[R_Z * B + bi];
+  const bool act_old = r[R_ACT_OLD * B + bi] != 0.0f, act = r[R_ACT * B + bi] != 0.0f;
+  const bool live = r[R_LIVE * B + bi] != 0.0f;
+  const float gL = io.dloss ? io.dloss[bi] : cfg.grad_scale;
   const float T = cfg.temperature;
 
   // theta gradients -> (s, tx, ty)
@@ -819,6 +822,14 @@ extern "C" int mog_air_step_forward(
   MOG_LAUNCH_RET();
 }
 
+extern "C" int mog_air_step_backward_steps(
+    int steps, int B, int HS, int train, int use_num_prior, float temperature, float prior_lo,
+    float prior_bias, float s_pm, float s_pv, float h_pm, float h_pv, float grad_scale,
+    const float* dloss, const float* rec, const float* eps_scale, const float* eps_shift,
+    const float* dtheta_fwd, const float* dtheta_back, const float* dot, const float* const* hid,
+    const float* const* w2, float* dout, long dout_hs, float* dhid, long dhid_hs,
+    const float* prior_lo_dev, void* stream);
+
 extern "C" int mog_air_step_backward(int B, int HS, int train, int use_num_prior,
                                      float temperature, float prior_lo, float prior_bias,
                                      float s_pm, float s_pv, float h_pm, float h_pv,
@@ -829,17 +840,33 @@ extern "C" int mog_air_step_backward(int B, int HS, int train, int use_num_prior
                                      const float* const* hid, const float* const* w2,
                                      float* dout, long dout_hs, float* dhid, long dhid_hs,
                                      const float* prior_lo_dev, void* stream) {
-  MOG_CHECK_ARG(B >= 0 && rec && eps_scale && eps_shift && dtheta_fwd && dtheta_back && dot);
+  return mog_air_step_backward_steps(1, B, HS, train, use_num_prior, temperature, prior_lo,
+                                     prior_bias, s_pm, s_pv, h_pm, h_pv, grad_scale, dloss, rec,
+                                     eps_scale, eps_shift, dtheta_fwd, dtheta_back, dot, hid, w2,
+                                     dout, dout_hs, dhid, dhid_hs, prior_lo_dev, stream);
+}
+
+extern "C" int mog_air_step_backward_steps(
+    int steps, int B, int HS, int train, int use_num_prior, float temperature, float prior_lo,
+    float prior_bias, float s_pm, float s_pv, float h_pm, float h_pv, float grad_scale,
+    const float* dloss, const float* rec, const float* eps_scale, const float* eps_shift,
+    const float* dtheta_fwd, const float* dtheta_back, const float* dot, const float* const* hid,
+    const float* const* w2, float* dout, long dout_hs, float* dhid, long dhid_hs,
+    const float* prior_lo_dev, void* stream) {
+  MOG_CHECK_ARG(steps >= 1 && B >= 0 && rec && eps_scale && eps_shift && dtheta_fwd &&
+                dtheta_back && dot);
   MOG_CHECK_ARG(hid && w2 && dout && dhid);
   if (B == 0) return 0;
+  const int rows = steps * B;  // the head-hidden kernels see the steps as one batch
   StepCfg c;
   c.B = B; c.H = 0; c.HS = HS; c.HZ = HS; c.train = train; c.use_num_prior = use_num_prior;
   c.step = 0; c.thr = 0.0f; c.temperature = temperature; c.prior_lo = prior_lo;
   c.prior_bias = prior_bias; c.s_pm = s_pm; c.s_pv = s_pv; c.s_plv = 0.0f; c.h_pm = h_pm;
   c.h_pv = h_pv; c.h_plv = 0.0f; c.grad_scale = grad_scale; c.prior_lo_dev = prior_lo_dev;
-  StepBwdIO io{rec, eps_scale, eps_shift, dtheta_fwd, dtheta_back, dot, dloss, dout, dout_hs};
+  StepBwdIO io{rec, eps_scale, eps_shift, dtheta_fwd, dtheta_back, dot, dloss, dout, dout_hs,
+               steps};
   hipStream_t s = mog_stream(stream);
-  step_bwd_kernel<<<mog_cdiv(B, 256), 256, 0, s>>>(c, io);
+  step_bwd_kernel<<<mog_cdiv(rows, 256), 256, 0, s>>>(c, io);
   HeadPtrs hp;
   for (int i = 0; i < 5; ++i) {
     MOG_CHECK_ARG(hid[i] && w2[i]);
@@ -848,11 +875,11 @@ extern "C" int mog_air_step_backward(int B, int HS, int train, int use_num_prior
   bool vec = HS % 4 == 0 && (dhid_hs % 4) == 0 && (reinterpret_cast<uintptr_t>(dhid) & 15) == 0;
   for (int i = 0; i < 5; ++i) vec = vec && (reinterpret_cast<uintptr_t>(hid[i]) & 15) == 0;
   if (vec)
-    heads_hidden_bwd4_kernel<<<dim3(mog_cdiv((long)B * (HS / 4), 256), 5), 256, 0, s>>>(
-        hp, dout, dout_hs, dhid, dhid_hs, B, HS);
+    heads_hidden_bwd4_kernel<<<dim3(mog_cdiv((long)rows * (HS / 4), 256), 5), 256, 0, s>>>(
+        hp, dout, dout_hs, dhid, dhid_hs, rows, HS);
   else
-    heads_hidden_bwd_kernel<<<mog_cdiv(5L * B * HS, 256), 256, 0, s>>>(hp, dout, dout_hs, dhid,
-                                                                        dhid_hs, B, HS);
+    heads_hidden_bwd_kernel<<<mog_cdiv(5L * rows * HS, 256), 256, 0, s>>>(hp, dout, dout_hs, dhid,
+                                                                           dhid_hs, rows, HS);
   MOG_LAUNCH_RET();
 }
 

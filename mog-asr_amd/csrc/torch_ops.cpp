@@ -419,25 +419,27 @@ void air_step_backward_(int64_t B, int64_t HS, bool train, bool use_num_prior,
                         const Tensor& eps_shift, const Tensor& dtheta_fwd,
                         const Tensor& dtheta_back, const Tensor& dot, at::TensorList hid,
                         at::TensorList w2, Tensor dout, int64_t dout_hs, Tensor dhid,
-                        int64_t dhid_hs, const optional<Tensor>& prior_lo_dev) {
+                        int64_t dhid_hs, const optional<Tensor>& prior_lo_dev, int64_t steps) {
   Op o("air_step_backward_");
   TORCH_CHECK(hid.size() == 5 && w2.size() == 5, o.name, ": 5 heads");
-  float* pdo = o.f(dout, 4 * dout_hs + 2 * B, "dout");
-  float* pdh = o.f(dhid, dhid_hs == HS ? 5 * B * HS : 4 * dhid_hs + B * HS, "dhid");
-  auto h = o.list(hid, F32, B * HS, "hid"), w = o.list(w2, F32, HS, "w2");
+  TORCH_CHECK(steps >= 1, o.name, ": steps >= 1");
+  const int64_t R = steps * B;  // rows of all the launch's steps
+  float* pdo = o.f(dout, 4 * dout_hs + 2 * R, "dout");
+  float* pdh = o.f(dhid, dhid_hs == HS ? 5 * R * HS : 4 * dhid_hs + R * HS, "dhid");
+  auto h = o.list(hid, F32, R * HS, "hid"), w = o.list(w2, F32, HS, "w2");
   float* pl = o.f(dloss, B, "dloss");
-  float* pr = o.f(rec, 17 * B, "rec");
-  float* pes = o.f(eps_scale, B, "eps_scale");
-  float* peh = o.f(eps_shift, 2 * B, "eps_shift");
-  float* ptf = o.f(dtheta_fwd, 6 * B, "dtheta_fwd");
-  float* ptb = o.f(dtheta_back, 6 * B, "dtheta_back");
-  float* pd = o.f(dot, B, "dot");
+  float* pr = o.f(rec, 17 * R, "rec");
+  float* pes = o.f(eps_scale, R, "eps_scale");
+  float* peh = o.f(eps_shift, 2 * R, "eps_shift");
+  float* ptf = o.f(dtheta_fwd, 6 * R, "dtheta_fwd");
+  float* ptb = o.f(dtheta_back, 6 * R, "dtheta_back");
+  float* pd = o.f(dot, R, "dot");
   float* pplo = o.f(prior_lo_dev, 1, "prior_lo_dev");
   GUARD(o);
-  check(mog_air_step_backward(B, HS, train, use_num_prior, temperature, prior_lo, prior_bias, s_pm,
-                              s_pv, h_pm, h_pv, grad_scale, pl, pr, pes, peh, ptf, ptb, pd,
-                              arr<float>(h), arr<float>(w), pdo, dout_hs, pdh, dhid_hs, pplo,
-                              o.stream()),
+  check(mog_air_step_backward_steps(steps, B, HS, train, use_num_prior, temperature, prior_lo,
+                                    prior_bias, s_pm, s_pv, h_pm, h_pv, grad_scale, pl, pr, pes,
+                                    peh, ptf, ptb, pd, arr<float>(h), arr<float>(w), pdo, dout_hs,
+                                    pdh, dhid_hs, pplo, o.stream()),
         o.name);
 }
 
@@ -1102,7 +1104,8 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "float prior_lo, float prior_bias, float s_pm, float s_pv, float h_pm, float h_pv, "
       "float grad_scale, Tensor? dloss, Tensor rec, Tensor eps_scale, Tensor eps_shift, "
       "Tensor dtheta_fwd, Tensor dtheta_back, Tensor dot, Tensor[] hid, Tensor[] w2, "
-      "Tensor(a!) dout, int dout_hs, Tensor(b!) dhid, int dhid_hs, Tensor? prior_lo_dev=None) -> ()");
+      "Tensor(a!) dout, int dout_hs, Tensor(b!) dhid, int dhid_hs, Tensor? prior_lo_dev=None, "
+      "int steps=1) -> ()");
   m.def(
       "generation_prior_(int G, int Z, float s_pm, float s_plv, float h_pm, float h_plv, "
       "float v_pm, float v_plv, Tensor eps_scale, Tensor eps_shift, Tensor eps_z, "

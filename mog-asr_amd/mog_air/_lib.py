@@ -46,6 +46,8 @@ _SIGS = {
                              P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "mog_air_step_backward": [I, I, I, I, F, F, F, F, F, F, F, F, P, P, P, P, P, P, P, P, P,
                               P, L, P, L, P],
+    "mog_air_step_backward_steps": [I, I, I, I, I, F, F, F, F, F, F, F, F, P, P, P, P, P, P, P,
+                                    P, P, P, L, P, L, P],
     "mog_vae_sample_forward": [I, I, F, F, F, P, P, P, P, P, I, P, P, P, P],
     "mog_stn_vae_step_forward": ([I] * 8 + [P] * 7 + [I, ULL, ULL] + [P] * 2 + [F] * 4 + [P] * 14
                                  + [I, P]),

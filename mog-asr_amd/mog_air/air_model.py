@@ -801,7 +801,17 @@ class AIRModel:
         with self._timed("stn_read_bwd", self._stn_bwd_work(TB, write=False)):
             ops.stn_backward(X, ws.th_f, (W, W), ws.dg_all, want_dU=False, dtheta=ws.dth_f_all,
                              n=TB)
-        for t in range(T):
+        if self.marginal is None:
+            # every step's inputs are final here (the STN backwards ran over
+            # all T*B rows above): the T steps' head backward in one launch
+            _ops.air_step_backward_(
+                B, HS, self.train, False, temperature, prior_lo, 0.0,
+                float(self.scale_prior_mean), float(self.scale_prior_variance),
+                float(self.shift_prior_mean), float(self.shift_prior_variance), float(gscale),
+                None, ws.rec, ws.eps_scale, ws.eps_shift, ws.dth_f_all, ws.dth_b_all, ws.dot_all,
+                [ws.hid[z] for z in range(5)], w2, ws.dout[0], T * B * 2, ws.dhid, HS,
+                self._prior_arg(), T)
+        for t in range(T if self.marginal is not None else 0):
             hid_t = [ws.hid[z, t] for z in range(5)]
             _ops.air_step_backward_(
                 B, HS, self.train, self.marginal is not None, temperature, prior_lo,

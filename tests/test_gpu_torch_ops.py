@@ -621,3 +621,40 @@ def test_air_step_backward_per_image_dloss():
         uni = run(v, None)
         for a, b in zip(mix, uni):
             np.testing.assert_array_equal(a[:, rows], b[:, rows])
+
+
+def test_air_step_backward_steps_match_single_steps_bitwise():
+    """air_step_backward_ over T loop steps in one launch (steps=T: records
+    [T][17][B], the other operands over T*B rows, the dloss per image) writes
+    exactly what T single-step launches write."""
+    T_ = 3
+    steps = [_air_step_inputs(21 + t) for t in range(T_)]
+    refs = [_step_c_abi(*ins, _STEP_CFG, False) for ins in steps]
+    B, HS = steps[0][0].shape[0], steps[0][1][0].shape[1]
+    W2 = steps[0][3]
+    rng = np.random.default_rng(22)
+
+    def rn(*s):
+        return torch.tensor(rng.standard_normal(s).astype(np.float32), device=DEV)
+
+    Gf, Gb, Gz = rn(T_, B, 6), rn(T_, B, 6), rn(T_, B)
+    es = torch.stack([ins[5] for ins in steps])
+    eh = torch.stack([ins[6] for ins in steps])
+    rec = torch.stack([r["rec"] for r in refs]).contiguous()
+    hid = [torch.stack([r["hid"][z] for r in refs]).contiguous() for z in range(5)]
+    dl = torch.tensor(rng.uniform(0.5, 2.0, B).astype(np.float32), device=DEV)
+    thr, tmp, plo, pb, s_pm, s_pv, s_plv, h_pm, h_pv, h_plv = _STEP_CFG
+    for dloss in (None, dl):
+        d1, h1 = torch.empty((5, T_, B, 2), device=DEV), torch.empty((T_, B, 5 * HS), device=DEV)
+        for t in range(T_):
+            torch.ops.mog_air.air_step_backward_(
+                B, HS, True, False, tmp, plo, 0.0, s_pm, s_pv, h_pm, h_pv, 1.0 / B, dloss, rec[t],
+                es[t], eh[t], Gf[t], Gb[t], Gz[t], [x[t] for x in hid], W2, d1[0, t], T_ * B * 2,
+                h1[t], HS)
+        d2, h2 = torch.empty_like(d1), torch.empty_like(h1)
+        torch.ops.mog_air.air_step_backward_(
+            B, HS, True, False, tmp, plo, 0.0, s_pm, s_pv, h_pm, h_pv, 1.0 / B, dloss, rec, es, eh,
+            Gf, Gb, Gz, hid, W2, d2[0], T_ * B * 2, h2, HS, None, T_)
+        torch.cuda.synchronize()
+        assert torch.equal(d1, d2) and torch.equal(h1, h2)
+        assert float(h2.abs().sum()) > 0
