@@ -135,6 +135,12 @@ int mog_gemm_f32_kseg_group(int nprob, const int* nseg, const float* const* A,
 int mog_stn_forward(const float* U, int N, int Hin, int Win, const float* theta, int Hout,
                     int Wout, void* out, const float* z, const float* mask, int mode,
                     void* stream);
+/* The same with image n reading U[n % u_period] (u_period > 0; 0: U[n]):
+ * every loop step's glimpse read of AIR's shared input canvas in one launch
+ * (N = T * B, u_period = B). */
+int mog_stn_forward_periodic(const float* U, int u_period, int N, int Hin, int Win,
+                             const float* theta, int Hout, int Wout, void* out, const float* z,
+                             const float* mask, int mode, void* stream);
 /* STN write of N images into per-image canvas parts (mode-1 semantics without
  * the read-modify-write): parts[n] = mask[n] ? z[n] * STN(U[n], theta[n]) : 0,
  * stored only on the rows part_rows[n] = lo | hi << 16 (even bounds; rows

@@ -56,7 +56,8 @@ __global__ __launch_bounds__(256) void stn_fwd_kernel(const float* __restrict__ 
                                                       int Win, const float* __restrict__ theta,
                                                       int Hout, int Wout, void* outv,
                                                       const float* __restrict__ z,
-                                                      const float* __restrict__ mask) {
+                                                      const float* __restrict__ mask,
+                                                      int u_period) {
 #pragma clang fp contract(off)
   const int n = blockIdx.x;
   const int P = Hout * Wout;
@@ -64,7 +65,7 @@ __global__ __launch_bounds__(256) void stn_fwd_kernel(const float* __restrict__ 
   float th[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) th[k] = theta[n * 6 + k];
-  const float* Un = U + (size_t)n * Hin * Win;
+  const float* Un = U + (size_t)(u_period > 0 ? n % u_period : n) * Hin * Win;
   const float zn = MODE == 1 ? z[n] : 0.0f;
   const RowMap rm = row_map(Wout);
   const int w = threadIdx.x >> 6;
@@ -795,20 +796,30 @@ extern "C" int mog_stn_write_parts(const float* U, int N, int Hin, int Win, cons
 }
 
 // transformer(U, theta, out_size) forward; see include/mog_air.h
-extern "C" int mog_stn_forward(const float* U, int N, int Hin, int Win, const float* theta,
-                               int Hout, int Wout, void* out, const float* z,
-                               const float* mask, int mode, void* stream) {
+extern "C" int mog_stn_forward_periodic(const float* U, int u_period, int N, int Hin, int Win,
+                                        const float* theta, int Hout, int Wout, void* out,
+                                        const float* z, const float* mask, int mode,
+                                        void* stream) {
   MOG_CHECK_ARG(U && theta && out && N >= 0 && Hin > 0 && Win > 0 && Hout > 0 && Wout > 0);
-  MOG_CHECK_ARG(mode >= 0 && mode <= 2 && (mode != 1 || (z && mask)));
+  MOG_CHECK_ARG(mode >= 0 && mode <= 2 && (mode != 1 || (z && mask)) && u_period >= 0);
   if (N == 0) return 0;
   hipStream_t s = mog_stream(stream);
   if (mode == 1)
-    stn_fwd_kernel<1><<<N, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, z, mask);
+    stn_fwd_kernel<1><<<N, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, z, mask, u_period);
   else if (mode == 2)
-    stn_fwd_kernel<2><<<N, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, nullptr, nullptr);
+    stn_fwd_kernel<2><<<N, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, nullptr, nullptr,
+                                        u_period);
   else
-    stn_fwd_kernel<0><<<N, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, nullptr, nullptr);
+    stn_fwd_kernel<0><<<N, 256, 0, s>>>(U, Hin, Win, theta, Hout, Wout, out, nullptr, nullptr,
+                                        u_period);
   MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_stn_forward(const float* U, int N, int Hin, int Win, const float* theta,
+                               int Hout, int Wout, void* out, const float* z,
+                               const float* mask, int mode, void* stream) {
+  return mog_stn_forward_periodic(U, 0, N, Hin, Win, theta, Hout, Wout, out, z, mask, mode,
+                                  stream);
 }
 
 static int stn_backward_launch(const float* U, int N, int Hin, int Win, const float* theta,

@@ -233,15 +233,18 @@ void cvt_bf16_batch_(at::TensorList src, at::TensorList dst, at::IntArrayRef dim
 // ------------------------------------------------------------------ STN ----
 void stn_forward_(const Tensor& U, int64_t N, int64_t Hin, int64_t Win, const Tensor& theta,
                   int64_t Hout, int64_t Wout, Tensor out, const optional<Tensor>& z,
-                  const optional<Tensor>& mask, int64_t mode) {
+                  const optional<Tensor>& mask, int64_t mode, int64_t u_period) {
   Op o("stn_forward_");
+  TORCH_CHECK(u_period >= 0, o.name, ": u_period >= 0");
   void* po = o.need(out, mode == 2 ? BF16 : F32, N * Hout * Wout, "out");
-  float* pu = o.f(U, N * Hin * Win, "U");
+  float* pu = o.f(U, (u_period > 0 ? std::min(u_period, N) : N) * Hin * Win, "U");
   float* pt = o.f(theta, N * 6, "theta");
   float* pz = o.f(z, N, "z");
   float* pm = o.f(mask, N, "mask");
   GUARD(o);
-  check(mog_stn_forward(pu, N, Hin, Win, pt, Hout, Wout, po, pz, pm, mode, o.stream()), o.name);
+  check(mog_stn_forward_periodic(pu, u_period, N, Hin, Win, pt, Hout, Wout, po, pz, pm, mode,
+                                 o.stream()),
+        o.name);
 }
 
 void stn_backward_(const Tensor& U, int64_t N, int64_t Hin, int64_t Win, const Tensor& theta,
@@ -1067,7 +1070,7 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
   m.def("cvt_bf16_batch_(Tensor[] src, Tensor(a!)[] dst, int[] dims) -> ()");
   m.def(
       "stn_forward_(Tensor U, int N, int Hin, int Win, Tensor theta, int Hout, int Wout, "
-      "Tensor(a!) out, Tensor? z, Tensor? mask, int mode) -> ()");
+      "Tensor(a!) out, Tensor? z, Tensor? mask, int mode, int u_period=0) -> ()");
   m.def(
       "stn_backward_(Tensor U, int N, int Hin, int Win, Tensor theta, int Hout, int Wout, "
       "Tensor G, Tensor? gscale, Tensor(a!)? dU, Tensor(b!)? dtheta, Tensor(c!)? dot, "

@@ -34,6 +34,7 @@ _SIGS = {
     "mog_gemm_x3_nt": [P, P, L, P, P, I, I, I, I, I, I, I, I, P],
     "mog_gemm_f32_sigmoid_philox": [P, P, P, P, I, I, I, I, I, I, F, ULL, ULL, P],
     "mog_stn_forward": [P, I, I, I, P, I, I, P, P, P, I, P],
+    "mog_stn_forward_periodic": [P, I, I, I, I, P, I, I, P, P, P, I, P],
     "mog_stn_backward": [P, I, I, I, P, I, I, P, P, P, P, P, I, I, P],
     "mog_stn_backward_sigmoid_bf16": [P, I, I, I, P, I, I, P, P, P, P, P, I, I, P],
     "mog_stn_backward_sigmoid_f32": [P, I, I, I, P, I, I, P, P, P, P, P, I, I, P],

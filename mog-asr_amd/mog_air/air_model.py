@@ -622,8 +622,8 @@ class AIRModel:
             Zp = self._pad8(Z)
             self._pack_bf16()
             wt = self._wt
-            for t in range(t0, t1):
-                ops.stn_forward(X, ws.th_f[t], (W, W), out=ws.gb[t])
+            # every step's glimpse read of the shared input canvas in one launch
+            ops.stn_forward(X, v(ws.th_f), (W, W), out=v(ws.gb), n=TB)
             gemm_bf16([v(ws.gb)], [wt["recognition_1"]], [v(ws.a1b)], TB, R1, W2, W2, W2, R1,
                       epi=BF_SOFTPLUS, bias=[vb["recognition_1"]])
             gemm_bf16([v(ws.a1b)], [wt["recognition_2"]], [v(ws.a2b)], TB, R2, R1, R1, R1, R2,
@@ -641,8 +641,7 @@ class AIRModel:
                       aux_scale=lik_std)
         else:
             vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
-            for t in range(t0, t1):
-                ops.stn_forward(X, ws.th_f[t], (W, W), out=ws.g[t])
+            ops.stn_forward(X, v(ws.th_f), (W, W), out=v(ws.g), n=TB)
             gemm([v(ws.g)], [vw["recognition_1"]], [v(ws.a1)], TB, R1, W2, W2, R1, R1,
                  epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]])
             gemm([v(ws.a1)], [vw["recognition_2"]], [v(ws.a2)], TB, R2, R1, R1, R2, R2,

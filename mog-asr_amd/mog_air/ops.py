@@ -188,12 +188,14 @@ def dense(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torc
 
 def stn_forward(U: torch.Tensor, theta: torch.Tensor, out_hw, out: Optional[torch.Tensor] = None,
                 z: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
-                accumulate: bool = False) -> torch.Tensor:
+                accumulate: bool = False, n: Optional[int] = None) -> torch.Tensor:
     """transformer() of air/transformer.py:18 for U [N,Hin,Win] (or [N,Hin*Win] with
-    Hin=Win) and theta [N,6].  A bf16 ``out`` receives the bf16 image."""
+    Hin=Win) and theta [N,6].  A bf16 ``out`` receives the bf16 image.  n > N:
+    n images, image i reading U[i % N] (every loop step's read of one canvas)."""
     _chk(U, "U")
     _chk(theta, "theta")
-    N = U.shape[0]
+    period = U.shape[0] if n is not None and n != U.shape[0] else 0
+    N = U.shape[0] if n is None else n
     if U.dim() == 3:
         Hin, Win = U.shape[1], U.shape[2]
     else:
@@ -210,7 +212,7 @@ def stn_forward(U: torch.Tensor, theta: torch.Tensor, out_hw, out: Optional[torc
         mode = 1
     else:
         mode = 2 if out.dtype == torch.bfloat16 else 0
-    _ops.stn_forward_(U, N, Hin, Win, theta, Ho, Wo, out, z, mask, mode)
+    _ops.stn_forward_(U, N, Hin, Win, theta, Ho, Wo, out, z, mask, mode, period)
     return out
 
 

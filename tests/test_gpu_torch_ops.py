@@ -658,3 +658,22 @@ def test_air_step_backward_steps_match_single_steps_bitwise():
         torch.cuda.synchronize()
         assert torch.equal(d1, d2) and torch.equal(h1, h2)
         assert float(h2.abs().sum()) > 0
+
+
+def test_stn_forward_periodic_matches_per_step_reads_bitwise():
+    """stn_forward with n = T*B images over a B-image U (image i reads U[i % B]:
+    every loop step's glimpse read of the shared canvas in one launch) writes
+    exactly what T reads of B images write, fp32 and bf16 outputs."""
+    from mog_air import ops as mops
+    rng = np.random.default_rng(31)
+    B, T_ = 37, 3
+    U = torch.tensor(rng.random((B, 2500)).astype(np.float32), device=DEV)
+    th = torch.tensor(np.concatenate([_theta(rng, B) for _ in range(T_)]), device=DEV).view(T_, B, 6)
+    for dt in (torch.float32, torch.bfloat16):
+        one = torch.empty((T_, B, 784), device=DEV, dtype=dt)
+        for t in range(T_):
+            mops.stn_forward(U, th[t], (28, 28), out=one[t])
+        allr = torch.empty_like(one)
+        mops.stn_forward(U, th.view(T_ * B, 6), (28, 28), out=allr.view(T_ * B, 784), n=T_ * B)
+        torch.cuda.synchronize()
+        assert torch.equal(one, allr)
