@@ -991,6 +991,20 @@ int launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, con
     launch_epi<32, 32, 32, 1, false, true, true>(epi, dim3(E.nx, E.ny, batch), s, P, E);
     return 0;
   }
+  // the NT form of a small batch off the LDS-DMA path (an operand off the
+  // 16-byte alignment, e.g. K = Z = 50: the latent layer's input gradient at the
+  // batch of 64): 32 x 32 x 32 tiles as above.  MOG_NT_SMALL=0 keeps 64 x 64 x 16.
+  static const char* nt_env = getenv("MOG_NT_SMALL");
+  if (D.kseg == 0 && !ta && tb && D.splitk == 1 && (nt_env == nullptr || atoi(nt_env) != 0) &&
+      (long)mog_cdiv(D.M, 64) * mog_cdiv(D.N, 64) * batch < 128) {
+    GemmDims E = D;
+    E.kchunk = ((E.K + 31) / 32) * 32;
+    if (E.kchunk == 0) E.kchunk = 32;
+    E.nx = mog_cdiv(E.N, 32);
+    E.ny = mog_cdiv(E.M, 32);
+    launch_epi<32, 32, 32, 1, false, true, false>(epi, dim3(E.nx, E.ny, batch), s, P, E);
+    return 0;
+  }
   if (b128) launch_tile<128, 128, 16, 1>(ta, tb, epi, s, P, D, batch);
   else launch_tile<64, 64, 16, 1>(ta, tb, epi, s, P, D, batch);
   return 0;
