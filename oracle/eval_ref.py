@@ -5,7 +5,9 @@ vectorised host implementation mog_air/evaluation.py.
 IoU_evaluation: evaluation_detection.py:5-25; evaluation: :28-98 (boxes
 :43-57, empty cases :66-74, thresholds 0.5 + 0.05 i :76-84, best IoUs
 :85-86, Hungarian global IoU :88-90).  Pinned by the known-answer cases in
-tests/test_pipeline.py (no golden vectors ship with the reference).
+tests/test_pipeline.py and, since round 6, by outputs of the reference
+module itself (tests/golden/eval_detection.npz, scripts/make_eval_golden.py,
+checked in tests/test_eval_golden.py).
 """
 import numpy as np
 from scipy.optimize import linear_sum_assignment
