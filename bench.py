@@ -65,7 +65,7 @@ KERNEL_NAMES = {
     "stn_vae_step_all": "stn_vae_step_kernel (fused bf16, all T steps' rows)",
     "stn_vae_step_f32_all": "stn_vae_step_f32_kernel (fused fp32 STN read + VAE + STN write)",
     "vae_wgrad_x3": "gemm_x3_tn_kernel<false,3>: VAE weight gradients, fp32 operands split "
-                    "in-kernel (bf16 cores)",
+                    "in-kernel (bf16 cores; priced on fp32 flops)",
     "vae_dgrad_x3": "gemm_x3_nt_kernel: VAE input gradients dY W^T (bf16 cores, 3-piece)",
     "vae_dgrad_f32": "gemm_f32 transB: VAE input gradients (fp32 chain)",
     "wgrad_f32": "gemm_f32 transA split-K: heads / small VAE weight gradients",
@@ -95,32 +95,47 @@ def kernel_work(name, B, precision, C2=2500, H=256, T=3):
     return None
 
 
-def pmc_traffic(tag):
+def pmc_field(tag, field):
+    """A field of profiles/pmc_summary.json's entry for `tag` (the rocprofv3
+    kernel-trace / PMC figures of the same kernel in the same workload)."""
     try:
         with open(PMC_SUMMARY) as f:
-            return json.load(f).get(tag, {}).get("hbm_bytes_per_launch")
+            return json.load(f).get(tag, {}).get(field)
     except (OSError, ValueError):
         return None
+
+
+def pmc_traffic(tag):
+    return pmc_field(tag, "hbm_bytes_per_launch")
 
 
 def roofline(events, B, precision):
     """The dominant kernel group of the timed step: every tagged launch
     (AIRModel._timed: one kernel launch each, on the stream it runs on, with
-    its algorithmic flops or bytes), grouped by tag; the group with the
-    largest total time is the line's roofline.  achieved = the group's
+    its algorithmic flops or bytes), grouped by tag.  achieved = the group's
     algorithmic work / its summed launch durations; peak: the fp32 or bf16
-    dense MFMA peak, or 8 TB/s of HBM.  Launches on the side streams share the
-    chip with the main stream's (their durations include that).  Every group
-    is listed under ``launches_priced``."""
+    dense MFMA peak, or 8 TB/s of HBM.  The fp32 gradients on the bf16 matrix
+    cores (three-piece splits, tag work ending in "x3") are priced on their
+    fp32 flops against the fp32 peak, with the six bf16 products they issue
+    against the bf16 peak beside it (``x3_bf16_products_frac``).
+
+    Only main-stream groups can be the line's roofline: a side-stream
+    launch's HIP events also count the time its first workgroups wait for
+    CUs that the main stream's kernel holds, so its event time is not its
+    kernel time (rocprofv3's kernel trace ranks the groups by kernel time;
+    DESIGN.md §4.9).  The largest main-stream total wins; every group,
+    side-stream ones flagged, is listed under ``launches_priced``."""
     rows = []
     for name, evs in events.items():
-        durs, amount, bound, peak_key = [], 0.0, None, None
-        for e0, e1, work in evs:
+        durs, amount, bound, peak_key, x3, side = [], 0.0, None, None, False, False
+        for e0, e1, work, on_side in evs:
             if work is None:
                 work = kernel_work(name, B, precision)
             if work is None:
                 continue
-            bound, a, peak_key = work
+            bound, a, peak_key = work[:3]
+            x3 = len(work) > 3 and work[3] == "x3"
+            side = side or on_side
             durs.append(e0.elapsed_time(e1) * 1e-3)  # seconds
             amount += a
         if not durs:
@@ -129,14 +144,18 @@ def roofline(events, B, precision):
         extra = {}
         if bound == "mfma":
             achieved, unit, peak = amount / total / 1e12, "TFLOP/s", PEAKS[peak_key]
+            if x3:
+                extra["x3_bf16_products_frac"] = 6.0 * achieved / BF16_MFMA_PEAK_TFLOPS
         else:
             achieved, unit, peak = amount / total / 1e9, "GB/s", HBM_PEAK_GBS
             extra["frac_of_measured_copy"] = achieved / copy_bandwidth(torch.device(
                 "cuda", torch.cuda.current_device()))
         rows.append({"kernel": name, "what": KERNEL_NAMES.get(name, name), "bound": bound,
+                     "stream": "side" if side else "main",
                      "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak,
                      **extra,
                      "traffic": pmc_traffic(f"{name}_{precision}_b{B}"),
+                     "profiled_avg_us": pmc_field(f"{name}_{precision}_b{B}", "profiled_avg_us"),
                      "launches": len(durs), "avg_launch_us": total / len(durs) * 1e6,
                      "total_us": total * 1e6,
                      "algorithmic_per_launch": amount / len(durs),
@@ -144,9 +163,11 @@ def roofline(events, B, precision):
     if not rows:
         return None
     rows.sort(key=lambda r: -r["total_us"])
-    out = dict(rows[0])
-    out["launches_priced"] = [{k: r[k] for k in ("kernel", "frac", "avg_launch_us", "total_us",
-                                                 "launches", "unit", "achieved")} for r in rows]
+    main = [r for r in rows if r["stream"] == "main"] or rows
+    out = dict(main[0])
+    out["launches_priced"] = [{k: r[k] for k in ("kernel", "stream", "frac", "avg_launch_us",
+                                                 "total_us", "launches", "unit", "achieved")}
+                              for r in rows]
     return out
 
 
@@ -336,6 +357,15 @@ def fused_step_roofline(batch: int, launches: int, dev, canvas: int = 50, save: 
            "algorithmic_bytes_per_image_step": per}
     if save:
         out["saved_activation_bytes_per_image_step"] = SAVED_BYTES
+    if canvas != 50:
+        # the kernel stores only the window rows of each canvas part, so the
+        # full-canvas read-modify-write of SURVEY §8 D.3 overstates its bytes
+        # (at C = 64 the priced rate exceeds a measured copy): priced on the
+        # bytes it moves (rocprofv3 FETCH + WRITE), or not at all
+        out["algorithmic_frac_not_a_roofline"] = out.pop("frac")
+        out.pop("frac_of_measured_copy")
+        out["frac"] = traffic / avg / 1e9 / HBM_PEAK_GBS if traffic else None
+        out["frac_basis"] = "actual HBM bytes (pmc_summary traffic) / launch time"
     del m, ws
     torch.cuda.empty_cache()
     return out

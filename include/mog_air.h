@@ -44,10 +44,10 @@ int mog_gemm_f32(int batch, const float* const* A, const float* const* B, float*
 /* fp32 weight gradient on the bf16 matrix cores (mog-asr_amd/csrc/gemm_x3.hip):
  * C[m][n] += sum_k A[k*lda+m] B[k*ldb+n] over `splitk` k-ranges, colsum[n] +=
  * sum_k B[k*ldb+n] when colsum != NULL.  Split-K partials: with `work` (>=
- * splitk * M * N floats) each range's product is stored there and a second
- * launch adds the ranges into C in a fixed order (deterministic; plain stores
- * instead of float atomics, which run at about 1.3 TB/s); work == NULL: float
- * atomics into C.  One k-range: C += product by a plain read-add-write.  Each fp32 operand is split
+ * splitk * M * N floats, + splitk * N with a colsum) each range's product and
+ * column sums are stored there and a second launch adds the ranges into C and
+ * colsum in a fixed order (deterministic; plain stores instead of float
+ * atomics, which run at about 1.3 TB/s); work == NULL: float atomics.  One k-range: C += product by a plain read-add-write.  Each fp32 operand is split
  * exactly into three bf16 pieces; the six products down to 2^-16 relative are
  * accumulated in fp32 (error of the order of one fp32 product rounding; not a
  * k-ordered chain, so tolerance-gated like every split-K gradient).  The x-part
@@ -483,16 +483,11 @@ int mog_rng_fill_batch(int nbuf, float* const* out, const long* n, unsigned long
 int mog_fill32_batch(int nbuf, void* const* dst, const long* n, const unsigned* value,
                      void* stream);
 
-/* ---- measurement / test instruments (no reference counterpart) ----------
+/* ---- measurement instrument (no reference counterpart) -------------------
  * dst[i] = src[i] for n4 float4s (16-byte aligned): the copy bandwidth the
- * bench quotes beside the HBM spec. */
+ * bench quotes beside the HBM spec.  (The test-only instruments mog_spin and
+ * mog_lds_poison live in libmog_air_test.so, include/mog_air_test.h.) */
 int mog_copy_f4(const float* src, float* dst, long n4, void* stream);
-/* One wave occupying `stream` for `ticks` of the 100 MHz wall clock (<= 1 s):
- * the stream-ordering tests hold one stream of a forked step back with it. */
-int mog_spin(long long ticks, void* stream);
-/* Fills the LDS of every CU with the 32-bit pattern `bits` (a NaN, say), so a
- * kernel launched next that reads LDS it did not write shows it. */
-int mog_lds_poison(unsigned bits, void* stream);
 
 #ifdef __cplusplus
 }

@@ -372,10 +372,10 @@ extern "C" int mog_gemm_bf16(int batch, const void* const* A, const void* const*
   D.nx = D.ny = 1;
   hipStream_t s = mog_stream(stream);
   // 128x128 only when it still gives >= 2 workgroups per CU (2 x 256 CUs);
-  // MOG_BF16_BIG_NT / MOG_BF16_BIG_TN override the workgroup threshold
+  // MOG_BF16_BIG_NT / MOG_BF16_BIG_TN (profiling build) override the threshold
   const long big = (long)mog_cdiv(M, 128) * mog_cdiv(N, 128) * batch * splitk;
   long thr = 512;
-  if (const char* e = getenv(tn ? "MOG_BF16_BIG_TN" : "MOG_BF16_BIG_NT")) thr = atol(e);
+  if (const char* e = mog_prof_env(tn ? "MOG_BF16_BIG_TN" : "MOG_BF16_BIG_NT")) thr = atol(e);
   if (M >= 128 && N >= 128 && big >= thr)
     launch_tile<128, 128>(tn != 0, epi, s, P, D, batch);
   else

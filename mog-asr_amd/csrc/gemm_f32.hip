@@ -899,11 +899,12 @@ int launch_dma(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, Gemm
 // remains for unaligned / K % 4 operands and K segments.  Measured and not
 // kept: BK = 32 (register staging -5..-25 %, LDS-DMA -3..-20 % on most
 // shapes), 128x64 / 64x128 tiles, a 3-stage register pipeline with fragment
-// prefetch (1 wave per SIMD at 128x128).  MOG_GEMM_TILE ("64" / "128")
-// forces a tile, MOG_GEMM_DMA=0 the register-staged kernel.
+// prefetch (1 wave per SIMD at 128x128).  Profiling build (mog_prof_env):
+// MOG_GEMM_TILE ("64" / "128") forces a tile, MOG_GEMM_DMA=0 the
+// register-staged kernel.
 int launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, const GemmDims& D,
                 int batch) {
-  static const char* force = getenv("MOG_GEMM_TILE");
+  static const char* force = mog_prof_env("MOG_GEMM_TILE");
   const long big = (long)mog_cdiv(D.M, 128) * mog_cdiv(D.N, 128) * batch * D.splitk;
   bool b128 = !ta && D.K >= 2048 && D.M >= 128 && D.N >= 128 && big >= 512;
   if (force != nullptr) b128 = atoi(force) == 128;
@@ -911,7 +912,7 @@ int launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, con
   // outside the k range and the operand's last row (K % 4 for k-contiguous
   // operands, M / N % 4 for row-contiguous ones); no K segments; the fused
   // bias-gradient column sum only from a row-contiguous B
-  static const char* dma_env = getenv("MOG_GEMM_DMA");
+  static const char* dma_env = mog_prof_env("MOG_GEMM_DMA");
   const bool dma = (dma_env == nullptr || atoi(dma_env) != 0) && D.kseg == 0 && D.vecA &&
                    D.vecB && (ta ? D.M % 4 == 0 : D.K % 4 == 0) &&
                    (tb ? D.K % 4 == 0 : D.N % 4 == 0) && !(tb && P.colsum[0] != nullptr);
@@ -952,12 +953,12 @@ int launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, con
     // faster for the weight gradients (transA, +1..6 %) and the transB input
     // gradients (dh +15 %), slower for the forward layers (recurrent -18 %,
     // T*B-row layers -2..5 %).  MOG_GEMM_BK=16|32 forces one depth.
-    static const char* bk_env = getenv("MOG_GEMM_BK");
+    static const char* bk_env = mog_prof_env("MOG_GEMM_BK");
     bool bk32 = ta || tb;
     if (bk_env != nullptr) bk32 = atoi(bk_env) == 32;
     if (bk32 && !b128) {
       // MOG_GEMM_NS=3|4: deeper 32-deep pipelines (48 / 64 KB per workgroup)
-      static const char* ns_env = getenv("MOG_GEMM_NS");
+      static const char* ns_env = mog_prof_env("MOG_GEMM_NS");
       const int ns = ns_env != nullptr ? atoi(ns_env) : 2;
       if (t12864) return launch_dma<128, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
       else if (ns == 4) return launch_dma<64, 64, 32, 4>(ta, tb, epi, s, P, D, batch);
@@ -980,7 +981,7 @@ int launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, con
   // workgroups, each a serial K = 64..320 chain): 32 x 32 tiles 32 deep --
   // four times the workgroups, half the barriers per k.  Same k order: same
   // bits.  MOG_KSEG_SMALL=0 keeps 64 x 64 x 16.
-  static const char* ks_env = getenv("MOG_KSEG_SMALL");
+  static const char* ks_env = mog_prof_env("MOG_KSEG_SMALL");
   if (D.kseg > 0 && !ta && tb && D.kseg % 32 == 0 && (ks_env == nullptr || atoi(ks_env) != 0) &&
       (long)mog_cdiv(D.M, 64) * mog_cdiv(D.N, 64) * batch < 128) {
     GemmDims E = D;
@@ -994,7 +995,7 @@ int launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, con
   // the NT form of a small batch off the LDS-DMA path (an operand off the
   // 16-byte alignment, e.g. K = Z = 50: the latent layer's input gradient at the
   // batch of 64): 32 x 32 x 32 tiles as above.  MOG_NT_SMALL=0 keeps 64 x 64 x 16.
-  static const char* nt_env = getenv("MOG_NT_SMALL");
+  static const char* nt_env = mog_prof_env("MOG_NT_SMALL");
   if (D.kseg == 0 && !ta && tb && D.splitk == 1 && (nt_env == nullptr || atoi(nt_env) != 0) &&
       (long)mog_cdiv(D.M, 64) * mog_cdiv(D.N, 64) * batch < 128) {
     GemmDims E = D;

@@ -1,7 +1,8 @@
 // fp32 weight gradient on the bf16 matrix cores: C[M][N] += sum_k A[k][m] B[k][n]
 // (both operands fp32, k-major: dW = X^T dY over the batch rows), split-K, optional
-// column sums of B (the bias gradient).  Split-K partials go to a workspace and
-// a second launch adds them into C in split order (deterministic; the float
+// column sums of B (the bias gradient).  Split-K partials (and the column sums'
+// per-split partials) go to a workspace and a second launch adds them into C
+// (and the column sums) in split order (deterministic; the float
 // atomics it replaces measured equal at 3 splits and 71.6 vs 87.7 us at 8 on
 // the bf16 x-rows gradient, scripts/x1_sweep.py); one split adds C += acc with
 // plain loads and stores.
@@ -352,7 +353,14 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_tn_kernel(X3Args D) {
       float v = 0.f;
 #pragma unroll
       for (int r = 0; r < RG; ++r) v += red[r * BN + t];
-      atomicAdd(D.colsum + n0 + t, v);
+      // split-K through the workspace: this split's column partial goes to
+      // work[nsplit][M][N] + [ks][N] and splitk_reduce_kernel adds the splits
+      // in split order (deterministic); one split: the only writer of these
+      // columns; float atomics otherwise
+      if (D.nsplit > 1 && D.work != nullptr)
+        D.work[(size_t)D.nsplit * M * N + (size_t)ks * N + n0 + t] = v;
+      else
+        atomicAdd(D.colsum + n0 + t, v);
     }
   }
   x3_epilogue(D, acc, m0 + wm, n0 + wn, ks, lane);
@@ -399,12 +407,22 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ s
 }
 
 // C[m][n] += sum over s = 0 .. nsplit-1 of work[s][m][n], in that order (the
-// split-K partials of the TN forms: deterministic, plain loads and stores)
+// split-K partials of the TN forms: deterministic, plain loads and stores);
+// with a column sum, colsum[n] += the splits' column partials (stored after
+// the [nsplit][M][N] partials, [nsplit][N]) likewise in split order -- thread
+// q handles column q (the grid covers max(M*N/4, N) threads)
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ W, int nsplit,
                                                             float* C, int M, int N, int ldc,
-                                                            bool vec) {
+                                                            bool vec, float* colsum) {
   const long MN = (long)M * N;
-  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  const long q = (long)blockIdx.x * 256 + threadIdx.x;
+  if (colsum != nullptr && q < N) {
+    const float* P = W + (size_t)nsplit * MN;
+    float v = P[q];
+    for (int s = 1; s < nsplit; ++s) v += P[(size_t)s * N + q];
+    colsum[q] += v;
+  }
+  const long i = q * 4;
   if (i >= MN) return;
   if (vec) {
     float4 v = *reinterpret_cast<const float4*>(W + i);
@@ -428,9 +446,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 void splitk_reduce(const X3Args& D, hipStream_t s) {
   const long n4 = ((long)D.M * D.N + 3) / 4;
+  const long nt = n4 > D.N ? n4 : (long)D.N;
   const bool vec = D.N % 4 == 0 && D.ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(D.C) & 15) == 0;
-  splitk_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), 256, 0, s>>>(D.work, D.nsplit, D.C, D.M,
-                                                                         D.N, D.ldc, vec);
+  splitk_reduce_kernel<<<dim3((unsigned)((nt + 255) / 256)), 256, 0, s>>>(
+      D.work, D.nsplit, D.C, D.M, D.N, D.ldc, vec, D.colsum);
 }
 
 // ---- NT form: C[M][N] = epi(sum_k A[m][k] B[n][k]) ------------------------
@@ -662,7 +681,8 @@ extern "C" int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb,
                                int splitk, int npieces, float* work, long work_elems,
                                void* stream) {
   MOG_CHECK_ARG(A3 && B3 && C && M >= 0 && N >= 0 && K >= 0 && splitk >= 1);
-  MOG_CHECK_ARG(work == nullptr || work_elems >= (long)splitk * M * N);
+  MOG_CHECK_ARG(work == nullptr ||
+                work_elems >= (long)splitk * M * N + (colsum ? (long)splitk * N : 0));
   MOG_CHECK_ARG(npieces == 3 || npieces == 1);
   // 16-byte chunks of 8 bf16: strides and piece strides multiples of 8 (a chunk
   // that starts below M ends inside the row; its columns >= M are not stored)
@@ -684,7 +704,8 @@ extern "C" int mog_gemm_f32_x3_tn(const float* A, const float* B, float* C, floa
                                   int M, int N, int K, int lda, int ldb, int ldc, int splitk,
                                   float* work, long work_elems, void* stream) {
   MOG_CHECK_ARG(A && B && C && M >= 0 && N >= 0 && K >= 0 && splitk >= 1);
-  MOG_CHECK_ARG(work == nullptr || work_elems >= (long)splitk * M * N);
+  MOG_CHECK_ARG(work == nullptr ||
+                work_elems >= (long)splitk * M * N + (colsum ? (long)splitk * N : 0));
   // float4 rows: 16-byte operands, widths and strides multiples of 4
   MOG_CHECK_ARG(al16(A) && al16(B) && M % 4 == 0 && N % 4 == 0 && lda % 4 == 0 &&
                 ldb % 4 == 0 && lda >= M && ldb >= N && ldc >= N);

@@ -28,6 +28,19 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 static inline hipStream_t mog_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Profiling / A-B overrides (forced tile forms, phase masks, per-phase
+// timing): read from the environment only in the profiling build
+// (-DMOG_PROFILING: `make PROFILE=1`, mog_air/_lib/prof/libmog_air.so, loaded
+// by the measurement scripts through MOG_AIR_LIB).  In the product library
+// this is a constant nullptr: its launch paths never read the environment, so
+// a test process and a bench process run the same code.
+#ifdef MOG_PROFILING
+#include <stdlib.h>
+static inline const char* mog_prof_env(const char* name) { return getenv(name); }
+#else
+static inline constexpr const char* mog_prof_env(const char*) { return nullptr; }
+#endif
+
 static inline unsigned mog_cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
 
 // wave64 sum via DPP-free shuffles

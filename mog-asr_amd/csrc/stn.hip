@@ -834,11 +834,11 @@ static int stn_backward_launch(const float* U, int N, int Hin, int Win, const fl
   int wpb = 4;  // waves (images) per workgroup, within 80 KiB of LDS
   while (wpb > 1 && slice * sizeof(float) * wpb > 80 * 1024) --wpb;
   MOG_CHECK_ARG(slice * sizeof(float) * wpb <= 160 * 1024);
-  // MOG_STN_TIMING=1 (profiling aid): per-wave phase durations to stderr
+  // MOG_STN_TIMING=1 (profiling build): per-wave phase durations to stderr
   static long long* tbuf = nullptr;
   static size_t tcap = 0;
   long long* ts = nullptr;
-  if (getenv("MOG_STN_TIMING")) {
+  if (mog_prof_env("MOG_STN_TIMING")) {
     if (tcap < (size_t)N * 8) {
       if (tbuf) (void)hipFree(tbuf);
       tcap = (size_t)N * 8;

@@ -771,14 +771,6 @@ void fill32_batch_(at::TensorList dst, at::IntArrayRef value) {
   check(mog_fill32_batch((int)p.size(), p.data(), n.data(), v.data(), o.stream()), o.name);
 }
 
-// stream-ordering test instrument (csrc/spin.hip): `anchor` names the device
-void spin_(const Tensor& anchor, int64_t ticks) {
-  Op o("spin_");
-  o.need(anchor, anchor.scalar_type(), 0, "anchor");
-  GUARD(o);
-  check(mog_spin(ticks, o.stream()), o.name);
-}
-
 void copy_f4_(const Tensor& src, Tensor dst) {
   Op o("copy_f4_");
   TORCH_CHECK(src.numel() == dst.numel() && src.numel() % 4 == 0, "copy_f4_: sizes");
@@ -786,13 +778,6 @@ void copy_f4_(const Tensor& src, Tensor dst) {
   float* pd = o.f(dst, dst.numel(), "dst");
   GUARD(o);
   check(mog_copy_f4(ps, pd, src.numel() / 4, o.stream()), o.name);
-}
-
-void lds_poison_(const Tensor& anchor, int64_t bits) {
-  Op o("lds_poison_");
-  o.need(anchor, anchor.scalar_type(), 0, "anchor");
-  GUARD(o);
-  check(mog_lds_poison((unsigned)bits, o.stream()), o.name);
 }
 
 // ---------------------------------------------- AIR-ASR cells and losses ----
@@ -959,11 +944,12 @@ void asr_step_backward_(int64_t B, bool train, int64_t fix_steps, double tempera
 }  // namespace
 
 // split-K partials of the TN forms: reduce = 1 -> a transient [splitk][M][N]
-// fp32 workspace from the caching allocator (on the op's stream) summed into C
-// in a fixed order after the GEMM (deterministic); 0 -> float atomics into C
+// (+ [splitk][N] column-sum partials) fp32 workspace from the caching
+// allocator (on the op's stream) summed into C and the column sums in a fixed
+// order after the GEMM (deterministic); 0 -> float atomics into C
 Tensor splitk_work(const Op& o, int64_t splitk, int64_t M, int64_t N, int64_t reduce) {
   if (!reduce || splitk <= 1 || M <= 0 || N <= 0) return Tensor();
-  return at::empty({splitk * M * N}, at::TensorOptions().dtype(F32).device(*o.dev));
+  return at::empty({splitk * (M * N + N)}, at::TensorOptions().dtype(F32).device(*o.dev));
 }
 
 void gemm_f32_x3_tn_(const Tensor& A, const Tensor& B, Tensor C, const optional<Tensor>& colsum,
@@ -1156,10 +1142,8 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "float clip, float lr_t, float beta1, float beta2, float eps) -> ()");
   m.def("add_(Tensor a, Tensor b, Tensor(a!) out, int n) -> ()");
   m.def("rng_fill_(Tensor(a!) out, int seed, int offset, bool normal) -> ()");
-  m.def("spin_(Tensor anchor, int ticks) -> ()");
   m.def("rng_fill_batch_(Tensor(a!)[] out, int seed, int[] offset, int[] normal) -> ()");
   m.def("fill32_batch_(Tensor(a!)[] dst, int[] value) -> ()");
-  m.def("lds_poison_(Tensor anchor, int bits) -> ()");
   m.def("copy_f4_(Tensor src, Tensor(a!) dst) -> ()");
   // AIR-ASR (air_number_bbox_location.py:384-1084)
   m.def(
@@ -1228,10 +1212,8 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("clip_adam_", &clip_adam_);
   m.impl("add_", &add_);
   m.impl("rng_fill_", &rng_fill_);
-  m.impl("spin_", &spin_);
   m.impl("rng_fill_batch_", &rng_fill_batch_);
   m.impl("fill32_batch_", &fill32_batch_);
-  m.impl("lds_poison_", &lds_poison_);
   m.impl("copy_f4_", &copy_f4_);
   m.impl("asr_pack_", &asr_pack_);
   m.impl("asr_unpack_", &asr_unpack_);

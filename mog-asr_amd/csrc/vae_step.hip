@@ -819,6 +819,24 @@ __global__ __launch_bounds__(256) void pack_frag_f32_kernel(PackF32 a) {
 }  // namespace
 
 
+// The fused step kernels run one 16-wave workgroup per CU and would leave a
+// few KiB of LDS free beside it; their launches pad the LDS request to the
+// CU's whole 160 KiB, so no workgroup of another kernel that uses LDS -- every
+// GEMM, the bf16 and x3 ones included -- can share a CU with them.  That is
+// what lets this file build with SLP vectorization (compiler-packed
+// v_pk_*_f32 arithmetic; without it the bf16 training step at 65,536 images
+// took 472 instead of 452 us, scripts/ab_fused.py): DESIGN.md §2 traced wrong
+// halves of packed fp32 pairs to bf16 MFMA waves of ANOTHER kernel on the same
+// CU, which the padding rules out (tests/test_gpu_streams.py runs the fused
+// kernels beside bf16 / x3 GEMMs and requires every output bit-identical).
+constexpr size_t CU_LDS_BYTES = 160 * 1024;
+template <class Kern>
+long lds_pad(Kern k) {
+  hipFuncAttributes a;
+  if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k)) != hipSuccess) return -1;
+  return a.sharedSizeBytes < CU_LDS_BYTES ? (long)(CU_LDS_BYTES - a.sharedSizeBytes) : 0;
+}
+
 extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int Z, int G1,
                                         int G2, const float* x, const float* theta_f,
                                         const float* theta_b, const float* mask,
@@ -857,7 +875,7 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   p.a2b = reinterpret_cast<__bf16*>(a2b); p.mu = mu; p.lv = lv; p.z = z;
   p.zb = reinterpret_cast<__bf16*>(zb); p.d1b = reinterpret_cast<__bf16*>(d1b);
   p.d2b = reinterpret_cast<__bf16*>(d2b); p.r = r;
-  const char* ph = getenv("MOG_VS_PHASES");
+  const char* ph = mog_prof_env("MOG_VS_PHASES");
   p.phases = ph ? atoi(ph) : 31;
   if (!save) p.phases &= ~16;
   p.B = B; p.C = C; p.lik_std = lik_std; p.v_pm = v_pm; p.v_pv = v_pv; p.v_plv = v_plv;
@@ -869,7 +887,7 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   // tiles halve the weight stream per image, but a partial last round (the
   // train step's T*B = 24,576 rows: 1.5 rounds of 64-image tiles, 3 of
   // 32-image ones) can cost more than they save: 225 -> 220 us, bf16 train
-  // step 2.32 -> 2.28 ms.  MOG_VS_MT overrides: 4 = 64 images x 16 waves,
+  // step 2.32 -> 2.28 ms.  MOG_VS_MT overrides (profiling build): 4 = 64 images x 16 waves,
   // 2 = 32 images x 8 waves, 3 = 32 images x 16 waves.
   static int ncu = 0;
   if (ncu == 0) {
@@ -882,7 +900,7 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   }
   const long r64 = ((long)B + 64L * ncu - 1) / (64L * ncu), r32 = ((long)B + 32L * ncu - 1) / (32L * ncu);
   int mt = r64 * 112 <= r32 * 73 ? 4 : 3;
-  if (const char* e = getenv("MOG_VS_MT")) {
+  if (const char* e = mog_prof_env("MOG_VS_MT")) {  // (profiling build)
     const int v = atoi(e);
     if (v == 2 || v == 3 || v == 4) mt = v;
   }
@@ -891,13 +909,13 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
   // several steps' rows in one launch also rule out the running loss
   // (rows of one image would race on it: mog_air_runloss replays it)
   MOG_CHECK_ARG(p.x_period == B || (p.x_period % M == 0 && !runloss));
-  // MOG_VS_TIMING=1 (profiling aid): per-phase durations, averaged over
+  // MOG_VS_TIMING=1 (profiling build): per-phase durations, averaged over
   // blocks, printed to stderr (synchronizes the stream)
   static long long* tbuf = nullptr;
   static size_t tcap = 0;
   const unsigned nblk = mog_cdiv(B, M);
   p.tstamp = nullptr;
-  if (getenv("MOG_VS_TIMING")) {
+  if (mog_prof_env("MOG_VS_TIMING")) {
     if (tcap < (size_t)nblk * 16) {
       if (tbuf) (void)hipFree(tbuf);
       tcap = (size_t)nblk * 16;
@@ -905,13 +923,20 @@ extern "C" int mog_stn_vae_step_forward(int B, int C, int W, int R1, int R2, int
     }
     p.tstamp = tbuf;
   }
-  // MOG_VS_LA (profiling): sampler gather lookahead of the 64-image form
-  static const int la = getenv("MOG_VS_LA") ? atoi(getenv("MOG_VS_LA")) : 3;
-  if (mt == 4 && la == 4) stn_vae_step_kernel<4, 16, 4, 4><<<nblk, 1024, 0, s>>>(p);
-  else if (mt == 4 && la == 5) stn_vae_step_kernel<4, 16, 4, 5><<<nblk, 1024, 0, s>>>(p);
-  else if (mt == 4) stn_vae_step_kernel<4, 16, 4><<<nblk, 1024, 0, s>>>(p);
+  // (the LDS padding of the 16-wave forms: see lds_pad)
+  static const long pad4 = lds_pad(stn_vae_step_kernel<4, 16, 4>);
+  static const long pad3 = lds_pad(stn_vae_step_kernel<2, 16, 4>);
+  if (pad4 < 0 || pad3 < 0) return MOG_ERR_INVALID;
+#ifdef MOG_PROFILING
+  // MOG_VS_LA (profiling build): sampler gather lookahead of the 64-image form
+  static const int la = mog_prof_env("MOG_VS_LA") ? atoi(mog_prof_env("MOG_VS_LA")) : 3;
+  if (mt == 4 && la == 4) stn_vae_step_kernel<4, 16, 4, 4><<<nblk, 1024, pad4, s>>>(p);
+  else if (mt == 4 && la == 5) stn_vae_step_kernel<4, 16, 4, 5><<<nblk, 1024, pad4, s>>>(p);
   else if (mt == 2) stn_vae_step_kernel<2, 8, 4><<<nblk, 512, 0, s>>>(p);
-  else stn_vae_step_kernel<2, 16, 4><<<nblk, 1024, 0, s>>>(p);
+  else
+#endif
+  if (mt == 4) stn_vae_step_kernel<4, 16, 4><<<nblk, 1024, pad4, s>>>(p);
+  else stn_vae_step_kernel<2, 16, 4><<<nblk, 1024, pad3, s>>>(p);
   if (p.tstamp) {
     std::vector<long long> h((size_t)nblk * 16);
     (void)hipStreamSynchronize(s);
@@ -996,7 +1021,7 @@ extern "C" int mog_stn_vae_step_forward_f32(
   static long long* tbuf = nullptr;
   static size_t tcap = 0;
   p.tstamp = nullptr;
-  if (getenv("MOG_VS_TIMING")) {
+  if (mog_prof_env("MOG_VS_TIMING")) {
     if (tcap < (size_t)nblk * 16) {
       if (tbuf) (void)hipFree(tbuf);
       tcap = (size_t)nblk * 16;
@@ -1004,7 +1029,9 @@ extern "C" int mog_stn_vae_step_forward_f32(
     }
     p.tstamp = tbuf;
   }
-  stn_vae_step_f32_kernel<<<nblk, 1024, 0, s>>>(p);
+  static const long padf = lds_pad(stn_vae_step_f32_kernel);  // (see lds_pad)
+  if (padf < 0) return MOG_ERR_INVALID;
+  stn_vae_step_f32_kernel<<<nblk, 1024, padf, s>>>(p);
   if (p.tstamp) {
     std::vector<long long> h((size_t)nblk * 16);
     (void)hipStreamSynchronize(s);

@@ -71,9 +71,7 @@ _SIGS = {
     "mog_rng_fill": [P, L, ULL, ULL, I, P],
     "mog_rng_fill_batch": [I, P, P, ULL, P, P, P],
     "mog_fill32_batch": [I, P, P, P, P],
-    "mog_spin": [LL, P],
     "mog_copy_f4": [P, P, L, P],
-    "mog_lds_poison": [ctypes.c_uint, P],
     "mog_generation_prior": [I, I, F, F, F, F, F, F, P, P, P, P, P, P, P, P],
     "mog_asr_pack": [I, I, I, I, P, P, P, P, P, P, P],
     "mog_asr_unpack": [I, I, I, I, P, P, P, P, P, P, I, P],
@@ -119,6 +117,28 @@ def load():
                        f"{src}); rebuild it with `make -C mog-asr_amd`")
     _lib = lib
     return lib
+
+
+# test-only instruments (include/mog_air_test.h): their own library
+TEST_LIB_PATH = os.path.join(_HERE, "_lib", "libmog_air_test.so")
+_TEST_SIGS = {"mog_spin": [LL, P], "mog_lds_poison": [ctypes.c_uint, P]}
+_test_lib = None
+
+
+def load_test():
+    """libmog_air_test.so (mog_spin, mog_lds_poison): the stream-ordering and
+    LDS-hygiene test instruments, kept out of the product library."""
+    global _test_lib
+    if _test_lib is None:
+        if not os.path.exists(TEST_LIB_PATH):
+            raise MogError(f"{TEST_LIB_PATH} not built (make -C mog-asr_amd)")
+        lib = ctypes.CDLL(TEST_LIB_PATH)
+        for name, args in _TEST_SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = I
+        _test_lib = lib
+    return _test_lib
 
 
 def library_build_id(lib=None) -> str:

@@ -21,8 +21,6 @@ No host synchronisation happens inside a train step.
 from __future__ import annotations
 
 import contextlib
-import math
-import os
 from typing import Dict, Optional
 
 import numpy as np
@@ -30,9 +28,11 @@ import torch
 
 from . import _lib
 from . import ops
-from .ops import (EPI_ATOMIC, EPI_RELU, EPI_SIGMOID_NOISE, EPI_SOFTPLUS, EPI_SOFTPLUS_BWD,
-                  EPI_STORE, dp, gemm, stream_ptr)
+from .ops import EPI_RELU, EPI_SIGMOID_NOISE, EPI_SOFTPLUS, EPI_SOFTPLUS_BWD, EPI_STORE, gemm
+from .graph import GraphCapture
 from .params import ParamStore, param_specs
+from .results import Results
+from .wgrads import WeightGradients
 
 _ops = ops._ops  # torch.ops.mog_air (csrc/torch_ops.cpp)
 
@@ -207,7 +207,7 @@ class _Workspace:
         self._bwd = True
 
 
-class AIRModel:
+class AIRModel(WeightGradients, GraphCapture, Results):
     """See module docstring.  Extra keyword-only arguments (not in the
     reference): ``device``, ``seed`` (weight init), ``noise_seed`` (device
     Philox noise), ``grad_world`` (data-parallel world size folded into the
@@ -235,12 +235,11 @@ class AIRModel:
             windows_size == 28 and tuple(vae_recognition_units) == (512, 256)
             and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512))
         # fp32: the same fused step at the reference precision over the T*B
-        # rows of the batched VAE (stn_vae_step_f32_kernel; MOG_FUSED_F32=0
+        # rows of the batched VAE (stn_vae_step_f32_kernel; fused_step=False
         # runs the unfused sequence it is bit-identical to)
         self.fused_f32 = bool(fused_step) and precision == "fp32" and (
             windows_size == 28 and tuple(vae_recognition_units) == (512, 256)
-            and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512)
-            and os.environ.get("MOG_FUSED_F32", "1") != "0")
+            and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512))
         # the glimpse VAE of all T steps after the loop, over T*B rows (AIR).
         # (Measured and not kept: step 0's VAE on a second stream under the
         # rest of the recurrent loop -- no gain at B = 8192, slower at 64.)
@@ -308,10 +307,12 @@ class AIRModel:
 
     # ----------------------------------------------------------- helpers ---
     # Optional per-kernel HIP-event timing (bench.py roofline): when
-    # ``kernel_events`` is a dict, every tagged launch records a (start, end,
-    # work) triple on the stream it is launched on; work = (bound, amount,
-    # peak) -- algorithmic flops ("mfma", peak "fp32" / "bf16") or bytes
-    # ("hbm") of that one launch, or None (bench.kernel_work prices the tag).
+    # ``kernel_events`` is a dict, every tagged launch records (start, end,
+    # work, side) on the stream it is launched on; work = (bound, amount,
+    # peak[, "x3"]) -- algorithmic flops ("mfma", peak "fp32" / "bf16"; "x3":
+    # fp32 flops issued as six bf16 products) or bytes ("hbm") of that one
+    # launch, or None (bench.kernel_work prices the tag); side: launched on
+    # one of the shared side streams.
     kernel_events = None
 
     class _NoTimer:
@@ -328,12 +329,16 @@ class AIRModel:
         def __enter__(self):
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e1 = torch.cuda.Event(enable_timing=True)
-            self.e0.record(torch.cuda.current_stream())
+            s = torch.cuda.current_stream()
+            self.e0.record(s)
+            # a launch on a side stream: its events also count the time its
+            # first workgroups wait for CUs the main stream's kernels hold
+            self.side = any(s == o for o in _STREAMS.get(s.device, ()))
             return self
 
         def __exit__(self, *a):
             self.e1.record(torch.cuda.current_stream())
-            self.sink.setdefault(self.name, []).append((self.e0, self.e1, self.work))
+            self.sink.setdefault(self.name, []).append((self.e0, self.e1, self.work, self.side))
             return False
 
     def _timed(self, name, work=None):
@@ -450,11 +455,6 @@ class AIRModel:
     # AIR's _forward joins side-stream noise after the x-projection (the ASR
     # subclass fills on the current stream)
     NOISE_ON_SIDE = True
-    # the x3 input gradients' weight pieces split in that side-stream prologue
-    # instead of on the backward's path (fp32 step 3.05 -> 3.02 ms).  Moving
-    # the gradient zeroing there too was measured and dropped: the step-
-    # gradient x3 test then failed 2 runs in 6 at ~2e-5 (in 6 runs without it: none)
-    EARLY_PREP = os.environ.get("MOG_EARLY_PREP", "1") == "1"
 
     # ----------------------------------------------------------- forward ---
     def _forward(self, X: torch.Tensor, targets: Optional[torch.Tensor], ws: _Workspace,
@@ -481,9 +481,11 @@ class AIRModel:
                 ops.split3_bf16(X, ws.X3, B, C2, C2, C2p, B * C2p)
             if need_grad and self.precision == "bf16":
                 self._x_bf16(X, ws)  # (likewise: the bf16 x-part gradient's A operand)
-            if (need_grad and self.EARLY_PREP and self.precision == "fp32" and self.VAE_DX_X3
+            if (need_grad and self.precision == "fp32" and self.VAE_DX_X3
                     and B * self.max_steps >= self.X3_DX_MIN_ROWS):
-                self._w3()  # the x3 input gradients' weight pieces, off the backward's path
+                # the x3 input gradients' weight pieces, split here instead of
+                # on the backward's path (fp32 step 3.05 -> 3.02 ms)
+                self._w3()
             if side is not None:
                 pre_done = torch.cuda.Event()
                 pre_done.record(side)
@@ -732,10 +734,17 @@ class AIRModel:
         # and run as one grouped launch at the end (_wgrad_group_end)
         self._wgroup = (self._wgroup_obj if (self.WGRAD_GROUP and B < self.SIDE_MIN_BATCH
                                              and self.grad_reducer is None) else None)
+        wg = self._wgroup
+        if wg is not None:
+            wg.probs = []  # (a fresh collection: nothing left from a failed step)
         try:
             self._backward_body(X, ws)
+        except BaseException:
+            if wg is not None:
+                wg.probs = []  # a failed body's partial problems never launch
+            raise
         finally:
-            wg, self._wgroup = self._wgroup, None
+            self._wgroup = None
         if wg is not None and wg.probs:
             flops = sum(2.0 * p[4] * p[5] * p[6] for p in wg.probs)
             with self._timed("wgrad_group", ("mfma", flops, "fp32")):
@@ -743,7 +752,7 @@ class AIRModel:
 
     # the grouped weight-gradient launch below SIDE_MIN_BATCH (batch 64: 11
     # launches of a few k-steps each -> one)
-    WGRAD_GROUP = os.environ.get("MOG_WGRAD_GROUP", "1") == "1"
+    WGRAD_GROUP = True
     _wgroup = None
 
     @property
@@ -841,9 +850,9 @@ class AIRModel:
             # one GPU, no bucket to hand over: the heads' weight gradients
             # follow the VAE's on the side stream, under the latency-bound
             # LSTM chain; the main stream joins them before Adam
-            # (on a third stream, beside the VAE's: HEADS_STREAM3)
-            side = self._stream3() if self.HEADS_STREAM3 else self._side_stream()
-            with torch.cuda.stream(self._fork(side)):
+            # -- on a third stream, beside the VAE's instead of queued after
+            # them (fp32 step 3.10 -> 3.05 ms)
+            with torch.cuda.stream(self._fork(self._stream3())):
                 self._weight_grads_heads(ws)
         else:
             # the heads' and the VAE's weight gradients are final here: their
@@ -869,13 +878,12 @@ class AIRModel:
         self._weight_grads_lstm(X, ws, side=heads_side, rec_done=rec_early)
         if heads_side:  # (everything on the side stream: VAE, heads, dW_rec)
             torch.cuda.current_stream().wait_stream(self._side_stream())
-            if self.HEADS_STREAM3 or self.REC_STREAM3:
-                torch.cuda.current_stream().wait_stream(self._stream3())
+            torch.cuda.current_stream().wait_stream(self._stream3())
 
     # single GPU: heads' weight gradients on the side stream (see _backward)
-    HEADS_WGRAD_SIDE = os.environ.get("MOG_HEADS_SIDE", "1") == "1"
+    HEADS_WGRAD_SIDE = True
     # ... and the LSTM kernel's recurrent-rows gradient beside the x-rows one
-    REC_WGRAD_SIDE = os.environ.get("MOG_REC_SIDE", "1") == "1"
+    REC_WGRAD_SIDE = True
     # the round-3 side-stream moves (noise + resets under the x-projection,
     # heads' weight gradients under the LSTM chain) from this batch: below it
     # the launches are too short to hide the cross-stream waits (batch 64:
@@ -886,8 +894,8 @@ class AIRModel:
     # 784-wide layers on the bf16 matrix cores with exact three-piece splits
     # (gemm_x3.hip NT form: dY split in the kernel, W split once per optimizer
     # step) -- the chain is on the step's critical path; fp32-level accuracy
-    # like the weight gradients.  MOG_VAE_DX_X3=0: the fp32 MFMA GEMMs.
-    VAE_DX_X3 = os.environ.get("MOG_VAE_DX_X3", "1") == "1"
+    # like the weight gradients.  False: the fp32 MFMA GEMMs.
+    VAE_DX_X3 = True
     _X3_DX = ("gen_mean", "generative_2", "recognition_2", "recognition_1")
 
     def _w3(self):
@@ -924,7 +932,7 @@ class AIRModel:
         if self.VAE_DX_X3 and K % 8 == 0 and N % 4 == 0 and M >= self.X3_DX_MIN_ROWS:
             w3 = self._w3()[name]
             # six bf16 MFMA products per fp32 product (gemm_x3.hip)
-            with self._timed("vae_dgrad_x3", ("mfma", 12.0 * M * N * K, "bf16")):
+            with self._timed("vae_dgrad_x3", ("mfma", 2.0 * M * N * K, "fp32", "x3")):
                 ops.gemm_x3_nt(dY, w3, N * K, out, M, N, K, K, K, N, aux=aux,
                                ldaux=N if aux is not None else 0)
             return
@@ -1216,144 +1224,6 @@ class AIRModel:
         gemm_bf16([ws.da1b[t]], [wn["recognition_1"]], [ws.dg], B, W2, R1, R1, R1, W2,
                   epi=BF_STORE)
 
-    # every weight gradient in one k pass (split-K 1, one atomic add per
-    # element onto the zeroed gradient): a bitwise-reproducible step, for the
-    # stream-ordering tests (tests/test_gpu_streams.py)
-    ONE_PASS_WGRADS = False
-
-    def _sk(self, splitk):
-        return 1 if self.ONE_PASS_WGRADS else splitk
-
-    def _dw_bf16(self, X, dY, out, K, M, N, lda, ldb, bias_out):
-        from .ops import BF_ATOMIC, gemm_bf16
-        big = M >= 128 and N >= 128
-        tiles = ((M + 127) // 128) * ((N + 127) // 128) if big else \
-            ((M + 63) // 64) * ((N + 63) // 64)
-        target = int(os.environ.get("MOG_DW_TARGET", "256"))
-        splitk = self._sk(max(1, min(K // 512, (target + tiles - 1) // tiles)))
-        with self._timed("wgrad_bf16", ("mfma", 2.0 * K * M * N, "bf16")):
-            gemm_bf16([X], [dY], [out], M, N, K, lda, ldb, N, tn=True, epi=BF_ATOMIC,
-                      splitk=splitk, colsum=[bias_out])
-
-    def _vae_weight_grads_bf16(self, ws, t=None):
-        """The VAE weight gradients over all T*B rows (bf16 operands), or over
-        loop step t's B rows (accumulated: the per-step form of AIR-ASR)."""
-        TB = ws.B * self.max_steps if t is None else ws.B
-        v = (lambda x: x) if t is None else (lambda x: x[t])  # noqa: E731
-        W2, R1, R2, Z, G1, G2 = self._vae_dims()
-        Zp = self._pad8(Z)
-        g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
-        gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
-        self._dw_bf16(v(ws.gb), v(ws.da1b), g("recognition_1"), TB, W2, R1, W2, R1,
-                      gb("recognition_1"))
-        self._dw_bf16(v(ws.a1b), v(ws.da2b), g("recognition_2"), TB, R1, R2, R1, R2,
-                      gb("recognition_2"))
-        self._dw_bf16(v(ws.a2b), v(ws.dmub), g("rec_mean"), TB, R2, Z, R2, Zp, gb("rec_mean"))
-        self._dw_bf16(v(ws.a2b), v(ws.dlvb), g("rec_log_variance"), TB, R2, Z, R2, Zp,
-                      gb("rec_log_variance"))
-        self._dw_bf16(v(ws.zb), v(ws.dd1b), g("generative_1"), TB, Z, G1, Zp, G1,
-                      gb("generative_1"))
-        self._dw_bf16(v(ws.d1b), v(ws.dd2b), g("generative_2"), TB, G1, G2, G1, G2,
-                      gb("generative_2"))
-        self._dw_bf16(v(ws.d2b), v(ws.dmb), g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
-
-    def _dw(self, X, dY, out, K, M, N, lda, ldb, bias_out=None):
-        """out[M,N] += X^T dY over K rows (split-K, atomics); bias_out += colsum(dY).
-        X, dY, out, bias_out may be lists (one batched launch)."""
-        if not isinstance(out, (list, tuple)):
-            X, dY, out = [X], [dY], [out]
-            bias_out = None if bias_out is None else [bias_out]
-        if self._wgroup is not None:  # collected: one grouped launch ends the backward
-            for x, dy, o, b in zip(X, dY, out, bias_out or [None] * len(out)):
-                self._wgroup.add(x, dy, o, M, N, K, lda, ldb, N, b)
-            return
-        tiles = ((M + 63) // 64) * ((N + 63) // 64) * len(out)
-        target = int(os.environ.get("MOG_DW32_TARGET", "2048"))
-        splitk = self._sk(max(1, min(K // 256, (target + tiles - 1) // tiles)))
-        with self._timed("wgrad_f32", ("mfma", 2.0 * K * M * N * len(out), "fp32")):
-            gemm(X, dY, out, M, N, K, lda, ldb, N, transA=True, epi=EPI_ATOMIC,
-                 splitk=splitk, colsum=bias_out)
-
-    # fp32 configuration: the VAE weight gradients whose operands are 16-byte
-    # rows (M, N multiples of 4: the 784/512/256-wide layers, 98 % of the
-    # flops) on the bf16 matrix cores with exact three-piece splits inside the
-    # GEMM (gemm_x3.hip: fp32-level accuracy, as the LSTM x-rows gradient,
-    # DESIGN.md §4.4); MOG_VAE_WGRAD_X3=0 keeps them on the fp32 split-K GEMM
-    VAE_WGRAD_X3 = os.environ.get("MOG_VAE_WGRAD_X3", "1") == "1"
-
-    # the x3 forms from this many rows: below it (the reference's batch of 64:
-    # 192 rows) their 128 x 128 tiles leave most CUs idle, and the fp32 GEMMs'
-    # small-M tiles finish first
-    X3_MIN_ROWS = 2048
-    # the NT input-gradient form from this many rows (the AIR step's T*B =
-    # 24,576 and the ASR step's per-step 8,192): below it its 128 x 128 tiles
-    # leave CUs idle and the fp32 GEMM finishes first.  (Round 4, after the
-    # NT load fixes: ASR fp32 step 9.46 -> 9.43 ms with 8,192 in; before
-    # them the NT form lost there, 9.6 -> 10.1 ms.)
-    X3_DX_MIN_ROWS = int(os.environ.get("MOG_X3_DX_MIN_ROWS", "8192"))
-
-    def _dw_x3(self, X, dY, out, K, M, N, lda, ldb, bias_out):
-        """out[M,N] += X^T dY over K rows (gemm_x3_tn), bias_out += colsum(dY)."""
-        if not (self.VAE_WGRAD_X3 and M % 4 == 0 and N % 4 == 0 and K >= self.X3_MIN_ROWS):
-            return self._dw(X, dY, out, K, M, N, lda, ldb, bias_out)
-        tiles = ((M + 127) // 128) * ((N + 127) // 128)
-        splitk = self._sk(max(1, min(K // 256, (512 + tiles - 1) // tiles)))
-        # six bf16 MFMA products per fp32 product (gemm_x3.hip); float atomics
-        # for the 19-64 split-K partials of these <= 0.4 M-element outputs
-        # (through the workspace: 160 -> 229 us per launch in the step)
-        with self._timed("vae_wgrad_x3", ("mfma", 12.0 * K * M * N, "bf16")):
-            ops.gemm_x3_tn(X, dY, out, M, N, K, lda, ldb, N, splitk=splitk, colsum=bias_out,
-                           reduce=False)
-
-    def _vae_wgrad_fp32(self, ws, name, t=None):
-        """One VAE layer's weight / bias gradient over all T*B rows (fp32), or
-        over loop step t's B rows (accumulated: the per-step form of AIR-ASR)."""
-        TB = ws.B * self.max_steps
-        W2, R1, R2, Z, G1, G2 = self._vae_dims()
-        g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
-        gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
-        if t is None:
-            v = lambda x: x  # noqa: E731
-        else:
-            TB = ws.B
-            v = lambda x: x[t]  # noqa: E731
-        if name == "recognition_1":
-            self._dw_x3(v(ws.g), v(ws.da1), g(name), TB, W2, R1, W2, R1, gb(name))
-        elif name == "recognition_2":
-            self._dw_x3(v(ws.a1), v(ws.da2), g(name), TB, R1, R2, R1, R2, gb(name))
-        elif name == "rec_mean":  # (with rec_log_variance: one batched launch)
-            self._dw([v(ws.a2)] * 2, [v(ws.dmu), v(ws.dlv)], [g("rec_mean"),
-                     g("rec_log_variance")], TB, R2, Z, R2, Z,
-                     [gb("rec_mean"), gb("rec_log_variance")])
-        elif name == "generative_1":
-            self._dw(v(ws.z), v(ws.dd1), g(name), TB, Z, G1, Z, G1, gb(name))
-        elif name == "generative_2":
-            self._dw_x3(v(ws.d1), v(ws.dd2), g(name), TB, G1, G2, G1, G2, gb(name))
-        elif name == "gen_mean":
-            self._dw_x3(v(ws.d2), v(ws.dm), g(name), TB, G2, W2, G2, W2, gb(name))
-
-    def _vae_weight_grads_fp32(self, ws):
-        for name in ("recognition_1", "recognition_2", "rec_mean", "generative_1",
-                     "generative_2", "gen_mean"):
-            self._vae_wgrad_fp32(ws, name)
-
-    def _weight_grads_glimpse(self, ws):
-        """Weight gradients of the VAE and the five heads (every loop step at
-        once, K = T*B rows)."""
-        if self.precision == "bf16":
-            self._vae_weight_grads_bf16(ws)
-        else:
-            self._vae_weight_grads_fp32(ws)
-        self._weight_grads_heads(ws)
-
-    # one GPU, from SIDE_MIN_BATCH: the heads' weight gradients on a third
-    # stream, beside the VAE's instead of queued after them (fp32 step 3.10 /
-    # 3.10 -> 3.05 / 3.07 ms; MOG_HEADS_STREAM3=0: after them on the side stream)
-    HEADS_STREAM3 = os.environ.get("MOG_HEADS_STREAM3", "1") == "1"
-    # ... and the recurrent rows' gradient after them there (3.06 / 3.08 ->
-    # 3.04 / 3.04 ms; MOG_REC_STREAM3=0: on the side stream)
-    REC_STREAM3 = os.environ.get("MOG_REC_STREAM3", "1") == "1"
-
     # the side and third streams are created once per process and device and
     # shared by every model (see _shared_streams)
     def _stream3(self):
@@ -1378,201 +1248,6 @@ class AIRModel:
             with torch.cuda.stream(stream):
                 ops.spin(self.SPIN_FORK)
         return stream
-
-    def _vae_weight_grads_async(self, ws):
-        """The VAE weight gradients on the side stream (ordered after
-        everything issued so far on the current stream); returns the events
-        that mark the heads' W1 refresh and their completion.  Below
-        SIDE_MIN_BATCH they run in line on the current stream (events None):
-        at the reference's batch of 64 the launches are a few microseconds
-        each, too short to hide a cross-stream wait."""
-        if ws.B < self.SIDE_MIN_BATCH:
-            if self.precision == "bf16":
-                self._vae_weight_grads_bf16(ws)
-            else:
-                self._vae_weight_grads_fp32(ws)
-            return None, None
-        side = self._fork(self._side_stream())
-        with torch.cuda.stream(side):
-            # the heads' concatenated W1 (B operand of the dh GEMM) first:
-            # off the main stream, which waits for it only at that GEMM
-            self._w1cat()
-            w1_done = torch.cuda.Event()
-            w1_done.record(side)
-            if self.precision == "bf16":
-                self._vae_weight_grads_bf16(ws)
-            else:
-                self._vae_weight_grads_fp32(ws)
-            done = torch.cuda.Event()
-            done.record(side)
-        return w1_done, done
-
-    def _w1cat(self):
-        """[W1_0 .. W1_4] side by side ([H, 5 HS]): the B operand of the heads'
-        dh GEMM, refreshed when the parameters change."""
-        if getattr(self, "_w1cat_version", None) != self.params.version:
-            if getattr(self, "_w1cat_buf", None) is None:
-                H, HS = self.rnn_units, self.scale_hidden_units
-                self._w1cat_buf = torch.empty((H, 5 * HS), device=self.device)
-            torch.cat([self._P(h + "/hidden/weights") for h in self._HEADS], dim=1,
-                      out=self._w1cat_buf)
-            self._w1cat_version = self.params.version
-        return self._w1cat_buf
-
-    def _weight_grads_heads(self, ws):
-        H, HS, TB = self.rnn_units, self.scale_hidden_units, ws.B * self.max_steps
-        heads = list(enumerate(self._HEADS))
-        dhid = ws.dhid.view(TB, 5, HS)
-        self._dw([ws.h] * 5, [dhid[:, zi] for zi, _ in heads],
-                 [self._G(h + "/hidden/weights") for _, h in heads], TB, H, HS, H, 5 * HS,
-                 [self._G(h + "/hidden/biases") for _, h in heads])
-        for k in (1, 2):
-            sel = [(zi, h) for zi, h in heads if (2 if h.startswith("shift") else 1) == k]
-            self._dw([ws.hid[zi] for zi, _ in sel], [ws.dout[zi] for zi, _ in sel],
-                     [self._G(h + "/output/weights") for _, h in sel], TB, HS, k, HS, 2,
-                     [self._G(h + "/output/biases") for _, h in sel])
-
-    # fp32 configuration: the x-part of the LSTM kernel gradient on the bf16
-    # matrix cores with exact three-piece operand splits (gemm_x3.hip,
-    # DESIGN.md §4.4).  2 (default): the operands split once per step, X on
-    # the side stream under the x-projection, dG before the GEMM (gemm_x3p_tn:
-    # 244 vs 428 us stand-alone, step 3.44 -> 3.37 ms); 1: split inside the
-    # GEMM (318 us, no change in the step); 0: the fp32 MFMA split-K GEMM.
-    X_GRAD_X3 = int(os.environ.get("MOG_X_GRAD_X3", "2"))
-    # the pre-split form from this batch: below it (the reference's batch of
-    # 64) the two split launches cost more than the fp32 chain's K = B pass
-    # (batch 64: x3p 12.3 + splits 9.6 us)
-    X3P_MIN_B = 256
-
-    def _x3p_xgrad(self, B):
-        return self.precision == "fp32" and self.X_GRAD_X3 == 2 and B >= self.X3P_MIN_B
-    X3_SPLITK = int(os.environ.get("MOG_X3_SPLITK", "8"))
-
-    # rows of the x-part of the LSTM kernel gradient per all-reduce bucket
-    # (multiple of the 64-row GEMM tile; data parallel only)
-    X_GRAD_CHUNK = 640
-
-    def _weight_grads_rec_side(self, ws):
-        """One GPU: the LSTM kernel's recurrent-rows gradient sum_t h[t-1]^T
-        dG[t] on a side stream, forked as soon as dG[1:] is final (before the
-        chain's step 0), so it overlaps that step instead of the x-rows
-        gradient."""
-        st = self._stream3() if self.REC_STREAM3 else self._side_stream()
-        with torch.cuda.stream(self._fork(st)):
-            self._dw_rec(ws)
-
-    def _dw_rec(self, ws):
-        """The LSTM kernel's recurrent rows: gK[C2:] += sum_t h[t-1]^T dG[t]
-        over (T-1) B rows.  From X3_MIN_ROWS (either precision: fp32-level, and
-        faster than the fp32 chain): on the bf16 matrix cores with exact
-        three-piece splits (gemm_x3_tn, as the fp32 VAE weight gradients;
-        256 x 1024 x 16,384 at B = 8192), else the fp32 split-K GEMM."""
-        B, T, H, C2 = ws.B, self.max_steps, self.rnn_units, self.C2
-        gK = self._G("rnn/basic_lstm_cell/kernel")
-        K = (T - 1) * B
-        if self.REC_WGRAD_X3 and K >= self.X3_MIN_ROWS:
-            tiles = ((H + 127) // 128) * ((4 * H + 127) // 128)
-            splitk = self._sk(max(1, min(K // 256, (512 + tiles - 1) // tiles)))
-            with self._timed("rec_wgrad_x3", ("mfma", 12.0 * K * H * 4 * H, "bf16")):
-                ops.gemm_x3_tn(ws.h, ws.dG[1:], gK[C2:], H, 4 * H, K, H, 4 * H, 4 * H,
-                               splitk=splitk, reduce=False)
-        else:
-            self._dw(ws.h, ws.dG[1:], gK[C2:], K, H, 4 * H, H, 4 * H)
-
-    REC_WGRAD_X3 = os.environ.get("MOG_REC_WGRAD_X3", "1") == "1"
-
-    def _weight_grads_lstm(self, X, ws, side=False, rec_done=False):
-        """LSTM kernel / bias gradients.  Data parallel: the x-part X^T dGsum
-        (2500 x 1024, 10 MB) is produced in row chunks, each handed to the
-        all-reduce as soon as it is final, so the collective of chunk i runs
-        under the GEMM of chunk i+1; the recurrent rows and the bias go last.
-        rec_done: the recurrent rows were forked already (_weight_grads_rec_side)."""
-        B, T, H, C2 = ws.B, self.max_steps, self.rnn_units, self.C2
-        gK = self._G("rnn/basic_lstm_cell/kernel")
-        gbK = self._G("rnn/basic_lstm_cell/bias")
-        if rec_done:
-            pass
-        elif T > 1 and side and self.REC_WGRAD_SIDE:
-            self._weight_grads_rec_side(ws)
-        elif T > 1:
-            self._dw_rec(ws)
-        chunk = self.X_GRAD_CHUNK if self.grad_reducer is not None else C2
-        base = self.params.offsets[self._SCOPE_PREFIX + "rnn/basic_lstm_cell/kernel"]
-        # bias gradient = colsum(sum_t dG_t) = colsum(dGsum), fused into chunk 0
-        m_last = 0
-        # (the x-rows gradient GEMM of every chunk is tagged; its operand
-        # conversions / splits are not: they are other launches)
-        x3p = self._x3p_xgrad(B)
-        for m0 in range(0, C2, chunk):
-            m_last = m0
-            m1 = min(C2, m0 + chunk)
-            bias = gbK if m0 == 0 else None
-            if self.precision == "bf16":
-                # bf16 configuration: X^T dGsum on bf16 operands (fp32
-                # accumulate); the forward x-projection stays fp32
-                self._x_grad_bf16(X, ws, gK, bias, m0, m1)
-            elif x3p:
-                if m0 == 0:
-                    if getattr(ws, "dG3", None) is None:
-                        ws.dG3 = torch.empty((3, B, 4 * H), device=self.device,
-                                             dtype=torch.bfloat16)
-                    ops.split3_bf16(ws.dGsum, ws.dG3, B, 4 * H, 4 * H, 4 * H, B * 4 * H)
-                C2p = self._pad8(C2)
-                with self._timed("lstm_x_projection_grad",
-                                 ("mfma", 12.0 * B * (m1 - m0) * 4 * H, "bf16")):
-                    ops.gemm_x3p_tn(ws.X3.view(-1)[m0:], B * C2p, ws.dG3, B * 4 * H, gK[m0:m1],
-                                    m1 - m0, 4 * H, B, C2p, 4 * H, 4 * H,
-                                    splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
-                                    colsum=bias, reduce=False)
-            elif self.X_GRAD_X3 == 1:
-                # fp32 operands split exactly into three bf16 pieces on the
-                # bf16 matrix cores (gemm_x3.hip: fp32-level accuracy)
-                with self._timed("lstm_x_projection_grad",
-                                 ("mfma", 12.0 * B * (m1 - m0) * 4 * H, "bf16")):
-                    ops.gemm_x3_tn(X[:, m0:], ws.dGsum, gK[m0:m1], m1 - m0, 4 * H, B, C2, 4 * H,
-                                   4 * H, splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
-                                   colsum=bias)
-            else:
-                self._dw(X[:, m0:], ws.dGsum, gK[m0:m1], B, m1 - m0, 4 * H, C2, 4 * H, bias)
-            if m1 < C2:
-                self._reduce_bucket(base + m0 * 4 * H, base + m1 * 4 * H)
-        self._reduce_bucket(base + m_last * 4 * H, self._bucket_split())
-
-    def _x_bf16(self, X, ws):
-        """X in bf16 [B][C2p] (zero pad columns): the A operand of the bf16
-        configuration's x-rows gradient, converted once per step -- in the
-        forward's side-stream prologue from SIDE_MIN_BATCH (X is the step's
-        input, final before the x-projection)."""
-        B, C2 = ws.B, self.C2
-        C2p = self._pad8(C2)
-        if getattr(ws, "Xb", None) is None:
-            ws.Xb = torch.zeros((B, C2p), device=self.device, dtype=torch.bfloat16)
-        _ops.cvt_bf16_batch_([X], [ws.Xb], [B, C2, C2, B, C2p, C2p, 0])
-        ws.xb_fresh = True
-
-    def _x_grad_bf16(self, X, ws, gK, bias_out, m0, m1):
-        """The bf16 configuration's x-rows gradient X^T dGsum on gemm_x3p_tn's
-        one-piece form (plain bf16 operands, 128 x 128 tiles): X was
-        converted in the forward (_x_bf16), dGsum is converted here."""
-        B, H, C2 = ws.B, self.rnn_units, self.C2
-        C2p = self._pad8(C2)
-        if m0 == 0:
-            if not getattr(ws, "xb_fresh", False):  # (no conversion in this step's forward)
-                self._x_bf16(X, ws)
-            ws.xb_fresh = False
-            if getattr(ws, "xb_ready", None) is not None:  # (converted on the side stream)
-                torch.cuda.current_stream().wait_event(ws.xb_ready)
-                ws.xb_ready = None
-            if getattr(ws, "dGsumb", None) is None:
-                ws.dGsumb = torch.empty((B, 4 * H), device=self.device, dtype=torch.bfloat16)
-            _ops.cvt_bf16_batch_([ws.dGsum], [ws.dGsumb], [B, 4 * H, 4 * H, B, 4 * H, 4 * H, 0])
-        # split-K 8 at B = 8192, partials summed through the workspace
-        # (scripts/x1_sweep.py, us for 1/2/3/4/6/8 splits: 138/84/77/73/73/72;
-        # with float atomics 77/76/81/88 from 3 splits)
-        with self._timed("lstm_x_projection_grad", ("mfma", 2.0 * B * (m1 - m0) * 4 * H, "bf16")):
-            ops.gemm_x3p_tn(ws.Xb.view(-1)[m0:], 0, ws.dGsumb, 0, gK[m0:m1], m1 - m0, 4 * H, B,
-                            C2p, 4 * H, 4 * H, splitk=self._sk(max(1, min(B // 1024, 8))),
-                            colsum=bias_out, npieces=1)
 
     # ------------------------------------------------------------- API ----
     def _prep(self, images, targets):
@@ -1604,108 +1279,6 @@ class AIRModel:
         self.params.apply_adam(self.hyper("learning_rate"), self.gradient_clipping_norm)
         self.params.global_step += 1
         self._X = X
-
-    # ---------------------------------------------------- graph capture ---
-    # A captured train step (hipGraph through torch.cuda.CUDAGraph): the whole
-    # forward + backward -- ~80 launches, every one of them with arguments that
-    # are the same from step to step -- replays as ONE graph launch.  What
-    # changes per step stays outside the graph or is read from device memory:
-    # the Philox noise fills (their counter offsets advance, eager launches
-    # before the replay; eps_x is filled too instead of being generated inside
-    # the VAE kernels), the annealed z_pres prior log-odds (a device scalar the
-    # step kernels read, filled before the replay) and TF Adam (lr_t from the
-    # fp32 beta powers, an eager launch after it).  The reference's batch of 64
-    # (training_air_original.py:22) is launch-bound without it.
-    _graph_noise = False  # eps_x filled into its buffer (graph mode)
-    _graph_mode = False   # inside train_step_graphed (eager first step, capture, replay)
-    _prior_dev = None     # device z_pres prior log-odds (graph mode only)
-    _prior_dev_val = None  # the value last written there
-    _graph = None
-    _graph_ws = None      # the workspace the graph was captured on (its pointers)
-
-    def _prior_arg(self):
-        """The device prior log-odds the step kernels read instead of the host
-        scalar: only in graph mode, where train_step_graphed refreshes it
-        before every replay.  Eager steps pass the host value (None here), so a
-        stale device value from an earlier graphed step is never read."""
-        return self._prior_dev if self._graph_mode else None
-
-    def _graph_ok(self):
-        others = [k for k in self.annealing_schedules if k != "z_pres_prior_log_odds"]
-        if others:
-            raise NotImplementedError(f"graph mode: annealed {others} would be frozen at capture")
-        if self.grad_reducer is not None or self.live_hook is not None:
-            raise NotImplementedError("graph mode is the single-device train step")
-
-    def train_step_graphed(self, images, targets=None, global_batch: Optional[int] = None) -> None:
-        """train_step_async with the forward + backward replayed from a captured
-        graph; bit-identical to it.  The first call at a batch shape runs the
-        step eagerly and captures the graph (capture executes nothing); later
-        calls copy the inputs into the graph's static buffers and replay."""
-        if not self.train:
-            raise RuntimeError("train_step on a model built with train=False")
-        self._graph_ok()
-        self._graph_mode = self._graph_noise = True
-        try:
-            self._train_step_graphed(images, targets, global_batch)
-        finally:
-            self._graph_mode = self._graph_noise = False
-
-    def _train_step_graphed(self, images, targets, global_batch):
-        X, tg = self._prep(images, targets)
-        key = (tuple(X.shape), None if tg is None else tuple(tg.shape), global_batch)
-        if self._graph is None or self._graph_key != key:
-            self._graph = self._graph_ws = None
-            if self._prior_dev is None:
-                self._prior_dev = torch.zeros(1, device=self.device)
-            self._prior_dev_val = float(self.hyper("z_pres_prior_log_odds"))
-            self._prior_dev.fill_(self._prior_dev_val)
-            self.train_step_async(X, tg, global_batch=global_batch)  # this call's step
-            self._capture(X, tg, global_batch)
-            self._graph_key = key
-            return
-        gX, gT = self._graph_io
-        if X.data_ptr() != gX.data_ptr():
-            gX.copy_(X)
-        if tg is not None and tg.data_ptr() != gT.data_ptr():
-            gT.copy_(tg)
-        # The graph holds raw pointers into the workspace it was captured on:
-        # replay on that one (kept alive by _graph_ws), even when an infer /
-        # step / compute_gradients at another batch has replaced self._ws since
-        ws = self._ws = self._graph_ws
-        self._fill_noise(ws, None)
-        if ws.noise_side:  # the graph's first launch reads it
-            torch.cuda.current_stream().wait_stream(self._side_stream())
-            ws.noise_side = False
-        lo = float(self.hyper("z_pres_prior_log_odds"))
-        if lo != self._prior_dev_val:  # (a fill launch only when the value moves)
-            self._prior_dev.fill_(lo)
-            self._prior_dev_val = lo
-        self._graph.replay()
-        self.params.apply_adam(self.hyper("learning_rate"), self.gradient_clipping_norm)
-        self.params.global_step += 1
-        self._X = gX
-        self._loss_inputs = (gX, gT)
-        ws.materialized = False
-        self._outputs_ready = True
-
-    def _capture(self, X, tg, global_batch):
-        ws = self._ws
-        gX = X.clone()
-        gT = tg.clone() if tg is not None else None
-        self._graph_io = (gX, gT)
-        # the weight packs are refreshed by a launch inside the graph on every
-        # replay (the parameters change every step): force it to be recorded
-        self._pack_version = self._pack32_version = self._w1cat_version = None
-        self._w3_version = None
-        torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
-        self._global_batch = global_batch
-        with torch.cuda.graph(g):
-            self._forward(gX, gT, ws, need_grad=True, outputs=False)
-            self._backward(gX, ws)
-        self._graph = g
-        self._graph_ws = ws
 
     def step(self, images, targets=None, noise=None, global_batch: Optional[int] = None):
         """``sess.run([training, loss, accuracy, mse_loss, global_step])``
@@ -1743,148 +1316,3 @@ class AIRModel:
         self._forward(X, tg, ws, need_grad=False)
         self._X = X
         return self
-
-    # ---------------------------------------------------- generation -------
-    def generate(self, num_steps: int, batch: Optional[int] = None, noise=None):
-        """The test model's ``generated_samples`` (air_model.py:1001-1146):
-        ``num_steps`` objects per canvas (``max_steps_generation_placeholder``),
-        each with prior-sampled scale / shift / latent, decoded by the
-        generative VAE (vae.py:51-86, sigmoid of mean + std * eps) and
-        STN-written; the canvas sums every step's window.  Returns the canvas
-        [G, C, C, 1]; ``generated_st_back`` [G, T, 2, 3] and
-        ``generated_num_digits`` [G] hold the loop's other outputs.  ``noise``
-        (optional) injects eps_scale [T,G], eps_shift [T,G,2], eps_z [T,G,Z],
-        eps_x [T,G,784]; otherwise device Philox noise is drawn.  Runs the
-        fp32 decoder GEMMs in either precision."""
-        G = int(batch if batch is not None else self.generation_batch_size)
-        T, C, W2, Z = int(num_steps), self.canvas_size, self.W2, self.vae_latent_dimensions
-        G1, G2 = self.vae_generative_units
-        dev = self.device
-        e = lambda *sh: torch.empty(sh, device=dev, dtype=torch.float32)  # noqa: E731
-        eps = {"eps_scale": e(T, G), "eps_shift": e(T, G, 2), "eps_z": e(T, G, Z),
-               "eps_x": e(T, G, W2)}
-        for k, buf in eps.items():
-            if noise is not None:
-                buf.copy_(torch.as_tensor(noise[k], dtype=torch.float32))
-            else:
-                ops.rng_fill(buf, self.noise_seed, self._noise_ctr, True)
-                self._noise_ctr += (buf.numel() + 3) // 4
-        canvas = torch.zeros((G, C * C), device=dev, dtype=torch.float32)
-        st_back = e(T, G, 6)
-        scale, shift, z = e(G), e(G, 2), e(G, Z)
-        d1, d2, r = e(G, G1), e(G, G2), e(G, W2)
-        ones = torch.ones(G, device=dev, dtype=torch.float32)
-        vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
-        vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
-        lik_std = float(self.hyper("vae_likelihood_std"))
-        for t in range(T):
-            _ops.generation_prior_(G, Z, float(self.scale_prior_mean),
-                                   self.scale_prior_log_variance, float(self.shift_prior_mean),
-                                   self.shift_prior_log_variance, float(self.vae_prior_mean),
-                                   self.vae_prior_log_variance, eps["eps_scale"][t],
-                                   eps["eps_shift"][t], eps["eps_z"][t], st_back[t], scale, shift,
-                                   z)
-            gemm([z], [vw["generative_1"]], [d1], G, G1, Z, Z, G1, G1, epi=EPI_SOFTPLUS,
-                 bias=[vb["generative_1"]])
-            gemm([d1], [vw["generative_2"]], [d2], G, G2, G1, G1, G2, G2, epi=EPI_SOFTPLUS,
-                 bias=[vb["generative_2"]])
-            gemm([d2], [vw["gen_mean"]], [r], G, W2, G2, G2, W2, W2, epi=EPI_SIGMOID_NOISE,
-                 bias=[vb["gen_mean"]], aux=[eps["eps_x"][t]], ldaux=W2, aux_scale=lik_std)
-            # every step is written (the stopping sum stays 0 < threshold, :1085-1097)
-            ops.stn_forward(r, st_back[t], (C, C), out=canvas, z=ones, mask=ones,
-                            accumulate=True)
-        self.generated_st_back = st_back.transpose(0, 1).reshape(G, T, 2, 3)
-        self.generated_num_digits = torch.full((G,), T, device=dev, dtype=torch.int32)
-        self.generated_samples = canvas.reshape(G, C, C, 1)
-        return self.generated_samples
-
-    # ------------------------------------------------------- outputs -------
-    def _T(self) -> int:
-        live = self._ws.live.detach().cpu().numpy()
-        return int(live[: self.max_steps].sum())
-
-    def _bt(self, t: torch.Tensor) -> torch.Tensor:
-        T = self._T()
-        return t[:T].transpose(0, 1)
-
-    @property
-    def executed_steps(self) -> int:
-        return self._T()
-
-    @property
-    def loss(self):
-        return float(self._ws.means[0])
-
-    @property
-    def accuracy(self):
-        return float(self._ws.means[1])
-
-    @property
-    def mse_loss(self):
-        return float(self._ws.means[2])
-
-    @property
-    def rec_num_digits(self):
-        return self._ws.digits
-
-    @property
-    def accuracy_instance(self):
-        return self._ws.acc_b
-
-    @property
-    def rec_scales(self):
-        return self._bt(self._ws.scale).unsqueeze(-1)
-
-    @property
-    def rec_shifts(self):
-        return self._bt(self._ws.shift)
-
-    @property
-    def rec_st_back(self):
-        return self._bt(self._ws.th_b).reshape(self._ws.B, -1, 2, 3)
-
-    @property
-    def rec_windows(self):
-        return self._bt(self._ws.r)
-
-    @property
-    def rec_latents(self):
-        return self._bt(self._ws.z)
-
-    @property
-    def z_pres_probs(self):
-        return self._bt(self._ws.zprob)
-
-    @property
-    def z_pres_kls(self):
-        return self._bt(self._ws.zkl)
-
-    @property
-    def scale_kls(self):
-        return self._bt(self._ws.skl)
-
-    @property
-    def shift_kls(self):
-        return self._bt(self._ws.shkl)
-
-    @property
-    def vae_kls(self):
-        return self._bt(self._ws.vkl)
-
-    @property
-    def reconstruction(self):
-        self._materialize()
-        return self._ws.recon
-
-    @property
-    def reconstruction_loss(self):
-        return self._ws.bce
-
-    @property
-    def canvas(self):
-        self._materialize()
-        return self._ws.canvas
-
-    @property
-    def per_image_loss(self):
-        return self._ws.loss_b

@@ -21,19 +21,17 @@ steps at the end, as the reference's TensorArrays are (:917-923).
 """
 from __future__ import annotations
 
-import os
-from typing import Dict, Optional, Sequence
+from typing import Dict
 
-import numpy as np
 import torch
 
 from . import _lib, ops
 from .air_model import AIRModel as _AirBase
-from .air_model import _SCOPES, _Workspace, _f32log, annealed_value
+from .air_model import _SCOPES, _Workspace, _f32log
 from .ops import EPI_RELU, EPI_STORE, gemm
+from .params import ParamStore
 
 _ops = ops._ops  # torch.ops.mog_air (csrc/torch_ops.cpp)
-from .params import ParamStore
 
 # asr_cell.hip record slots
 Q = {n: i for i, n in enumerate(
@@ -165,8 +163,7 @@ class AIRModel(_AirBase):
         # fp32: the fused fp32 step kernel per loop step (AIRModel._vae_forward_all)
         self.fused_f32 = bool(fused_step) and precision == "fp32" and (
             windows_size == 28 and tuple(vae_recognition_units) == (512, 256)
-            and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512)
-            and os.environ.get("MOG_FUSED_F32", "1") != "0")
+            and vae_latent_dimensions == 50 and tuple(vae_generative_units) == (256, 512))
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         if self.device.type != "cuda":
             raise RuntimeError("AIRModel runs on a HIP device only (no CPU fallback)")
@@ -317,7 +314,7 @@ class AIRModel(_AirBase):
 
     def _x3_asr(self, B: int) -> bool:
         """fp32: the inference LSTM's x-rows weight gradient X^T dGsum on the
-        three-piece bf16-core form (MOG_X_GRAD_X3=2, the default, as for AIR)
+        three-piece bf16-core form (X_GRAD_X3 = 2, the default, as for AIR)
         from the batch where the side stream pays (SIDE_MIN_BATCH)."""
         return self.precision == "fp32" and self.X_GRAD_X3 == 2 and B >= self.SIDE_MIN_BATCH
 
@@ -430,8 +427,8 @@ class AIRModel(_AirBase):
 
     # fp32 below FUSED_F32_MIN_ROWS: the generative half of each step's VAE
     # (which feeds only the canvas, never the loop) after the loop, over T*B
-    # rows (MOG_ASR_DEFER_DECODER=0: inside the loop, step by step)
-    DEFER_DECODER = os.environ.get("MOG_ASR_DEFER_DECODER", "1") == "1"
+    # rows (DEFER_DECODER = False: inside the loop, step by step)
+    DEFER_DECODER = True
 
     def _forward_loss(self, X, targets, ws, need_grad, outputs=True):
         """elbo (:917-935, recon :937-962) + pr_loss + element + margin
@@ -470,10 +467,17 @@ class AIRModel(_AirBase):
         # launches at the end (as AIRModel._backward)
         self._wgroup = (self._wgroup_obj if (self.WGRAD_GROUP and ws.B < self.SIDE_MIN_BATCH
                                              and self.grad_reducer is None) else None)
+        wg = self._wgroup
+        if wg is not None:
+            wg.probs = []  # (a fresh collection: nothing left from a failed step)
         try:
             self._backward_body(X, ws)
+        except BaseException:
+            if wg is not None:
+                wg.probs = []  # a failed body's partial problems never launch
+            raise
         finally:
-            wg, self._wgroup = self._wgroup, None
+            self._wgroup = None
             ws.dm_ready = ws.dec_ready = False
         if wg is not None and wg.probs:
             flops = sum(2.0 * p[4] * p[5] * p[6] for p in wg.probs)
@@ -596,7 +600,7 @@ class AIRModel(_AirBase):
             splitk = self._sk(max(1, min(K // 256, (512 + tiles - 1) // tiles)))
             for U, dG, out, bias in ((v(ws.U), v(ws.dG), gKi[self.C2:], None),
                                      (v(ws.Ug), v(ws.dGg), gKg, self._Ng("gen_rnn_running/bias"))):
-                with self._timed("rec_wgrad_x3", ("mfma", 12.0 * K * LU * 4 * H, "bf16")):
+                with self._timed("rec_wgrad_x3", ("mfma", 2.0 * K * LU * 4 * H, "fp32", "x3")):
                     ops.gemm_x3_tn(U, dG, out, LU, 4 * H, K, LU, 4 * H, 4 * H, splitk=splitk,
                                    colsum=bias, reduce=False)
             return
@@ -607,13 +611,13 @@ class AIRModel(_AirBase):
     # (with VAE_WGRAD_PER_STEP) the recurrent-rows gradients per step too (9.20 ->
     # 8.96 ms; the heads' gradients per step as well measured neutral, 9.01 vs
     # 9.26 ms for neither on a slower box, and stay after the loop)
-    U_WGRAD_PER_STEP = os.environ.get("MOG_ASR_UGRAD_STEPS", "1") == "1"
+    U_WGRAD_PER_STEP = True
 
     # one GPU, from SIDE_MIN_BATCH: the VAE weight gradients of loop step
     # t accumulate on the side stream as soon as that step's VAE backward is
     # done, under the latency-bound rest of the reversed loop, instead of over
-    # all T*B rows after it (MOG_ASR_WGRAD_STEPS=0: after the loop)
-    VAE_WGRAD_PER_STEP = os.environ.get("MOG_ASR_WGRAD_STEPS", "1") == "1"
+    # all T*B rows after it (VAE_WGRAD_PER_STEP = False: after the loop)
+    VAE_WGRAD_PER_STEP = True
     _VAE_WGRAD_LAYERS = ("recognition_1", "recognition_2", "rec_mean", "generative_1",
                          "generative_2", "gen_mean")
 
@@ -650,7 +654,7 @@ class AIRModel(_AirBase):
                 ws.dG3 = torch.empty((3, B, 4 * H), device=self.device, dtype=torch.bfloat16)
             ops.split3_bf16(ws.dGsum, ws.dG3, B, 4 * H, 4 * H, 4 * H, B * 4 * H)
             C2p = self._pad8(C2)
-            with self._timed("lstm_x_projection_grad", ("mfma", 12.0 * B * C2 * 4 * H, "bf16")):
+            with self._timed("lstm_x_projection_grad", ("mfma", 2.0 * B * C2 * 4 * H, "fp32", "x3")):
                 ops.gemm_x3p_tn(ws.X3.view(-1), B * C2p, ws.dG3, B * 4 * H, gKi[:C2], C2, 4 * H,
                                 B, C2p, 4 * H, 4 * H,
                                 splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
@@ -670,7 +674,7 @@ class AIRModel(_AirBase):
             self._heads_wgrad(ws, None)
 
     # (with the per-step gradients) the heads' gradients on the third stream
-    HEADS_S3 = os.environ.get("MOG_ASR_HEADS_S3", "1") == "1"
+    HEADS_S3 = True
 
     def _heads_wgrad(self, ws, t):
         """The heads' weight gradients (all T*B rows, or loop step t's B rows,

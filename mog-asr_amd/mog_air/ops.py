@@ -292,21 +292,17 @@ def rng_fill(out: torch.Tensor, seed: int, offset: int, normal: bool) -> None:
 
 def spin(ticks: int, device=None) -> None:
     """Hold the current stream for `ticks` of the 100 MHz wall clock (test
-    instrument, mog_spin)."""
-    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
-    global _SPIN_ANCHOR
-    if ticks == 0 and _SPIN_ANCHOR is not None:
+    instrument mog_spin of libmog_air_test.so)."""
+    if ticks == 0:
         return
-    if _SPIN_ANCHOR is None or _SPIN_ANCHOR.device != torch.device(dev):
-        _SPIN_ANCHOR = torch.empty(1, device=dev)
-    _ops.spin_(_SPIN_ANCHOR, int(ticks))
+    rc = _lib.load_test().mog_spin(int(ticks), stream_ptr())
+    if rc != 0:
+        raise _lib.MogError(f"mog_spin failed ({rc})")
 
 
 def lds_poison(bits: int = 0x7FC00000) -> None:
     """Fill every CU's LDS with a 32-bit pattern on the current stream (test
-    instrument, mog_lds_poison; default a quiet NaN)."""
-    spin(0)
-    _ops.lds_poison_(_SPIN_ANCHOR, int(bits))
-
-
-_SPIN_ANCHOR = None
+    instrument mog_lds_poison of libmog_air_test.so; default a quiet NaN)."""
+    rc = _lib.load_test().mog_lds_poison(int(bits) & 0xFFFFFFFF, stream_ptr())
+    if rc != 0:
+        raise _lib.MogError(f"mog_lds_poison failed ({rc})")

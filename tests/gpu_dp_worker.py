@@ -5,10 +5,15 @@ contiguous shard of the batch through ``compute_gradients`` with
 ``parallel.attach`` installed (bucketed async all-reduce, global loop
 predicate, ASR batch-mean hook) and saves what it saw.
 
-Kinds: air / asr (13 / 11 images: odd shards, the per-step VAE path) and
+Kinds: air / asr (13 / 11 images: odd shards, the per-step VAE path),
 air64 / air64b (128 images, 64-row shards, fp32 / bf16: the batched T*B-row
-VAE, the VAE weight gradients on the side stream joined before the bucket
-all-reduce -- the configuration bench.py and the trainer run).
+VAE; below AIRModel.SIDE_MIN_BATCH every launch stays on the main stream)
+and air1k / asr1k (2,048 images, 1,024 per rank, AIR without ``-ap`` as
+bench.py runs it, and AIR-ASR: from SIDE_MIN_BATCH the VAE weight gradients
+fork to the side stream and the main stream joins them (vae_done) before the
+glimpse bucket's all-reduce -- air_model.py _vae_weight_grads_async /
+_backward_body; the x3 weight gradients and the pre-split x-rows gradient
+run at these sizes too).
 
 Kind rccl1: ONE rank over RCCL (backend "nccl" on the HIP device; RCCL
 refuses two ranks on one GPU, so a one-GPU box can only run it at world 1),
@@ -17,7 +22,7 @@ installs nothing at world 1): the bucketed async all-reduces and the MAX
 all-reduce of the live flag go through RCCL on the device exactly as on an
 8-GPU node, and the gradient must equal the no-reducer run bit for bit.
 
-usage: gpu_dp_worker.py <out_prefix> air|asr|air64|air64b|rccl1"""
+usage: gpu_dp_worker.py <out_prefix> air|asr|air64|air64b|air1k|asr1k|rccl1"""
 import os
 import sys
 
@@ -34,12 +39,13 @@ from mog_air import parallel  # noqa: E402
 DEV = "cuda:0"
 
 
-BATCH = {"air": 13, "asr": 11, "air64": 128, "air64b": 128, "rccl1": 128}
+BATCH = {"air": 13, "asr": 11, "air64": 128, "air64b": 128, "rccl1": 128, "air1k": 2048,
+         "asr1k": 2048}
 
 
-def air_case(batch=13):
+def air_case(batch=13, num_prior=(1, 3)):
     from oracle import air_oracle as ao
-    cfg = ao.AirConfig(batch=batch, max_steps=3, train=True, num_prior=(1, 3),
+    cfg = ao.AirConfig(batch=batch, max_steps=3, train=True, num_prior=num_prior,
                        scale_prior_variance=0.05, z_pres_prior_log_odds=-0.01)
     P = ao.init_params(cfg, seed=71, bias_scale=0.05)
     nz = ao.make_noise(cfg, seed=72)
@@ -62,10 +68,10 @@ def air_model(cfg, P, world, scope, precision="fp32"):
     return m
 
 
-def asr_case():
+def asr_case(batch=11):
     from oracle import air_oracle as ao
     from oracle import asr_oracle as so
-    cfg = so.AsrConfig(batch=11, max_steps=4, constrains_num=(1, 3), constrains_num_gamma=0.5,
+    cfg = so.AsrConfig(batch=batch, max_steps=4, constrains_num=(1, 3), constrains_num_gamma=0.5,
                        constrains_margin_gamma=100.0, constrains_num_element_gamma=10.0,
                        constrains_bbox_gamma=1.0, constrains_sharesize_gamma=0.3,
                        constrains_area_gamma=0.2, constrains_area_minmax=(17.0, 23.0),
@@ -99,11 +105,11 @@ def asr_model(cfg, P, world, scope):
 
 def run(kind, lo, hi, world, scope, attach=True):
     """compute_gradients on images [lo, hi) of the case; returns a dict."""
-    if kind == "asr":
-        cfg, P, nz, x, k, G = asr_case()
+    if kind.startswith("asr"):
+        cfg, P, nz, x, k, G = asr_case(BATCH[kind])
         m = asr_model(cfg, P, world, scope)
     else:
-        cfg, P, nz, x, k, G = air_case(BATCH[kind])
+        cfg, P, nz, x, k, G = air_case(BATCH[kind], None if kind == "air1k" else (1, 3))
         m = air_model(cfg, P, world, scope, "bf16" if kind == "air64b" else "fp32")
     reducer = None
     if attach and world > 1:
@@ -126,9 +132,11 @@ def run(kind, lo, hi, world, scope, attach=True):
            "mean": np.array([m.loss])}
     if reducer is not None:
         out["buckets"] = np.array(reducer.log)
-    if kind == "asr":
+    if kind.startswith("asr"):
         out["margin"] = m._ws.margin.cpu().numpy()
     out["batched"] = np.array([int(getattr(m, "_batched_vae", lambda b: False)(hi - lo))])
+    # the side-stream fork of the VAE weight gradients (AIRModel.SIDE_MIN_BATCH)
+    out["side"] = np.array([int(hi - lo >= m.SIDE_MIN_BATCH)])
     return out
 
 

@@ -113,3 +113,71 @@ def test_small_batch_step_has_no_fork():
     torch.cuda.synchronize()
     assert forks == []
     assert np.isfinite(float(m._ws.means[0]))
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_fused_step_kernels_beside_mfma_gemms(precision):
+    """The fused STN-read -> VAE -> STN-write kernels (csrc/vae_step.hip) are
+    built WITH compiler-packed fp32 (v_pk_*_f32) arithmetic, which DESIGN.md
+    §2 found to return wrong halves when bf16 MFMA waves of another kernel
+    shared the CU.  Their launches request the CU's whole 160 KiB of LDS
+    (vae_step.hip lds_pad), so no GEMM workgroup can share a CU with them.
+    Launched on the main stream while the bf16 TN / NT and x3 TN / NT GEMMs
+    that triggered the fault run on the side stream (staggered by a spin so
+    the launches overlap at different points), every output of 8 such launches
+    must equal the launch run alone, bit for bit: r, z, the VAE KL, the canvas
+    parts and their row ranges (B = 8192: the train step's T*B = 24,576 rows,
+    three rounds of tiles over the CUs)."""
+    from mog_air import ops
+    from mog_air.ops import BF_ATOMIC, BF_STORE, gemm_bf16
+    B = 8192
+    m = _air(f"fx_{precision}", precision)
+    (x, k), = _data(B, 1)
+    m.infer(x, k)
+    torch.cuda.synchronize()
+    ws = m._ws
+    assert m._batched_vae(B) and ws.cparts is not None
+    if precision == "fp32":
+        assert m.fused_f32 and 3 * B >= m.FUSED_F32_MIN_ROWS
+    outs = ("r", "z", "vkl", "cparts", "prows")
+
+    def launch():
+        m._vae_forward_all(x, ws, 0.3, save=True)
+        return {n: getattr(ws, n).clone() for n in outs}
+
+    ref = launch()
+    torch.cuda.synchronize()
+    TB, dev = 3 * B, torch.device(DEV)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    Xf = torch.randn(TB, 784, generator=g).to(dev)
+    Yf = torch.randn(TB, 512, generator=g).to(dev)
+    Xb, Yb = Xf.bfloat16(), Yf.bfloat16()
+    Wb = torch.randn(512, 784, generator=g).to(dev).bfloat16()
+    W3 = torch.empty((3, 512, 784), device=dev, dtype=torch.bfloat16)
+    ops.split3_bf16(Wb.float(), W3, 512, 784, 784, 784, 512 * 784)
+    acc = torch.zeros(784, 512, device=dev)
+    outb = torch.zeros(TB, 512, device=dev)
+    outx = torch.zeros(TB, 784, device=dev)
+    aggressors = [
+        lambda: gemm_bf16([Xb], [Yb], [acc], 784, 512, TB, 784, 512, 512, tn=True, epi=BF_ATOMIC,
+                          splitk=4),
+        lambda: gemm_bf16([Xb], [Wb], [outb], TB, 512, 784, 784, 784, 512, epi=BF_STORE),
+        lambda: ops.gemm_x3_tn(Xf, Yf, acc, 784, 512, TB, 784, 512, 512, splitk=8, reduce=False),
+        lambda: ops.gemm_x3_nt(Yf, W3, 512 * 784, outx, TB, 784, 512, 512, 512, 784),
+    ]
+    main, side = torch.cuda.current_stream(), m._side_stream()
+    for r in range(8):
+        ev = torch.cuda.Event()
+        ev.record(main)
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                for fn in aggressors:
+                    fn()
+        ops.spin(20_000 * r)  # the fused launch lands at a different point each time
+        got = launch()
+        torch.cuda.synchronize()
+        for n in outs:
+            a, b = got[n], ref[n]
+            iv = torch.int32
+            assert torch.equal(a.view(iv), b.view(iv)), (n, r)

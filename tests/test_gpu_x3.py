@@ -230,7 +230,7 @@ def test_x3p_splitk_reduce_deterministic(npieces):
     B3 = torch.empty(3, K, 264, device=DEV, dtype=torch.bfloat16)
     ops.split3_bf16(A, A3, K, 304, 304, 304, K * 304)
     ops.split3_bf16(B, B3, K, N, N, 264, K * 264)
-    outs = []
+    outs, sums = [], []
     for red in (True, True, False):
         C = torch.ones(M, N, device=DEV)
         cs = torch.ones(N, device=DEV)
@@ -238,5 +238,33 @@ def test_x3p_splitk_reduce_deterministic(npieces):
                         colsum=cs, npieces=npieces, reduce=red)
         torch.cuda.synchronize()
         outs.append(C.cpu())
+        sums.append(cs.cpu())
     assert torch.equal(outs[0], outs[1])
+    # the column sums (the bias gradient) too: per-split partials added in
+    # split order by the reduce launch, no float atomics
+    assert torch.equal(sums[0], sums[1])
     assert float((outs[0] - outs[2]).abs().max()) <= 1e-5 * float(outs[2].abs().max())
+    Bd = (B3[0].double() + B3[1].double() + B3[2].double())[:, :N] if npieces == 3 else \
+        B3[0].double()[:, :N]
+    ref = 1.0 + Bd.sum(0).cpu()
+    assert float((sums[0].double() - ref).abs().max()) <= 1e-6 * float(Bd.abs().sum(0).max())
+
+
+def test_x3_tn_splitk_reduce_deterministic_colsum():
+    """The in-kernel-split TN form through the workspace: C and the column
+    sums bit-identical over two launches, and against float64."""
+    M, N, K = 260, 300, 5000
+    g = torch.Generator().manual_seed(8)
+    A = torch.randn(K, M, generator=g).to(DEV)
+    B = torch.randn(K, N, generator=g).to(DEV)
+    res = []
+    for _ in range(2):
+        C = torch.zeros(M, N, device=DEV)
+        cs = torch.zeros(N, device=DEV)
+        ops.gemm_x3_tn(A, B, C, M, N, K, M, N, N, splitk=9, colsum=cs, reduce=True)
+        torch.cuda.synchronize()
+        res.append((C.cpu(), cs.cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    Ad, Bd = A.double().cpu(), B.double().cpu()
+    assert _err(res[0][0], Ad.T @ Bd, Ad.abs().T @ Bd.abs()) <= 1e-6
+    assert _err(res[0][1], Bd.sum(0), Bd.abs().sum(0)) <= 1e-6

@@ -26,6 +26,21 @@ def test_library_exports_every_header_symbol():
     assert set(syms) == set(_lib._SIGS)
 
 
+def test_test_instruments_live_outside_the_product_library():
+    """mog_spin / mog_lds_poison (include/mog_air_test.h) are exported by
+    libmog_air_test.so only: the product library carries no test kernels."""
+    import re
+    from mog_air import _lib
+    with open(os.path.join(ROOT, "include", "mog_air_test.h")) as f:
+        src = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    syms = sorted(set(re.findall(r"\bint\s+(mog_\w+)\s*\(", src)))
+    assert syms == sorted(_lib._TEST_SIGS)
+    test_lib, lib = _lib.load_test(), _lib.load()
+    for s in syms:
+        assert hasattr(test_lib, s), s
+        assert not hasattr(lib, s), s
+
+
 def test_library_built_from_these_sources():
     """Build provenance: the source hash compiled into libmog_air.so
     (mog_build_id) equals the hash of the sources beside it, which
@@ -36,14 +51,17 @@ def test_library_built_from_these_sources():
 
 
 def test_all_headers_symbols_exported():
+    """Every include/*.h entry point is exported: the product headers by
+    libmog_air.so, include/mog_air_test.h by libmog_air_test.so."""
     from mog_air import _lib
     lib = ctypes.CDLL(_lib.LIB_PATH)
+    test_lib = ctypes.CDLL(_lib.TEST_LIB_PATH)
     inc = os.path.join(ROOT, "include")
     for fn in os.listdir(inc):
         src = open(os.path.join(inc, fn)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         for name in re.findall(r"\bint\s+(mog_\w+)\s*\(", src):
-            assert hasattr(lib, name), (fn, name)
+            assert hasattr(test_lib if fn == "mog_air_test.h" else lib, name), (fn, name)
 
 
 def test_torch_ops_extension_registers_every_launch_op():
