@@ -72,6 +72,8 @@ KERNEL_NAMES = {
     "rec_wgrad_x3": "gemm_x3_tn_kernel<false,3>: LSTM recurrent-rows weight gradient (bf16 cores, "
                     "3-piece)",
     "wgrad_bf16": "gemm_bf16 TN: bf16 VAE weight gradients",
+    "vae_wgrad_bf16": "wgrad_tn_bf16_kernel (+ its split reduction): the seven bf16 VAE weight "
+                      "gradients in one launch",
     "wgrad_group": "wgrad_group_kernel: every fp32-chain weight gradient of a small-batch step, "
                    "one launch",
     "stn_write_bwd": "stn_bwd_kernel: STN write backward (through the output sigmoid)",

@@ -88,6 +88,20 @@ int mog_build_id(char* out, int cap);
  * :454-456, K = the batch rows). */
 int mog_gemm_f32_wgrad_group(const long long* table, int nprob, void* stream);
 
+/* Grouped tall-K weight gradients on bf16 operands (the bf16 configuration's
+ * VAE weight / bias gradients, the MatMul / BiasAdd gradients of
+ * vae.py:18-46 over all T*B rows): for each problem i < nprob <= 8,
+ * out_i[M][N] (ldc) += X_i^T dY_i over K rows and colsum_i[N] += the column
+ * sums of dY_i (colsum or colsum[i] may be NULL), X_i [K][lda], dY_i [K][ldb]
+ * bf16, 16-byte aligned, lda / ldb multiples of 8, K x ld elements readable.
+ * dims: (M, N, lda, ldb, ldc) per problem.  The K rows are cut into nsplit
+ * splits whose partial tiles go to `work` (>= mog_wgrad_tn_work_elems floats)
+ * and are added in split order by a second launch: deterministic. */
+long mog_wgrad_tn_work_elems(int nprob, const int* dims, int nsplit);
+int mog_wgrad_tn_bf16(int nprob, const void* const* X, const void* const* dY, float* const* out,
+                      float* const* colsum, const int* dims, int K, int nsplit, float* work,
+                      long work_elems, void* stream);
+
 /* dX = epi(dY W^T) at fp32-level accuracy on the bf16 matrix cores (the VAE
  * input gradients; replaces the MatMul gradients of vae.py:18-46's dense
  * layers w.r.t. their inputs): C[M][N] = sum_k A[m][k] B[n][k], A fp32 [M][lda]

@@ -997,16 +997,71 @@ void gemm_x3p_tn_(const Tensor& A3, int64_t sa, const Tensor& B3, int64_t sb, Te
         o.name);
 }
 
-// the problem table holds device pointers the caller validated
-// (mog_air.ops.WgradGroup checks every operand's extent before building it)
-void gemm_f32_wgrad_group_(at::IntArrayRef table, const Tensor& anchor) {
-  Op o("gemm_f32_wgrad_group_");
-  TORCH_CHECK(table.size() % 10 == 0, o.name, ": table of 10 int64 per problem");
-  o.need(anchor, F32, 0, "anchor");  // fixes the device (and stream) of the launch
+// the grouped tall-K bf16 weight gradients (wgrad_tn.hip): out[i] += X[i]^T
+// dY[i] over K rows, colsum[i] += column sums of dY[i]; dims holds (M, N,
+// lda, ldb, ldc) per problem.  The kernel reads whole k-rows of both operands
+// (K x ld elements each); the [nsplit][tiles] partial workspace is a transient
+// of the caching allocator on the op's stream.
+void wgrad_tn_bf16_(at::TensorList X, at::TensorList dY, at::TensorList out,
+                    const c10::List<optional<Tensor>>& colsum, at::IntArrayRef dims, int64_t K,
+                    int64_t nsplit) {
+  Op o("wgrad_tn_bf16_");
+  const size_t n = out.size();
+  TORCH_CHECK(n >= 1 && n <= 8 && X.size() == n && dY.size() == n && colsum.size() == n &&
+                  dims.size() == 5 * n,
+              o.name, ": 1-8 problems, X / dY / out / colsum of one length n, 5 n dims");
+  vector<void*> xs, ys, os, cs;
+  vector<int> d;
+  for (size_t i = 0; i < n; ++i) {
+    const int64_t M = dims[5 * i], N = dims[5 * i + 1], lda = dims[5 * i + 2],
+                  ldb = dims[5 * i + 3], ldc = dims[5 * i + 4];
+    TORCH_CHECK(M > 0 && N > 0 && lda >= M && ldb >= N && ldc >= N, o.name,
+                ": bad dims of problem ", i);
+    os.push_back(o.f(out[i], mat(M, N, ldc), "out"));
+    xs.push_back(o.need(X[i], BF16, K * lda, "X"));
+    ys.push_back(o.need(dY[i], BF16, K * ldb, "dY"));
+    cs.push_back(o.f(static_cast<optional<Tensor>>(colsum[i]), N, "colsum"));
+    for (int64_t v : {M, N, lda, ldb, ldc}) d.push_back((int)v);
+  }
   GUARD(o);
-  check(mog_gemm_f32_wgrad_group(reinterpret_cast<const long long*>(table.data()),
-                                 (int)(table.size() / 10), o.stream()),
+  const long we = mog_wgrad_tn_work_elems((int)n, d.data(), (int)nsplit);
+  TORCH_CHECK(we > 0, o.name, ": bad problem set");
+  Tensor w = at::empty({we}, at::TensorOptions().dtype(F32).device(*o.dev));
+  check(mog_wgrad_tn_bf16((int)n, arr<void>(xs), arr<void>(ys), marr<float>(os),
+                          marr<float>(cs), d.data(), (int)K, (int)nsplit, w.data_ptr<float>(), we,
+                          o.stream()),
         o.name);
+}
+
+// out[i][M,N] += X[i]^T dY[i] over K rows (+ bias[i] += colsum(dY[i])) for
+// every problem i in ONE launch; dims holds (M, N, K, lda, ldb, ldc) per
+// problem.  Every operand is checked for the extent its problem touches and
+// the written ones are alias-annotated in the schema; the device pointer table
+// of the C ABI is built here.
+void gemm_f32_wgrad_group_(at::TensorList X, at::TensorList dY, at::TensorList out,
+                           const c10::List<optional<Tensor>>& bias, at::IntArrayRef dims) {
+  Op o("gemm_f32_wgrad_group_");
+  const size_t n = out.size();
+  TORCH_CHECK(n > 0 && X.size() == n && dY.size() == n && bias.size() == n && dims.size() == 6 * n,
+              o.name, ": X, dY, out, bias of one length n and 6 n dims");
+  vector<long long> table;
+  table.reserve(10 * n);
+  for (size_t i = 0; i < n; ++i) {
+    const int64_t M = dims[6 * i], N = dims[6 * i + 1], K = dims[6 * i + 2];
+    const int64_t lda = dims[6 * i + 3], ldb = dims[6 * i + 4], ldc = dims[6 * i + 5];
+    TORCH_CHECK(M > 0 && N > 0 && K >= 0 && lda >= M && ldb >= N && ldc >= N, o.name,
+                ": bad dims of problem ", i);
+    void* c = o.f(out[i], mat(M, N, ldc), "out");
+    void* a = o.f(X[i], mat(K, M, lda), "X");
+    void* b = o.f(dY[i], mat(K, N, ldb), "dY");
+    void* bi = o.f(static_cast<optional<Tensor>>(bias[i]), N, "bias");
+    for (long long v : {(long long)(uintptr_t)a, (long long)(uintptr_t)b, (long long)(uintptr_t)c,
+                        (long long)(uintptr_t)bi, (long long)M, (long long)N, (long long)K,
+                        (long long)lda, (long long)ldb, (long long)ldc})
+      table.push_back(v);
+  }
+  GUARD(o);
+  check(mog_gemm_f32_wgrad_group(table.data(), (int)n, o.stream()), o.name);
 }
 
 void gemm_x3_nt_(const Tensor& A, const Tensor& B3, int64_t sb, Tensor C,
@@ -1025,7 +1080,12 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
   m.def(
       "gemm_x3_nt_(Tensor A, Tensor B3, int sb, Tensor(a!) C, Tensor? aux, int M, int N, int K, "
       "int lda, int ldb, int ldc, int ldaux, int epi) -> ()");
-  m.def("gemm_f32_wgrad_group_(int[] table, Tensor anchor) -> ()");
+  m.def(
+      "gemm_f32_wgrad_group_(Tensor[] X, Tensor[] dY, Tensor(a!)[] out, Tensor(b!)?[] bias, "
+      "int[] dims) -> ()");
+  m.def(
+      "wgrad_tn_bf16_(Tensor[] X, Tensor[] dY, Tensor(a!)[] out, Tensor(b!)?[] colsum, int[] dims, "
+      "int K, int nsplit) -> ()");
   m.def(
       "split3_bf16_(Tensor src, Tensor(a!) dst, int rows, int cols, int ld_src, int ld_dst, "
       "int piece_stride) -> ()");
@@ -1186,6 +1246,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("gemm_x3_nt_", &gemm_x3_nt_);
   m.impl("gemm_x3p_tn_", &gemm_x3p_tn_);
   m.impl("gemm_f32_wgrad_group_", &gemm_f32_wgrad_group_);
+  m.impl("wgrad_tn_bf16_", &wgrad_tn_bf16_);
   m.impl("gemm_bf16_", &gemm_bf16_);
   m.impl("cvt_bf16_batch_", &cvt_bf16_batch_);
   m.impl("stn_forward_", &stn_forward_);

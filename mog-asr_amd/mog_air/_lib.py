@@ -30,6 +30,8 @@ _SIGS = {
     "mog_split3_bf16": [P, I, I, I, P, I, L, P],
     "mog_gemm_x3p_tn": [P, L, P, L, P, P, I, I, I, I, I, I, I, I, P, L, P],
     "mog_gemm_f32_wgrad_group": [P, I, P],
+    "mog_wgrad_tn_work_elems": [I, P, I],
+    "mog_wgrad_tn_bf16": [I, P, P, P, P, P, I, I, P, L, P],
     "mog_build_id": [P, I],
     "mog_gemm_x3_nt": [P, P, L, P, P, I, I, I, I, I, I, I, I, P],
     "mog_gemm_f32_sigmoid_philox": [P, P, P, P, I, I, I, I, I, I, F, ULL, ULL, P],
@@ -83,6 +85,9 @@ _SIGS = {
     "mog_asr_step_backward": [I, I, I, F, F, F, F, P, P, P, P, P, P, P, P, P, P, P, P, P],
 }
 
+# entry points that do not return an int status
+_RESTYPE = {"mog_wgrad_tn_work_elems": L}
+
 _lib = None
 
 
@@ -95,7 +100,7 @@ def header_symbols() -> List[str]:
     with open(HEADER_PATH) as f:
         src = f.read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\bint\s+(mog_\w+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(?:int|long)\s+(mog_\w+)\s*\(", src)))
 
 
 def load():
@@ -110,7 +115,7 @@ def load():
     for name, args in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = I
+        fn.restype = _RESTYPE.get(name, I)
     built, src = library_build_id(lib), source_build_id()
     if src is not None and built != src:
         raise MogError(f"{LIB_PATH} was built from other sources (library {built}, sources "

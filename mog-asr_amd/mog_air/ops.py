@@ -91,6 +91,17 @@ def gemm_x3_nt(A: torch.Tensor, B3: torch.Tensor, sb: int, C: torch.Tensor, M: i
                      1 if aux is not None else 0)
 
 
+def wgrad_tn_bf16(X: Sequence[torch.Tensor], dY: Sequence[torch.Tensor],
+                  out: Sequence[torch.Tensor], colsum: Sequence[Optional[torch.Tensor]],
+                  dims: Sequence[Sequence[int]], K: int, nsplit: int = 8) -> None:
+    """out[i] += X[i]^T dY[i] over K rows on bf16 operands, colsum[i] += the
+    column sums of dY[i], every problem in one launch (dims[i] = (M, N, lda,
+    ldb, ldc)); K split nsplit ways, the splits added in order by a second
+    launch: deterministic (mog_wgrad_tn_bf16)."""
+    _ops.wgrad_tn_bf16_(list(X), list(dY), list(out), list(colsum),
+                        [int(d) for ds in dims for d in ds], int(K), int(nsplit))
+
+
 class WgradGroup:
     """Weight gradients collected over a backward pass and run as ONE grouped
     launch (mog_gemm_f32_wgrad_group): each problem is out[M,N] += X^T dY
@@ -124,12 +135,14 @@ class WgradGroup:
         """In collection order; a problem whose output or bias range overlaps
         one already in the current launch starts the next launch (same
         stream, so the two accumulate in order)."""
-        table, ranges = [], []
+        batch, ranges = [], []
 
         def flush():
-            if table:
-                _ops.gemm_f32_wgrad_group_(list(table), self.probs[0][2])
-            table.clear()
+            if batch:
+                X, dY, out, bias, dims = zip(*batch)
+                _ops.gemm_f32_wgrad_group_(list(X), list(dY), list(out), list(bias),
+                                           [d for ds in dims for d in ds])
+            batch.clear()
             ranges.clear()
 
         for X, dY, out, b, M, N, K, lda, ldb, ldc in self.probs:
@@ -139,8 +152,7 @@ class WgradGroup:
             if any(lo < h and l2 < hi for lo, hi in mine for l2, h in ranges):
                 flush()
             ranges.extend(mine)
-            table += [X.data_ptr(), dY.data_ptr(), out.data_ptr(),
-                      0 if b is None else b.data_ptr(), M, N, K, lda, ldb, ldc]
+            batch.append((X, dY, out, b, (M, N, K, lda, ldb, ldc)))
         flush()
         self.probs = []
 

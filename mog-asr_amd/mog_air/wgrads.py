@@ -47,6 +47,12 @@ class WeightGradients:
             gemm_bf16([X], [dY], [out], M, N, K, lda, ldb, N, tn=True, epi=BF_ATOMIC,
                       splitk=splitk, colsum=[bias_out])
 
+    # the grouped tall-K kernel (wgrad_tn.hip: all seven layers in one launch,
+    # K split over the XCDs, partials added in order) from this many rows;
+    # below it the per-layer split-K GEMMs
+    WGRAD_TN_MIN_ROWS = 2048
+    WGRAD_TN_SPLITS = 8
+
     def _vae_weight_grads_bf16(self, ws, t=None):
         """The VAE weight gradients over all T*B rows (bf16 operands), or over
         loop step t's B rows (accumulated: the per-step form of AIR-ASR)."""
@@ -56,18 +62,24 @@ class WeightGradients:
         Zp = self._pad8(Z)
         g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
         gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
-        self._dw_bf16(v(ws.gb), v(ws.da1b), g("recognition_1"), TB, W2, R1, W2, R1,
-                      gb("recognition_1"))
-        self._dw_bf16(v(ws.a1b), v(ws.da2b), g("recognition_2"), TB, R1, R2, R1, R2,
-                      gb("recognition_2"))
-        self._dw_bf16(v(ws.a2b), v(ws.dmub), g("rec_mean"), TB, R2, Z, R2, Zp, gb("rec_mean"))
-        self._dw_bf16(v(ws.a2b), v(ws.dlvb), g("rec_log_variance"), TB, R2, Z, R2, Zp,
-                      gb("rec_log_variance"))
-        self._dw_bf16(v(ws.zb), v(ws.dd1b), g("generative_1"), TB, Z, G1, Zp, G1,
-                      gb("generative_1"))
-        self._dw_bf16(v(ws.d1b), v(ws.dd2b), g("generative_2"), TB, G1, G2, G1, G2,
-                      gb("generative_2"))
-        self._dw_bf16(v(ws.d2b), v(ws.dmb), g("gen_mean"), TB, G2, W2, G2, W2, gb("gen_mean"))
+        # (X, dY, layer, M, N, lda, ldb) of the seven layers
+        probs = [(v(ws.gb), v(ws.da1b), "recognition_1", W2, R1, W2, R1),
+                 (v(ws.a1b), v(ws.da2b), "recognition_2", R1, R2, R1, R2),
+                 (v(ws.a2b), v(ws.dmub), "rec_mean", R2, Z, R2, Zp),
+                 (v(ws.a2b), v(ws.dlvb), "rec_log_variance", R2, Z, R2, Zp),
+                 (v(ws.zb), v(ws.dd1b), "generative_1", Z, G1, Zp, G1),
+                 (v(ws.d1b), v(ws.dd2b), "generative_2", G1, G2, G1, G2),
+                 (v(ws.d2b), v(ws.dmb), "gen_mean", G2, W2, G2, W2)]
+        if TB >= self.WGRAD_TN_MIN_ROWS:
+            flops = sum(2.0 * TB * M * N for _, _, _, M, N, _, _ in probs)
+            with self._timed("vae_wgrad_bf16", ("mfma", flops, "bf16")):
+                ops.wgrad_tn_bf16([p[0] for p in probs], [p[1] for p in probs],
+                                  [g(p[2]) for p in probs], [gb(p[2]) for p in probs],
+                                  [(M, N, lda, ldb, N) for _, _, _, M, N, lda, ldb in probs],
+                                  TB, self.WGRAD_TN_SPLITS)
+            return
+        for X, dY, name, M, N, lda, ldb in probs:
+            self._dw_bf16(X, dY, g(name), TB, M, N, lda, ldb, gb(name))
 
     def _dw(self, X, dY, out, K, M, N, lda, ldb, bias_out=None):
         """out[M,N] += X^T dY over K rows (split-K, atomics); bias_out += colsum(dY).

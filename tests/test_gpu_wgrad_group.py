@@ -131,3 +131,23 @@ def test_asr_batch64_step_grouped_matches_per_gradient_launches():
         a, b = grads[0][k], grads[1][k]
         tol = 2e-5 if b.numel() > 64 else 2e-4
         assert (a - b).norm().item() <= tol * (b.norm().item() + 1e-30), k
+
+
+def test_wgrad_group_op_schema_and_extents():
+    """torch.ops.mog_air.gemm_f32_wgrad_group_ takes tensors (out / bias
+    alias-annotated as written, opcheck's schema test) and checks each
+    problem's extents in C++: an output too small for its M x N is refused
+    before anything launches."""
+    from torch.library import opcheck
+    op = torch.ops.mog_air.gemm_f32_wgrad_group_
+    g = torch.Generator().manual_seed(6)
+    A = torch.randn(64, 48, generator=g).to(DEV)
+    B = torch.randn(64, 32, generator=g).to(DEV)
+    C = torch.zeros(48, 32, device=DEV)
+    b = torch.zeros(32, device=DEV)
+    opcheck(op.default, ([A], [B], [C], [b], [48, 32, 64, 48, 32, 32]),
+            test_utils=("test_schema",))
+    with pytest.raises(RuntimeError, match="out"):
+        op([A], [B], [torch.zeros(10, 32, device=DEV)], [None], [48, 32, 64, 48, 32, 32])
+    with pytest.raises(RuntimeError, match="dY"):
+        op([A], [B[:8].clone()], [C], [None], [48, 32, 64, 48, 32, 32])
