@@ -101,6 +101,14 @@ long mog_wgrad_tn_work_elems(int nprob, const int* dims, int nsplit);
 int mog_wgrad_tn_bf16(int nprob, const void* const* X, const void* const* dY, float* const* out,
                       float* const* colsum, const int* dims, int K, int nsplit, float* work,
                       long work_elems, void* stream);
+/* The same grouped weight gradients on fp32 operands at fp32-level accuracy
+ * (the fp32 configuration's VAE weight / bias gradients): X_i, dY_i fp32,
+ * 16-byte aligned, lda / ldb multiples of 4; exact three-piece bf16 splits
+ * inside the kernel, six MFMA products per block (as mog_gemm_f32_x3_tn);
+ * deterministic. */
+int mog_wgrad_tn_x3(int nprob, const float* const* X, const float* const* dY, float* const* out,
+                    float* const* colsum, const int* dims, int K, int nsplit, float* work,
+                    long work_elems, void* stream);
 
 /* dX = epi(dY W^T) at fp32-level accuracy on the bf16 matrix cores (the VAE
  * input gradients; replaces the MatMul gradients of vae.py:18-46's dense

@@ -49,13 +49,13 @@
 #include <type_traits>
 
 #include "mog_common.h"
+#include "x3_split.h"
 
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 128, BN = 128, BK = 32;
@@ -77,34 +77,6 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 __device__ __forceinline__ int tsw(int r) { return ((r & 3) << 2) | (((r >> 3) & 1) << 4); }
 // bf16 offset of (k-row r, column c), c a multiple of 4, in a TN operand image
 __device__ __forceinline__ int tpos(int r, int c) { return r * LDR + (((c >> 2) ^ tsw(r)) << 2); }
-
-// the three truncated bf16 pieces of one float (as fp32 bit patterns whose low
-// halves are zero, except lo's, which the packing drops)
-__device__ __forceinline__ void split1(float f, unsigned& hi, unsigned& mid, unsigned& lo) {
-  hi = __float_as_uint(f) & 0xffff0000u;
-  const float r1 = f - __uint_as_float(hi);  // exact
-  mid = __float_as_uint(r1) & 0xffff0000u;
-  lo = __float_as_uint(r1 - __uint_as_float(mid));  // exact, <= 8 significant bits
-}
-
-__device__ __forceinline__ unsigned pack2(unsigned a, unsigned b) {
-  return (a >> 16) | (b & 0xffff0000u);
-}
-
-// the pieces of four floats, packed two bf16 per dword
-__device__ __forceinline__ void split4(const float4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
-  unsigned h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
-  split1(v.x, h0, m0, l0);
-  split1(v.y, h1, m1, l1);
-  split1(v.z, h2, m2, l2);
-  split1(v.w, h3, m3, l3);
-  p0.x = pack2(h0, h1);
-  p0.y = pack2(h2, h3);
-  p1.x = pack2(m0, m1);
-  p1.y = pack2(m2, m3);
-  p2.x = pack2(l0, l1);
-  p2.y = pack2(l2, l3);
-}
 
 struct X3Args {
   const float* A;

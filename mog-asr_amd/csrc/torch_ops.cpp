@@ -1002,10 +1002,10 @@ void gemm_x3p_tn_(const Tensor& A3, int64_t sa, const Tensor& B3, int64_t sb, Te
 // lda, ldb, ldc) per problem.  The kernel reads whole k-rows of both operands
 // (K x ld elements each); the [nsplit][tiles] partial workspace is a transient
 // of the caching allocator on the op's stream.
-void wgrad_tn_bf16_(at::TensorList X, at::TensorList dY, at::TensorList out,
-                    const c10::List<optional<Tensor>>& colsum, at::IntArrayRef dims, int64_t K,
-                    int64_t nsplit) {
-  Op o("wgrad_tn_bf16_");
+void wgrad_tn_(at::TensorList X, at::TensorList dY, at::TensorList out,
+               const c10::List<optional<Tensor>>& colsum, at::IntArrayRef dims, int64_t K,
+               int64_t nsplit, bool x3) {
+  Op o(x3 ? "wgrad_tn_x3_" : "wgrad_tn_bf16_");
   const size_t n = out.size();
   TORCH_CHECK(n >= 1 && n <= 8 && X.size() == n && dY.size() == n && colsum.size() == n &&
                   dims.size() == 5 * n,
@@ -1018,8 +1018,8 @@ void wgrad_tn_bf16_(at::TensorList X, at::TensorList dY, at::TensorList out,
     TORCH_CHECK(M > 0 && N > 0 && lda >= M && ldb >= N && ldc >= N, o.name,
                 ": bad dims of problem ", i);
     os.push_back(o.f(out[i], mat(M, N, ldc), "out"));
-    xs.push_back(o.need(X[i], BF16, K * lda, "X"));
-    ys.push_back(o.need(dY[i], BF16, K * ldb, "dY"));
+    xs.push_back(o.need(X[i], x3 ? F32 : BF16, K * lda, "X"));
+    ys.push_back(o.need(dY[i], x3 ? F32 : BF16, K * ldb, "dY"));
     cs.push_back(o.f(static_cast<optional<Tensor>>(colsum[i]), N, "colsum"));
     for (int64_t v : {M, N, lda, ldb, ldc}) d.push_back((int)v);
   }
@@ -1027,10 +1027,25 @@ void wgrad_tn_bf16_(at::TensorList X, at::TensorList dY, at::TensorList out,
   const long we = mog_wgrad_tn_work_elems((int)n, d.data(), (int)nsplit);
   TORCH_CHECK(we > 0, o.name, ": bad problem set");
   Tensor w = at::empty({we}, at::TensorOptions().dtype(F32).device(*o.dev));
-  check(mog_wgrad_tn_bf16((int)n, arr<void>(xs), arr<void>(ys), marr<float>(os),
-                          marr<float>(cs), d.data(), (int)K, (int)nsplit, w.data_ptr<float>(), we,
-                          o.stream()),
-        o.name);
+  const int rc = x3 ? mog_wgrad_tn_x3((int)n, arr<float>(xs), arr<float>(ys), marr<float>(os),
+                                      marr<float>(cs), d.data(), (int)K, (int)nsplit,
+                                      w.data_ptr<float>(), we, o.stream())
+                   : mog_wgrad_tn_bf16((int)n, arr<void>(xs), arr<void>(ys), marr<float>(os),
+                                       marr<float>(cs), d.data(), (int)K, (int)nsplit,
+                                       w.data_ptr<float>(), we, o.stream());
+  check(rc, o.name);
+}
+
+void wgrad_tn_bf16_(at::TensorList X, at::TensorList dY, at::TensorList out,
+                    const c10::List<optional<Tensor>>& colsum, at::IntArrayRef dims, int64_t K,
+                    int64_t nsplit) {
+  wgrad_tn_(X, dY, out, colsum, dims, K, nsplit, false);
+}
+
+void wgrad_tn_x3_(at::TensorList X, at::TensorList dY, at::TensorList out,
+                  const c10::List<optional<Tensor>>& colsum, at::IntArrayRef dims, int64_t K,
+                  int64_t nsplit) {
+  wgrad_tn_(X, dY, out, colsum, dims, K, nsplit, true);
 }
 
 // out[i][M,N] += X[i]^T dY[i] over K rows (+ bias[i] += colsum(dY[i])) for
@@ -1085,6 +1100,9 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "int[] dims) -> ()");
   m.def(
       "wgrad_tn_bf16_(Tensor[] X, Tensor[] dY, Tensor(a!)[] out, Tensor(b!)?[] colsum, int[] dims, "
+      "int K, int nsplit) -> ()");
+  m.def(
+      "wgrad_tn_x3_(Tensor[] X, Tensor[] dY, Tensor(a!)[] out, Tensor(b!)?[] colsum, int[] dims, "
       "int K, int nsplit) -> ()");
   m.def(
       "split3_bf16_(Tensor src, Tensor(a!) dst, int rows, int cols, int ld_src, int ld_dst, "
@@ -1247,6 +1265,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("gemm_x3p_tn_", &gemm_x3p_tn_);
   m.impl("gemm_f32_wgrad_group_", &gemm_f32_wgrad_group_);
   m.impl("wgrad_tn_bf16_", &wgrad_tn_bf16_);
+  m.impl("wgrad_tn_x3_", &wgrad_tn_x3_);
   m.impl("gemm_bf16_", &gemm_bf16_);
   m.impl("cvt_bf16_batch_", &cvt_bf16_batch_);
   m.impl("stn_forward_", &stn_forward_);

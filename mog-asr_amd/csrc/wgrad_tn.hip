@@ -24,7 +24,16 @@
 // Columns past M / N load neighbouring data (rows past the k-range load 0
 // through the buffer range check); they reach only tile rows / columns that
 // the reduction never stores.
+//
+// The fp32 form (wgrad_tn_x3_kernel: the fp32 configuration's VAE weight
+// gradients at fp32-level accuracy) is the same grouped, XCD-split,
+// workspace-reduced GEMM with gemm_x3.hip's exact three-piece operand splits:
+// fp32 k-tiles staged through registers, split as they are written into six
+// bf16 images (A0 A1 A2 B0 B1 B2, the same swizzled layout), six MFMA
+// products per 16x16x32 block; the column sums take the ones-MFMA of each B
+// piece (b = b0 + b1 + b2 exactly).
 #include "mog_common.h"
+#include "x3_split.h"
 
 namespace {
 
@@ -42,8 +51,8 @@ constexpr int TILE_F = WT * WT;       // floats of one partial tile
 constexpr int OOB = (int)0x80000000u; // a buffer offset past every range
 
 struct WgProblem {
-  const __bf16* X;   // [K][lda]
-  const __bf16* dY;  // [K][ldb]
+  const void* X;     // [K][lda] bf16 (wgrad_tn_bf16_kernel) or fp32 (wgrad_tn_x3_kernel)
+  const void* dY;    // [K][ldb]
   float* out;        // [M][ldc]
   float* colsum;     // [N] or null
   int M, N, lda, ldb, ldc;
@@ -110,12 +119,8 @@ __device__ __forceinline__ floatx4 quad_transpose(const floatx4& a, int lane) {
   return floatx4{r0, r1, r2, r3};
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256, 3) void wgrad_tn_bf16_kernel(WgArgs D) {
-  __shared__ __attribute__((aligned(1024))) __bf16 lds[NS * STAGE];
-  // workgroup b -> split s (on XCD s % 8) and tile
-  const int b = blockIdx.x;
-  int s, tile;
+// workgroup b -> split s (on XCD s % 8 when nsplit is a multiple of 8) and tile
+__device__ __forceinline__ void block_job(const WgArgs& D, int b, int& s, int& tile) {
   if ((D.nsplit & 7) == 0 && D.xcd_map) {
     const int x = b & 7, j = b >> 3;
     s = x + 8 * (j / D.T);
@@ -124,6 +129,37 @@ __global__ __launch_bounds__(256, 3) void wgrad_tn_bf16_kernel(WgArgs D) {
     s = b / D.T;
     tile = b % D.T;
   }
+}
+
+// this split's 128 x 128 partial tile into the workspace: lane quads
+// transposed so a lane stores four consecutive columns of one row (16-byte
+// stores); the column-sum partials (first row of tiles) after the tiles
+__device__ __forceinline__ void store_partial(const WgArgs& D, const floatx4 (&acc)[4][4],
+                                              const floatx4 (&csa)[2], bool do_cs, int s,
+                                              int tile, int wm, int wn, int cni, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  float* W = D.work + ((size_t)s * D.T + tile) * TILE_F;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const floatx4 v = quad_transpose(acc[mi][ni], lane);
+      const int row = wm + mi * 16 + 4 * g + (li & 3);
+      const int col = wn + ni * 16 + (li & ~3);
+      *reinterpret_cast<floatx4*>(W + row * WT + col) = v;
+    }
+  if (do_cs && g == 0) {
+    float* Wc = D.work + (size_t)D.nsplit * D.T * TILE_F + ((size_t)s * D.T + tile) * WT;
+    Wc[wn + cni * 16 + li] = csa[0][0];
+    Wc[wn + (cni + 1) * 16 + li] = csa[1][0];
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256, 3) void wgrad_tn_bf16_kernel(WgArgs D) {
+  __shared__ __attribute__((aligned(1024))) __bf16 lds[NS * STAGE];
+  int s, tile;
+  block_job(D, blockIdx.x, s, tile);
   const WgProblem P = find_problem(D, tile);
   const int lt = tile - P.tile0;
   const int by = lt / P.tx, bx = lt - by * P.tx;
@@ -137,9 +173,9 @@ __global__ __launch_bounds__(256, 3) void wgrad_tn_bf16_kernel(WgArgs D) {
 
   // operand descriptors over whole rows: [K][ld] bf16
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<__bf16*>(P.X), 0, (int)((long)D.K * P.lda * 2), 0x00020000);
+      const_cast<void*>(P.X), 0, (int)((long)D.K * P.lda * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<__bf16*>(P.dY), 0, (int)((long)D.K * P.ldb * 2), 0x00020000);
+      const_cast<void*>(P.dY), 0, (int)((long)D.K * P.ldb * 2), 0x00020000);
   // DMA roles: wave w fills 1-KiB blocks q = w and w + 4 of each image (k-rows
   // 4q .. 4q+3); lane l -> k-row 4q + l/16, LDS chunk l%16 = global chunk
   // (l%16) ^ swz(row)
@@ -297,23 +333,136 @@ __global__ __launch_bounds__(256, 3) void wgrad_tn_bf16_kernel(WgArgs D) {
     }
   }
 
-  // this split's partial tile: lane quads transposed so a lane stores four
-  // consecutive columns of one row (16-byte stores)
-  float* W = D.work + ((size_t)s * D.T + tile) * TILE_F;
+  store_partial(D, acc, csa, do_cs, s, tile, wm, wn, cni, lane);
+}
+
+__global__ __launch_bounds__(256, 2) void wgrad_tn_x3_kernel(WgArgs D) {
+  // one stage of six images (48 KB: two workgroups per CU overlap each
+  // other's split and MFMA phases, as gemm_x3.hip's TN form)
+  __shared__ __attribute__((aligned(1024))) __bf16 lds[6 * IMG];
+  int s, tile;
+  block_job(D, blockIdx.x, s, tile);
+  const WgProblem P = find_problem(D, tile);
+  const int lt = tile - P.tile0;
+  const int by = lt / P.tx, bx = lt - by * P.tx;
+  const int m0 = by * WT, n0 = bx * WT;
+  const int kbeg = s * D.kchunk;
+  const int kend = min(D.K, kbeg + D.kchunk);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const bool do_cs = P.colsum != nullptr && by == 0;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(P.X), 0, (int)((long)D.K * P.lda * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(P.dY), 0, (int)((long)D.K * P.ldb * 4), 0x00020000);
+  // staging roles: float4 i of this thread is k-row t/32 + 8 i, columns
+  // 4 (t % 32) .. + 3 of the tile
+  const int sr = t >> 5, sc = (t & 31) * 4;
+  int aoff[4], boff[4], krow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    krow[i] = kbeg + sr + 8 * i;
+    aoff[i] = (krow[i] * P.lda + m0 + sc) * 4;
+    boff[i] = (krow[i] * P.ldb + n0 + sc) * 4;
+  }
+  const int astep = BK * P.lda * 4, bstep = BK * P.ldb * 4;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 ra4[4], rb4[4];
+  auto load = [&](int it) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool in = krow[i] + it * BK < kend;
+      ra4[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, in ? aoff[i] + it * astep : OOB, 0, 0);
+      rb4[i] = __builtin_amdgcn_raw_buffer_load_b128(rb, in ? boff[i] + it * bstep : OOB, 0, 0);
+    }
+  };
+  auto f4 = [](const u32x4& v) {
+    return float4{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                  __uint_as_float(v[3])};
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int o = tpos<0>(sr + 8 * i, sc);
+      u32x2 p0, p1, p2;
+      split4(f4(ra4[i]), p0, p1, p2);
+      *reinterpret_cast<u32x2*>(lds + 0 * IMG + o) = p0;
+      *reinterpret_cast<u32x2*>(lds + 1 * IMG + o) = p1;
+      *reinterpret_cast<u32x2*>(lds + 2 * IMG + o) = p2;
+      split4(f4(rb4[i]), p0, p1, p2);
+      *reinterpret_cast<u32x2*>(lds + 3 * IMG + o) = p0;
+      *reinterpret_cast<u32x2*>(lds + 4 * IMG + o) = p1;
+      *reinterpret_cast<u32x2*>(lds + 5 * IMG + o) = p2;
+    }
+  };
+
+  floatx4 acc[4][4];
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const floatx4 v = quad_transpose(acc[mi][ni], lane);
-      const int row = wm + mi * 16 + 4 * g + (li & 3);
-      const int col = wn + ni * 16 + (li & ~3);
-      *reinterpret_cast<floatx4*>(W + row * WT + col) = v;
-    }
-  if (do_cs && g == 0) {
-    float* Wc = D.work + (size_t)D.nsplit * D.T * TILE_F + ((size_t)s * D.T + tile) * WT;
-    Wc[wn + cni * 16 + li] = csa[0][0];
-    Wc[wn + (cni + 1) * 16 + li] = csa[1][0];
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
+  floatx4 csa[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+  const int cni = 2 * (w >> 1);
+  const bool chi = cni != 0;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  int ao[4][2], bo[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    ao[i][0] = tpos<0>(8 * g + tq, wm + 16 * i + 4 * tp);
+    ao[i][1] = tpos<0>(8 * g + tq + 4, wm + 16 * i + 4 * tp);
+    bo[i][0] = tpos<0>(8 * g + tq, wn + 16 * i + 4 * tp);
+    bo[i][1] = tpos<0>(8 * g + tq + 4, wn + 16 * i + 4 * tp);
   }
+  auto frag = [&](int img, const int (&o)[2]) -> bf16x8 {
+    const __bf16* base = lds + img * IMG;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + o[0]));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + o[1]));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto compute = [&]() {
+    // the B pieces held for the k-tile, the A pieces one at a time, smallest
+    // products first (a2 b0; a1 b1, a1 b0; a0 b2, a0 b1, a0 b0)
+    bf16x8 b[3][4];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b[p][i] = frag(3 + p, bo[i]);
+#pragma unroll
+    for (int pa = 2; pa >= 0; --pa) {
+      bf16x8 a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = frag(pa, ao[i]);
+#pragma unroll
+      for (int pb = 2 - pa; pb >= 0; --pb)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            acc[mi][ni] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi], b[pb][ni], acc[mi][ni], 0, 0, 0);
+    }
+    if (do_cs) {
+#pragma unroll
+      for (int p = 2; p >= 0; --p) {
+        csa[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, chi ? b[p][2] : b[p][0], csa[0], 0, 0, 0);
+        csa[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, chi ? b[p][3] : b[p][1], csa[1], 0, 0, 0);
+      }
+    }
+  };
+  const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nk > 0) load(0);
+  for (int it = 0; it < nk; ++it) {
+    store();
+    if (it + 1 < nk) load(it + 1);
+    __syncthreads();
+    compute();
+    __syncthreads();
+  }
+  store_partial(D, acc, csa, do_cs, s, tile, wm, wn, cni, lane);
 }
 
 // out += sum over splits s = 0 .. nsplit-1 of the partial tiles, in that order;
@@ -371,12 +520,18 @@ extern "C" long mog_wgrad_tn_work_elems(int nprob, const int* dims, int nsplit) 
   return (long)nsplit * group_tiles(nprob, dims) * (TILE_F + WT);
 }
 
-extern "C" int mog_wgrad_tn_bf16(int nprob, const void* const* X, const void* const* dY,
-                                 float* const* out, float* const* colsum, const int* dims, int K,
-                                 int nsplit, float* work, long work_elems, void* stream) {
+namespace {
+
+// the launch of either form: elem = 2 (bf16 operands, pitches multiples of
+// 8) or 4 (fp32, the x3 form, pitches multiples of 4): 16-byte chunks of
+// whole rows inside the 32-bit buffer range
+int wgrad_tn_launch(int elem, int nprob, const void* const* X, const void* const* dY,
+                    float* const* out, float* const* colsum, const int* dims, int K, int nsplit,
+                    float* work, long work_elems, void* stream) {
   MOG_CHECK_ARG(nprob >= 1 && nprob <= MAXP && X && dY && out && dims && K >= 0 && nsplit >= 1);
   MOG_CHECK_ARG(work != nullptr && al16(work) &&
                 work_elems >= mog_wgrad_tn_work_elems(nprob, dims, nsplit));
+  const int vec = 16 / elem;
   WgArgs D{};
   D.np = nprob;
   D.K = K;
@@ -384,15 +539,13 @@ extern "C" int mog_wgrad_tn_bf16(int nprob, const void* const* X, const void* co
   for (int i = 0; i < nprob; ++i) {
     const int M = dims[5 * i], N = dims[5 * i + 1], lda = dims[5 * i + 2], ldb = dims[5 * i + 3],
               ldc = dims[5 * i + 4];
-    // 16-byte chunks: row pitches multiples of 8 bf16; whole rows inside the
-    // 32-bit buffer range
-    MOG_CHECK_ARG(M >= 1 && N >= 1 && lda >= M && ldb >= N && ldc >= N && lda % 8 == 0 &&
-                  ldb % 8 == 0);
-    MOG_CHECK_ARG((long)K * lda * 2 < (1L << 31) && (long)K * ldb * 2 < (1L << 31));
+    MOG_CHECK_ARG(M >= 1 && N >= 1 && lda >= M && ldb >= N && ldc >= N && lda % vec == 0 &&
+                  ldb % vec == 0);
+    MOG_CHECK_ARG((long)K * lda * elem < (1L << 31) && (long)K * ldb * elem < (1L << 31));
     MOG_CHECK_ARG(X[i] && dY[i] && out[i] && al16(X[i]) && al16(dY[i]));
     WgProblem& P = D.p[i];
-    P.X = reinterpret_cast<const __bf16*>(X[i]);
-    P.dY = reinterpret_cast<const __bf16*>(dY[i]);
+    P.X = X[i];
+    P.dY = dY[i];
     P.out = out[i];
     P.colsum = colsum ? colsum[i] : nullptr;
     P.M = M; P.N = N; P.lda = lda; P.ldb = ldb; P.ldc = ldc;
@@ -411,13 +564,32 @@ extern "C" int mog_wgrad_tn_bf16(int nprob, const void* const* X, const void* co
   if (const char* e = mog_prof_env("MOG_WG_MAP")) D.xcd_map = atoi(e);
   if (K == 0) return 0;
   hipStream_t s = mog_stream(stream);
-  int mode = 0;
-  if (const char* e = mog_prof_env("MOG_WG_MODE")) mode = atoi(e);
   const dim3 grid((unsigned)(T * nsplit));
-  if (mode == 2) wgrad_tn_bf16_kernel<2><<<grid, 256, 0, s>>>(D);
-
-  else wgrad_tn_bf16_kernel<0><<<grid, 256, 0, s>>>(D);
+  if (elem == 4) {
+    wgrad_tn_x3_kernel<<<grid, 256, 0, s>>>(D);
+  } else {
+    int mode = 0;
+    if (const char* e = mog_prof_env("MOG_WG_MODE")) mode = atoi(e);
+    if (mode == 2) wgrad_tn_bf16_kernel<2><<<grid, 256, 0, s>>>(D);
+    else wgrad_tn_bf16_kernel<0><<<grid, 256, 0, s>>>(D);
+  }
   const long nthr = (long)T * (TILE_F / 4) + (long)T * WT;
   wgrad_tn_reduce_kernel<<<dim3((unsigned)((nthr + 255) / 256)), 256, 0, s>>>(D);
   MOG_LAUNCH_RET();
+}
+
+}  // namespace
+
+extern "C" int mog_wgrad_tn_bf16(int nprob, const void* const* X, const void* const* dY,
+                                 float* const* out, float* const* colsum, const int* dims, int K,
+                                 int nsplit, float* work, long work_elems, void* stream) {
+  return wgrad_tn_launch(2, nprob, X, dY, out, colsum, dims, K, nsplit, work, work_elems, stream);
+}
+
+extern "C" int mog_wgrad_tn_x3(int nprob, const float* const* X, const float* const* dY,
+                               float* const* out, float* const* colsum, const int* dims, int K,
+                               int nsplit, float* work, long work_elems, void* stream) {
+  return wgrad_tn_launch(4, nprob, reinterpret_cast<const void* const*>(X),
+                         reinterpret_cast<const void* const*>(dY), out, colsum, dims, K, nsplit,
+                         work, work_elems, stream);
 }

@@ -32,6 +32,7 @@ _SIGS = {
     "mog_gemm_f32_wgrad_group": [P, I, P],
     "mog_wgrad_tn_work_elems": [I, P, I],
     "mog_wgrad_tn_bf16": [I, P, P, P, P, P, I, I, P, L, P],
+    "mog_wgrad_tn_x3": [I, P, P, P, P, P, I, I, P, L, P],
     "mog_build_id": [P, I],
     "mog_gemm_x3_nt": [P, P, L, P, P, I, I, I, I, I, I, I, I, P],
     "mog_gemm_f32_sigmoid_philox": [P, P, P, P, I, I, I, I, I, I, F, ULL, ULL, P],

@@ -536,8 +536,7 @@ class AIRModel(_AirBase):
                     if self.precision == "bf16":
                         self._vae_weight_grads_bf16(ws, t)
                     else:
-                        for name in self._VAE_WGRAD_LAYERS:
-                            self._vae_wgrad_fp32(ws, name, t)
+                        self._vae_weight_grads_fp32(ws, t)
             ops.stn_backward(X, ws.th_f[t], (W, W), ws.dg, want_dU=False, dtheta=ws.dth_f)
             hid = [ws.hid8[k, t] for k in range(8)]
             dpre = [ws.dpre[k, t] for k in range(8)]
@@ -618,8 +617,6 @@ class AIRModel(_AirBase):
     # done, under the latency-bound rest of the reversed loop, instead of over
     # all T*B rows after it (VAE_WGRAD_PER_STEP = False: after the loop)
     VAE_WGRAD_PER_STEP = True
-    _VAE_WGRAD_LAYERS = ("recognition_1", "recognition_2", "rec_mean", "generative_1",
-                         "generative_2", "gen_mean")
 
     def _weight_grads(self, X, ws):
         B, T, H, Z = ws.B, self.max_steps, self.rnn_units, self.vae_latent_dimensions

@@ -102,6 +102,15 @@ def wgrad_tn_bf16(X: Sequence[torch.Tensor], dY: Sequence[torch.Tensor],
                         [int(d) for ds in dims for d in ds], int(K), int(nsplit))
 
 
+def wgrad_tn_x3(X: Sequence[torch.Tensor], dY: Sequence[torch.Tensor],
+                out: Sequence[torch.Tensor], colsum: Sequence[Optional[torch.Tensor]],
+                dims: Sequence[Sequence[int]], K: int, nsplit: int = 8) -> None:
+    """wgrad_tn_bf16 on fp32 operands at fp32-level accuracy (exact
+    three-piece bf16 splits in the kernel; mog_wgrad_tn_x3)."""
+    _ops.wgrad_tn_x3_(list(X), list(dY), list(out), list(colsum),
+                      [int(d) for ds in dims for d in ds], int(K), int(nsplit))
+
+
 class WgradGroup:
     """Weight gradients collected over a backward pass and run as ONE grouped
     launch (mog_gemm_f32_wgrad_group): each problem is out[M,N] += X^T dY

@@ -52,6 +52,9 @@ class WeightGradients:
     # below it the per-layer split-K GEMMs
     WGRAD_TN_MIN_ROWS = 2048
     WGRAD_TN_SPLITS = 8
+    # the x3 form: 16 splits (350 vs 427 us at 8 for the four layers at
+    # 24,576 rows, scripts/wgrad_shapes.py)
+    WGRAD_TN_X3_SPLITS = 16
 
     def _vae_weight_grads_bf16(self, ws, t=None):
         """The VAE weight gradients over all T*B rows (bf16 operands), or over
@@ -156,10 +159,36 @@ class WeightGradients:
         elif name == "gen_mean":
             self._dw_x3(v(ws.d2), v(ws.dm), g(name), TB, G2, W2, G2, W2, gb(name))
 
-    def _vae_weight_grads_fp32(self, ws):
+    def _vae_weight_grads_fp32(self, ws, t=None):
+        """The fp32 VAE weight gradients over all T*B rows, or over loop step
+        t's B rows (the per-step form of AIR-ASR).  From WGRAD_TN_MIN_ROWS the
+        four 16-byte-row layers (98 % of the flops) run as ONE grouped x3
+        launch (wgrad_tn.hip: fp32-level accuracy, K split over the XCDs,
+        partials added in order -- deterministic), the three 50-wide layers
+        on the fp32 split-K GEMM."""
+        TB = ws.B * self.max_steps if t is None else ws.B
+        v = (lambda x: x) if t is None else (lambda x: x[t])  # noqa: E731
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        big = [(v(ws.g), v(ws.da1), "recognition_1", W2, R1),
+               (v(ws.a1), v(ws.da2), "recognition_2", R1, R2),
+               (v(ws.d1), v(ws.dd2), "generative_2", G1, G2),
+               (v(ws.d2), v(ws.dm), "gen_mean", G2, W2)]
+        if (self.VAE_WGRAD_X3 and TB >= self.WGRAD_TN_MIN_ROWS
+                and all(M % 4 == 0 and N % 4 == 0 for _, _, _, M, N in big)):
+            g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
+            gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
+            flops = sum(2.0 * TB * M * N for _, _, _, M, N in big)
+            with self._timed("vae_wgrad_x3", ("mfma", flops, "fp32", "x3")):
+                ops.wgrad_tn_x3([b[0] for b in big], [b[1] for b in big],
+                                [g(b[2]) for b in big], [gb(b[2]) for b in big],
+                                [(M, N, M, N, N) for _, _, _, M, N in big], TB,
+                                self.WGRAD_TN_X3_SPLITS)
+            for name in ("rec_mean", "generative_1"):
+                self._vae_wgrad_fp32(ws, name, t)
+            return
         for name in ("recognition_1", "recognition_2", "rec_mean", "generative_1",
                      "generative_2", "gen_mean"):
-            self._vae_wgrad_fp32(ws, name)
+            self._vae_wgrad_fp32(ws, name, t)
 
     def _weight_grads_glimpse(self, ws):
         """Weight gradients of the VAE and the five heads (every loop step at

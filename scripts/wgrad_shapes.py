@@ -90,3 +90,16 @@ for i, (M, N) in enumerate(X3):
 fl3 = sum(2.0 * K * M * N for M, N in X3)
 print(json.dumps({"variant": "gemm_x3_tn per layer", "K": K, "us_per_layer": per,
                   "us_total": sum(per), "frac_fp32": fl3 / (sum(per) * 1e-6) / 157.3e12}))
+ref3 = [(a.double().t() @ b.double()) for a, b in zip(Af, Bf)]
+for nsplit in [int(x) for x in os.environ.get("WG_X3_SPLITS", "8,7,16").split(",")]:
+    def go3():
+        ops.wgrad_tn_x3(Af, Bf, Cf, bf, [(M, N, M, N, N) for M, N in X3], K, nsplit)
+    for c in Cf:
+        c.zero_()
+    go3()
+    torch.cuda.synchronize()
+    err = max(((c.double() - r).abs().max() / r.abs().max()).item() for c, r in zip(Cf, ref3))
+    us = timeit(go3)
+    print(json.dumps({"variant": "wgrad_tn_x3 grouped", "K": K, "nsplit": nsplit, "us_total": us,
+                      "frac_fp32": fl3 / (us * 1e-6) / 157.3e12,
+                      "frac_bf16_x6": 6 * fl3 / (us * 1e-6) / 2.5e15, "max_rel_err": err}))

@@ -91,3 +91,37 @@ def test_wgrad_tn_checks_extents():
     with pytest.raises(RuntimeError, match="out"):
         ops.wgrad_tn_bf16([X], [dY], [torch.zeros(10, 64, device=DEV)], [None],
                           [(64, 64, 64, 64, 64)], 64, 8)
+
+
+@pytest.mark.parametrize("K,nsplit", [(2500, 8), (1001, 7)])
+def test_wgrad_tn_x3_matches_float64(K, nsplit):
+    """The fp32 form (mog_wgrad_tn_x3: exact three-piece splits, six
+    products): fp32-level accuracy against a float64 product of the fp32
+    operands -- the fp32 configuration's four large VAE layers plus ragged
+    shapes -- accumulated onto existing values, and bitwise deterministic."""
+    shapes = [(784, 512, 784, 512), (512, 256, 512, 256), (256, 512, 256, 512),
+              (512, 784, 512, 784), (132, 68, 136, 72)]
+    g = torch.Generator().manual_seed(K)
+    Xs = [torch.randn(K, lda, generator=g).to(DEV) for _, _, lda, _ in shapes]
+    Ys = [(torch.randn(K, ldb, generator=g) * 1e-2).to(DEV) for _, _, _, ldb in shapes]
+    C0 = [torch.randn(M, N, generator=g).to(DEV) for M, N, _, _ in shapes]
+    b0 = [torch.randn(N, generator=g).to(DEV) for _, N, _, _ in shapes]
+    res = []
+    for _ in range(2):
+        Cs = [c.clone() for c in C0]
+        bs = [b.clone() for b in b0]
+        ops.wgrad_tn_x3(Xs, Ys, Cs, bs, [(M, N, lda, ldb, N) for M, N, lda, ldb in shapes], K,
+                        nsplit)
+        torch.cuda.synchronize()
+        res.append((Cs, bs))
+    for a, b in zip(res[0][0] + res[0][1], res[1][0] + res[1][1]):
+        assert torch.equal(a, b)
+    Cs, bs = res[0]
+    for i, (M, N, _, _) in enumerate(shapes):
+        Xd, Yd = Xs[i].double().cpu()[:, :M], Ys[i].double().cpu()[:, :N]
+        ref = Xd.t() @ Yd + C0[i].double().cpu()
+        scale = Xd.abs().t() @ Yd.abs() + C0[i].double().cpu().abs()
+        assert ((Cs[i].double().cpu() - ref).abs() / scale).max().item() <= 1e-5, i
+        bref = Yd.sum(0) + b0[i].double().cpu()
+        bscale = Yd.abs().sum(0) + b0[i].double().cpu().abs()
+        assert ((bs[i].double().cpu() - bref).abs() / bscale).max().item() <= 1e-5, i
