@@ -103,7 +103,7 @@ int mog_wgrad_tn_bf16(int nprob, const void* const* X, const void* const* dY, fl
                       long work_elems, void* stream);
 /* The same grouped weight gradients on fp32 operands at fp32-level accuracy
  * (the fp32 configuration's VAE weight / bias gradients): X_i, dY_i fp32,
- * 16-byte aligned, lda / ldb multiples of 4; exact three-piece bf16 splits
+ * 16-byte aligned, lda / ldb even; exact three-piece bf16 splits
  * inside the kernel, six MFMA products per block (as mog_gemm_f32_x3_tn);
  * deterministic. */
 int mog_wgrad_tn_x3(int nprob, const float* const* X, const float* const* dY, float* const* out,

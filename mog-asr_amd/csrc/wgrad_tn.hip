@@ -369,12 +369,21 @@ __global__ __launch_bounds__(256, 2) void wgrad_tn_x3_kernel(WgArgs D) {
   const int astep = BK * P.lda * 4, bstep = BK * P.ldb * 4;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   u32x4 ra4[4], rb4[4];
+  // operands whose row pitch is not a multiple of 4 floats (the 50-wide
+  // latent layers) load each 16-byte chunk as two 8-byte halves
+  const bool pitch8 = ((P.lda | P.ldb) & 3) != 0;
+  auto ld16 = [&](__amdgpu_buffer_rsrc_t r, int off) -> u32x4 {
+    if (!pitch8) return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    const u32x2 lo = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    const u32x2 hi = __builtin_amdgcn_raw_buffer_load_b64(r, off == OOB ? OOB : off + 8, 0, 0);
+    return u32x4{lo[0], lo[1], hi[0], hi[1]};
+  };
   auto load = [&](int it) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool in = krow[i] + it * BK < kend;
-      ra4[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, in ? aoff[i] + it * astep : OOB, 0, 0);
-      rb4[i] = __builtin_amdgcn_raw_buffer_load_b128(rb, in ? boff[i] + it * bstep : OOB, 0, 0);
+      ra4[i] = ld16(ra, in ? aoff[i] + it * astep : OOB);
+      rb4[i] = ld16(rb, in ? boff[i] + it * bstep : OOB);
     }
   };
   auto f4 = [](const u32x4& v) {
@@ -522,16 +531,18 @@ extern "C" long mog_wgrad_tn_work_elems(int nprob, const int* dims, int nsplit) 
 
 namespace {
 
-// the launch of either form: elem = 2 (bf16 operands, pitches multiples of
-// 8) or 4 (fp32, the x3 form, pitches multiples of 4): 16-byte chunks of
-// whole rows inside the 32-bit buffer range
+// the launch of either form: elem = 2 (bf16 operands) or 4 (fp32, the x3
+// form); whole rows inside the 32-bit buffer range
 int wgrad_tn_launch(int elem, int nprob, const void* const* X, const void* const* dY,
                     float* const* out, float* const* colsum, const int* dims, int K, int nsplit,
                     float* work, long work_elems, void* stream) {
   MOG_CHECK_ARG(nprob >= 1 && nprob <= MAXP && X && dY && out && dims && K >= 0 && nsplit >= 1);
   MOG_CHECK_ARG(work != nullptr && al16(work) &&
                 work_elems >= mog_wgrad_tn_work_elems(nprob, dims, nsplit));
-  const int vec = 16 / elem;
+  // bf16: 16-byte rows (pitches multiples of 8); fp32: 8-byte rows
+  // (pitches even: the x3 kernel loads 16-byte chunks as two halves when a
+  // pitch is not a multiple of 4)
+  const int vec = elem == 2 ? 8 : 2;
   WgArgs D{};
   D.np = nprob;
   D.K = K;

@@ -592,16 +592,13 @@ class AIRModel(_AirBase):
         v = (lambda x: x[t]) if t is not None else (lambda x: x)  # noqa: E731
         gKi = self._Kpad("infer_rnn_running/kernel", "grad")
         gKg = self._Kpad("gen_rnn_running/kernel", "grad")
-        if self.REC_WGRAD_X3 and K >= self.X3_MIN_ROWS:
-            # on the bf16 matrix cores with exact three-piece splits (as AIR's
-            # recurrent rows, AIRModel._dw_rec): 312 x 1024 x K per cell
-            tiles = ((LU + 127) // 128) * ((4 * H + 127) // 128)
-            splitk = self._sk(max(1, min(K // 256, (512 + tiles - 1) // tiles)))
-            for U, dG, out, bias in ((v(ws.U), v(ws.dG), gKi[self.C2:], None),
-                                     (v(ws.Ug), v(ws.dGg), gKg, self._Ng("gen_rnn_running/bias"))):
-                with self._timed("rec_wgrad_x3", ("mfma", 2.0 * K * LU * 4 * H, "fp32", "x3")):
-                    ops.gemm_x3_tn(U, dG, out, LU, 4 * H, K, LU, 4 * H, 4 * H, splitk=splitk,
-                                   colsum=bias, reduce=False)
+        if self.REC_WGRAD_X3 and K >= self.WGRAD_TN_MIN_ROWS:
+            # both cells in one grouped x3 launch (as AIR's recurrent rows,
+            # AIRModel._dw_rec): 312 x 1024 x K each, deterministic
+            with self._timed("rec_wgrad_x3", ("mfma", 2 * 2.0 * K * LU * 4 * H, "fp32", "x3")):
+                ops.wgrad_tn_x3([v(ws.U), v(ws.Ug)], [v(ws.dG), v(ws.dGg)],
+                                [gKi[self.C2:], gKg], [None, self._Ng("gen_rnn_running/bias")],
+                                [(LU, 4 * H, LU, 4 * H, 4 * H)] * 2, K, self.WGRAD_TN_X3_SPLITS)
             return
         self._dw(v(ws.U), v(ws.dG), gKi[self.C2:], K, LU, 4 * H, LU, 4 * H)
         self._dw(v(ws.Ug), v(ws.dGg), gKg, K, LU, 4 * H, LU, 4 * H,

@@ -161,30 +161,30 @@ class WeightGradients:
 
     def _vae_weight_grads_fp32(self, ws, t=None):
         """The fp32 VAE weight gradients over all T*B rows, or over loop step
-        t's B rows (the per-step form of AIR-ASR).  From WGRAD_TN_MIN_ROWS the
-        four 16-byte-row layers (98 % of the flops) run as ONE grouped x3
-        launch (wgrad_tn.hip: fp32-level accuracy, K split over the XCDs,
-        partials added in order -- deterministic), the three 50-wide layers
-        on the fp32 split-K GEMM."""
+        t's B rows (the per-step form of AIR-ASR): from WGRAD_TN_MIN_ROWS the
+        seven layers in ONE grouped x3 launch (wgrad_tn.hip: fp32-level
+        accuracy, K split over the XCDs, partials added in order --
+        deterministic)."""
         TB = ws.B * self.max_steps if t is None else ws.B
         v = (lambda x: x) if t is None else (lambda x: x[t])  # noqa: E731
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
-        big = [(v(ws.g), v(ws.da1), "recognition_1", W2, R1),
-               (v(ws.a1), v(ws.da2), "recognition_2", R1, R2),
-               (v(ws.d1), v(ws.dd2), "generative_2", G1, G2),
-               (v(ws.d2), v(ws.dm), "gen_mean", G2, W2)]
+        probs = [(v(ws.g), v(ws.da1), "recognition_1", W2, R1),
+                 (v(ws.a1), v(ws.da2), "recognition_2", R1, R2),
+                 (v(ws.a2), v(ws.dmu), "rec_mean", R2, Z),
+                 (v(ws.a2), v(ws.dlv), "rec_log_variance", R2, Z),
+                 (v(ws.z), v(ws.dd1), "generative_1", Z, G1),
+                 (v(ws.d1), v(ws.dd2), "generative_2", G1, G2),
+                 (v(ws.d2), v(ws.dm), "gen_mean", G2, W2)]
         if (self.VAE_WGRAD_X3 and TB >= self.WGRAD_TN_MIN_ROWS
-                and all(M % 4 == 0 and N % 4 == 0 for _, _, _, M, N in big)):
+                and all(M % 2 == 0 and N % 2 == 0 for _, _, _, M, N in probs)):
             g = lambda n: self._G("vae/" + n + "/weights")  # noqa: E731
             gb = lambda n: self._G("vae/" + n + "/biases")  # noqa: E731
-            flops = sum(2.0 * TB * M * N for _, _, _, M, N in big)
+            flops = sum(2.0 * TB * M * N for _, _, _, M, N in probs)
             with self._timed("vae_wgrad_x3", ("mfma", flops, "fp32", "x3")):
-                ops.wgrad_tn_x3([b[0] for b in big], [b[1] for b in big],
-                                [g(b[2]) for b in big], [gb(b[2]) for b in big],
-                                [(M, N, M, N, N) for _, _, _, M, N in big], TB,
+                ops.wgrad_tn_x3([p[0] for p in probs], [p[1] for p in probs],
+                                [g(p[2]) for p in probs], [gb(p[2]) for p in probs],
+                                [(M, N, M, N, N) for _, _, _, M, N in probs], TB,
                                 self.WGRAD_TN_X3_SPLITS)
-            for name in ("rec_mean", "generative_1"):
-                self._vae_wgrad_fp32(ws, name, t)
             return
         for name in ("recognition_1", "recognition_2", "rec_mean", "generative_1",
                      "generative_2", "gen_mean"):
@@ -284,19 +284,19 @@ class WeightGradients:
 
     def _dw_rec(self, ws):
         """The LSTM kernel's recurrent rows: gK[C2:] += sum_t h[t-1]^T dG[t]
-        over (T-1) B rows.  From X3_MIN_ROWS (either precision: fp32-level, and
-        faster than the fp32 chain): on the bf16 matrix cores with exact
-        three-piece splits (gemm_x3_tn, as the fp32 VAE weight gradients;
-        256 x 1024 x 16,384 at B = 8192), else the fp32 split-K GEMM."""
+        over (T-1) B rows.  From WGRAD_TN_MIN_ROWS (either precision:
+        fp32-level, and faster than the fp32 chain): on the bf16 matrix cores
+        with exact three-piece splits (the grouped x3 kernel of the fp32 VAE
+        weight gradients, one problem, 256 x 1024 x 16,384 at B = 8192), else
+        the fp32 split-K GEMM."""
         B, T, H, C2 = ws.B, self.max_steps, self.rnn_units, self.C2
         gK = self._G("rnn/basic_lstm_cell/kernel")
         K = (T - 1) * B
-        if self.REC_WGRAD_X3 and K >= self.X3_MIN_ROWS:
-            tiles = ((H + 127) // 128) * ((4 * H + 127) // 128)
-            splitk = self._sk(max(1, min(K // 256, (512 + tiles - 1) // tiles)))
+        if self.REC_WGRAD_X3 and K >= self.WGRAD_TN_MIN_ROWS:
+            # the grouped x3 kernel with one problem: deterministic
             with self._timed("rec_wgrad_x3", ("mfma", 2.0 * K * H * 4 * H, "fp32", "x3")):
-                ops.gemm_x3_tn(ws.h, ws.dG[1:], gK[C2:], H, 4 * H, K, H, 4 * H, 4 * H,
-                               splitk=splitk, reduce=False)
+                ops.wgrad_tn_x3([ws.h], [ws.dG[1:]], [gK[C2:]], [None],
+                                [(H, 4 * H, H, 4 * H, 4 * H)], K, self.WGRAD_TN_X3_SPLITS)
         else:
             self._dw(ws.h, ws.dG[1:], gK[C2:], K, H, 4 * H, H, 4 * H)
 
