@@ -233,6 +233,27 @@ int mog_air_step_forward(int B, int HS, int HZ, int step, int train, int use_num
                          float* zprob_out, float* zkl_out, float* skl_out, float* shkl_out,
                          float* zmask, float* zval, float* zc, const float* prior_lo_dev,
                          void* stream);
+/* Every loop step in ONE launch (AIR, air_model.py:435-736 with the LSTM
+ * chain run first: the heads read h_t only, the step's VAE never feeds the
+ * recurrence): steps <= 8; every per-step operand over steps * B rows back to
+ * back (step t at the pointer + t * B * width; rec [steps][17][B]; hid head z
+ * step t at hid[z] + t * hid_step); prior_bias: HOST array of `steps` values
+ * (the per-step marginal bias, air_model.py:600-620).  Writes the bits of
+ * `steps` mog_air_step_forward calls except what depends on the batch-wide
+ * loop predicate: runloss is not written, rec's z_pres-term slot holds the
+ * term the step adds IF it is live, and mog_air_runloss(..., live) applies
+ * live[] (set here, reduced over ranks in between under data parallelism). */
+int mog_air_step_forward_steps(int steps, int B, int HS, int HZ, int train, int use_num_prior,
+                               float thr, float temperature, float prior_lo,
+                               const float* prior_bias, float s_pm, float s_pv, float s_plv,
+                               float h_pm, float h_pv, float h_plv, const float* const* hid,
+                               long hid_step, const float* const* w2, const float* const* b2,
+                               const float* eps_scale, const float* eps_shift, const float* u,
+                               float* stop, int* digits, int* live, float* rec,
+                               float* theta_fwd, float* theta_back, float* scale_out,
+                               float* shift_out, float* zprob_out, float* zkl_out,
+                               float* skl_out, float* shkl_out, float* zmask, float* zval,
+                               float* zc, const float* prior_lo_dev, void* stream);
 /* Backward of the above: writes dout [5][B, 2] and dhid [5][B, HS] (head
  * strides dout_hs / dhid_hs elements; dhid_hs == HS means the heads side by
  * side, [B][5][HS] with rows 5 HS apart).  The KL terms this step added to the
@@ -275,9 +296,13 @@ int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, float v_plv, co
  * bit-identical to accumulating step by step.  rec: [T][rec_step_stride]
  * (mog_air_step_forward records), skl/shkl/vkl: [T, B].  Lets the VAE of all
  * T steps run after the recurrent loop as one set of launches over T*B rows
- * (AIR: the VAE output never feeds the recurrence). */
-int mog_air_runloss(int T, int B, const float* rec, long rec_step_stride, const float* skl,
-                    const float* shkl, const float* vkl, float* runloss, void* stream);
+ * (AIR: the VAE output never feeds the recurrence).  live (may be NULL): the
+ * loop-predicate flags [T+1] of mog_air_step_forward_steps, applied first: the
+ * z_pres term of a step that is not live becomes 0 and rec's z_pres-term and
+ * live slots are rewritten to what T single-step launches record. */
+int mog_air_runloss(int T, int B, float* rec, long rec_step_stride, const float* skl,
+                    const float* shkl, const float* vkl, float* runloss, const int* live,
+                    void* stream);
 /* ---- fused per-object step, bf16 configuration ----
  * One launch per loop step: glimpse = STN(x, theta_f) (transformer.py:18-175),
  * the glimpse VAE (vae.py:5-48: recognition 784->512->256 softplus, mean /

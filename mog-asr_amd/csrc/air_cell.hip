@@ -323,6 +323,140 @@ __global__ __launch_bounds__(256) void step_fwd_kernel(StepCfg cfg, HeadPtrs hp,
   if (io.zc) io.zc[b] = act ? z : 0.0f;
 }
 
+// Every loop step of the batch in ONE launch (AIR: the heads read h_t only --
+// the step's VAE never feeds the recurrence -- so once the LSTM chain has run,
+// every step's head outputs are available and only the per-image loop state
+// is sequential).  Operands of step t at step-0 pointer + t * (B * width);
+// the step values are the ones step_fwd_kernel computes, in the same order.
+// What depends on the batch-wide loop predicate is NOT resolved here: live[t]
+// is known only once every image of step t - 1 (and every rank, under data
+// parallelism) has run, so rec[R_ZTERM] holds the z_pres term the step adds
+// IF it is live (act_old ? zkl : kl_end), rec[R_LIVE] 1, and runloss is not
+// touched: mog_air_runloss with `live` applies the predicate and replays the
+// running loss (runloss_kernel), which gives the bits of T single-step
+// launches.  Lanes: 8 per loop step (lanes 0..6 one head-output chain each),
+// LPI = 8 * steps rounded to a power of two per image; every step's state-free
+// values (sampling, theta, z_pres, KLs) in lane 0 of its group at once; lane 0
+// of the image then walks the steps for the stopping sum, counts, masks.
+constexpr int MAX_STEPS_FWD = 8;
+struct StepsFwdIO {
+  StepFwdIO s;       // step-0 pointers (runloss unused)
+  long hid_step;     // elements between two steps' rows of one head's hidden layer
+  int steps;
+  float prior_bias[MAX_STEPS_FWD];
+};
+
+template <int LPI>
+__global__ __launch_bounds__(256) void step_fwd_steps_kernel(StepCfg cfg, HeadPtrs hp,
+                                                             StepsFwdIO q) {
+#pragma clang fp contract(off)
+  constexpr int IPB = 256 / LPI;  // images per block
+  const int B = cfg.B, T = q.steps;
+  const StepFwdIO& io = q.s;
+  const int b = blockIdx.x * IPB + threadIdx.x / LPI;
+  const int li = threadIdx.x % LPI;
+  const int t = li >> 3, j = li & 7, g0 = li & ~7;
+  const int head = j == 0 ? 0 : j == 1 ? 1 : j <= 3 ? 2 : j <= 5 ? 3 : 4;
+  const int col = (j == 3 || j == 5) ? 1 : 0;
+  const int kw = (head == 2 || head == 3) ? 2 : 1;
+  const int bc = min(b, B - 1), tc = min(t, T - 1);
+  const long rb = (long)tc * B + bc;  // row of (step tc, image bc)
+  // every input up front (see step_fwd_kernel)
+  const float e_s = io.eps_scale[rb], e_h0 = io.eps_shift[2 * rb], e_h1 = io.eps_shift[2 * rb + 1];
+  const float uu = io.u[rb];
+  const float stop0 = io.stop[bc];
+  const int dig0 = io.digits[bc];
+  const float pbias = q.prior_bias[tc];
+  float v = 0.0f;
+  if (b < B && t < T && j < 7) {
+    const int K = head == 4 ? cfg.HZ : cfg.HS;
+    v = chain_dot(hp.hid[head] + tc * q.hid_step + (size_t)bc * K, hp.w2[head] + col, K, kw) +
+        hp.b2[head][col];
+  }
+  const float sm = __shfl(v, g0, LPI), slv = __shfl(v, g0 + 1, LPI);
+  const float hm0 = __shfl(v, g0 + 2, LPI), hm1 = __shfl(v, g0 + 3, LPI);
+  const float hv0 = __shfl(v, g0 + 4, LPI), hv1 = __shfl(v, g0 + 5, LPI);
+  const float lo = __shfl(v, g0 + 6, LPI);
+
+  // the step's state-free values, as step_fwd_kernel computes them
+  const float svar = mog_expf(slv);
+  const float s = mog_sigmoidf(sm + e_s * sqrtf(svar));
+  const float hvar0 = mog_expf(hv0), hvar1 = mog_expf(hv1);
+  const float tx = mog_tanhf(hm0 + e_h0 * sqrtf(hvar0));
+  const float ty = mog_tanhf(hm1 + e_h1 * sqrtf(hvar1));
+  const float eps = 1e-9f;
+  const float noise = mog_logf(uu + eps) - mog_logf((1.0f - uu) + eps);
+  const float y = (lo + noise) / cfg.temperature;
+  float z = mog_sigmoidf(y);
+  if (!cfg.train) z = rintf(z);
+  float kl_end = 0.0f;
+  if (cfg.use_num_prior) kl_end = concrete_kl(y, -100.0f, cfg.temperature, lo, cfg.temperature);
+  const float zkl = concrete_kl(y, prior_log_odds(cfg) + pbias, cfg.temperature, lo,
+                                cfg.temperature);
+  const float skl = 0.5f * gauss_kl_term(cfg.s_plv, slv, svar, cfg.s_pv, sm, cfg.s_pm);
+  const float shs = gauss_kl_term(cfg.h_plv, hv0, hvar0, cfg.h_pv, hm0, cfg.h_pm) +
+                    gauss_kl_term(cfg.h_plv, hv1, hvar1, cfg.h_pv, hm1, cfg.h_pm);
+  const float shkl = 0.5f * shs;
+  if (b < B && t < T && j == 0) {
+    float* tf = io.theta_fwd + rb * 6;
+    tf[0] = s; tf[1] = 0.0f; tf[2] = tx; tf[3] = 0.0f; tf[4] = s; tf[5] = ty;
+    const float is = 1.0f / s;
+    float* tb = io.theta_back + rb * 6;
+    tb[0] = is; tb[1] = 0.0f; tb[2] = -tx / s; tb[3] = 0.0f; tb[4] = is; tb[5] = -ty / s;
+    io.scale_out[rb] = s;
+    io.shift_out[2 * rb] = tx;
+    io.shift_out[2 * rb + 1] = ty;
+    io.zprob_out[rb] = mog_sigmoidf(lo);
+    io.zkl_out[rb] = zkl;
+    io.skl_out[rb] = skl;
+    io.shkl_out[rb] = shkl;
+    float* r = io.rec + (size_t)tc * R_NREC * B;
+    r[R_SM * B + bc] = sm; r[R_SLV * B + bc] = slv;
+    r[R_HM0 * B + bc] = hm0; r[R_HM1 * B + bc] = hm1;
+    r[R_HLV0 * B + bc] = hv0; r[R_HLV1 * B + bc] = hv1;
+    r[R_LO * B + bc] = lo; r[R_S * B + bc] = s; r[R_TX * B + bc] = tx; r[R_TY * B + bc] = ty;
+    r[R_Y * B + bc] = y; r[R_Z * B + bc] = z;
+  }
+  // the loop state, step by step (lane 0 of the image; every lane shuffles)
+  float zs[MAX_STEPS_FWD], zk[MAX_STEPS_FWD], ke[MAX_STEPS_FWD];
+#pragma unroll
+  for (int u = 0; u < MAX_STEPS_FWD; ++u) {
+    if (8 * u < LPI) {
+      zs[u] = __shfl(z, 8 * u, LPI);
+      zk[u] = __shfl(zkl, 8 * u, LPI);
+      ke[u] = __shfl(kl_end, 8 * u, LPI);
+    }
+  }
+  if (b >= B || li != 0) return;
+  float stop_old = stop0;
+  int dig = dig0;
+#pragma unroll
+  for (int u = 0; u < MAX_STEPS_FWD; ++u) {
+    if (8 * u >= LPI || u >= T) break;
+    const long ru = (long)u * B + b;
+    const bool act_old = stop_old < cfg.thr;
+    const float zterm = act_old ? zk[u] : ke[u];  // (applied if live: mog_air_runloss)
+    const float stop_new = stop_old + (1.0f - zs[u]);
+    const bool act = stop_new < cfg.thr;
+    if (act) {
+      dig = dig + 1;
+      io.live[u + 1] = 1;
+    }
+    io.zmask[ru] = act ? 1.0f : 0.0f;
+    io.zval[ru] = zs[u];
+    if (io.zc) io.zc[ru] = act ? zs[u] : 0.0f;
+    float* r = io.rec + (size_t)u * R_NREC * B;
+    r[R_ACT_OLD * B + b] = act_old ? 1.0f : 0.0f;
+    r[R_ACT * B + b] = act ? 1.0f : 0.0f;
+    r[R_LIVE * B + b] = 1.0f;
+    r[R_ZC * B + b] = act ? zs[u] : 0.0f;
+    r[R_ZTERM * B + b] = zterm;
+    stop_old = stop_new;
+  }
+  io.stop[b] = stop_old;
+  io.digits[b] = dig;
+}
+
 struct StepBwdIO {
   const float* rec;         // [R_NREC, B]
   const float* eps_scale;   // [B]
@@ -500,17 +634,26 @@ __global__ __launch_bounds__(256) void vae_sample_fwd_kernel(VaeCfg c, const flo
 // Per-image running loss of all T steps replayed from the step records in the
 // order the step kernels accumulate it (step_fwd_kernel, then the VAE KL):
 // for the VAE of every step run after the loop (AIR, all T*B rows at once).
-__global__ __launch_bounds__(256) void runloss_kernel(int T, int B, const float* __restrict__ rec,
+// With `live` (the records of step_fwd_steps_kernel): the loop predicate is
+// applied first -- the z_pres term of a step that is not live is 0 and its
+// records say so (rec[R_ZTERM], rec[R_LIVE] rewritten).
+__global__ __launch_bounds__(256) void runloss_kernel(int T, int B, float* __restrict__ rec,
                                                       long rstride, const float* __restrict__ skl,
                                                       const float* __restrict__ shkl,
                                                       const float* __restrict__ vkl,
-                                                      float* runloss) {
+                                                      float* runloss, const int* live) {
 #pragma clang fp contract(off)
   const int b = blockIdx.x * 256 + threadIdx.x;
   if (b >= B) return;
   float rl = 0.0f;
   for (int t = 0; t < T; ++t) {
-    const float* r = rec + t * rstride;
+    float* r = rec + t * rstride;
+    if (live) {
+      const bool lv = live[t] != 0;
+      const float zt = lv ? r[R_ZTERM * B + b] : 0.0f;
+      r[R_ZTERM * B + b] = zt;
+      r[R_LIVE * B + b] = lv ? 1.0f : 0.0f;
+    }
     rl = rl + r[R_ZTERM * B + b];
     if (r[R_ACT * B + b] != 0.0f) {
       const size_t i = (size_t)t * B + b;
@@ -822,6 +965,50 @@ extern "C" int mog_air_step_forward(
   MOG_LAUNCH_RET();
 }
 
+extern "C" int mog_air_step_forward_steps(
+    int steps, int B, int HS, int HZ, int train, int use_num_prior, float thr, float temperature,
+    float prior_lo, const float* prior_bias, float s_pm, float s_pv, float s_plv, float h_pm,
+    float h_pv, float h_plv, const float* const* hid, long hid_step, const float* const* w2,
+    const float* const* b2, const float* eps_scale, const float* eps_shift, const float* u,
+    float* stop, int* digits, int* live, float* rec, float* theta_fwd, float* theta_back,
+    float* scale_out, float* shift_out, float* zprob_out, float* zkl_out, float* skl_out,
+    float* shkl_out, float* zmask, float* zval, float* zc, const float* prior_lo_dev,
+    void* stream) {
+  MOG_CHECK_ARG(steps >= 1 && steps <= MAX_STEPS_FWD && B >= 0 && prior_bias);
+  MOG_CHECK_ARG(hid && w2 && b2 && eps_scale && eps_shift && u && stop);
+  MOG_CHECK_ARG(digits && live && rec && theta_fwd && theta_back && scale_out && shift_out);
+  MOG_CHECK_ARG(zprob_out && zkl_out && skl_out && shkl_out && zmask && zval);
+  MOG_CHECK_ARG(hid_step >= (long)B * (HS > HZ ? HS : HZ));
+  if (B == 0) return 0;
+  StepCfg c;
+  c.B = B; c.H = 0; c.HS = HS; c.HZ = HZ; c.train = train; c.use_num_prior = use_num_prior;
+  c.step = 0; c.thr = thr; c.temperature = temperature; c.prior_lo = prior_lo;
+  c.prior_bias = 0.0f; c.s_pm = s_pm; c.s_pv = s_pv; c.s_plv = s_plv; c.h_pm = h_pm;
+  c.h_pv = h_pv; c.h_plv = h_plv; c.grad_scale = 0.0f; c.prior_lo_dev = prior_lo_dev;
+  HeadPtrs hp;
+  for (int i = 0; i < 5; ++i) {
+    MOG_CHECK_ARG(hid[i] && w2[i] && b2[i]);
+    hp.hid[i] = hid[i]; hp.w2[i] = w2[i]; hp.b2[i] = b2[i];
+  }
+  StepsFwdIO q;
+  q.s = StepFwdIO{eps_scale, eps_shift, u,         stop,      nullptr,  digits,  live,
+                  rec,       theta_fwd, theta_back, scale_out, shift_out, zprob_out, zkl_out,
+                  skl_out,   shkl_out,  zmask,     zval,      zc};
+  q.hid_step = hid_step;
+  q.steps = steps;
+  for (int t = 0; t < MAX_STEPS_FWD; ++t) q.prior_bias[t] = t < steps ? prior_bias[t] : 0.0f;
+  hipStream_t s = mog_stream(stream);
+  const int lpi = steps == 1 ? 8 : steps == 2 ? 16 : steps <= 4 ? 32 : 64;
+  const int grid = mog_cdiv((long)B * lpi, 256);
+  switch (lpi) {
+    case 8: step_fwd_steps_kernel<8><<<grid, 256, 0, s>>>(c, hp, q); break;
+    case 16: step_fwd_steps_kernel<16><<<grid, 256, 0, s>>>(c, hp, q); break;
+    case 32: step_fwd_steps_kernel<32><<<grid, 256, 0, s>>>(c, hp, q); break;
+    default: step_fwd_steps_kernel<64><<<grid, 256, 0, s>>>(c, hp, q); break;
+  }
+  MOG_LAUNCH_RET();
+}
+
 extern "C" int mog_air_step_backward_steps(
     int steps, int B, int HS, int train, int use_num_prior, float temperature, float prior_lo,
     float prior_bias, float s_pm, float s_pv, float h_pm, float h_pv, float grad_scale,
@@ -896,14 +1083,14 @@ extern "C" int mog_vae_sample_forward(int B, int Z, float v_pm, float v_pv, floa
   MOG_LAUNCH_RET();
 }
 
-extern "C" int mog_air_runloss(int T, int B, const float* rec, long rec_step_stride,
+extern "C" int mog_air_runloss(int T, int B, float* rec, long rec_step_stride,
                                const float* skl, const float* shkl, const float* vkl,
-                               float* runloss, void* stream) {
+                               float* runloss, const int* live, void* stream) {
   MOG_CHECK_ARG(T >= 1 && B >= 0 && rec && skl && shkl && vkl && runloss);
   MOG_CHECK_ARG(rec_step_stride >= (long)R_NREC * B);
   if (B == 0) return 0;
-  runloss_kernel<<<mog_cdiv(B, 256), 256, 0, mog_stream(stream)>>>(T, B, rec, rec_step_stride,
-                                                                   skl, shkl, vkl, runloss);
+  runloss_kernel<<<mog_cdiv(B, 256), 256, 0, mog_stream(stream)>>>(
+      T, B, rec, rec_step_stride, skl, shkl, vkl, runloss, live);
   MOG_LAUNCH_RET();
 }
 

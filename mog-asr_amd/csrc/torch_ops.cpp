@@ -415,6 +415,56 @@ void air_step_forward_(int64_t B, int64_t HS, int64_t HZ, int64_t step, bool tra
         o.name);
 }
 
+// every loop step in one launch (mog_air_step_forward_steps): operands over
+// steps * B rows, hid[z] over steps * B rows of HS (HZ for the z_pres head)
+void air_step_forward_steps_(int64_t steps, int64_t B, int64_t HS, int64_t HZ, bool train,
+                             bool use_num_prior, double thr, double temperature, double prior_lo,
+                             at::ArrayRef<double> prior_bias, double s_pm, double s_pv,
+                             double s_plv, double h_pm, double h_pv, double h_plv,
+                             at::TensorList hid, at::TensorList w2, at::TensorList b2,
+                             const Tensor& eps_scale, const Tensor& eps_shift, const Tensor& u,
+                             Tensor stop, Tensor digits, Tensor live, Tensor rec,
+                             Tensor theta_fwd, Tensor theta_back, Tensor scale, Tensor shift,
+                             Tensor zprob, Tensor zkl, Tensor skl, Tensor shkl, Tensor zmask,
+                             Tensor zval, Tensor zc, const optional<Tensor>& prior_lo_dev) {
+  Op o("air_step_forward_steps_");
+  TORCH_CHECK(hid.size() == 5 && w2.size() == 5 && b2.size() == 5, o.name, ": 5 heads");
+  TORCH_CHECK(steps >= 1 && steps <= 8 && (int64_t)prior_bias.size() == steps, o.name,
+              ": 1 <= steps <= 8 and one prior bias per step");
+  TORCH_CHECK(HZ == HS, o.name, ": the heads' hidden rows are one [5, steps * B, HS] layout");
+  const int64_t R = steps * B;
+  float* pst = o.f(stop, B, "stop");
+  auto h = o.list(hid, F32, R * HS, "hid"), w = o.list(w2, F32, HS, "w2"),
+       b = o.list(b2, F32, 1, "b2");
+  float* pes = o.f(eps_scale, R, "eps_scale");
+  float* peh = o.f(eps_shift, 2 * R, "eps_shift");
+  float* pu = o.f(u, R, "u");
+  int* pd = o.i(digits, B, "digits");
+  int* pl = o.i(live, steps + 1, "live");
+  float* pr = o.f(rec, 17 * R, "rec");
+  float* ptf = o.f(theta_fwd, 6 * R, "theta_fwd");
+  float* ptb = o.f(theta_back, 6 * R, "theta_back");
+  float* psc = o.f(scale, R, "scale");
+  float* psh = o.f(shift, 2 * R, "shift");
+  float* pzp = o.f(zprob, R, "zprob");
+  float* pzk = o.f(zkl, R, "zkl");
+  float* psk = o.f(skl, R, "skl");
+  float* phk = o.f(shkl, R, "shkl");
+  float* pzm = o.f(zmask, R, "zmask");
+  float* pzv = o.f(zval, R, "zval");
+  float* pzc = o.f(zc, R, "zc");
+  float* pplo = o.f(prior_lo_dev, 1, "prior_lo_dev");
+  float pb[8];
+  for (int64_t t = 0; t < steps; ++t) pb[t] = (float)prior_bias[t];
+  GUARD(o);
+  check(mog_air_step_forward_steps(steps, B, HS, HZ, train, use_num_prior, thr, temperature,
+                                   prior_lo, pb, s_pm, s_pv, s_plv, h_pm, h_pv, h_plv,
+                                   arr<float>(h), B * HS, arr<float>(w), arr<float>(b), pes, peh,
+                                   pu, pst, pd, pl, pr, ptf, ptb, psc, psh, pzp, pzk, psk, phk,
+                                   pzm, pzv, pzc, pplo, o.stream()),
+        o.name);
+}
+
 void air_step_backward_(int64_t B, int64_t HS, bool train, bool use_num_prior,
                         double temperature, double prior_lo, double prior_bias, double s_pm,
                         double s_pv, double h_pm, double h_pv, double grad_scale,
@@ -484,16 +534,18 @@ void vae_sample_forward_(int64_t B, int64_t Z, double v_pm, double v_pv, double 
         o.name);
 }
 
-void air_runloss_(int64_t T, int64_t B, const Tensor& rec, int64_t rec_step_stride,
-                  const Tensor& skl, const Tensor& shkl, const Tensor& vkl, Tensor runloss) {
+void air_runloss_(int64_t T, int64_t B, Tensor rec, int64_t rec_step_stride, const Tensor& skl,
+                  const Tensor& shkl, const Tensor& vkl, Tensor runloss,
+                  const optional<Tensor>& live) {
   Op o("air_runloss_");
   float* prl = o.f(runloss, B, "runloss");
   float* pr = o.f(rec, (T - 1) * rec_step_stride + 17 * B, "rec");
   float* ps = o.f(skl, T * B, "skl");
   float* ph = o.f(shkl, T * B, "shkl");
   float* pv = o.f(vkl, T * B, "vkl");
+  int* pl = live.has_value() ? o.i(*live, T, "live") : nullptr;
   GUARD(o);
-  check(mog_air_runloss(T, B, pr, rec_step_stride, ps, ph, pv, prl, o.stream()), o.name);
+  check(mog_air_runloss(T, B, pr, rec_step_stride, ps, ph, pv, prl, pl, o.stream()), o.name);
 }
 
 void vae_sample_backward_(int64_t B, int64_t Z, double v_pm, double v_pv, double grad_scale,
@@ -1167,6 +1219,15 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "Tensor(j!) zprob, Tensor(k!) zkl, Tensor(l!) skl, Tensor(m!) shkl, Tensor(n!) zmask, "
       "Tensor(o!) zval, Tensor(p!) zc, Tensor? prior_lo_dev=None) -> ()");
   m.def(
+      "air_step_forward_steps_(int steps, int B, int HS, int HZ, bool train, bool use_num_prior, "
+      "float thr, float temperature, float prior_lo, float[] prior_bias, float s_pm, float s_pv, "
+      "float s_plv, float h_pm, float h_pv, float h_plv, Tensor[] hid, Tensor[] w2, "
+      "Tensor[] b2, Tensor eps_scale, Tensor eps_shift, Tensor u, Tensor(a!) stop, "
+      "Tensor(c!) digits, Tensor(d!) live, Tensor(e!) rec, "
+      "Tensor(f!) theta_fwd, Tensor(g!) theta_back, Tensor(h!) scale, Tensor(i!) shift, "
+      "Tensor(j!) zprob, Tensor(k!) zkl, Tensor(l!) skl, Tensor(m!) shkl, Tensor(n!) zmask, "
+      "Tensor(o!) zval, Tensor(p!) zc, Tensor? prior_lo_dev=None) -> ()");
+  m.def(
       "air_step_backward_(int B, int HS, bool train, bool use_num_prior, float temperature, "
       "float prior_lo, float prior_bias, float s_pm, float s_pv, float h_pm, float h_pv, "
       "float grad_scale, Tensor? dloss, Tensor rec, Tensor eps_scale, Tensor eps_shift, "
@@ -1185,8 +1246,8 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "Tensor lv, Tensor eps, Tensor(a!) z, Tensor(b!)? z_bf16, int ld_zb, Tensor act, "
       "Tensor(c!)? runloss, Tensor(d!) vkl) -> ()");
   m.def(
-      "air_runloss_(int T, int B, Tensor rec, int rec_step_stride, Tensor skl, Tensor shkl, "
-      "Tensor vkl, Tensor(a!) runloss) -> ()");
+      "air_runloss_(int T, int B, Tensor(b!) rec, int rec_step_stride, Tensor skl, Tensor shkl, "
+      "Tensor vkl, Tensor(a!) runloss, Tensor? live=None) -> ()");
   m.def(
       "vae_sample_backward_(int B, int Z, float v_pm, float v_pv, float grad_scale, Tensor mu, "
       "Tensor lv, Tensor eps, Tensor dz, Tensor act, Tensor(a!)? dmu, Tensor(b!)? dlv, "
@@ -1277,6 +1338,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("lstm_cell_forward2_", &lstm_cell_forward2_);
   m.impl("lstm_cell_backward2_", &lstm_cell_backward2_);
   m.impl("air_step_forward_", &air_step_forward_);
+  m.impl("air_step_forward_steps_", &air_step_forward_steps_);
   m.impl("air_step_backward_", &air_step_backward_);
   m.impl("generation_prior_", &generation_prior_);
   m.impl("vae_sample_forward_", &vae_sample_forward_);

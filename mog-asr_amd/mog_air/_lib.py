@@ -48,6 +48,8 @@ _SIGS = {
     "mog_lstm_cell_backward_pair": [P, I, I, P],
     "mog_air_step_forward": [I, I, I, I, I, I, F, F, F, F, F, F, F, F, F, F, P, P, P, P, P, P,
                              P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "mog_air_step_forward_steps": [I, I, I, I, I, I, F, F, F, P, F, F, F, F, F, F, P, L, P, P, P,
+                                   P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "mog_air_step_backward": [I, I, I, I, F, F, F, F, F, F, F, F, P, P, P, P, P, P, P, P, P,
                               P, L, P, L, P],
     "mog_air_step_backward_steps": [I, I, I, I, I, F, F, F, F, F, F, F, F, P, P, P, P, P, P, P,
@@ -58,7 +60,7 @@ _SIGS = {
     "mog_pack_frag_f32": [I, P, P, P, P, P],
     "mog_stn_vae_step_forward_f32": ([I, I] + [P] * 7 + [I, ULL, ULL] + [P] * 2 + [F] * 4
                                      + [P] * 19 + [I, P]),
-    "mog_air_runloss": [I, I, P, L, P, P, P, P, P],
+    "mog_air_runloss": [I, I, P, L, P, P, P, P, P, P],
     "mog_stn_write_parts": [P, I, I, I, P, I, I, P, P, P, P, P],
     "mog_vae_sample_backward": [I, I, F, F, F, P, P, P, P, P, P, P, P, P, I, P],
     "mog_sigmoid_backward": [P, P, P, L, I, P],

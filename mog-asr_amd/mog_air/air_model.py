@@ -455,6 +455,10 @@ class AIRModel(WeightGradients, GraphCapture, Results):
     # AIR's _forward joins side-stream noise after the x-projection (the ASR
     # subclass fills on the current stream)
     NOISE_ON_SIDE = True
+    # batched VAE: every step's heads and scalars in one launch each after
+    # the LSTM chain (False: per step, as the unbatched loop;
+    # tests/test_gpu_steps_fwd.py compares the two bitwise)
+    STEPS_ONE_LAUNCH = True
 
     # ----------------------------------------------------------- forward ---
     def _forward(self, X: torch.Tensor, targets: Optional[torch.Tensor], ws: _Workspace,
@@ -503,8 +507,10 @@ class AIRModel(WeightGradients, GraphCapture, Results):
         b1 = [self._P(h + "/hidden/biases") for h in self._HEADS]
         w2 = [self._P(h + "/output/weights") for h in self._HEADS]
         b2 = [self._P(h + "/output/biases") for h in self._HEADS]
-        vw = {n: self._P("vae/" + n + "/weights") for n in self._VAE}
-        vb = {n: self._P("vae/" + n + "/biases") for n in self._VAE}
+        # batched VAE: the LSTM chain first, then every step's heads over T*B
+        # rows and every step's scalars in one launch each (the heads read h_t
+        # only; mog_air_step_forward_steps)
+        steps_all = batched and T <= 8 and self.STEPS_ONE_LAUNCH
         for t in range(T):
             if t == 0:
                 _ops.lstm_cell_forward_(ws.Gx, bK, None, ws.c[0], ws.h[0], B, H)
@@ -512,6 +518,8 @@ class AIRModel(WeightGradients, GraphCapture, Results):
                 gemm([ws.h[t - 1]], [Wh], [ws.G[t]], B, 4 * H, H, H, 4 * H, 4 * H, bias=[bK],
                      Cin=[ws.Gx])
                 _ops.lstm_cell_forward_(ws.G[t], None, ws.c[t - 1], ws.c[t], ws.h[t], B, H)
+            if steps_all:
+                continue
             hid_t = [ws.hid[z, t] for z in range(5)]
             gemm([ws.h[t]] * 5, w1, hid_t, B, HS, H, H, HS, HS, epi=EPI_RELU, bias=b1)
             bias_t = float(self.marginal[t]) if self.marginal is not None else 0.0
@@ -541,11 +549,30 @@ class AIRModel(WeightGradients, GraphCapture, Results):
             # STN write + masked canvas accumulation (air_model.py:580-588, 665-675)
             ops.stn_forward(ws.r[t], ws.th_b[t], (C, C), out=ws.canvas, z=ws.zval[t],
                             mask=ws.zmask[t], accumulate=True)
+        if steps_all:
+            TB = T * B
+            gemm([ws.h.view(TB, H)] * 5, w1, [ws.hid[z].view(TB, HS) for z in range(5)], TB, HS,
+                 H, H, HS, HS, epi=EPI_RELU, bias=b1)
+            biases = [float(self.marginal[t]) if self.marginal is not None else 0.0
+                      for t in range(T)]
+            _ops.air_step_forward_steps_(
+                T, B, HS, HS, self.train, self.marginal is not None, thr, temperature, prior_lo,
+                biases, float(self.scale_prior_mean), float(self.scale_prior_variance),
+                self.scale_prior_log_variance, float(self.shift_prior_mean),
+                float(self.shift_prior_variance), self.shift_prior_log_variance,
+                [ws.hid[z] for z in range(5)], w2, b2, ws.eps_scale, ws.eps_shift, ws.u, ws.stop,
+                ws.digits, ws.live, ws.rec, ws.th_f, ws.th_b, ws.scale, ws.shift, ws.zprob,
+                ws.zkl, ws.skl, ws.shkl, ws.zmask, ws.zval, ws.zc, self._prior_arg())
+            if self.live_hook is not None:
+                for t in range(T):
+                    self.live_hook(ws.live, t)
         if batched:
             self._vae_forward_all(X, ws, float(lik_std), save=need_grad)
             # the running loss in the loop's order (z_pres term, scale, shift
-            # and VAE KLs per step), replayed from the step records
-            _ops.air_runloss_(T, B, ws.rec, R_NREC * B, ws.skl, ws.shkl, ws.vkl, ws.runloss)
+            # and VAE KLs per step), replayed from the step records; with the
+            # one-launch steps, the loop predicate live[t] applied here first
+            _ops.air_runloss_(T, B, ws.rec, R_NREC * B, ws.skl, ws.shkl, ws.vkl, ws.runloss,
+                              ws.live if steps_all else None)
         self._forward_loss(X, targets, ws, need_grad, outputs)
 
     def _parts_layout(self, B: int) -> bool:

@@ -1,5 +1,5 @@
-"""Copies the round-5 bench evidence out of gpurun_out/ (scripts/final_r05.sh,
-scripts/prof_r05.sh) into profiles/: the bench JSON line measured under
+"""Copies a round's bench evidence (ROUND, default r06) out of gpurun_out/ (scripts/final_pass.sh,
+scripts/prof_evidence.sh) into profiles/: the bench JSON line measured under
 rocprofv3 and that run's --stats kernel summary; with --traces also the
 per-workload kernel traces (start / duration / queue / grid / name)."""
 import csv
@@ -10,23 +10,24 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-O = os.path.join(ROOT, "gpurun_out", "r05prof")
+R = os.environ.get("ROUND", "r06")
+O = os.path.join(ROOT, "gpurun_out", R + "prof")
 P = os.path.join(ROOT, "profiles")
 
 
 def main():
     line = [ln for ln in open(os.path.join(O, "bench.log")) if ln.startswith("{")][-1]
     json.loads(line)
-    with open(os.path.join(P, "r05_bench.json"), "w") as f:
+    with open(os.path.join(P, R + "_bench.json"), "w") as f:
         f.write(line)
     stats = glob.glob(os.path.join(O, "bench", "**", "*kernel_stats.csv"), recursive=True)
-    shutil.copy(stats[0], os.path.join(P, "r05_bench_kernel_stats.csv"))
+    shutil.copy(stats[0], os.path.join(P, R + "_bench_kernel_stats.csv"))
     if "--traces" in sys.argv:
         for td in sorted(glob.glob(os.path.join(O, "t_*"))):
             tr = glob.glob(os.path.join(td, "**", "*kernel_trace.csv"), recursive=True)[0]
             rows = list(csv.DictReader(open(tr)))
             t0 = min(int(r["Start_Timestamp"]) for r in rows)
-            name = os.path.join(P, "r05_trace_" + os.path.basename(td)[2:] + ".csv")
+            name = os.path.join(P, R + "_trace_" + os.path.basename(td)[2:] + ".csv")
             with open(name, "w", newline="") as f:
                 w = csv.writer(f)
                 w.writerow(["start_us", "dur_us", "stream", "grid_x", "kernel"])

@@ -1,5 +1,5 @@
-"""Round-5 per-workload kernel tables and the bench's traffic entries, from
-rocprofv3 passes of scripts/prof_one.py (scripts/prof_r05.sh): per kernel
+"""Per-workload kernel tables and the bench's traffic entries, from
+rocprofv3 passes of scripts/prof_one.py (scripts/prof_evidence.sh): per kernel
 symbol the dispatches, average duration (kernel trace) and HBM bytes per
 dispatch from separate FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md
 §HBM: FETCH_SIZE halves a wide coalesced read on gfx950, so it is doubled;
@@ -8,7 +8,7 @@ merges one entry per bench.py roofline tag -- "<tag>_<precision>_b<B>",
 hbm_bytes_per_launch averaged over the tag's dispatches -- into
 profiles/pmc_summary.json (stale tags of earlier rounds are dropped).
 
-usage: python scripts/pmc_r05.py <dir with t_*/f_*/w_* pass outputs> <out.json>"""
+usage: python scripts/pmc_tables.py <dir with t_*/f_*/w_* pass outputs> <out.json> [round tag]"""
 import csv
 import glob
 import json
@@ -92,6 +92,7 @@ def pick(v, which):
 
 def main():
     root, out = sys.argv[1], sys.argv[2]
+    rnd = sys.argv[3] if len(sys.argv) > 3 else "r06"
     tables, data = {}, {}
     for td in sorted(glob.glob(os.path.join(root, "t_*"))):
         w = os.path.basename(td)[2:]
@@ -111,10 +112,10 @@ def main():
         summary = json.load(open(SUMMARY))
     except (OSError, ValueError):
         summary = {}
-    summary = {k: v for k, v in summary.items() if k.startswith("_") or "source" in v and "round 5" in v["source"]}
+    summary = {k: v for k, v in summary.items() if k.startswith("_") or "source" in v and v["source"].endswith(f"({rnd})")}
     summary["_note"] = ("hbm_bytes_per_launch = 2*FETCH_SIZE + WRITE_SIZE per dispatch (gfx950 "
                         "FETCH_SIZE halving corrected), from separate --pmc passes of "
-                        "scripts/prof_one.py workloads (scripts/prof_r05.sh); key = bench.py "
+                        "scripts/prof_one.py workloads (scripts/prof_evidence.sh); key = bench.py "
                         "roofline tag _ precision _ b<batch>, averaged over the tag's dispatches")
     for tag, (w, pred, which) in TAGS.items():
         if w not in data:
@@ -133,7 +134,7 @@ def main():
         summary[tag] = {"kernel_symbols": syms, "workload": w, "dispatches": len(durs),
                         "profiled_avg_us": sum(durs) / len(durs), "fetch_bytes": fetch,
                         "write_bytes": write, "hbm_bytes_per_launch": fetch + write,
-                        "source": "scripts/prof_r05.sh (round 5)"}
+                        "source": f"scripts/prof_evidence.sh ({rnd})"}
     with open(SUMMARY, "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps({k: (v.get("profiled_avg_us"), v.get("hbm_bytes_per_launch"))
