@@ -932,11 +932,21 @@ int launch_auto(bool ta, bool tb, int epi, hipStream_t s, const GemmPtrs& P, con
       small = !ta && (atoi(force) == 3264 || atoi(force) == 3232);
       tiny = !ta && atoi(force) == 3232;
     }
+    // Four stages with fragment double-buffering: each workgroup walks a long
+    // serial k chain (no split-K), so two k-tiles of DMA stay in flight and a
+    // tile's fragments are read while the previous one's MFMAs run (captured
+    // batch-64 step 0.396 -> 0.391 ms, AIR-ASR 1.355 -> 1.347 ms; three stages,
+    // without the fragment double-buffering, 0.438 ms).  MOG_GEMM_TNS=2
+    // (profiling build) keeps the two-stage form.
+    static const char* tns_env = mog_prof_env("MOG_GEMM_TNS");
+    const bool tns2 = tns_env != nullptr && atoi(tns_env) == 2;
     if (tiny) {
-      return launch_dma<32, 32, 32, 2>(ta, tb, epi, s, P, D, batch);
+      if (tns2) return launch_dma<32, 32, 32, 2>(ta, tb, epi, s, P, D, batch);
+      return launch_dma<32, 32, 32, 4>(ta, tb, epi, s, P, D, batch);
     }
     if (small) {
-      return launch_dma<32, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
+      if (tns2) return launch_dma<32, 64, 32, 2>(ta, tb, epi, s, P, D, batch);
+      return launch_dma<32, 64, 32, 4>(ta, tb, epi, s, P, D, batch);
     }
     // stages (measured, scripts/bench_gemm_f32.py): 4 with fragment
     // double-buffering for the split-K weight gradients (transA), 3 for the
