@@ -1,1 +1,1 @@
-#define MOG_BUILD_ID "339fa036a2ccd2e6"
+#define MOG_BUILD_ID "04e17c3b3e5eaa98"

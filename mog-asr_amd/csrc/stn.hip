@@ -758,8 +758,16 @@ __global__ __launch_bounds__(256, 4) void stn_bwd_kernel(
   // descriptor below is then provably uniform -- otherwise hipcc wraps every
   // buffer load of the T pass in a waterfall loop and serialises them
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int n = blockIdx.x * (blockDim.x >> 6) + wv;
-  if (n >= N) return;  // no workgroup barriers below
+  const int q = blockIdx.x * (blockDim.x >> 6) + wv;
+  if (q >= N) return;  // no workgroup barriers below
+  // rows sharing a periodic operand (AIR's T loop steps of one image: the
+  // canvas cotangent of the write backward, the input canvas of the read
+  // backward) run back to back on neighbouring waves, so the shared image is
+  // read from HBM once and from L2 by the other steps; each row is still
+  // computed by one wave alone, so the results do not change
+  const int per = u_period > 0 ? u_period : g_period;
+  const int nt = per > 0 && N % per == 0 ? N / per : 1;
+  const int n = nt > 1 ? (q % nt) * per + q / nt : q;
   TS(0);
   const int HWin = Hin * Win;
   const bool want_dU = dU != nullptr;

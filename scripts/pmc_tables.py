@@ -23,10 +23,11 @@ SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 # | "5not4" / "5is4": all but / only every fifth, from the fifth)
 TAGS = {
     "stn_vae_step_f32_all_fp32_b8192": ("step_fp32_8192", lambda k: "stn_vae_step_f32_kernel" in k, "all"),
-    # gemm_x3_tn_kernel<false,3> runs the four VAE weight gradients, then (launched
-    # later in the step) the LSTM recurrent rows: five per step in that order
-    "vae_wgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_x3_tn_kernel<false, 3>" in k, "5not4"),
-    "rec_wgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_x3_tn_kernel<false, 3>" in k, "5is4"),
+    # wgrad_tn_x3_kernel runs the seven VAE weight gradients (grouped), then,
+    # later in the step, the LSTM recurrent rows: two per step in that order
+    # (each followed by its wgrad_tn_reduce_kernel, not counted here)
+    "vae_wgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: k.startswith("wgrad_tn_x3_kernel"), "even"),
+    "rec_wgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: k.startswith("wgrad_tn_x3_kernel"), "odd"),
     "vae_dgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_x3_nt_kernel" in k, "all"),
     "lstm_x_projection_grad_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_x3_tn_kernel<true, 3>" in k, "all"),
     "lstm_x_projection_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_f32_dma_kernel<128, 128, 16, 3, false, false, 0>" in k, "all"),
@@ -36,12 +37,15 @@ TAGS = {
     "wgrad_f32_fp32_b8192": ("step_fp32_8192", lambda k: ("gemm_f32_dma_kernel" in k or "gemm_f32_kernel" in k)
                              and "true, false, 5" in k, "all"),
     "stn_vae_step_all_bf16_b8192": ("step_bf16_8192", lambda k: k.startswith("void stn_vae_step_kernel"), "all"),
-    "wgrad_bf16_bf16_b8192": ("step_bf16_8192", lambda k: "gemm_bf16_kernel" in k and "true, 4>" in k, "all"),
+    "vae_wgrad_bf16_bf16_b8192": ("step_bf16_8192", lambda k: "wgrad_tn_bf16_kernel" in k, "all"),
     "lstm_x_projection_grad_bf16_b8192": ("step_bf16_8192", lambda k: "gemm_x3_tn_kernel<true, 1>" in k, "all"),
     "lstm_x_projection_bf16_b8192": ("step_bf16_8192", lambda k: "gemm_f32_dma_kernel<128, 128, 16, 3, false, false, 0>" in k, "all"),
     "stn_vae_step_b65536": ("fused_bf16_65536_50", lambda k: k.startswith("void stn_vae_step_kernel"), "last5"),
     "stn_vae_step_b65536_c64": ("fused_bf16_65536_64", lambda k: k.startswith("void stn_vae_step_kernel"), "last5"),
 }
+
+
+STEP_N, STEP_KEEP = 15, 5  # prof_one.py's train-step workloads: 10 warm-up + 5 steps
 
 
 def short(sym):
@@ -123,10 +127,14 @@ def main():
         tr, fe, wr = data[w]
         syms = [k for k in tr if pred(k)]
         durs, fb, wb = [], [], []
+        # train-step workloads (prof_one.py: STEP_N steps, of which the last
+        # STEP_KEEP are kept -- the clocks settle over the first ones)
+        keep = (lambda v: v[len(v) - len(v) // STEP_N * STEP_KEEP:]) if w.startswith("step_") \
+            else (lambda v: v)
         for k in syms:
-            durs += pick(tr[k], which)
-            fb += pick(fe.get(k, []), which)
-            wb += pick(wr.get(k, []), which)
+            durs += pick(keep(tr[k]), which)
+            fb += pick(keep(fe.get(k, [])), which)
+            wb += pick(keep(wr.get(k, [])), which)
         if not durs or not fb or not wb:
             continue
         fetch = 2 * sum(fb) / len(fb) * 1024

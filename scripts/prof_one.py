@@ -3,8 +3,10 @@ be mixed with others' (kernel trace, --pmc FETCH_SIZE / WRITE_SIZE):
 
   fused_bf16 [B] [C]  the north-star fused step launch (bench.fused_step_roofline:
                       training form, one loop step), 5 launches after 2 warm-ups
-  step_fp32 [B]       the headline fp32 train step (bench defaults), 3 steps after 2
-  step_bf16 [B]       configs[1]'s bf16 train step, 3 steps after 2
+  step_fp32 [B]       the headline fp32 train step (bench defaults), 5 steps after 10
+                      (the clocks settle over the first steps: the tables keep
+                      the last 5 steps' dispatches)
+  step_bf16 [B]       configs[1]'s bf16 train step, 5 steps after 10
   fused_f32 [B]       the fp32 fused step over B rows (bench.fp32_step_roofline)
   asr_fp32 / asr_bf16 [B]  configs[2]'s AIR-ASR train step, 3 steps after 2
 
@@ -19,6 +21,9 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 
+STEPS, WARM = 5, 10  # train-step workloads (scripts/pmc_tables.py keeps the last STEPS)
+
+
 def main():
     w = sys.argv[1]
     dev = torch.device("cuda:0")
@@ -30,8 +35,8 @@ def main():
     elif w in ("step_fp32", "step_bf16"):
         B = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
         prec = w.split("_")[1]
-        el, m = bench.timed_train(prec, B, 3, 2, dev, scope="prof_" + prec)
-        print(f"{w} B={B}: {el / 3 * 1e3:.3f} ms per step")
+        el, m = bench.timed_train(prec, B, STEPS, WARM, dev, scope="prof_" + prec)
+        print(f"{w} B={B}: {el / STEPS * 1e3:.3f} ms per step")
     elif w in ("asr_fp32", "asr_bf16"):
         B = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
         prec = w.split("_")[1]
