@@ -23,7 +23,7 @@ def main():
     stats = glob.glob(os.path.join(O, "bench", "**", "*kernel_stats.csv"), recursive=True)
     shutil.copy(stats[0], os.path.join(P, R + "_bench_kernel_stats.csv"))
     if "--traces" in sys.argv:
-        for td in sorted(glob.glob(os.path.join(O, "t_*"))):
+        for td in sorted(d for d in glob.glob(os.path.join(O, "t_*")) if os.path.isdir(d)):
             tr = glob.glob(os.path.join(td, "**", "*kernel_trace.csv"), recursive=True)[0]
             rows = list(csv.DictReader(open(tr)))
             t0 = min(int(r["Start_Timestamp"]) for r in rows)
