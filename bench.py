@@ -74,6 +74,8 @@ KERNEL_NAMES = {
     "wgrad_bf16": "gemm_bf16 TN: bf16 VAE weight gradients",
     "vae_wgrad_bf16": "wgrad_tn_bf16_kernel (+ its split reduction): the seven bf16 VAE weight "
                       "gradients in one launch",
+    "heads_wgrad_x3": "wgrad_tn_x3_kernel: the five heads' hidden-layer weight gradients, grouped "
+                      "(bf16 cores, 3-piece, deterministic)",
     "wgrad_group": "wgrad_group_kernel: every fp32-chain weight gradient of a small-batch step, "
                    "one launch",
     "stn_write_bwd": "stn_bwd_kernel: STN write backward (through the output sigmoid)",

@@ -427,6 +427,17 @@ int mog_batch_mean(const float* a0, const float* a1, const float* a2, const floa
                    float* out, void* stream);
 /* out[n] += sum_r X[r*ld + n]  (BiasAddGrad) */
 int mog_colsum_add(const float* X, int R, int N, int ld, float* out, void* stream);
+/* Weight and bias gradients of the heads' 1- / 2-column output layers
+ * (air_model.py:462-499 backward): gw[z] [HS, k[z]] += hid[z]^T dout[z],
+ * gb[z] [k[z]] += column sums of dout[z] (gb may be NULL), over R rows; hid[z]
+ * [R, HS], dout[z] [R, 2] (the unused column of a 1-column head ignored).
+ * Deterministic: 128-row chunks summed in row order into `work`, the chunks
+ * added in chunk order by a second launch.  nheads <= 5, HS < 128;
+ * work_elems >= mog_heads_output_wgrad_work_elems(nheads, R, HS). */
+long mog_heads_output_wgrad_work_elems(int nheads, int R, int HS);
+int mog_heads_output_wgrad(int nheads, const float* const* hid, const float* const* dout,
+                           float* const* gw, float* const* gb, const int* k, int R, int HS,
+                           float* work, long work_elems, void* stream);
 int mog_add(const float* a, const float* b, float* out, long n, void* stream);
 
 /* ---- optimizer (air_model.py:941-999) ------------------------------------

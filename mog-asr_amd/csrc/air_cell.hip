@@ -595,6 +595,65 @@ __global__ __launch_bounds__(256) void heads_hidden_bwd4_kernel(HeadPtrs hp, con
       make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// Weight / bias gradients of the heads' output layers (air_model.py:462-499:
+// dW2_z = hid_z^T dout_z, db2_z = colsum dout_z over the R = T*B rows; HS x 1
+// or HS x 2 each), deterministic: row chunk s of head z sums its CH rows in
+// row order into work[z][s][.] (thread t < 2 HS: weight (t % HS, t / HS);
+// 2 HS, 2 HS + 1: the bias columns), then heads_out_reduce_kernel adds the
+// chunks in chunk order into the gradients.  (At the batch sizes that split K
+// the 1- / 2-column products wasted most of a 64- or 128-wide MFMA tile;
+// this reads the hidden activations once.)
+constexpr int HO_CH = 128, HO_MAXH = 5;
+struct HeadsOut {
+  const float* hid[HO_MAXH];  // [R][HS]
+  const float* dout[HO_MAXH]; // [R][2]
+  float* gw[HO_MAXH];         // [HS][k]
+  float* gb[HO_MAXH];         // [k]
+  int k[HO_MAXH];
+  int R, HS, S;
+  float* work;                // [nheads][S][2 HS + 2]
+};
+
+__global__ __launch_bounds__(256) void heads_out_partial_kernel(HeadsOut a) {
+  const int z = blockIdx.y, sc = blockIdx.x, t = threadIdx.x;
+  const int HS = a.HS, W = 2 * HS + 2;
+  if (t >= W) return;
+  const int r0 = sc * HO_CH, r1 = min(a.R, r0 + HO_CH);
+  const float* hid = a.hid[z];
+  const float* dout = a.dout[z];
+  const bool bias = t >= 2 * HS;
+  const int l = bias ? 0 : t % HS, c = bias ? t - 2 * HS : t / HS;
+  float acc = 0.0f;
+  int b = r0;
+  for (; b + 8 <= r1; b += 8) {
+    float h[8], d[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      h[i] = bias ? 1.0f : hid[(size_t)(b + i) * HS + l];
+      d[i] = dout[(size_t)(b + i) * 2 + c];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc = fmaf(h[i], d[i], acc);
+  }
+  for (; b < r1; ++b) acc = fmaf(bias ? 1.0f : hid[(size_t)b * HS + l], dout[(size_t)b * 2 + c], acc);
+  a.work[((size_t)z * a.S + sc) * W + t] = acc;
+}
+
+__global__ __launch_bounds__(256) void heads_out_reduce_kernel(HeadsOut a) {
+  const int z = blockIdx.x, t = threadIdx.x;
+  const int HS = a.HS, W = 2 * HS + 2;
+  if (t >= W) return;
+  const bool bias = t >= 2 * HS;
+  const int l = bias ? 0 : t % HS, c = bias ? t - 2 * HS : t / HS;
+  if (c >= a.k[z]) return;
+  const float* w = a.work + (size_t)z * a.S * W + t;
+  float sum = 0.0f;
+  for (int sc = 0; sc < a.S; ++sc) sum = sum + w[(size_t)sc * W];
+  float* dst = bias ? a.gb[z] + c : a.gw[z] + l * a.k[z] + c;
+  if (bias && a.gb[z] == nullptr) return;
+  *dst = *dst + sum;
+}
+
 // --------------------------------------------------------- VAE sample ---
 struct VaeCfg {
   int B, Z;
@@ -1147,6 +1206,32 @@ extern "C" int mog_batch_mean(const float* a0, const float* a1, const float* a2,
                               int B, float* out, void* stream) {
   MOG_CHECK_ARG(out && B > 0);
   batch_mean_kernel<<<1, 1024, 0, mog_stream(stream)>>>(a0, a1, a2, a3, B, 1.0f / (float)B, out);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" long mog_heads_output_wgrad_work_elems(int nheads, int R, int HS) {
+  if (nheads < 1 || nheads > HO_MAXH || R < 0 || HS < 1 || HS > 127) return -1;
+  return (long)nheads * mog_cdiv(R > 0 ? R : 1, HO_CH) * (2 * HS + 2);
+}
+
+extern "C" int mog_heads_output_wgrad(int nheads, const float* const* hid,
+                                      const float* const* dout, float* const* gw,
+                                      float* const* gb, const int* k, int R, int HS, float* work,
+                                      long work_elems, void* stream) {
+  MOG_CHECK_ARG(nheads >= 1 && nheads <= HO_MAXH && hid && dout && gw && k && work);
+  MOG_CHECK_ARG(R >= 0 && HS >= 1 && HS <= 127);
+  MOG_CHECK_ARG(work_elems >= mog_heads_output_wgrad_work_elems(nheads, R, HS));
+  if (R == 0) return 0;
+  HeadsOut a{};
+  for (int z = 0; z < nheads; ++z) {
+    MOG_CHECK_ARG(hid[z] && dout[z] && gw[z] && (k[z] == 1 || k[z] == 2));
+    a.hid[z] = hid[z]; a.dout[z] = dout[z]; a.gw[z] = gw[z]; a.gb[z] = gb ? gb[z] : nullptr;
+    a.k[z] = k[z];
+  }
+  a.R = R; a.HS = HS; a.S = (int)mog_cdiv(R, HO_CH); a.work = work;
+  hipStream_t s = mog_stream(stream);
+  heads_out_partial_kernel<<<dim3(a.S, nheads), 256, 0, s>>>(a);
+  heads_out_reduce_kernel<<<nheads, 256, 0, s>>>(a);
   MOG_LAUNCH_RET();
 }
 

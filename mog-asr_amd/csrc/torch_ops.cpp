@@ -1088,6 +1088,39 @@ void wgrad_tn_(at::TensorList X, at::TensorList dY, at::TensorList out,
   check(rc, o.name);
 }
 
+// the heads' output-layer weight / bias gradients (mog_heads_output_wgrad),
+// the chunk-partial workspace a transient of the caching allocator
+void heads_output_wgrad_(at::TensorList hid, at::TensorList dout, at::TensorList gw,
+                         const c10::List<optional<Tensor>>& gb, at::IntArrayRef k, int64_t R,
+                         int64_t HS) {
+  Op o("heads_output_wgrad_");
+  const size_t n = hid.size();
+  TORCH_CHECK(n >= 1 && n <= 5 && dout.size() == n && gw.size() == n && gb.size() == n &&
+                  k.size() == n,
+              o.name, ": 1-5 heads, one hid / dout / gw / gb / k each");
+  vector<int> kk;
+  for (size_t i = 0; i < n; ++i) {
+    TORCH_CHECK(k[i] == 1 || k[i] == 2, o.name, ": k is 1 or 2");
+    kk.push_back((int)k[i]);
+  }
+  auto gws = [&] {
+    vector<void*> v;
+    for (size_t i = 0; i < n; ++i) v.push_back(o.f(gw[i], HS * k[i], "gw"));
+    return v;
+  }();
+  auto h = o.list(hid, F32, R * HS, "hid"), d = o.list(dout, F32, R * 2, "dout");
+  vector<void*> b;
+  for (size_t i = 0; i < n; ++i) b.push_back(o.f(static_cast<optional<Tensor>>(gb[i]), k[i], "gb"));
+  GUARD(o);
+  const long we = mog_heads_output_wgrad_work_elems((int)n, (int)R, (int)HS);
+  TORCH_CHECK(we > 0, o.name, ": bad shape");
+  Tensor w = at::empty({we}, at::TensorOptions().dtype(F32).device(*o.dev));
+  check(mog_heads_output_wgrad((int)n, arr<float>(h), arr<float>(d), marr<float>(gws),
+                               marr<float>(b), kk.data(), (int)R, (int)HS, w.data_ptr<float>(),
+                               we, o.stream()),
+        o.name);
+}
+
 void wgrad_tn_bf16_(at::TensorList X, at::TensorList dY, at::TensorList out,
                     const c10::List<optional<Tensor>>& colsum, at::IntArrayRef dims, int64_t K,
                     int64_t nsplit) {
@@ -1209,6 +1242,9 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "Tensor(a!) dG0, Tensor(b!) dc_prev0, Tensor(c!)? dGsum0, Tensor G1, Tensor? c_prev1, "
       "Tensor c_cur1, Tensor dh1, Tensor? dc1, Tensor(d!) dG1, Tensor(e!) dc_prev1, "
       "Tensor(f!)? dGsum1, int B, int H) -> ()");
+  m.def(
+      "heads_output_wgrad_(Tensor[] hid, Tensor[] dout, Tensor(a!)[] gw, Tensor(b!)?[] gb, "
+      "int[] k, int R, int HS) -> ()");
   m.def(
       "air_step_forward_(int B, int HS, int HZ, int step, bool train, bool use_num_prior, "
       "float thr, float temperature, float prior_lo, float prior_bias, float s_pm, float s_pv, "
@@ -1337,6 +1373,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("gemm_f32_kseg_group_", &gemm_f32_kseg_group_);
   m.impl("lstm_cell_forward2_", &lstm_cell_forward2_);
   m.impl("lstm_cell_backward2_", &lstm_cell_backward2_);
+  m.impl("heads_output_wgrad_", &heads_output_wgrad_);
   m.impl("air_step_forward_", &air_step_forward_);
   m.impl("air_step_forward_steps_", &air_step_forward_steps_);
   m.impl("air_step_backward_", &air_step_backward_);

@@ -70,6 +70,8 @@ _SIGS = {
     "mog_recon_loss": [P, P, P, I, L, P, I, P, P, P, I, I, F, P, P, P, P, P, P, P],
     "mog_batch_mean": [P, P, P, P, I, P, P],
     "mog_colsum_add": [P, I, I, I, P, P],
+    "mog_heads_output_wgrad_work_elems": [I, I, I],
+    "mog_heads_output_wgrad": [I, P, P, P, P, P, I, I, P, L, P],
     "mog_add": [P, P, P, L, P],
     "mog_optim_chunk_elems": [],
     "mog_clip_adam": [P, P, P, P, P, P, P, P, I, P, F, F, F, F, F, P],
@@ -89,7 +91,7 @@ _SIGS = {
 }
 
 # entry points that do not return an int status
-_RESTYPE = {"mog_wgrad_tn_work_elems": L}
+_RESTYPE = {"mog_wgrad_tn_work_elems": L, "mog_heads_output_wgrad_work_elems": L}
 
 _lib = None
 

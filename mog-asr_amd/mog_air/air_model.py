@@ -198,8 +198,11 @@ class _Workspace:
         self.dz_all, self.tmp_a2_all = e(T, B, Z), e(T, B, R2)
         self.dth_f_all, self.dth_b_all, self.dot_all = e(T, B, 6), e(T, B, 6), e(T, B)
         self.dout = e(5, T, B, 2)
-        # heads side by side per row ([T, B, 5, HS]): dh is one GEMM over K = 5 HS
-        self.dhid = e(T, B, 5, HS)
+        # heads side by side per row ([T, B, 5, HS]): dh is one GEMM over K = 5 HS;
+        # 4 HS floats of slack after it, so that head z's column view spans
+        # T*B whole rows from its origin (the grouped weight-gradient kernels
+        # read K x ld elements of an operand, mog_wgrad_tn_x3)
+        self.dhid = e(T * B * 5 * HS + 4 * HS)[:T * B * 5 * HS].view(T, B, 5, HS)
         self.dh = e(T, B, H)
         self.dc = e(2, B, H)
         self.dG = e(T, B, 4 * H)

@@ -243,14 +243,33 @@ class WeightGradients:
         H, HS, TB = self.rnn_units, self.scale_hidden_units, ws.B * self.max_steps
         heads = list(enumerate(self._HEADS))
         dhid = ws.dhid.view(TB, 5, HS)
+        g = self._G
+        if (self._wgroup is None and TB >= self.WGRAD_TN_MIN_ROWS
+                and H % 2 == 0 and HS % 2 == 0 and HS < 128):
+            # deterministic from the split-K batch sizes on: the five hidden
+            # layers on the grouped x3 kernel (splits added in order), the 1- /
+            # 2-column output layers by chunk partials added in chunk order
+            # (mog_heads_output_wgrad)
+            flops = 2.0 * TB * H * HS * 5
+            with self._timed("heads_wgrad_x3", ("mfma", flops, "fp32", "x3")):
+                ops.wgrad_tn_x3([ws.h] * 5, [dhid[:, zi] for zi, _ in heads],
+                                [g(h + "/hidden/weights") for _, h in heads],
+                                [g(h + "/hidden/biases") for _, h in heads],
+                                [(H, HS, H, 5 * HS, HS)] * 5, TB, self.WGRAD_TN_X3_SPLITS)
+            _ops.heads_output_wgrad_([ws.hid[zi] for zi, _ in heads],
+                                     [ws.dout[zi] for zi, _ in heads],
+                                     [g(h + "/output/weights") for _, h in heads],
+                                     [g(h + "/output/biases") for _, h in heads],
+                                     [2 if h.startswith("shift") else 1 for _, h in heads], TB, HS)
+            return
         self._dw([ws.h] * 5, [dhid[:, zi] for zi, _ in heads],
-                 [self._G(h + "/hidden/weights") for _, h in heads], TB, H, HS, H, 5 * HS,
-                 [self._G(h + "/hidden/biases") for _, h in heads])
+                 [g(h + "/hidden/weights") for _, h in heads], TB, H, HS, H, 5 * HS,
+                 [g(h + "/hidden/biases") for _, h in heads])
         for k in (1, 2):
             sel = [(zi, h) for zi, h in heads if (2 if h.startswith("shift") else 1) == k]
             self._dw([ws.hid[zi] for zi, _ in sel], [ws.dout[zi] for zi, _ in sel],
-                     [self._G(h + "/output/weights") for _, h in sel], TB, HS, k, HS, 2,
-                     [self._G(h + "/output/biases") for _, h in sel])
+                     [g(h + "/output/weights") for _, h in sel], TB, HS, k, HS, 2,
+                     [g(h + "/output/biases") for _, h in sel])
 
     # fp32 configuration: the x-part of the LSTM kernel gradient on the bf16
     # matrix cores with exact three-piece operand splits (gemm_x3.hip,
@@ -344,7 +363,7 @@ class WeightGradients:
                     ops.gemm_x3p_tn(ws.X3.view(-1)[m0:], B * C2p, ws.dG3, B * 4 * H, gK[m0:m1],
                                     m1 - m0, 4 * H, B, C2p, 4 * H, 4 * H,
                                     splitk=self._sk(max(1, min(B // 256, self.X3_SPLITK))),
-                                    colsum=bias, reduce=False)
+                                    colsum=bias, reduce=True)
             elif self.X_GRAD_X3 == 1:
                 # fp32 operands split exactly into three bf16 pieces on the
                 # bf16 matrix cores (gemm_x3.hip: fp32-level accuracy)

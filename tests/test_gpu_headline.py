@@ -160,3 +160,18 @@ def test_configs1_bf16_gradients_vs_one_pass(data, bf16):
     one = _step("bf16", *data, "headline_bf16_1p", one_pass=True)
     np.testing.assert_array_equal(one["loss_b"], bf16["loss_b"])
     _grad_gate(bf16["grad"], one["grad"])
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_headline_step_deterministic(data, fp32, bf16, precision):
+    """Run to run at the bench's size: a second fresh model's step gives the
+    same loss and gradient bits -- every weight-gradient partial is summed in
+    a fixed order (grouped x3 / bf16 TN kernels with workspaces, the heads'
+    output layers with one writer per element, the x-rows gradient's splits
+    reduced in order; DESIGN.md §2 "Deterministic step")."""
+    first = fp32 if precision == "fp32" else bf16
+    again = _step(precision, *data, f"headline_{precision}_again")
+    assert again["loss"] == first["loss"]
+    for n, g in first["grad"].items():
+        assert np.array_equal(np.ascontiguousarray(g).view(np.int32),
+                              np.ascontiguousarray(again["grad"][n]).view(np.int32)), n

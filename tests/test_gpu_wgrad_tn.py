@@ -125,3 +125,32 @@ def test_wgrad_tn_x3_matches_float64(K, nsplit):
         bref = Yd.sum(0) + b0[i].double().cpu()
         bscale = Yd.abs().sum(0) + b0[i].double().cpu().abs()
         assert ((bs[i].double().cpu() - bref).abs() / bscale).max().item() <= 1e-5, i
+
+
+def test_heads_output_wgrad_vs_float64_and_deterministic():
+    """mog_heads_output_wgrad (the heads' 1- / 2-column output layers,
+    air_model.py:462-499 backward): gw += hid^T dout[:, :k], gb += colsum,
+    within 1e-5 of float64 (fp32 sums of 128-row chunks) and bitwise equal across launches; the
+    unused column of a 1-column head is ignored; a ragged last chunk."""
+    import mog_air.torch_ops  # noqa: F401
+    ops = torch.ops.mog_air
+    g = torch.Generator().manual_seed(5)
+    R, HS, ks = 3000, 64, [1, 1, 2, 2, 1]
+    hid = [torch.randn(R, HS, generator=g).to(DEV) for _ in ks]
+    dout = [torch.randn(R, 2, generator=g).to(DEV) for _ in ks]
+    gw0 = [(torch.randn(HS, k, generator=g) * 0.1).to(DEV) for k in ks]
+    gb0 = [(torch.randn(k, generator=g) * 0.1).to(DEV) for k in ks]
+    outs = []
+    for _ in range(2):
+        gw = [w.clone() for w in gw0]
+        gb = [b.clone() for b in gb0]
+        ops.heads_output_wgrad_(hid, dout, gw, gb, ks, R, HS)
+        torch.cuda.synchronize()
+        outs.append((gw, gb))
+    for z, k in enumerate(ks):
+        want_w = gw0[z].double() + hid[z].double().T @ dout[z][:, :k].double()
+        want_b = gb0[z].double() + dout[z][:, :k].double().sum(0)
+        got_w, got_b = outs[0][0][z], outs[0][1][z]
+        assert torch.linalg.norm(got_w.double() - want_w) <= 1e-5 * torch.linalg.norm(want_w)
+        assert torch.linalg.norm(got_b.double() - want_b) <= 1e-5 * torch.linalg.norm(want_b)
+        assert torch.equal(outs[0][0][z], outs[1][0][z]) and torch.equal(outs[0][1][z], outs[1][1][z])
