@@ -66,6 +66,12 @@ int mog_gemm_f32_x3_tn(const float* A, const float* B, float* C, float* colsum, 
  * (the bf16 configuration's weight gradient of the LSTM kernel's x rows). */
 int mog_split3_bf16(const float* src, int rows, int cols, int ld_src, void* dst, int ld_dst,
                     long piece_stride, void* stream);
+/* The pieces of a SUM of nsum <= 8 fp32 matrices src + j * sum_stride, added
+ * from the last to the first from +0 (the reversed LSTM loop's order of the
+ * gate-gradient step sum dGsum, bit for bit): the x-rows gradient's B operand
+ * straight from every step's dG, without the running sum in HBM. */
+int mog_split3_sum_bf16(const float* src, int nsum, long sum_stride, int rows, int cols,
+                        int ld_src, void* dst, int ld_dst, long piece_stride, void* stream);
 int mog_gemm_x3p_tn(const void* A3, long sa, const void* B3, long sb, float* C, float* colsum,
                     int M, int N, int K, int lda, int ldb, int ldc, int splitk, int npieces,
                     float* work, long work_elems, void* stream);

@@ -1,1 +1,1 @@
-#define MOG_BUILD_ID "8192430ebfa658c4"
+#define MOG_BUILD_ID "90b378e38f6fd0e0"

@@ -625,15 +625,17 @@ __global__ __launch_bounds__(256) void heads_out_partial_kernel(HeadsOut a) {
   const int l = bias ? 0 : t % HS, c = bias ? t - 2 * HS : t / HS;
   float acc = 0.0f;
   int b = r0;
-  for (; b + 8 <= r1; b += 8) {
-    float h[8], d[8];
+  // 32 rows' operands in flight per round trip (the loads of a chunk would
+  // otherwise be one latency each)
+  for (; b + 32 <= r1; b += 32) {
+    float h[32], d[32];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 32; ++i) {
       h[i] = bias ? 1.0f : hid[(size_t)(b + i) * HS + l];
       d[i] = dout[(size_t)(b + i) * 2 + c];
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc = fmaf(h[i], d[i], acc);
+    for (int i = 0; i < 32; ++i) acc = fmaf(h[i], d[i], acc);
   }
   for (; b < r1; ++b) acc = fmaf(bias ? 1.0f : hid[(size_t)b * HS + l], dout[(size_t)b * 2 + c], acc);
   a.work[((size_t)z * a.S + sc) * W + t] = acc;
@@ -648,7 +650,15 @@ __global__ __launch_bounds__(256) void heads_out_reduce_kernel(HeadsOut a) {
   if (c >= a.k[z]) return;
   const float* w = a.work + (size_t)z * a.S * W + t;
   float sum = 0.0f;
-  for (int sc = 0; sc < a.S; ++sc) sum = sum + w[(size_t)sc * W];
+  // in chunk order; 32 partials loaded per round trip
+  for (int s0 = 0; s0 < a.S; s0 += 32) {
+    float v[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = s0 + i < a.S ? w[(size_t)(s0 + i) * W] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i)
+      if (s0 + i < a.S) sum = sum + v[i];
+  }
   float* dst = bias ? a.gb[z] + c : a.gw[z] + l * a.k[z] + c;
   if (bias && a.gb[z] == nullptr) return;
   *dst = *dst + sum;

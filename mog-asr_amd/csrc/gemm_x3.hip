@@ -378,6 +378,40 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ s
   *reinterpret_cast<u32x2*>(d + 2 * pstride) = p2;
 }
 
+// The same pieces of a sum of nsum fp32 matrices src + j * sum_stride, added
+// from the LAST to the first starting from +0 (((0 + s[n-1]) + s[n-2]) + ...
+// + s[0]: the order in which the LSTM chain's reversed loop accumulated the
+// gate gradients' step sum, bit for bit), so the sum never goes to HBM
+__global__ __launch_bounds__(256) void split3_sum_kernel(const float* __restrict__ src, int nsum,
+                                                         long sum_stride, int rows, int cols,
+                                                         int ld_src, __bf16* dst, int ld_dst,
+                                                         long pstride) {
+#pragma clang fp contract(off)
+  const int q4 = ld_dst / 4;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)rows * q4) return;
+  const int r = (int)(i / q4), c = (int)(i % q4) * 4;
+  float4 v = float4{0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    const float* p = src + (size_t)r * ld_src + c;
+    float4 t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < nsum) t[j] = *reinterpret_cast<const float4*>(p + (size_t)j * sum_stride);
+#pragma unroll
+    for (int j = 7; j >= 0; --j)
+      if (j < nsum) {
+        v.x = v.x + t[j].x; v.y = v.y + t[j].y; v.z = v.z + t[j].z; v.w = v.w + t[j].w;
+      }
+  }
+  u32x2 p0, p1, p2;
+  split4(v, p0, p1, p2);
+  __bf16* d = dst + (size_t)r * ld_dst + c;
+  *reinterpret_cast<u32x2*>(d) = p0;
+  *reinterpret_cast<u32x2*>(d + pstride) = p1;
+  *reinterpret_cast<u32x2*>(d + 2 * pstride) = p2;
+}
+
 // C[m][n] += sum over s = 0 .. nsplit-1 of work[s][m][n], in that order (the
 // split-K partials of the TN forms: deterministic, plain loads and stores);
 // with a column sum, colsum[n] += the splits' column partials (stored after
@@ -645,6 +679,22 @@ extern "C" int mog_split3_bf16(const float* src, int rows, int cols, int ld_src,
   if (n == 0) return 0;
   split3_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, mog_stream(stream)>>>(
       src, rows, cols, ld_src, reinterpret_cast<__bf16*>(dst), ld_dst, piece_stride);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_split3_sum_bf16(const float* src, int nsum, long sum_stride, int rows,
+                                   int cols, int ld_src, void* dst, int ld_dst, long piece_stride,
+                                   void* stream) {
+  MOG_CHECK_ARG(src && dst && nsum >= 1 && nsum <= 8 && sum_stride % 4 == 0 &&
+                (nsum == 1 || sum_stride >= (long)(rows - 1) * ld_src + cols));
+  MOG_CHECK_ARG(rows >= 0 && cols >= 0 && cols % 4 == 0 && ld_src % 4 == 0 &&
+                ld_dst % 4 == 0 && ld_dst >= cols && ld_src >= cols && piece_stride % 4 == 0 &&
+                piece_stride >= (long)rows * ld_dst && al16(src) && al16(dst));
+  const long n = (long)rows * (ld_dst / 4);
+  if (n == 0) return 0;
+  split3_sum_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, mog_stream(stream)>>>(
+      src, nsum, sum_stride, rows, cols, ld_src, reinterpret_cast<__bf16*>(dst), ld_dst,
+      piece_stride);
   MOG_LAUNCH_RET();
 }
 

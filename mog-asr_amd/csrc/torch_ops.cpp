@@ -1029,6 +1029,18 @@ void split3_bf16_(const Tensor& src, Tensor dst, int64_t rows, int64_t cols, int
   check(mog_split3_bf16(a, rows, cols, ld_src, d, ld_dst, piece_stride, o.stream()), o.name);
 }
 
+void split3_sum_bf16_(const Tensor& src, int64_t nsum, int64_t sum_stride, Tensor dst,
+                      int64_t rows, int64_t cols, int64_t ld_src, int64_t ld_dst,
+                      int64_t piece_stride) {
+  Op o("split3_sum_bf16_");
+  const float* a = o.f(src, (nsum - 1) * sum_stride + mat(rows, cols, ld_src), "src");
+  void* d = o.need(dst, BF16, 2 * piece_stride + mat(rows, ld_dst, ld_dst), "dst");
+  GUARD(o);
+  check(mog_split3_sum_bf16(a, nsum, sum_stride, rows, cols, ld_src, d, ld_dst, piece_stride,
+                            o.stream()),
+        o.name);
+}
+
 void gemm_x3p_tn_(const Tensor& A3, int64_t sa, const Tensor& B3, int64_t sb, Tensor C,
                   const optional<Tensor>& colsum, int64_t M, int64_t N, int64_t K, int64_t lda,
                   int64_t ldb, int64_t ldc, int64_t splitk, int64_t npieces, int64_t reduce) {
@@ -1246,6 +1258,9 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "heads_output_wgrad_(Tensor[] hid, Tensor[] dout, Tensor(a!)[] gw, Tensor(b!)?[] gb, "
       "int[] k, int R, int HS) -> ()");
   m.def(
+      "split3_sum_bf16_(Tensor src, int nsum, int sum_stride, Tensor(a!) dst, int rows, "
+      "int cols, int ld_src, int ld_dst, int piece_stride) -> ()");
+  m.def(
       "air_step_forward_(int B, int HS, int HZ, int step, bool train, bool use_num_prior, "
       "float thr, float temperature, float prior_lo, float prior_bias, float s_pm, float s_pv, "
       "float s_plv, float h_pm, float h_pv, float h_plv, Tensor[] hid, Tensor[] w2, "
@@ -1374,6 +1389,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("lstm_cell_forward2_", &lstm_cell_forward2_);
   m.impl("lstm_cell_backward2_", &lstm_cell_backward2_);
   m.impl("heads_output_wgrad_", &heads_output_wgrad_);
+  m.impl("split3_sum_bf16_", &split3_sum_bf16_);
   m.impl("air_step_forward_", &air_step_forward_);
   m.impl("air_step_forward_steps_", &air_step_forward_steps_);
   m.impl("air_step_backward_", &air_step_backward_);

@@ -28,6 +28,7 @@ _SIGS = {
     "mog_gemm_f32_kseg": [I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "mog_gemm_f32_x3_tn": [P, P, P, P, I, I, I, I, I, I, I, P, L, P],
     "mog_split3_bf16": [P, I, I, I, P, I, L, P],
+    "mog_split3_sum_bf16": [P, I, L, I, I, I, P, I, L, P],
     "mog_gemm_x3p_tn": [P, L, P, L, P, P, I, I, I, I, I, I, I, I, P, L, P],
     "mog_gemm_f32_wgrad_group": [P, I, P],
     "mog_wgrad_tn_work_elems": [I, P, I],

@@ -759,7 +759,12 @@ class AIRModel(WeightGradients, GraphCapture, Results):
         TB = T * B
         st = self.params
         # the gradient buffer and the LSTM chain's dG sum, zeroed in one launch
-        _ops.fill32_batch_([st.grad, ws.dGsum], [0, 0])
+        # (the fp32 x3p x-rows gradient reads every step's dG instead of the
+        # sum: mog_split3_sum_bf16)
+        if self._x3p_xgrad(B):
+            _ops.fill32_batch_([st.grad], [0])
+        else:
+            _ops.fill32_batch_([st.grad, ws.dGsum], [0, 0])
         # small batch, one GPU: the fp32-chain weight gradients are collected
         # and run as one grouped launch at the end (_wgrad_group_end)
         self._wgroup = (self._wgroup_obj if (self.WGRAD_GROUP and B < self.SIDE_MIN_BATCH
@@ -893,11 +898,12 @@ class AIRModel(WeightGradients, GraphCapture, Results):
             split = self._bucket_split()
             self._reduce_bucket(split, self.params.total)
         rec_early = T > 1 and heads_side and self.REC_WGRAD_SIDE
+        dGsum = None if self._x3p_xgrad(B) else ws.dGsum
         for t in reversed(range(T)):
             dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
             _ops.lstm_cell_backward_(ws.Gx if t == 0 else ws.G[t], bK if t == 0 else None,
                                      ws.c[t - 1] if t > 0 else None, ws.c[t], ws.dh[t], dc_in,
-                                     ws.dG[t], ws.dc[t % 2], ws.dGsum, B, H)
+                                     ws.dG[t], ws.dc[t % 2], dGsum, B, H)
             if t == 1 and rec_early:
                 # dG[1:] is final: the recurrent rows' gradient runs beside the
                 # chain's last step instead of beside the x-rows gradient

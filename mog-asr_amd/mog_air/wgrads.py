@@ -356,7 +356,10 @@ class WeightGradients:
                     if getattr(ws, "dG3", None) is None:
                         ws.dG3 = torch.empty((3, B, 4 * H), device=self.device,
                                              dtype=torch.bfloat16)
-                    ops.split3_bf16(ws.dGsum, ws.dG3, B, 4 * H, 4 * H, 4 * H, B * 4 * H)
+                    # the pieces of sum_t dG_t, summed in the reversed loop's
+                    # order without the running sum (mog_split3_sum_bf16)
+                    _ops.split3_sum_bf16_(ws.dG, T, B * 4 * H, ws.dG3, B, 4 * H, 4 * H, 4 * H,
+                                          B * 4 * H)
                 C2p = self._pad8(C2)
                 with self._timed("lstm_x_projection_grad",
                                  ("mfma", 2.0 * B * (m1 - m0) * 4 * H, "fp32", "x3")):
