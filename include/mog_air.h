@@ -208,6 +208,15 @@ int mog_lstm_cell_forward(const float* G, const float* bias, const float* c_prev
 int mog_lstm_cell_backward(const float* G, const float* bias, const float* c_prev,
                            const float* c_cur, const float* dh, const float* dc, float* dG,
                            float* dc_prev, float* dGsum, int B, int H, void* stream);
+/* The same with dh = dh + parts[0] + ... + parts[nparts-1] (nparts <= 4, each
+ * [B, H], part_stride elements apart, added in part order): the hidden-state
+ * gradient GEMM dG_{t+1} Wh^T split over K into nparts products that this
+ * launch sums -- at the reference's batch of 64 the split cuts that GEMM's
+ * serial K = 4H chain per workgroup by nparts, with no reduction launch. */
+int mog_lstm_cell_backward_parts(const float* G, const float* bias, const float* c_prev,
+                                 const float* c_cur, const float* dh, const float* dh_parts,
+                                 int nparts, long part_stride, const float* dc, float* dG,
+                                 float* dc_prev, float* dGsum, int B, int H, void* stream);
 /* Two independent cells of one batch in one launch (AIR-ASR's inference and
  * generative LSTMCells, asr_model.py's loop): `cells` is a HOST array of
  * 2 x 5 device pointers {G, bias, c_prev, c_out, h_out} (forward) or

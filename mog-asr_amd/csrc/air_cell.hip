@@ -71,6 +71,11 @@ struct LstmBwd {
   float* dG;
   float* dc_prev;
   float* dGsum;
+  // dh += parts[0] + parts[1] + ... (nparts K-slices of the hidden-state
+  // gradient GEMM, part_stride elements apart), added in part order
+  const float* dh_parts = nullptr;
+  int nparts = 0;
+  long part_stride = 0;
 };
 
 __device__ __forceinline__ void lstm_bwd_body(const LstmBwd& a, int B, int H, long idx) {
@@ -87,7 +92,16 @@ __device__ __forceinline__ void lstm_bwd_body(const LstmBwd& a, int B, int H, lo
   float* sp = a.dGsum ? a.dGsum + (size_t)b * 4 * H : a.dG + (size_t)b * 4 * H;
   float gi = g[u], gj = g[H + u], gf = g[2 * H + u], go = g[3 * H + u];
   const float bi = bp[u], bj = bp[H + u], bf = bp[2 * H + u], bo = bp[3 * H + u];
-  const float cpv = cp[idx], ctv = a.c_cur[idx], dhv = a.dh[idx], dcv = dp[idx];
+  const float cpv = cp[idx], ctv = a.c_cur[idx], dcv = dp[idx];
+  float dhv = a.dh[idx];
+  if (a.nparts > 0) {
+    float pv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pv[j] = j < a.nparts ? a.dh_parts[j * a.part_stride + idx] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < a.nparts) dhv = dhv + pv[j];
+  }
   const float s0 = sp[u], s1 = sp[H + u], s2 = sp[2 * H + u], s3 = sp[3 * H + u];
   if (a.bias) {
     gi = gi + bi; gj = gj + bj; gf = gf + bf; go = go + bo;
@@ -974,6 +988,23 @@ extern "C" int mog_lstm_cell_backward(const float* G, const float* bias, const f
   if (B == 0) return 0;
   lstm_bwd_kernel<<<mog_cdiv((long)B * H, 256), 256, 0, mog_stream(stream)>>>(
       LstmBwd{G, bias, c_prev, c_cur, dh, dc, dG, dc_prev, dGsum}, B, H);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_lstm_cell_backward_parts(const float* G, const float* bias,
+                                            const float* c_prev, const float* c_cur,
+                                            const float* dh, const float* dh_parts, int nparts,
+                                            long part_stride, const float* dc, float* dG,
+                                            float* dc_prev, float* dGsum, int B, int H,
+                                            void* stream) {
+  MOG_CHECK_ARG(G && c_cur && dh && dG && B >= 0 && H > 0 && nparts >= 0 && nparts <= 4);
+  MOG_CHECK_ARG(nparts == 0 || (dh_parts && part_stride >= (long)B * H));
+  if (B == 0) return 0;
+  LstmBwd a{G, bias, c_prev, c_cur, dh, dc, dG, dc_prev, dGsum};
+  a.dh_parts = dh_parts;
+  a.nparts = nparts;
+  a.part_stride = part_stride;
+  lstm_bwd_kernel<<<mog_cdiv((long)B * H, 256), 256, 0, mog_stream(stream)>>>(a, B, H);
   MOG_LAUNCH_RET();
 }
 

@@ -339,6 +339,30 @@ void lstm_cell_backward_(const Tensor& G, const optional<Tensor>& bias,
         o.name);
 }
 
+// the cell backward summing the K-split parts of the dh GEMM into dh
+// (mog_lstm_cell_backward_parts)
+void lstm_cell_backward_parts_(const Tensor& G, const optional<Tensor>& bias,
+                               const optional<Tensor>& c_prev, const Tensor& c_cur,
+                               const Tensor& dh, const Tensor& dh_parts, int64_t nparts,
+                               const optional<Tensor>& dc, Tensor dG, Tensor dc_prev,
+                               const optional<Tensor>& dGsum, int64_t B, int64_t H) {
+  Op o("lstm_cell_backward_parts_");
+  float* pdg = o.f(dG, B * 4 * H, "dG");
+  float* pdcp = o.f(dc_prev, B * H, "dc_prev");
+  float* pg = o.f(G, B * 4 * H, "G");
+  float* pb = o.f(bias, 4 * H, "bias");
+  float* pcp = o.f(c_prev, B * H, "c_prev");
+  float* pcc = o.f(c_cur, B * H, "c_cur");
+  float* pdh = o.f(dh, B * H, "dh");
+  float* ppt = o.f(dh_parts, nparts * B * H, "dh_parts");
+  float* pdc = o.f(dc, B * H, "dc");
+  float* pgs = o.f(dGsum, B * 4 * H, "dGsum");
+  GUARD(o);
+  check(mog_lstm_cell_backward_parts(pg, pb, pcp, pcc, pdh, ppt, (int)nparts, B * H, pdc, pdg,
+                                     pdcp, pgs, B, H, o.stream()),
+        o.name);
+}
+
 // the two cells of one batch in one launch (no bias: both cells' gate GEMMs
 // add theirs)
 void lstm_cell_forward2_(const Tensor& G0, const optional<Tensor>& c_prev0, Tensor c_out0,
@@ -1261,6 +1285,10 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "split3_sum_bf16_(Tensor src, int nsum, int sum_stride, Tensor(a!) dst, int rows, "
       "int cols, int ld_src, int ld_dst, int piece_stride) -> ()");
   m.def(
+      "lstm_cell_backward_parts_(Tensor G, Tensor? bias, Tensor? c_prev, Tensor c_cur, "
+      "Tensor dh, Tensor dh_parts, int nparts, Tensor? dc, Tensor(a!) dG, Tensor(b!) dc_prev, "
+      "Tensor(c!)? dGsum, int B, int H) -> ()");
+  m.def(
       "air_step_forward_(int B, int HS, int HZ, int step, bool train, bool use_num_prior, "
       "float thr, float temperature, float prior_lo, float prior_bias, float s_pm, float s_pv, "
       "float s_plv, float h_pm, float h_pv, float h_plv, Tensor[] hid, Tensor[] w2, "
@@ -1390,6 +1418,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("lstm_cell_backward2_", &lstm_cell_backward2_);
   m.impl("heads_output_wgrad_", &heads_output_wgrad_);
   m.impl("split3_sum_bf16_", &split3_sum_bf16_);
+  m.impl("lstm_cell_backward_parts_", &lstm_cell_backward_parts_);
   m.impl("air_step_forward_", &air_step_forward_);
   m.impl("air_step_forward_steps_", &air_step_forward_steps_);
   m.impl("air_step_backward_", &air_step_backward_);

@@ -44,6 +44,7 @@ _SIGS = {
     "mog_stn_backward_sigmoid_f32": [P, I, I, I, P, I, I, P, P, P, P, P, I, I, P],
     "mog_lstm_cell_forward": [P, P, P, P, P, I, I, P],
     "mog_lstm_cell_backward": [P, P, P, P, P, P, P, P, P, I, I, P],
+    "mog_lstm_cell_backward_parts": [P, P, P, P, P, P, I, L, P, P, P, P, I, I, P],
     "mog_gemm_f32_kseg_group": [I, P, P, P, P, P, I, I, I, I, I, I, I, P],
     "mog_lstm_cell_forward_pair": [P, I, I, P],
     "mog_lstm_cell_backward_pair": [P, I, I, P],

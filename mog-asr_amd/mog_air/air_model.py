@@ -899,16 +899,33 @@ class AIRModel(WeightGradients, GraphCapture, Results):
             self._reduce_bucket(split, self.params.total)
         rec_early = T > 1 and heads_side and self.REC_WGRAD_SIDE
         dGsum = None if self._x3p_xgrad(B) else ws.dGsum
+        # a small batch's dh GEMM (K = 4H walked serially by a dozen workgroups)
+        # split over K into DH_PARTS products that the next cell backward adds
+        # to the heads' dh in part order (mog_lstm_cell_backward_parts)
+        parts = self.DH_PARTS if B < self.SIDE_MIN_BATCH and (4 * H) % (4 * self.DH_PARTS) == 0 \
+            else 0
+        if parts and getattr(ws, "dh_parts", None) is None:
+            ws.dh_parts = torch.empty((parts, B, H), device=self.device)
         for t in reversed(range(T)):
             dc_in = ws.dc[(t + 1) % 2] if t < T - 1 else None
-            _ops.lstm_cell_backward_(ws.Gx if t == 0 else ws.G[t], bK if t == 0 else None,
-                                     ws.c[t - 1] if t > 0 else None, ws.c[t], ws.dh[t], dc_in,
-                                     ws.dG[t], ws.dc[t % 2], dGsum, B, H)
+            G_t, b_t = (ws.Gx, bK) if t == 0 else (ws.G[t], None)
+            c_prev = ws.c[t - 1] if t > 0 else None
+            if parts and t < T - 1:
+                _ops.lstm_cell_backward_parts_(G_t, b_t, c_prev, ws.c[t], ws.dh[t], ws.dh_parts,
+                                               parts, dc_in, ws.dG[t], ws.dc[t % 2], dGsum, B, H)
+            else:
+                _ops.lstm_cell_backward_(G_t, b_t, c_prev, ws.c[t], ws.dh[t], dc_in, ws.dG[t],
+                                         ws.dc[t % 2], dGsum, B, H)
             if t == 1 and rec_early:
                 # dG[1:] is final: the recurrent rows' gradient runs beside the
                 # chain's last step instead of beside the x-rows gradient
                 self._weight_grads_rec_side(ws)
-            if t > 0:
+            if t > 0 and parts:
+                kp = 4 * H // parts
+                gemm([ws.dG[t][:, j * kp:] for j in range(parts)],
+                     [Wh[:, j * kp:] for j in range(parts)], [ws.dh_parts[j] for j in range(parts)],
+                     B, H, kp, 4 * H, 4 * H, H, transB=True)
+            elif t > 0:
                 gemm([ws.dG[t]], [Wh], [ws.dh[t - 1]], B, H, 4 * H, 4 * H, 4 * H, H,
                      transB=True, Cin=[ws.dh[t - 1]])
         self._weight_grads_lstm(X, ws, side=heads_side, rec_done=rec_early)
@@ -920,6 +937,9 @@ class AIRModel(WeightGradients, GraphCapture, Results):
     HEADS_WGRAD_SIDE = True
     # ... and the LSTM kernel's recurrent-rows gradient beside the x-rows one
     REC_WGRAD_SIDE = True
+    # K-split of the small-batch dh GEMM (0: one chain per output, Cin = the
+    # heads' dh)
+    DH_PARTS = 4
     # the round-3 side-stream moves (noise + resets under the x-projection,
     # heads' weight gradients under the LSTM chain) from this batch: below it
     # the launches are too short to hide the cross-stream waits (batch 64:

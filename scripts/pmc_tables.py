@@ -23,19 +23,18 @@ SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 # | "5not4" / "5is4": all but / only every fifth, from the fifth)
 TAGS = {
     "stn_vae_step_f32_all_fp32_b8192": ("step_fp32_8192", lambda k: "stn_vae_step_f32_kernel" in k, "all"),
-    # wgrad_tn_x3_kernel runs the seven VAE weight gradients (grouped), then,
-    # later in the step, the LSTM recurrent rows: two per step in that order
-    # (each followed by its wgrad_tn_reduce_kernel, not counted here)
-    "vae_wgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: k.startswith("wgrad_tn_x3_kernel"), "even"),
-    "rec_wgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: k.startswith("wgrad_tn_x3_kernel"), "odd"),
+    # wgrad_tn_x3_kernel runs the seven VAE weight gradients (grouped), the
+    # five heads' hidden layers, then the LSTM recurrent rows: three per step
+    # in that order (each followed by its wgrad_tn_reduce_kernel, not counted)
+    "vae_wgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: k.startswith("wgrad_tn_x3_kernel"), "mod3_0"),
+    "heads_wgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: k.startswith("wgrad_tn_x3_kernel"), "mod3_1"),
+    "rec_wgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: k.startswith("wgrad_tn_x3_kernel"), "mod3_2"),
     "vae_dgrad_x3_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_x3_nt_kernel" in k, "all"),
     "lstm_x_projection_grad_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_x3_tn_kernel<true, 3>" in k, "all"),
     "lstm_x_projection_fp32_b8192": ("step_fp32_8192", lambda k: "gemm_f32_dma_kernel<128, 128, 16, 3, false, false, 0>" in k, "all"),
     # the step runs the STN write backward, then the read backward
     "stn_write_bwd_fp32_b8192": ("step_fp32_8192", lambda k: k.startswith("stn_bwd_kernel"), "even"),
     "stn_read_bwd_fp32_b8192": ("step_fp32_8192", lambda k: k.startswith("stn_bwd_kernel"), "odd"),
-    "wgrad_f32_fp32_b8192": ("step_fp32_8192", lambda k: ("gemm_f32_dma_kernel" in k or "gemm_f32_kernel" in k)
-                             and "true, false, 5" in k, "all"),
     "stn_vae_step_all_bf16_b8192": ("step_bf16_8192", lambda k: k.startswith("void stn_vae_step_kernel"), "all"),
     "vae_wgrad_bf16_bf16_b8192": ("step_bf16_8192", lambda k: "wgrad_tn_bf16_kernel" in k, "all"),
     "lstm_x_projection_grad_bf16_b8192": ("step_bf16_8192", lambda k: "gemm_x3_tn_kernel<true, 1>" in k, "all"),
@@ -89,6 +88,8 @@ def pick(v, which):
         return v[-5:]
     if which == "5not4":
         return [x for i, x in enumerate(v) if i % 5 != 4]
+    if which.startswith("mod3_"):
+        return v[int(which[-1])::3]
     if which == "5is4":
         return v[4::5]
     return v
