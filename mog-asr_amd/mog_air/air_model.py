@@ -902,8 +902,8 @@ class AIRModel(WeightGradients, GraphCapture, Results):
         # a small batch's dh GEMM (K = 4H walked serially by a dozen workgroups)
         # split over K into DH_PARTS products that the next cell backward adds
         # to the heads' dh in part order (mog_lstm_cell_backward_parts)
-        parts = self.DH_PARTS if B < self.SIDE_MIN_BATCH and (4 * H) % (4 * self.DH_PARTS) == 0 \
-            else 0
+        parts = self.DH_PARTS if (B < self.SIDE_MIN_BATCH and self.DH_PARTS > 1
+                                  and (4 * H) % (4 * self.DH_PARTS) == 0) else 0
         if parts and getattr(ws, "dh_parts", None) is None:
             ws.dh_parts = torch.empty((parts, B, H), device=self.device)
         for t in reversed(range(T)):
