@@ -503,6 +503,12 @@ int mog_asr_pack(int B, int Z, int H, int ld, const float* z, const float* ss, c
  * dhg += dUg[:, Z+3:] */
 int mog_asr_unpack(int B, int Z, int H, int ld, const float* dU, const float* dUg, float* dz,
                    float* dss, float* dh, float* dhg, int acc_dz, void* stream);
+/* The same with dU / dUg given as nparts <= 4 K parts of their GEMM (part j at
+ * + j * part_stride elements), summed in part order (the small-batch recurrent
+ * input gradient split over K = 4H, as mog_lstm_cell_backward_parts). */
+int mog_asr_unpack_parts(int B, int Z, int H, int ld, const float* dU, const float* dUg,
+                         int nparts, long part_stride, float* dz, float* dss, float* dh,
+                         float* dhg, int acc_dz, void* stream);
 /* heads, latents, theta, concrete z_pres, KLs, entropy, stop / counts /
  * live flag of one step (:414-772) */
 int mog_asr_step_forward(int B, int step, int train, int fix_steps, float thr, float temperature,

@@ -1,1 +1,1 @@
-#define MOG_BUILD_ID "133e133ff922464d"
+#define MOG_BUILD_ID "ca2c22374b1b1d55"

@@ -112,13 +112,28 @@ __global__ __launch_bounds__(256) void asr_pack_kernel(int B, int Z, int H, int 
 __global__ __launch_bounds__(256) void asr_unpack_kernel(int B, int Z, int H, int ld,
                                                          const float* dU, const float* dUg,
                                                          float* dz, float* dss, float* dh,
-                                                         float* dhg, int acc_dz) {
+                                                         float* dhg, int acc_dz, int nparts,
+                                                         long part_stride) {
 #pragma clang fp contract(off)
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)B * (Z + 3 + H)) return;
   const int n = Z + 3 + H;
   const int b = i / n, k = i - (long)b * n;
-  const float a = dU[(size_t)b * ld + k], g = dUg[(size_t)b * ld + k];
+  float a = dU[(size_t)b * ld + k], g = dUg[(size_t)b * ld + k];
+  if (nparts > 1) {  // dU / dUg as K parts of their GEMM: summed in part order
+    float pa[4], pg[4];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      pa[j] = j < nparts ? dU[j * part_stride + (size_t)b * ld + k] : 0.0f;
+      pg[j] = j < nparts ? dUg[j * part_stride + (size_t)b * ld + k] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+      if (j < nparts) {
+        a = a + pa[j];
+        g = g + pg[j];
+      }
+  }
   if (k < Z) {
     const size_t o = (size_t)b * Z + k;
     dz[o] = acc_dz ? dz[o] + (a + g) : a + g;  // (the same sum as add_(dz, carry))
@@ -709,7 +724,19 @@ extern "C" int mog_asr_unpack(int B, int Z, int H, int ld, const float* dU, cons
                 dhg);
   if (B == 0) return 0;
   asr_unpack_kernel<<<mog_cdiv((long)B * (Z + 3 + H), 256), 256, 0, mog_stream(stream)>>>(
-      B, Z, H, ld, dU, dUg, dz, dss, dh, dhg, acc_dz);
+      B, Z, H, ld, dU, dUg, dz, dss, dh, dhg, acc_dz, 1, 0);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_asr_unpack_parts(int B, int Z, int H, int ld, const float* dU,
+                                    const float* dUg, int nparts, long part_stride, float* dz,
+                                    float* dss, float* dh, float* dhg, int acc_dz,
+                                    void* stream) {
+  MOG_CHECK_ARG(B >= 0 && Z > 0 && H > 0 && ld >= Z + 3 + H && dU && dUg && dz && dss && dh &&
+                dhg && nparts >= 1 && nparts <= 4 && (nparts == 1 || part_stride >= (long)B * ld));
+  if (B == 0) return 0;
+  asr_unpack_kernel<<<mog_cdiv((long)B * (Z + 3 + H), 256), 256, 0, mog_stream(stream)>>>(
+      B, Z, H, ld, dU, dUg, dz, dss, dh, dhg, acc_dz, nparts, part_stride);
   MOG_LAUNCH_RET();
 }
 

@@ -888,6 +888,22 @@ void asr_unpack_(int64_t B, int64_t Z, int64_t H, int64_t ld, const Tensor& dU, 
         o.name);
 }
 
+void asr_unpack_parts_(int64_t B, int64_t Z, int64_t H, int64_t ld, const Tensor& dU,
+                       const Tensor& dUg, int64_t nparts, Tensor dz, Tensor dss, Tensor dh,
+                       Tensor dhg, int64_t acc_dz) {
+  Op o("asr_unpack_parts_");
+  float* pdz = o.f(dz, B * Z, "dz");
+  float* pds = o.f(dss, B * 3, "dss");
+  float* pdh = o.f(dh, B * H, "dh");
+  float* pdg = o.f(dhg, B * H, "dhg");
+  float* pu = o.f(dU, nparts * B * ld, "dU");
+  float* pug = o.f(dUg, nparts * B * ld, "dUg");
+  GUARD(o);
+  check(mog_asr_unpack_parts(B, Z, H, ld, pu, pug, (int)nparts, B * ld, pdz, pds, pdh, pdg,
+                             (int)acc_dz, o.stream()),
+        o.name);
+}
+
 void asr_step_forward_(int64_t B, int64_t step, bool train, int64_t fix_steps, double thr,
                        double temperature, double s_pm, double s_pv, double s_plv,
                        double gamma_num, at::TensorList w, const c10::List<optional<Tensor>>& hid,
@@ -1289,6 +1305,9 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "Tensor dh, Tensor dh_parts, int nparts, Tensor? dc, Tensor(a!) dG, Tensor(b!) dc_prev, "
       "Tensor(c!)? dGsum, int B, int H) -> ()");
   m.def(
+      "asr_unpack_parts_(int B, int Z, int H, int ld, Tensor dU, Tensor dUg, int nparts, "
+      "Tensor(a!) dz, Tensor(b!) dss, Tensor(c!) dh, Tensor(d!) dhg, int acc_dz) -> ()");
+  m.def(
       "air_step_forward_(int B, int HS, int HZ, int step, bool train, bool use_num_prior, "
       "float thr, float temperature, float prior_lo, float prior_bias, float s_pm, float s_pv, "
       "float s_plv, float h_pm, float h_pv, float h_plv, Tensor[] hid, Tensor[] w2, "
@@ -1419,6 +1438,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("heads_output_wgrad_", &heads_output_wgrad_);
   m.impl("split3_sum_bf16_", &split3_sum_bf16_);
   m.impl("lstm_cell_backward_parts_", &lstm_cell_backward_parts_);
+  m.impl("asr_unpack_parts_", &asr_unpack_parts_);
   m.impl("air_step_forward_", &air_step_forward_);
   m.impl("air_step_forward_steps_", &air_step_forward_steps_);
   m.impl("air_step_backward_", &air_step_backward_);

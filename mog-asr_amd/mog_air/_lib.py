@@ -84,6 +84,7 @@ _SIGS = {
     "mog_generation_prior": [I, I, F, F, F, F, F, F, P, P, P, P, P, P, P, P],
     "mog_asr_pack": [I, I, I, I, P, P, P, P, P, P, P],
     "mog_asr_unpack": [I, I, I, I, P, P, P, P, P, P, I, P],
+    "mog_asr_unpack_parts": [I, I, I, I, P, P, I, L, P, P, P, P, I, P],
     "mog_asr_step_forward": [I, I, I, I, F, F, F, F, F, F, P, P, P, P, P, P, P, P, P, P, P, P,
                              P, P, P, P, P, P, P],
     "mog_asr_terms": [I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],

@@ -524,6 +524,13 @@ class AIRModel(_AirBase):
         # and the decoder half of every step's VAE backward (dz_t before the
         # loop's carry), likewise over T*B rows
         self._vae_decoder_backward_all(ws)
+        # a small batch's recurrent-input gradient in DH_PARTS K slices
+        # (AIRModel.DH_PARTS: the serial K = 4H chain per workgroup cut)
+        parts = self.DH_PARTS if (B < self.SIDE_MIN_BATCH and self.DH_PARTS > 1
+                                  and (4 * H) % (4 * self.DH_PARTS) == 0) else 0
+        if parts and getattr(ws, "dUp", None) is None:
+            ws.dUp = torch.empty((parts,) + tuple(ws.dU.shape), device=self.device)
+            ws.dUgp = torch.empty((parts,) + tuple(ws.dUg.shape), device=self.device)
         for t in reversed(range(T)):
             if self.precision == "bf16":
                 self._vae_backward_bf16(ws, t, gscale)
@@ -569,7 +576,19 @@ class AIRModel(_AirBase):
                 # step t's recurrent-rows gradients likewise (dG_t, dGg_t final)
                 with torch.cuda.stream(self._fork(side)):
                     self._u_rows_wgrad(ws, t)
-            if t > 0:
+            if t > 0 and parts:
+                # a small batch: the same product in `parts` K slices (one batched
+                # launch of 2 x parts), summed in part order by the unpack
+                kp = 4 * H // parts
+                gemm([ws.dG[t][:, j * kp:] for j in range(parts)]
+                     + [ws.dGg[t][:, j * kp:] for j in range(parts)],
+                     [Ki[C2:][:, j * kp:] for j in range(parts)]
+                     + [Kg[:, j * kp:] for j in range(parts)],
+                     [ws.dUp[j] for j in range(parts)] + [ws.dUgp[j] for j in range(parts)],
+                     B, LU, kp, 4 * H, 4 * H, LU, transB=True)
+                _ops.asr_unpack_parts_(B, Z, H, LU, ws.dUp, ws.dUgp, parts, ws.dz_all[t - 1],
+                                       ws.dss_carry, ws.dh[t - 1], ws.dhg[t - 1], 1)
+            elif t > 0:
                 # N = LU: the 3 pad columns of dU / dUg are scratch (unpack skips them)
                 # (both LSTMCells in one batched launch: same shapes and chains)
                 gemm([ws.dG[t], ws.dGg[t]], [Ki[C2:], Kg], [ws.dU, ws.dUg], B, LU, 4 * H,

@@ -1,6 +1,6 @@
 """A/B of a model class switch on the captured batch-64 AIR step (the bench's
 config_1_batch64_fp32 workload): alternating rounds, ms per step.
-usage: python scripts/b64_ab.py ATTR[=v1,v2] [rounds] [steps] [B]  (default values True,False)"""
+usage: python scripts/b64_ab.py ATTR[=v1,v2] [rounds] [steps] [B] [asr]  (default values True,False)"""
 import os
 import sys
 
@@ -16,10 +16,12 @@ VALS = [int(v) for v in vs.split(",")] if vs else [True, False]
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 200
 B = int(sys.argv[4]) if len(sys.argv) > 4 else 64
+ASR = sys.argv[5:6] == ["asr"]  # configs[2]'s AIR-ASR step instead of AIR's
 dev = torch.device("cuda:0")
 models = {}
 for v in VALS:
-    m = bench.make_model("fp32", dev, 1, 0, f"ab{int(v)}")
+    m = (bench.make_asr_model("fp32", dev, f"ab{int(v)}") if ASR
+         else bench.make_model("fp32", dev, 1, 0, f"ab{int(v)}"))
     setattr(m, attr, v)
     models[v] = m
 res = {v: [] for v in VALS}
