@@ -561,6 +561,10 @@ int mog_rng_fill_batch(int nbuf, float* const* out, const long* n, unsigned long
  * values, air_model.py:815-826) and the zeroed gradient accumulators. */
 int mog_fill32_batch(int nbuf, void* const* dst, const long* n, const unsigned* value,
                      void* stream);
+/* Up to 8 copies of n[j] 32-bit words src[j] -> dst[j] in one launch (a
+ * captured step's inputs into the graph's static buffers). */
+int mog_copy32_batch(int nbuf, void* const* dst, const void* const* src, const long* n,
+                     void* stream);
 
 /* ---- measurement instrument (no reference counterpart) -------------------
  * dst[i] = src[i] for n4 float4s (16-byte aligned): the copy bandwidth the

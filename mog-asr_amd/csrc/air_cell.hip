@@ -936,6 +936,28 @@ __global__ __launch_bounds__(256) void fill32_batch_kernel(FillBatch f) {
   }
 }
 
+// Up to FILL_MAX copies of 32-bit words in one launch (grid row j: copy j):
+// a captured step's inputs into the graph's static buffers
+struct CopyBatch {
+  unsigned* dst[FILL_MAX];
+  const unsigned* src[FILL_MAX];
+  long n[FILL_MAX];
+};
+__global__ __launch_bounds__(256) void copy32_batch_kernel(CopyBatch f) {
+  const int j = blockIdx.y;
+  const long n = f.n[j], stride = (long)gridDim.x * 256 * 4;
+  unsigned* d = f.dst[j];
+  const unsigned* a = f.src[j];
+  const bool vec = ((reinterpret_cast<size_t>(d) | reinterpret_cast<size_t>(a)) & 15) == 0;
+  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+    if (vec && i + 4 <= n) {
+      *reinterpret_cast<uint4*>(d + i) = *reinterpret_cast<const uint4*>(a + i);
+    } else {
+      for (long k = i; k < n && k < i + 4; ++k) d[k] = a[k];
+    }
+  }
+}
+
 // out[i] = a[i] + b[i]
 __global__ __launch_bounds__(256) void add_kernel(const float* a, const float* b, float* out,
                                                   long n) {
@@ -1303,6 +1325,28 @@ extern "C" int mog_fill32_batch(int nbuf, void* const* dst, const long* n, const
   if (nbuf == 0 || mx == 0) return 0;
   const long blocks = std::min<long>((long)mog_cdiv((mx + 3) / 4, 256), 2048);
   fill32_batch_kernel<<<dim3((unsigned)blocks, nbuf), 256, 0, mog_stream(stream)>>>(f);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_copy32_batch(int nbuf, void* const* dst, const void* const* src,
+                                const long* n, void* stream) {
+  MOG_CHECK_ARG(nbuf >= 0 && nbuf <= FILL_MAX && (nbuf == 0 || (dst && src && n)));
+  CopyBatch f;
+  long mx = 0;
+  for (int j = 0; j < FILL_MAX; ++j) {
+    const bool on = j < nbuf;
+    f.dst[j] = on ? reinterpret_cast<unsigned*>(dst[j]) : nullptr;
+    f.src[j] = on ? reinterpret_cast<const unsigned*>(src[j]) : nullptr;
+    f.n[j] = on ? n[j] : 0;
+    if (on) {
+      MOG_CHECK_ARG(dst[j] && src[j] && n[j] >= 0 &&
+                    ((reinterpret_cast<size_t>(dst[j]) | reinterpret_cast<size_t>(src[j])) & 3) == 0);
+      mx = n[j] > mx ? n[j] : mx;
+    }
+  }
+  if (nbuf == 0 || mx == 0) return 0;
+  const long blocks = std::min<long>((long)mog_cdiv((mx + 3) / 4, 256), 2048);
+  copy32_batch_kernel<<<dim3((unsigned)blocks, nbuf), 256, 0, mog_stream(stream)>>>(f);
   MOG_LAUNCH_RET();
 }
 

@@ -831,6 +831,27 @@ void rng_fill_batch_(at::TensorList out, int64_t seed, at::IntArrayRef offset,
         o.name);
 }
 
+// up to 8 same-size 32-bit copies in one launch (mog_copy32_batch)
+void copy32_batch_(at::TensorList dst, at::TensorList src) {
+  Op o("copy32_batch_");
+  TORCH_CHECK(dst.size() == src.size() && dst.size() <= 8, o.name, ": up to 8 dst / src pairs");
+  vector<void*> d, a;
+  vector<long> n;
+  for (size_t j = 0; j < dst.size(); ++j) {
+    TORCH_CHECK(dst[j].element_size() == 4 && src[j].element_size() == 4 &&
+                    dst[j].numel() == src[j].numel() && dst[j].is_contiguous() &&
+                    src[j].is_contiguous(),
+                o.name, ": contiguous 32-bit tensors of one size per pair");
+    d.push_back(o.need(dst[j], dst[j].scalar_type(), dst[j].numel(), "dst"));
+    a.push_back(o.need(src[j], src[j].scalar_type(), src[j].numel(), "src"));
+    n.push_back((long)dst[j].numel());
+  }
+  GUARD(o);
+  check(mog_copy32_batch((int)d.size(), d.data(), const_cast<const void* const*>(a.data()),
+                         n.data(), o.stream()),
+        o.name);
+}
+
 void fill32_batch_(at::TensorList dst, at::IntArrayRef value) {
   Op o("fill32_batch_");
   TORCH_CHECK(dst.size() == value.size(), o.name, ": lengths");
@@ -1307,6 +1328,7 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
   m.def(
       "asr_unpack_parts_(int B, int Z, int H, int ld, Tensor dU, Tensor dUg, int nparts, "
       "Tensor(a!) dz, Tensor(b!) dss, Tensor(c!) dh, Tensor(d!) dhg, int acc_dz) -> ()");
+  m.def("copy32_batch_(Tensor(a!)[] dst, Tensor[] src) -> ()");
   m.def(
       "air_step_forward_(int B, int HS, int HZ, int step, bool train, bool use_num_prior, "
       "float thr, float temperature, float prior_lo, float prior_bias, float s_pm, float s_pv, "
@@ -1439,6 +1461,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("split3_sum_bf16_", &split3_sum_bf16_);
   m.impl("lstm_cell_backward_parts_", &lstm_cell_backward_parts_);
   m.impl("asr_unpack_parts_", &asr_unpack_parts_);
+  m.impl("copy32_batch_", &copy32_batch_);
   m.impl("air_step_forward_", &air_step_forward_);
   m.impl("air_step_forward_steps_", &air_step_forward_steps_);
   m.impl("air_step_backward_", &air_step_backward_);

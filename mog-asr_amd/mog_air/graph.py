@@ -8,6 +8,8 @@ from typing import Optional
 
 import torch
 
+from . import ops
+
 
 class GraphCapture:
     # A captured train step (hipGraph through torch.cuda.CUDAGraph): the whole
@@ -69,10 +71,16 @@ class GraphCapture:
             self._graph_key = key
             return
         gX, gT = self._graph_io
+        # the inputs into the graph's static buffers, both in one launch
+        dst, src = [], []
         if X.data_ptr() != gX.data_ptr():
-            gX.copy_(X)
+            dst.append(gX)
+            src.append(X)
         if tg is not None and tg.data_ptr() != gT.data_ptr():
-            gT.copy_(tg)
+            dst.append(gT)
+            src.append(tg)
+        if dst:
+            ops._ops.copy32_batch_(dst, src)
         # The graph holds raw pointers into the workspace it was captured on:
         # replay on that one (kept alive by _graph_ws), even when an infer /
         # step / compute_gradients at another batch has replaced self._ws since

@@ -255,7 +255,7 @@ class WeightGradients:
                 ops.wgrad_tn_x3([ws.h] * 5, [dhid[:, zi] for zi, _ in heads],
                                 [g(h + "/hidden/weights") for _, h in heads],
                                 [g(h + "/hidden/biases") for _, h in heads],
-                                [(H, HS, H, 5 * HS, HS)] * 5, TB, self.HEADS_SPLITS)
+                                [(H, HS, H, 5 * HS, HS)] * 5, TB, self.WGRAD_TN_X3_SPLITS)
             _ops.heads_output_wgrad_([ws.hid[zi] for zi, _ in heads],
                                      [ws.dout[zi] for zi, _ in heads],
                                      [g(h + "/output/weights") for _, h in heads],
@@ -320,7 +320,6 @@ class WeightGradients:
             self._dw(ws.h, ws.dG[1:], gK[C2:], K, H, 4 * H, H, 4 * H)
 
     REC_WGRAD_X3 = True
-    HEADS_SPLITS = 16
 
     def _weight_grads_lstm(self, X, ws, side=False, rec_done=False):
         """LSTM kernel / bias gradients.  Data parallel: the x-part X^T dGsum
