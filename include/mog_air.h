@@ -565,6 +565,11 @@ int mog_fill32_batch(int nbuf, void* const* dst, const long* n, const unsigned* 
  * captured step's inputs into the graph's static buffers). */
 int mog_copy32_batch(int nbuf, void* const* dst, const void* const* src, const long* n,
                      void* stream);
+/* Up to 8 fp32 transposes in one launch: dst[j] [cols][rows] = src[j] [rows][cols]
+ * (the small-batch forward's W^T copies of the VAE layers whose N or K is the
+ * 50-wide latent: NT GEMM forms with the same k-ordered chains). */
+int mog_transpose32_batch(int nbuf, float* const* dst, const float* const* src, const int* rows,
+                          const int* cols, void* stream);
 
 /* ---- measurement instrument (no reference counterpart) -------------------
  * dst[i] = src[i] for n4 float4s (16-byte aligned): the copy bandwidth the

@@ -1,1 +1,1 @@
-#define MOG_BUILD_ID "30dcc98b066801c4"
+#define MOG_BUILD_ID "8c6f1e38a6b5d2e4"

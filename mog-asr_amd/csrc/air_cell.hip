@@ -958,6 +958,25 @@ __global__ __launch_bounds__(256) void copy32_batch_kernel(CopyBatch f) {
   }
 }
 
+// Up to FILL_MAX matrix transposes in one launch (grid row j: matrix j,
+// dst[c][r] = src[r][c], rows x cols): the small-batch forward's transposed
+// copies of the VAE layers whose N or K (the latent 50) misses the LDS-DMA
+// alignment, refreshed inside the captured step
+struct TransBatch {
+  float* dst[FILL_MAX];
+  const float* src[FILL_MAX];
+  int rows[FILL_MAX], cols[FILL_MAX];
+};
+__global__ __launch_bounds__(256) void transpose32_batch_kernel(TransBatch f) {
+  const int j = blockIdx.y;
+  const long n = (long)f.rows[j] * f.cols[j], stride = (long)gridDim.x * 256;
+  const int cols = f.cols[j], rows = f.rows[j];
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const int c = (int)(i / rows), r = (int)(i - (long)c * rows);  // dst order: coalesced stores
+    f.dst[j][i] = f.src[j][(size_t)r * cols + c];
+  }
+}
+
 // out[i] = a[i] + b[i]
 __global__ __launch_bounds__(256) void add_kernel(const float* a, const float* b, float* out,
                                                   long n) {
@@ -1347,6 +1366,22 @@ extern "C" int mog_copy32_batch(int nbuf, void* const* dst, const void* const* s
   if (nbuf == 0 || mx == 0) return 0;
   const long blocks = std::min<long>((long)mog_cdiv((mx + 3) / 4, 256), 2048);
   copy32_batch_kernel<<<dim3((unsigned)blocks, nbuf), 256, 0, mog_stream(stream)>>>(f);
+  MOG_LAUNCH_RET();
+}
+
+extern "C" int mog_transpose32_batch(int nbuf, float* const* dst, const float* const* src,
+                                     const int* rows, const int* cols, void* stream) {
+  MOG_CHECK_ARG(nbuf >= 0 && nbuf <= FILL_MAX && (nbuf == 0 || (dst && src && rows && cols)));
+  TransBatch f{};
+  long mx = 0;
+  for (int j = 0; j < nbuf; ++j) {
+    MOG_CHECK_ARG(dst[j] && src[j] && rows[j] >= 0 && cols[j] >= 0);
+    f.dst[j] = dst[j]; f.src[j] = src[j]; f.rows[j] = rows[j]; f.cols[j] = cols[j];
+    mx = std::max<long>(mx, (long)rows[j] * cols[j]);
+  }
+  if (nbuf == 0 || mx == 0) return 0;
+  const long blocks = std::min<long>((long)mog_cdiv(mx, 256), 1024);
+  transpose32_batch_kernel<<<dim3((unsigned)blocks, nbuf), 256, 0, mog_stream(stream)>>>(f);
   MOG_LAUNCH_RET();
 }
 

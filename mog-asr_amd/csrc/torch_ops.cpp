@@ -852,6 +852,28 @@ void copy32_batch_(at::TensorList dst, at::TensorList src) {
         o.name);
 }
 
+// fp32 transposes in one launch (mog_transpose32_batch)
+void transpose32_batch_(at::TensorList dst, at::TensorList src) {
+  Op o("transpose32_batch_");
+  TORCH_CHECK(dst.size() == src.size() && dst.size() <= 8, o.name, ": up to 8 pairs");
+  vector<void*> d, a;
+  vector<int> r, c;
+  for (size_t j = 0; j < dst.size(); ++j) {
+    TORCH_CHECK(src[j].dim() == 2 && dst[j].dim() == 2 && src[j].is_contiguous() &&
+                    dst[j].is_contiguous() && dst[j].size(0) == src[j].size(1) &&
+                    dst[j].size(1) == src[j].size(0),
+                o.name, ": contiguous 2-d src [r][c] and dst [c][r]");
+    d.push_back(o.f(dst[j], dst[j].numel(), "dst"));
+    a.push_back(o.f(src[j], src[j].numel(), "src"));
+    r.push_back((int)src[j].size(0));
+    c.push_back((int)src[j].size(1));
+  }
+  GUARD(o);
+  check(mog_transpose32_batch((int)d.size(), marr<float>(d), arr<float>(a), r.data(), c.data(),
+                              o.stream()),
+        o.name);
+}
+
 void fill32_batch_(at::TensorList dst, at::IntArrayRef value) {
   Op o("fill32_batch_");
   TORCH_CHECK(dst.size() == value.size(), o.name, ": lengths");
@@ -1329,6 +1351,7 @@ TORCH_LIBRARY_FRAGMENT(mog_air, m) {
       "asr_unpack_parts_(int B, int Z, int H, int ld, Tensor dU, Tensor dUg, int nparts, "
       "Tensor(a!) dz, Tensor(b!) dss, Tensor(c!) dh, Tensor(d!) dhg, int acc_dz) -> ()");
   m.def("copy32_batch_(Tensor(a!)[] dst, Tensor[] src) -> ()");
+  m.def("transpose32_batch_(Tensor(a!)[] dst, Tensor[] src) -> ()");
   m.def(
       "air_step_forward_(int B, int HS, int HZ, int step, bool train, bool use_num_prior, "
       "float thr, float temperature, float prior_lo, float prior_bias, float s_pm, float s_pv, "
@@ -1462,6 +1485,7 @@ TORCH_LIBRARY_IMPL(mog_air, CUDA, m) {
   m.impl("lstm_cell_backward_parts_", &lstm_cell_backward_parts_);
   m.impl("asr_unpack_parts_", &asr_unpack_parts_);
   m.impl("copy32_batch_", &copy32_batch_);
+  m.impl("transpose32_batch_", &transpose32_batch_);
   m.impl("air_step_forward_", &air_step_forward_);
   m.impl("air_step_forward_steps_", &air_step_forward_steps_);
   m.impl("air_step_backward_", &air_step_backward_);

@@ -81,6 +81,7 @@ _SIGS = {
     "mog_rng_fill_batch": [I, P, P, ULL, P, P, P],
     "mog_fill32_batch": [I, P, P, P, P],
     "mog_copy32_batch": [I, P, P, P, P],
+    "mog_transpose32_batch": [I, P, P, P, P, P],
     "mog_copy_f4": [P, P, L, P],
     "mog_generation_prior": [I, I, F, F, F, F, F, F, P, P, P, P, P, P, P, P],
     "mog_asr_pack": [I, I, I, I, P, P, P, P, P, P, P],

@@ -678,12 +678,24 @@ class AIRModel(WeightGradients, GraphCapture, Results):
                  epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]])
             gemm([v(ws.a1)], [vw["recognition_2"]], [v(ws.a2)], TB, R2, R1, R1, R2, R2,
                  epi=EPI_SOFTPLUS, bias=[vb["recognition_2"]])
-            gemm([v(ws.a2), v(ws.a2)], [vw["rec_mean"], vw["rec_log_variance"]],
-                 [v(ws.mu), v(ws.lv)], TB, Z, R2, R2, Z, Z,
-                 bias=[vb["rec_mean"], vb["rec_log_variance"]])
-            self._vae_sample_fwd_all(ws, None, 0, t0, t1)
-            gemm([v(ws.z)], [vw["generative_1"]], [v(ws.d1)], TB, G1, Z, Z, G1, G1,
-                 epi=EPI_SOFTPLUS, bias=[vb["generative_1"]])
+            if Z % 4 and TB < self.SIDE_MIN_BATCH:
+                # a small batch: the latent layers as NT products of W^T copies
+                # (N = Z / K = Z miss the LDS-DMA alignment, and their row-major
+                # form ran on 64 x 64 tiles, a few workgroups); the same
+                # k-ordered chains, so the same bits
+                wt = self._vae_wT()
+                gemm([v(ws.a2), v(ws.a2)], [wt[0], wt[1]], [v(ws.mu), v(ws.lv)], TB, Z, R2, R2,
+                     R2, Z, transB=True, bias=[vb["rec_mean"], vb["rec_log_variance"]])
+                self._vae_sample_fwd_all(ws, None, 0, t0, t1)
+                gemm([v(ws.z)], [wt[2]], [v(ws.d1)], TB, G1, Z, Z, Z, G1, transB=True,
+                     epi=EPI_SOFTPLUS, bias=[vb["generative_1"]])
+            else:
+                gemm([v(ws.a2), v(ws.a2)], [vw["rec_mean"], vw["rec_log_variance"]],
+                     [v(ws.mu), v(ws.lv)], TB, Z, R2, R2, Z, Z,
+                     bias=[vb["rec_mean"], vb["rec_log_variance"]])
+                self._vae_sample_fwd_all(ws, None, 0, t0, t1)
+                gemm([v(ws.z)], [vw["generative_1"]], [v(ws.d1)], TB, G1, Z, Z, G1, G1,
+                     epi=EPI_SOFTPLUS, bias=[vb["generative_1"]])
             gemm([v(ws.d1)], [vw["generative_2"]], [v(ws.d2)], TB, G2, G1, G1, G2, G2,
                  epi=EPI_SOFTPLUS, bias=[vb["generative_2"]])
             if ws.eps_x_offset is not None:
@@ -699,6 +711,20 @@ class AIRModel(WeightGradients, GraphCapture, Results):
         # the loss kernel adds the parts in step order (:665-675)
         _ops.stn_write_parts_(v(ws.r), TB, W, W, r_(ws.th_b), C, C, r_(ws.zval), r_(ws.zmask),
                               r_(ws.cparts), r_(ws.prows))
+
+    def _vae_wT(self):
+        """W^T of rec_mean, rec_log_variance [Z][R2] and generative_1 [G1][Z],
+        transposed in one launch on every call (a captured step re-runs it:
+        the parameters change between replays)."""
+        W2, R1, R2, Z, G1, G2 = self._vae_dims()
+        buf = self.__dict__.get("_vae_wT_buf")
+        if buf is None:
+            buf = self.__dict__["_vae_wT_buf"] = [
+                torch.empty((Z, R2), device=self.device), torch.empty((Z, R2), device=self.device),
+                torch.empty((G1, Z), device=self.device)]
+        _ops.transpose32_batch_(buf, [self._P("vae/" + n + "/weights") for n in
+                                      ("rec_mean", "rec_log_variance", "generative_1")])
+        return buf
 
     def _stn_vae_step_bf16(self, TB, C, X, r_, sv, gen, off, wt, bias, lik_std, ws, B):
         """The bf16 fused step over the TB rows of loop steps r_ (x row = row % B)."""
