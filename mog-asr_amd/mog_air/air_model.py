@@ -678,7 +678,7 @@ class AIRModel(WeightGradients, GraphCapture, Results):
                  epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]])
             gemm([v(ws.a1)], [vw["recognition_2"]], [v(ws.a2)], TB, R2, R1, R1, R2, R2,
                  epi=EPI_SOFTPLUS, bias=[vb["recognition_2"]])
-            if Z % 4 and TB < self.SIDE_MIN_BATCH:
+            if self._latent_nt(TB):
                 # a small batch: the latent layers as NT products of W^T copies
                 # (N = Z / K = Z miss the LDS-DMA alignment, and their row-major
                 # form ran on 64 x 64 tiles, a few workgroups); the same
@@ -714,17 +714,24 @@ class AIRModel(WeightGradients, GraphCapture, Results):
 
     def _vae_wT(self):
         """W^T of rec_mean, rec_log_variance [Z][R2] and generative_1 [G1][Z],
-        transposed in one launch on every call (a captured step re-runs it:
-        the parameters change between replays)."""
+        transposed in one launch when the parameters changed (a captured step
+        records the launch: GraphCapture._capture resets the version)."""
         W2, R1, R2, Z, G1, G2 = self._vae_dims()
         buf = self.__dict__.get("_vae_wT_buf")
         if buf is None:
             buf = self.__dict__["_vae_wT_buf"] = [
                 torch.empty((Z, R2), device=self.device), torch.empty((Z, R2), device=self.device),
                 torch.empty((G1, Z), device=self.device)]
-        _ops.transpose32_batch_(buf, [self._P("vae/" + n + "/weights") for n in
-                                      ("rec_mean", "rec_log_variance", "generative_1")])
+        if getattr(self, "_vae_wT_version", None) != self.params.version:
+            _ops.transpose32_batch_(buf, [self._P("vae/" + n + "/weights") for n in
+                                          ("rec_mean", "rec_log_variance", "generative_1")])
+            self._vae_wT_version = self.params.version
         return buf
+
+    def _latent_nt(self, rows):
+        """The latent layers as NT products of W^T copies (_vae_wT) below
+        SIDE_MIN_BATCH rows: their N or K = Z misses the LDS-DMA alignment."""
+        return self.vae_latent_dimensions % 4 != 0 and rows < self.SIDE_MIN_BATCH
 
     def _stn_vae_step_bf16(self, TB, C, X, r_, sv, gen, off, wt, bias, lik_std, ws, B):
         """The bf16 fused step over the TB rows of loop steps r_ (x row = row % B)."""
@@ -1088,9 +1095,14 @@ class AIRModel(WeightGradients, GraphCapture, Results):
              epi=EPI_SOFTPLUS, bias=[vb["recognition_1"]])
         gemm([ws.a1[t]], [vw["recognition_2"]], [ws.a2[t]], B, R2, R1, R1, R2, R2,
              epi=EPI_SOFTPLUS, bias=[vb["recognition_2"]])
-        gemm([ws.a2[t], ws.a2[t]], [vw["rec_mean"], vw["rec_log_variance"]],
-             [ws.mu[t], ws.lv[t]], B, Z, R2, R2, Z, Z,
-             bias=[vb["rec_mean"], vb["rec_log_variance"]])
+        if self._latent_nt(B):
+            wt = self._vae_wT()
+            gemm([ws.a2[t], ws.a2[t]], wt[:2], [ws.mu[t], ws.lv[t]], B, Z, R2, R2, R2, Z,
+                 transB=True, bias=[vb["rec_mean"], vb["rec_log_variance"]])
+        else:
+            gemm([ws.a2[t], ws.a2[t]], [vw["rec_mean"], vw["rec_log_variance"]],
+                 [ws.mu[t], ws.lv[t]], B, Z, R2, R2, Z, Z,
+                 bias=[vb["rec_mean"], vb["rec_log_variance"]])
         self._vae_sample_fwd(ws, t, None, 0)
 
     def _vae_decoder_fp32(self, ws, lik_std, t0, t1):
@@ -1101,8 +1113,12 @@ class AIRModel(WeightGradients, GraphCapture, Results):
         v = lambda a: a[t0:t1].reshape(n, -1)  # noqa: E731
         vw = {k: self._P("vae/" + k + "/weights") for k in self._VAE[4:]}
         vb = {k: self._P("vae/" + k + "/biases") for k in self._VAE[4:]}
-        gemm([v(ws.z)], [vw["generative_1"]], [v(ws.d1)], n, G1, Z, Z, G1, G1,
-             epi=EPI_SOFTPLUS, bias=[vb["generative_1"]])
+        if self._latent_nt(n):
+            gemm([v(ws.z)], [self._vae_wT()[2]], [v(ws.d1)], n, G1, Z, Z, Z, G1, transB=True,
+                 epi=EPI_SOFTPLUS, bias=[vb["generative_1"]])
+        else:
+            gemm([v(ws.z)], [vw["generative_1"]], [v(ws.d1)], n, G1, Z, Z, G1, G1,
+                 epi=EPI_SOFTPLUS, bias=[vb["generative_1"]])
         gemm([v(ws.d1)], [vw["generative_2"]], [v(ws.d2)], n, G2, G1, G1, G2, G2,
              epi=EPI_SOFTPLUS, bias=[vb["generative_2"]])
         gemm([v(ws.d2)], [vw["gen_mean"]], [v(ws.r)], n, W2, G2, G2, W2, W2,

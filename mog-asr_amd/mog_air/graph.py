@@ -109,7 +109,7 @@ class GraphCapture:
         # the weight packs are refreshed by a launch inside the graph on every
         # replay (the parameters change every step): force it to be recorded
         self._pack_version = self._pack32_version = self._w1cat_version = None
-        self._w3_version = None
+        self._w3_version = self._vae_wT_version = None
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         self._global_batch = global_batch
@@ -118,3 +118,7 @@ class GraphCapture:
             self._backward(gX, ws)
         self._graph = g
         self._graph_ws = ws
+        # capture executed nothing: the weight packs / copies recorded above
+        # are not in their buffers yet, so the next eager use must refresh them
+        self._pack_version = self._pack32_version = self._w1cat_version = None
+        self._w3_version = self._vae_wT_version = None
